@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: metric-AMG preconditioner applications (one V-cycle each) per
+second and achieved HBM GB/s on the bidomain_3d nrefs=6 system
+(BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--nrefs 6] [--dim 3]
+
+A step = one preconditioner application z = B r (one V-cycle from x0 = 0) on
+a resident seeded r (uniform(-1,1), seed 1234) -- the unit of work of the
+reference's hot loop (`BB * r` inside ConjGrad, src/bidomain_3d.py:149-150).
+The timed region runs K applies kernel by kernel on one stream with HIP
+events around the dominant kernel (level-0 residual SpMV) of every step;
+`value` = K * n_gpus / max-over-ranks wall time.  N > 1: until the
+row-partitioned multi-GPU cycle lands, every rank applies the full
+preconditioner on its own GPU (independent replicas, "scaling": "weak").
+The cpu_baseline leg times the oracle's C restatement (oracle/vcycle_ref.c)
+of the same cycle on the same hierarchy on the host cores (rank 0, N = 1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "V-cycle applies/sec + HBM GB/s, bidomain_3d nrefs=6 @1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md); 6290 measured copy
+
+
+def log(*a):
+    print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--dim', type=int, default=3)
+    ap.add_argument('--nrefs', type=int, default=6)
+    ap.add_argument('--gamma', type=float, default=1e6)
+    ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
+    ap.add_argument('--no-breakdown', action='store_true')
+    ap.add_argument('--pcg', action='store_true', help='also run one full PCG solve')
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    import metric_amg_examples_amd as M
+
+    n = M.problems.finest_n(args.dim, args.nrefs)
+    t0 = time.time()
+    sysm = M.problems.bidomain(args.dim, n, args.gamma)
+    t_gen = time.time() - t0
+    log('rank %d: generated %dD n=%d N=%d nnz=%d in %.1fs' % (rank, args.dim, n, sysm.N, sysm.nnz, t_gen))
+    t0 = time.time()
+    H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+    t_setup = time.time() - t0
+    t0 = time.time()
+    B = M.MetricAMG.from_host(H, sysm.W)
+    t_upload = time.time() - t0
+    sizes = [H.sizes(l) for l in range(H.num_levels)]
+    log('rank %d: host setup %.1fs, upload %.1fs, levels %s' % (
+        rank, t_setup, t_upload, [(s['n'], s['nnzA']) for s in sizes]))
+
+    r = torch.as_tensor(M.problems.seeded_rhs(sysm.N)).to(dev)
+    z = torch.empty_like(r)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+            torch.cuda.synchronize(dev)
+
+    # warmup (graph path + eager path)
+    for _ in range(max(1, args.warmup)):
+        B.apply_device(r, z, stream)
+    B.time_apply(r, z, max(1, args.warmup), 0, stream)
+    barrier()
+
+    # ---- timed region: K eager applies, events around the dominant kernel
+    t0 = time.perf_counter()
+    ms_ev, kms, cbytes = B.time_apply(r, z, args.steps, 0, stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        wall = t.item()
+    ms_per_step = 1e3 * wall / args.steps
+    value = args.steps * world / wall
+    apply_bytes = B.apply_bytes
+    dom_bytes = cbytes[0]                   # level-0 residual: one launch per apply
+    dom_ms = kms[0]
+
+    # graph-replay throughput (same work, one hipGraph launch per apply)
+    barrier()
+    g0 = torch.cuda.Event(enable_timing=True)
+    g1 = torch.cuda.Event(enable_timing=True)
+    g0.record(stream)
+    for _ in range(args.steps):
+        B.apply_device(r, z, stream)
+    g1.record(stream)
+    barrier()
+    graph_ms = g0.elapsed_time(g1) / args.steps
+
+    breakdown = None
+    if not args.no_breakdown:
+        ms_all, kms_all, _ = B.time_apply(r, z, max(3, args.steps // 4), 1, stream)
+        names = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_prolong',
+                 'coarse_levels', 'coarsest_dense', 'misc']
+        breakdown = {nm: {'ms': round(kms_all[i], 4),
+                          'GB': round(cbytes[i] / 1e9, 4),
+                          'GBps': round(cbytes[i] / 1e9 / (kms_all[i] * 1e-3), 1) if kms_all[i] > 0 else None}
+                     for i, nm in enumerate(names)}
+        breakdown['instrumented_ms_per_apply'] = round(ms_all, 4)
+
+    pcg = None
+    if args.pcg and rank == 0:
+        b = M.problems.seeded_rhs(sysm.N)
+        Aop = sysm
+        B._Aop = Aop
+        solver = M.ConjGrad(Aop, precond=B, tolerance=1e-8, maxiter=500)
+        t0 = time.time()
+        solver * b
+        pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
+               'seconds': round(time.time() - t0, 3)}
+
+    # ---- CPU baseline: oracle C restatement on the same hierarchy, host cores
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+        import cref
+        levels = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
+        levels[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
+        ch = cref.CHierarchy(levels)
+        rh = M.problems.seeded_rhs(sysm.N)
+        ch.apply(rh)                                         # warm (page-in)
+        t0 = time.time()
+        for _ in range(args.cpu_sample):
+            zc = ch.apply(rh)
+        tc = (time.time() - t0) / args.cpu_sample
+        zg = z.cpu().numpy()
+        err = float(np.linalg.norm(zc - zg) / np.linalg.norm(zc))
+        cpu = {'value': round(1.0 / tc, 4), 'unit': 'V-cycle applies/s', 'cores': ch.threads(),
+               'kind': 'port',
+               'sample': '%d applies of the full %s hierarchy (oracle/vcycle_ref.c, OpenMP), '
+                         'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, 'nrefs=%d' % args.nrefs, err)}
+        del ch, levels
+
+    traffic = None
+    tpath = os.path.join(ROOT, 'profiles', 'traffic_r01.json')
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get('N') == sysm.N:
+                traffic = tj.get('dominant_bytes_per_launch')
+        except Exception:
+            traffic = None
+
+    achieved = dom_bytes / 1e9 / (dom_ms * 1e-3) if dom_ms > 0 else None
+    out = {
+        'metric': METRIC,
+        'value': round(value, 3),
+        'unit': 'V-cycle applies/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_per_step, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic (P1 bidomain matrix generated in-library; r = uniform(-1,1), seed 1234)',
+        'config': {
+            'workload': 'bidomain_%dd nrefs=%d gamma=%g metric_mono (profile mi355x_sa_v, nodal SA V-cycle)'
+                        % (args.dim, args.nrefs, args.gamma),
+            'n': n, 'N': sysm.N, 'nnz': sysm.nnz,
+            'levels': [[s['n'], s['nnzA']] for s in sizes],
+            'parallelism': 'replicas' if world > 1 else 'single',
+        },
+        'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),
+        'apply_GB_alg': round(apply_bytes / 1e9, 4),
+        'graph_ms_per_step': round(graph_ms, 4),
+        'roofline': {
+            'bound': 'hbm', 'kernel': 'level-0 residual r = b - A0 x (csr_kernel<*,RESID,0>)',
+            'achieved': round(achieved, 1) if achieved else None,
+            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+            'traffic': traffic,
+            'bytes_per_launch': dom_bytes, 'ms_per_launch': round(dom_ms, 4),
+        },
+        'cpu_baseline': cpu,
+        'setup_s': {'generate': round(t_gen, 2), 'host_setup': round(t_setup, 2),
+                    'upload': round(t_upload, 2)},
+        'breakdown': breakdown,
+        'pcg': pcg,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    B.close()
+    H.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,199 @@
+/*
+ * mamg.h -- C-ABI of the MI355X-native metric-AMG preconditioner.
+ *
+ * This is the drop-in boundary for the reference's `metric_mono` hot path.
+ * In the reference the boundary is Python -> SWIG (haznics) -> HAZmath C:
+ *
+ *   metricAMG(A, W, idofs=interface_dofs, parameters=parameters)
+ *       /root/reference/src/utils.py:86  (without idofs: :88)
+ *   BB * r   (cbc.block operator -> HAZmath precond fct, one cycle per call,
+ *             `maxit: 1` /root/reference/src/amg_parameters.py:71)
+ *       invoked by ConjGrad  /root/reference/src/bidomain_3d.py:149-150
+ *   haznics.create_dvector / dvec_create_p / create_ivector  src/utils.py:104-111
+ *   PETSc_to_dCSRmat(A)                                      src/utils.py:96,108
+ *   haznics.fenics_metric_amg_solver_dcsr(A, b, x, idofs)    src/utils.py:119
+ *
+ * Conventions: plain pointers and sizes only; 0 = success, negative = error
+ * (message via mamg_last_error(), thread-local); no exceptions cross the ABI;
+ * the caller owns every input buffer (setup reads them, never keeps them);
+ * the handle owns all device memory.  One handle per host thread / stream.
+ * All arithmetic is IEEE binary64.  Matrices are CSR with int64 row pointers,
+ * int32 column indices, column indices sorted within a row.
+ */
+#ifndef MAMG_H
+#define MAMG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAMG_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+enum {
+  MAMG_OK = 0,
+  MAMG_ERR_ARG = -1,          /* bad argument / shape                         */
+  MAMG_ERR_HIP = -2,          /* HIP runtime error (no device, OOM, launch)   */
+  MAMG_ERR_SETUP = -3,        /* hierarchy construction failed                */
+  MAMG_ERR_UNSUPPORTED = -4,  /* parameter combination not implemented        */
+  MAMG_ERR_NOMEM = -5,        /* host allocation failed                       */
+  MAMG_ERR_BREAKDOWN = -6     /* PCG: <r,Br> < 0 (indefinite preconditioner)  */
+};
+
+/* ---- parameter enums (HAZmath names, build-defined values) ---------- */
+enum { MAMG_UA_AMG = 1, MAMG_SA_AMG = 2 };                       /* AMG_type   */
+enum { MAMG_V_CYCLE = 1, MAMG_W_CYCLE = 2 };                     /* cycle_type */
+enum {                                                          /* smoother   */
+  MAMG_SMOOTHER_JACOBI = 1,      /* x += w D^-1 r, w = relaxation             */
+  MAMG_SMOOTHER_L1DIAG = 2,      /* x += w L1^-1 r, L1_ii = sum_j |a_ij|      */
+  MAMG_SMOOTHER_JACOBI_RHO = 3,  /* x += (w/rho(D^-1A)) D^-1 r  (default)     */
+  MAMG_SMOOTHER_GS = 10,         /* HAZmath sequential smoothers: rejected    */
+  MAMG_SMOOTHER_SGS = 11
+};
+enum {                                                   /* aggregation_type  */
+  MAMG_VMB = 1, MAMG_MIS = 2, MAMG_MWM = 3, MAMG_HEC = 4, MAMG_HEM = 5
+};                                                       /* only MIS accepted */
+enum {                                                   /* Schwarz_type      */
+  MAMG_SCHWARZ_FORWARD = 1, MAMG_SCHWARZ_BACKWARD = 2, MAMG_SCHWARZ_SYMMETRIC = 3,
+  MAMG_SCHWARZ_BLOCK_JACOBI = 4  /* additive non-overlapping seed blocks (GPU) */
+};
+enum { MAMG_OFF = 0, MAMG_ON = 1 };
+enum { MAMG_COARSE_DENSE = 32 };  /* coarse_solver: 32 (UMFPACK in HAZmath)  */
+
+/* Parameter dictionary keys of /root/reference/src/amg_parameters.py:67-89
+ * (and src/utils.py:60-82), same names, POD, versioned by abi_version. */
+typedef struct mamg_params {
+  int32_t abi_version;       /* = MAMG_ABI_VERSION                           */
+  int32_t AMG_type;          /* MAMG_SA_AMG (default) | MAMG_UA_AMG          */
+  int32_t cycle_type;        /* MAMG_V_CYCLE (default) | MAMG_W_CYCLE        */
+  int32_t max_levels;        /* 20                                           */
+  int32_t maxit;             /* cycles per apply, 1                          */
+  int32_t smoother;          /* MAMG_SMOOTHER_JACOBI_RHO                     */
+  double relaxation;         /* 4/3                                          */
+  int32_t presmooth_iter;    /* 1                                            */
+  int32_t postsmooth_iter;   /* 1                                            */
+  int32_t coarse_dof;        /* 100                                          */
+  int32_t coarse_solver;     /* 32 -> dense direct                           */
+  int32_t coarse_scaling;    /* MAMG_OFF (ON unsupported: non-linear cycle)  */
+  int32_t aggregation_type;  /* MAMG_MIS (deterministic parallel MIS-2)      */
+  double strong_coupled;     /* SoC threshold theta, 0.0                     */
+  int32_t max_aggregation;   /* accepted, unused by MIS-2 (documented)       */
+  int32_t amli_degree;       /* accepted, unused (no AMLI cycle)             */
+  int32_t Schwarz_levels;    /* 1: seed-block Jacobi on level 0 if idofs     */
+  int32_t Schwarz_mmsize;    /* max dofs per seed block, 100                 */
+  int32_t Schwarz_maxlvl;    /* accepted; blocks are distance-1 (see DESIGN) */
+  int32_t Schwarz_type;      /* MAMG_SCHWARZ_BLOCK_JACOBI                    */
+  int32_t Schwarz_blksolver; /* 32 -> dense block inverse                    */
+  int32_t print_level;       /* 0 silent                                     */
+  double sa_omega;           /* prolongator smoothing numerator, 4/3         */
+  int32_t rho_iters;         /* 0: Gershgorin bound of rho(D^-1 A)           */
+  int32_t max_coarse_dense;  /* largest coarsest level for dense solve, 8192 */
+  int32_t device;            /* HIP device ordinal, 0                        */
+  int32_t spmv_lanes;        /* 0 = auto; else lanes per row (2..64, pow2)   */
+  /* nodal (systems) aggregation, build-defined extension: dofs field-major,
+   * dof = f*nv + node for f < num_functions (the monolithic [u1; u2] order of
+   * ii_convert, src/bidomain_3d.py:124,138).  >1 aggregates nodes with a
+   * block-norm strength and keeps one coarse column per field/aggregate. */
+  int32_t num_functions;     /* 1                                            */
+  int32_t node_block_smoother; /* nodal: node-block Jacobi where no seed blocks (1) */
+  int32_t sa_block_diag;     /* nodal: smooth P with node-block D^-1 (1)     */
+} mamg_params;
+
+/* Host CSR view (caller-owned). */
+typedef struct mamg_csr {
+  int64_t nrows, ncols, nnz;
+  const int64_t* rowptr;   /* nrows+1 */
+  const int32_t* colind;   /* nnz, sorted per row */
+  const double* values;    /* nnz */
+} mamg_csr;
+
+typedef struct mamg_handle mamg_handle;   /* device hierarchy + workspace   */
+typedef struct mamg_hier mamg_hier;       /* host hierarchy (setup result)  */
+
+/* ---- library ---------------------------------------------------------- */
+int mamg_abi_version(void);
+const char* mamg_last_error(void);
+void mamg_params_default(mamg_params* p);
+
+/* ---- problem generators (the reference's FEniCS assembly restated;
+ *      src/bidomain_2d.py:51-99, meshes src/utils.py:149-182) ------------- */
+/* Sizes of the monolithic bidomain system on UnitSquare/UnitCube(n). */
+int mamg_gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz);
+/* Fill caller buffers rowptr[nrows+1], colind[nnz], values[nnz]. */
+int mamg_gen_bidomain(int dim, int64_t n, double gamma, double kappa1,
+                      double kappa2, int64_t* rowptr, int32_t* colind,
+                      double* values);
+
+/* ---- host setup (no GPU needed).  The hierarchy keeps a VIEW of A (level
+ *      0): the caller keeps A alive until mamg_hier_free. ------------------ */
+/* Replaces metricAMG.__init__'s HAZmath setup (src/utils.py:86).  idofs may
+ * be NULL (n_idofs = 0): then no seed blocks (src/utils.py:88). */
+int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, mamg_hier** out);
+void mamg_hier_free(mamg_hier* h);
+int mamg_hier_num_levels(const mamg_hier* h);
+/* Sizes of level l: n, nnz(A), nnz(P), nnz(R), nnz(WB) (0 if point smoother),
+ * ncoarse (n of level l+1, 0 on the coarsest). */
+int mamg_hier_level_sizes(const mamg_hier* h, int l, int64_t* sizes6);
+/* Export level l into caller buffers (any pointer may be NULL to skip):
+ * A (ptr,col,val), P, R, WB (CSR), winv[n], agg[n] (int64), Ainv[n*n]. */
+int mamg_hier_level_export(const mamg_hier* h, int l,
+                           int64_t* Aptr, int32_t* Acol, double* Aval,
+                           int64_t* Pptr, int32_t* Pcol, double* Pval,
+                           int64_t* Rptr, int32_t* Rcol, double* Rval,
+                           int64_t* Wptr, int32_t* Wcol, double* Wval,
+                           double* winv, int64_t* agg, double* Ainv);
+
+/* ---- device hierarchy ------------------------------------------------- */
+/* Host setup + upload.  Level-0 matrix is uploaded from A directly. */
+int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+               const mamg_params* params, mamg_handle** out);
+/* Upload an existing host hierarchy (level 0 matrix taken from A). */
+int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
+                mamg_handle** out);
+void mamg_destroy(mamg_handle* h);
+
+int64_t mamg_nrows(const mamg_handle* h);
+int mamg_num_levels(const mamg_handle* h);
+/* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
+ * kernel class; see DESIGN.md section 4. */
+int mamg_apply_bytes(const mamg_handle* h, double* total_bytes);
+
+/* z = B r : one preconditioner application (`maxit` cycles from x0 = 0).
+ * Host pointers (copies in/out, synchronous). */
+int mamg_apply(mamg_handle* h, const double* r, double* z);
+/* Device pointers, enqueued on `stream` (hipStream_t, NULL = default).
+ * r is not modified; r and z must not alias. */
+int mamg_apply_device(mamg_handle* h, const double* d_r, double* d_z,
+                      void* stream);
+/* y = A x with the level-0 operator (device pointers). */
+int mamg_spmv_device(mamg_handle* h, const double* d_x, double* d_y,
+                     void* stream);
+
+/* Device-resident preconditioned CG with cbc.block ConjGrad semantics
+ * (src/bidomain_3d.py:149-160): x0 = d_x on entry, residuals = sqrt(<r,Br>),
+ * stop when residual <= tol (times residual[0] if relativeconv) or after
+ * maxiter iterations.  residuals[maxiter+1], alphas[maxiter], betas[maxiter]
+ * are host buffers; *niters = len(residuals)-1.  Returns MAMG_ERR_BREAKDOWN
+ * (x restored as cbc.block does) if <r,Br> < 0. */
+int mamg_pcg_device(mamg_handle* h, const double* d_b, double* d_x, double tol,
+                    int maxiter, int relativeconv, double* residuals,
+                    double* alphas, double* betas, int* niters, void* stream);
+
+/* Timing hook for bench/profiling: run `reps` applies eagerly (kernel by
+ * kernel, no graph) on `stream`, timed with HIP events recorded on that
+ * stream.  *ms_per_apply = mean wall time per apply.  kernel_ms[16] (if
+ * non-NULL) = mean ms per apply per kernel class:
+ * mode 0 instruments only class 0 (the level-0 residual SpMV, the dominant
+ * kernel), mode 1 instruments every launch.  class_bytes[16] (if non-NULL) =
+ * algorithmic HBM bytes per apply of each class. */
+int mamg_time_apply(mamg_handle* h, const double* d_r, double* d_z, int reps,
+                    int mode, double* ms_per_apply, double* kernel_ms,
+                    double* class_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAMG_H */

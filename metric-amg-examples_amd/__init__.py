@@ -1,0 +1,14 @@
+"""metric-amg-examples_amd: MI355X-native metric-AMG preconditioner.
+
+Drop-in for the reference's `metric_mono` hot path:
+    from metric_amg_examples_amd import metricAMG, ConjGrad, parameters
+    BB = metricAMG(AA_, W, idofs=interface_dofs, parameters=parameters.parameters_metric_mi355x)
+    AAinv = ConjGrad(AA_, precond=BB, tolerance=1e-8, maxiter=500)
+    xx = AAinv * bb_
+"""
+from . import _lib, parameters, problems
+from .amg import HostHierarchy, MetricAMG, metricAMG
+from .krylov import ConjGrad, lanczos_eigenvalues
+
+__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'ConjGrad', 'lanczos_eigenvalues',
+           'parameters', 'problems', '_lib']

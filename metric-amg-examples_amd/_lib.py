@@ -1,0 +1,126 @@
+"""ctypes binding of libmamg.so (include/mamg.h).
+
+The product path: this module is the thin ctypes C-ABI the north star asks
+for (Python host code -> libmamg.so -> HIP).  It fails loudly if the built
+library is missing; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('MAMG_LIB', os.path.join(_HERE, 'libmamg.so'))
+
+MAMG_ABI_VERSION = 1
+OK, ERR_ARG, ERR_HIP, ERR_SETUP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_BREAKDOWN = 0, -1, -2, -3, -4, -5, -6
+
+
+class MamgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__('mamg error %d: %s' % (code, msg))
+        self.code = code
+
+
+class mamg_params(C.Structure):
+    _fields_ = [
+        ('abi_version', C.c_int32), ('AMG_type', C.c_int32), ('cycle_type', C.c_int32),
+        ('max_levels', C.c_int32), ('maxit', C.c_int32), ('smoother', C.c_int32),
+        ('relaxation', C.c_double), ('presmooth_iter', C.c_int32),
+        ('postsmooth_iter', C.c_int32), ('coarse_dof', C.c_int32),
+        ('coarse_solver', C.c_int32), ('coarse_scaling', C.c_int32),
+        ('aggregation_type', C.c_int32), ('strong_coupled', C.c_double),
+        ('max_aggregation', C.c_int32), ('amli_degree', C.c_int32),
+        ('Schwarz_levels', C.c_int32), ('Schwarz_mmsize', C.c_int32),
+        ('Schwarz_maxlvl', C.c_int32), ('Schwarz_type', C.c_int32),
+        ('Schwarz_blksolver', C.c_int32), ('print_level', C.c_int32),
+        ('sa_omega', C.c_double), ('rho_iters', C.c_int32),
+        ('max_coarse_dense', C.c_int32), ('device', C.c_int32), ('spmv_lanes', C.c_int32),
+        ('num_functions', C.c_int32), ('node_block_smoother', C.c_int32),
+        ('sa_block_diag', C.c_int32),
+    ]
+
+
+class mamg_csr(C.Structure):
+    _fields_ = [('nrows', C.c_int64), ('ncols', C.c_int64), ('nnz', C.c_int64),
+                ('rowptr', C.POINTER(C.c_int64)), ('colind', C.POINTER(C.c_int32)),
+                ('values', C.POINTER(C.c_double))]
+
+
+P_I64 = C.POINTER(C.c_int64)
+P_I32 = C.POINTER(C.c_int32)
+P_F64 = C.POINTER(C.c_double)
+VP = C.c_void_p
+
+# every symbol include/mamg.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    'mamg_abi_version': (C.c_int, []),
+    'mamg_last_error': (C.c_char_p, []),
+    'mamg_params_default': (None, [C.POINTER(mamg_params)]),
+    'mamg_gen_bidomain_size': (C.c_int, [C.c_int, C.c_int64, P_I64, P_I64]),
+    'mamg_gen_bidomain': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                    P_I64, P_I32, P_F64]),
+    'mamg_host_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64,
+                                  C.POINTER(mamg_params), C.POINTER(VP)]),
+    'mamg_hier_free': (None, [VP]),
+    'mamg_hier_num_levels': (C.c_int, [VP]),
+    'mamg_hier_level_sizes': (C.c_int, [VP, C.c_int, P_I64]),
+    'mamg_hier_level_export': (C.c_int, [VP, C.c_int] + [P_I64, P_I32, P_F64] * 4
+                               + [P_F64, P_I64, P_F64]),
+    'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                             C.POINTER(VP)]),
+    'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),
+    'mamg_destroy': (None, [VP]),
+    'mamg_nrows': (C.c_int64, [VP]),
+    'mamg_num_levels': (C.c_int, [VP]),
+    'mamg_apply_bytes': (C.c_int, [VP, P_F64]),
+    'mamg_apply': (C.c_int, [VP, P_F64, P_F64]),
+    'mamg_apply_device': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_spmv_device': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_pcg_device': (C.c_int, [VP, VP, VP, C.c_double, C.c_int, C.c_int, P_F64, P_F64,
+                                  P_F64, P_I32, VP]),
+    'mamg_time_apply': (C.c_int, [VP, VP, VP, C.c_int, C.c_int, P_F64, P_F64, P_F64, VP]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmamg.so once; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError('libmamg.so not built (%s); run __graft_entry__.build() '
+                              'or make -C metric-amg-examples_amd/csrc' % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.mamg_abi_version() != MAMG_ABI_VERSION:
+            raise ImportError('libmamg ABI mismatch')
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise MamgError(rc, lib().mamg_last_error().decode(errors='replace'))
+    return rc
+
+
+def ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def as_csr_struct(indptr: np.ndarray, indices: np.ndarray, data: np.ndarray, ncols: int):
+    """Build a mamg_csr view (arrays must stay alive while it is used)."""
+    n = len(indptr) - 1
+    s = mamg_csr()
+    s.nrows, s.ncols, s.nnz = n, ncols, int(indptr[-1])
+    s.rowptr = ptr(indptr, C.c_int64)
+    s.colind = ptr(indices, C.c_int32)
+    s.values = ptr(data, C.c_double)
+    return s

@@ -1,0 +1,283 @@
+"""MetricAMG: drop-in for cbc.block's ``block.algebraic.hazmath.metricAMG``.
+
+Reference call sites:
+  Minv = metricAMG(A, W, idofs=interface_dofs, parameters=parameters)
+      /root/reference/src/utils.py:86   (without idofs :88)
+  R.T * Minv * R                        src/utils.py:53 (block form)
+  ConjGrad(AA_, precond=BB, ...)        src/bidomain_3d.py:149
+``MetricAMG`` runs the host setup + upload through libmamg's C-ABI
+(``mamg_setup``) and applies one multigrid cycle per ``B * r`` on the GPU
+(``mamg_apply`` / ``mamg_apply_device``).  There is no CPU fallback: without
+libmamg.so or a HIP device the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .parameters import make_params
+
+
+def csr_arrays(A):
+    """scipy sparse | (indptr, indices, data[, shape]) | problems.System ->
+    (indptr int64, indices int32, data float64, nrows, ncols), sorted."""
+    if hasattr(A, 'indptr') and hasattr(A, 'indices') and hasattr(A, 'data') \
+            and not hasattr(A, 'tocsr'):
+        indptr, indices, data = A.indptr, A.indices, A.data
+        n = len(indptr) - 1
+        shape = (n, n)
+    elif hasattr(A, 'tocsr'):
+        M = A.tocsr()
+        if not M.has_sorted_indices:
+            M = M.sorted_indices()
+        indptr, indices, data, shape = M.indptr, M.indices, M.data, M.shape
+    else:
+        indptr, indices, data = A[0], A[1], A[2]
+        n = len(indptr) - 1
+        shape = A[3] if len(A) > 3 else (n, n)
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    data = np.ascontiguousarray(data, dtype=np.float64)
+    if indptr.ndim != 1 or len(indptr) != shape[0] + 1 or indptr[0] != 0 \
+            or len(indices) != indptr[-1] or len(data) != indptr[-1]:
+        raise ValueError('inconsistent CSR arrays: len(indptr)=%d, indptr[-1]=%d, '
+                         'len(indices)=%d, len(data)=%d'
+                         % (len(indptr), indptr[-1], len(indices), len(data)))
+    return indptr, indices, data, int(shape[0]), int(shape[1])
+
+
+def _dims(W, n):
+    if W is None:
+        return [n]
+    dims = []
+    for w in W:
+        dims.append(int(w.dim()) if hasattr(w, 'dim') else int(w))
+    if sum(dims) != n:
+        raise ValueError('sum of W dims %d != matrix size %d' % (sum(dims), n))
+    return dims
+
+
+def _device_ptr(x):
+    """(pointer, keepalive) for a torch CUDA tensor / object with data_ptr()."""
+    if hasattr(x, 'data_ptr') and getattr(x, 'is_cuda', False):
+        if x.dtype.__str__() != 'torch.float64' or not x.is_contiguous():
+            raise TypeError('device vectors must be contiguous float64')
+        return C.c_void_p(x.data_ptr())
+    if isinstance(x, int):
+        return C.c_void_p(x)
+    raise TypeError('expected a CUDA tensor or a raw device pointer')
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if hasattr(stream, 'cuda_stream'):
+        return C.c_void_p(stream.cuda_stream)
+    return C.c_void_p(int(stream))
+
+
+class MetricAMG:
+    """One multigrid cycle per application, on the GPU.
+
+    A: CSR operator (scipy sparse, (indptr, indices, data), or System).
+    W: list of function spaces / block sizes (only sizes are used).
+    idofs: interface dofs seeding the level-0 Schwarz blocks (src/utils.py:84).
+    parameters: dict with the reference's key names (see parameters.py).
+    """
+
+    def __init__(self, A, W=None, idofs=None, parameters=None, **overrides):
+        self._L = _lib.lib()
+        indptr, indices, data, n, m = csr_arrays(A)
+        if n != m:
+            raise ValueError('A must be square')
+        self.shape = (n, n)
+        self.W = _dims(W, n)
+        self.params = make_params(parameters, **overrides)
+        self._A = (indptr, indices, data)        # level 0 stays referenced
+        self._Aop = A
+        csr = _lib.as_csr_struct(indptr, indices, data, m)
+        if idofs is not None:
+            self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
+            ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
+        else:
+            self.idofs, ip, ni = None, None, 0
+        h = C.c_void_p()
+        _lib.check(self._L.mamg_setup(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h)))
+        self._h = h
+
+    @classmethod
+    def from_host(cls, H: 'HostHierarchy', W=None):
+        """Upload an existing HostHierarchy (``mamg_upload``) instead of
+        running the setup again."""
+        self = cls.__new__(cls)
+        self._L = _lib.lib()
+        indptr, indices, data = H._A
+        n = len(indptr) - 1
+        self.shape = (n, n)
+        self.W = _dims(W, n)
+        self.params = H.params
+        self._A = H._A
+        self._Aop = None
+        self.idofs = H.idofs
+        csr = _lib.as_csr_struct(indptr, indices, data, n)
+        h = C.c_void_p()
+        _lib.check(self._L.mamg_upload(H._h, C.byref(csr), C.byref(self.params), C.byref(h)))
+        self._h = h
+        return self
+
+    # -- properties --------------------------------------------------------
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def num_levels(self) -> int:
+        return self._L.mamg_num_levels(self._h)
+
+    @property
+    def apply_bytes(self) -> float:
+        b = C.c_double()
+        _lib.check(self._L.mamg_apply_bytes(self._h, C.byref(b)))
+        return b.value
+
+    # -- application -------------------------------------------------------
+    def matvec(self, r):
+        """z = B r.  numpy in -> numpy out (host copies); CUDA tensor in ->
+        CUDA tensor out (device-resident, current torch stream)."""
+        if isinstance(r, np.ndarray):
+            rr = np.ascontiguousarray(r, dtype=np.float64)
+            if rr.shape != (self.shape[0],):
+                raise ValueError('vector size mismatch')
+            z = np.empty_like(rr)
+            _lib.check(self._L.mamg_apply(self._h, _lib.ptr(rr, C.c_double),
+                                          _lib.ptr(z, C.c_double)))
+            return z
+        import torch
+        z = torch.empty_like(r)
+        self.apply_device(r, z, torch.cuda.current_stream())
+        return z
+
+    def apply_device(self, r, z, stream=None):
+        _lib.check(self._L.mamg_apply_device(self._h, _device_ptr(r), _device_ptr(z),
+                                             _stream_ptr(stream)))
+        return z
+
+    def spmv_device(self, x, y, stream=None):
+        _lib.check(self._L.mamg_spmv_device(self._h, _device_ptr(x), _device_ptr(y),
+                                            _stream_ptr(stream)))
+        return y
+
+    def __mul__(self, r):
+        return self.matvec(r)
+
+    __call__ = matvec
+
+    def time_apply(self, r, z, reps, mode=0, stream=None):
+        """(ms per apply, kernel_ms[16], class_bytes[16]) via HIP events."""
+        ms = C.c_double()
+        kms = (C.c_double * 16)()
+        cb = (C.c_double * 16)()
+        _lib.check(self._L.mamg_time_apply(self._h, _device_ptr(r), _device_ptr(z), int(reps),
+                                           int(mode), C.byref(ms), kms, cb, _stream_ptr(stream)))
+        return ms.value, list(kms), list(cb)
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.mamg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+metricAMG = MetricAMG     # the reference's spelling (src/utils.py:2,86)
+
+
+class HostHierarchy:
+    """Host-only setup (``mamg_host_setup``): the hierarchy the device path
+    uploads, exported level by level.  Used by tests and the bench's CPU
+    baseline; needs no GPU."""
+
+    def __init__(self, A, idofs=None, parameters=None, **overrides):
+        self._L = _lib.lib()
+        indptr, indices, data, n, m = csr_arrays(A)
+        self._A = (indptr, indices, data)
+        self.params = make_params(parameters, **overrides)
+        csr = _lib.as_csr_struct(indptr, indices, data, m)
+        self._csr = csr
+        if idofs is not None:
+            self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
+            ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
+        else:
+            self.idofs, ip, ni = None, None, 0
+        h = C.c_void_p()
+        _lib.check(self._L.mamg_host_setup(C.byref(csr), ip, ni, C.byref(self.params),
+                                           C.byref(h)))
+        self._h = h
+
+    @property
+    def num_levels(self):
+        return self._L.mamg_hier_num_levels(self._h)
+
+    def sizes(self, l):
+        s = (C.c_int64 * 6)()
+        _lib.check(self._L.mamg_hier_level_sizes(self._h, l, s))
+        return dict(n=s[0], nnzA=s[1], nnzP=s[2], nnzR=s[3], nnzW=s[4], ncoarse=s[5])
+
+    def level(self, l, with_A=True):
+        """dict of numpy arrays for level l (A, P, R, WB as (indptr, indices,
+        data, shape); winv; agg; Ainv)."""
+        s = self.sizes(l)
+        n, nc = s['n'], s['ncoarse']
+        out = {}
+
+        def alloc(nr, nnz):
+            return (np.zeros(nr + 1, np.int64), np.zeros(nnz, np.int32), np.zeros(nnz, np.float64))
+
+        A = alloc(n, s['nnzA']) if with_A else (None, None, None)
+        coarsest = nc == 0
+        P = alloc(n, s['nnzP']) if not coarsest else (None, None, None)
+        R = alloc(nc, s['nnzR']) if not coarsest else (None, None, None)
+        Wb = alloc(n, s['nnzW']) if s['nnzW'] else (None, None, None)
+        winv = np.zeros(n) if (not coarsest and not s['nnzW']) else None
+        agg = np.zeros(n // max(1, self.params.num_functions), np.int64) if not coarsest else None
+        Ainv = np.zeros(n * n) if coarsest else None
+
+        def p(a, t):
+            return None if a is None else _lib.ptr(a, t)
+
+        args = []
+        for M in (A, P, R, Wb):
+            args += [p(M[0], C.c_int64), p(M[1], C.c_int32), p(M[2], C.c_double)]
+        _lib.check(self._L.mamg_hier_level_export(
+            self._h, l, *args, p(winv, C.c_double), p(agg, C.c_int64), p(Ainv, C.c_double)))
+        if with_A:
+            out['A'] = A + ((n, n),)
+        if not coarsest:
+            out['P'] = P + ((n, nc),)
+            out['R'] = R + ((nc, n),)
+            out['agg'] = agg
+        if s['nnzW']:
+            out['WB'] = Wb + ((n, n),)
+        if winv is not None:
+            out['winv'] = winv
+        if Ainv is not None:
+            out['Ainv'] = Ainv.reshape(n, n)
+        out['n'] = n
+        return out
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.mamg_hier_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,267 @@
+// capi.cpp -- extern "C" boundary (include/mamg.h).  No exceptions cross it:
+// every entry point catches, records a thread-local message and returns a
+// negative status.
+#include <cstring>
+#include <exception>
+#include <new>
+#include <string>
+
+#include "device.h"
+#include "host.h"
+
+namespace mamg {
+namespace {
+thread_local std::string g_err;
+}
+void set_error(const std::string& s) { g_err = s; }
+}  // namespace mamg
+
+struct mamg_hier {
+  mamg::Hierarchy H;   // level 0 is a view of the caller's CSR (must outlive this)
+};
+
+struct mamg_handle {
+  mamg::DeviceHandle* d = nullptr;
+};
+
+using mamg::set_error;
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                       \
+  }                                                     \
+  catch (const std::bad_alloc&) {                       \
+    set_error("host allocation failed");                \
+    return MAMG_ERR_NOMEM;                              \
+  }                                                     \
+  catch (const std::exception& e) {                     \
+    set_error(std::string("internal error: ") + e.what()); \
+    return MAMG_ERR_SETUP;                              \
+  }
+
+namespace {
+int to_view(const mamg_csr* A, mamg::CsrView* v) {
+  if (!A || !A->rowptr || (A->nnz > 0 && (!A->colind || !A->values))) {
+    set_error("null CSR pointer");
+    return MAMG_ERR_ARG;
+  }
+  if (A->nrows <= 0 || A->ncols <= 0 || A->rowptr[0] != 0 || A->rowptr[A->nrows] != A->nnz) {
+    set_error("inconsistent CSR sizes (rowptr[0] must be 0 and rowptr[n] == nnz)");
+    return MAMG_ERR_ARG;
+  }
+  if (A->nrows > INT32_MAX || A->ncols > INT32_MAX) {
+    set_error("matrix dimension exceeds int32 column index range");
+    return MAMG_ERR_ARG;
+  }
+  v->n = A->nrows;
+  v->m = A->ncols;
+  v->ptr = A->rowptr;
+  v->col = A->colind;
+  v->val = A->values;
+  return MAMG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mamg_abi_version(void) { return MAMG_ABI_VERSION; }
+const char* mamg_last_error(void) { return mamg::g_err.c_str(); }
+
+void mamg_params_default(mamg_params* p) {
+  std::memset(p, 0, sizeof(*p));
+  p->abi_version = MAMG_ABI_VERSION;
+  p->AMG_type = MAMG_SA_AMG;
+  p->cycle_type = MAMG_V_CYCLE;
+  p->max_levels = 20;
+  p->maxit = 1;
+  p->smoother = MAMG_SMOOTHER_JACOBI_RHO;
+  p->relaxation = 4.0 / 3.0;
+  p->presmooth_iter = 1;
+  p->postsmooth_iter = 1;
+  p->coarse_dof = 100;
+  p->coarse_solver = MAMG_COARSE_DENSE;
+  p->coarse_scaling = MAMG_OFF;
+  p->aggregation_type = MAMG_MIS;
+  p->strong_coupled = 0.0;
+  p->max_aggregation = 100;
+  p->amli_degree = 3;
+  p->Schwarz_levels = 1;
+  p->Schwarz_mmsize = 100;
+  p->Schwarz_maxlvl = 1;
+  p->Schwarz_type = MAMG_SCHWARZ_BLOCK_JACOBI;
+  p->Schwarz_blksolver = MAMG_COARSE_DENSE;
+  p->print_level = 0;
+  p->sa_omega = 4.0 / 3.0;
+  p->rho_iters = 0;
+  p->max_coarse_dense = 8192;
+  p->device = 0;
+  p->spmv_lanes = 0;
+  p->num_functions = 1;
+  p->node_block_smoother = 1;
+  p->sa_block_diag = 1;
+}
+
+int mamg_gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz) {
+  GUARD_BEGIN
+  int rc = mamg::gen_bidomain_size(dim, n, nrows, nnz);
+  if (rc) set_error("gen_bidomain_size: dim must be 2 or 3 and n >= 1");
+  return rc;
+  GUARD_END
+}
+
+int mamg_gen_bidomain(int dim, int64_t n, double gamma, double kappa1, double kappa2,
+                      int64_t* rowptr, int32_t* colind, double* values) {
+  GUARD_BEGIN
+  if (!rowptr || !colind || !values) { set_error("null output buffer"); return MAMG_ERR_ARG; }
+  int rc = mamg::gen_bidomain(dim, n, gamma, kappa1, kappa2, rowptr, colind, values);
+  if (rc) set_error("gen_bidomain: bad dim/n");
+  return rc;
+  GUARD_END
+}
+
+int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, mamg_hier** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  mamg_hier* h = new mamg_hier();
+  std::string err;
+  rc = mamg::host_setup(v, idofs, n_idofs, *params, &h->H, &err);
+  if (rc) { set_error(err); delete h; return rc; }
+  *out = h;
+  return MAMG_OK;
+  GUARD_END
+}
+
+void mamg_hier_free(mamg_hier* h) { delete h; }
+
+int mamg_hier_num_levels(const mamg_hier* h) { return h ? (int)h->H.levels.size() : MAMG_ERR_ARG; }
+
+int mamg_hier_level_sizes(const mamg_hier* h, int l, int64_t* s) {
+  if (!h || l < 0 || l >= (int)h->H.levels.size() || !s) { set_error("bad level"); return MAMG_ERR_ARG; }
+  const auto& L = h->H.levels[l];
+  s[0] = L.n;
+  s[1] = h->H.A(l).nnz();
+  s[2] = L.P.nnz();
+  s[3] = L.R.nnz();
+  s[4] = L.WB.nnz();
+  s[5] = L.coarsest ? 0 : h->H.levels[l + 1].n;
+  return MAMG_OK;
+}
+
+int mamg_hier_level_export(const mamg_hier* h, int l, int64_t* Aptr, int32_t* Acol, double* Aval,
+                           int64_t* Pptr, int32_t* Pcol, double* Pval, int64_t* Rptr,
+                           int32_t* Rcol, double* Rval, int64_t* Wptr, int32_t* Wcol,
+                           double* Wval, double* winv, int64_t* agg, double* Ainv) {
+  if (!h || l < 0 || l >= (int)h->H.levels.size()) { set_error("bad level"); return MAMG_ERR_ARG; }
+  const auto& L = h->H.levels[l];
+  auto cp = [](const mamg::CsrView& M, int64_t* p, int32_t* c, double* v) {
+    if (p && M.ptr) std::memcpy(p, M.ptr, (M.n + 1) * sizeof(int64_t));
+    if (c && M.col) std::memcpy(c, M.col, M.nnz() * sizeof(int32_t));
+    if (v && M.val) std::memcpy(v, M.val, M.nnz() * sizeof(double));
+  };
+  cp(h->H.A(l), Aptr, Acol, Aval);
+  if (!L.P.ptr.empty()) cp(L.P.view(), Pptr, Pcol, Pval);
+  if (!L.R.ptr.empty()) cp(L.R.view(), Rptr, Rcol, Rval);
+  if (!L.WB.ptr.empty()) cp(L.WB.view(), Wptr, Wcol, Wval);
+  if (winv && !L.winv.empty()) std::memcpy(winv, L.winv.data(), L.winv.size() * sizeof(double));
+  if (agg && !L.agg.empty()) std::memcpy(agg, L.agg.data(), L.agg.size() * sizeof(int64_t));
+  if (Ainv && !L.Ainv.empty()) std::memcpy(Ainv, L.Ainv.data(), L.Ainv.size() * sizeof(double));
+  return MAMG_OK;
+}
+
+int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+               const mamg_params* params, mamg_handle** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  mamg::Hierarchy H;
+  std::string err;
+  rc = mamg::host_setup(v, idofs, n_idofs, *params, &H, &err);
+  if (rc) { set_error(err); return rc; }
+  mamg::DeviceHandle* d = nullptr;
+  rc = mamg::dev_upload(H, v, *params, &d, &err);
+  if (rc) { set_error(err); return rc; }
+  *out = new mamg_handle{d};
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
+                mamg_handle** out) {
+  GUARD_BEGIN
+  if (!h || !out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v = h->H.A0;
+  if (A) {
+    int rc = to_view(A, &v);
+    if (rc) return rc;
+    if (v.n != h->H.A0.n || v.nnz() != h->H.A0.nnz()) {
+      set_error("A does not match the hierarchy's level-0 matrix");
+      return MAMG_ERR_ARG;
+    }
+  }
+  std::string err;
+  mamg::DeviceHandle* d = nullptr;
+  int rc = mamg::dev_upload(h->H, v, *params, &d, &err);
+  if (rc) { set_error(err); return rc; }
+  *out = new mamg_handle{d};
+  return MAMG_OK;
+  GUARD_END
+}
+
+void mamg_destroy(mamg_handle* h) {
+  if (!h) return;
+  mamg::dev_destroy(h->d);
+  delete h;
+}
+
+int64_t mamg_nrows(const mamg_handle* h) { return h ? mamg::dev_nrows(h->d) : (int64_t)MAMG_ERR_ARG; }
+int mamg_num_levels(const mamg_handle* h) { return h ? mamg::dev_num_levels(h->d) : MAMG_ERR_ARG; }
+
+int mamg_apply_bytes(const mamg_handle* h, double* total) {
+  if (!h || !total) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *total = mamg::dev_apply_bytes(h->d);
+  return MAMG_OK;
+}
+
+#define DEV_CALL(call)                    \
+  GUARD_BEGIN                             \
+  if (!h) { set_error("null handle"); return MAMG_ERR_ARG; } \
+  std::string err;                        \
+  int rc = (call);                        \
+  if (rc) set_error(err);                 \
+  return rc;                              \
+  GUARD_END
+
+int mamg_apply(mamg_handle* h, const double* r, double* z) {
+  DEV_CALL(mamg::dev_apply_host(h->d, r, z, &err))
+}
+
+int mamg_apply_device(mamg_handle* h, const double* d_r, double* d_z, void* stream) {
+  DEV_CALL(mamg::dev_apply(h->d, d_r, d_z, stream, &err))
+}
+
+int mamg_spmv_device(mamg_handle* h, const double* d_x, double* d_y, void* stream) {
+  DEV_CALL(mamg::dev_spmv(h->d, d_x, d_y, stream, &err))
+}
+
+int mamg_pcg_device(mamg_handle* h, const double* d_b, double* d_x, double tol, int maxiter,
+                    int relativeconv, double* residuals, double* alphas, double* betas,
+                    int* niters, void* stream) {
+  DEV_CALL(mamg::dev_pcg(h->d, d_b, d_x, tol, maxiter, relativeconv, residuals, alphas, betas,
+                         niters, stream, &err))
+}
+
+int mamg_time_apply(mamg_handle* h, const double* d_r, double* d_z, int reps, int mode,
+                    double* ms_per_apply, double* kernel_ms, double* class_bytes, void* stream) {
+  DEV_CALL(mamg::dev_time_apply(h->d, d_r, d_z, reps, mode, ms_per_apply, kernel_ms, class_bytes,
+                                stream, &err))
+}
+
+}  // extern "C"

@@ -1,0 +1,27 @@
+// device.h -- device hierarchy interface (no HIP types; implemented in device.hip)
+#pragma once
+#include <string>
+
+#include "host.h"
+
+namespace mamg {
+
+struct DeviceHandle;
+
+int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
+               std::string* err);
+void dev_destroy(DeviceHandle* h);
+int64_t dev_nrows(const DeviceHandle* h);
+int dev_num_levels(const DeviceHandle* h);
+double dev_apply_bytes(const DeviceHandle* h);
+int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
+int dev_apply_host(DeviceHandle* h, const double* r, double* z, std::string* err);
+int dev_spmv(DeviceHandle* h, const double* d_x, double* d_y, void* stream, std::string* err);
+int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int maxiter,
+            int relativeconv, double* residuals, double* alphas, double* betas,
+            int* niters, void* stream, std::string* err);
+int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, int mode,
+                   double* ms, double* kernel_ms, double* class_bytes, void* stream,
+                   std::string* err);
+
+}  // namespace mamg

@@ -1,0 +1,663 @@
+// device.hip -- CDNA4 (gfx950) apply path of the metric-AMG preconditioner.
+//
+// Replaces the HAZmath multigrid cycle behind `BB * r` (cbc.block operator,
+// one cycle per call: `maxit: 1` /root/reference/src/amg_parameters.py:71,
+// called by ConjGrad /root/reference/src/bidomain_3d.py:149-150) and the
+// cbc.block PCG loop itself (mamg_pcg_device).
+//
+// Layout in HBM (per level l): A_l, P_l, R_l = P_l^T, W_B (level 0 seed-block
+// smoother) as CSR {int64 rowptr, int32 col, fp64 val}; point-smoother weights
+// winv_l[n_l]; the coarsest level's dense inverse (row-major fp64); work
+// vectors t, t2, r, b, x, c, e per level.  Everything stays resident; one apply
+// touches no host memory.
+//
+// Kernels (all HBM-bound, 2 flop per 12 B of matrix):
+//   csr_kernel<VL, EPI, TAG>: row-group CSR SpMV, VL lanes per row (VL a power
+//     of two <= 64, chosen from the mean row length), lanes stride the row's
+//     contiguous (col, val) window with coalesced loads, x gathered through
+//     L2/MALL, the VL partial sums reduced with wavefront shuffles (DPP), and a
+//     fused epilogue: y = s | y += s | r = b - s | x' = x + w (b - s).
+//     TAG separates level-0 launches (distinct kernel symbol per rocprof row).
+//   scale_kernel (first sweep from x = 0), gemv_kernel (coarsest dense solve),
+//   axpy, CG vector kernels, deterministic two-stage dot product.
+// One apply = a fixed schedule of launches (built once per (r, z) pair) that
+// is captured into a hipGraph; each launch carries its algorithmic bytes so
+// roofline numbers come from the hierarchy, not from counters.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "device.h"
+
+namespace mamg {
+namespace {
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      *err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
+      return MAMG_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
+
+enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3 };
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+template <int VL, int EPI, int TAG>
+__global__ __launch_bounds__(256) void csr_kernel(
+    int64_t n, const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x,
+    const double* y, const double* __restrict__ b, const double* __restrict__ w,
+    double* out) {
+  const int lane = threadIdx.x & (VL - 1);
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / VL;
+  double s0 = 0.0, s1 = 0.0;
+  if (row < n) {
+    const int64_t p0 = ptr[row], p1 = ptr[row + 1];
+    int64_t k = p0 + lane;
+    for (; k + VL < p1; k += 2 * VL) {
+      const int32_t c0 = col[k], c1 = col[k + VL];
+      const double v0 = val[k], v1 = val[k + VL];
+      s0 += v0 * x[c0];
+      s1 += v1 * x[c1];
+    }
+    if (k < p1) s0 += val[k] * x[col[k]];
+  }
+  double s = s0 + s1;
+#pragma unroll
+  for (int off = VL / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, VL);
+  if (row < n && lane == 0) {
+    if (EPI == EPI_Y) out[row] = s;
+    else if (EPI == EPI_YADD) out[row] = y[row] + s;
+    else if (EPI == EPI_RESID) out[row] = b[row] - s;
+    else out[row] = y[row] + w[row] * (b[row] - s);
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(int64_t n, const double* __restrict__ w,
+                                                    const double* __restrict__ b,
+                                                    double* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = w[i] * b[i];
+}
+
+__global__ __launch_bounds__(256) void axpy_kernel(int64_t n, const double* __restrict__ e,
+                                                   double* x) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = x[i] + e[i];
+}
+
+// coarsest level: x = Ainv b, one wave per row
+__global__ __launch_bounds__(256) void gemv_kernel(int64_t n, const double* __restrict__ Ainv,
+                                                   const double* __restrict__ b,
+                                                   double* __restrict__ x) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  double s = 0.0;
+  if (row < n) {
+    const double* a = Ainv + row * n;
+    for (int64_t j = lane; j < n; j += 64) s += a[j] * b[j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (row < n && lane == 0) x[row] = s;
+}
+
+// ---- CG vector kernels ------------------------------------------------------
+constexpr int DOT_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void dot_partial_kernel(int64_t n, const double* __restrict__ a,
+                                                          const double* __restrict__ b,
+                                                          double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    s += a[i] * b[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void dot_final_kernel(int nb, const double* __restrict__ part,
+                                                        double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void cg_xr_kernel(int64_t n, double alpha,
+                                                    const double* __restrict__ d,
+                                                    const double* __restrict__ q,
+                                                    double* __restrict__ x,
+                                                    double* __restrict__ r) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    x[i] = x[i] + alpha * d[i];
+    r[i] = r[i] - alpha * q[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void cg_d_kernel(int64_t n, double beta,
+                                                   const double* __restrict__ z,
+                                                   double* __restrict__ d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) d[i] = z[i] + beta * d[i];
+}
+
+__global__ __launch_bounds__(256) void cg_undo_kernel(int64_t n, double alpha,
+                                                      const double* __restrict__ d,
+                                                      double* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = x[i] - alpha * d[i];
+}
+
+inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
+
+// ---------------------------------------------------------------------------
+// device structures
+// ---------------------------------------------------------------------------
+struct DCsr {
+  int64_t n = 0, m = 0, nnz = 0;
+  int64_t* ptr = nullptr;
+  int32_t* col = nullptr;
+  double* val = nullptr;
+  int lanes = 8;
+};
+
+struct DLevel {
+  int64_t n = 0;
+  bool coarsest = false;
+  DCsr A, P, R, WB;
+  double* winv = nullptr;
+  double* Ainv = nullptr;
+  double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr,
+         *c = nullptr, *e = nullptr;
+};
+
+enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3 };
+// kernel classes (kernel_ms / class_bytes slots)
+enum Cls {
+  C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
+  C_L0_SMOOTH = 1,  // post-smooth SpMV on A0 (fused Jacobi, or residual for W_B)
+  C_L0_WB = 2,      // level-0 smoother application (W_B SpMV or scale)
+  C_L0_R = 3,       // level-0 restriction
+  C_L0_P = 4,       // level-0 prolongation
+  C_COARSE = 5,     // all SpMV-class launches on levels >= 1
+  C_DENSE = 6,      // coarsest dense solve
+  C_MISC = 7,       // W-cycle / maxit corrections
+  NCLS = 8
+};
+
+struct Op {
+  int kind = OP_CSR, epi = EPI_Y, cls = 0, tag = 1;
+  const DCsr* M = nullptr;
+  int64_t n = 0;
+  const double *x = nullptr, *y = nullptr, *b = nullptr, *w = nullptr;
+  double* out = nullptr;
+  double bytes = 0.0;
+};
+
+struct Graph {
+  const double* r = nullptr;
+  double* z = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+};
+
+}  // namespace
+
+struct DeviceHandle {
+  mamg_params p;
+  int device = 0;
+  std::vector<DLevel> L;
+  std::vector<void*> allocs;
+  hipStream_t cap = nullptr;
+  std::vector<Graph> graphs;
+  double* hr = nullptr;            // host-apply staging (device)
+  double* hz = nullptr;
+  double *cr = nullptr, *cz = nullptr, *cd = nullptr, *cq = nullptr;  // PCG
+  double* part = nullptr;
+  double* dres = nullptr;
+  double* hres = nullptr;          // pinned host scalar
+  double apply_bytes = 0.0;
+  ~DeviceHandle() {
+    for (auto& g : graphs) {
+      if (g.exec) (void)hipGraphExecDestroy(g.exec);
+      if (g.graph) (void)hipGraphDestroy(g.graph);
+    }
+    for (void* a : allocs) (void)hipFree(a);
+    if (hres) (void)hipHostFree(hres);
+    if (cap) (void)hipStreamDestroy(cap);
+  }
+};
+
+namespace {
+
+template <class T>
+int dalloc(DeviceHandle* h, T** p, int64_t count, std::string* err) {
+  *p = nullptr;
+  if (count <= 0) return MAMG_OK;
+  void* q = nullptr;
+  HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
+  h->allocs.push_back(q);
+  *p = (T*)q;
+  return MAMG_OK;
+}
+
+int pick_lanes(int64_t n, int64_t nnz) {
+  const double avg = n ? (double)nnz / (double)n : 1.0;
+  int l = 2;
+  while (l < 64 && 2.0 * l <= avg) l *= 2;
+  return l;
+}
+
+int upload_csr(DeviceHandle* h, const CsrView& M, DCsr* D, int lanes, std::string* err) {
+  D->n = M.n;
+  D->m = M.m;
+  D->nnz = M.nnz();
+  D->lanes = lanes > 0 ? lanes : pick_lanes(M.n, D->nnz);
+  int rc;
+  if ((rc = dalloc(h, &D->ptr, M.n + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nnz, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nnz, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, M.ptr, (M.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (D->nnz) {
+    HIPCHK(hipMemcpy(D->col, M.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, M.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+
+// ---- algorithmic bytes ------------------------------------------
+double csr_bytes(const DCsr& M, int epi) {
+  double b = 12.0 * M.nnz + 8.0 * (M.n + 1) + 8.0 * M.m + 8.0 * M.n;  // A, x, out
+  if (epi == EPI_YADD) b += 8.0 * M.n;
+  if (epi == EPI_RESID) b += 8.0 * M.n;
+  if (epi == EPI_JACOBI) b += 16.0 * M.n;
+  return b;
+}
+
+Op csr_op(const DCsr& M, int epi, int cls, int tag, const double* x, const double* y,
+          const double* b, const double* w, double* out) {
+  Op o;
+  o.kind = OP_CSR; o.epi = epi; o.cls = cls; o.tag = tag; o.M = &M; o.n = M.n;
+  o.x = x; o.y = y; o.b = b; o.w = w; o.out = out;
+  o.bytes = csr_bytes(M, epi);
+  return o;
+}
+
+// cycle from zero initial guess: xout = MG_l(b)
+void cycle_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
+  const DLevel& L = h->L[l];
+  const mamg_params& p = h->p;
+  const bool l0 = l == 0;
+  if (L.coarsest) {
+    Op o;
+    o.kind = OP_GEMV; o.cls = C_DENSE; o.n = L.n; o.x = b; o.w = L.Ainv; o.out = xout;
+    o.bytes = 8.0 * L.n * L.n + 16.0 * L.n;
+    ops->push_back(o);
+    return;
+  }
+  const DLevel& C = h->L[l + 1];
+  const bool blk = L.WB.n > 0;
+  const int tagA = l0 ? 0 : 1;
+  const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
+  const int clsW = l0 ? C_L0_WB : C_COARSE;
+  double* X = L.t;
+  double* X2 = L.t2;
+  // first pre-smoothing sweep from x = 0
+  if (blk) {
+    ops->push_back(csr_op(L.WB, EPI_Y, clsW, tagA, b, nullptr, nullptr, nullptr, X));
+  } else {
+    Op o;
+    o.kind = OP_SCALE; o.cls = clsW; o.n = L.n; o.w = L.winv; o.x = b; o.out = X;
+    o.bytes = 24.0 * L.n;
+    ops->push_back(o);
+  }
+  for (int s = 1; s < p.presmooth_iter; ++s) {
+    if (blk) {
+      ops->push_back(csr_op(L.A, EPI_RESID, clsS, tagA, X, nullptr, b, nullptr, L.r));
+      ops->push_back(csr_op(L.WB, EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, X2));
+    } else {
+      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, L.winv, X2));
+    }
+    std::swap(X, X2);
+  }
+  // residual, restriction, coarse cycle(s), prolongation
+  ops->push_back(csr_op(L.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, nullptr, b, nullptr, L.r));
+  ops->push_back(csr_op(L.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, nullptr, nullptr, nullptr, C.b));
+  cycle_ops(h, l + 1, C.b, C.x, ops);
+  if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
+    ops->push_back(csr_op(C.A, EPI_RESID, C_MISC, 1, C.x, nullptr, C.b, nullptr, C.c));
+    cycle_ops(h, l + 1, C.c, C.e, ops);
+    Op o;
+    o.kind = OP_AXPY; o.cls = C_MISC; o.n = C.n; o.x = C.e; o.out = C.x; o.bytes = 24.0 * C.n;
+    ops->push_back(o);
+  }
+  ops->push_back(csr_op(L.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, X, nullptr, nullptr, X));
+  // post-smoothing; the last sweep writes xout
+  for (int s = 0; s < p.postsmooth_iter; ++s) {
+    double* out = (s == p.postsmooth_iter - 1) ? xout : X2;
+    if (blk) {
+      ops->push_back(csr_op(L.A, EPI_RESID, clsS, tagA, X, nullptr, b, nullptr, L.r));
+      ops->push_back(csr_op(L.WB, EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, out));
+    } else {
+      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, L.winv, out));
+    }
+    if (out == X2) std::swap(X, X2);
+  }
+}
+
+void apply_ops(const DeviceHandle* h, const double* r, double* z, std::vector<Op>* ops) {
+  ops->clear();
+  cycle_ops(h, 0, r, z, ops);
+  const DLevel& L0 = h->L[0];
+  for (int it = 1; it < h->p.maxit; ++it) {   // z += MG(r - A z)
+    ops->push_back(csr_op(L0.A, EPI_RESID, C_MISC, 1, z, nullptr, r, nullptr, L0.c));
+    cycle_ops(h, 0, L0.c, L0.e, ops);
+    Op o;
+    o.kind = OP_AXPY; o.cls = C_MISC; o.n = L0.n; o.x = L0.e; o.out = z; o.bytes = 24.0 * L0.n;
+    ops->push_back(o);
+  }
+}
+
+template <int VL, int TAG>
+void launch_csr_vl(const Op& o, hipStream_t s) {
+  const DCsr& M = *o.M;
+  const unsigned g = nblocks(M.n * (int64_t)VL);
+  if (g == 0) return;
+  switch (o.epi) {
+    case EPI_Y:
+      csr_kernel<VL, EPI_Y, TAG><<<g, 256, 0, s>>>(M.n, M.ptr, M.col, M.val, o.x, o.y, o.b, o.w, o.out);
+      break;
+    case EPI_YADD:
+      csr_kernel<VL, EPI_YADD, TAG><<<g, 256, 0, s>>>(M.n, M.ptr, M.col, M.val, o.x, o.y, o.b, o.w, o.out);
+      break;
+    case EPI_RESID:
+      csr_kernel<VL, EPI_RESID, TAG><<<g, 256, 0, s>>>(M.n, M.ptr, M.col, M.val, o.x, o.y, o.b, o.w, o.out);
+      break;
+    default:
+      csr_kernel<VL, EPI_JACOBI, TAG><<<g, 256, 0, s>>>(M.n, M.ptr, M.col, M.val, o.x, o.y, o.b, o.w, o.out);
+      break;
+  }
+}
+
+template <int TAG>
+void launch_csr_tag(const Op& o, hipStream_t s) {
+  switch (o.M->lanes) {
+    case 2: launch_csr_vl<2, TAG>(o, s); break;
+    case 4: launch_csr_vl<4, TAG>(o, s); break;
+    case 8: launch_csr_vl<8, TAG>(o, s); break;
+    case 16: launch_csr_vl<16, TAG>(o, s); break;
+    case 32: launch_csr_vl<32, TAG>(o, s); break;
+    default: launch_csr_vl<64, TAG>(o, s); break;
+  }
+}
+
+void launch(const Op& o, hipStream_t s) {
+  switch (o.kind) {
+    case OP_CSR:
+      if (o.tag == 0) launch_csr_tag<0>(o, s); else launch_csr_tag<1>(o, s);
+      break;
+    case OP_SCALE:
+      if (o.n) scale_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.w, o.x, o.out);
+      break;
+    case OP_AXPY:
+      if (o.n) axpy_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.x, o.out);
+      break;
+    case OP_GEMV:
+      if (o.n) gemv_kernel<<<(unsigned)((o.n + 3) / 4), 256, 0, s>>>(o.n, o.w, o.x, o.out);
+      break;
+  }
+}
+
+int get_graph(DeviceHandle* h, const double* r, double* z, hipGraphExec_t* exec, std::string* err) {
+  for (auto& g : h->graphs)
+    if (g.r == r && g.z == z) { *exec = g.exec; return MAMG_OK; }
+  if (h->graphs.size() >= 16) {   // evict oldest
+    auto& g = h->graphs.front();
+    (void)hipGraphExecDestroy(g.exec);
+    (void)hipGraphDestroy(g.graph);
+    h->graphs.erase(h->graphs.begin());
+  }
+  std::vector<Op> ops;
+  apply_ops(h, r, z, &ops);
+  Graph g;
+  g.r = r; g.z = z;
+  HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
+  for (const Op& o : ops) launch(o, h->cap);
+  HIPCHK(hipStreamEndCapture(h->cap, &g.graph));
+  HIPCHK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+  h->graphs.push_back(g);
+  *exec = g.exec;
+  return MAMG_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
+               std::string* err) {
+  std::unique_ptr<DeviceHandle> h(new DeviceHandle());
+  h->p = p;
+  h->device = p.device;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (ndev <= 0) { *err = "no HIP device"; return MAMG_ERR_HIP; }
+  HIPCHK(hipSetDevice(p.device));
+  HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
+  const int nl = (int)H.levels.size();
+  h->L.resize(nl);
+  int rc;
+  for (int l = 0; l < nl; ++l) {
+    const HostLevel& hl = H.levels[l];
+    DLevel& D = h->L[l];
+    D.n = hl.n;
+    D.coarsest = hl.coarsest;
+    if (D.coarsest) {
+      if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
+      HIPCHK(hipMemcpy(D.Ainv, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
+      if (l > 0 && (rc = upload_csr(h.get(), H.A(l), &D.A, 0, err))) return rc;
+      if (l == 0 && (rc = upload_csr(h.get(), A0, &D.A, p.spmv_lanes, err))) return rc;
+    } else {
+      if ((rc = upload_csr(h.get(), l == 0 ? A0 : H.A(l), &D.A, l == 0 ? p.spmv_lanes : 0, err)))
+        return rc;
+      if ((rc = upload_csr(h.get(), hl.P.view(), &D.P, 0, err))) return rc;
+      if ((rc = upload_csr(h.get(), hl.R.view(), &D.R, 0, err))) return rc;
+      if (hl.WB.n > 0) {
+        if ((rc = upload_csr(h.get(), hl.WB.view(), &D.WB, 0, err))) return rc;
+      } else {
+        if ((rc = dalloc(h.get(), &D.winv, D.n, err))) return rc;
+        HIPCHK(hipMemcpy(D.winv, hl.winv.data(), D.n * sizeof(double), hipMemcpyHostToDevice));
+      }
+    }
+    double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
+    for (double** v : vecs)
+      if ((rc = dalloc(h.get(), v, D.n, err))) return rc;
+  }
+  const int64_t n0 = h->L[0].n;
+  double** v0[] = {&h->hr, &h->hz};
+  for (double** v : v0)
+    if ((rc = dalloc(h.get(), v, n0, err))) return rc;
+  std::vector<Op> ops;
+  apply_ops(h.get(), h->hr, h->hz, &ops);
+  for (const Op& o : ops) h->apply_bytes += o.bytes;
+  HIPCHK(hipDeviceSynchronize());
+  *out = h.release();
+  return MAMG_OK;
+}
+
+void dev_destroy(DeviceHandle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  delete h;
+}
+
+int64_t dev_nrows(const DeviceHandle* h) { return h->L[0].n; }
+int dev_num_levels(const DeviceHandle* h) { return (int)h->L.size(); }
+double dev_apply_bytes(const DeviceHandle* h) { return h->apply_bytes; }
+
+int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
+  if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
+  HIPCHK(hipSetDevice(h->device));
+  hipGraphExec_t exec;
+  int rc = get_graph(h, d_r, d_z, &exec, err);
+  if (rc) return rc;
+  HIPCHK(hipGraphLaunch(exec, (hipStream_t)stream));
+  return MAMG_OK;
+}
+
+int dev_apply_host(DeviceHandle* h, const double* r, double* z, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  const int64_t n = h->L[0].n;
+  HIPCHK(hipMemcpyAsync(h->hr, r, n * sizeof(double), hipMemcpyHostToDevice, h->cap));
+  hipGraphExec_t exec;
+  int rc = get_graph(h, h->hr, h->hz, &exec, err);
+  if (rc) return rc;
+  HIPCHK(hipGraphLaunch(exec, h->cap));
+  HIPCHK(hipMemcpyAsync(z, h->hz, n * sizeof(double), hipMemcpyDeviceToHost, h->cap));
+  HIPCHK(hipStreamSynchronize(h->cap));
+  return MAMG_OK;
+}
+
+int dev_spmv(DeviceHandle* h, const double* d_x, double* d_y, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  const DLevel& L0 = h->L[0];
+  launch(csr_op(L0.A, EPI_Y, C_MISC, 1, d_x, nullptr, nullptr, nullptr, d_y), (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+namespace {
+int dot(DeviceHandle* h, int64_t n, const double* a, const double* b, hipStream_t s, double* out,
+        std::string* err) {
+  dot_partial_kernel<<<DOT_BLOCKS, 256, 0, s>>>(n, a, b, h->part);
+  dot_final_kernel<<<1, 256, 0, s>>>(DOT_BLOCKS, h->part, h->dres);
+  HIPCHK(hipMemcpyAsync(h->hres, h->dres, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *out = *h->hres;
+  return MAMG_OK;
+}
+}  // namespace
+
+int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int maxiter,
+            int relativeconv, double* residuals, double* alphas, double* betas, int* niters,
+            void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = h->L[0].n;
+  int rc;
+  if (!h->cr) {
+    double** v[] = {&h->cr, &h->cz, &h->cd, &h->cq};
+    for (double** q : v)
+      if ((rc = dalloc(h, q, n, err))) return rc;
+    if ((rc = dalloc(h, &h->part, DOT_BLOCKS, err))) return rc;
+    if ((rc = dalloc(h, &h->dres, 1, err))) return rc;
+    HIPCHK(hipHostMalloc((void**)&h->hres, sizeof(double), hipHostMallocDefault));
+  }
+  const DLevel& L0 = h->L[0];
+  const unsigned g = nblocks(n);
+  launch(csr_op(L0.A, EPI_RESID, C_MISC, 1, d_x, nullptr, d_b, nullptr, h->cr), s);  // r = b - A x
+  if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;                          // z = B r
+  HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  double rz;
+  if ((rc = dot(h, n, h->cr, h->cz, s, &rz, err))) return rc;
+  if (rz < 0) { *err = "Matrix is not positive"; *niters = 0; return MAMG_ERR_BREAKDOWN; }
+  residuals[0] = std::sqrt(rz);
+  const double tol_eff = relativeconv ? tol * residuals[0] : tol;
+  int it = 0;
+  int status = MAMG_OK;
+  while (residuals[it] > tol_eff && it < maxiter) {
+    launch(csr_op(L0.A, EPI_Y, C_MISC, 1, h->cd, nullptr, nullptr, nullptr, h->cq), s);  // q = A d
+    double dz;
+    if ((rc = dot(h, n, h->cd, h->cq, s, &dz, err))) return rc;
+    if (dz == 0.0) break;
+    const double alpha = rz / dz;
+    cg_xr_kernel<<<g, 256, 0, s>>>(n, alpha, h->cd, h->cq, d_x, h->cr);
+    if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;
+    const double rz_prev = rz;
+    if ((rc = dot(h, n, h->cr, h->cz, s, &rz, err))) return rc;
+    if (rz < 0) {
+      cg_undo_kernel<<<g, 256, 0, s>>>(n, alpha, h->cd, d_x);
+      *err = "ConjGrad breakdown (<r,Br> < 0)";
+      status = MAMG_ERR_BREAKDOWN;
+      break;
+    }
+    const double beta = rz / rz_prev;
+    cg_d_kernel<<<g, 256, 0, s>>>(n, beta, h->cz, h->cd);
+    residuals[it + 1] = std::sqrt(rz);
+    alphas[it] = alpha;
+    betas[it] = beta;
+    ++it;
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipGetLastError());
+  *niters = it;
+  return status;
+}
+
+int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
+                   double* kernel_ms, double* class_bytes, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<Op> ops;
+  apply_ops(h, d_r, d_z, &ops);
+  if (class_bytes) {
+    for (int c = 0; c < 16; ++c) class_bytes[c] = 0.0;
+    for (const Op& o : ops) class_bytes[o.cls] += o.bytes;
+  }
+  if (reps <= 0) { *ms = 0.0; return MAMG_OK; }
+  // events: per rep, per instrumented op, one (start, end) pair
+  std::vector<int> inst;
+  for (size_t k = 0; k < ops.size(); ++k)
+    if (mode == 1 || ops[k].cls == C_L0_RESID) inst.push_back((int)k);
+  std::vector<hipEvent_t> ev(2 * inst.size() * (size_t)reps + 2);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(ev[0], s));
+  size_t q = 2;
+  for (int rp = 0; rp < reps; ++rp) {
+    size_t ii = 0;
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const bool timed = ii < inst.size() && inst[ii] == (int)k;
+      if (timed) HIPCHK(hipEventRecord(ev[q], s));
+      launch(ops[k], s);
+      if (timed) { HIPCHK(hipEventRecord(ev[q + 1], s)); q += 2; ++ii; }
+    }
+  }
+  HIPCHK(hipEventRecord(ev[1], s));
+  HIPCHK(hipEventSynchronize(ev[1]));
+  HIPCHK(hipGetLastError());
+  float tot = 0.f;
+  HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[1]));
+  *ms = tot / reps;
+  if (kernel_ms) {
+    for (int c = 0; c < 16; ++c) kernel_ms[c] = 0.0;
+    q = 2;
+    for (int rp = 0; rp < reps; ++rp)
+      for (size_t ii = 0; ii < inst.size(); ++ii) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, ev[q], ev[q + 1]));
+        kernel_ms[ops[inst[ii]].cls] += t / reps;
+        q += 2;
+      }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return MAMG_OK;
+}
+
+}  // namespace mamg

@@ -1,0 +1,82 @@
+// host.h -- host-side data structures of the metric-AMG hierarchy.
+//
+// The host setup restates the oracle's algorithm (oracle/mamg_oracle.py) as a
+// fixed sequence of IEEE binary64 operations; this translation unit family is
+// compiled with -ffp-contract=off so that the hierarchy is bitwise identical
+// to the oracle's (tests/test_host_setup.py checks this).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mamg.h"
+
+namespace mamg {
+
+struct CsrView {            // non-owning (caller's level-0 matrix)
+  int64_t n = 0, m = 0;
+  const int64_t* ptr = nullptr;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  int64_t nnz() const { return n ? ptr[n] : 0; }
+};
+
+struct Csr {                // owning
+  int64_t n = 0, m = 0;
+  std::vector<int64_t> ptr;
+  std::vector<int32_t> col;
+  std::vector<double> val;
+  int64_t nnz() const { return ptr.empty() ? 0 : ptr[n]; }
+  CsrView view() const {
+    CsrView v;
+    v.n = n; v.m = m; v.ptr = ptr.data(); v.col = col.data(); v.val = val.data();
+    return v;
+  }
+};
+
+struct HostLevel {
+  Csr A;                    // level 0: empty (the caller's matrix is used)
+  std::vector<double> winv; // point smoother weights (empty if WB used)
+  Csr WB;                   // seed-block smoother (level 0 with idofs)
+  Csr P, R;                 // prolongation / restriction (R = P^T)
+  std::vector<int64_t> agg; // aggregate id per row (-1 isolated)
+  int64_t nagg = 0;
+  double w_sa = 0.0;
+  std::vector<double> Ainv; // dense inverse on the coarsest level (row-major)
+  bool coarsest = false;
+  int64_t n = 0;
+};
+
+struct Hierarchy {
+  mamg_params params;
+  CsrView A0;               // level-0 matrix (caller-owned during setup)
+  std::vector<HostLevel> levels;
+  CsrView A(int l) const { return l == 0 ? A0 : levels[l].A.view(); }
+};
+
+// setup.cpp
+int host_setup(const CsrView& A, const int32_t* idofs, int64_t n_idofs,
+               const mamg_params& p, Hierarchy* out, std::string* err);
+int check_params(const mamg_params& p, std::string* err);
+
+// gen.cpp
+int gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz);
+int gen_bidomain(int dim, int64_t n, double gamma, double k1, double k2,
+                 int64_t* rowptr, int32_t* colind, double* values);
+
+// hash shared with the oracle (oracle/mamg_oracle.py:hash32)
+inline uint32_t hash32(uint64_t i, int level) {
+  uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
+  uint32_t lv = (uint32_t)(((uint64_t)(int64_t)level * 0x85EBCA77ull) & 0xFFFFFFFFull);
+  x = x * 0x9E3779B1u + lv;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+void set_error(const std::string& s);
+
+}  // namespace mamg

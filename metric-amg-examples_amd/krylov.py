@@ -1,0 +1,148 @@
+"""ConjGrad with cbc.block semantics, driving the GPU preconditioner.
+
+Reference use (/root/reference/src/bidomain_3d.py:149-160):
+    AAinv = ConjGrad(AA_, precond=BB, tolerance=1E-8, show=4, maxiter=500,
+                     callback=cbk)
+    xx = AAinv * bb_
+    niters = len(AAinv.residuals) - 1
+    r_norm = AAinv.residuals[-1]
+    eigenvalues = AAinv.eigenvalue_estimates()
+cbc.block ``cgN`` [ext, recalled]: residuals are sqrt(<r, B r>), the
+tolerance is absolute unless relativeconv, x0 = 0 unless initial_guess,
+breakdown when <r, B r> < 0 (x restored) or <d, A d> == 0.
+
+When ``precond`` is a MetricAMG built on the same operator and no callback
+is given, the whole loop runs device-resident (``mamg_pcg_device``: level-0
+SpMV, fused CG vector kernels, deterministic dots, hipGraph V-cycle);
+otherwise the loop runs on the host with one ``B * r`` per iteration through
+the C-ABI, exactly like the reference's cbc.block loop.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .amg import MetricAMG
+
+
+def lanczos_eigenvalues(alphas, betas):
+    """Eigenvalues of the CG Lanczos tridiagonal (cbc.block
+    eigenvalue_estimates): T00 = 1/a0, Tkk = 1/ak + b(k-1)/a(k-1),
+    T(k,k-1) = sqrt(b(k-1))/a(k-1)."""
+    n = len(alphas)
+    if n == 0:
+        return np.array([1.0])
+    T = np.zeros((n, n))
+    T[0, 0] = 1.0 / alphas[0]
+    for k in range(1, n):
+        T[k, k] = 1.0 / alphas[k] + betas[k - 1] / alphas[k - 1]
+        T[k, k - 1] = np.sqrt(betas[k - 1]) / alphas[k - 1]
+        T[k - 1, k] = T[k, k - 1]
+    return np.sort(np.linalg.eigvalsh(T))
+
+
+class ConjGrad:
+    def __init__(self, A, precond=None, tolerance=1e-5, initial_guess=None, maxiter=200,
+                 show=1, callback=None, relativeconv=False, device=None, **kwargs):
+        self.A = A
+        self.B = precond
+        self.tolerance = float(tolerance)
+        self.initial_guess = initial_guess
+        self.maxiter = int(maxiter)
+        self.show = show
+        self.callback = callback
+        self.relativeconv = bool(relativeconv)
+        self.device = device
+        self.residuals, self.alphas, self.betas = [], [], []
+        self.breakdown = False
+
+    # ------------------------------------------------------------------
+    def _device_ok(self):
+        if self.device is False or self.callback is not None:
+            return False
+        B = self.B
+        return isinstance(B, MetricAMG) and B._Aop is self.A
+
+    def __mul__(self, b):
+        if self._device_ok() or self.device is True:
+            return self._solve_device(b)
+        return self._solve_host(b)
+
+    def _solve_device(self, b):
+        import torch
+        B = self.B
+        n = B.shape[0]
+        bt = torch.as_tensor(np.ascontiguousarray(b, dtype=np.float64)).cuda()
+        x0 = np.zeros(n) if self.initial_guess is None else np.asarray(self.initial_guess, np.float64)
+        xt = torch.as_tensor(np.ascontiguousarray(x0)).cuda()
+        res = np.zeros(self.maxiter + 1)
+        al = np.zeros(max(self.maxiter, 1))
+        be = np.zeros(max(self.maxiter, 1))
+        it = C.c_int(0)
+        stream = torch.cuda.current_stream()
+        rc = B._L.mamg_pcg_device(B.handle, C.c_void_p(bt.data_ptr()), C.c_void_p(xt.data_ptr()),
+                                  self.tolerance, self.maxiter, int(self.relativeconv),
+                                  _lib.ptr(res, C.c_double), _lib.ptr(al, C.c_double),
+                                  _lib.ptr(be, C.c_double), C.byref(it),
+                                  C.c_void_p(stream.cuda_stream))
+        k = it.value
+        if rc == _lib.ERR_BREAKDOWN:
+            self.breakdown = True
+            warnings.warn('ConjGrad breakdown: ' + B._L.mamg_last_error().decode())
+            if k == 0 and res[0] == 0.0:
+                raise ValueError('Matrix is not positive')
+        else:
+            _lib.check(rc)
+        self.residuals = list(res[:k + 1])
+        self.alphas = list(al[:k])
+        self.betas = list(be[:k])
+        torch.cuda.synchronize()
+        return xt.cpu().numpy()
+
+    def _solve_host(self, b):
+        A, B = self.A, self.B
+        applyB = (lambda r: B * r) if B is not None else (lambda r: r.copy())
+        x = np.zeros_like(b) if self.initial_guess is None else np.array(self.initial_guess, np.float64)
+        r = b - A @ x
+        z = applyB(r)
+        d = z.copy()
+        rz = float(np.dot(r, z))
+        if rz < 0:
+            raise ValueError('Matrix is not positive')
+        residuals = [np.sqrt(rz)]
+        alphas, betas = [], []
+        tol = self.tolerance * residuals[0] if self.relativeconv else self.tolerance
+        it = 0
+        while residuals[-1] > tol and it < self.maxiter:
+            z = A @ d
+            dz = float(np.dot(d, z))
+            if dz == 0:
+                self.breakdown = True
+                break
+            alpha = rz / dz
+            x = x + alpha * d
+            r = r - alpha * z
+            z = applyB(r)
+            rz_prev = rz
+            rz = float(np.dot(r, z))
+            if rz < 0:
+                self.breakdown = True
+                warnings.warn('ConjGrad breakdown')
+                x = x - alpha * d
+                break
+            beta = rz / rz_prev
+            d = z + beta * d
+            residuals.append(np.sqrt(rz))
+            alphas.append(alpha)
+            betas.append(beta)
+            if self.callback is not None:
+                self.callback(k=it, x=x, r=r)
+            it += 1
+        self.residuals, self.alphas, self.betas = residuals, alphas, betas
+        return x
+
+    def eigenvalue_estimates(self):
+        return lanczos_eigenvalues(self.alphas, self.betas)

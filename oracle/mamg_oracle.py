@@ -1,0 +1,769 @@
+"""CPU restatement of the metric-AMG hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` may import this module.  The product (``metric-amg-examples_amd``)
+never imports, links or calls it; it is the *checker*.
+
+PARITY STATUS: **parity unpinned** against the reference.
+The reference (anabudisa/metric-amg-examples) contains no solver code; the
+hot path lives in HAZmath (C) behind cbc.block / haznics, none of which is in
+``/root/reference`` or installable here.  There are no golden vectors,
+recorded iteration counts or KATs in the reference.  This oracle therefore
+restates a *precisely specified* algorithm profile ("mi355x_sa_v")
+built from the reference's own call sites and parameter dictionaries, and is
+itself pinned only by hand-checkable known-answer tests
+(``tests/test_oracle.py``: 1-D Laplacian aggregation/RAP, P1 stencils, CG on
+scipy's direct solve).
+
+Reference anchors (file:line in /root/reference):
+  * matrix definition        src/bidomain_2d.py:51-99  (a00/a01/a10/a11 :64-68,
+                             Dirichlet tags (1,2) :73), 3-D reuse
+                             src/bidomain_3d.py:119, BC faces src/utils.py:159-160,
+                             177-178; defaults kappa1=2, kappa2=3
+                             src/bidomain_3d.py:64-65
+  * monolithic block order   src/bidomain_3d.py:124,138,154-155  ([u1; u2])
+  * interface dofs           src/bidomain_3d.py:138 (all u2 dofs)
+  * parameter keys           src/amg_parameters.py:67-89, src/utils.py:60-82
+  * PCG call                 src/bidomain_3d.py:149-160 (tol 1e-8, maxiter 500,
+                             niters = len(residuals)-1, cond from Lanczos)
+  * [ext] cbc.block ``cgN``  preconditioned residual sqrt(<r,Br>), absolute
+                             tolerance, eigenvalue estimates from the CG
+                             alpha/beta tridiagonal (recalled; not in repo)
+
+Floating-point contract (what makes the product's setup *bitwise* equal to
+this oracle): every setup quantity is a fixed sequence of IEEE-754 binary64
+operations -- no FMA contraction, sums accumulated sequentially in CSR order
+starting from 0.0 (scipy's ``csr_matvec``/``csr_matmat`` order), exact zeros
+produced by cancellation in a sparse product/difference dropped (scipy's
+rule), row entries kept sorted by column.
+"""
+from __future__ import annotations
+
+import dataclasses
+import numpy as np
+import scipy.sparse as sp
+
+# --------------------------------------------------------------------------
+# deterministic hash (MIS-2 priorities); same uint32 arithmetic in C++/HIP
+# --------------------------------------------------------------------------
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def hash32(i, level: int) -> np.ndarray:
+    """lowbias-style integer hash of (index, level) -> uint32."""
+    x = (np.asarray(i, dtype=np.uint64) & _M32)
+    lv = np.uint64((int(level) * 0x85EBCA77) & 0xFFFFFFFF)
+    x = (x * np.uint64(0x9E3779B1) + lv) & _M32
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & _M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & _M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+# --------------------------------------------------------------------------
+# problem generator: bidomain P1 on dolfin's structured meshes
+# --------------------------------------------------------------------------
+# Kuhn (path-simplex) split: every cell is a monotone lattice path from the
+# cell's lower corner to its upper corner.  dolfin UnitSquareMesh(n,n) 'right'
+# = paths (x,y),(y,x); UnitCubeMesh(n,n,n) = the 6 axis permutations.
+_K_PATH = {2: np.array([[1, -1, 0], [-1, 2, -1], [0, -1, 1]], dtype=np.int64),
+           3: np.array([[1, -1, 0, 0], [-1, 2, -1, 0], [0, -1, 2, -1],
+                        [0, 0, -1, 1]], dtype=np.int64)}
+
+
+def _paths(dim):
+    import itertools
+    return list(itertools.permutations(range(dim)))
+
+
+def p1_integer_stencils(dim: int, n: int):
+    """Integer-count stiffness (cK) and mass (cM) matrices on the vertex graph.
+
+    K = kfac * cK with kfac = h/6 (3-D) or 1/2 (2-D); M = mfac * cM with
+    mfac = h^3/120 (3-D) or h^2/24 (2-D).  Counts are exact integers, so the
+    assembled values do not depend on assembly order.
+    Returns (indptr, indices, cK, cM) CSR over nv=(n+1)^dim vertices, sorted.
+    """
+    nn = n + 1
+    nv = nn ** dim
+    stride = [1, nn, nn * nn][:dim]
+    cells0 = np.arange(n ** dim, dtype=np.int64)
+    # lower-corner vertex index of each cell
+    coords = []
+    rem = cells0.copy()
+    for d in range(dim):
+        coords.append(rem % n)
+        rem //= n
+    base = np.zeros_like(cells0)
+    for d in range(dim):
+        base += coords[d] * stride[d]
+    Kloc = _K_PATH[dim]
+    rows, cols, ck, cm = [], [], [], []
+    for path in _paths(dim):
+        verts = [base]
+        cur = base
+        for ax in path:
+            cur = cur + stride[ax]
+            verts.append(cur)
+        for a in range(dim + 1):
+            for b in range(dim + 1):
+                rows.append(verts[a])
+                cols.append(verts[b])
+                ck.append(np.full(base.shape, Kloc[a, b], dtype=np.int64))
+                cm.append(np.full(base.shape, 2 if a == b else 1, dtype=np.int64))
+    key = np.concatenate(rows) * nv + np.concatenate(cols)
+    uniq, inv = np.unique(key, return_inverse=True)       # sorted (row, col)
+    cKv = np.bincount(inv, weights=np.concatenate(ck)).round().astype(np.int64)
+    cMv = np.bincount(inv, weights=np.concatenate(cm)).round().astype(np.int64)
+    r, c = uniq // nv, uniq % nv
+    indptr = np.zeros(nv + 1, dtype=np.int64)
+    np.add.at(indptr, r + 1, 1)
+    indptr = np.cumsum(indptr)
+    # pattern = mass pattern (every vertex pair sharing a cell; cM >= 1)
+    return indptr, c.astype(np.int64), cKv, cMv
+
+
+def bc_vertices(dim: int, n: int) -> np.ndarray:
+    """Dirichlet vertices: x=0,1 in 2-D (tags 1,2, src/utils.py:159-160);
+    z=0,1 in 3-D (tags 1,2, src/utils.py:177-178)."""
+    nn = n + 1
+    v = np.arange(nn ** dim, dtype=np.int64)
+    if dim == 2:
+        ax = v % nn                      # x coordinate index
+    else:
+        ax = v // (nn * nn)              # z coordinate index
+    return (ax == 0) | (ax == n)
+
+
+def bidomain_system(dim: int, n: int, gamma: float, kappa1: float = 2.0,
+                    kappa2: float = 3.0):
+    """Monolithic bidomain matrix [[k1 K + g M, -g M], [-g M, k2 K + g M]].
+
+    Block order [u1; u2] as ii_convert produces (src/bidomain_3d.py:124,138).
+    Dirichlet dofs (both fields) are eliminated symmetrically: row/column
+    removed, diagonal 1.0.  Returns dict(A=csr, nv=, idofs=, bc=).
+    """
+    indptr, indices, cK, cM = p1_integer_stencils(dim, n)
+    nv = len(indptr) - 1
+    h = 1.0 / n
+    if dim == 3:
+        kf1 = kappa1 * h / 6.0
+        kf2 = kappa2 * h / 6.0
+        mf = gamma * h * h * h / 120.0
+    else:
+        kf1 = kappa1 / 2.0
+        kf2 = kappa2 / 2.0
+        mf = gamma * h * h / 24.0
+    fK = cK.astype(np.float64)
+    fM = cM.astype(np.float64)
+    a11 = kf1 * fK + mf * fM
+    a22 = kf2 * fK + mf * fM
+    a12 = -(mf * fM)
+    rlen = np.diff(indptr)
+    r = np.repeat(np.arange(nv, dtype=np.int64), rlen)
+    c = indices
+    rows = np.concatenate([r, r, r + nv, r + nv])
+    cols = np.concatenate([c, c + nv, c, c + nv])
+    vals = np.concatenate([a11, a12, a12, a22])
+    bcv = bc_vertices(dim, n)
+    isbc = np.concatenate([bcv, bcv])
+    keep = ~(isbc[rows] | isbc[cols])
+    d = np.flatnonzero(isbc)
+    rows = np.concatenate([rows[keep], d])
+    cols = np.concatenate([cols[keep], d])
+    vals = np.concatenate([vals[keep], np.ones(len(d))])
+    N = 2 * nv
+    A = _csr_from_coo_unique(rows, cols, vals, N, N)
+    idofs = np.arange(nv, 2 * nv, dtype=np.int32)
+    return dict(A=A, nv=nv, idofs=idofs, bc=isbc, dim=dim, n=n, gamma=gamma)
+
+
+def _csr_from_coo_unique(rows, cols, vals, nr, nc):
+    order = np.lexsort((cols, rows))
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    indptr = np.zeros(nr + 1, dtype=np.int64)
+    np.add.at(indptr, rows + 1, 1)
+    indptr = np.cumsum(indptr)
+    A = sp.csr_matrix((vals.astype(np.float64), cols.astype(np.int64), indptr),
+                      shape=(nr, nc))
+    A.has_sorted_indices = True
+    return A
+
+
+def laplace1d(n: int) -> sp.csr_matrix:
+    """Tridiagonal [-1 2 -1] (KAT input)."""
+    A = sp.diags([-np.ones(n - 1), 2 * np.ones(n), -np.ones(n - 1)], [-1, 0, 1],
+                 format='csr')
+    A.sort_indices()
+    return A
+
+
+# --------------------------------------------------------------------------
+# setup
+# --------------------------------------------------------------------------
+@dataclasses.dataclass
+class Params:
+    """Algorithm profile; keys mirror src/amg_parameters.py:67-89 names."""
+    AMG_type: str = 'SA'          # 'SA' | 'UA'
+    cycle_type: str = 'V'         # 'V' | 'W'
+    max_levels: int = 20
+    maxit: int = 1
+    smoother: str = 'JACOBI_RHO'  # 'L1DIAG' | 'JACOBI' | 'JACOBI_RHO'
+    relaxation: float = 4.0 / 3.0
+    presmooth_iter: int = 1
+    postsmooth_iter: int = 1
+    coarse_dof: int = 100
+    strong_coupled: float = 0.0   # SoC threshold theta
+    Schwarz_levels: int = 1       # 1: seed-block Jacobi on level 0 (needs idofs)
+    Schwarz_mmsize: int = 100     # max dofs per seed block
+    sa_omega: float = 4.0 / 3.0   # prolongator smoothing  w = sa_omega / rho
+    rho_iters: int = 0            # 0: Gershgorin bound; >0: inf-norm power its
+    max_coarse_dense: int = 8192
+    num_functions: int = 1        # >1: nodal aggregation over field-major dofs
+    node_block_smoother: int = 1  # nodal: node-block Jacobi where no seed blocks
+    sa_block_diag: int = 1        # nodal: smooth P with node-block D^-1
+
+
+def _rowsum_seq(A: sp.csr_matrix, x: np.ndarray) -> np.ndarray:
+    """y_i = sum_j A_ij x_j accumulated sequentially in CSR order (csr_matvec)."""
+    return A @ x
+
+
+def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
+    """Symmetric SoC: j strong for i iff |a_ij| >= theta*sqrt(|a_ii||a_jj|)
+    and |a_ij| > 1e-12*sqrt(|a_ii||a_jj|) (j != i); then S <- S | S^T.
+    Returns boolean-valued CSR (values 1.0), sorted, no diagonal."""
+    n = A.shape[0]
+    d = np.abs(A.diagonal())
+    r = np.repeat(np.arange(n), np.diff(A.indptr))
+    c = A.indices
+    av = np.abs(A.data)
+    s = np.sqrt(d[r] * d[c])
+    strong = (r != c) & (av >= theta * s) & (av > 1e-12 * s)
+    S = sp.csr_matrix((np.ones(int(strong.sum())), (r[strong], c[strong])),
+                      shape=(n, n))
+    S = ((S + S.T) != 0).astype(np.float64).tocsr()
+    S.sort_indices()
+    return S
+
+
+def _row_max(S: sp.csr_matrix, vals: np.ndarray) -> np.ndarray:
+    """max over row neighbours of vals (uint64); 0 for empty rows."""
+    n = S.shape[0]
+    out = np.zeros(n, dtype=np.uint64)
+    rl = np.diff(S.indptr)
+    nz = np.flatnonzero(rl > 0)
+    if len(nz):
+        out[nz] = np.maximum.reduceat(vals[S.indices], S.indptr[nz])
+    return out
+
+
+ST_OUT, ST_UND, ST_IN = 0, 1, 2
+
+
+def mis2(S: sp.csr_matrix, level: int) -> np.ndarray:
+    """Distance-2 maximal independent set, round-synchronous, hash priorities.
+
+    key_i = state<<62 | (prio & 0x7fffffff)<<31 | i.  Per round:
+    m1 = max(key, rowmax(key)); m2 = max(m1, rowmax(m1)); undecided i with
+    m2_i == key_i -> IN, with state(m2_i) == IN -> OUT.  Nodes with no strong
+    neighbours start OUT (excluded from aggregation).
+    Returns state array (uint8)."""
+    n = S.shape[0]
+    rl = np.diff(S.indptr)
+    state = np.where(rl > 0, ST_UND, ST_OUT).astype(np.uint64)
+    idx = np.arange(n, dtype=np.uint64)
+    pr = hash32(np.arange(n), level) & np.uint64(0x7FFFFFFF)
+    low = (pr << np.uint64(31)) | idx
+    rounds = 0
+    while True:
+        und = state == ST_UND
+        if not und.any():
+            break
+        key = (state << np.uint64(62)) | low
+        m1 = np.maximum(key, _row_max(S, key))
+        m2 = np.maximum(m1, _row_max(S, m1))
+        win = und & (m2 == key)
+        lose = und & ~win & ((m2 >> np.uint64(62)) == ST_IN)
+        state = np.where(win, ST_IN, np.where(lose, ST_OUT, state))
+        rounds += 1
+        if rounds > 10000:
+            raise RuntimeError('mis2 did not converge')
+    return state.astype(np.uint8)
+
+
+def node_strength(A: sp.csr_matrix, nf: int, theta: float):
+    """Nodal strength for nf fields laid out field-major (dof = f*nv + I).
+
+    s_IJ = sqrt(sum over the nf x nf block (I,J) of a^2), accumulated
+    sequentially in CSR order (rows f*nv+I for f = 0..nf-1, columns sorted).
+    J strong for I iff s_IJ >= theta*sqrt(s_II s_JJ) and
+    s_IJ > 1e-12*sqrt(s_II s_JJ) (J != I); then S <- S | S^T.
+    Returns (S, Wn): strong pattern (values 1.0) and the s_IJ matrix."""
+    n = A.shape[0]
+    nv = n // nf
+    r = np.repeat(np.arange(n), np.diff(A.indptr))
+    I = r % nv
+    J = A.indices % nv
+    key = I * nv + J
+    uniq, inv = np.unique(key, return_inverse=True)
+    s2 = np.bincount(inv, weights=A.data * A.data)   # sequential, CSR order
+    s = np.sqrt(s2)
+    ui, uj = uniq // nv, uniq % nv
+    Wn = _csr_from_coo_unique(ui, uj, s, nv, nv)
+    d = np.zeros(nv)
+    dmask = ui == uj
+    d[ui[dmask]] = s[dmask]
+    sd = np.sqrt(d[ui] * d[uj])
+    strong = (ui != uj) & (s >= theta * sd) & (s > 1e-12 * sd)
+    S = sp.csr_matrix((np.ones(int(strong.sum())), (ui[strong], uj[strong])), shape=(nv, nv))
+    S = ((S + S.T) != 0).astype(np.float64).tocsr()
+    S.sort_indices()
+    return S, Wn
+
+
+def tentative_nodal(agg: np.ndarray, nagg: int, nf: int) -> sp.csr_matrix:
+    """dof f*nv + I -> coarse dof f*nagg + agg[I] (one column per field and
+    aggregate: the constant near-kernel of every field; coarse level stays
+    field-major with nv_c = nagg)."""
+    nv = len(agg)
+    has = np.tile(agg >= 0, nf)
+    cols = np.concatenate([f * nagg + agg for f in range(nf)])
+    indptr = np.concatenate([[0], np.cumsum(has)]).astype(np.int64)
+    T = sp.csr_matrix((np.ones(int(has.sum())), cols[has].astype(np.int64), indptr),
+                      shape=(nf * nv, nf * nagg))
+    T.has_sorted_indices = True
+    return T
+
+
+def node_blocks(n: int, nf: int):
+    """block id per dof for nf x nf node blocks: bid(f*nv + I) = I."""
+    nv = n // nf
+    return np.tile(np.arange(nv, dtype=np.int64), nf), nv
+
+
+def aggregate_mis2(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
+    """MIS-2 aggregation.  Roots numbered in index order; distance-1
+    neighbours join their (unique) adjacent root; remaining non-isolated nodes
+    join the phase-2 aggregate of the strong neighbour with the largest
+    weight (|a_ij|, or s_IJ for nodal aggregation; ties: smallest aggregate
+    id).  Isolated nodes: agg = -1."""
+    A = Wabs
+    n = A.shape[0]
+    state = mis2(S, level)
+    roots = np.flatnonzero(state == ST_IN)
+    agg = np.full(n, -1, dtype=np.int64)
+    agg[roots] = np.arange(len(roots))
+    # phase 2: neighbours of roots
+    r = np.repeat(np.arange(n), np.diff(S.indptr))
+    c = S.indices
+    isroot = np.zeros(n, dtype=bool)
+    isroot[roots] = True
+    m = isroot[c] & ~isroot[r]
+    agg2 = agg.copy()
+    agg2[r[m]] = agg[c[m]]
+    # phase 3: remaining non-isolated
+    nonisol = np.diff(S.indptr) > 0
+    need = nonisol & (agg2 < 0)
+    if need.any():
+        W = A.multiply(S).tocsr()        # weights on strong pattern
+        W.sort_indices()
+        wr = np.repeat(np.arange(n), np.diff(W.indptr))
+        wc = W.indices
+        wv = W.data
+        cand = need[wr] & (agg2[wc] >= 0)
+        cr, cw, ca = wr[cand], wv[cand], agg2[wc[cand]]
+        order = np.lexsort((ca, -cw, cr))
+        cr, ca = cr[order], ca[order]
+        first = np.ones(len(cr), dtype=bool)
+        first[1:] = cr[1:] != cr[:-1]
+        agg3 = agg2.copy()
+        agg3[cr[first]] = ca[first]
+        # nodes adjacent (strongly) only through pattern entries absent from A
+        if (nonisol & (agg3 < 0)).any():
+            raise RuntimeError('aggregation left a non-isolated node unassigned')
+        agg2 = agg3
+    return agg2, len(roots)
+
+
+def tentative(agg: np.ndarray, nagg: int) -> sp.csr_matrix:
+    n = len(agg)
+    has = agg >= 0
+    indptr = np.concatenate([[0], np.cumsum(has)]).astype(np.int64)
+    T = sp.csr_matrix((np.ones(int(has.sum())), agg[has].astype(np.int64), indptr),
+                      shape=(n, nagg))
+    T.has_sorted_indices = True
+    return T
+
+
+def rho_estimate(A: sp.csr_matrix, dinv: np.ndarray, iters: int) -> float:
+    """Estimate rho(D^-1 A).  iters == 0: Gershgorin bound
+    max_i dinv_i * sum_j |a_ij|.  iters > 0: inf-norm power iteration from a
+    hash-based start vector."""
+    absA = abs(A)
+    if iters == 0:
+        rs = _rowsum_seq(absA, np.ones(A.shape[0]))
+        return float(np.max(dinv * rs))
+    n = A.shape[0]
+    v = (hash32(np.arange(n), 977).astype(np.float64) / 4294967296.0) * 2.0 - 1.0
+    rho = 0.0
+    for _ in range(iters):
+        w = dinv * _rowsum_seq(A, v)
+        mv = float(np.max(np.abs(v)))
+        mw = float(np.max(np.abs(w)))
+        rho = mw / mv
+        v = w / mw
+    return rho
+
+
+def smooth_prolongator(A, T, omega_sa, rho_iters):
+    """P = T - (w * dinv) (A T), w = omega_sa / rho(D^-1 A), dinv = 1/a_ii."""
+    dinv = 1.0 / A.diagonal()
+    rho = rho_estimate(A, dinv, rho_iters)
+    w = omega_sa / rho
+    AT = (A @ T).tocsr()
+    AT.sort_indices()
+    c = w * dinv
+    X = (sp.diags(c, format='csr') @ AT).tocsr()
+    P = (T - X).tocsr()
+    P.sort_indices()
+    return P, w
+
+
+def smooth_prolongator_block(A, T, omega_sa, blocks):
+    """Nodal SA: P = T - w (D_B^-1 (A T)), D_B = node-block diagonal,
+    w = omega_sa / rho_B, rho_B = max_i sum_j |(D_B^-1 A)_ij|."""
+    bid, nb = blocks
+    Dinv = block_inverse_csr(A, bid, nb)
+    G = (Dinv @ A).tocsr()
+    G.sort_indices()
+    rho = float(np.max(_rowsum_seq(abs(G), np.ones(A.shape[0]))))
+    w = omega_sa / rho
+    AT = (A @ T).tocsr()
+    AT.sort_indices()
+    Y = (Dinv @ AT).tocsr()
+    Y.sort_indices()
+    Y.data = w * Y.data
+    P = (T - Y).tocsr()
+    P.sort_indices()
+    return P, w
+
+
+def galerkin(A, P):
+    """R = P^T (sorted CSR); A_c = R @ (A @ P), both products in SMMP order."""
+    R = P.T.tocsr()
+    R.sort_indices()
+    AP = (A @ P).tocsr()
+    AP.sort_indices()
+    Ac = (R @ AP).tocsr()
+    Ac.sort_indices()
+    return R, Ac
+
+
+def smoother_weights(A, p: Params):
+    """winv_i = relaxation / d_i with d_i = a_ii (JACOBI) or sum_j |a_ij|
+    (L1DIAG, sequential CSR-order sum); JACOBI_RHO: d_i = a_ii * rho(D^-1 A)
+    (spectrally scaled Jacobi, same rho estimate as prolongator smoothing)."""
+    if p.smoother == 'JACOBI':
+        d = A.diagonal().copy()
+    elif p.smoother == 'JACOBI_RHO':
+        dg = A.diagonal().copy()
+        rho = rho_estimate(A, 1.0 / dg, p.rho_iters)
+        d = dg * rho
+    elif p.smoother == 'L1DIAG':
+        d = _rowsum_seq(abs(A), np.ones(A.shape[0]))
+    else:
+        raise ValueError(p.smoother)
+    return p.relaxation / d
+
+
+def dense_inverse(Ad: np.ndarray) -> np.ndarray:
+    """Gauss-Jordan without pivoting (A SPD); fixed op order:
+    row_k /= p;  row_i -= M_ik * row_k  (product, then subtraction)."""
+    return batched_inverse(Ad[None, :, :])[0]
+
+
+def batched_inverse(B: np.ndarray) -> np.ndarray:
+    """Gauss-Jordan (no pivoting) on a batch (nb, s, s); same op order as
+    ``dense_inverse`` applied block by block."""
+    nb, n, _ = B.shape
+    M = np.concatenate([B.astype(np.float64),
+                        np.broadcast_to(np.eye(n), (nb, n, n))], axis=2).copy()
+    for k in range(n):
+        p = M[:, k, k].copy()
+        if not np.all(p > 0.0):
+            raise np.linalg.LinAlgError('non-positive pivot at %d' % k)
+        M[:, k, :] = M[:, k, :] / p[:, None]
+        f = M[:, :, k].copy()
+        f[:, k] = 0.0
+        M -= f[:, :, None] * M[:, k, None, :]
+    return M[:, :, n:].copy()
+
+
+def seed_blocks(A: sp.csr_matrix, seeds: np.ndarray, mmsize: int):
+    """Non-overlapping Schwarz blocks seeded by ``idofs`` (src/utils.py:84-86).
+
+    Each non-seed dof j joins the block of the seed s maximising |a_js| over
+    j's off-diagonal seed neighbours (ties: smallest s); a seed's block keeps
+    at most mmsize-1 joiners (lowest indices), the rest stay singletons.
+    Blocks are numbered by their owner (seed or singleton) index; dofs inside
+    a block are sorted.  Returns (bid[n], nblocks)."""
+    n = A.shape[0]
+    isseed = np.zeros(n, dtype=bool)
+    isseed[np.asarray(seeds, dtype=np.int64)] = True
+    r = np.repeat(np.arange(n), np.diff(A.indptr))
+    c = A.indices
+    v = np.abs(A.data)
+    m = (~isseed[r]) & isseed[c] & (r != c)
+    cr, cc, cv = r[m], c[m], v[m]
+    order = np.lexsort((cc, -cv, cr))
+    cr, cc = cr[order], cc[order]
+    first = np.ones(len(cr), dtype=bool)
+    first[1:] = cr[1:] != cr[:-1]
+    jr, js = cr[first], cc[first]            # joiner -> seed (jr ascending)
+    # cap joiners per seed at mmsize-1 (lowest joiner indices kept)
+    o2 = np.lexsort((jr, js))
+    jr, js = jr[o2], js[o2]
+    newgrp = np.ones(len(js), dtype=bool)
+    newgrp[1:] = js[1:] != js[:-1]
+    grpstart = np.maximum.accumulate(np.where(newgrp, np.arange(len(js)), 0))
+    rank = np.arange(len(js)) - grpstart
+    keep = rank < (mmsize - 1)
+    owner = np.arange(n)
+    owner[jr[keep]] = js[keep]
+    uo, bid = np.unique(owner, return_inverse=True)
+    return bid.astype(np.int64), len(uo)
+
+
+def block_inverse_csr(A: sp.csr_matrix, bid: np.ndarray, nb: int):
+    """D_B^-1 as CSR: row i holds (D_B^-1)_{ij} for j in block(i), sorted."""
+    n = A.shape[0]
+    order = np.lexsort((np.arange(n), bid))          # dofs grouped by block
+    starts = np.searchsorted(bid[order], np.arange(nb + 1))
+    size = np.diff(starts)
+    pos = np.empty(n, dtype=np.int64)
+    pos[order] = np.arange(n) - np.repeat(starts[:-1], size)
+    r = np.repeat(np.arange(n), np.diff(A.indptr))
+    c = A.indices
+    inb = bid[r] == bid[c]
+    rows_out, cols_out, vals_out = [], [], []
+    for s in np.unique(size):
+        blks = np.flatnonzero(size == s)
+        loc = np.full(nb, -1, dtype=np.int64)
+        loc[blks] = np.arange(len(blks))
+        dense = np.zeros((len(blks), s, s))
+        m = inb & (size[bid[r]] == s)
+        dense[loc[bid[r[m]]], pos[r[m]], pos[c[m]]] = A.data[m]
+        inv = batched_inverse(dense)
+        members = order[np.repeat(starts[blks], s) + np.tile(np.arange(s), len(blks))]
+        members = members.reshape(len(blks), s)
+        rr = np.repeat(members, s, axis=1).ravel()        # row dof
+        cc = np.tile(members, (1, s)).ravel()             # col dof
+        rows_out.append(rr)
+        cols_out.append(cc)
+        vals_out.append(inv.reshape(len(blks), s * s))
+    rows = np.concatenate(rows_out)
+    cols = np.concatenate(cols_out)
+    vals = np.concatenate([v.ravel() for v in vals_out])
+    return _csr_from_coo_unique(rows, cols, vals, n, n)
+
+
+def block_smoother(A: sp.csr_matrix, seeds, p: Params, blocks=None) -> sp.csr_matrix:
+    """W_B = (relaxation / rho_B) D_B^-1, rho_B = max_i sum_j |(D_B^-1 A)_ij|
+    (Gershgorin bound; SpGEMM in SMMP order, sequential abs row sums).
+    Blocks: seed blocks from ``seeds``, or an explicit (bid, nb)."""
+    if blocks is None:
+        bid, nb = seed_blocks(A, seeds, p.Schwarz_mmsize)
+    else:
+        bid, nb = blocks
+    Dinv = block_inverse_csr(A, bid, nb)
+    G = (Dinv @ A).tocsr()
+    G.sort_indices()
+    rho = float(np.max(_rowsum_seq(abs(G), np.ones(A.shape[0]))))
+    s = p.relaxation / rho
+    W = Dinv.copy()
+    W.data = s * W.data
+    return W, bid, nb
+
+
+@dataclasses.dataclass
+class Level:
+    A: sp.csr_matrix
+    winv: np.ndarray = None          # point smoother weights (vector)
+    WB: sp.csr_matrix = None         # block smoother (level 0 with seeds)
+    P: sp.csr_matrix = None
+    R: sp.csr_matrix = None
+    agg: np.ndarray = None
+    nagg: int = 0
+    w_sa: float = 0.0
+    Ainv: np.ndarray = None
+    bid: np.ndarray = None
+
+    def smooth_apply(self, r):
+        return self.WB @ r if self.WB is not None else self.winv * r
+
+
+class Hierarchy:
+    def __init__(self, levels, params):
+        self.levels = levels
+        self.params = params
+
+    # ---------------------------------------------------------------- apply
+    def cycle(self, l: int, b: np.ndarray) -> np.ndarray:
+        """Multigrid cycle from a zero initial guess (V, or W: the coarse
+        problem is visited twice, 2nd visit on the updated residual)."""
+        p = self.params
+        lev = self.levels[l]
+        if lev.Ainv is not None:
+            return lev.Ainv @ b
+        A = lev.A
+        x = lev.smooth_apply(b)                      # first sweep from x = 0
+        for _ in range(p.presmooth_iter - 1):
+            x = x + lev.smooth_apply(b - A @ x)
+        r = b - A @ x
+        bc = lev.R @ r
+        e = self.cycle(l + 1, bc)
+        if p.cycle_type == 'W' and self.levels[l + 1].Ainv is None:
+            e = e + self.cycle(l + 1, bc - self.levels[l + 1].A @ e)
+        x = x + lev.P @ e
+        for _ in range(p.postsmooth_iter):
+            x = x + lev.smooth_apply(b - A @ x)
+        return x
+
+    def apply(self, r: np.ndarray) -> np.ndarray:
+        """z = B r: ``maxit`` cycles (src/amg_parameters.py:71), x0 = 0."""
+        z = self.cycle(0, r)
+        A0 = self.levels[0].A
+        for _ in range(self.params.maxit - 1):
+            z = z + self.cycle(0, r - A0 @ z)
+        return z
+
+    def __call__(self, r):
+        return self.apply(r)
+
+    def info(self):
+        return [(lv.A.shape[0], lv.A.nnz, 0 if lv.P is None else lv.P.nnz)
+                for lv in self.levels]
+
+
+def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarchy:
+    p = params or Params()
+    A = A.tocsr()
+    A.sort_indices()
+    levels = []
+    cur = A
+    for l in range(p.max_levels):
+        lev = Level(A=cur)
+        levels.append(lev)
+        n = cur.shape[0]
+        last = (n <= p.coarse_dof) or (l == p.max_levels - 1)
+        nf = p.num_functions
+        if not last:
+            if nf > 1:
+                S, Wn = node_strength(cur, nf, p.strong_coupled)
+                agg, nagg = aggregate_mis2(Wn, S, l)
+                last = nagg == 0 or nf * nagg >= n
+            else:
+                S = strength(cur, p.strong_coupled)
+                agg, nagg = aggregate_mis2(abs(cur), S, l)
+                last = nagg == 0 or nagg >= n
+        if last:
+            if n > p.max_coarse_dense:
+                raise RuntimeError('coarsest level %d too large for dense solve' % n)
+            lev.Ainv = dense_inverse(cur.toarray())
+            break
+        if l < p.Schwarz_levels and idofs is not None and l == 0:
+            lev.WB, lev.bid, _ = block_smoother(cur, idofs, p)
+        elif nf > 1 and p.node_block_smoother:
+            lev.WB, lev.bid, _ = block_smoother(cur, None, p, node_blocks(n, nf))
+        else:
+            lev.winv = smoother_weights(cur, p)
+        lev.agg, lev.nagg = agg, nagg
+        T = tentative_nodal(agg, nagg, nf) if nf > 1 else tentative(agg, nagg)
+        if p.AMG_type == 'SA':
+            if nf > 1 and p.sa_block_diag:
+                P, lev.w_sa = smooth_prolongator_block(cur, T, p.sa_omega, node_blocks(n, nf))
+            else:
+                P, lev.w_sa = smooth_prolongator(cur, T, p.sa_omega, p.rho_iters)
+        elif p.AMG_type == 'UA':
+            P = T
+        else:
+            raise ValueError(p.AMG_type)
+        lev.P = P
+        lev.R, cur = galerkin(cur, P)
+    return Hierarchy(levels, p)
+
+
+# --------------------------------------------------------------------------
+# PCG, cbc.block ``cgN`` semantics [ext, recalled]
+# --------------------------------------------------------------------------
+class CGResult:
+    def __init__(self, x, residuals, alphas, betas):
+        self.x, self.residuals, self.alphas, self.betas = x, residuals, alphas, betas
+
+    @property
+    def niters(self):
+        return len(self.residuals) - 1
+
+    def eigenvalue_estimates(self):
+        return lanczos_eigs(self.alphas, self.betas)
+
+
+def pcg(A, B, b, tolerance=1e-8, maxiter=500, x0=None, relativeconv=False):
+    """r = b - A x; z = B r; d = z; rz = <r,z>; residuals = [sqrt(rz)];
+    while residuals[-1] > tol and iter < maxiter: ... (cbc.block cgN)."""
+    x = np.zeros_like(b) if x0 is None else x0.copy()
+    r = b - A @ x
+    z = B(r)
+    d = z.copy()
+    rz = float(np.dot(r, z))
+    if rz < 0:
+        raise ValueError('Matrix is not positive')
+    residuals = [np.sqrt(rz)]
+    alphas, betas = [], []
+    tol = tolerance * residuals[0] if relativeconv else tolerance
+    it = 0
+    while residuals[-1] > tol and it < maxiter:
+        z = A @ d
+        dz = float(np.dot(d, z))
+        if dz == 0:
+            break
+        alpha = rz / dz
+        x = x + alpha * d
+        r = r - alpha * z
+        z = B(r)
+        rz_prev = rz
+        rz = float(np.dot(r, z))
+        if rz < 0:
+            x = x - alpha * d
+            break
+        beta = rz / rz_prev
+        d = z + beta * d
+        residuals.append(np.sqrt(rz))
+        alphas.append(alpha)
+        betas.append(beta)
+        it += 1
+    return CGResult(x, residuals, alphas, betas)
+
+
+def lanczos_eigs(alphas, betas):
+    """Eigenvalues of the CG Lanczos tridiagonal: T00 = 1/a0,
+    Tkk = 1/ak + b(k-1)/a(k-1), T(k,k-1) = sqrt(b(k-1))/a(k-1)."""
+    n = len(alphas)
+    if n == 0:
+        return np.array([1.0])
+    T = np.zeros((n, n))
+    T[0, 0] = 1.0 / alphas[0]
+    for k in range(1, n):
+        T[k, k] = 1.0 / alphas[k] + betas[k - 1] / alphas[k - 1]
+        T[k, k - 1] = np.sqrt(betas[k - 1]) / alphas[k - 1]
+        T[k - 1, k] = T[k, k - 1]
+    e = np.linalg.eigvalsh(T)
+    return np.sort(e)
+
+
+def seeded_rhs(N: int, seed: int = 1234) -> np.ndarray:
+    """uniform(-1,1) fp64 from numpy's default_rng(seed)."""
+    return np.random.default_rng(seed).uniform(-1.0, 1.0, N)

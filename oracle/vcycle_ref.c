@@ -1,0 +1,129 @@
+/*
+ * vcycle_ref.c -- plain-C restatement of Hierarchy.cycle / Hierarchy.apply
+ * (oracle/mamg_oracle.py).  TEST INFRASTRUCTURE ONLY: called by tests/ and by
+ * bench.py's cpu_baseline leg (OpenMP over rows, host cores).  Never linked
+ * into the product.  Parity status: see mamg_oracle.py (parity unpinned
+ * against HAZmath, which is absent from /root/reference).
+ *
+ * Cycle from x = 0 on level l (V, or W = second coarse visit on the updated
+ * residual):  x = S b ; (nu1-1) x += S (b - A x) ; r = b - A x ; bc = R r ;
+ * e = cycle(l+1, bc) [; e += cycle(l+1, bc - Ac e)] ; x += P e ;
+ * nu2 times x += S (b - A x).   S = W_B (block) or diag(winv) (point).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  int64_t n, m;
+  const int64_t* ptr;
+  const int32_t* col;
+  const double* val;
+} ocsr;
+
+typedef struct {
+  int64_t n;
+  int coarsest;
+  ocsr A, P, R, W;        /* W.n == 0 -> point smoother winv */
+  const double* winv;
+  const double* Ainv;     /* coarsest, row-major n x n */
+  double *t, *r, *b, *x, *c, *e, *u; /* work vectors, length n */
+} olevel;
+
+static void spmv(const ocsr* M, const double* x, double* y) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < M->n; ++i) {
+    double s = 0.0;
+    for (int64_t k = M->ptr[i]; k < M->ptr[i + 1]; ++k) s += M->val[k] * x[M->col[k]];
+    y[i] = s;
+  }
+}
+
+/* r = b - A x */
+static void resid(const ocsr* A, const double* x, const double* b, double* r) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < A->n; ++i) {
+    double s = 0.0;
+    for (int64_t k = A->ptr[i]; k < A->ptr[i + 1]; ++k) s += A->val[k] * x[A->col[k]];
+    r[i] = b[i] - s;
+  }
+}
+
+/* y = S v (smoother application) */
+static void smooth_apply(const olevel* L, const double* v, double* y) {
+  if (L->W.n > 0) {
+    spmv(&L->W, v, y);
+  } else {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < L->n; ++i) y[i] = L->winv[i] * v[i];
+  }
+}
+
+static void axpy1(int64_t n, const double* a, double* y) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) y[i] = y[i] + a[i];
+}
+
+static void cycle(olevel* L, int l, int wcyc, int nu1, int nu2, const double* b, double* x) {
+  olevel* lv = &L[l];
+  const int64_t n = lv->n;
+  if (lv->coarsest) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      double s = 0.0;
+      for (int64_t j = 0; j < n; ++j) s += lv->Ainv[i * n + j] * b[j];
+      x[i] = s;
+    }
+    return;
+  }
+  olevel* C = &L[l + 1];
+  smooth_apply(lv, b, x);
+  for (int s = 1; s < nu1; ++s) {
+    resid(&lv->A, x, b, lv->r);
+    smooth_apply(lv, lv->r, lv->u);
+    axpy1(n, lv->u, x);
+  }
+  resid(&lv->A, x, b, lv->r);
+  spmv(&lv->R, lv->r, C->b);
+  cycle(L, l + 1, wcyc, nu1, nu2, C->b, C->x);
+  if (wcyc && !C->coarsest) {
+    resid(&C->A, C->x, C->b, C->c);
+    cycle(L, l + 1, wcyc, nu1, nu2, C->c, C->e);
+    axpy1(C->n, C->e, C->x);
+  }
+  spmv(&lv->P, C->x, lv->t);
+  axpy1(n, lv->t, x);
+  for (int s = 0; s < nu2; ++s) {
+    resid(&lv->A, x, b, lv->r);
+    smooth_apply(lv, lv->r, lv->u);
+    axpy1(n, lv->u, x);
+  }
+}
+
+/* z = B r : maxit cycles from z = 0 (Hierarchy.apply) */
+int oracle_apply(olevel* L, int nlev, int wcyc, int nu1, int nu2, int maxit, const double* r,
+                 double* z) {
+  if (nlev < 1) return -1;
+  cycle(L, 0, wcyc, nu1, nu2, r, z);
+  for (int it = 1; it < maxit; ++it) {
+    resid(&L[0].A, z, r, L[0].c);
+    cycle(L, 0, wcyc, nu1, nu2, L[0].c, L[0].e);
+    axpy1(L[0].n, L[0].e, z);
+  }
+  return 0;
+}
+
+int oracle_num_threads(void) {
+  int n = 1;
+#pragma omp parallel
+  {
+#pragma omp single
+    {
+#ifdef _OPENMP
+      extern int omp_get_num_threads(void);
+      n = omp_get_num_threads();
+#endif
+    }
+  }
+  return n;
+}

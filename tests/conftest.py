@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'oracle')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs a HIP device (MI355X)')
+
+
+@pytest.fixture(scope='session')
+def lib_built():
+    """Build libmamg.so and the oracle C library once (cross-compiles on CPU)."""
+    import subprocess
+    so = os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg.so')
+    subprocess.check_call(['make', '-s', '-j8', '-C', os.path.join(ROOT, 'metric-amg-examples_amd', 'csrc')])
+    subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
+    assert os.path.exists(so)
+    return so

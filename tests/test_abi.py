@@ -1,0 +1,113 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol
+include/mamg.h declares, validates parameters with explicit errors (no
+silent fallback), and the generator sizes match the survey's formulas."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, 'include', 'mamg.h')).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(mamg_[a-z_0-9]+)\s*\(', txt)))
+
+
+def test_exports_every_declared_symbol(lib_built):
+    import metric_amg_examples_amd as M
+    L = M._lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+        assert s in M._lib.SIGNATURES, 'ctypes prototype missing for %s' % s
+
+
+def test_params_struct_layout(lib_built):
+    import metric_amg_examples_amd as M
+    p = M.parameters.make_params()
+    assert p.abi_version == 1 and p.AMG_type == 2 and p.cycle_type == 1
+    assert abs(p.relaxation - 4.0 / 3.0) < 1e-15 and p.coarse_dof == 100
+    assert p.num_functions == 1 and p.node_block_smoother == 1
+    d = M.parameters.params_to_dict(p)
+    assert set(M.parameters.KEYS) - {'prectype'} <= set(d)
+
+
+@pytest.mark.parametrize('bad,code', [
+    (dict(smoother=11), -4),                 # SGS rejected
+    (dict(aggregation_type=5), -4),          # HEM rejected
+    (dict(coarse_scaling=1), -4),
+    (dict(Schwarz_type=3), -4),              # multiplicative Schwarz rejected
+    (dict(cycle_type=3), -4),
+    (dict(max_levels=0), -1),
+    (dict(spmv_lanes=3), -1),
+    (dict(num_functions=0), -1),
+])
+def test_rejects_unsupported(lib_built, bad, code):
+    import metric_amg_examples_amd as M
+    from mamg_oracle import laplace1d
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy(laplace1d(30), **bad)
+    assert ei.value.code == code
+    assert len(str(ei.value)) > 20
+
+
+def test_reference_presets_map_and_report(lib_built):
+    import metric_amg_examples_amd as M
+    P = M.parameters
+    mapped, notes = P.to_gpu_profile(P.hazmath_parameters_metric_schwarz)
+    assert mapped['smoother'] == P.SMOOTHER_JACOBI_RHO and mapped['aggregation_type'] == P.MIS
+    assert mapped['Schwarz_type'] == P.SCHWARZ_BLOCK_JACOBI and mapped['coarse_scaling'] == P.OFF
+    assert len(notes) >= 3
+    # the raw reference preset is rejected loudly
+    from mamg_oracle import laplace1d
+    with pytest.raises(M._lib.MamgError):
+        M.HostHierarchy(laplace1d(30), parameters=P.hazmath_parameters_metric_schwarz)
+    # the mapped one builds (UA + W-cycle)
+    H = M.HostHierarchy(laplace1d(300), parameters=P.parameters_metric_schwarz)
+    assert H.num_levels >= 2
+    with pytest.raises(KeyError):
+        P.make_params({'no_such_key': 1})
+
+
+def test_generator_sizes(lib_built):
+    import metric_amg_examples_amd as M
+    L = M._lib.lib()
+    N, nnz = C.c_int64(), C.c_int64()
+    # bidomain_3d nrefs=6 -> n=256, N = 2*257^3
+    assert L.mamg_gen_bidomain_size(3, 256, C.byref(N), C.byref(nnz)) == 0
+    assert N.value == 33949186 and 9.9e8 < nnz.value < 1.02e9
+    assert L.mamg_gen_bidomain_size(2, 1024, C.byref(N), C.byref(nnz)) == 0
+    assert N.value == 2101250
+    assert L.mamg_gen_bidomain_size(4, 8, C.byref(N), C.byref(nnz)) == -1
+    assert M.problems.finest_n(3, 6) == 256 and M.problems.finest_n(2, 6) == 1024
+
+
+def test_bad_csr_rejected(lib_built):
+    import metric_amg_examples_amd as M
+    ip = np.array([0, 1, 5], np.int64)        # rowptr[n] != nnz
+    ix = np.array([0, 1], np.int32)
+    dv = np.ones(2)
+    with pytest.raises(ValueError):
+        M.HostHierarchy((ip, ix, dv))
+    # column out of range / non-monotone rowptr: rejected by the C side
+    ip = np.array([0, 1, 2], np.int64)
+    ix = np.array([0, 7], np.int32)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy((ip, ix, dv))
+    assert ei.value.code == -1
+
+
+def test_no_cpu_fallback_without_gpu(lib_built):
+    import torch
+    import metric_amg_examples_amd as M
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from mamg_oracle import laplace1d
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.MetricAMG(laplace1d(30))
+    assert ei.value.code == -2                # HIP error, never a CPU fallback

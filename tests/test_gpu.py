@@ -1,0 +1,194 @@
+"""GPU parity: the HIP apply path (through the C-ABI) against the CPU oracle.
+
+Tolerances (fp64): one preconditioner application z = B r agrees with the
+oracle's to ||dz|| / ||z|| <= 1e-10 (the setup is bitwise identical; only
+summation order inside the GPU SpMVs differs).  PCG: iteration count equal to
+the oracle's, every residual within 1e-6 relative.  At full benchmark sizes
+the checks are size-independent properties (symmetry, linearity, determinism
+of graph replays, <Br, r> > 0).
+"""
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+APPLY_TOL = 1e-10
+
+
+def _mamg():
+    import metric_amg_examples_amd as M
+    return M
+
+
+def to_c(kw):
+    c = dict(kw)
+    if 'AMG_type' in c:
+        c['AMG_type'] = {'SA': 2, 'UA': 1}[c['AMG_type']]
+    if 'cycle_type' in c:
+        c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    return c
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+APPLY_CASES = [
+    (2, 32, 1.0, dict(num_functions=2)),
+    (2, 64, 1e6, dict(num_functions=2)),
+    (3, 8, 1e6, dict(num_functions=2)),
+    (3, 16, 1e4, dict(num_functions=2)),
+    (3, 16, 1e10, dict(num_functions=2)),
+    (3, 16, 1.0, dict()),
+    (2, 32, 1e3, dict(AMG_type='UA', cycle_type='W')),
+    (3, 16, 1e2, dict(num_functions=2, cycle_type='W')),
+    (2, 32, 1e3, dict(num_functions=2, presmooth_iter=2, postsmooth_iter=3, maxit=2)),
+    (2, 32, 1e3, dict(num_functions=2, node_block_smoother=0, sa_block_diag=0)),
+]
+
+
+@pytest.mark.parametrize('dim,n,g,kw', APPLY_CASES)
+def test_apply_matches_oracle(lib_built, dim, n, g, kw):
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, **to_c(kw))
+    h = mo.setup(A, mo.Params(**kw), idofs=s.idofs)
+    assert B.num_levels == len(h.levels)
+    for seed in (1234, 7):
+        r = mo.seeded_rhs(s.N, seed)
+        zo = h.apply(r)
+        z = B * r                                   # host pointers
+        assert rel(z, zo) < APPLY_TOL
+        zt = B.matvec(torch.as_tensor(r).cuda())    # device pointers, graph
+        torch.cuda.synchronize()
+        assert rel(zt.cpu().numpy(), zo) < APPLY_TOL
+
+
+@pytest.mark.parametrize('dim,n,g', [(2, 64, 1.0), (3, 16, 1e6), (3, 16, 1e10), (2, 128, 1e4)])
+def test_pcg_iterations_match_oracle(lib_built, dim, n, g):
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    b = mo.seeded_rhs(s.N)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)   # device PCG
+    x = solver * b
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    ref = mo.pcg(A, h, b, 1e-8, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+    assert rel(x, ref.x) < 1e-6
+    e1, e2 = solver.eigenvalue_estimates(), ref.eigenvalue_estimates()
+    assert abs(e1[-1] / e1[0] - e2[-1] / e2[0]) < 1e-4 * (e2[-1] / e2[0])
+    # host-loop ConjGrad (cbc.block structure, B*r through the C-ABI) agrees too
+    host = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500, device=False)
+    xh = host * b
+    assert len(host.residuals) == len(ref.residuals)
+    assert rel(xh, ref.x) < 1e-6
+
+
+def test_callback_and_relativeconv(lib_built):
+    M = _mamg()
+    s = M.problems.bidomain(2, 32, 1e2)
+    A = s.scipy()
+    b = mo.seeded_rhs(s.N)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    seen = []
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-6, maxiter=200, relativeconv=True,
+                        callback=lambda k, x, r: seen.append(k))
+    solver * b
+    assert seen == list(range(len(solver.residuals) - 1))
+    assert solver.residuals[-1] <= 1e-6 * solver.residuals[0]
+
+
+def test_spmv_matches_scipy(lib_built):
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e3)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    x = np.random.default_rng(3).standard_normal(s.N)
+    y = torch.empty(s.N, dtype=torch.float64, device='cuda')
+    B.spmv_device(torch.as_tensor(x).cuda(), y)
+    torch.cuda.synchronize()
+    assert rel(y.cpu().numpy(), A @ x) < 1e-14
+
+
+@pytest.mark.parametrize('lanes', [2, 4, 8, 16, 32, 64])
+def test_lane_widths_agree(lib_built, lanes):
+    M = _mamg()
+    s = M.problems.bidomain(3, 8, 1e4)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, spmv_lanes=lanes)
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    assert rel(B * r, h.apply(r)) < APPLY_TOL
+
+
+def test_edge_cases(lib_built):
+    M = _mamg()
+    # coarsest immediately (n <= coarse_dof): pure dense solve
+    A = mo.laplace1d(50)
+    B = M.MetricAMG(A)
+    r = mo.seeded_rhs(50)
+    assert B.num_levels == 1
+    assert rel(B * r, np.linalg.solve(A.toarray(), r)) < 1e-12
+    # 1x1
+    import scipy.sparse as sp
+    B1 = M.MetricAMG(sp.csr_matrix(np.array([[4.0]])))
+    assert abs((B1 * np.array([2.0]))[0] - 0.5) < 1e-15
+    # isolated (identity) rows mixed with a Laplacian
+    L = sp.block_diag([mo.laplace1d(400), sp.eye(30)]).tocsr()
+    L.sort_indices()
+    B2 = M.MetricAMG(L, coarse_dof=20)
+    h = mo.setup(L, mo.Params(coarse_dof=20))
+    r = mo.seeded_rhs(430)
+    assert rel(B2 * r, h.apply(r)) < APPLY_TOL
+    # bad vector size
+    with pytest.raises(ValueError):
+        B2 * np.ones(3)
+
+
+def test_multiple_handles_and_graph_cache(lib_built):
+    import torch
+    M = _mamg()
+    s1 = M.problems.bidomain(2, 32, 1.0)
+    s2 = M.problems.bidomain(3, 8, 1e6)
+    B1 = M.MetricAMG(s1.scipy(), s1.W, idofs=s1.idofs, num_functions=2)
+    B2 = M.MetricAMG(s2.scipy(), s2.W, idofs=s2.idofs, num_functions=2)
+    r1 = torch.as_tensor(mo.seeded_rhs(s1.N)).cuda()
+    r2 = torch.as_tensor(mo.seeded_rhs(s2.N)).cuda()
+    outs = []
+    z1 = torch.empty_like(r1)
+    for _ in range(5):                     # many distinct (r, z) pairs + replays
+        B1.apply_device(r1, z1)
+        outs.append(z1.clone())
+        B2.matvec(r2)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])     # deterministic replays (bitwise)
+    B1.close()
+    B2.close()
+
+
+def test_large_properties_3d(lib_built):
+    """bidomain_3d nrefs=5 (BASELINE config 3, N = 4.29M): symmetry,
+    linearity, positivity, determinism of the device apply."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 128, 1e6)
+    B = M.MetricAMG(s, s.W, idofs=s.idofs, num_functions=2)
+    g = torch.Generator(device='cuda').manual_seed(5)
+    r = torch.rand(s.N, dtype=torch.float64, device='cuda', generator=g) * 2 - 1
+    q = torch.rand(s.N, dtype=torch.float64, device='cuda', generator=g) * 2 - 1
+    Br, Bq = B.matvec(r), B.matvec(q)
+    a, b = torch.dot(Br, q).item(), torch.dot(r, Bq).item()
+    assert abs(a - b) <= 1e-9 * (abs(a) + abs(b))
+    assert torch.dot(Br, r).item() > 0
+    lin = B.matvec(2.0 * r + q)
+    assert (torch.linalg.norm(lin - (2.0 * Br + Bq)) / torch.linalg.norm(lin)).item() < 1e-12
+    assert torch.equal(B.matvec(r), Br)

@@ -1,0 +1,89 @@
+"""The product's host setup (libmamg mamg_host_setup, C++) is bitwise equal to
+the oracle's (numpy/scipy): generator, aggregates, P, R, smoother weights /
+block inverses, coarse operators and the coarsest dense inverse.  CPU only."""
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+CASES = [
+    (2, 16, 1.0, {}),
+    (3, 8, 1e6, {}),
+    (2, 32, 1e3, dict(AMG_type='UA', cycle_type='W')),
+    (2, 32, 1e3, dict(strong_coupled=0.08)),
+    (3, 16, 1e4, dict(num_functions=2)),
+    (3, 16, 1.0, dict(num_functions=2)),
+    (2, 64, 1e10, dict(num_functions=2)),
+    (3, 16, 1e6, dict(num_functions=2, strong_coupled=0.08)),
+    (2, 32, 1e3, dict(num_functions=2, node_block_smoother=0, sa_block_diag=0)),
+    (3, 8, 1e2, dict(num_functions=2, smoother='L1DIAG', node_block_smoother=0)),
+    (3, 8, 1e2, dict(num_functions=2, smoother='JACOBI', relaxation=0.5, node_block_smoother=0)),
+    (2, 16, 1e2, dict(rho_iters=10, node_block_smoother=0)),
+]
+
+
+def to_c(kw):
+    c = dict(kw)
+    if 'AMG_type' in c:
+        c['AMG_type'] = {'SA': 2, 'UA': 1}[c['AMG_type']]
+    if 'cycle_type' in c:
+        c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    if 'smoother' in c:
+        c['smoother'] = {'JACOBI': 1, 'L1DIAG': 2, 'JACOBI_RHO': 3}[c['smoother']]
+    return c
+
+
+def eq_csr(e, M):
+    return (np.array_equal(e[0], M.indptr) and np.array_equal(e[1], M.indices)
+            and np.array_equal(e[2], M.data))
+
+
+@pytest.mark.parametrize('dim,n,g,kw', CASES)
+def test_bitwise_hierarchy(lib_built, dim, n, g, kw):
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(dim, n, g)
+    o = mo.bidomain_system(dim, n, g)
+    A = s.scipy()
+    assert np.array_equal(A.indptr, o['A'].indptr) and np.array_equal(A.indices, o['A'].indices)
+    assert np.array_equal(A.data, o['A'].data)                 # generator bitwise
+    H = M.HostHierarchy(s, idofs=s.idofs, **to_c(kw))
+    h = mo.setup(o['A'], mo.Params(**kw), idofs=o['idofs'])
+    assert H.num_levels == len(h.levels)
+    for l, lv in enumerate(h.levels):
+        ex = H.level(l)
+        if l > 0:
+            assert eq_csr(ex['A'], lv.A), 'A level %d' % l
+        if lv.Ainv is not None:
+            assert np.array_equal(ex['Ainv'], lv.Ainv)
+            continue
+        assert np.array_equal(ex['agg'], lv.agg), 'agg level %d' % l
+        assert eq_csr(ex['P'], lv.P) and eq_csr(ex['R'], lv.R), 'P/R level %d' % l
+        if lv.WB is not None:
+            assert eq_csr(ex['WB'], lv.WB), 'WB level %d' % l
+        else:
+            assert np.array_equal(ex['winv'], lv.winv), 'winv level %d' % l
+
+
+def test_no_idofs_and_scipy_input(lib_built):
+    import metric_amg_examples_amd as M
+    o = mo.bidomain_system(2, 16, 10.0)
+    H = M.HostHierarchy(o['A'], idofs=None)
+    h = mo.setup(o['A'], mo.Params(), idofs=None)
+    assert H.num_levels == len(h.levels)
+    assert np.array_equal(H.level(0)['winv'], h.levels[0].winv)
+
+
+def test_laplace1d_kat(lib_built):
+    # 1-D Laplacian: MIS-2 aggregates of a path; UA Galerkin product exact
+    import metric_amg_examples_amd as M
+    A = mo.laplace1d(40)
+    H = M.HostHierarchy(A, AMG_type=1, coarse_dof=4)
+    h = mo.setup(A, mo.Params(AMG_type='UA', coarse_dof=4))
+    assert np.array_equal(H.level(0)['agg'], h.levels[0].agg)
+    T = h.levels[0].P.toarray()
+    Ac = T.T @ A.toarray() @ T
+    e = H.level(1)
+    n1 = e['n']
+    import scipy.sparse as sp
+    got = sp.csr_matrix((e['A'][2], e['A'][1], e['A'][0]), shape=(n1, n1)).toarray()
+    assert np.array_equal(got, Ac)

