@@ -192,12 +192,15 @@ def main():
             'n': n, 'N': sysm.N, 'nnz': sysm.nnz,
             'levels': [[s['n'], s['nnzA']] for s in sizes],
             'parallelism': 'replicas' if world > 1 else 'single',
+            'device_layout': B.layout,
         },
         'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),
         'apply_GB_alg': round(apply_bytes / 1e9, 4),
         'graph_ms_per_step': round(graph_ms, 4),
         'roofline': {
-            'bound': 'hbm', 'kernel': 'level-0 residual r = b - A0 x (csr_kernel<*,RESID,0>)',
+            'bound': 'hbm',
+            'kernel': 'level-0 residual r = b - A0 x (%s<*,RESID,...,0>)'
+                      % ('bsr2_kernel' if B.layout == 'bsr2' else 'csr_kernel'),
             'achieved': round(achieved, 1) if achieved else None,
             'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,

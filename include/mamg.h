@@ -157,6 +157,9 @@ void mamg_destroy(mamg_handle* h);
 
 int64_t mamg_nrows(const mamg_handle* h);
 int mamg_num_levels(const mamg_handle* h);
+/* Device layout chosen at upload: 0 = CSR (general), 1 = BSR2 (nodal
+ * hierarchy with num_functions == 2 and node-block smoothers). */
+int mamg_device_layout(const mamg_handle* h);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */
 int mamg_apply_bytes(const mamg_handle* h, double* total_bytes);

@@ -137,6 +137,11 @@ class MetricAMG:
         return self._L.mamg_num_levels(self._h)
 
     @property
+    def layout(self) -> str:
+        """device layout: 'csr' (general) or 'bsr2' (nodal, 2 fields)."""
+        return ('csr', 'bsr2')[self._L.mamg_device_layout(self._h)]
+
+    @property
     def apply_bytes(self) -> float:
         b = C.c_double()
         _lib.check(self._L.mamg_apply_bytes(self._h, C.byref(b)))

@@ -223,6 +223,7 @@ void mamg_destroy(mamg_handle* h) {
 
 int64_t mamg_nrows(const mamg_handle* h) { return h ? mamg::dev_nrows(h->d) : (int64_t)MAMG_ERR_ARG; }
 int mamg_num_levels(const mamg_handle* h) { return h ? mamg::dev_num_levels(h->d) : MAMG_ERR_ARG; }
+int mamg_device_layout(const mamg_handle* h) { return h ? mamg::dev_layout(h->d) : MAMG_ERR_ARG; }
 
 int mamg_apply_bytes(const mamg_handle* h, double* total) {
   if (!h || !total) { set_error("null argument"); return MAMG_ERR_ARG; }

@@ -1,0 +1,78 @@
+// convert.cpp -- host-side layout conversion for the BSR2 device path
+// (compiled by g++ with OpenMP, like the rest of the host code).
+#include <omp.h>
+
+#include <algorithm>
+
+#include "host.h"
+
+namespace mamg {
+
+// ---- host conversion: field-major CSR (rows f*nr+I, cols g*nc+J) -> BSR2 ---
+
+void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) {
+  B->nr = nr;
+  B->nc = nc;
+  B->ptr.assign(nr + 1, 0);
+  // pass 1: number of distinct node columns per node row
+#pragma omp parallel
+  {
+    std::vector<int32_t> js;
+#pragma omp for schedule(dynamic, 4096)
+    for (int64_t I = 0; I < nr; ++I) {
+      js.clear();
+      for (int f = 0; f < 2; ++f) {
+        const int64_t r = f * nr + I;
+        for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) js.push_back((int32_t)(M.col[k] % nc));
+      }
+      std::sort(js.begin(), js.end());
+      B->ptr[I + 1] = (int64_t)(std::unique(js.begin(), js.end()) - js.begin());
+    }
+  }
+  for (int64_t I = 0; I < nr; ++I) B->ptr[I + 1] += B->ptr[I];
+  const int64_t nb = B->ptr[nr];
+  B->col.resize(nb);
+  B->val.assign(4 * nb, 0.0);
+#pragma omp parallel
+  {
+    std::vector<int32_t> js;
+#pragma omp for schedule(dynamic, 4096)
+    for (int64_t I = 0; I < nr; ++I) {
+      js.clear();
+      for (int f = 0; f < 2; ++f) {
+        const int64_t r = f * nr + I;
+        for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) js.push_back((int32_t)(M.col[k] % nc));
+      }
+      std::sort(js.begin(), js.end());
+      js.erase(std::unique(js.begin(), js.end()), js.end());
+      const int64_t o = B->ptr[I];
+      for (size_t t = 0; t < js.size(); ++t) B->col[o + t] = js[t];
+      for (int f = 0; f < 2; ++f) {
+        const int64_t r = f * nr + I;
+        for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
+          const int32_t J = (int32_t)(M.col[k] % nc);
+          const int g = (int)(M.col[k] / nc);
+          const int64_t t = std::lower_bound(js.begin(), js.end(), J) - js.begin();
+          B->val[4 * (o + t) + 2 * f + g] = M.val[k];
+        }
+      }
+    }
+  }
+}
+
+// W_B (or node-block smoother) -> one 2x2 block per node; false if some entry
+// couples different nodes (then the BSR2 layout cannot fuse the smoother)
+bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk) {
+  blk->assign(4 * nv, 0.0);
+  for (int64_t i = 0; i < W.n; ++i) {
+    const int64_t I = i % nv, f = i / nv;
+    for (int64_t k = W.ptr[i]; k < W.ptr[i + 1]; ++k) {
+      const int64_t j = W.col[k];
+      if (j % nv != I) return false;
+      (*blk)[4 * I + 2 * f + j / nv] = W.val[k];
+    }
+  }
+  return true;
+}
+
+}  // namespace mamg

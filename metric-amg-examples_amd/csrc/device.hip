@@ -5,24 +5,26 @@
 // called by ConjGrad /root/reference/src/bidomain_3d.py:149-150) and the
 // cbc.block PCG loop itself (mamg_pcg_device).
 //
-// Layout in HBM (per level l): A_l, P_l, R_l = P_l^T, W_B (level 0 seed-block
-// smoother) as CSR {int64 rowptr, int32 col, fp64 val}; point-smoother weights
-// winv_l[n_l]; the coarsest level's dense inverse (row-major fp64); work
-// vectors t, t2, r, b, x, c, e per level.  Everything stays resident; one apply
-// touches no host memory.
+// Two device layouts of the same hierarchy (chosen at upload):
+//  * CSR (general): every level as CSR {int64 rowptr, int32 col, fp64 val},
+//    vectors in the caller's dof order.  Kernel: csr_kernel<VL,EPI,TAG>.
+//  * BSR2 (nodal hierarchies, num_functions == 2, block-aligned smoother):
+//    every level as 2x2 block CSR, node-major {int64 bptr, int32 node col,
+//    4 fp64 per block}; internal vectors node-interleaved (x[2I+f]) so one
+//    16-byte load gathers a node's pair; the level-0 block-Jacobi smoother is
+//    kept as one 2x2 block per node and fused into the SpMV epilogue
+//    (x' = x + W_I (b_I - (A x)_I)).  The caller's r / z stay field-major
+//    ([u1; u2], src/bidomain_3d.py:124,138): level-0 kernels read/write them
+//    with a field stride.  Index bytes drop from 4 per value to 1, gathers
+//    halve; measured 2.2x faster level-0 SpMV than CSR (bench/spmv_micro.hip).
 //
-// Kernels (all HBM-bound, 2 flop per 12 B of matrix):
-//   csr_kernel<VL, EPI, TAG>: row-group CSR SpMV, VL lanes per row (VL a power
-//     of two <= 64, chosen from the mean row length), lanes stride the row's
-//     contiguous (col, val) window with coalesced loads, x gathered through
-//     L2/MALL, the VL partial sums reduced with wavefront shuffles (DPP), and a
-//     fused epilogue: y = s | y += s | r = b - s | x' = x + w (b - s).
-//     TAG separates level-0 launches (distinct kernel symbol per rocprof row).
-//   scale_kernel (first sweep from x = 0), gemv_kernel (coarsest dense solve),
-//   axpy, CG vector kernels, deterministic two-stage dot product.
-// One apply = a fixed schedule of launches (built once per (r, z) pair) that
-// is captured into a hipGraph; each launch carries its algorithmic bytes so
-// roofline numbers come from the hierarchy, not from counters.
+// Kernels (all HBM-bound, ~0.17 flop/B): VL lanes per
+// row (node), VL a power of two chosen from the mean row length; lanes stride
+// the row's contiguous block window (coalesced 32-byte block loads), x
+// gathered through L2/MALL, partial sums reduced with wavefront shuffles, and
+// a fused epilogue.  One apply = a fixed schedule of launches captured into a
+// hipGraph; each launch carries its algorithmic bytes (roofline from the
+// hierarchy, not from counters).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,10 +47,14 @@ namespace {
     }                                                                                \
   } while (0)
 
-enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3 };
+// epilogues: y = s | y = y0 + s | r = b - s | x' = x + w (b - s) (point) |
+// x' = x + W_I (b_I - s_I) (2x2 block, BSR only)
+enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4 };
+
+typedef double dv4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
-// kernels
+// CSR kernels (general layout)
 // ---------------------------------------------------------------------------
 template <int VL, int EPI, int TAG>
 __global__ __launch_bounds__(256) void csr_kernel(
@@ -79,6 +85,101 @@ __global__ __launch_bounds__(256) void csr_kernel(
     else if (EPI == EPI_RESID) out[row] = b[row] - s;
     else out[row] = y[row] + w[row] * (b[row] - s);
   }
+}
+
+// ---------------------------------------------------------------------------
+// BSR2 kernels (nodal layout).  Vector element (node I, field f):
+//   node-major:  v[2I + f]          (stride argument 0)
+//   field-major: v[f * stride + I]  (the caller's [u1; u2] order)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double vget(const double* v, int64_t stride, int64_t I, int f) {
+  return stride ? v[f * stride + I] : v[2 * I + f];
+}
+__device__ __forceinline__ void vset(double* v, int64_t stride, int64_t I, int f, double a) {
+  if (stride) v[f * stride + I] = a; else v[2 * I + f] = a;
+}
+
+template <int VL, int EPI, bool XFM, int TAG>
+__global__ __launch_bounds__(256) void bsr2_kernel(
+    int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
+    const dv4* __restrict__ bval, const double* __restrict__ x, int64_t xs,
+    const double* y, const double* __restrict__ b, int64_t bs,
+    const dv4* __restrict__ W, double* out, int64_t os) {
+  const int lane = threadIdx.x & (VL - 1);
+  const int64_t node = ((int64_t)blockIdx.x * 256 + threadIdx.x) / VL;
+  double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+  if (node < nr) {
+    const int64_t p0 = bptr[node], p1 = bptr[node + 1];
+    int64_t k = p0 + lane;
+    for (; k + VL < p1; k += 2 * VL) {
+      const int32_t c0 = bcol[k], c1 = bcol[k + VL];
+      const dv4 v0 = bval[k], v1 = bval[k + VL];
+      double a0, a1, e0, e1;
+      if (XFM) {
+        a0 = x[c0]; a1 = x[xs + c0]; e0 = x[c1]; e1 = x[xs + c1];
+      } else {
+        const double2 a = reinterpret_cast<const double2*>(x)[c0];
+        const double2 e = reinterpret_cast<const double2*>(x)[c1];
+        a0 = a.x; a1 = a.y; e0 = e.x; e1 = e.y;
+      }
+      s0 += v0.x * a0; s0 += v0.y * a1;
+      s1 += v0.z * a0; s1 += v0.w * a1;
+      t0 += v1.x * e0; t0 += v1.y * e1;
+      t1 += v1.z * e0; t1 += v1.w * e1;
+    }
+    if (k < p1) {
+      const int32_t c0 = bcol[k];
+      const dv4 v0 = bval[k];
+      double a0, a1;
+      if (XFM) {
+        a0 = x[c0]; a1 = x[xs + c0];
+      } else {
+        const double2 a = reinterpret_cast<const double2*>(x)[c0];
+        a0 = a.x; a1 = a.y;
+      }
+      s0 += v0.x * a0; s0 += v0.y * a1;
+      s1 += v0.z * a0; s1 += v0.w * a1;
+    }
+  }
+  s0 += t0;
+  s1 += t1;
+#pragma unroll
+  for (int off = VL / 2; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off, VL);
+    s1 += __shfl_xor(s1, off, VL);
+  }
+  if (node < nr && lane == 0) {
+    double o0, o1;
+    if (EPI == EPI_Y) {
+      o0 = s0; o1 = s1;
+    } else if (EPI == EPI_YADD) {
+      o0 = y[2 * node] + s0; o1 = y[2 * node + 1] + s1;
+    } else if (EPI == EPI_RESID) {
+      o0 = vget(b, bs, node, 0) - s0; o1 = vget(b, bs, node, 1) - s1;
+    } else {  // EPI_BJAC
+      const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
+      const dv4 w = W[node];
+      o0 = y[2 * node] + (w.x * r0 + w.y * r1);
+      o1 = y[2 * node + 1] + (w.z * r0 + w.w * r1);
+    }
+    vset(out, os, node, 0, o0);
+    vset(out, os, node, 1, o1);
+  }
+}
+
+// block-diagonal apply: out(I) = [y(I) +] W_I b(I)
+template <bool ADD>
+__global__ __launch_bounds__(256) void bd2_kernel(int64_t nv, const dv4* __restrict__ W,
+                                                  const double* __restrict__ b, int64_t bs,
+                                                  const double* y, double* out, int64_t os) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  const double b0 = vget(b, bs, I, 0), b1 = vget(b, bs, I, 1);
+  const dv4 w = W[I];
+  double o0 = w.x * b0 + w.y * b1, o1 = w.z * b0 + w.w * b1;
+  if (ADD) { o0 += y[2 * I]; o1 += y[2 * I + 1]; }
+  vset(out, os, I, 0, o0);
+  vset(out, os, I, 1, o1);
 }
 
 __global__ __launch_bounds__(256) void scale_kernel(int64_t n, const double* __restrict__ w,
@@ -178,22 +279,32 @@ struct DCsr {
   int lanes = 8;
 };
 
+struct DBsr {              // 2x2 blocks, node-major
+  int64_t nr = 0, nc = 0, nb = 0;
+  int64_t* ptr = nullptr;
+  int32_t* col = nullptr;
+  dv4* val = nullptr;
+  int lanes = 8;
+};
+
 struct DLevel {
-  int64_t n = 0;
+  int64_t n = 0;           // dofs
   bool coarsest = false;
-  DCsr A, P, R, WB;
+  DCsr A, P, R, WB;        // CSR layout
+  DBsr Ab, Pb, Rb;         // BSR2 layout
+  dv4* Wd = nullptr;       // BSR2 layout: 2x2 smoother block per node
   double* winv = nullptr;
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr,
          *c = nullptr, *e = nullptr;
 };
 
-enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3 };
+enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
-  C_L0_SMOOTH = 1,  // post-smooth SpMV on A0 (fused Jacobi, or residual for W_B)
-  C_L0_WB = 2,      // level-0 smoother application (W_B SpMV or scale)
+  C_L0_SMOOTH = 1,  // post-smooth SpMV on A0 (fused Jacobi / block Jacobi)
+  C_L0_WB = 2,      // level-0 smoother application outside an SpMV
   C_L0_R = 3,       // level-0 restriction
   C_L0_P = 4,       // level-0 prolongation
   C_COARSE = 5,     // all SpMV-class launches on levels >= 1
@@ -205,9 +316,13 @@ enum Cls {
 struct Op {
   int kind = OP_CSR, epi = EPI_Y, cls = 0, tag = 1;
   const DCsr* M = nullptr;
+  const DBsr* Mb = nullptr;
   int64_t n = 0;
   const double *x = nullptr, *y = nullptr, *b = nullptr, *w = nullptr;
+  const dv4* W = nullptr;
   double* out = nullptr;
+  int64_t xs = 0, bs = 0, os = 0;   // BSR2 field strides (0 = node-major)
+  bool xfm = false;
   double bytes = 0.0;
 };
 
@@ -223,6 +338,7 @@ struct Graph {
 struct DeviceHandle {
   mamg_params p;
   int device = 0;
+  bool bsr = false;
   std::vector<DLevel> L;
   std::vector<void*> allocs;
   hipStream_t cap = nullptr;
@@ -258,10 +374,12 @@ int dalloc(DeviceHandle* h, T** p, int64_t count, std::string* err) {
   return MAMG_OK;
 }
 
+// lanes per row: ~3 entries per lane (bench/spmv_micro.hip: 8 lanes best for
+// the ~30 nnz CSR rows and the ~15 block BSR rows of the level-0 operator)
 int pick_lanes(int64_t n, int64_t nnz) {
   const double avg = n ? (double)nnz / (double)n : 1.0;
   int l = 2;
-  while (l < 64 && 2.0 * l <= avg) l *= 2;
+  while (l < 64 && 3.0 * (2 * l) <= avg + 1e-9) l *= 2;
   return l;
 }
 
@@ -282,12 +400,53 @@ int upload_csr(DeviceHandle* h, const CsrView& M, DCsr* D, int lanes, std::strin
   return MAMG_OK;
 }
 
-// ---- algorithmic bytes ------------------------------------------
+// lanes per node row for 2x2 blocks: ~2 blocks per lane (VL = 8 for the
+// ~15-block level-0 rows: 1.87 ms vs 2.00 ms at VL = 4, bench/spmv_micro.hip)
+int pick_lanes_bsr(int64_t nr, int64_t nb) {
+  const double avg = nr ? (double)nb / (double)nr : 1.0;
+  int l = 2;
+  while (l < 64 && 2.0 * (2 * l) <= 2.0 * avg) l *= 2;
+  return l;
+}
+
+int upload_bsr(DeviceHandle* h, const HBsr& B, DBsr* D, int lanes, std::string* err) {
+  D->nr = B.nr;
+  D->nc = B.nc;
+  D->nb = B.ptr[B.nr];
+  D->lanes = lanes > 0 ? lanes : pick_lanes_bsr(B.nr, D->nb);
+  int rc;
+  if ((rc = dalloc(h, &D->ptr, B.nr + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nb, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), (B.nr + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (D->nb) {
+    HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+
+int upload_csr_as_bsr(DeviceHandle* h, const CsrView& M, int64_t nr, int64_t nc, DBsr* D, int lanes,
+                      std::string* err) {
+  HBsr B;
+  to_bsr2(M, nr, nc, &B);
+  return upload_bsr(h, B, D, lanes, err);
+}
+
+// ---- algorithmic bytes (per layout) ------------------------------
 double csr_bytes(const DCsr& M, int epi) {
   double b = 12.0 * M.nnz + 8.0 * (M.n + 1) + 8.0 * M.m + 8.0 * M.n;  // A, x, out
   if (epi == EPI_YADD) b += 8.0 * M.n;
   if (epi == EPI_RESID) b += 8.0 * M.n;
   if (epi == EPI_JACOBI) b += 16.0 * M.n;
+  return b;
+}
+
+double bsr_bytes(const DBsr& M, int epi) {
+  double b = 36.0 * M.nb + 8.0 * (M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;  // A, x, out
+  if (epi == EPI_YADD) b += 16.0 * M.nr;
+  if (epi == EPI_RESID) b += 16.0 * M.nr;
+  if (epi == EPI_BJAC) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;       // y, b, W
   return b;
 }
 
@@ -300,18 +459,34 @@ Op csr_op(const DCsr& M, int epi, int cls, int tag, const double* x, const doubl
   return o;
 }
 
-// cycle from zero initial guess: xout = MG_l(b)
-void cycle_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
+Op bsr_op(const DBsr& M, int epi, int cls, int tag, const double* x, int64_t xs, const double* y,
+          const double* b, int64_t bs, const dv4* W, double* out, int64_t os) {
+  Op o;
+  o.kind = OP_BSR; o.epi = epi; o.cls = cls; o.tag = tag; o.Mb = &M; o.n = M.nr;
+  o.x = x; o.xs = xs; o.xfm = xs != 0; o.y = y; o.b = b; o.bs = bs; o.W = W; o.out = out; o.os = os;
+  o.bytes = bsr_bytes(M, epi);
+  return o;
+}
+
+Op gemv_op(const DLevel& L, const double* b, double* out) {
+  Op o;
+  o.kind = OP_GEMV; o.cls = C_DENSE; o.n = L.n; o.x = b; o.w = L.Ainv; o.out = out;
+  o.bytes = 8.0 * L.n * L.n + 16.0 * L.n;
+  return o;
+}
+
+Op axpy_op(int64_t n, const double* e, double* x) {
+  Op o;
+  o.kind = OP_AXPY; o.cls = C_MISC; o.n = n; o.x = e; o.out = x; o.bytes = 24.0 * n;
+  return o;
+}
+
+// ---- CSR layout: cycle from zero initial guess: xout = MG_l(b) --------------
+void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
   const DLevel& L = h->L[l];
   const mamg_params& p = h->p;
   const bool l0 = l == 0;
-  if (L.coarsest) {
-    Op o;
-    o.kind = OP_GEMV; o.cls = C_DENSE; o.n = L.n; o.x = b; o.w = L.Ainv; o.out = xout;
-    o.bytes = 8.0 * L.n * L.n + 16.0 * L.n;
-    ops->push_back(o);
-    return;
-  }
+  if (L.coarsest) { ops->push_back(gemv_op(L, b, xout)); return; }
   const DLevel& C = h->L[l + 1];
   const bool blk = L.WB.n > 0;
   const int tagA = l0 ? 0 : 1;
@@ -319,7 +494,6 @@ void cycle_ops(const DeviceHandle* h, int l, const double* b, double* xout, std:
   const int clsW = l0 ? C_L0_WB : C_COARSE;
   double* X = L.t;
   double* X2 = L.t2;
-  // first pre-smoothing sweep from x = 0
   if (blk) {
     ops->push_back(csr_op(L.WB, EPI_Y, clsW, tagA, b, nullptr, nullptr, nullptr, X));
   } else {
@@ -337,19 +511,15 @@ void cycle_ops(const DeviceHandle* h, int l, const double* b, double* xout, std:
     }
     std::swap(X, X2);
   }
-  // residual, restriction, coarse cycle(s), prolongation
   ops->push_back(csr_op(L.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, nullptr, b, nullptr, L.r));
   ops->push_back(csr_op(L.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, nullptr, nullptr, nullptr, C.b));
-  cycle_ops(h, l + 1, C.b, C.x, ops);
+  cycle_ops_csr(h, l + 1, C.b, C.x, ops);
   if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
     ops->push_back(csr_op(C.A, EPI_RESID, C_MISC, 1, C.x, nullptr, C.b, nullptr, C.c));
-    cycle_ops(h, l + 1, C.c, C.e, ops);
-    Op o;
-    o.kind = OP_AXPY; o.cls = C_MISC; o.n = C.n; o.x = C.e; o.out = C.x; o.bytes = 24.0 * C.n;
-    ops->push_back(o);
+    cycle_ops_csr(h, l + 1, C.c, C.e, ops);
+    ops->push_back(axpy_op(C.n, C.e, C.x));
   }
   ops->push_back(csr_op(L.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, X, nullptr, nullptr, X));
-  // post-smoothing; the last sweep writes xout
   for (int s = 0; s < p.postsmooth_iter; ++s) {
     double* out = (s == p.postsmooth_iter - 1) ? xout : X2;
     if (blk) {
@@ -362,17 +532,80 @@ void cycle_ops(const DeviceHandle* h, int l, const double* b, double* xout, std:
   }
 }
 
-void apply_ops(const DeviceHandle* h, const double* r, double* z, std::vector<Op>* ops) {
-  ops->clear();
-  cycle_ops(h, 0, r, z, ops);
-  const DLevel& L0 = h->L[0];
-  for (int it = 1; it < h->p.maxit; ++it) {   // z += MG(r - A z)
-    ops->push_back(csr_op(L0.A, EPI_RESID, C_MISC, 1, z, nullptr, r, nullptr, L0.c));
-    cycle_ops(h, 0, L0.c, L0.e, ops);
+// ---- BSR2 layout.  b / xout of level 0 are the caller's field-major vectors
+// (stride nv0); all other vectors are node-interleaved (stride 0).
+void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
+                   int64_t os, std::vector<Op>* ops) {
+  const DLevel& L = h->L[l];
+  const mamg_params& p = h->p;
+  const bool l0 = l == 0;
+  if (L.coarsest) { ops->push_back(gemv_op(L, b, xout)); return; }   // l > 0 here
+  const DLevel& C = h->L[l + 1];
+  const int64_t nv = L.n / 2;
+  const int tagA = l0 ? 0 : 1;
+  const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
+  const int clsW = l0 ? C_L0_WB : C_COARSE;
+  double* X = L.t;
+  double* X2 = L.t2;
+  {   // first sweep from x = 0: X = W b
     Op o;
-    o.kind = OP_AXPY; o.cls = C_MISC; o.n = L0.n; o.x = L0.e; o.out = z; o.bytes = 24.0 * L0.n;
+    o.kind = OP_BD; o.cls = clsW; o.n = nv; o.W = L.Wd; o.b = b; o.bs = bs; o.out = X;
+    o.bytes = 32.0 * nv + 16.0 * nv + 16.0 * nv;
     ops->push_back(o);
   }
+  for (int s = 1; s < p.presmooth_iter; ++s) {
+    ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, X2, 0));
+    std::swap(X, X2);
+  }
+  ops->push_back(bsr_op(L.Ab, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs,
+                        nullptr, L.r, 0));
+  ops->push_back(bsr_op(L.Rb, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, 0, nullptr, nullptr, 0,
+                        nullptr, C.b, 0));
+  cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops);
+  if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
+    ops->push_back(bsr_op(C.Ab, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0));
+    cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops);
+    ops->push_back(axpy_op(C.n, C.e, C.x));
+  }
+  ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
+                        nullptr, X, 0));
+  for (int s = 0; s < p.postsmooth_iter; ++s) {
+    const bool last = s == p.postsmooth_iter - 1;
+    double* out = last ? xout : X2;
+    ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, out, last ? os : 0));
+    if (!last) std::swap(X, X2);
+  }
+}
+
+void apply_ops(const DeviceHandle* h, const double* r, double* z, std::vector<Op>* ops) {
+  ops->clear();
+  const DLevel& L0 = h->L[0];
+  if (h->bsr && !L0.coarsest) {
+    const int64_t nv = L0.n / 2;
+    cycle_ops_bsr(h, 0, r, nv, z, nv, ops);
+    for (int it = 1; it < h->p.maxit; ++it) {   // z += MG(r - A z), field-major
+      ops->push_back(bsr_op(L0.Ab, EPI_RESID, C_MISC, 1, z, nv, nullptr, r, nv, nullptr, L0.c, nv));
+      cycle_ops_bsr(h, 0, L0.c, nv, L0.e, nv, ops);
+      ops->push_back(axpy_op(L0.n, L0.e, z));
+    }
+    return;
+  }
+  cycle_ops_csr(h, 0, r, z, ops);
+  for (int it = 1; it < h->p.maxit; ++it) {
+    ops->push_back(csr_op(L0.A, EPI_RESID, C_MISC, 1, z, nullptr, r, nullptr, L0.c));
+    cycle_ops_csr(h, 0, L0.c, L0.e, ops);
+    ops->push_back(axpy_op(L0.n, L0.e, z));
+  }
+}
+
+// y = A0 x / r = b - A0 x on caller-layout vectors (PCG, spmv)
+Op a0_op(const DeviceHandle* h, int epi, const double* x, const double* b, double* out) {
+  const DLevel& L0 = h->L[0];
+  if (h->bsr && L0.Ab.nr > 0) {
+    const int64_t nv = L0.n / 2;
+    return bsr_op(L0.Ab, epi, C_MISC, 1, x, nv, nullptr, b, nv, nullptr, out, nv);
+  }
+  return csr_op(L0.A, epi, C_MISC, 1, x, nullptr, b, nullptr, out);
 }
 
 template <int VL, int TAG>
@@ -408,10 +641,48 @@ void launch_csr_tag(const Op& o, hipStream_t s) {
   }
 }
 
+template <int VL, bool XFM, int TAG>
+void launch_bsr_x(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const unsigned g = nblocks(M.nr * (int64_t)VL);
+  if (g == 0) return;
+#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
+  switch (o.epi) {
+    case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    default: bsr2_kernel<VL, EPI_BJAC, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+  }
+#undef BSR_ARGS
+}
+
+template <int VL, int TAG>
+void launch_bsr_vl(const Op& o, hipStream_t s) {
+  if (o.xfm) launch_bsr_x<VL, true, TAG>(o, s); else launch_bsr_x<VL, false, TAG>(o, s);
+}
+
+template <int TAG>
+void launch_bsr_tag(const Op& o, hipStream_t s) {
+  switch (o.Mb->lanes) {
+    case 2: launch_bsr_vl<2, TAG>(o, s); break;
+    case 4: launch_bsr_vl<4, TAG>(o, s); break;
+    case 8: launch_bsr_vl<8, TAG>(o, s); break;
+    case 16: launch_bsr_vl<16, TAG>(o, s); break;
+    case 32: launch_bsr_vl<32, TAG>(o, s); break;
+    default: launch_bsr_vl<64, TAG>(o, s); break;
+  }
+}
+
 void launch(const Op& o, hipStream_t s) {
   switch (o.kind) {
     case OP_CSR:
       if (o.tag == 0) launch_csr_tag<0>(o, s); else launch_csr_tag<1>(o, s);
+      break;
+    case OP_BSR:
+      if (o.tag == 0) launch_bsr_tag<0>(o, s); else launch_bsr_tag<1>(o, s);
+      break;
+    case OP_BD:
+      if (o.n) bd2_kernel<false><<<nblocks(o.n), 256, 0, s>>>(o.n, o.W, o.b, o.bs, nullptr, o.out, 0);
       break;
     case OP_SCALE:
       if (o.n) scale_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.w, o.x, o.out);
@@ -447,6 +718,21 @@ int get_graph(DeviceHandle* h, const double* r, double* z, hipGraphExec_t* exec,
   return MAMG_OK;
 }
 
+// BSR2 layout usable: 2 fields, every level's smoother node-block diagonal
+bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
+  if (p.num_functions != 2) return false;
+  for (size_t l = 0; l < H.levels.size(); ++l) {
+    const HostLevel& hl = H.levels[l];
+    if (hl.n % 2) return false;
+    if (hl.coarsest) continue;
+    if (hl.WB.n == 0) return false;                     // point smoother: CSR path
+    std::vector<double> blk;
+    if (!node_blocks_of(hl.WB.view(), hl.n / 2, &blk)) return false;
+  }
+  (void)A0;
+  return true;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -462,20 +748,45 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
   const int nl = (int)H.levels.size();
   h->L.resize(nl);
+  h->bsr = bsr_eligible(H, A0, p);
   int rc;
   for (int l = 0; l < nl; ++l) {
     const HostLevel& hl = H.levels[l];
     DLevel& D = h->L[l];
     D.n = hl.n;
     D.coarsest = hl.coarsest;
+    const CsrView Al = l == 0 ? A0 : H.A(l);
+    const int lanesA = l == 0 ? p.spmv_lanes : 0;
     if (D.coarsest) {
       if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
-      HIPCHK(hipMemcpy(D.Ainv, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
-      if (l > 0 && (rc = upload_csr(h.get(), H.A(l), &D.A, 0, err))) return rc;
-      if (l == 0 && (rc = upload_csr(h.get(), A0, &D.A, p.spmv_lanes, err))) return rc;
+      if (h->bsr && l > 0) {      // node-interleaved coarsest vectors: permute
+        std::vector<double> Ap(D.n * D.n);
+        const int64_t nv = D.n / 2;
+        auto pos = [nv](int64_t i) { return 2 * (i % nv) + i / nv; };
+        for (int64_t i = 0; i < D.n; ++i)
+          for (int64_t j = 0; j < D.n; ++j) Ap[pos(i) * D.n + pos(j)] = hl.Ainv[i * D.n + j];
+        HIPCHK(hipMemcpy(D.Ainv, Ap.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
+      } else {
+        HIPCHK(hipMemcpy(D.Ainv, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
+      }
+      if (l == 0) {
+        if ((rc = upload_csr(h.get(), Al, &D.A, lanesA, err))) return rc;
+      } else if (h->bsr) {
+        if ((rc = upload_csr_as_bsr(h.get(), Al, D.n / 2, D.n / 2, &D.Ab, 0, err))) return rc;
+      } else {
+        if ((rc = upload_csr(h.get(), Al, &D.A, 0, err))) return rc;
+      }
+    } else if (h->bsr) {
+      const int64_t nv = D.n / 2, nvc = H.levels[l + 1].n / 2;
+      if ((rc = upload_csr_as_bsr(h.get(), Al, nv, nv, &D.Ab, lanesA, err))) return rc;
+      if ((rc = upload_csr_as_bsr(h.get(), hl.P.view(), nv, nvc, &D.Pb, 0, err))) return rc;
+      if ((rc = upload_csr_as_bsr(h.get(), hl.R.view(), nvc, nv, &D.Rb, 0, err))) return rc;
+      std::vector<double> blk;
+      node_blocks_of(hl.WB.view(), nv, &blk);
+      if ((rc = dalloc(h.get(), &D.Wd, nv, err))) return rc;
+      HIPCHK(hipMemcpy(D.Wd, blk.data(), 4 * nv * sizeof(double), hipMemcpyHostToDevice));
     } else {
-      if ((rc = upload_csr(h.get(), l == 0 ? A0 : H.A(l), &D.A, l == 0 ? p.spmv_lanes : 0, err)))
-        return rc;
+      if ((rc = upload_csr(h.get(), Al, &D.A, lanesA, err))) return rc;
       if ((rc = upload_csr(h.get(), hl.P.view(), &D.P, 0, err))) return rc;
       if ((rc = upload_csr(h.get(), hl.R.view(), &D.R, 0, err))) return rc;
       if (hl.WB.n > 0) {
@@ -511,6 +822,7 @@ void dev_destroy(DeviceHandle* h) {
 int64_t dev_nrows(const DeviceHandle* h) { return h->L[0].n; }
 int dev_num_levels(const DeviceHandle* h) { return (int)h->L.size(); }
 double dev_apply_bytes(const DeviceHandle* h) { return h->apply_bytes; }
+int dev_layout(const DeviceHandle* h) { return h->bsr ? 1 : 0; }
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
@@ -537,8 +849,7 @@ int dev_apply_host(DeviceHandle* h, const double* r, double* z, std::string* err
 
 int dev_spmv(DeviceHandle* h, const double* d_x, double* d_y, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
-  const DLevel& L0 = h->L[0];
-  launch(csr_op(L0.A, EPI_Y, C_MISC, 1, d_x, nullptr, nullptr, nullptr, d_y), (hipStream_t)stream);
+  launch(a0_op(h, EPI_Y, d_x, nullptr, d_y), (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
 }
@@ -570,10 +881,9 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     if ((rc = dalloc(h, &h->dres, 1, err))) return rc;
     HIPCHK(hipHostMalloc((void**)&h->hres, sizeof(double), hipHostMallocDefault));
   }
-  const DLevel& L0 = h->L[0];
   const unsigned g = nblocks(n);
-  launch(csr_op(L0.A, EPI_RESID, C_MISC, 1, d_x, nullptr, d_b, nullptr, h->cr), s);  // r = b - A x
-  if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;                          // z = B r
+  launch(a0_op(h, EPI_RESID, d_x, d_b, h->cr), s);                 // r = b - A x
+  if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;         // z = B r
   HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
   double rz;
   if ((rc = dot(h, n, h->cr, h->cz, s, &rz, err))) return rc;
@@ -583,7 +893,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
   int it = 0;
   int status = MAMG_OK;
   while (residuals[it] > tol_eff && it < maxiter) {
-    launch(csr_op(L0.A, EPI_Y, C_MISC, 1, h->cd, nullptr, nullptr, nullptr, h->cq), s);  // q = A d
+    launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), s);              // q = A d
     double dz;
     if ((rc = dot(h, n, h->cd, h->cq, s, &dz, err))) return rc;
     if (dz == 0.0) break;

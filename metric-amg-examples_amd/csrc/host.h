@@ -64,6 +64,17 @@ int gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz);
 int gen_bidomain(int dim, int64_t n, double gamma, double k1, double k2,
                  int64_t* rowptr, int32_t* colind, double* values);
 
+// convert.cpp: field-major CSR (rows f*nr+I, cols g*nc+J, 2 fields) -> 2x2 BSR
+struct HBsr {
+  int64_t nr = 0, nc = 0;
+  std::vector<int64_t> ptr;
+  std::vector<int32_t> col;
+  std::vector<double> val;   // 4 per block: (0,0) (0,1) (1,0) (1,1)
+};
+void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B);
+// smoother matrix -> one 2x2 block per node; false if it couples two nodes
+bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk);
+
 // hash shared with the oracle (oracle/mamg_oracle.py:hash32)
 inline uint32_t hash32(uint64_t i, int level) {
   uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
