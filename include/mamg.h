@@ -146,6 +146,27 @@ int mamg_hier_level_export(const mamg_hier* h, int l,
                            int64_t* Wptr, int32_t* Wcol, double* Wval,
                            double* winv, int64_t* agg, double* Ainv);
 
+/* ---- multi-GPU partition plan (host only) --------- */
+/* Rank `rank` of `nranks`: contiguous node ranges per level, ghost lists,
+ * send lists, rank-local BSR2 matrices.  Levels with <= rep_nodes nodes (and
+ * all coarser ones) are replicated. */
+typedef struct mamg_plan mamg_plan;
+int mamg_hier_dist_plan(const mamg_hier* h, int rank, int nranks, int64_t rep_nodes,
+                        mamg_plan** out);
+void mamg_plan_free(mamg_plan* p);
+int mamg_plan_num_levels(const mamg_plan* p);
+/* s[16]: nv, replicated, coarsest, o0, o1, nghost, nsend, nbA, nrA, ncA,
+ *        nbP, nrP, ncP, nbR, nrR, ncR */
+int mamg_plan_level_sizes(const mamg_plan* p, int l, int64_t* s);
+/* Export (any pointer may be NULL): ghosts[nghost], ghost_off[nranks+1],
+ * send_idx[nsend], send_off[nranks+1], A/P/Rp as BSR2 (ptr, col, val[4 nb]),
+ * W[4 nloc]. */
+int mamg_plan_level_export(const mamg_plan* p, int l, int64_t* ghosts, int64_t* ghost_off,
+                           int64_t* send_idx, int64_t* send_off,
+                           int64_t* Aptr, int32_t* Acol, double* Aval,
+                           int64_t* Pptr, int32_t* Pcol, double* Pval,
+                           int64_t* Rptr, int32_t* Rcol, double* Rval, double* W);
+
 /* ---- device hierarchy ------------------------------------------------- */
 /* Host setup + upload.  Level-0 matrix is uploaded from A directly. */
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,

@@ -7,8 +7,8 @@ Drop-in for the reference's `metric_mono` hot path:
     xx = AAinv * bb_
 """
 from . import _lib, parameters, problems
-from .amg import HostHierarchy, MetricAMG, metricAMG
+from .amg import DistPlan, HostHierarchy, MetricAMG, metricAMG
 from .krylov import ConjGrad, lanczos_eigenvalues
 
-__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'ConjGrad', 'lanczos_eigenvalues',
+__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'ConjGrad', 'lanczos_eigenvalues',
            'parameters', 'problems', '_lib']

@@ -69,6 +69,12 @@ SIGNATURES = {
     'mamg_hier_level_sizes': (C.c_int, [VP, C.c_int, P_I64]),
     'mamg_hier_level_export': (C.c_int, [VP, C.c_int] + [P_I64, P_I32, P_F64] * 4
                                + [P_F64, P_I64, P_F64]),
+    'mamg_hier_dist_plan': (C.c_int, [VP, C.c_int, C.c_int, C.c_int64, C.POINTER(VP)]),
+    'mamg_plan_free': (None, [VP]),
+    'mamg_plan_num_levels': (C.c_int, [VP]),
+    'mamg_plan_level_sizes': (C.c_int, [VP, C.c_int, P_I64]),
+    'mamg_plan_level_export': (C.c_int, [VP, C.c_int, P_I64, P_I64, P_I64, P_I64]
+                               + [P_I64, P_I32, P_F64] * 3 + [P_F64]),
     'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                              C.POINTER(VP)]),
     'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),

@@ -286,3 +286,66 @@ class HostHierarchy:
             self.close()
         except Exception:
             pass
+
+
+class DistPlan:
+    """Rank-local partition plan of the multi-GPU V-cycle (``mamg_hier_dist_plan``):
+    node ranges, ghost / send lists and rank-local 2x2-block matrices per level."""
+
+    def __init__(self, H: HostHierarchy, rank: int, nranks: int, rep_nodes: int = 32768):
+        self._L = _lib.lib()
+        self.H = H
+        self.rank, self.nranks = rank, nranks
+        h = C.c_void_p()
+        _lib.check(self._L.mamg_hier_dist_plan(H._h, rank, nranks, rep_nodes, C.byref(h)))
+        self._h = h
+
+    @property
+    def num_levels(self):
+        return self._L.mamg_plan_num_levels(self._h)
+
+    def level(self, l):
+        s = (C.c_int64 * 16)()
+        _lib.check(self._L.mamg_plan_level_sizes(self._h, l, s))
+        (nv, rep, coarsest, o0, o1, ng, ns, nbA, nrA, ncA, nbP, nrP, ncP, nbR, nrR, ncR) = list(s)
+        nr = self.nranks
+        out = dict(nv=nv, replicated=bool(rep), coarsest=bool(coarsest), o0=o0, o1=o1,
+                   nloc=o1 - o0, ghosts=np.zeros(ng, np.int64), ghost_off=np.zeros(nr + 1, np.int64),
+                   send_idx=np.zeros(ns, np.int64), send_off=np.zeros(nr + 1, np.int64))
+
+        def alloc(nb, nrows):
+            return (np.zeros(nrows + 1, np.int64), np.zeros(nb, np.int32), np.zeros(4 * nb))
+
+        A = alloc(nbA, nrA)
+        P = alloc(nbP, nrP) if nrP else (None, None, None)
+        R = alloc(nbR, nrR) if nrR else (None, None, None)
+        W = np.zeros(4 * (o1 - o0)) if not coarsest else None
+
+        def p(a, t):
+            return None if a is None else _lib.ptr(a, t)
+
+        args = []
+        for M in (A, P, R):
+            args += [p(M[0], C.c_int64), p(M[1], C.c_int32), p(M[2], C.c_double)]
+        _lib.check(self._L.mamg_plan_level_export(
+            self._h, l, p(out['ghosts'], C.c_int64), p(out['ghost_off'], C.c_int64),
+            p(out['send_idx'], C.c_int64), p(out['send_off'], C.c_int64), *args,
+            p(W, C.c_double)))
+        out['A'] = (A[0], A[1], A[2].reshape(-1, 2, 2), nrA, ncA)
+        if nrP:
+            out['P'] = (P[0], P[1], P[2].reshape(-1, 2, 2), nrP, ncP)
+            out['R'] = (R[0], R[1], R[2].reshape(-1, 2, 2), nrR, ncR)
+        if W is not None:
+            out['W'] = W.reshape(-1, 2, 2)
+        return out
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.mamg_plan_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

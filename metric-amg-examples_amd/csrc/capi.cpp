@@ -7,6 +7,7 @@
 #include <string>
 
 #include "device.h"
+#include "dist.h"
 #include "host.h"
 
 namespace mamg {
@@ -22,6 +23,10 @@ struct mamg_hier {
 
 struct mamg_handle {
   mamg::DeviceHandle* d = nullptr;
+};
+
+struct mamg_plan {
+  mamg::DistPlan P;
 };
 
 using mamg::set_error;
@@ -169,6 +174,55 @@ int mamg_hier_level_export(const mamg_hier* h, int l, int64_t* Aptr, int32_t* Ac
   if (winv && !L.winv.empty()) std::memcpy(winv, L.winv.data(), L.winv.size() * sizeof(double));
   if (agg && !L.agg.empty()) std::memcpy(agg, L.agg.data(), L.agg.size() * sizeof(int64_t));
   if (Ainv && !L.Ainv.empty()) std::memcpy(Ainv, L.Ainv.data(), L.Ainv.size() * sizeof(double));
+  return MAMG_OK;
+}
+
+int mamg_hier_dist_plan(const mamg_hier* h, int rank, int nranks, int64_t rep_nodes,
+                        mamg_plan** out) {
+  GUARD_BEGIN
+  if (!h || !out) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg_plan* p = new mamg_plan();
+  std::string err;
+  int rc = mamg::build_dist_plan(h->H, h->H.A0, rank, nranks, rep_nodes, &p->P, &err);
+  if (rc) { set_error(err); delete p; return rc; }
+  *out = p;
+  return MAMG_OK;
+  GUARD_END
+}
+
+void mamg_plan_free(mamg_plan* p) { delete p; }
+int mamg_plan_num_levels(const mamg_plan* p) { return p ? (int)p->P.levels.size() : MAMG_ERR_ARG; }
+
+int mamg_plan_level_sizes(const mamg_plan* p, int l, int64_t* s) {
+  if (!p || l < 0 || l >= (int)p->P.levels.size() || !s) { set_error("bad level"); return MAMG_ERR_ARG; }
+  const mamg::DistLevel& D = p->P.levels[l];
+  const int64_t v[16] = {D.nv, D.replicated, D.coarsest, D.o0, D.o1, (int64_t)D.ghosts.size(),
+                         (int64_t)D.send_idx.size(),
+                         D.A.ptr.empty() ? 0 : D.A.ptr[D.A.nr], D.A.nr, D.A.nc,
+                         D.P.ptr.empty() ? 0 : D.P.ptr[D.P.nr], D.P.nr, D.P.nc,
+                         D.Rp.ptr.empty() ? 0 : D.Rp.ptr[D.Rp.nr], D.Rp.nr, D.Rp.nc};
+  std::memcpy(s, v, sizeof(v));
+  return MAMG_OK;
+}
+
+int mamg_plan_level_export(const mamg_plan* p, int l, int64_t* ghosts, int64_t* ghost_off,
+                           int64_t* send_idx, int64_t* send_off, int64_t* Aptr, int32_t* Acol,
+                           double* Aval, int64_t* Pptr, int32_t* Pcol, double* Pval, int64_t* Rptr,
+                           int32_t* Rcol, double* Rval, double* W) {
+  if (!p || l < 0 || l >= (int)p->P.levels.size()) { set_error("bad level"); return MAMG_ERR_ARG; }
+  const mamg::DistLevel& D = p->P.levels[l];
+  auto cpv = [](auto* dst, const auto& src) {
+    if (dst && !src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(src[0]));
+  };
+  cpv(ghosts, D.ghosts);
+  cpv(ghost_off, D.ghost_off);
+  cpv(send_idx, D.send_idx);
+  cpv(send_off, D.send_off);
+  cpv(Aptr, D.A.ptr); cpv(Acol, D.A.col); cpv(Aval, D.A.val);
+  cpv(Pptr, D.P.ptr); cpv(Pcol, D.P.col); cpv(Pval, D.P.val);
+  cpv(Rptr, D.Rp.ptr); cpv(Rcol, D.Rp.col); cpv(Rval, D.Rp.val);
+  cpv(W, D.W);
   return MAMG_OK;
 }
 

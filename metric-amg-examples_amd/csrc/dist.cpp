@@ -1,0 +1,224 @@
+// dist.cpp -- row-partition plan for the multi-GPU V-cycle.
+//
+// Every rank runs the same deterministic host setup, so the plan of every rank
+// is computable locally (no setup-time communication).  Per level l, nodes are
+// split into nranks contiguous ranges of equal size (level 0 = z-slabs of the
+// structured mesh; coarse aggregates are numbered by root index, so their
+// ranges are slab-like too).  A level is *replicated* (computed redundantly on
+// every rank, no exchange) once it has <= rep_nodes nodes, and so are all
+// coarser levels.
+//
+// Rank-local data of a distributed level l (node-interleaved vectors
+// [owned | ghost], ghosts sorted by global id, hence grouped by owner rank):
+//   A_loc : owned rows, columns in local numbering
+//   P_loc : owned fine rows, columns = level l+1 local (or global if l+1 is
+//           replicated)
+//   Rp_loc: transpose of P_loc -- rows = level l+1 [owned | ghost] (or all
+//           nodes), columns = owned fine nodes.  R r is formed as partial
+//           sums, then ghost partials are sent to their owners and added in
+//           rank order (deterministic).
+//   ghosts(l) = external columns of A_loc  U  external columns of P_{l-1} loc
+//   send list to q = the owned nodes that are ghosts of q, in q's order.
+#include <omp.h>
+
+#include <algorithm>
+#include <numeric>
+
+#include "dist.h"
+
+namespace mamg {
+namespace {
+
+// owner rank of global node J under the equal-size split
+inline int owner_of(const std::vector<int64_t>& own, int64_t J) {
+  return (int)(std::upper_bound(own.begin(), own.end(), J) - own.begin()) - 1;
+}
+
+// external (non-owned) node columns touched by rows [r0, r1) of B
+void external_cols(const HBsr& B, int64_t r0, int64_t r1, int64_t o0, int64_t o1,
+                   std::vector<int64_t>* out) {
+  std::vector<int64_t> v;
+  for (int64_t I = r0; I < r1; ++I)
+    for (int64_t k = B.ptr[I]; k < B.ptr[I + 1]; ++k) {
+      const int64_t J = B.col[k];
+      if (J < o0 || J >= o1) v.push_back(J);
+    }
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  out->insert(out->end(), v.begin(), v.end());
+}
+
+void sort_unique(std::vector<int64_t>* v) {
+  std::sort(v->begin(), v->end());
+  v->erase(std::unique(v->begin(), v->end()), v->end());
+}
+
+// slice rows [r0, r1) of B and remap columns with map(J) -> local index
+template <class F>
+void slice_remap(const HBsr& B, int64_t r0, int64_t r1, int64_t nc_local, F map, HBsr* out) {
+  out->nr = r1 - r0;
+  out->nc = nc_local;
+  out->ptr.assign(out->nr + 1, 0);
+  for (int64_t I = r0; I < r1; ++I) out->ptr[I - r0 + 1] = out->ptr[I - r0] + (B.ptr[I + 1] - B.ptr[I]);
+  const int64_t nb = out->ptr[out->nr];
+  out->col.resize(nb);
+  out->val.resize(4 * nb);
+  for (int64_t I = r0; I < r1; ++I) {
+    // local column order may differ from global order (ghosts after owned):
+    // keep the block order sorted by local column for coalesced-ish gathers
+    std::vector<std::pair<int32_t, int64_t>> e;
+    for (int64_t k = B.ptr[I]; k < B.ptr[I + 1]; ++k) e.emplace_back((int32_t)map(B.col[k]), k);
+    std::sort(e.begin(), e.end());
+    int64_t o = out->ptr[I - r0];
+    for (auto& pr : e) {
+      out->col[o] = pr.first;
+      for (int q = 0; q < 4; ++q) out->val[4 * o + q] = B.val[4 * pr.second + q];
+      ++o;
+    }
+  }
+}
+
+// transpose a (nr x nc) 2x2-block matrix: blocks transposed too
+void transpose_bsr(const HBsr& B, HBsr* T) {
+  T->nr = B.nc;
+  T->nc = B.nr;
+  T->ptr.assign(T->nr + 1, 0);
+  const int64_t nb = B.ptr[B.nr];
+  for (int64_t k = 0; k < nb; ++k) T->ptr[B.col[k] + 1]++;
+  for (int64_t i = 0; i < T->nr; ++i) T->ptr[i + 1] += T->ptr[i];
+  T->col.resize(nb);
+  T->val.resize(4 * nb);
+  std::vector<int64_t> nx(T->ptr.begin(), T->ptr.end() - 1);
+  for (int64_t I = 0; I < B.nr; ++I)
+    for (int64_t k = B.ptr[I]; k < B.ptr[I + 1]; ++k) {
+      const int64_t d = nx[B.col[k]]++;
+      T->col[d] = (int32_t)I;
+      const double* v = &B.val[4 * k];
+      T->val[4 * d + 0] = v[0];
+      T->val[4 * d + 1] = v[2];
+      T->val[4 * d + 2] = v[1];
+      T->val[4 * d + 3] = v[3];
+    }
+}
+
+}  // namespace
+
+int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
+                    DistPlan* plan, std::string* err) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
+  if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
+  const int nl = (int)H.levels.size();
+  plan->rank = rank;
+  plan->nranks = nranks;
+  plan->levels.assign(nl, DistLevel());
+  // global BSR2 matrices per level
+  std::vector<HBsr> A(nl), P(nl);
+  std::vector<std::vector<double>> W(nl);
+  for (int l = 0; l < nl; ++l) {
+    const HostLevel& hl = H.levels[l];
+    const int64_t nv = hl.n / 2;
+    DistLevel& D = plan->levels[l];
+    D.nv = nv;
+    D.coarsest = hl.coarsest;
+    to_bsr2(l == 0 ? A0 : H.A(l), nv, nv, &A[l]);
+    if (!hl.coarsest) {
+      const int64_t nvc = H.levels[l + 1].n / 2;
+      to_bsr2(hl.P.view(), nv, nvc, &P[l]);
+      if (hl.WB.n == 0 || !node_blocks_of(hl.WB.view(), nv, &W[l])) {
+        *err = "multi-GPU path needs node-block smoothers on every level";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+    }
+  }
+  if (nl < 2) { *err = "multi-GPU path needs at least two levels"; return MAMG_ERR_UNSUPPORTED; }
+  // replication: from the first small level down; the coarsest is always
+  // replicated (dense solve); level 0 never is
+  bool rep = false;
+  for (int l = 0; l < nl; ++l) {
+    DistLevel& D = plan->levels[l];
+    if (l > 0 && (D.nv <= rep_nodes || D.coarsest)) rep = true;
+    D.replicated = rep;
+    D.own.resize(nranks + 1);
+    for (int q = 0; q <= nranks; ++q) D.own[q] = rep ? (q == 0 ? 0 : D.nv) : (D.nv * q) / nranks;
+  }
+  // ghost lists of every rank (needed for send lists)
+  std::vector<std::vector<std::vector<int64_t>>> ghosts(nl, std::vector<std::vector<int64_t>>(nranks));
+#pragma omp parallel for collapse(2) schedule(dynamic, 1)
+  for (int l = 0; l < nl; ++l)
+    for (int q = 0; q < nranks; ++q) {
+      const DistLevel& D = plan->levels[l];
+      if (D.replicated) continue;
+      const int64_t o0 = D.own[q], o1 = D.own[q + 1];
+      std::vector<int64_t> g;
+      external_cols(A[l], o0, o1, o0, o1, &g);
+      if (l > 0) {
+        const DistLevel& F = plan->levels[l - 1];
+        external_cols(P[l - 1], F.own[q], F.own[q + 1], o0, o1, &g);
+      }
+      sort_unique(&g);
+      ghosts[l][q] = std::move(g);
+    }
+  for (int l = 0; l < nl; ++l) {
+    DistLevel& D = plan->levels[l];
+    if (D.replicated) {
+      D.o0 = 0; D.o1 = D.nv; D.nloc = D.nv;
+      D.A = std::move(A[l]);
+      D.W = W[l];
+      D.ghost_off.assign(nranks + 1, 0);
+      D.send_off.assign(nranks + 1, 0);
+      continue;
+    }
+    D.o0 = D.own[rank];
+    D.o1 = D.own[rank + 1];
+    D.nloc = D.o1 - D.o0;
+    D.ghosts = ghosts[l][rank];
+    // ghost groups per owner rank
+    D.ghost_off.assign(nranks + 1, 0);
+    for (int64_t g : D.ghosts) D.ghost_off[owner_of(D.own, g) + 1]++;
+    for (int q = 0; q < nranks; ++q) D.ghost_off[q + 1] += D.ghost_off[q];
+    // send lists: my owned nodes that are ghosts of q, in q's ghost order
+    D.send_off.assign(nranks + 1, 0);
+    D.send_idx.clear();
+    for (int q = 0; q < nranks; ++q) {
+      if (q != rank) {
+        for (int64_t g : ghosts[l][q])
+          if (g >= D.o0 && g < D.o1) D.send_idx.push_back(g - D.o0);
+      }
+      D.send_off[q + 1] = (int64_t)D.send_idx.size();
+    }
+    // local A
+    const int64_t o0 = D.o0, o1 = D.o1, nloc = D.nloc;
+    const std::vector<int64_t>& gl = D.ghosts;
+    auto mapA = [&](int64_t J) -> int64_t {
+      if (J >= o0 && J < o1) return J - o0;
+      return nloc + (std::lower_bound(gl.begin(), gl.end(), J) - gl.begin());
+    };
+    slice_remap(A[l], o0, o1, nloc + (int64_t)gl.size(), mapA, &D.A);
+    D.W.assign(W[l].begin() + 4 * o0, W[l].begin() + 4 * o1);
+  }
+  // P_loc / Rp_loc (need level l+1 numbering)
+  for (int l = 0; l + 1 < nl; ++l) {
+    DistLevel& D = plan->levels[l];
+    if (D.replicated) {
+      D.P = std::move(P[l]);
+      transpose_bsr(D.P, &D.Rp);
+      continue;
+    }
+    const DistLevel& C = plan->levels[l + 1];
+    const int64_t c0 = C.o0, c1 = C.o1, cnloc = C.nloc;
+    const std::vector<int64_t>& cg = C.ghosts;
+    const bool crep = C.replicated;
+    auto mapC = [&](int64_t J) -> int64_t {
+      if (crep) return J;
+      if (J >= c0 && J < c1) return J - c0;
+      return cnloc + (std::lower_bound(cg.begin(), cg.end(), J) - cg.begin());
+    };
+    const int64_t ncl = crep ? C.nv : cnloc + (int64_t)cg.size();
+    slice_remap(P[l], D.o0, D.o1, ncl, mapC, &D.P);
+    transpose_bsr(D.P, &D.Rp);
+  }
+  (void)err;
+  return MAMG_OK;
+}
+
+}  // namespace mamg

@@ -1,0 +1,34 @@
+// dist.h -- rank-local plan of the row-partitioned V-cycle (see dist.cpp).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "host.h"
+
+namespace mamg {
+
+struct DistLevel {
+  int64_t nv = 0;                 // global nodes
+  bool coarsest = false;
+  bool replicated = false;        // computed redundantly on every rank
+  std::vector<int64_t> own;       // [nranks+1] node ranges
+  int64_t o0 = 0, o1 = 0, nloc = 0;
+  std::vector<int64_t> ghosts;    // global ids, sorted (grouped by owner)
+  std::vector<int64_t> ghost_off; // [nranks+1] ghost ranges per owner rank
+  std::vector<int64_t> send_idx;  // owned local node indices, per dest rank
+  std::vector<int64_t> send_off;  // [nranks+1]
+  HBsr A;                         // owned rows x [owned | ghost] (replicated: global)
+  HBsr P;                         // owned fine rows x level l+1 local (or global)
+  HBsr Rp;                        // transpose of P (partial restriction)
+  std::vector<double> W;          // 4 per owned node
+};
+
+struct DistPlan {
+  int rank = 0, nranks = 1;
+  std::vector<DistLevel> levels;
+};
+
+int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
+                    DistPlan* plan, std::string* err);
+
+}  // namespace mamg

@@ -1,0 +1,184 @@
+"""CPU restatement of the row-partitioned V-cycle -- TEST INFRASTRUCTURE ONLY.
+
+Runs the distributed algorithm of DESIGN.md section 6 / csrc/dist.cpp on the product's
+rank-local plans (``metric_amg_examples_amd.DistPlan``) with numpy, exchanging
+halos through a Comm object: ``GlooComm`` (torch.distributed, one process per
+rank) or ``ThreadComm`` (ranks as threads of one process, queue exchange).
+Tests compare the gathered result with the single-rank oracle
+(mamg_oracle.Hierarchy.apply): the partition must not change the cycle beyond
+summation order.
+
+Per distributed level (V-cycle, nu1 = nu2 = 1):
+  X = W b ; halo(X) ; r = b - A X ;
+  part = Rp r ; [next distributed: reverse-add ghost partials to owners |
+                 next replicated: all-reduce] ; xc = cycle(l+1, bc) ;
+  [next distributed: halo(xc)] ; X += P xc ; halo(X) ; z = X + W (b - A X)
+Replicated levels run the same cycle on global arrays without exchange.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+
+import numpy as np
+
+
+def bsr_mv(M, x2):
+    """M = (ptr, col, val[nb,2,2], nr, nc); x2 (nc, 2) -> (nr, 2)."""
+    ptr, col, val, nr, _ = M
+    y = np.zeros((nr, 2))
+    if len(col):
+        rows = np.repeat(np.arange(nr), np.diff(ptr))
+        np.add.at(y, rows, np.einsum('kfg,kg->kf', val, x2[col]))
+    return y
+
+
+def bd_mv(W, b2):
+    return np.einsum('ifg,ig->if', W, b2)
+
+
+class ThreadComm:
+    """In-process exchange between rank threads (queues per ordered pair)."""
+
+    def __init__(self, nranks):
+        self.n = nranks
+        self.q = {(a, b): queue.Queue() for a in range(nranks) for b in range(nranks)}
+        self.bar = threading.Barrier(nranks)
+        self.red = [None] * nranks
+
+    def view(self, rank):
+        return _ThreadView(self, rank)
+
+
+class _ThreadView:
+    def __init__(self, c, rank):
+        self.c, self.rank, self.n = c, rank, c.n
+
+    def sendrecv(self, sends, recv_shapes):
+        """sends: {q: array}, recv_shapes: {q: shape} -> {q: array}"""
+        for q, a in sends.items():
+            self.c.q[(self.rank, q)].put(np.array(a, copy=True))
+        return {q: self.c.q[(q, self.rank)].get(timeout=60).reshape(s)
+                for q, s in recv_shapes.items()}
+
+    def allreduce_sum(self, a):
+        self.c.red[self.rank] = np.array(a, copy=True)
+        self.c.bar.wait()
+        out = self.c.red[0].copy()
+        for r in range(1, self.n):           # fixed rank order
+            out = out + self.c.red[r]
+        self.c.bar.wait()
+        return out
+
+
+class GlooComm:
+    """torch.distributed (gloo) exchange; one process per rank."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.d = dist
+        self.rank, self.n = dist.get_rank(), dist.get_world_size()
+
+    def sendrecv(self, sends, recv_shapes):
+        import torch
+        reqs, bufs = [], {}
+        for q, s in recv_shapes.items():
+            bufs[q] = torch.zeros(int(np.prod(s)), dtype=torch.float64)
+            reqs.append(self.d.irecv(bufs[q], src=q))
+        for q, a in sends.items():
+            reqs.append(self.d.isend(torch.as_tensor(np.ascontiguousarray(a).ravel()), dst=q))
+        for r in reqs:
+            r.wait()
+        return {q: bufs[q].numpy().reshape(recv_shapes[q]) for q in recv_shapes}
+
+    def allreduce_sum(self, a):
+        import torch
+        parts = [torch.zeros(a.size, dtype=torch.float64) for _ in range(self.n)]
+        self.d.all_gather(parts, torch.as_tensor(np.ascontiguousarray(a).ravel()))
+        out = parts[0].numpy().reshape(a.shape).copy()
+        for r in range(1, self.n):
+            out = out + parts[r].numpy().reshape(a.shape)
+        return out
+
+
+class DistCycle:
+    def __init__(self, plan_levels, Ainv_nodemajor, comm):
+        self.L = plan_levels
+        self.Ainv = Ainv_nodemajor
+        self.comm = comm
+
+    # forward halo: fill ghost rows of x2 (nloc+ng, 2)
+    def halo(self, lv, x2):
+        me, n = self.comm.rank, self.comm.n
+        so, si, go = lv['send_off'], lv['send_idx'], lv['ghost_off']
+        sends = {q: x2[si[so[q]:so[q + 1]]] for q in range(n) if q != me and so[q + 1] > so[q]}
+        shapes = {q: (go[q + 1] - go[q], 2) for q in range(n) if q != me and go[q + 1] > go[q]}
+        got = self.comm.sendrecv(sends, shapes)
+        for q, a in got.items():
+            x2[lv['nloc'] + go[q]: lv['nloc'] + go[q + 1]] = a
+
+    # reverse: ghost partials -> owners, added in rank order
+    def reverse_add(self, lv, part):
+        me, n = self.comm.rank, self.comm.n
+        so, si, go = lv['send_off'], lv['send_idx'], lv['ghost_off']
+        nloc = lv['nloc']
+        sends = {q: part[nloc + go[q]: nloc + go[q + 1]] for q in range(n)
+                 if q != me and go[q + 1] > go[q]}
+        shapes = {q: (so[q + 1] - so[q], 2) for q in range(n) if q != me and so[q + 1] > so[q]}
+        got = self.comm.sendrecv(sends, shapes)
+        out = part[:nloc].copy()
+        for q in sorted(got):
+            np.add.at(out, si[so[q]:so[q + 1]], got[q])
+        return out
+
+    def cycle(self, l, b2):
+        lv = self.L[l]
+        if lv['coarsest']:
+            return (self.Ainv @ b2.ravel()).reshape(-1, 2)
+        C = self.L[l + 1]
+        if lv['replicated']:
+            X = bd_mv(lv['W'], b2)
+            r = b2 - bsr_mv(lv['A'], X)
+            xc = self.cycle(l + 1, bsr_mv(lv['R'], r))
+            X = X + bsr_mv(lv['P'], xc)
+            return X + bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
+        nloc, ng = lv['nloc'], len(lv['ghosts'])
+        Xg = np.zeros((nloc + ng, 2))
+        Xg[:nloc] = bd_mv(lv['W'], b2)
+        self.halo(lv, Xg)
+        r = b2 - bsr_mv(lv['A'], Xg)
+        part = bsr_mv(lv['R'], r)
+        if C['replicated']:
+            bc = self.comm.allreduce_sum(part)
+        else:
+            bc = self.reverse_add(C, part)
+        xc = self.cycle(l + 1, bc)
+        if not C['replicated']:
+            xcg = np.zeros((C['nloc'] + len(C['ghosts']), 2))
+            xcg[:C['nloc']] = xc
+            self.halo(C, xcg)
+        else:
+            xcg = xc
+        Xg[:nloc] = Xg[:nloc] + bsr_mv(lv['P'], xcg)
+        self.halo(lv, Xg)
+        return Xg[:nloc] + bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
+
+    def apply_local(self, r_local_fieldmajor):
+        """r_local: [u1 owned ; u2 owned] (length 2*nloc) -> z_local, same layout."""
+        nloc = self.L[0]['nloc']
+        b2 = np.stack([r_local_fieldmajor[:nloc], r_local_fieldmajor[nloc:]], axis=1)
+        z2 = self.cycle(0, b2)
+        return np.concatenate([z2[:, 0], z2[:, 1]])
+
+
+def nodemajor_Ainv(Ainv):
+    n = Ainv.shape[0]
+    nv = n // 2
+    pos = np.array([2 * (i % nv) + i // nv for i in range(n)])
+    out = np.empty_like(Ainv)
+    out[np.ix_(pos, pos)] = Ainv
+    return out
+
+
+def local_slice(v, nv, o0, o1):
+    return np.concatenate([v[o0:o1], v[nv + o0: nv + o1]])

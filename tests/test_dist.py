@@ -1,0 +1,143 @@
+"""Multi-GPU partition logic on CPU (no GPU): the product's rank-local plans
+(mamg_hier_dist_plan) drive a numpy restatement of the distributed cycle
+(oracle/dist_ref.py) whose gathered result must equal the single-rank
+oracle apply -- with ranks as threads (P = 1..4) and as a world-size-2 gloo
+process group (127.0.0.1)."""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+import dist_ref as dr
+import mamg_oracle as mo
+
+
+def _setup(n=16, g=1e4, dim=3):
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(dim, n, g)
+    H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2)
+    return M, s, H
+
+
+def _gather(s, lvls0, outs):
+    z = np.zeros(s.N)
+    for L0, o in zip(lvls0, outs):
+        nloc = L0['nloc']
+        z[L0['o0']:L0['o1']] = o[:nloc]
+        z[s.nv + L0['o0']:s.nv + L0['o1']] = o[nloc:]
+    return z
+
+
+@pytest.mark.parametrize('P,rep', [(1, 100), (2, 100), (2, 10 ** 6), (3, 100), (4, 100)])
+def test_dist_cycle_threads(lib_built, P, rep):
+    M, s, H = _setup()
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    Ainv = dr.nodemajor_Ainv(H.level(H.num_levels - 1)['Ainv'])
+    plans = [M.DistPlan(H, p, P, rep) for p in range(P)]
+    lvls = [[pl.level(l) for l in range(pl.num_levels)] for pl in plans]
+    comm = dr.ThreadComm(P)
+    outs = [None] * P
+
+    def run(p):
+        L0 = lvls[p][0]
+        dc = dr.DistCycle(lvls[p], Ainv, comm.view(p))
+        outs[p] = dc.apply_local(dr.local_slice(r, s.nv, L0['o0'], L0['o1']))
+
+    th = [threading.Thread(target=run, args=(p,)) for p in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    z = _gather(s, [lv[0] for lv in lvls], outs)
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-13
+
+
+def test_plan_invariants(lib_built):
+    M, s, H = _setup(n=16)
+    P = 3
+    plans = [M.DistPlan(H, p, P, 100) for p in range(P)]
+    for l in range(plans[0].num_levels):
+        L = [pl.level(l) for pl in plans]
+        if L[0]['replicated']:
+            assert all(x['nloc'] == x['nv'] for x in L)
+            continue
+        # ownership covers every node exactly once
+        assert L[0]['o0'] == 0 and L[-1]['o1'] == L[0]['nv']
+        assert all(L[p]['o1'] == L[p + 1]['o0'] for p in range(P - 1))
+        for p in range(P):
+            g = L[p]['ghosts']
+            assert np.all(np.diff(g) > 0)
+            assert not np.any((g >= L[p]['o0']) & (g < L[p]['o1']))
+            # my send list to q == q's ghosts that I own, same order
+            for q in range(P):
+                if q == p:
+                    continue
+                mine = L[p]['send_idx'][L[p]['send_off'][q]:L[p]['send_off'][q + 1]] + L[p]['o0']
+                gq = L[q]['ghosts']
+                want = gq[(gq >= L[p]['o0']) & (gq < L[p]['o1'])]
+                assert np.array_equal(mine, want)
+                go = L[q]['ghost_off']
+                assert np.array_equal(gq[go[p]:go[p + 1]], want)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _gloo_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, 'oracle')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import dist_ref
+        import mamg_oracle
+        import metric_amg_examples_amd as M
+        s = M.problems.bidomain(3, 16, 1e4)
+        H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2)
+        plan = M.DistPlan(H, rank, world, 100)
+        lv = [plan.level(l) for l in range(plan.num_levels)]
+        Ainv = dist_ref.nodemajor_Ainv(H.level(H.num_levels - 1)['Ainv'])
+        r = mamg_oracle.seeded_rhs(s.N)
+        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm())
+        z = dc.apply_local(dist_ref.local_slice(r, s.nv, lv[0]['o0'], lv[0]['o1']))
+        q.put((rank, lv[0]['o0'], lv[0]['o1'], z))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_cycle_gloo_world2(lib_built):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e4)
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    z = np.zeros(s.N)
+    for rank, o0, o1, zl in res:
+        nloc = o1 - o0
+        z[o0:o1] = zl[:nloc]
+        z[s.nv + o0:s.nv + o1] = zl[nloc:]
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-13
