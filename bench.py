@@ -4,17 +4,20 @@ second and achieved HBM GB/s on the bidomain_3d nrefs=6 system
 (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--nrefs 6] [--dim 3]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (multi-GPU)
 
 A step = one preconditioner application z = B r (one V-cycle from x0 = 0) on
 a resident seeded r (uniform(-1,1), seed 1234) -- the unit of work of the
 reference's hot loop (`BB * r` inside ConjGrad, src/bidomain_3d.py:149-150).
 The timed region runs K applies kernel by kernel on one stream with HIP
-events around the dominant kernel (level-0 residual SpMV) of every step;
-`value` = K * n_gpus / max-over-ranks wall time.  N > 1: until the
-row-partitioned multi-GPU cycle lands, every rank applies the full
-preconditioner on its own GPU (independent replicas, "scaling": "weak").
-The cpu_baseline leg times the oracle's C restatement (oracle/vcycle_ref.c)
-of the same cycle on the same hierarchy on the host cores (rank 0, N = 1).
+events around the dominant kernel (level-0 residual SpMV) of every step,
+bracketed by barrier + synchronize.  value = K / max-over-ranks wall time
+(applies of the whole problem per second).
+N = 1: the whole hierarchy on one GPU (BSR2 layout, hipGraph replay also
+reported).  N > 1: the same problem row-partitioned over N GPUs (one process
+per GPU, RCCL halo exchange over xGMI; strong scaling).
+The cpu_baseline leg (rank 0, N = 1) times the oracle's C restatement
+(oracle/vcycle_ref.c) of the same cycle on the same hierarchy on the host.
 """
 import argparse
 import json
@@ -29,10 +32,20 @@ sys.path.insert(0, ROOT)
 
 METRIC = "V-cycle applies/sec + HBM GB/s, bidomain_3d nrefs=6 @1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md); 6290 measured copy
+CLASS_NAMES = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_prolong',
+               'coarse_levels', 'coarsest_dense', 'misc', 'comm']
 
 
 def log(*a):
     print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def breakdown_dict(kms, cbytes, ms_all):
+    out = {nm: {'ms': round(kms[i], 4), 'GB': round(cbytes[i] / 1e9, 4),
+                'GBps': round(cbytes[i] / 1e9 / (kms[i] * 1e-3), 1) if kms[i] > 0 else None}
+           for i, nm in enumerate(CLASS_NAMES)}
+    out['instrumented_ms_per_apply'] = round(ms_all, 4)
+    return out
 
 
 def main():
@@ -43,21 +56,22 @@ def main():
     ap.add_argument('--dim', type=int, default=3)
     ap.add_argument('--nrefs', type=int, default=6)
     ap.add_argument('--gamma', type=float, default=1e6)
+    ap.add_argument('--rep-nodes', type=int, default=32768,
+                    help='multi-GPU: replicate levels with <= this many nodes')
     ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
-    ap.add_argument('--pcg', action='store_true', help='also run one full PCG solve')
+    ap.add_argument('--pcg', action='store_true', help='also run one full PCG solve (N = 1)')
     args = ap.parse_args()
 
     import torch
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
 
     import metric_amg_examples_amd as M
 
@@ -66,18 +80,6 @@ def main():
     sysm = M.problems.bidomain(args.dim, n, args.gamma)
     t_gen = time.time() - t0
     log('rank %d: generated %dD n=%d N=%d nnz=%d in %.1fs' % (rank, args.dim, n, sysm.N, sysm.nnz, t_gen))
-    t0 = time.time()
-    H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
-    t_setup = time.time() - t0
-    t0 = time.time()
-    B = M.MetricAMG.from_host(H, sysm.W)
-    t_upload = time.time() - t0
-    sizes = [H.sizes(l) for l in range(H.num_levels)]
-    log('rank %d: host setup %.1fs, upload %.1fs, levels %s' % (
-        rank, t_setup, t_upload, [(s['n'], s['nnzA']) for s in sizes]))
-
-    r = torch.as_tensor(M.problems.seeded_rhs(sysm.N)).to(dev)
-    z = torch.empty_like(r)
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
@@ -86,7 +88,48 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize(dev)
 
-    # warmup (graph path + eager path)
+    def allmax(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return t.item()
+
+    def allsum(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
+        return t.item()
+
+    r_full = M.problems.seeded_rhs(sysm.N)
+    H = None
+    if world == 1:
+        t0 = time.time()
+        H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+        t_setup = time.time() - t0
+        t0 = time.time()
+        B = M.MetricAMG.from_host(H, sysm.W)
+        t_upload = time.time() - t0
+        sizes = [H.sizes(l) for l in range(H.num_levels)]
+        levels = [[s['n'], s['nnzA']] for s in sizes]
+        layout = B.layout
+        r = torch.as_tensor(r_full).to(dev)
+    else:
+        uid = [M.DistMetricAMG.unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(uid, src=0)
+        t0 = time.time()
+        B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
+                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local)
+        t_setup = time.time() - t0
+        t_upload = 0.0
+        levels = None
+        layout = 'bsr2-dist'
+        r = torch.as_tensor(B.local_slice(r_full)).to(dev)
+        log('rank %d: nodes [%d, %d) of %d, setup+upload %.1fs' % (rank, B.o0, B.o1, B.nv, t_setup))
+    z = torch.zeros_like(r)
+
+    # warmup
     for _ in range(max(1, args.warmup)):
         B.apply_device(r, z, stream)
     B.time_apply(r, z, max(1, args.warmup), 0, stream)
@@ -96,47 +139,37 @@ def main():
     t0 = time.perf_counter()
     ms_ev, kms, cbytes = B.time_apply(r, z, args.steps, 0, stream)
     barrier()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        wall = t.item()
+    wall = allmax(time.perf_counter() - t0)
     ms_per_step = 1e3 * wall / args.steps
-    value = args.steps * world / wall
-    apply_bytes = B.apply_bytes
-    dom_bytes = cbytes[0]                   # level-0 residual: one launch per apply
+    value = args.steps / wall
+    apply_bytes = allsum(B.apply_bytes)
+    dom_bytes = cbytes[0]                   # level-0 residual: one launch per apply (per rank)
     dom_ms = kms[0]
 
-    # graph-replay throughput (same work, one hipGraph launch per apply)
-    barrier()
-    g0 = torch.cuda.Event(enable_timing=True)
-    g1 = torch.cuda.Event(enable_timing=True)
-    g0.record(stream)
-    for _ in range(args.steps):
-        B.apply_device(r, z, stream)
-    g1.record(stream)
-    barrier()
-    graph_ms = g0.elapsed_time(g1) / args.steps
+    graph_ms = None
+    if world == 1:                          # hipGraph replay of the same work
+        barrier()
+        g0 = torch.cuda.Event(enable_timing=True)
+        g1 = torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        for _ in range(args.steps):
+            B.apply_device(r, z, stream)
+        g1.record(stream)
+        barrier()
+        graph_ms = round(g0.elapsed_time(g1) / args.steps, 4)
 
     breakdown = None
     if not args.no_breakdown:
         ms_all, kms_all, _ = B.time_apply(r, z, max(3, args.steps // 4), 1, stream)
-        names = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_prolong',
-                 'coarse_levels', 'coarsest_dense', 'misc']
-        breakdown = {nm: {'ms': round(kms_all[i], 4),
-                          'GB': round(cbytes[i] / 1e9, 4),
-                          'GBps': round(cbytes[i] / 1e9 / (kms_all[i] * 1e-3), 1) if kms_all[i] > 0 else None}
-                     for i, nm in enumerate(names)}
-        breakdown['instrumented_ms_per_apply'] = round(ms_all, 4)
+        barrier()
+        breakdown = breakdown_dict(kms_all, cbytes, ms_all)
 
     pcg = None
-    if args.pcg and rank == 0:
-        b = M.problems.seeded_rhs(sysm.N)
-        Aop = sysm
-        B._Aop = Aop
-        solver = M.ConjGrad(Aop, precond=B, tolerance=1e-8, maxiter=500)
+    if args.pcg and world == 1:
+        B._Aop = sysm
+        solver = M.ConjGrad(sysm, precond=B, tolerance=1e-8, maxiter=500)
         t0 = time.time()
-        solver * b
+        solver * r_full
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
                'seconds': round(time.time() - t0, 3)}
 
@@ -145,34 +178,34 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import cref
-        levels = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
-        levels[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
-        ch = cref.CHierarchy(levels)
-        rh = M.problems.seeded_rhs(sysm.N)
-        ch.apply(rh)                                         # warm (page-in)
+        lv = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
+        lv[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
+        ch = cref.CHierarchy(lv)
+        ch.apply(r_full)                                     # warm (page-in)
         t0 = time.time()
         for _ in range(args.cpu_sample):
-            zc = ch.apply(rh)
+            zc = ch.apply(r_full)
         tc = (time.time() - t0) / args.cpu_sample
         zg = z.cpu().numpy()
         err = float(np.linalg.norm(zc - zg) / np.linalg.norm(zc))
         cpu = {'value': round(1.0 / tc, 4), 'unit': 'V-cycle applies/s', 'cores': ch.threads(),
                'kind': 'port',
-               'sample': '%d applies of the full %s hierarchy (oracle/vcycle_ref.c, OpenMP), '
-                         'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, 'nrefs=%d' % args.nrefs, err)}
-        del ch, levels
+               'sample': '%d applies of the full nrefs=%d hierarchy (oracle/vcycle_ref.c, OpenMP), '
+                         'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, args.nrefs, err)}
+        del ch, lv
 
     traffic = None
-    tpath = os.path.join(ROOT, 'profiles', 'traffic_r01.json')
-    if os.path.exists(tpath):
+    tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
+    if os.path.exists(tpath) and world == 1:
         try:
             tj = json.load(open(tpath))
-            if tj.get('N') == sysm.N:
+            if tj.get('N') == sysm.N and tj.get('layout') == layout:
                 traffic = tj.get('dominant_bytes_per_launch')
         except Exception:
             traffic = None
 
     achieved = dom_bytes / 1e9 / (dom_ms * 1e-3) if dom_ms > 0 else None
+    kname = 'bsr2_kernel' if layout.startswith('bsr2') else 'csr_kernel'
     out = {
         'metric': METRIC,
         'value': round(value, 3),
@@ -182,25 +215,24 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': round(ms_per_step, 4),
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': 'strong',
         'vs_baseline': None,
         'dtype': 'f64',
         'data': 'synthetic (P1 bidomain matrix generated in-library; r = uniform(-1,1), seed 1234)',
         'config': {
             'workload': 'bidomain_%dd nrefs=%d gamma=%g metric_mono (profile mi355x_sa_v, nodal SA V-cycle)'
                         % (args.dim, args.nrefs, args.gamma),
-            'n': n, 'N': sysm.N, 'nnz': sysm.nnz,
-            'levels': [[s['n'], s['nnzA']] for s in sizes],
-            'parallelism': 'replicas' if world > 1 else 'single',
-            'device_layout': B.layout,
+            'n': n, 'N': sysm.N, 'nnz': sysm.nnz, 'levels': levels,
+            'parallelism': 'single' if world == 1 else 'row-partition x%d (RCCL halo)' % world,
+            'device_layout': layout,
         },
         'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),
         'apply_GB_alg': round(apply_bytes / 1e9, 4),
-        'graph_ms_per_step': round(graph_ms, 4),
+        'graph_ms_per_step': graph_ms,
         'roofline': {
             'bound': 'hbm',
-            'kernel': 'level-0 residual r = b - A0 x (%s<*,RESID,...,0>)'
-                      % ('bsr2_kernel' if B.layout == 'bsr2' else 'csr_kernel'),
+            'kernel': 'level-0 residual r = b - A0 x (%s<*,RESID,...,0>)%s'
+                      % (kname, '' if world == 1 else ', rank 0 slice'),
             'achieved': round(achieved, 1) if achieved else None,
             'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
@@ -216,7 +248,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     B.close()
-    H.close()
+    if H is not None:
+        H.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -167,6 +167,32 @@ int mamg_plan_level_export(const mamg_plan* p, int l, int64_t* ghosts, int64_t* 
                            int64_t* Pptr, int32_t* Pcol, double* Pval,
                            int64_t* Rptr, int32_t* Rcol, double* Rval, double* W);
 
+/* ---- multi-GPU apply (one process per GPU, RCCL over xGMI) ------------- */
+typedef struct mamg_dhandle mamg_dhandle;
+/* size of the RCCL unique id (128); rank 0 creates it, every rank passes it */
+int mamg_comm_id_bytes(void);
+int mamg_comm_unique_id(void* id);
+/* Every rank passes the same global A / idofs / params (the host setup is
+ * replicated and deterministic) and uploads only its node range of each
+ * level; levels with <= rep_nodes nodes are replicated.  V-cycle only. */
+int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, int rank, int nranks, const void* comm_id,
+                    int64_t rep_nodes, mamg_dhandle** out);
+/* local node range [o0, o1) of level 0; local vectors are field-major
+ * [u1(o0:o1); u2(o0:o1)] of length 2*(o1-o0) */
+int mamg_dist_range(const mamg_dhandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
+int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes);
+int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r_local, double* d_z_local,
+                           void* stream);
+int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int reps, int mode,
+                         double* ms_per_apply, double* kernel_ms, double* class_bytes,
+                         void* stream);
+/* Test mode: handles created with comm_id == NULL (no RCCL) on one device;
+ * apply all n ranks in lockstep, exchanges as device copies. */
+int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double** d_z,
+                            void* stream);
+void mamg_dist_destroy(mamg_dhandle* h);
+
 /* ---- device hierarchy ------------------------------------------------- */
 /* Host setup + upload.  Level-0 matrix is uploaded from A directly. */
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,

@@ -75,6 +75,16 @@ SIGNATURES = {
     'mamg_plan_level_sizes': (C.c_int, [VP, C.c_int, P_I64]),
     'mamg_plan_level_export': (C.c_int, [VP, C.c_int, P_I64, P_I64, P_I64, P_I64]
                                + [P_I64, P_I32, P_F64] * 3 + [P_F64]),
+    'mamg_comm_id_bytes': (C.c_int, []),
+    'mamg_comm_unique_id': (C.c_int, [C.c_char_p]),
+    'mamg_setup_dist': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                                  C.c_int, C.c_int, C.c_char_p, C.c_int64, C.POINTER(VP)]),
+    'mamg_dist_range': (C.c_int, [VP, P_I64, P_I64, P_I64]),
+    'mamg_dist_apply_bytes': (C.c_int, [VP, P_F64]),
+    'mamg_dist_apply_device': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_dist_time_apply': (C.c_int, [VP, VP, VP, C.c_int, C.c_int, P_F64, P_F64, P_F64, VP]),
+    'mamg_dist_virtual_apply': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
+    'mamg_dist_destroy': (None, [VP]),
     'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                              C.POINTER(VP)]),
     'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),

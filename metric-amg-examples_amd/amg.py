@@ -349,3 +349,88 @@ class DistPlan:
             self.close()
         except Exception:
             pass
+
+
+class DistMetricAMG:
+    """Multi-GPU preconditioner: one process per GPU (``mamg_setup_dist``).
+
+    Every rank passes the same global A (the deterministic host setup is
+    replicated) and applies B to its local slice r_local = [u1(o0:o1);
+    u2(o0:o1)] (field-major, length 2*(o1-o0)).  comm_id: bytes from
+    ``DistMetricAMG.unique_id()`` on rank 0, broadcast to all ranks; None
+    builds a virtual (single-GPU, no RCCL) rank for tests."""
+
+    def __init__(self, A, W=None, idofs=None, parameters=None, rank=0, nranks=1, comm_id=None,
+                 rep_nodes=32768, **overrides):
+        self._L = _lib.lib()
+        indptr, indices, data, n, m = csr_arrays(A)
+        self.shape = (n, n)
+        self.W = _dims(W, n)
+        self.params = make_params(parameters, **overrides)
+        self._A = (indptr, indices, data)
+        csr = _lib.as_csr_struct(indptr, indices, data, m)
+        if idofs is not None:
+            self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
+            ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
+        else:
+            self.idofs, ip, ni = None, None, 0
+        h = C.c_void_p()
+        _lib.check(self._L.mamg_setup_dist(C.byref(csr), ip, ni, C.byref(self.params), rank, nranks,
+                                           comm_id, int(rep_nodes), C.byref(h)))
+        self._h = h
+        self.rank, self.nranks = rank, nranks
+        o0, o1, nv = C.c_int64(), C.c_int64(), C.c_int64()
+        _lib.check(self._L.mamg_dist_range(h, C.byref(o0), C.byref(o1), C.byref(nv)))
+        self.o0, self.o1, self.nv = o0.value, o1.value, nv.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = _lib.lib()
+        buf = C.create_string_buffer(L.mamg_comm_id_bytes())
+        _lib.check(L.mamg_comm_unique_id(buf))
+        return buf.raw
+
+    @property
+    def nloc(self):
+        return self.o1 - self.o0
+
+    def local_slice(self, v):
+        return np.concatenate([v[self.o0:self.o1], v[self.nv + self.o0:self.nv + self.o1]])
+
+    @property
+    def apply_bytes(self):
+        b = C.c_double()
+        _lib.check(self._L.mamg_dist_apply_bytes(self._h, C.byref(b)))
+        return b.value
+
+    def apply_device(self, r, z, stream=None):
+        _lib.check(self._L.mamg_dist_apply_device(self._h, _device_ptr(r), _device_ptr(z),
+                                                  _stream_ptr(stream)))
+        return z
+
+    def time_apply(self, r, z, reps, mode=0, stream=None):
+        ms = C.c_double()
+        kms = (C.c_double * 16)()
+        cb = (C.c_double * 16)()
+        _lib.check(self._L.mamg_dist_time_apply(self._h, _device_ptr(r), _device_ptr(z), int(reps),
+                                                int(mode), C.byref(ms), kms, cb, _stream_ptr(stream)))
+        return ms.value, list(kms), list(cb)
+
+    @staticmethod
+    def virtual_apply(handles, rs, zs, stream=None):
+        n = len(handles)
+        H = (C.c_void_p * n)(*[h._h.value for h in handles])
+        R = (C.c_void_p * n)(*[_device_ptr(r).value for r in rs])
+        Z = (C.c_void_p * n)(*[_device_ptr(z).value for z in zs])
+        _lib.check(_lib.lib().mamg_dist_virtual_apply(H, n, R, Z, _stream_ptr(stream)))
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.mamg_dist_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

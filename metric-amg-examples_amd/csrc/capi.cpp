@@ -29,6 +29,10 @@ struct mamg_plan {
   mamg::DistPlan P;
 };
 
+struct mamg_dhandle {
+  mamg::DistHandle* d = nullptr;
+};
+
 using mamg::set_error;
 
 #define GUARD_BEGIN try {
@@ -42,6 +46,15 @@ using mamg::set_error;
     set_error(std::string("internal error: ") + e.what()); \
     return MAMG_ERR_SETUP;                              \
   }
+
+#define DEV_CALL(call)                    \
+  GUARD_BEGIN                             \
+  if (!h) { set_error("null handle"); return MAMG_ERR_ARG; } \
+  std::string err;                        \
+  int rc = (call);                        \
+  if (rc) set_error(err);                 \
+  return rc;                              \
+  GUARD_END
 
 namespace {
 int to_view(const mamg_csr* A, mamg::CsrView* v) {
@@ -226,6 +239,81 @@ int mamg_plan_level_export(const mamg_plan* p, int l, int64_t* ghosts, int64_t* 
   return MAMG_OK;
 }
 
+int mamg_comm_id_bytes(void) { return 128; }
+
+int mamg_comm_unique_id(void* id) {
+  GUARD_BEGIN
+  if (!id) { set_error("null id buffer"); return MAMG_ERR_ARG; }
+  std::string err;
+  int rc = mamg::dist_get_unique_id(id, &err);
+  if (rc) set_error(err);
+  return rc;
+  GUARD_END
+}
+
+int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, int rank, int nranks, const void* comm_id,
+                    int64_t rep_nodes, mamg_dhandle** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  mamg::Hierarchy H;
+  std::string err;
+  rc = mamg::host_setup(v, idofs, n_idofs, *params, &H, &err);
+  if (rc) { set_error(err); return rc; }
+  mamg::DistHandle* d = nullptr;
+  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err);
+  if (rc) { set_error(err); return rc; }
+  *out = new mamg_dhandle{d};
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_dist_range(const mamg_dhandle* h, int64_t* o0, int64_t* o1, int64_t* nv) {
+  if (!h || !o0 || !o1 || !nv) { set_error("null argument"); return MAMG_ERR_ARG; }
+  mamg::dist_range(h->d, o0, o1, nv);
+  return MAMG_OK;
+}
+
+int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes) {
+  if (!h || !bytes) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *bytes = mamg::dist_apply_bytes(h->d);
+  return MAMG_OK;
+}
+
+int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r, double* d_z, void* stream) {
+  DEV_CALL(mamg::dist_apply(h->d, d_r, d_z, stream, &err))
+}
+
+int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int reps, int mode,
+                         double* ms, double* kernel_ms, double* class_bytes, void* stream) {
+  DEV_CALL(mamg::dist_time_apply(h->d, d_r, d_z, reps, mode, ms, kernel_ms, class_bytes, stream, &err))
+}
+
+int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double** d_z,
+                            void* stream) {
+  GUARD_BEGIN
+  if (!hs || n < 1 || !d_r || !d_z) { set_error("null argument"); return MAMG_ERR_ARG; }
+  std::vector<mamg::DistHandle*> H(n);
+  std::vector<const double*> R(d_r, d_r + n);
+  std::vector<double*> Z(d_z, d_z + n);
+  for (int i = 0; i < n; ++i) H[i] = hs[i]->d;
+  std::string err;
+  int rc = mamg::dist_virtual_apply(H, R, Z, stream, &err);
+  if (rc) set_error(err);
+  return rc;
+  GUARD_END
+}
+
+void mamg_dist_destroy(mamg_dhandle* h) {
+  if (!h) return;
+  mamg::dist_destroy(h->d);
+  delete h;
+}
+
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
@@ -284,15 +372,6 @@ int mamg_apply_bytes(const mamg_handle* h, double* total) {
   *total = mamg::dev_apply_bytes(h->d);
   return MAMG_OK;
 }
-
-#define DEV_CALL(call)                    \
-  GUARD_BEGIN                             \
-  if (!h) { set_error("null handle"); return MAMG_ERR_ARG; } \
-  std::string err;                        \
-  int rc = (call);                        \
-  if (rc) set_error(err);                 \
-  return rc;                              \
-  GUARD_END
 
 int mamg_apply(mamg_handle* h, const double* r, double* z) {
   DEV_CALL(mamg::dev_apply_host(h->d, r, z, &err))

@@ -25,4 +25,18 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
                    double* ms, double* kernel_ms, double* class_bytes, void* stream,
                    std::string* err);
 
+// multi-GPU (device.hip, second half)
+struct DistHandle;
+int dist_get_unique_id(void* id, std::string* err);
+int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
+                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err);
+void dist_destroy(DistHandle* h);
+void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
+double dist_apply_bytes(const DistHandle* h);
+int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
+int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
+                    double* kernel_ms, double* class_bytes, void* stream, std::string* err);
+int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
+                       const std::vector<double*>& z, void* stream, std::string* err);
+
 }  // namespace mamg

@@ -310,6 +310,7 @@ enum Cls {
   C_COARSE = 5,     // all SpMV-class launches on levels >= 1
   C_DENSE = 6,      // coarsest dense solve
   C_MISC = 7,       // W-cycle / maxit corrections
+  C_COMM = 8,       // multi-GPU: halo pack/unpack + RCCL exchanges
   NCLS = 8
 };
 
@@ -967,6 +968,468 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
       }
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
+  return MAMG_OK;
+}
+
+}  // namespace mamg
+
+// ===========================================================================
+// Multi-GPU V-cycle (row-partitioned, RCCL over xGMI).  Plan: dist.cpp.
+// ===========================================================================
+#include <rccl/rccl.h>
+
+#include "dist.h"
+
+namespace mamg {
+namespace {
+
+#define NCCLCHK(expr)                                                                \
+  do {                                                                               \
+    ncclResult_t r_ = (expr);                                                        \
+    if (r_ != ncclSuccess) {                                                         \
+      *err = std::string(#expr) + ": " + ncclGetErrorString(r_);                     \
+      return MAMG_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
+
+__global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const int64_t* __restrict__ idx,
+                                                    const double* __restrict__ x,
+                                                    double* __restrict__ buf) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) {
+    const double2 v = reinterpret_cast<const double2*>(x)[idx[k]];
+    reinterpret_cast<double2*>(buf)[k] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void addidx2_kernel(int64_t n, const int64_t* __restrict__ idx,
+                                                      const double* __restrict__ buf, double* x) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) {
+    double2* px = reinterpret_cast<double2*>(x) + idx[k];
+    const double2 a = *px, v = reinterpret_cast<const double2*>(buf)[k];
+    *px = make_double2(a.x + v.x, a.y + v.y);
+  }
+}
+
+struct DDLevel {
+  int64_t nv = 0, nloc = 0, ng = 0;
+  bool replicated = false, coarsest = false;
+  DBsr A, P, R;
+  dv4* W = nullptr;
+  double* Ainv = nullptr;
+  double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
+  int64_t* send_idx = nullptr;
+  double *sendbuf = nullptr, *recvbuf = nullptr;
+  std::vector<int64_t> send_off, ghost_off;
+};
+
+enum DKind { D_OP = 0, D_HALO = 1, D_REVERSE = 2, D_ALLREDUCE = 3 };
+
+struct DOp {
+  int dk = D_OP;
+  Op op;
+  int level = 0;
+  double* buf = nullptr;
+  int64_t count = 0;
+  double bytes = 0.0;
+  int cls = 0;
+};
+
+}  // namespace
+
+struct DistHandle {
+  mamg_params p;
+  int rank = 0, nranks = 1, device = 0;
+  ncclComm_t comm = nullptr;
+  std::vector<DDLevel> L;
+  std::vector<void*> allocs;
+  double apply_bytes = 0.0;
+  int64_t nv0 = 0, o0 = 0, o1 = 0;
+  ~DistHandle() {
+    for (void* a : allocs) (void)hipFree(a);
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+};
+
+namespace {
+
+template <class T>
+int ddalloc(DistHandle* h, T** p, int64_t count, std::string* err) {
+  *p = nullptr;
+  if (count <= 0) return MAMG_OK;
+  void* q = nullptr;
+  HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
+  HIPCHK(hipMemset(q, 0, (size_t)count * sizeof(T)));
+  h->allocs.push_back(q);
+  *p = (T*)q;
+  return MAMG_OK;
+}
+
+int dupload_bsr(DistHandle* h, const HBsr& B, DBsr* D, std::string* err) {
+  D->nr = B.nr;
+  D->nc = B.nc;
+  D->nb = B.ptr.empty() ? 0 : B.ptr[B.nr];
+  D->lanes = pick_lanes_bsr(B.nr, D->nb);
+  int rc;
+  if ((rc = ddalloc(h, &D->ptr, B.nr + 1, err))) return rc;
+  if ((rc = ddalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
+  if ((rc = ddalloc(h, &D->val, std::max<int64_t>(D->nb, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), (B.nr + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (D->nb) {
+    HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+
+DOp wrap(const Op& o) {
+  DOp d;
+  d.dk = D_OP; d.op = o; d.bytes = o.bytes; d.cls = o.cls;
+  return d;
+}
+
+DOp halo_op(int level, double* x, const DDLevel& D, int cls) {
+  DOp d;
+  d.dk = D_HALO; d.level = level; d.buf = x; d.cls = cls;
+  const int64_t ns = D.send_off.empty() ? 0 : D.send_off.back();
+  d.bytes = 8.0 * ns + 16.0 * ns * 2 + 16.0 * D.ng;   // idx, pack r/w, ghost writes
+  return d;
+}
+
+// multi-GPU cycle from x = 0 (V-cycle, nu1 = nu2 = 1): see dist.cpp / dist_ref.py
+void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
+                std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[l];
+  const bool l0 = l == 0;
+  const int tagA = l0 ? 0 : 1;
+  if (D.coarsest) {
+    Op o;
+    o.kind = OP_GEMV; o.cls = C_DENSE; o.n = 2 * D.nv; o.x = b; o.w = D.Ainv; o.out = xout;
+    o.bytes = 8.0 * o.n * o.n + 16.0 * o.n;
+    ops->push_back(wrap(o));
+    return;
+  }
+  const DDLevel& C = h->L[l + 1];
+  double* X = D.t;
+  {
+    Op o;
+    o.kind = OP_BD; o.cls = l0 ? C_L0_WB : C_COARSE; o.n = D.nloc; o.W = D.W; o.b = b; o.bs = bs;
+    o.out = X; o.bytes = 64.0 * D.nloc;
+    ops->push_back(wrap(o));
+  }
+  if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
+  ops->push_back(wrap(bsr_op(D.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs,
+                             nullptr, D.r, 0)));
+  ops->push_back(wrap(bsr_op(D.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, D.r, 0, nullptr, nullptr, 0,
+                             nullptr, C.b, 0)));
+  if (!D.replicated) {
+    DOp d;
+    d.cls = C_COMM;
+    if (C.replicated) {
+      d.dk = D_ALLREDUCE; d.buf = C.b; d.count = 2 * C.nv; d.bytes = 16.0 * C.nv * 2;
+    } else {
+      d.dk = D_REVERSE; d.level = l + 1; d.buf = C.b;
+      const int64_t ns = C.send_off.back();
+      d.bytes = 16.0 * C.ng + 16.0 * ns * 3 + 8.0 * ns;
+    }
+    ops->push_back(d);
+  }
+  dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
+  if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
+                             nullptr, X, 0)));
+  if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
+  ops->push_back(wrap(bsr_op(D.A, EPI_BJAC, l0 ? C_L0_SMOOTH : C_COARSE, tagA, X, 0, X, b, bs, D.W,
+                             xout, os)));
+}
+
+int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
+  if (d.dk == D_OP) {
+    launch(d.op, s);
+    return MAMG_OK;
+  }
+  if (d.dk == D_ALLREDUCE) {
+    NCCLCHK(ncclAllReduce(d.buf, d.buf, d.count, ncclDouble, ncclSum, h->comm, s));
+    return MAMG_OK;
+  }
+  const DDLevel& D = h->L[d.level];
+  const int64_t ns = D.send_off.back();
+  if (d.dk == D_HALO) {
+    if (ns) pack2_kernel<<<nblocks(ns), 256, 0, s>>>(ns, D.send_idx, d.buf, D.sendbuf);
+    NCCLCHK(ncclGroupStart());
+    for (int q = 0; q < h->nranks; ++q) {
+      if (q == h->rank) continue;
+      const int64_t sc = D.send_off[q + 1] - D.send_off[q];
+      const int64_t gc = D.ghost_off[q + 1] - D.ghost_off[q];
+      if (sc) NCCLCHK(ncclSend(D.sendbuf + 2 * D.send_off[q], 2 * sc, ncclDouble, q, h->comm, s));
+      if (gc) NCCLCHK(ncclRecv(d.buf + 2 * (D.nloc + D.ghost_off[q]), 2 * gc, ncclDouble, q, h->comm, s));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return MAMG_OK;
+  }
+  // D_REVERSE: ghost partials -> owners; owners add in rank order
+  NCCLCHK(ncclGroupStart());
+  for (int q = 0; q < h->nranks; ++q) {
+    if (q == h->rank) continue;
+    const int64_t sc = D.send_off[q + 1] - D.send_off[q];
+    const int64_t gc = D.ghost_off[q + 1] - D.ghost_off[q];
+    if (gc) NCCLCHK(ncclSend(d.buf + 2 * (D.nloc + D.ghost_off[q]), 2 * gc, ncclDouble, q, h->comm, s));
+    if (sc) NCCLCHK(ncclRecv(D.recvbuf + 2 * D.send_off[q], 2 * sc, ncclDouble, q, h->comm, s));
+  }
+  NCCLCHK(ncclGroupEnd());
+  for (int q = 0; q < h->nranks; ++q) {
+    const int64_t sc = D.send_off[q + 1] - D.send_off[q];
+    if (q == h->rank || !sc) continue;
+    addidx2_kernel<<<nblocks(sc), 256, 0, s>>>(sc, D.send_idx + D.send_off[q],
+                                               D.recvbuf + 2 * D.send_off[q], d.buf);
+  }
+  return MAMG_OK;
+}
+
+void dapply_ops(const DistHandle* h, const double* r, double* z, std::vector<DOp>* ops) {
+  ops->clear();
+  const int64_t nloc = h->L[0].nloc;
+  dcycle_ops(h, 0, r, nloc, z, nloc, ops);
+}
+
+}  // namespace
+
+int dist_get_unique_id(void* id, std::string* err) {
+  ncclUniqueId u;
+  NCCLCHK(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return MAMG_OK;
+}
+
+int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
+                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err) {
+  if (p.cycle_type != MAMG_V_CYCLE || p.maxit != 1 || p.presmooth_iter != 1 || p.postsmooth_iter != 1) {
+    *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  DistPlan plan;
+  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, &plan, err);
+  if (rc) return rc;
+  std::unique_ptr<DistHandle> h(new DistHandle());
+  h->p = p;
+  h->rank = rank;
+  h->nranks = nranks;
+  h->device = p.device;
+  HIPCHK(hipSetDevice(p.device));
+  if (comm_id) {                         // RCCL communicator; NULL = virtual (tests)
+    ncclUniqueId uid;
+    std::memcpy(&uid, comm_id, sizeof(uid));
+    NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
+  }
+  const int nl = (int)plan.levels.size();
+  h->L.resize(nl);
+  for (int l = 0; l < nl; ++l) {
+    DistLevel& P = plan.levels[l];
+    DDLevel& D = h->L[l];
+    D.nv = P.nv;
+    D.nloc = P.nloc;
+    D.ng = (int64_t)P.ghosts.size();
+    D.replicated = P.replicated;
+    D.coarsest = P.coarsest;
+    D.send_off = P.send_off;
+    D.ghost_off = P.ghost_off;
+    if (D.coarsest) {
+      const HostLevel& hl = H.levels[l];
+      const int64_t n = hl.n, nv = n / 2;
+      std::vector<double> Ap(n * n);
+      auto pos = [nv](int64_t i) { return 2 * (i % nv) + i / nv; };
+      for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < n; ++j) Ap[pos(i) * n + pos(j)] = hl.Ainv[i * n + j];
+      if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
+      HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+      if ((rc = dupload_bsr(h.get(), P.A, &D.A, err))) return rc;
+      if ((rc = dupload_bsr(h.get(), P.P, &D.P, err))) return rc;
+      if ((rc = dupload_bsr(h.get(), P.Rp, &D.R, err))) return rc;
+      if ((rc = ddalloc(h.get(), &D.W, D.nloc, err))) return rc;
+      HIPCHK(hipMemcpy(D.W, P.W.data(), 4 * D.nloc * sizeof(double), hipMemcpyHostToDevice));
+    }
+    const int64_t full = D.nloc + D.ng;
+    if ((rc = ddalloc(h.get(), &D.b, 2 * full, err))) return rc;
+    if ((rc = ddalloc(h.get(), &D.x, 2 * full, err))) return rc;
+    if ((rc = ddalloc(h.get(), &D.t, 2 * full, err))) return rc;
+    if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
+    const int64_t ns = P.send_idx.size();
+    if (ns) {
+      if ((rc = ddalloc(h.get(), &D.send_idx, ns, err))) return rc;
+      HIPCHK(hipMemcpy(D.send_idx, P.send_idx.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice));
+      if ((rc = ddalloc(h.get(), &D.sendbuf, 2 * ns, err))) return rc;
+      if ((rc = ddalloc(h.get(), &D.recvbuf, 2 * ns, err))) return rc;
+    }
+  }
+  h->nv0 = plan.levels[0].nv;
+  h->o0 = plan.levels[0].o0;
+  h->o1 = plan.levels[0].o1;
+  std::vector<DOp> ops;
+  dapply_ops(h.get(), nullptr, nullptr, &ops);
+  for (const DOp& d : ops) h->apply_bytes += d.bytes;
+  HIPCHK(hipDeviceSynchronize());
+  *out = h.release();
+  return MAMG_OK;
+}
+
+void dist_destroy(DistHandle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  delete h;
+}
+
+void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv) {
+  *o0 = h->o0; *o1 = h->o1; *nv = h->nv0;
+}
+
+double dist_apply_bytes(const DistHandle* h) { return h->apply_bytes; }
+
+int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<DOp> ops;
+  dapply_ops(h, d_r, d_z, &ops);
+  for (const DOp& d : ops) {
+    int rc = run_dop(h, d, (hipStream_t)stream, err);
+    if (rc) return rc;
+  }
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
+                    double* kernel_ms, double* class_bytes, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<DOp> ops;
+  dapply_ops(h, d_r, d_z, &ops);
+  if (class_bytes) {
+    for (int c = 0; c < 16; ++c) class_bytes[c] = 0.0;
+    for (const DOp& d : ops) class_bytes[d.cls] += d.bytes;
+  }
+  if (reps <= 0) { *ms = 0.0; return MAMG_OK; }
+  std::vector<int> inst;
+  for (size_t k = 0; k < ops.size(); ++k)
+    if (mode == 1 || ops[k].cls == C_L0_RESID) inst.push_back((int)k);
+  std::vector<hipEvent_t> ev(2 * inst.size() * (size_t)reps + 2);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(ev[0], s));
+  size_t q = 2;
+  int rc;
+  for (int rp = 0; rp < reps; ++rp) {
+    size_t ii = 0;
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const bool timed = ii < inst.size() && inst[ii] == (int)k;
+      if (timed) HIPCHK(hipEventRecord(ev[q], s));
+      if ((rc = run_dop(h, ops[k], s, err))) return rc;
+      if (timed) { HIPCHK(hipEventRecord(ev[q + 1], s)); q += 2; ++ii; }
+    }
+  }
+  HIPCHK(hipEventRecord(ev[1], s));
+  HIPCHK(hipEventSynchronize(ev[1]));
+  HIPCHK(hipGetLastError());
+  float tot = 0.f;
+  HIPCHK(hipEventElapsedTime(&tot, ev[0], ev[1]));
+  *ms = tot / reps;
+  if (kernel_ms) {
+    for (int c = 0; c < 16; ++c) kernel_ms[c] = 0.0;
+    q = 2;
+    for (int rp = 0; rp < reps; ++rp)
+      for (size_t ii = 0; ii < inst.size(); ++ii) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, ev[q], ev[q + 1]));
+        kernel_ms[ops[inst[ii]].cls] += t / reps;
+        q += 2;
+      }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return MAMG_OK;
+}
+
+}  // namespace mamg
+
+// ---------------------------------------------------------------------------
+// Virtual communicator (tests on a single GPU): P rank handles on one device,
+// executed in lockstep on one stream; exchanges are device copies between the
+// ranks' buffers with exactly the counts/offsets the RCCL path uses.
+// ---------------------------------------------------------------------------
+namespace mamg {
+
+__global__ __launch_bounds__(256) void vsum_kernel(int64_t n, const double* __restrict__ a,
+                                                   double* acc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) acc[i] = acc[i] + a[i];
+}
+
+int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
+                       const std::vector<double*>& z, void* stream, std::string* err) {
+  const int P = (int)hs.size();
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(hs[0]->device));
+  std::vector<std::vector<DOp>> ops(P);
+  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
+  for (int p = 1; p < P; ++p)
+    if (ops[p].size() != ops[0].size()) { *err = "rank schedules differ"; return MAMG_ERR_SETUP; }
+  for (size_t k = 0; k < ops[0].size(); ++k) {
+    const int dk = ops[0][k].dk;
+    if (dk == D_OP) {
+      for (int p = 0; p < P; ++p) launch(ops[p][k].op, s);
+    } else if (dk == D_HALO) {
+      for (int p = 0; p < P; ++p) {
+        const DDLevel& D = hs[p]->L[ops[p][k].level];
+        const int64_t ns = D.send_off.back();
+        if (ns) pack2_kernel<<<nblocks(ns), 256, 0, s>>>(ns, D.send_idx, ops[p][k].buf, D.sendbuf);
+      }
+      for (int p = 0; p < P; ++p) {          // p receives from q
+        const DDLevel& D = hs[p]->L[ops[p][k].level];
+        for (int q = 0; q < P; ++q) {
+          if (q == p) continue;
+          const int64_t gc = D.ghost_off[q + 1] - D.ghost_off[q];
+          if (!gc) continue;
+          const DDLevel& Q = hs[q]->L[ops[q][k].level];
+          const int64_t sc = Q.send_off[p + 1] - Q.send_off[p];
+          if (sc != gc) { *err = "halo count mismatch"; return MAMG_ERR_SETUP; }
+          HIPCHK(hipMemcpyAsync(ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]),
+                                Q.sendbuf + 2 * Q.send_off[p], 2 * gc * sizeof(double),
+                                hipMemcpyDeviceToDevice, s));
+        }
+      }
+    } else if (dk == D_REVERSE) {
+      for (int q = 0; q < P; ++q) {          // owner q receives partials from p
+        const DDLevel& Q = hs[q]->L[ops[q][k].level];
+        for (int p = 0; p < P; ++p) {
+          if (p == q) continue;
+          const int64_t sc = Q.send_off[p + 1] - Q.send_off[p];
+          if (!sc) continue;
+          const DDLevel& D = hs[p]->L[ops[p][k].level];
+          const int64_t gc = D.ghost_off[q + 1] - D.ghost_off[q];
+          if (sc != gc) { *err = "reverse count mismatch"; return MAMG_ERR_SETUP; }
+          HIPCHK(hipMemcpyAsync(Q.recvbuf + 2 * Q.send_off[p],
+                                ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]),
+                                2 * sc * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+      }
+      for (int q = 0; q < P; ++q) {
+        const DDLevel& Q = hs[q]->L[ops[q][k].level];
+        for (int p = 0; p < P; ++p) {
+          const int64_t sc = Q.send_off[p + 1] - Q.send_off[p];
+          if (p == q || !sc) continue;
+          addidx2_kernel<<<nblocks(sc), 256, 0, s>>>(sc, Q.send_idx + Q.send_off[p],
+                                                     Q.recvbuf + 2 * Q.send_off[p], ops[q][k].buf);
+        }
+      }
+    } else {                                 // D_ALLREDUCE: sum in rank order
+      const int64_t n = ops[0][k].count;
+      for (int p = 1; p < P; ++p)
+        vsum_kernel<<<nblocks(n), 256, 0, s>>>(n, ops[p][k].buf, ops[0][k].buf);
+      for (int p = 1; p < P; ++p)
+        HIPCHK(hipMemcpyAsync(ops[p][k].buf, ops[0][k].buf, n * sizeof(double),
+                              hipMemcpyDeviceToDevice, s));
+    }
+  }
+  HIPCHK(hipGetLastError());
   return MAMG_OK;
 }
 
