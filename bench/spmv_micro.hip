@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mamg.h"
@@ -143,6 +144,20 @@ __global__ __launch_bounds__(256) void bsr_soa_k(int64_t nv, const int64_t* __re
   if (node < nv && lane == 0) y2[node] = make_double2(s0, s1);
 }
 
+// FETCH_SIZE calibration: stream-read n elements of width W bytes per lane
+// (exactly n*W bytes), write one value per block
+template <class T>
+__global__ __launch_bounds__(256) void calib_read_k(int64_t n, const T* __restrict__ a,
+                                                    double* __restrict__ out) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const T v = a[i];
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(T) / 4); ++w) s += (double)reinterpret_cast<const int*>(&v)[w];
+  }
+  if (s == 1234.5) out[blockIdx.x] = s;   // practically never: keeps the loads live
+}
+
 // plain copy for the achievable-bandwidth reference
 __global__ __launch_bounds__(256) void copy_k(int64_t n4, const double4* __restrict__ a,
                                               double4* __restrict__ b) {
@@ -166,7 +181,28 @@ float timeit(F f, int reps) {
   return ms / reps;
 }
 
+int calib(int reps) {
+  // 2 GiB buffer, far above the 256 MiB MALL: every byte comes from HBM
+  const int64_t bytes = (int64_t)2 << 30;
+  char* a;
+  double* out;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&out, 1 << 20));
+  CK(hipMemset(a, 1, bytes));
+  printf("calibration: each kernel reads exactly %ld bytes (compare FETCH_SIZE*1024)\n", (long)bytes);
+#define CAL(T, name)                                                                       \
+  {                                                                                        \
+    const int64_t n = bytes / (int64_t)sizeof(T);                                          \
+    float ms = timeit([&] { hipLaunchKernelGGL(calib_read_k<T>, dim3(256 * 16), dim3(256), 0, 0, n, (const T*)a, out); }, reps); \
+    printf("calib %-8s (%2d B/lane): %.3f ms %.0f GB/s\n", name, (int)sizeof(T), ms, bytes / ms / 1e6); \
+  }
+  CAL(int, "int32") CAL(double, "f64") CAL(double2, "f64x2") CAL(dv4, "f64x4")
+  CK(hipFree(a));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "calib") return calib(argc > 2 ? atoi(argv[2]) : 3);
   const int n = argc > 1 ? atoi(argv[1]) : 256;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;
   int64_t N, nnz;

@@ -8,36 +8,37 @@
 
 namespace mamg {
 
-// ---- host conversion: field-major CSR (rows f*nr+I, cols g*nc+J) -> BSR2 ---
-
-void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) {
-  B->nr = nr;
+// ---- field-major CSR (rows f*nr+I, cols g*nc+J, 2 fields) -> 2x2 BSR -------
+// node rows [r0, r1); block row I-r0 holds the distinct node columns J of the
+// two rows f*nr+I (sorted), values (0,0) (0,1) (1,0) (1,1), absent = 0.
+void to_bsr2_rows(const CsrView& M, int64_t nr, int64_t nc, int64_t r0, int64_t r1, HBsr* B) {
+  const int64_t n = r1 - r0;
+  B->nr = n;
   B->nc = nc;
-  B->ptr.assign(nr + 1, 0);
-  // pass 1: number of distinct node columns per node row
+  B->ptr.assign(n + 1, 0);
 #pragma omp parallel
   {
     std::vector<int32_t> js;
 #pragma omp for schedule(dynamic, 4096)
-    for (int64_t I = 0; I < nr; ++I) {
+    for (int64_t I = r0; I < r1; ++I) {
       js.clear();
       for (int f = 0; f < 2; ++f) {
         const int64_t r = f * nr + I;
         for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) js.push_back((int32_t)(M.col[k] % nc));
       }
       std::sort(js.begin(), js.end());
-      B->ptr[I + 1] = (int64_t)(std::unique(js.begin(), js.end()) - js.begin());
+      B->ptr[I - r0 + 1] = (int64_t)(std::unique(js.begin(), js.end()) - js.begin());
     }
   }
-  for (int64_t I = 0; I < nr; ++I) B->ptr[I + 1] += B->ptr[I];
-  const int64_t nb = B->ptr[nr];
+  for (int64_t i = 0; i < n; ++i) B->ptr[i + 1] += B->ptr[i];
+  const int64_t nb = B->ptr[n];
   B->col.resize(nb);
   B->val.assign(4 * nb, 0.0);
 #pragma omp parallel
   {
     std::vector<int32_t> js;
 #pragma omp for schedule(dynamic, 4096)
-    for (int64_t I = 0; I < nr; ++I) {
+    for (int64_t I = r0; I < r1; ++I) {
       js.clear();
       for (int f = 0; f < 2; ++f) {
         const int64_t r = f * nr + I;
@@ -45,7 +46,7 @@ void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) {
       }
       std::sort(js.begin(), js.end());
       js.erase(std::unique(js.begin(), js.end()), js.end());
-      const int64_t o = B->ptr[I];
+      const int64_t o = B->ptr[I - r0];
       for (size_t t = 0; t < js.size(); ++t) B->col[o + t] = js[t];
       for (int f = 0; f < 2; ++f) {
         const int64_t r = f * nr + I;
@@ -59,6 +60,8 @@ void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) {
     }
   }
 }
+
+void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) { to_bsr2_rows(M, nr, nc, 0, nr, B); }
 
 // W_B (or node-block smoother) -> one 2x2 block per node; false if some entry
 // couples different nodes (then the BSR2 layout cannot fuse the smoother)

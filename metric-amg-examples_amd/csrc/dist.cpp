@@ -6,7 +6,7 @@
 // structured mesh; coarse aggregates are numbered by root index, so their
 // ranges are slab-like too).  A level is *replicated* (computed redundantly on
 // every rank, no exchange) once it has <= rep_nodes nodes, and so are all
-// coarser levels.
+// coarser levels; the coarsest (dense solve) always is.
 //
 // Rank-local data of a distributed level l (node-interleaved vectors
 // [owned | ghost], ghosts sorted by global id, hence grouped by owner rank):
@@ -19,6 +19,8 @@
 //           rank order (deterministic).
 //   ghosts(l) = external columns of A_loc  U  external columns of P_{l-1} loc
 //   send list to q = the owned nodes that are ghosts of q, in q's order.
+// Only owned rows are converted to blocks (no global copy of A_0 per rank);
+// ghost sets of all ranks come straight from the field-major CSR.
 #include <omp.h>
 
 #include <algorithm>
@@ -29,19 +31,21 @@
 namespace mamg {
 namespace {
 
-// owner rank of global node J under the equal-size split
 inline int owner_of(const std::vector<int64_t>& own, int64_t J) {
   return (int)(std::upper_bound(own.begin(), own.end(), J) - own.begin()) - 1;
 }
 
-// external (non-owned) node columns touched by rows [r0, r1) of B
-void external_cols(const HBsr& B, int64_t r0, int64_t r1, int64_t o0, int64_t o1,
-                   std::vector<int64_t>* out) {
+// node columns (mod nc) of field-major CSR rows f*nr+I, I in [r0,r1), outside [o0,o1)
+void external_node_cols(const CsrView& M, int64_t nr, int64_t nc, int64_t r0, int64_t r1,
+                        int64_t o0, int64_t o1, std::vector<int64_t>* out) {
   std::vector<int64_t> v;
-  for (int64_t I = r0; I < r1; ++I)
-    for (int64_t k = B.ptr[I]; k < B.ptr[I + 1]; ++k) {
-      const int64_t J = B.col[k];
-      if (J < o0 || J >= o1) v.push_back(J);
+  for (int f = 0; f < 2; ++f)
+    for (int64_t I = r0; I < r1; ++I) {
+      const int64_t r = f * nr + I;
+      for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
+        const int64_t J = M.col[k] % nc;
+        if (J < o0 || J >= o1) v.push_back(J);
+      }
     }
   std::sort(v.begin(), v.end());
   v.erase(std::unique(v.begin(), v.end()), v.end());
@@ -53,27 +57,22 @@ void sort_unique(std::vector<int64_t>* v) {
   v->erase(std::unique(v->begin(), v->end()), v->end());
 }
 
-// slice rows [r0, r1) of B and remap columns with map(J) -> local index
+// remap the columns of a (row-local) block matrix in place, keeping each
+// row's blocks sorted by local column
 template <class F>
-void slice_remap(const HBsr& B, int64_t r0, int64_t r1, int64_t nc_local, F map, HBsr* out) {
-  out->nr = r1 - r0;
-  out->nc = nc_local;
-  out->ptr.assign(out->nr + 1, 0);
-  for (int64_t I = r0; I < r1; ++I) out->ptr[I - r0 + 1] = out->ptr[I - r0] + (B.ptr[I + 1] - B.ptr[I]);
-  const int64_t nb = out->ptr[out->nr];
-  out->col.resize(nb);
-  out->val.resize(4 * nb);
-  for (int64_t I = r0; I < r1; ++I) {
-    // local column order may differ from global order (ghosts after owned):
-    // keep the block order sorted by local column for coalesced-ish gathers
-    std::vector<std::pair<int32_t, int64_t>> e;
-    for (int64_t k = B.ptr[I]; k < B.ptr[I + 1]; ++k) e.emplace_back((int32_t)map(B.col[k]), k);
+void remap_cols(HBsr* B, int64_t nc_local, F map) {
+  B->nc = nc_local;
+  std::vector<std::pair<int32_t, int64_t>> e;
+  std::vector<double> v;
+  for (int64_t I = 0; I < B->nr; ++I) {
+    const int64_t p0 = B->ptr[I], p1 = B->ptr[I + 1];
+    e.clear();
+    for (int64_t k = p0; k < p1; ++k) e.emplace_back((int32_t)map(B->col[k]), k);
     std::sort(e.begin(), e.end());
-    int64_t o = out->ptr[I - r0];
-    for (auto& pr : e) {
-      out->col[o] = pr.first;
-      for (int q = 0; q < 4; ++q) out->val[4 * o + q] = B.val[4 * pr.second + q];
-      ++o;
+    v.assign(B->val.begin() + 4 * p0, B->val.begin() + 4 * p1);
+    for (int64_t t = 0; t < p1 - p0; ++t) {
+      B->col[p0 + t] = e[t].first;
+      for (int q = 0; q < 4; ++q) B->val[4 * (p0 + t) + q] = v[4 * (e[t].second - p0) + q];
     }
   }
 }
@@ -108,40 +107,28 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
   const int nl = (int)H.levels.size();
+  if (nl < 2) { *err = "multi-GPU path needs at least two levels"; return MAMG_ERR_UNSUPPORTED; }
   plan->rank = rank;
   plan->nranks = nranks;
   plan->levels.assign(nl, DistLevel());
-  // global BSR2 matrices per level
-  std::vector<HBsr> A(nl), P(nl);
-  std::vector<std::vector<double>> W(nl);
-  for (int l = 0; l < nl; ++l) {
-    const HostLevel& hl = H.levels[l];
-    const int64_t nv = hl.n / 2;
-    DistLevel& D = plan->levels[l];
-    D.nv = nv;
-    D.coarsest = hl.coarsest;
-    to_bsr2(l == 0 ? A0 : H.A(l), nv, nv, &A[l]);
-    if (!hl.coarsest) {
-      const int64_t nvc = H.levels[l + 1].n / 2;
-      to_bsr2(hl.P.view(), nv, nvc, &P[l]);
-      if (hl.WB.n == 0 || !node_blocks_of(hl.WB.view(), nv, &W[l])) {
-        *err = "multi-GPU path needs node-block smoothers on every level";
-        return MAMG_ERR_UNSUPPORTED;
-      }
-    }
-  }
-  if (nl < 2) { *err = "multi-GPU path needs at least two levels"; return MAMG_ERR_UNSUPPORTED; }
-  // replication: from the first small level down; the coarsest is always
-  // replicated (dense solve); level 0 never is
+  auto Aview = [&](int l) { return l == 0 ? A0 : H.A(l); };
+  // replication: from the first small level down; coarsest always; level 0 never
   bool rep = false;
   for (int l = 0; l < nl; ++l) {
+    const HostLevel& hl = H.levels[l];
     DistLevel& D = plan->levels[l];
+    D.nv = hl.n / 2;
+    D.coarsest = hl.coarsest;
     if (l > 0 && (D.nv <= rep_nodes || D.coarsest)) rep = true;
     D.replicated = rep;
     D.own.resize(nranks + 1);
     for (int q = 0; q <= nranks; ++q) D.own[q] = rep ? (q == 0 ? 0 : D.nv) : (D.nv * q) / nranks;
+    if (!hl.coarsest && hl.WB.n == 0) {
+      *err = "multi-GPU path needs node-block smoothers on every level";
+      return MAMG_ERR_UNSUPPORTED;
+    }
   }
-  // ghost lists of every rank (needed for send lists)
+  // ghost lists of every rank on distributed levels (send lists need them)
   std::vector<std::vector<std::vector<int64_t>>> ghosts(nl, std::vector<std::vector<int64_t>>(nranks));
 #pragma omp parallel for collapse(2) schedule(dynamic, 1)
   for (int l = 0; l < nl; ++l)
@@ -150,20 +137,26 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       if (D.replicated) continue;
       const int64_t o0 = D.own[q], o1 = D.own[q + 1];
       std::vector<int64_t> g;
-      external_cols(A[l], o0, o1, o0, o1, &g);
+      external_node_cols(Aview(l), D.nv, D.nv, o0, o1, o0, o1, &g);
       if (l > 0) {
         const DistLevel& F = plan->levels[l - 1];
-        external_cols(P[l - 1], F.own[q], F.own[q + 1], o0, o1, &g);
+        external_node_cols(H.levels[l - 1].P.view(), F.nv, D.nv, F.own[q], F.own[q + 1], o0, o1, &g);
       }
       sort_unique(&g);
       ghosts[l][q] = std::move(g);
     }
   for (int l = 0; l < nl; ++l) {
     DistLevel& D = plan->levels[l];
+    const HostLevel& hl = H.levels[l];
+    std::vector<double> Wfull;
+    if (!hl.coarsest && !node_blocks_of(hl.WB.view(), D.nv, &Wfull)) {
+      *err = "multi-GPU path needs node-block smoothers on every level";
+      return MAMG_ERR_UNSUPPORTED;
+    }
     if (D.replicated) {
       D.o0 = 0; D.o1 = D.nv; D.nloc = D.nv;
-      D.A = std::move(A[l]);
-      D.W = W[l];
+      to_bsr2(Aview(l), D.nv, D.nv, &D.A);
+      D.W = std::move(Wfull);
       D.ghost_off.assign(nranks + 1, 0);
       D.send_off.assign(nranks + 1, 0);
       continue;
@@ -172,52 +165,48 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
     D.o1 = D.own[rank + 1];
     D.nloc = D.o1 - D.o0;
     D.ghosts = ghosts[l][rank];
-    // ghost groups per owner rank
     D.ghost_off.assign(nranks + 1, 0);
     for (int64_t g : D.ghosts) D.ghost_off[owner_of(D.own, g) + 1]++;
     for (int q = 0; q < nranks; ++q) D.ghost_off[q + 1] += D.ghost_off[q];
-    // send lists: my owned nodes that are ghosts of q, in q's ghost order
     D.send_off.assign(nranks + 1, 0);
     D.send_idx.clear();
     for (int q = 0; q < nranks; ++q) {
-      if (q != rank) {
+      if (q != rank)
         for (int64_t g : ghosts[l][q])
           if (g >= D.o0 && g < D.o1) D.send_idx.push_back(g - D.o0);
-      }
       D.send_off[q + 1] = (int64_t)D.send_idx.size();
     }
-    // local A
     const int64_t o0 = D.o0, o1 = D.o1, nloc = D.nloc;
     const std::vector<int64_t>& gl = D.ghosts;
-    auto mapA = [&](int64_t J) -> int64_t {
+    to_bsr2_rows(Aview(l), D.nv, D.nv, o0, o1, &D.A);
+    remap_cols(&D.A, nloc + (int64_t)gl.size(), [&](int64_t J) -> int64_t {
       if (J >= o0 && J < o1) return J - o0;
       return nloc + (std::lower_bound(gl.begin(), gl.end(), J) - gl.begin());
-    };
-    slice_remap(A[l], o0, o1, nloc + (int64_t)gl.size(), mapA, &D.A);
-    D.W.assign(W[l].begin() + 4 * o0, W[l].begin() + 4 * o1);
+    });
+    D.W.assign(Wfull.begin() + 4 * o0, Wfull.begin() + 4 * o1);
   }
-  // P_loc / Rp_loc (need level l+1 numbering)
+  // P_loc / Rp_loc (need the level l+1 numbering)
   for (int l = 0; l + 1 < nl; ++l) {
     DistLevel& D = plan->levels[l];
+    const DistLevel& C = plan->levels[l + 1];
+    const CsrView Pv = H.levels[l].P.view();
     if (D.replicated) {
-      D.P = std::move(P[l]);
+      to_bsr2(Pv, D.nv, C.nv, &D.P);
       transpose_bsr(D.P, &D.Rp);
       continue;
     }
-    const DistLevel& C = plan->levels[l + 1];
     const int64_t c0 = C.o0, c1 = C.o1, cnloc = C.nloc;
     const std::vector<int64_t>& cg = C.ghosts;
     const bool crep = C.replicated;
-    auto mapC = [&](int64_t J) -> int64_t {
+    to_bsr2_rows(Pv, D.nv, C.nv, D.o0, D.o1, &D.P);
+    const int64_t ncl = crep ? C.nv : cnloc + (int64_t)cg.size();
+    remap_cols(&D.P, ncl, [&](int64_t J) -> int64_t {
       if (crep) return J;
       if (J >= c0 && J < c1) return J - c0;
       return cnloc + (std::lower_bound(cg.begin(), cg.end(), J) - cg.begin());
-    };
-    const int64_t ncl = crep ? C.nv : cnloc + (int64_t)cg.size();
-    slice_remap(P[l], D.o0, D.o1, ncl, mapC, &D.P);
+    });
     transpose_bsr(D.P, &D.Rp);
   }
-  (void)err;
   return MAMG_OK;
 }
 

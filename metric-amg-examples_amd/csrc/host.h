@@ -72,6 +72,8 @@ struct HBsr {
   std::vector<double> val;   // 4 per block: (0,0) (0,1) (1,0) (1,1)
 };
 void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B);
+// node rows [r0, r1) only (B.nr = r1 - r0)
+void to_bsr2_rows(const CsrView& M, int64_t nr, int64_t nc, int64_t r0, int64_t r1, HBsr* B);
 // smoother matrix -> one 2x2 block per node; false if it couples two nodes
 bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk);
 
