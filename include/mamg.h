@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MAMG_ABI_VERSION 1
+#define MAMG_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 enum {
@@ -99,6 +99,10 @@ typedef struct mamg_params {
   int32_t num_functions;     /* 1                                            */
   int32_t node_block_smoother; /* nodal: node-block Jacobi where no seed blocks (1) */
   int32_t sa_block_diag;     /* nodal: smooth P with node-block D^-1 (1)     */
+  /* BSR2 device path: fold prolongation into the first post-smoothing sweep,
+   * x = x1 + P e + W (r1 - (A P) e), with A P kept from the Galerkin product
+   * (one pass over [P | AP] instead of P then A).  1 */
+  int32_t post_fusion;
 } mamg_params;
 
 /* Host CSR view (caller-owned). */

@@ -116,6 +116,7 @@ void mamg_params_default(mamg_params* p) {
   p->num_functions = 1;
   p->node_block_smoother = 1;
   p->sa_block_diag = 1;
+  p->post_fusion = 1;
 }
 
 int mamg_gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz) {

@@ -63,6 +63,29 @@ void to_bsr2_rows(const CsrView& M, int64_t nr, int64_t nc, int64_t r0, int64_t 
 
 void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B) { to_bsr2_rows(M, nr, nc, 0, nr, B); }
 
+void merge_bsr_rows(const HBsr& P, const HBsr& Q, HBsr* M) {
+  const int64_t nr = P.nr;
+  M->nr = nr;
+  M->nc = P.nc;
+  M->ptr.assign(2 * nr + 1, 0);
+  for (int64_t I = 0; I < nr; ++I) {
+    M->ptr[2 * I + 1] = M->ptr[2 * I] + (P.ptr[I + 1] - P.ptr[I]);
+    M->ptr[2 * I + 2] = M->ptr[2 * I + 1] + (Q.ptr[I + 1] - Q.ptr[I]);
+  }
+  const int64_t nb = M->ptr[2 * nr];
+  M->col.resize(nb);
+  M->val.resize(4 * nb);
+#pragma omp parallel for schedule(static)
+  for (int64_t I = 0; I < nr; ++I) {
+    int64_t d = M->ptr[2 * I];
+    for (const HBsr* S : {&P, &Q})
+      for (int64_t k = S->ptr[I]; k < S->ptr[I + 1]; ++k, ++d) {
+        M->col[d] = S->col[k];
+        for (int q = 0; q < 4; ++q) M->val[4 * d + q] = S->val[4 * k + q];
+      }
+  }
+}
+
 // W_B (or node-block smoother) -> one 2x2 block per node; false if some entry
 // couples different nodes (then the BSR2 layout cannot fuse the smoother)
 bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk) {

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -99,14 +100,25 @@ __device__ __forceinline__ void vset(double* v, int64_t stride, int64_t I, int f
   if (stride) v[f * stride + I] = a; else v[2 * I + f] = a;
 }
 
+// XCD-aware row order: the dispatcher hands workgroup b to XCD b % 8, so
+// consecutive workgroups (neighbouring rows, which gather the same x entries)
+// would land in 8 different L2s.  Renumber so that every XCD walks one
+// contiguous range of rows (bijective for any grid size).
+__device__ __forceinline__ int64_t row_block(int remap) {
+  const uint32_t b = blockIdx.x;
+  if (!remap) return b;
+  const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = b & 7;
+  return (int64_t)(x * q + (x < r ? x : r) + (b >> 3));
+}
+
 template <int VL, int EPI, bool XFM, int TAG>
 __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
     const dv4* __restrict__ bval, const double* __restrict__ x, int64_t xs,
     const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap) {
   const int lane = threadIdx.x & (VL - 1);
-  const int64_t node = ((int64_t)blockIdx.x * 256 + threadIdx.x) / VL;
+  const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
   double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
   if (node < nr) {
     const int64_t p0 = bptr[node], p1 = bptr[node + 1];
@@ -164,6 +176,58 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
     }
     vset(out, os, node, 0, o0);
     vset(out, os, node, 1, o1);
+  }
+}
+
+// prolongation fused into the first post-smoothing sweep (post_fusion):
+//   out(I) = x1(I) + (P e)(I) + W_I (r1(I) - (AP e)(I))
+// which equals x2 + W (b - A x2) for x2 = x1 + P e, since r1 = b - A x1 and
+// A x2 = A x1 + (AP) e.  Row I of the merged matrix holds P's blocks in
+// [mptr[2I], mptr[2I+1]) then AP's in [mptr[2I+1], mptr[2I+2]): one contiguous
+// window per node, both sums gathered from the same coarse vector e.
+template <int VL, int TAG>
+__global__ __launch_bounds__(256) void bsr2_post_kernel(
+    int64_t nr, const int64_t* __restrict__ mptr, const int32_t* __restrict__ bcol,
+    const dv4* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
+    const double* __restrict__ r1, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
+  const int lane = threadIdx.x & (VL - 1);
+  const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
+  const double2* e2 = reinterpret_cast<const double2*>(e);
+  double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
+  if (node < nr) {
+    const int64_t k0 = mptr[2 * node], km = mptr[2 * node + 1], k1 = mptr[2 * node + 2];
+    int64_t k = k0 + lane;
+    for (; k + VL < k1; k += 2 * VL) {
+      const int32_t c0 = bcol[k], c1 = bcol[k + VL];
+      const dv4 v0 = bval[k], v1 = bval[k + VL];
+      const double2 a = e2[c0], b = e2[c1];
+      const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
+      const double w0 = v1.x * b.x + v1.y * b.y, w1 = v1.z * b.x + v1.w * b.y;
+      const bool pa = k < km, pb = k + VL < km;
+      p0 += pa ? u0 : 0.0; p1 += pa ? u1 : 0.0; q0 += pa ? 0.0 : u0; q1 += pa ? 0.0 : u1;
+      p0 += pb ? w0 : 0.0; p1 += pb ? w1 : 0.0; q0 += pb ? 0.0 : w0; q1 += pb ? 0.0 : w1;
+    }
+    if (k < k1) {
+      const int32_t c0 = bcol[k];
+      const dv4 v0 = bval[k];
+      const double2 a = e2[c0];
+      const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
+      const bool pa = k < km;
+      p0 += pa ? u0 : 0.0; p1 += pa ? u1 : 0.0; q0 += pa ? 0.0 : u0; q1 += pa ? 0.0 : u1;
+    }
+  }
+#pragma unroll
+  for (int off = VL / 2; off > 0; off >>= 1) {
+    p0 += __shfl_xor(p0, off, VL);
+    p1 += __shfl_xor(p1, off, VL);
+    q0 += __shfl_xor(q0, off, VL);
+    q1 += __shfl_xor(q1, off, VL);
+  }
+  if (node < nr && lane == 0) {
+    const dv4 w = W[node];
+    const double d0 = r1[2 * node] - q0, d1 = r1[2 * node + 1] - q1;
+    vset(out, os, node, 0, x1[2 * node] + p0 + (w.x * d0 + w.y * d1));
+    vset(out, os, node, 1, x1[2 * node + 1] + p1 + (w.z * d0 + w.w * d1));
   }
 }
 
@@ -268,6 +332,17 @@ __global__ __launch_bounds__(256) void cg_undo_kernel(int64_t n, double alpha,
 
 inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 
+// tuning knobs, read at upload: MAMG_XCD_REMAP (0/1,
+// default 1), MAMG_POST_LANES (0 = auto)
+int g_remap = 1;
+int g_post_lanes = 0;
+void read_knobs() {
+  const char* e = std::getenv("MAMG_XCD_REMAP");
+  g_remap = e ? std::atoi(e) != 0 : 1;
+  e = std::getenv("MAMG_POST_LANES");
+  g_post_lanes = e ? std::atoi(e) : 0;
+}
+
 // ---------------------------------------------------------------------------
 // device structures
 // ---------------------------------------------------------------------------
@@ -292,6 +367,7 @@ struct DLevel {
   bool coarsest = false;
   DCsr A, P, R, WB;        // CSR layout
   DBsr Ab, Pb, Rb;         // BSR2 layout
+  DBsr PAb;                // BSR2 post fusion: merged [P | AP] rows (ptr: 2 nr + 1)
   dv4* Wd = nullptr;       // BSR2 layout: 2x2 smoother block per node
   double* winv = nullptr;
   double* Ainv = nullptr;
@@ -299,7 +375,7 @@ struct DLevel {
          *c = nullptr, *e = nullptr;
 };
 
-enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5 };
+enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -410,16 +486,18 @@ int pick_lanes_bsr(int64_t nr, int64_t nb) {
   return l;
 }
 
+// (also uploads a merged [P | AP] matrix: then B.ptr has 2 nr + 1 entries)
 int upload_bsr(DeviceHandle* h, const HBsr& B, DBsr* D, int lanes, std::string* err) {
+  const int64_t np = (int64_t)B.ptr.size();
   D->nr = B.nr;
   D->nc = B.nc;
-  D->nb = B.ptr[B.nr];
+  D->nb = B.ptr[np - 1];
   D->lanes = lanes > 0 ? lanes : pick_lanes_bsr(B.nr, D->nb);
   int rc;
-  if ((rc = dalloc(h, &D->ptr, B.nr + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->ptr, np, err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
   if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nb, 1), err))) return rc;
-  HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), (B.nr + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), np * sizeof(int64_t), hipMemcpyHostToDevice));
   if (D->nb) {
     HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
@@ -466,6 +544,17 @@ Op bsr_op(const DBsr& M, int epi, int cls, int tag, const double* x, int64_t xs,
   o.kind = OP_BSR; o.epi = epi; o.cls = cls; o.tag = tag; o.Mb = &M; o.n = M.nr;
   o.x = x; o.xs = xs; o.xfm = xs != 0; o.y = y; o.b = b; o.bs = bs; o.W = W; o.out = out; o.os = os;
   o.bytes = bsr_bytes(M, epi);
+  return o;
+}
+
+// merged [P | AP] blocks + 2 nr + 1 pointers, e gathered once, x1 r1 W out
+Op post_op(const DLevel& L, int cls, int tag, const double* e, const double* x1, double* out,
+           int64_t os) {
+  const DBsr& M = L.PAb;
+  Op o;
+  o.kind = OP_POST; o.cls = cls; o.tag = tag; o.Mb = &M; o.n = M.nr;
+  o.x = e; o.y = x1; o.b = L.r; o.W = L.Wd; o.out = out; o.os = os;
+  o.bytes = 36.0 * M.nb + 8.0 * (2 * M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr * 3 + 32.0 * M.nr;
   return o;
 }
 
@@ -568,9 +657,17 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops);
     ops->push_back(axpy_op(C.n, C.e, C.x));
   }
-  ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
-                        nullptr, X, 0));
-  for (int s = 0; s < p.postsmooth_iter; ++s) {
+  int s0 = 0;
+  if (L.PAb.nr > 0 && p.postsmooth_iter >= 1) {   // prolongation + first post sweep
+    const bool last = p.postsmooth_iter == 1;
+    ops->push_back(post_op(L, clsS, tagA, C.x, X, last ? xout : X2, last ? os : 0));
+    if (!last) std::swap(X, X2);
+    s0 = 1;
+  } else {
+    ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
+                          nullptr, X, 0));
+  }
+  for (int s = s0; s < p.postsmooth_iter; ++s) {
     const bool last = s == p.postsmooth_iter - 1;
     double* out = last ? xout : X2;
     ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, out, last ? os : 0));
@@ -647,7 +744,7 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
+#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_remap
   switch (o.epi) {
     case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
@@ -660,6 +757,27 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
 template <int VL, int TAG>
 void launch_bsr_vl(const Op& o, hipStream_t s) {
   if (o.xfm) launch_bsr_x<VL, true, TAG>(o, s); else launch_bsr_x<VL, false, TAG>(o, s);
+}
+
+template <int VL, int TAG>
+void launch_post_vl(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const unsigned g = nblocks(M.nr * (int64_t)VL);
+  if (g == 0) return;
+  bsr2_post_kernel<VL, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
+                                              o.out, o.os, g_remap);
+}
+
+template <int TAG>
+void launch_post_tag(const Op& o, hipStream_t s) {
+  switch (o.Mb->lanes) {
+    case 2: launch_post_vl<2, TAG>(o, s); break;
+    case 4: launch_post_vl<4, TAG>(o, s); break;
+    case 8: launch_post_vl<8, TAG>(o, s); break;
+    case 16: launch_post_vl<16, TAG>(o, s); break;
+    case 32: launch_post_vl<32, TAG>(o, s); break;
+    default: launch_post_vl<64, TAG>(o, s); break;
+  }
 }
 
 template <int TAG>
@@ -681,6 +799,9 @@ void launch(const Op& o, hipStream_t s) {
       break;
     case OP_BSR:
       if (o.tag == 0) launch_bsr_tag<0>(o, s); else launch_bsr_tag<1>(o, s);
+      break;
+    case OP_POST:
+      if (o.tag == 0) launch_post_tag<0>(o, s); else launch_post_tag<1>(o, s);
       break;
     case OP_BD:
       if (o.n) bd2_kernel<false><<<nblocks(o.n), 256, 0, s>>>(o.n, o.W, o.b, o.bs, nullptr, o.out, 0);
@@ -750,6 +871,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   const int nl = (int)H.levels.size();
   h->L.resize(nl);
   h->bsr = bsr_eligible(H, A0, p);
+  read_knobs();
   int rc;
   for (int l = 0; l < nl; ++l) {
     const HostLevel& hl = H.levels[l];
@@ -780,7 +902,15 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
     } else if (h->bsr) {
       const int64_t nv = D.n / 2, nvc = H.levels[l + 1].n / 2;
       if ((rc = upload_csr_as_bsr(h.get(), Al, nv, nv, &D.Ab, lanesA, err))) return rc;
-      if ((rc = upload_csr_as_bsr(h.get(), hl.P.view(), nv, nvc, &D.Pb, 0, err))) return rc;
+      if (p.post_fusion && p.postsmooth_iter >= 1 && hl.AP.n == hl.n) {
+        HBsr Pn, APn, M;
+        to_bsr2(hl.P.view(), nv, nvc, &Pn);
+        to_bsr2(hl.AP.view(), nv, nvc, &APn);
+        merge_bsr_rows(Pn, APn, &M);
+        if ((rc = upload_bsr(h.get(), M, &D.PAb, g_post_lanes, err))) return rc;
+      } else {
+        if ((rc = upload_csr_as_bsr(h.get(), hl.P.view(), nv, nvc, &D.Pb, 0, err))) return rc;
+      }
       if ((rc = upload_csr_as_bsr(h.get(), hl.R.view(), nvc, nv, &D.Rb, 0, err))) return rc;
       std::vector<double> blk;
       node_blocks_of(hl.WB.view(), nv, &blk);

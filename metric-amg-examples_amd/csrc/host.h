@@ -39,6 +39,7 @@ struct HostLevel {
   std::vector<double> winv; // point smoother weights (empty if WB used)
   Csr WB;                   // seed-block smoother (level 0 with idofs)
   Csr P, R;                 // prolongation / restriction (R = P^T)
+  Csr AP;                   // A P (Galerkin intermediate; kept for post fusion)
   std::vector<int64_t> agg; // aggregate id per row (-1 isolated)
   int64_t nagg = 0;
   double w_sa = 0.0;
@@ -76,6 +77,9 @@ void to_bsr2(const CsrView& M, int64_t nr, int64_t nc, HBsr* B);
 void to_bsr2_rows(const CsrView& M, int64_t nr, int64_t nc, int64_t r0, int64_t r1, HBsr* B);
 // smoother matrix -> one 2x2 block per node; false if it couples two nodes
 bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk);
+// rows of P then rows of Q (same nr): M.ptr has 2 nr + 1 entries, row I of P in
+// [ptr[2I], ptr[2I+1]), row I of Q in [ptr[2I+1], ptr[2I+2])
+void merge_bsr_rows(const HBsr& P, const HBsr& Q, HBsr* M);
 
 // hash shared with the oracle (oracle/mamg_oracle.py:hash32)
 inline uint32_t hash32(uint64_t i, int level) {

@@ -795,9 +795,9 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
       lev.P = std::move(T);
     }
     transpose(lev.P.view(), &lev.R);
-    Csr AP;
-    spgemm(cur, lev.P.view(), &AP);
-    spgemm(lev.R.view(), AP.view(), &next);
+    spgemm(cur, lev.P.view(), &lev.AP);
+    spgemm(lev.R.view(), lev.AP.view(), &next);
+    if (!p.post_fusion || nf != 2) lev.AP = Csr();
     if (p.print_level > 0)
       std::fprintf(stderr, "[mamg] level %d: n=%lld nnz=%lld nagg=%lld nnzP=%lld\n", l,
                    (long long)n, (long long)cur.nnz(), (long long)nagg, (long long)lev.P.nnz());

@@ -35,7 +35,7 @@ KEYS = ('prectype', 'AMG_type', 'cycle_type', 'max_levels', 'maxit', 'smoother',
         'Schwarz_maxlvl', 'Schwarz_type', 'Schwarz_blksolver', 'print_level',
         # build-defined extensions
         'sa_omega', 'rho_iters', 'max_coarse_dense', 'device', 'spmv_lanes',
-        'num_functions', 'node_block_smoother', 'sa_block_diag')
+        'num_functions', 'node_block_smoother', 'sa_block_diag', 'post_fusion')
 
 # ---- the GPU profile "mi355x_sa_v"  -------------------
 parameters_metric_mi355x = {

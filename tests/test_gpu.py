@@ -46,7 +46,14 @@ APPLY_CASES = [
     (3, 16, 1e2, dict(num_functions=2, cycle_type='W')),
     (2, 32, 1e3, dict(num_functions=2, presmooth_iter=2, postsmooth_iter=3, maxit=2)),
     (2, 32, 1e3, dict(num_functions=2, node_block_smoother=0, sa_block_diag=0)),
+    (3, 16, 1e6, dict(num_functions=2, post_fusion=0)),
+    (2, 32, 1e3, dict(num_functions=2, post_fusion=0, cycle_type='W')),
 ]
+DEVICE_ONLY = ('post_fusion',)       # schedule knobs: same cycle, no oracle counterpart
+
+
+def oracle_kw(kw):
+    return {k: v for k, v in kw.items() if k not in DEVICE_ONLY}
 
 
 @pytest.mark.parametrize('dim,n,g,kw', APPLY_CASES)
@@ -56,7 +63,7 @@ def test_apply_matches_oracle(lib_built, dim, n, g, kw):
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
     B = M.MetricAMG(A, s.W, idofs=s.idofs, **to_c(kw))
-    h = mo.setup(A, mo.Params(**kw), idofs=s.idofs)
+    h = mo.setup(A, mo.Params(**oracle_kw(kw)), idofs=s.idofs)
     assert B.num_levels == len(h.levels)
     # gamma >= 1e8 makes A_l badly conditioned (entries span ~gamma); the
     # summation-order difference is then amplified: 1e-8 there
@@ -153,6 +160,24 @@ def test_bsr2_and_csr_layouts_agree(lib_built, dim, n, g, kw):
     assert Bc.layout == 'csr'
     hc = mo.setup(A, mo.Params(num_functions=2, node_block_smoother=0, **kw), idofs=None)
     assert rel(Bc * r, hc.apply(r)) < APPLY_TOL
+
+
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (3, 16, 1e4, dict(cycle_type='W')),
+                                        (2, 64, 1.0, dict(maxit=2, postsmooth_iter=3)),
+                                        (3, 8, 1e2, dict(presmooth_iter=2, postsmooth_iter=2))])
+def test_post_fusion_equals_unfused(lib_built, dim, n, g, kw):
+    """z = x1 + P e + W (r1 - (AP) e) (one pass over [P | AP]) is the same
+    cycle as prolongation followed by a block-Jacobi sweep: fused and unfused
+    schedules agree to summation order."""
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    Bf = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+    Bu = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, post_fusion=0, **to_c(kw))
+    assert Bf.layout == Bu.layout == 'bsr2'
+    for seed in (1234, 99):
+        r = mo.seeded_rhs(s.N, seed)
+        assert rel(Bf * r, Bu * r) < 1e-12
 
 
 def test_bsr2_spmv_and_pcg_field_major(lib_built):
