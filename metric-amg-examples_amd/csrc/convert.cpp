@@ -86,6 +86,74 @@ void merge_bsr_rows(const HBsr& P, const HBsr& Q, HBsr* M) {
   }
 }
 
+int to_sell(const HBsr& B, bool sym, int C, int sigma, HSell* S, std::string* err) {
+  const int64_t nr = B.nr, ns = (nr + C - 1) / C;
+  const bool merged = (int64_t)B.ptr.size() == 2 * nr + 1;
+  auto row0 = [&](int64_t I, int64_t* a, int64_t* m, int64_t* e) {
+    if (merged) { *a = B.ptr[2 * I]; *m = B.ptr[2 * I + 1]; *e = B.ptr[2 * I + 2]; }
+    else { *a = B.ptr[I]; *m = *a; *e = B.ptr[I + 1]; }
+  };
+  S->perm.clear();
+  if (sigma > 1) {   // sort rows by decreasing length inside windows of sigma rows
+    S->perm.resize(nr);
+#pragma omp parallel for schedule(static)
+    for (int64_t w0 = 0; w0 < nr; w0 += sigma) {
+      const int64_t w1 = std::min(nr, w0 + sigma);
+      for (int64_t I = w0; I < w1; ++I) S->perm[I] = (int32_t)I;
+      std::stable_sort(S->perm.begin() + w0, S->perm.begin() + w1, [&](int32_t x, int32_t y) {
+        int64_t a, m, e, a2, m2, e2;
+        row0(x, &a, &m, &e);
+        row0(y, &a2, &m2, &e2);
+        return e - a > e2 - a2;
+      });
+    }
+  }
+  auto row = [&](int64_t slot, int64_t* a, int64_t* m, int64_t* e) {
+    row0(sigma > 1 ? S->perm[slot] : slot, a, m, e);
+  };
+  S->nr = nr;
+  S->meta.assign(nr, 0);
+  S->soff.assign(ns + 1, 0);
+  int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t I = s * C; I < std::min(nr, (s + 1) * C); ++I) {
+      int64_t a, m, e;
+      row(I, &a, &m, &e);
+      if (e - a >= 0xffff) { bad = 1; continue; }
+      S->meta[I] = (int32_t)((e - a) | ((m - a) << 16));
+      w = std::max(w, e - a);
+    }
+    S->soff[s + 1] = C * w;
+  }
+  if (bad) { *err = "SELL: row longer than 65534 blocks"; return MAMG_ERR_UNSUPPORTED; }
+  for (int64_t s = 0; s < ns; ++s) S->soff[s + 1] += S->soff[s];
+  const int64_t nbs = S->soff[ns];
+  S->nbs = nbs;
+  const int per = sym ? 3 : 4;
+  S->col.assign(nbs, 0);
+  S->val.assign(per * nbs, 0.0);
+#pragma omp parallel for schedule(static)
+  for (int64_t I = 0; I < nr; ++I) {
+    int64_t a, m, e;
+    row(I, &a, &m, &e);
+    int64_t kk = S->soff[I / C] + (I % C);
+    for (int64_t k = a; k < e; ++k, kk += C) {
+      S->col[kk] = B.col[k];
+      const double* v = &B.val[4 * k];
+      if (sym) {
+        S->val[2 * kk] = v[0];
+        S->val[2 * kk + 1] = v[3];
+        S->val[2 * nbs + kk] = v[1];
+      } else {
+        for (int q = 0; q < 4; ++q) S->val[4 * kk + q] = v[q];
+      }
+    }
+  }
+  return MAMG_OK;
+}
+
 // W_B (or node-block smoother) -> one 2x2 block per node; false if some entry
 // couples different nodes (then the BSR2 layout cannot fuse the smoother)
 bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk) {

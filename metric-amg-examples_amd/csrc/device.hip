@@ -111,21 +111,37 @@ __device__ __forceinline__ int64_t row_block(int remap) {
   return (int64_t)(x * q + (x < r ? x : r) + (b >> 3));
 }
 
-template <int VL, int EPI, bool XFM, int TAG>
+// block k of a BSR2 value array: 4 doubles (0,0) (0,1) (1,0) (1,1) per block,
+// or in the symmetric-block format (SYM) two aligned streams: the diagonal
+// pairs {(0,0), (1,1)} (16 B per block) then the off-diagonals (0,1) = (1,0)
+// (8 B per block) starting at v + 2 nb
+template <bool SYM>
+__device__ __forceinline__ dv4 blk(const double* __restrict__ v, const double* __restrict__ off,
+                                   int64_t k) {
+  if (SYM) {
+    const double2 d = reinterpret_cast<const double2*>(v)[k];
+    const double b = off[k];
+    return dv4{d.x, b, b, d.y};
+  }
+  return reinterpret_cast<const dv4*>(v)[k];
+}
+
+template <int VL, int EPI, bool XFM, bool SYM, int TAG>
 __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
-    const dv4* __restrict__ bval, const double* __restrict__ x, int64_t xs,
+    const double* __restrict__ bval, const double* __restrict__ x, int64_t xs,
     const double* y, const double* __restrict__ b, int64_t bs,
     const dv4* __restrict__ W, double* out, int64_t os, int remap) {
   const int lane = threadIdx.x & (VL - 1);
   const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
+  const double* offd = SYM ? bval + 2 * bptr[nr] : nullptr;
   double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
   if (node < nr) {
     const int64_t p0 = bptr[node], p1 = bptr[node + 1];
     int64_t k = p0 + lane;
     for (; k + VL < p1; k += 2 * VL) {
       const int32_t c0 = bcol[k], c1 = bcol[k + VL];
-      const dv4 v0 = bval[k], v1 = bval[k + VL];
+      const dv4 v0 = blk<SYM>(bval, offd, k), v1 = blk<SYM>(bval, offd, k + VL);
       double a0, a1, e0, e1;
       if (XFM) {
         a0 = x[c0]; a1 = x[xs + c0]; e0 = x[c1]; e1 = x[xs + c1];
@@ -141,7 +157,7 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
     }
     if (k < p1) {
       const int32_t c0 = bcol[k];
-      const dv4 v0 = bval[k];
+      const dv4 v0 = blk<SYM>(bval, offd, k);
       double a0, a1;
       if (XFM) {
         a0 = x[c0]; a1 = x[xs + c0];
@@ -188,7 +204,7 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
 template <int VL, int TAG>
 __global__ __launch_bounds__(256) void bsr2_post_kernel(
     int64_t nr, const int64_t* __restrict__ mptr, const int32_t* __restrict__ bcol,
-    const dv4* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
+    const double* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
     const double* __restrict__ r1, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
   const int lane = threadIdx.x & (VL - 1);
   const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
@@ -199,7 +215,7 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
     int64_t k = k0 + lane;
     for (; k + VL < k1; k += 2 * VL) {
       const int32_t c0 = bcol[k], c1 = bcol[k + VL];
-      const dv4 v0 = bval[k], v1 = bval[k + VL];
+      const dv4 v0 = blk<false>(bval, nullptr, k), v1 = blk<false>(bval, nullptr, k + VL);
       const double2 a = e2[c0], b = e2[c1];
       const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
       const double w0 = v1.x * b.x + v1.y * b.y, w1 = v1.z * b.x + v1.w * b.y;
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
     }
     if (k < k1) {
       const int32_t c0 = bcol[k];
-      const dv4 v0 = bval[k];
+      const dv4 v0 = blk<false>(bval, nullptr, k);
       const double2 a = e2[c0];
       const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
       const bool pa = k < km;
@@ -229,6 +245,124 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
     vset(out, os, node, 0, x1[2 * node] + p0 + (w.x * d0 + w.y * d1));
     vset(out, os, node, 1, x1[2 * node + 1] + p1 + (w.z * d0 + w.w * d1));
   }
+}
+
+// ---------------------------------------------------------------------------
+// Sliced-ELL variant of BSR2 (SELL-64) for the large short-row level-0
+// operators (A_0: ~15 blocks per node, [P | AP]: ~13).  One lane per node;
+// slice s = nodes [64 s, 64 s + 64) = one wavefront; block j of the slice's
+// lane l sits at soff[s] + 64 j + l, so every load of the row loop is one
+// fully coalesced 64-lane access (2 KB of blocks, 256 B of columns) with no
+// cross-lane reduction.  meta[I] = row length | (P-part length << 16) (the
+// split is used by the fused post kernel only).  Each lane loops only to its
+// own length; padding is storage, never loaded.  Sums run in block order.
+// ---------------------------------------------------------------------------
+constexpr int SELL_C = 64;
+constexpr int SELL_U = 4;     // blocks in flight per lane
+
+template <bool XFM>
+__device__ __forceinline__ double2 xget(const double* x, int64_t xs, int32_t c) {
+  if (XFM) return double2{x[c], x[xs + c]};
+  return reinterpret_cast<const double2*>(x)[c];
+}
+
+template <int EPI, bool XFM, bool SYM, int TAG>
+__global__ __launch_bounds__(256) void sell2_kernel(
+    int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
+    const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
+    const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os) {
+  const int64_t node = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (node >= nr) return;
+  const double* offd = SYM ? bval + 2 * nbs : nullptr;
+  const int len = meta[node] & 0xffff;
+  int64_t k = soff[node / SELL_C] + (node & (SELL_C - 1));
+  double s0 = 0.0, s1 = 0.0;
+  int j = 0;
+  for (; j + SELL_U <= len; j += SELL_U, k += SELL_U * SELL_C) {
+    int32_t c[SELL_U];
+    dv4 v[SELL_U];
+    double2 a[SELL_U];
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) { c[u] = bcol[k + u * SELL_C]; v[u] = blk<SYM>(bval, offd, k + u * SELL_C); }
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) {
+      s0 += v[u].x * a[u].x; s0 += v[u].y * a[u].y;
+      s1 += v[u].z * a[u].x; s1 += v[u].w * a[u].y;
+    }
+  }
+  for (; j < len; ++j, k += SELL_C) {
+    const dv4 v = blk<SYM>(bval, offd, k);
+    const double2 a = xget<XFM>(x, xs, bcol[k]);
+    s0 += v.x * a.x; s0 += v.y * a.y;
+    s1 += v.z * a.x; s1 += v.w * a.y;
+  }
+  double o0, o1;
+  if (EPI == EPI_Y) {
+    o0 = s0; o1 = s1;
+  } else if (EPI == EPI_YADD) {
+    o0 = y[2 * node] + s0; o1 = y[2 * node + 1] + s1;
+  } else if (EPI == EPI_RESID) {
+    o0 = vget(b, bs, node, 0) - s0; o1 = vget(b, bs, node, 1) - s1;
+  } else {  // EPI_BJAC
+    const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
+    const dv4 w = W[node];
+    o0 = y[2 * node] + (w.x * r0 + w.y * r1);
+    o1 = y[2 * node + 1] + (w.z * r0 + w.w * r1);
+  }
+  vset(out, os, node, 0, o0);
+  vset(out, os, node, 1, o1);
+}
+
+// fused prolongation + first post sweep on a SELL-64 [P | AP] (see
+// bsr2_post_kernel).  Rows are sorted by length inside windows of
+// SELL_SIGMA rows (slot i holds row perm[i]) so a wavefront's lanes have
+// near-equal trip counts; blocks [0, plen) of a row are P's, [plen, len) AP's,
+// selected per block (one loop, no divergence between the two parts).
+constexpr int SELL_SIGMA = 4096;
+
+template <int TAG>
+__global__ __launch_bounds__(256) void sell2_post_kernel(
+    int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ bcol,
+    const double* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
+    const double* __restrict__ r1, const dv4* __restrict__ W, double* out, int64_t os) {
+  const int64_t slot = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (slot >= nr) return;
+  const int64_t node = perm[slot];
+  const int32_t m = meta[slot];
+  const int len = m & 0xffff, plen = m >> 16;
+  int64_t k = soff[slot / SELL_C] + (slot & (SELL_C - 1));
+  double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
+  int j = 0;
+  for (; j + SELL_U <= len; j += SELL_U, k += SELL_U * SELL_C) {
+    int32_t c[SELL_U];
+    dv4 v[SELL_U];
+    double2 a[SELL_U];
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) { c[u] = bcol[k + u * SELL_C]; v[u] = blk<false>(bval, nullptr, k + u * SELL_C); }
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) a[u] = xget<false>(e, 0, c[u]);
+#pragma unroll
+    for (int u = 0; u < SELL_U; ++u) {
+      const double u0 = v[u].x * a[u].x + v[u].y * a[u].y, u1 = v[u].z * a[u].x + v[u].w * a[u].y;
+      const bool isp = j + u < plen;
+      p0 += isp ? u0 : 0.0; p1 += isp ? u1 : 0.0; q0 += isp ? 0.0 : u0; q1 += isp ? 0.0 : u1;
+    }
+  }
+  for (; j < len; ++j, k += SELL_C) {
+    const dv4 v = blk<false>(bval, nullptr, k);
+    const double2 a = xget<false>(e, 0, bcol[k]);
+    const double u0 = v.x * a.x + v.y * a.y, u1 = v.z * a.x + v.w * a.y;
+    const bool isp = j < plen;
+    p0 += isp ? u0 : 0.0; p1 += isp ? u1 : 0.0; q0 += isp ? 0.0 : u0; q1 += isp ? 0.0 : u1;
+  }
+  const dv4 w = W[node];
+  const double d0 = r1[2 * node] - q0, d1 = r1[2 * node + 1] - q1;
+  vset(out, os, node, 0, x1[2 * node] + p0 + (w.x * d0 + w.y * d1));
+  vset(out, os, node, 1, x1[2 * node + 1] + p1 + (w.z * d0 + w.w * d1));
 }
 
 // block-diagonal apply: out(I) = [y(I) +] W_I b(I)
@@ -332,15 +466,50 @@ __global__ __launch_bounds__(256) void cg_undo_kernel(int64_t n, double alpha,
 
 inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 
-// tuning knobs, read at upload: MAMG_XCD_REMAP (0/1,
-// default 1), MAMG_POST_LANES (0 = auto)
+// tuning knobs, read at upload (bench/variants.py):
+//   MAMG_XCD_REMAP  0 off, 1 restriction ops only (default), 2 every BSR op
+//   MAMG_POST_LANES lanes per row of the fused post kernel (0 = auto)
+//   MAMG_SYM_BLOCKS 0 disables the symmetric-block format (default 1)
+//   MAMG_SELL       0 disables the SELL-64 storage (default 1), used for
+//                   matrices with >= MAMG_SELL_MIN_ROWS (2^20) node rows
+//   MAMG_SELL_POST  1: SELL-64-sigma for the merged [P | AP] too (default 0)
 int g_remap = 1;
 int g_post_lanes = 0;
+int g_sym = 1;
+int g_sell = 1;
+int g_sell_post = 0;
+int64_t g_sell_min_rows = 1 << 20;
 void read_knobs() {
+  const char* sp = std::getenv("MAMG_SELL_POST");
+  g_sell_post = sp ? std::atoi(sp) : 0;
+  const char* s = std::getenv("MAMG_SELL");
+  g_sell = s ? std::atoi(s) : 1;
+  s = std::getenv("MAMG_SELL_MIN_ROWS");
+  g_sell_min_rows = s ? std::atoll(s) : (1 << 20);
   const char* e = std::getenv("MAMG_XCD_REMAP");
-  g_remap = e ? std::atoi(e) != 0 : 1;
+  g_remap = e ? std::atoi(e) : 1;
   e = std::getenv("MAMG_POST_LANES");
   g_post_lanes = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_SYM_BLOCKS");
+  g_sym = e ? std::atoi(e) != 0 : 1;
+}
+
+// every block symmetric (bitwise): then 3 doubles per block carry it exactly
+bool blocks_symmetric(const HBsr& B) {
+  const int64_t nb = B.ptr[B.nr];
+  int64_t bad = 0;
+  for (int64_t k = 0; k < nb; ++k)
+    bad |= std::memcmp(&B.val[4 * k + 1], &B.val[4 * k + 2], sizeof(double)) != 0;
+  return bad == 0;
+}
+void pack_sym(const HBsr& B, std::vector<double>* v3) {
+  const int64_t nb = B.ptr[B.nr];
+  v3->resize(3 * nb);
+  for (int64_t k = 0; k < nb; ++k) {
+    (*v3)[2 * k] = B.val[4 * k];
+    (*v3)[2 * k + 1] = B.val[4 * k + 3];
+    (*v3)[2 * nb + k] = B.val[4 * k + 1];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -358,8 +527,16 @@ struct DBsr {              // 2x2 blocks, node-major
   int64_t nr = 0, nc = 0, nb = 0;
   int64_t* ptr = nullptr;
   int32_t* col = nullptr;
-  dv4* val = nullptr;
+  double* val = nullptr;   // 4 doubles per block, 3 if sym
   int lanes = 8;
+  bool sym = false;        // symmetric-block format (every block has (0,1) == (1,0))
+  // SELL-64 storage (sell == true): ptr unused; soff per slice, meta per row,
+  // col / val hold nbs (>= nb, padded) slots
+  bool sell = false;
+  int64_t nbs = 0;
+  int64_t* soff = nullptr;
+  int32_t* meta = nullptr;
+  int32_t* perm = nullptr;  // SELL-C-sigma: row held by each slot (merged matrices)
 };
 
 struct DLevel {
@@ -400,8 +577,11 @@ struct Op {
   double* out = nullptr;
   int64_t xs = 0, bs = 0, os = 0;   // BSR2 field strides (0 = node-major)
   bool xfm = false;
+  int remap = 0;                    // XCD-contiguous row order (restriction ops)
   double bytes = 0.0;
 };
+
+inline int remap_of(const Op& o) { return g_remap == 2 ? 1 : (g_remap == 1 ? o.remap : 0); }
 
 struct Graph {
   const double* r = nullptr;
@@ -486,30 +666,72 @@ int pick_lanes_bsr(int64_t nr, int64_t nb) {
   return l;
 }
 
+// SELL-64 copy of a BSR2 matrix (host packing: convert.cpp to_sell)
+int upload_sell(DeviceHandle* h, const HBsr& B, DBsr* D, std::string* err) {
+  HSell S;
+  const bool merged = (int64_t)B.ptr.size() == 2 * B.nr + 1;
+  int rc = to_sell(B, D->sym, SELL_C, merged ? SELL_SIGMA : 1, &S, err);
+  if (rc) return rc;
+  const int64_t ns = (int64_t)S.soff.size() - 1;
+  const int per = D->sym ? 3 : 4;
+  D->sell = true;
+  D->nbs = S.nbs;
+  if ((rc = dalloc(h, &D->soff, ns + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->meta, std::max<int64_t>(S.nr, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(S.nbs, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * S.nbs, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->soff, S.soff.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (S.nr) HIPCHK(hipMemcpy(D->meta, S.meta.data(), S.nr * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (!S.perm.empty()) {
+    if ((rc = dalloc(h, &D->perm, S.nr, err))) return rc;
+    HIPCHK(hipMemcpy(D->perm, S.perm.data(), S.nr * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  if (S.nbs) {
+    HIPCHK(hipMemcpy(D->col, S.col.data(), S.nbs * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, S.val.data(), per * S.nbs * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+
 // (also uploads a merged [P | AP] matrix: then B.ptr has 2 nr + 1 entries)
-int upload_bsr(DeviceHandle* h, const HBsr& B, DBsr* D, int lanes, std::string* err) {
+int upload_bsr(DeviceHandle* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
+               bool sym = false) {
   const int64_t np = (int64_t)B.ptr.size();
   D->nr = B.nr;
   D->nc = B.nc;
   D->nb = B.ptr[np - 1];
   D->lanes = lanes > 0 ? lanes : pick_lanes_bsr(B.nr, D->nb);
   int rc;
+  // SELL-64 for many short rows (one lane per row needs >> 256 CUs x 64 rows)
+  const bool merged_rows = np == 2 * B.nr + 1;
+  if (g_sell && B.nr >= g_sell_min_rows && D->nb <= 40 * B.nr && (!merged_rows || g_sell_post)) {
+    D->sym = sym && g_sym && np == B.nr + 1 && blocks_symmetric(B);
+    return upload_sell(h, B, D, err);
+  }
   if ((rc = dalloc(h, &D->ptr, np, err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
-  if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nb, 1), err))) return rc;
+  D->sym = sym && g_sym && np == B.nr + 1 && blocks_symmetric(B);
+  const int per = D->sym ? 3 : 4;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
   HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), np * sizeof(int64_t), hipMemcpyHostToDevice));
   if (D->nb) {
     HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+    if (D->sym) {
+      std::vector<double> v3;
+      pack_sym(B, &v3);
+      HIPCHK(hipMemcpy(D->val, v3.data(), D->nb * 3 * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+      HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+    }
   }
   return MAMG_OK;
 }
 
 int upload_csr_as_bsr(DeviceHandle* h, const CsrView& M, int64_t nr, int64_t nc, DBsr* D, int lanes,
-                      std::string* err) {
+                      std::string* err, bool sym = false) {
   HBsr B;
   to_bsr2(M, nr, nc, &B);
-  return upload_bsr(h, B, D, lanes, err);
+  return upload_bsr(h, B, D, lanes, err, sym);
 }
 
 // ---- algorithmic bytes (per layout) ------------------------------
@@ -521,8 +743,12 @@ double csr_bytes(const DCsr& M, int epi) {
   return b;
 }
 
+double index_bytes(const DBsr& M, int64_t ptr_entries) {
+  return M.sell ? 4.0 * M.nr + 8.0 * (M.nr / SELL_C + 2) : 8.0 * ptr_entries;
+}
+
 double bsr_bytes(const DBsr& M, int epi) {
-  double b = 36.0 * M.nb + 8.0 * (M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;  // A, x, out
+  double b = (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;  // A, x, out
   if (epi == EPI_YADD) b += 16.0 * M.nr;
   if (epi == EPI_RESID) b += 16.0 * M.nr;
   if (epi == EPI_BJAC) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;       // y, b, W
@@ -554,7 +780,7 @@ Op post_op(const DLevel& L, int cls, int tag, const double* e, const double* x1,
   Op o;
   o.kind = OP_POST; o.cls = cls; o.tag = tag; o.Mb = &M; o.n = M.nr;
   o.x = e; o.y = x1; o.b = L.r; o.W = L.Wd; o.out = out; o.os = os;
-  o.bytes = 36.0 * M.nb + 8.0 * (2 * M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr * 3 + 32.0 * M.nr;
+  o.bytes = 36.0 * M.nb + index_bytes(M, 2 * M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr * 3 + 32.0 * M.nr;
   return o;
 }
 
@@ -651,6 +877,7 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
                         nullptr, L.r, 0));
   ops->push_back(bsr_op(L.Rb, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, 0, nullptr, nullptr, 0,
                         nullptr, C.b, 0));
+  ops->back().remap = 1;
   cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops);
   if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
     ops->push_back(bsr_op(C.Ab, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0));
@@ -739,24 +966,52 @@ void launch_csr_tag(const Op& o, hipStream_t s) {
   }
 }
 
-template <int VL, bool XFM, int TAG>
+template <int VL, bool XFM, bool SYM, int TAG>
 void launch_bsr_x(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_remap
+#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o)
   switch (o.epi) {
-    case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
-    case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
-    case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
-    default: bsr2_kernel<VL, EPI_BJAC, XFM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    default: bsr2_kernel<VL, EPI_BJAC, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
   }
 #undef BSR_ARGS
 }
 
+template <bool XFM, bool SYM, int TAG>
+void launch_sell_x(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const unsigned g = nblocks(M.nr);
+  if (g == 0) return;
+#define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
+  switch (o.epi) {
+    case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    default: sell2_kernel<EPI_BJAC, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+  }
+#undef SELL_ARGS
+}
+
+template <int TAG>
+void launch_sell(const Op& o, hipStream_t s) {
+  if (o.Mb->sym) {
+    if (o.xfm) launch_sell_x<true, true, TAG>(o, s); else launch_sell_x<false, true, TAG>(o, s);
+  } else {
+    if (o.xfm) launch_sell_x<true, false, TAG>(o, s); else launch_sell_x<false, false, TAG>(o, s);
+  }
+}
+
 template <int VL, int TAG>
 void launch_bsr_vl(const Op& o, hipStream_t s) {
-  if (o.xfm) launch_bsr_x<VL, true, TAG>(o, s); else launch_bsr_x<VL, false, TAG>(o, s);
+  if (o.Mb->sym) {
+    if (o.xfm) launch_bsr_x<VL, true, true, TAG>(o, s); else launch_bsr_x<VL, false, true, TAG>(o, s);
+  } else {
+    if (o.xfm) launch_bsr_x<VL, true, false, TAG>(o, s); else launch_bsr_x<VL, false, false, TAG>(o, s);
+  }
 }
 
 template <int VL, int TAG>
@@ -765,11 +1020,18 @@ void launch_post_vl(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
   bsr2_post_kernel<VL, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
-                                              o.out, o.os, g_remap);
+                                              o.out, o.os, remap_of(o));
 }
 
 template <int TAG>
 void launch_post_tag(const Op& o, hipStream_t s) {
+  if (o.Mb->sell) {
+    const DBsr& M = *o.Mb;
+    if (M.nr)
+      sell2_post_kernel<TAG><<<nblocks(M.nr), 256, 0, s>>>(M.nr, M.soff, M.meta, M.perm, M.col, M.val,
+                                                           o.x, o.y, o.b, o.W, o.out, o.os);
+    return;
+  }
   switch (o.Mb->lanes) {
     case 2: launch_post_vl<2, TAG>(o, s); break;
     case 4: launch_post_vl<4, TAG>(o, s); break;
@@ -782,6 +1044,7 @@ void launch_post_tag(const Op& o, hipStream_t s) {
 
 template <int TAG>
 void launch_bsr_tag(const Op& o, hipStream_t s) {
+  if (o.Mb->sell) { launch_sell<TAG>(o, s); return; }
   switch (o.Mb->lanes) {
     case 2: launch_bsr_vl<2, TAG>(o, s); break;
     case 4: launch_bsr_vl<4, TAG>(o, s); break;
@@ -901,7 +1164,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
       }
     } else if (h->bsr) {
       const int64_t nv = D.n / 2, nvc = H.levels[l + 1].n / 2;
-      if ((rc = upload_csr_as_bsr(h.get(), Al, nv, nv, &D.Ab, lanesA, err))) return rc;
+      if ((rc = upload_csr_as_bsr(h.get(), Al, nv, nv, &D.Ab, lanesA, err, true))) return rc;
       if (p.post_fusion && p.postsmooth_iter >= 1 && hl.AP.n == hl.n) {
         HBsr Pn, APn, M;
         to_bsr2(hl.P.view(), nv, nvc, &Pn);
@@ -1196,7 +1459,7 @@ int ddalloc(DistHandle* h, T** p, int64_t count, std::string* err) {
   return MAMG_OK;
 }
 
-int dupload_bsr(DistHandle* h, const HBsr& B, DBsr* D, std::string* err) {
+int dupload_bsr(DistHandle* h, const HBsr& B, DBsr* D, std::string* err, bool sym = false) {
   D->nr = B.nr;
   D->nc = B.nc;
   D->nb = B.ptr.empty() ? 0 : B.ptr[B.nr];
@@ -1204,11 +1467,19 @@ int dupload_bsr(DistHandle* h, const HBsr& B, DBsr* D, std::string* err) {
   int rc;
   if ((rc = ddalloc(h, &D->ptr, B.nr + 1, err))) return rc;
   if ((rc = ddalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
-  if ((rc = ddalloc(h, &D->val, std::max<int64_t>(D->nb, 1), err))) return rc;
+  D->sym = sym && g_sym && blocks_symmetric(B);
+  const int per = D->sym ? 3 : 4;
+  if ((rc = ddalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
   HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), (B.nr + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (D->nb) {
     HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+    if (D->sym) {
+      std::vector<double> v3;
+      pack_sym(B, &v3);
+      HIPCHK(hipMemcpy(D->val, v3.data(), D->nb * 3 * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+      HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
+    }
   }
   return MAMG_OK;
 }
@@ -1253,6 +1524,7 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
                              nullptr, D.r, 0)));
   ops->push_back(wrap(bsr_op(D.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, D.r, 0, nullptr, nullptr, 0,
                              nullptr, C.b, 0)));
+  ops->back().op.remap = 1;
   if (!D.replicated) {
     DOp d;
     d.cls = C_COMM;
@@ -1346,6 +1618,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   h->rank = rank;
   h->nranks = nranks;
   h->device = p.device;
+  read_knobs();
   HIPCHK(hipSetDevice(p.device));
   if (comm_id) {                         // RCCL communicator; NULL = virtual (tests)
     ncclUniqueId uid;
@@ -1374,7 +1647,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else {
-      if ((rc = dupload_bsr(h.get(), P.A, &D.A, err))) return rc;
+      if ((rc = dupload_bsr(h.get(), P.A, &D.A, err, true))) return rc;
       if ((rc = dupload_bsr(h.get(), P.P, &D.P, err))) return rc;
       if ((rc = dupload_bsr(h.get(), P.Rp, &D.R, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.W, D.nloc, err))) return rc;

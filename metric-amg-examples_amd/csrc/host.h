@@ -80,6 +80,19 @@ bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk);
 // rows of P then rows of Q (same nr): M.ptr has 2 nr + 1 entries, row I of P in
 // [ptr[2I], ptr[2I+1]), row I of Q in [ptr[2I+1], ptr[2I+2])
 void merge_bsr_rows(const HBsr& P, const HBsr& Q, HBsr* M);
+// sliced-ELL (slice height C) copy of a plain (ptr nr + 1) or merged (2 nr + 1)
+// BSR2 matrix: block j of row I at soff[I / C] + C j + I % C; meta[I] = row
+// length | (first-part length << 16); sym: diagonal pairs (2 per slot) then
+// off-diagonals (1 per slot, at 2 nbs), else 4 doubles per slot; padding = 0
+struct HSell {
+  int64_t nr = 0, nbs = 0;
+  std::vector<int64_t> soff;
+  std::vector<int32_t> meta;
+  std::vector<int32_t> col;
+  std::vector<double> val;
+  std::vector<int32_t> perm;   // sigma > 1: row of each slot (rows sorted by length per window)
+};
+int to_sell(const HBsr& B, bool sym, int C, int sigma, HSell* S, std::string* err);
 
 // hash shared with the oracle (oracle/mamg_oracle.py:hash32)
 inline uint32_t hash32(uint64_t i, int level) {

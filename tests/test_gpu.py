@@ -180,6 +180,52 @@ def test_post_fusion_equals_unfused(lib_built, dim, n, g, kw):
         assert rel(Bf * r, Bu * r) < 1e-12
 
 
+@pytest.mark.parametrize('remap', ['0', '1', '2'])
+def test_symmetric_blocks_and_xcd_remap_bitwise(lib_built, monkeypatch, remap):
+    """The symmetric-block format (3 doubles per 2x2 block, chosen at upload
+    when every block of A_l has (0,1) == (1,0) bitwise -- the bidomain A_0)
+    and the XCD row order change only where data lives and which workgroup
+    computes a row: the apply is bitwise identical to the plain layout."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    outs = []
+    for sym in ('1', '0'):
+        monkeypatch.setenv('MAMG_SYM_BLOCKS', sym)
+        monkeypatch.setenv('MAMG_XCD_REMAP', remap if sym == '1' else '0')
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        outs.append(B * r)
+        B.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (3, 16, 1e10, dict()),
+                                        (2, 64, 1e3, dict(maxit=2, presmooth_iter=2, postsmooth_iter=2)),
+                                        (3, 16, 1e4, dict(cycle_type='W')),
+                                        (3, 8, 1e2, dict(post_fusion=0))])
+def test_sell_layout_matches_oracle(lib_built, monkeypatch, dim, n, g, kw):
+    """SELL-64 storage (one lane per node row; used for the level-0 operators
+    at benchmark size) forced onto every short-row level of small problems:
+    all epilogues, field-major x (maxit > 1, PCG), the fused post kernel."""
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    monkeypatch.setenv('MAMG_SELL_POST', '1')
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+    h = mo.setup(A, mo.Params(num_functions=2, **oracle_kw(kw)), idofs=s.idofs)
+    tol = APPLY_TOL if g < 1e8 else 1e-8
+    for seed in (1234, 5):
+        r = mo.seeded_rhs(s.N, seed)
+        assert rel(B * r, h.apply(r)) < tol
+    b = mo.seeded_rhs(s.N)
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)   # device PCG (A_0 SpMV)
+    solver * b
+    ref = mo.pcg(A, h, b, 1e-8, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+
+
 def test_bsr2_spmv_and_pcg_field_major(lib_built):
     import torch
     M = _mamg()
