@@ -126,6 +126,13 @@ __device__ __forceinline__ dv4 blk(const double* __restrict__ v, const double* _
   return reinterpret_cast<const dv4*>(v)[k];
 }
 
+// x(node c) as a pair: node-interleaved (one 16-byte load) or field-major
+template <bool XFM>
+__device__ __forceinline__ double2 xget(const double* x, int64_t xs, int32_t c) {
+  if (XFM) return double2{x[c], x[xs + c]};
+  return reinterpret_cast<const double2*>(x)[c];
+}
+
 template <int VL, int EPI, bool XFM, bool SYM, int TAG>
 __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
@@ -137,36 +144,22 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
   const double* offd = SYM ? bval + 2 * bptr[nr] : nullptr;
   double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
   if (node < nr) {
+    // chunks of 2 VL blocks, branch-free: every lane issues both loads of a
+    // chunk at once (index clamped into the row, contribution selected away),
+    // so a row costs one load -> gather chain per chunk instead of a loop
+    // chain followed by a divergent tail chain
     const int64_t p0 = bptr[node], p1 = bptr[node + 1];
-    int64_t k = p0 + lane;
-    for (; k + VL < p1; k += 2 * VL) {
-      const int32_t c0 = bcol[k], c1 = bcol[k + VL];
-      const dv4 v0 = blk<SYM>(bval, offd, k), v1 = blk<SYM>(bval, offd, k + VL);
-      double a0, a1, e0, e1;
-      if (XFM) {
-        a0 = x[c0]; a1 = x[xs + c0]; e0 = x[c1]; e1 = x[xs + c1];
-      } else {
-        const double2 a = reinterpret_cast<const double2*>(x)[c0];
-        const double2 e = reinterpret_cast<const double2*>(x)[c1];
-        a0 = a.x; a1 = a.y; e0 = e.x; e1 = e.y;
-      }
-      s0 += v0.x * a0; s0 += v0.y * a1;
-      s1 += v0.z * a0; s1 += v0.w * a1;
-      t0 += v1.x * e0; t0 += v1.y * e1;
-      t1 += v1.z * e0; t1 += v1.w * e1;
-    }
-    if (k < p1) {
-      const int32_t c0 = bcol[k];
-      const dv4 v0 = blk<SYM>(bval, offd, k);
-      double a0, a1;
-      if (XFM) {
-        a0 = x[c0]; a1 = x[xs + c0];
-      } else {
-        const double2 a = reinterpret_cast<const double2*>(x)[c0];
-        a0 = a.x; a1 = a.y;
-      }
-      s0 += v0.x * a0; s0 += v0.y * a1;
-      s1 += v0.z * a0; s1 += v0.w * a1;
+    for (int64_t base = p0; base < p1; base += 2 * VL) {
+      const int64_t ka = base + lane, kb = ka + VL;
+      const bool ha = ka < p1, hb = kb < p1;
+      const int64_t la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
+      const int32_t c0 = bcol[la], c1 = bcol[lb];
+      const dv4 v0 = blk<SYM>(bval, offd, la), v1 = blk<SYM>(bval, offd, lb);
+      const double2 a = xget<XFM>(x, xs, c0), e = xget<XFM>(x, xs, c1);
+      s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
+      s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
+      t0 += hb ? v1.x * e.x + v1.y * e.y : 0.0;
+      t1 += hb ? v1.z * e.x + v1.w * e.y : 0.0;
     }
   }
   s0 += t0;
@@ -201,7 +194,9 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
 // A x2 = A x1 + (AP) e.  Row I of the merged matrix holds P's blocks in
 // [mptr[2I], mptr[2I+1]) then AP's in [mptr[2I+1], mptr[2I+2]): one contiguous
 // window per node, both sums gathered from the same coarse vector e.
-template <int VL, int TAG>
+// PRE: the row's epilogue operands (x1, r1, W) are loaded by lane 0 before
+// the block loop, so their latency overlaps the loop instead of following it
+template <int VL, bool PRE, int TAG>
 __global__ __launch_bounds__(256) void bsr2_post_kernel(
     int64_t nr, const int64_t* __restrict__ mptr, const int32_t* __restrict__ bcol,
     const double* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
@@ -210,26 +205,27 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
   const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
   const double2* e2 = reinterpret_cast<const double2*>(e);
   double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
-  if (node < nr) {
+  dv4 w = {0.0, 0.0, 0.0, 0.0};
+  double2 xx = {0.0, 0.0}, rr = {0.0, 0.0};
+  if (PRE && node < nr && lane == 0) {
+    w = W[node];
+    xx = reinterpret_cast<const double2*>(x1)[node];
+    rr = reinterpret_cast<const double2*>(r1)[node];
+  }
+  if (node < nr) {   // branch-free chunks of 2 VL blocks (see bsr2_kernel)
     const int64_t k0 = mptr[2 * node], km = mptr[2 * node + 1], k1 = mptr[2 * node + 2];
-    int64_t k = k0 + lane;
-    for (; k + VL < k1; k += 2 * VL) {
-      const int32_t c0 = bcol[k], c1 = bcol[k + VL];
-      const dv4 v0 = blk<false>(bval, nullptr, k), v1 = blk<false>(bval, nullptr, k + VL);
+    for (int64_t base = k0; base < k1; base += 2 * VL) {
+      const int64_t ka = base + lane, kb = ka + VL;
+      const bool ha = ka < k1, hb = kb < k1;
+      const int64_t la = ha ? ka : k1 - 1, lb = hb ? kb : k1 - 1;
+      const int32_t c0 = bcol[la], c1 = bcol[lb];
+      const dv4 v0 = blk<false>(bval, nullptr, la), v1 = blk<false>(bval, nullptr, lb);
       const double2 a = e2[c0], b = e2[c1];
-      const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
-      const double w0 = v1.x * b.x + v1.y * b.y, w1 = v1.z * b.x + v1.w * b.y;
-      const bool pa = k < km, pb = k + VL < km;
+      const double u0 = ha ? v0.x * a.x + v0.y * a.y : 0.0, u1 = ha ? v0.z * a.x + v0.w * a.y : 0.0;
+      const double w0 = hb ? v1.x * b.x + v1.y * b.y : 0.0, w1 = hb ? v1.z * b.x + v1.w * b.y : 0.0;
+      const bool pa = ka < km, pb = kb < km;
       p0 += pa ? u0 : 0.0; p1 += pa ? u1 : 0.0; q0 += pa ? 0.0 : u0; q1 += pa ? 0.0 : u1;
       p0 += pb ? w0 : 0.0; p1 += pb ? w1 : 0.0; q0 += pb ? 0.0 : w0; q1 += pb ? 0.0 : w1;
-    }
-    if (k < k1) {
-      const int32_t c0 = bcol[k];
-      const dv4 v0 = blk<false>(bval, nullptr, k);
-      const double2 a = e2[c0];
-      const double u0 = v0.x * a.x + v0.y * a.y, u1 = v0.z * a.x + v0.w * a.y;
-      const bool pa = k < km;
-      p0 += pa ? u0 : 0.0; p1 += pa ? u1 : 0.0; q0 += pa ? 0.0 : u0; q1 += pa ? 0.0 : u1;
     }
   }
 #pragma unroll
@@ -240,10 +236,14 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
     q1 += __shfl_xor(q1, off, VL);
   }
   if (node < nr && lane == 0) {
-    const dv4 w = W[node];
-    const double d0 = r1[2 * node] - q0, d1 = r1[2 * node + 1] - q1;
-    vset(out, os, node, 0, x1[2 * node] + p0 + (w.x * d0 + w.y * d1));
-    vset(out, os, node, 1, x1[2 * node + 1] + p1 + (w.z * d0 + w.w * d1));
+    if (!PRE) {
+      w = W[node];
+      xx = reinterpret_cast<const double2*>(x1)[node];
+      rr = reinterpret_cast<const double2*>(r1)[node];
+    }
+    const double d0 = rr.x - q0, d1 = rr.y - q1;
+    vset(out, os, node, 0, xx.x + p0 + (w.x * d0 + w.y * d1));
+    vset(out, os, node, 1, xx.y + p1 + (w.z * d0 + w.w * d1));
   }
 }
 
@@ -260,13 +260,7 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
 constexpr int SELL_C = 64;
 constexpr int SELL_U = 4;     // blocks in flight per lane
 
-template <bool XFM>
-__device__ __forceinline__ double2 xget(const double* x, int64_t xs, int32_t c) {
-  if (XFM) return double2{x[c], x[xs + c]};
-  return reinterpret_cast<const double2*>(x)[c];
-}
-
-template <int EPI, bool XFM, bool SYM, int TAG>
+template <int EPI, bool XFM, bool SYM, int U, bool PRE, int TAG>
 __global__ __launch_bounds__(256) void sell2_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
@@ -277,40 +271,49 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int len = meta[node] & 0xffff;
   int64_t k = soff[node / SELL_C] + (node & (SELL_C - 1));
+  // PRE: epilogue operands first (their latency overlaps the row loop)
+  double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
+  dv4 w = {0.0, 0.0, 0.0, 0.0};
+  auto epi_loads = [&]() {
+    if (EPI == EPI_RESID || EPI == EPI_BJAC) bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
+    if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
+    if (EPI == EPI_BJAC) w = W[node];
+  };
+  if (PRE) epi_loads();
   double s0 = 0.0, s1 = 0.0;
-  int j = 0;
-  for (; j + SELL_U <= len; j += SELL_U, k += SELL_U * SELL_C) {
-    int32_t c[SELL_U];
-    dv4 v[SELL_U];
-    double2 a[SELL_U];
+  // chunks of U blocks, branch-free (slot clamped into the row, contribution
+  // selected away): one load -> gather chain per chunk
+  for (int j = 0; j < len; j += U) {
+    int32_t c[U];
+    dv4 v[U];
+    double2 a[U];
 #pragma unroll
-    for (int u = 0; u < SELL_U; ++u) { c[u] = bcol[k + u * SELL_C]; v[u] = blk<SYM>(bval, offd, k + u * SELL_C); }
+    for (int u = 0; u < U; ++u) {
+      const int64_t kk = k + (int64_t)SELL_C * (j + u < len ? j + u : len - 1);
+      c[u] = bcol[kk];
+      v[u] = blk<SYM>(bval, offd, kk);
+    }
 #pragma unroll
-    for (int u = 0; u < SELL_U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+    for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
 #pragma unroll
-    for (int u = 0; u < SELL_U; ++u) {
-      s0 += v[u].x * a[u].x; s0 += v[u].y * a[u].y;
-      s1 += v[u].z * a[u].x; s1 += v[u].w * a[u].y;
+    for (int u = 0; u < U; ++u) {
+      const bool ok = j + u < len;
+      s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+      s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
     }
   }
-  for (; j < len; ++j, k += SELL_C) {
-    const dv4 v = blk<SYM>(bval, offd, k);
-    const double2 a = xget<XFM>(x, xs, bcol[k]);
-    s0 += v.x * a.x; s0 += v.y * a.y;
-    s1 += v.z * a.x; s1 += v.w * a.y;
-  }
+  if (!PRE) epi_loads();
   double o0, o1;
   if (EPI == EPI_Y) {
     o0 = s0; o1 = s1;
   } else if (EPI == EPI_YADD) {
-    o0 = y[2 * node] + s0; o1 = y[2 * node + 1] + s1;
+    o0 = yy.x + s0; o1 = yy.y + s1;
   } else if (EPI == EPI_RESID) {
-    o0 = vget(b, bs, node, 0) - s0; o1 = vget(b, bs, node, 1) - s1;
+    o0 = bb.x - s0; o1 = bb.y - s1;
   } else {  // EPI_BJAC
-    const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
-    const dv4 w = W[node];
-    o0 = y[2 * node] + (w.x * r0 + w.y * r1);
-    o1 = y[2 * node + 1] + (w.z * r0 + w.w * r1);
+    const double r0 = bb.x - s0, r1 = bb.y - s1;
+    o0 = yy.x + (w.x * r0 + w.y * r1);
+    o1 = yy.y + (w.z * r0 + w.w * r1);
   }
   vset(out, os, node, 0, o0);
   vset(out, os, node, 1, o1);
@@ -473,13 +476,26 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_SELL       0 disables the SELL-64 storage (default 1), used for
 //                   matrices with >= MAMG_SELL_MIN_ROWS (2^20) node rows
 //   MAMG_SELL_POST  1: SELL-64-sigma for the merged [P | AP] too (default 0)
+//   MAMG_PREFETCH   0: fused post kernel loads its epilogue operands last
+//   MAMG_SELL_U     SELL blocks per chunk (4, 8, 16) / MAMG_SELL_PRE epilogue
+//                   loads before the row loop (level-0 SELL kernels)
 int g_remap = 1;
 int g_post_lanes = 0;
 int g_sym = 1;
 int g_sell = 1;
 int g_sell_post = 0;
+int g_sell_u = 8;
+int g_sell_pre = 0;
+int g_prefetch = 1;
 int64_t g_sell_min_rows = 1 << 20;
 void read_knobs() {
+  const char* su = std::getenv("MAMG_SELL_U");
+  g_sell_u = su ? std::atoi(su) : 8;
+  if (g_sell_u != 4 && g_sell_u != 8 && g_sell_u != 16) g_sell_u = 8;
+  su = std::getenv("MAMG_SELL_PRE");
+  g_sell_pre = su ? std::atoi(su) : 0;
+  const char* pf = std::getenv("MAMG_PREFETCH");
+  g_prefetch = pf ? std::atoi(pf) : 1;
   const char* sp = std::getenv("MAMG_SELL_POST");
   g_sell_post = sp ? std::atoi(sp) : 0;
   const char* s = std::getenv("MAMG_SELL");
@@ -981,19 +997,34 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
 #undef BSR_ARGS
 }
 
-template <bool XFM, bool SYM, int TAG>
-void launch_sell_x(const Op& o, hipStream_t s) {
+template <bool XFM, bool SYM, int U, bool PRE, int TAG>
+void launch_sell_u(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
   switch (o.epi) {
-    case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    default: sell2_kernel<EPI_BJAC, XFM, SYM, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    default: sell2_kernel<EPI_BJAC, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
   }
 #undef SELL_ARGS
+}
+
+template <bool XFM, bool SYM, int TAG>
+void launch_sell_x(const Op& o, hipStream_t s) {
+  if (TAG == 0) {   // the level-0 operator: tuning variants (bench/variants.py)
+    switch (g_sell_u * 2 + (g_sell_pre ? 1 : 0)) {
+      case 8: launch_sell_u<XFM, SYM, 4, false, TAG>(o, s); return;
+      case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
+      case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
+      case 17: launch_sell_u<XFM, SYM, 8, true, TAG>(o, s); return;
+      case 32: launch_sell_u<XFM, SYM, 16, false, TAG>(o, s); return;
+      default: launch_sell_u<XFM, SYM, 16, true, TAG>(o, s); return;
+    }
+  }
+  launch_sell_u<XFM, SYM, 8, false, TAG>(o, s);
 }
 
 template <int TAG>
@@ -1019,8 +1050,12 @@ void launch_post_vl(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-  bsr2_post_kernel<VL, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
-                                              o.out, o.os, remap_of(o));
+  if (g_prefetch)
+    bsr2_post_kernel<VL, true, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
+                                                      o.out, o.os, remap_of(o));
+  else
+    bsr2_post_kernel<VL, false, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
+                                                       o.out, o.os, remap_of(o));
 }
 
 template <int TAG>
