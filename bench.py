@@ -10,8 +10,9 @@ A step = one preconditioner application z = B r (one V-cycle from x0 = 0) on
 a resident seeded r (uniform(-1,1), seed 1234) -- the unit of work of the
 reference's hot loop (`BB * r` inside ConjGrad, src/bidomain_3d.py:149-150).
 The timed region runs K applies kernel by kernel on one stream with HIP
-events around the dominant kernel (level-0 residual SpMV) of every step,
-bracketed by barrier + synchronize.  value = K / max-over-ranks wall time
+events around the two dominant kernels of every step (level-0 residual SpMV
+and the fused prolongation + post-smoothing kernel), bracketed by barrier +
+synchronize; `roofline` is the one with the larger time.  value = K / max-over-ranks wall time
 (applies of the whole problem per second).
 N = 1: the whole hierarchy on one GPU (BSR2 layout, hipGraph replay also
 reported).  N > 1: the same problem row-partitioned over N GPUs (one process
@@ -143,8 +144,6 @@ def main():
     ms_per_step = 1e3 * wall / args.steps
     value = args.steps / wall
     apply_bytes = allsum(B.apply_bytes)
-    dom_bytes = cbytes[0]                   # level-0 residual: one launch per apply (per rank)
-    dom_ms = kms[0]
 
     graph_ms = None
     if world == 1:                          # hipGraph replay of the same work
@@ -194,18 +193,38 @@ def main():
                          'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, args.nrefs, err)}
         del ch, lv
 
-    traffic = None
+    # measured HBM bytes per launch of the two dominant kernels (rocprofv3
+    # FETCH_SIZE + WRITE_SIZE, calibrated; profiles/traffic.json, written by
+    # scripts/traffic.py from the committed PMC summaries of this config)
+    traffic = {}
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
     if os.path.exists(tpath) and world == 1:
         try:
             tj = json.load(open(tpath))
             if tj.get('N') == sysm.N and tj.get('layout') == layout:
-                traffic = tj.get('dominant_bytes_per_launch')
-        except Exception:
-            traffic = None
+                traffic = tj.get('kernels', {})
+        except (OSError, ValueError):
+            traffic = {}
 
-    achieved = dom_bytes / 1e9 / (dom_ms * 1e-3) if dom_ms > 0 else None
-    kname = 'bsr2_kernel' if layout.startswith('bsr2') else 'csr_kernel'
+    fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
+    if layout == 'csr':
+        names = ('csr_kernel<*,RESID,0>', 'csr_kernel<*,BJAC/JACOBI,0>')
+    else:
+        names = ('%s<RESID,...,0>' % ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel'),
+                 'bsr2_post_kernel<8,...,0>' if fmt0.get('post_fused', True) else 'bsr2_kernel<*,BJAC,...,0>')
+    descr = ('level-0 residual r = b - A0 x', 'level-0 prolongation + post-smoothing '
+             'z = x1 + P e + W (r1 - (AP) e)')
+    rooflines = []
+    for c, key in ((0, 'L0_resid'), (1, 'L0_smooth_spmv')):
+        if kms[c] <= 0:
+            continue
+        ach = cbytes[c] / 1e9 / (kms[c] * 1e-3)
+        rooflines.append({
+            'bound': 'hbm', 'kernel': '%s (%s)%s' % (descr[c], names[c], '' if world == 1 else ', rank 0 slice'),
+            'achieved': round(ach, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+            'frac': round(ach / HBM_PEAK_GBPS, 4), 'traffic': traffic.get(key),
+            'bytes_per_launch': cbytes[c], 'ms_per_launch': round(kms[c], 4)})
+    roofline = max(rooflines, key=lambda r: r['ms_per_launch']) if rooflines else None
     out = {
         'metric': METRIC,
         'value': round(value, 3),
@@ -229,16 +248,9 @@ def main():
         'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),
         'apply_GB_alg': round(apply_bytes / 1e9, 4),
         'graph_ms_per_step': graph_ms,
-        'roofline': {
-            'bound': 'hbm',
-            'kernel': 'level-0 residual r = b - A0 x (%s<*,RESID,...,0>)%s'
-                      % (kname, '' if world == 1 else ', rank 0 slice'),
-            'achieved': round(achieved, 1) if achieved else None,
-            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
-            'frac': round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-            'traffic': traffic,
-            'bytes_per_launch': dom_bytes, 'ms_per_launch': round(dom_ms, 4),
-        },
+        'roofline': roofline,
+        'roofline_kernels': rooflines,
+        'level0_format': fmt0,
         'cpu_baseline': cpu,
         'setup_s': {'generate': round(t_gen, 2), 'host_setup': round(t_setup, 2),
                     'upload': round(t_upload, 2)},

@@ -1,8 +1,7 @@
 // spmv_micro.hip -- kernel-variant microbenchmark for the level-0 operator
 // (bidomain 3-D, nrefs=6: N = 34M, nnz = 1.0e9).  Times CSR and 2x2-BSR SpMV
 // variants with HIP events and checks each against the CSR result.
-// Build: hipcc -O3 --offload-arch=gfx950 -I../include spmv_micro.hip
-//        -L../metric-amg-examples_amd -lmamg -Wl,-rpath,...
+// Build: make -C bench
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -158,6 +157,18 @@ __global__ __launch_bounds__(256) void calib_read_k(int64_t n, const T* __restri
   if (s == 1234.5) out[blockIdx.x] = s;   // practically never: keeps the loads live
 }
 
+// WRITE_SIZE calibration: stream-write n elements of T (exactly n*sizeof(T)
+// bytes); HALF: only the first 64 B of every 128 B line (partial-line writes,
+// the pattern of a field-major epilogue store) -> n*sizeof(T)/2 bytes
+template <class T, bool HALF>
+__global__ __launch_bounds__(256) void calib_write_k(int64_t n, T* __restrict__ a) {
+  constexpr int64_t per_half_line = 64 / sizeof(T);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (HALF && ((i / per_half_line) & 1)) continue;
+    a[i] = T{};
+  }
+}
+
 // plain copy for the achievable-bandwidth reference
 __global__ __launch_bounds__(256) void copy_k(int64_t n4, const double4* __restrict__ a,
                                               double4* __restrict__ b) {
@@ -197,6 +208,14 @@ int calib(int reps) {
     printf("calib %-8s (%2d B/lane): %.3f ms %.0f GB/s\n", name, (int)sizeof(T), ms, bytes / ms / 1e6); \
   }
   CAL(int, "int32") CAL(double, "f64") CAL(double2, "f64x2") CAL(dv4, "f64x4")
+#define CALW(T, H, name)                                                                   \
+  {                                                                                        \
+    const int64_t n = bytes / (int64_t)sizeof(T);                                          \
+    float ms = timeit([&] { hipLaunchKernelGGL((calib_write_k<T, H>), dim3(256 * 16), dim3(256), 0, 0, n, (T*)a); }, reps); \
+    printf("calibw %-8s (%2d B/lane, %s): writes %ld bytes, %.3f ms\n", name, (int)sizeof(T),   \
+           H ? "half lines" : "full lines", (long)(H ? bytes / 2 : bytes), ms);              \
+  }
+  CALW(double, false, "f64") CALW(double2, false, "f64x2") CALW(double, true, "f64") CALW(double2, true, "f64x2")
   CK(hipFree(a));
   return 0;
 }

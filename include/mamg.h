@@ -211,6 +211,12 @@ int mamg_num_levels(const mamg_handle* h);
 /* Device layout chosen at upload: 0 = CSR (general), 1 = BSR2 (nodal
  * hierarchy with num_functions == 2 and node-block smoothers). */
 int mamg_device_layout(const mamg_handle* h);
+/* Storage of level l's operator on the device (BSR2 layout), bit flags:
+ * MAMG_FMT_SELL (sliced-ELL, one lane per node row), MAMG_FMT_SYM (3 doubles
+ * per symmetric 2x2 block), MAMG_FMT_POST_FUSED (prolongation fused with the
+ * first post sweep through a stored [P | AP]).  Returns flags >= 0, or < 0. */
+enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4 };
+int mamg_level_format(const mamg_handle* h, int level);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */
 int mamg_apply_bytes(const mamg_handle* h, double* total_bytes);
@@ -240,8 +246,9 @@ int mamg_pcg_device(mamg_handle* h, const double* d_b, double* d_x, double tol,
  * kernel, no graph) on `stream`, timed with HIP events recorded on that
  * stream.  *ms_per_apply = mean wall time per apply.  kernel_ms[16] (if
  * non-NULL) = mean ms per apply per kernel class:
- * mode 0 instruments only class 0 (the level-0 residual SpMV, the dominant
- * kernel), mode 1 instruments every launch.  class_bytes[16] (if non-NULL) =
+ * mode 0 instruments only classes 0 and 1 (the level-0 residual SpMV and the
+ * level-0 post-smoothing / fused prolongation kernel, the two dominant
+ * kernels), mode 1 instruments every launch.  class_bytes[16] (if non-NULL) =
  * algorithmic HBM bytes per apply of each class. */
 int mamg_time_apply(mamg_handle* h, const double* d_r, double* d_z, int reps,
                     int mode, double* ms_per_apply, double* kernel_ms,

@@ -92,6 +92,7 @@ SIGNATURES = {
     'mamg_nrows': (C.c_int64, [VP]),
     'mamg_num_levels': (C.c_int, [VP]),
     'mamg_device_layout': (C.c_int, [VP]),
+    'mamg_level_format': (C.c_int, [VP, C.c_int]),
     'mamg_apply_bytes': (C.c_int, [VP, P_F64]),
     'mamg_apply': (C.c_int, [VP, P_F64, P_F64]),
     'mamg_apply_device': (C.c_int, [VP, VP, VP, VP]),

@@ -141,6 +141,13 @@ class MetricAMG:
         """device layout: 'csr' (general) or 'bsr2' (nodal, 2 fields)."""
         return ('csr', 'bsr2')[self._L.mamg_device_layout(self._h)]
 
+    def level_format(self, level: int) -> dict:
+        """Device storage of level ``level`` (BSR2 layout): sliced-ELL rows,
+        symmetric 2x2 blocks, fused [P | AP] post-smoothing."""
+        f = self._L.mamg_level_format(self._h, int(level))
+        _lib.check(min(f, 0))
+        return {'sell': bool(f & 1), 'sym': bool(f & 2), 'post_fused': bool(f & 4)}
+
     @property
     def apply_bytes(self) -> float:
         b = C.c_double()

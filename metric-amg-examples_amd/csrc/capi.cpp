@@ -367,6 +367,13 @@ void mamg_destroy(mamg_handle* h) {
 int64_t mamg_nrows(const mamg_handle* h) { return h ? mamg::dev_nrows(h->d) : (int64_t)MAMG_ERR_ARG; }
 int mamg_num_levels(const mamg_handle* h) { return h ? mamg::dev_num_levels(h->d) : MAMG_ERR_ARG; }
 int mamg_device_layout(const mamg_handle* h) { return h ? mamg::dev_layout(h->d) : MAMG_ERR_ARG; }
+int mamg_level_format(const mamg_handle* h, int level) {
+  if (!h || level < 0 || level >= mamg::dev_num_levels(h->d)) {
+    mamg::set_error("mamg_level_format: bad handle or level");
+    return MAMG_ERR_ARG;
+  }
+  return mamg::dev_level_format(h->d, level);
+}
 
 int mamg_apply_bytes(const mamg_handle* h, double* total) {
   if (!h || !total) { set_error("null argument"); return MAMG_ERR_ARG; }

@@ -1252,6 +1252,11 @@ int64_t dev_nrows(const DeviceHandle* h) { return h->L[0].n; }
 int dev_num_levels(const DeviceHandle* h) { return (int)h->L.size(); }
 double dev_apply_bytes(const DeviceHandle* h) { return h->apply_bytes; }
 int dev_layout(const DeviceHandle* h) { return h->bsr ? 1 : 0; }
+int dev_level_format(const DeviceHandle* h, int level) {
+  const DLevel& L = h->L[level];
+  return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) |
+         (L.PAb.nr > 0 ? MAMG_FMT_POST_FUSED : 0);
+}
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
@@ -1364,7 +1369,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
   // events: per rep, per instrumented op, one (start, end) pair
   std::vector<int> inst;
   for (size_t k = 0; k < ops.size(); ++k)
-    if (mode == 1 || ops[k].cls == C_L0_RESID) inst.push_back((int)k);
+    if (mode == 1 || ops[k].cls == C_L0_RESID || ops[k].cls == C_L0_SMOOTH) inst.push_back((int)k);
   std::vector<hipEvent_t> ev(2 * inst.size() * (size_t)reps + 2);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventRecord(ev[0], s));
@@ -1750,7 +1755,7 @@ int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int
   if (reps <= 0) { *ms = 0.0; return MAMG_OK; }
   std::vector<int> inst;
   for (size_t k = 0; k < ops.size(); ++k)
-    if (mode == 1 || ops[k].cls == C_L0_RESID) inst.push_back((int)k);
+    if (mode == 1 || ops[k].cls == C_L0_RESID || ops[k].cls == C_L0_SMOOTH) inst.push_back((int)k);
   std::vector<hipEvent_t> ev(2 * inst.size() * (size_t)reps + 2);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventRecord(ev[0], s));
