@@ -198,7 +198,8 @@ int mamg_hier_dist_plan(const mamg_hier* h, int rank, int nranks, int64_t rep_no
   *out = nullptr;
   mamg_plan* p = new mamg_plan();
   std::string err;
-  int rc = mamg::build_dist_plan(h->H, h->H.A0, rank, nranks, rep_nodes, &p->P, &err);
+  int rc = mamg::build_dist_plan(h->H, h->H.A0, rank, nranks, rep_nodes, h->H.params.post_fusion != 0,
+                                 &p->P, &err);
   if (rc) { set_error(err); delete p; return rc; }
   *out = p;
   return MAMG_OK;

@@ -53,6 +53,7 @@ namespace {
 enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4 };
 
 typedef double dv4 __attribute__((ext_vector_type(4)));
+typedef double dv2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------
 // CSR kernels (general layout)
@@ -115,15 +116,23 @@ __device__ __forceinline__ int64_t row_block(int remap) {
 // or in the symmetric-block format (SYM) two aligned streams: the diagonal
 // pairs {(0,0), (1,1)} (16 B per block) then the off-diagonals (0,1) = (1,0)
 // (8 B per block) starting at v + 2 nb
-template <bool SYM>
+// NT: non-temporal (streaming) loads, so the matrix stream does not evict
+// the gathered vector from L2
+template <bool NT, class T>
+__device__ __forceinline__ T ldg(const T* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <bool SYM, bool NT = false>
 __device__ __forceinline__ dv4 blk(const double* __restrict__ v, const double* __restrict__ off,
                                    int64_t k) {
   if (SYM) {
-    const double2 d = reinterpret_cast<const double2*>(v)[k];
-    const double b = off[k];
+    const dv2 d = ldg<NT>(reinterpret_cast<const dv2*>(v) + k);
+    const double b = ldg<NT>(off + k);
     return dv4{d.x, b, b, d.y};
   }
-  return reinterpret_cast<const dv4*>(v)[k];
+  return ldg<NT>(reinterpret_cast<const dv4*>(v) + k);
 }
 
 // x(node c) as a pair: node-interleaved (one 16-byte load) or field-major
@@ -194,9 +203,9 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
 // A x2 = A x1 + (AP) e.  Row I of the merged matrix holds P's blocks in
 // [mptr[2I], mptr[2I+1]) then AP's in [mptr[2I+1], mptr[2I+2]): one contiguous
 // window per node, both sums gathered from the same coarse vector e.
-// PRE: the row's epilogue operands (x1, r1, W) are loaded by lane 0 before
-// the block loop, so their latency overlaps the loop instead of following it
-template <int VL, bool PRE, int TAG>
+// The row's epilogue operands (x1, r1, W) are loaded by lane 0 before the
+// block loop, so their latency overlaps the loop instead of following it.
+template <int VL, bool NT, int TAG>
 __global__ __launch_bounds__(256) void bsr2_post_kernel(
     int64_t nr, const int64_t* __restrict__ mptr, const int32_t* __restrict__ bcol,
     const double* __restrict__ bval, const double* __restrict__ e, const double* __restrict__ x1,
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
   double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
   dv4 w = {0.0, 0.0, 0.0, 0.0};
   double2 xx = {0.0, 0.0}, rr = {0.0, 0.0};
-  if (PRE && node < nr && lane == 0) {
+  if (node < nr && lane == 0) {
     w = W[node];
     xx = reinterpret_cast<const double2*>(x1)[node];
     rr = reinterpret_cast<const double2*>(r1)[node];
@@ -218,8 +227,8 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
       const int64_t ka = base + lane, kb = ka + VL;
       const bool ha = ka < k1, hb = kb < k1;
       const int64_t la = ha ? ka : k1 - 1, lb = hb ? kb : k1 - 1;
-      const int32_t c0 = bcol[la], c1 = bcol[lb];
-      const dv4 v0 = blk<false>(bval, nullptr, la), v1 = blk<false>(bval, nullptr, lb);
+      const int32_t c0 = ldg<NT>(bcol + la), c1 = ldg<NT>(bcol + lb);
+      const dv4 v0 = blk<false, NT>(bval, nullptr, la), v1 = blk<false, NT>(bval, nullptr, lb);
       const double2 a = e2[c0], b = e2[c1];
       const double u0 = ha ? v0.x * a.x + v0.y * a.y : 0.0, u1 = ha ? v0.z * a.x + v0.w * a.y : 0.0;
       const double w0 = hb ? v1.x * b.x + v1.y * b.y : 0.0, w1 = hb ? v1.z * b.x + v1.w * b.y : 0.0;
@@ -236,11 +245,6 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
     q1 += __shfl_xor(q1, off, VL);
   }
   if (node < nr && lane == 0) {
-    if (!PRE) {
-      w = W[node];
-      xx = reinterpret_cast<const double2*>(x1)[node];
-      rr = reinterpret_cast<const double2*>(r1)[node];
-    }
     const double d0 = rr.x - q0, d1 = rr.y - q1;
     vset(out, os, node, 0, xx.x + p0 + (w.x * d0 + w.y * d1));
     vset(out, os, node, 1, xx.y + p1 + (w.z * d0 + w.w * d1));
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
 constexpr int SELL_C = 64;
 constexpr int SELL_U = 4;     // blocks in flight per lane
 
-template <int EPI, bool XFM, bool SYM, int U, bool PRE, int TAG>
+template <int EPI, bool XFM, bool SYM, int U, bool NT, int TAG>
 __global__ __launch_bounds__(256) void sell2_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
@@ -271,15 +275,6 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int len = meta[node] & 0xffff;
   int64_t k = soff[node / SELL_C] + (node & (SELL_C - 1));
-  // PRE: epilogue operands first (their latency overlaps the row loop)
-  double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
-  dv4 w = {0.0, 0.0, 0.0, 0.0};
-  auto epi_loads = [&]() {
-    if (EPI == EPI_RESID || EPI == EPI_BJAC) bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
-    if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
-    if (EPI == EPI_BJAC) w = W[node];
-  };
-  if (PRE) epi_loads();
   double s0 = 0.0, s1 = 0.0;
   // chunks of U blocks, branch-free (slot clamped into the row, contribution
   // selected away): one load -> gather chain per chunk
@@ -290,8 +285,8 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < len ? j + u : len - 1);
-      c[u] = bcol[kk];
-      v[u] = blk<SYM>(bval, offd, kk);
+      c[u] = ldg<NT>(bcol + kk);
+      v[u] = blk<SYM, NT>(bval, offd, kk);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
@@ -302,7 +297,12 @@ __global__ __launch_bounds__(256) void sell2_kernel(
       s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
     }
   }
-  if (!PRE) epi_loads();
+  // epilogue operands after the loop (measured: loading them first is slower)
+  double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
+  dv4 w = {0.0, 0.0, 0.0, 0.0};
+  if (EPI == EPI_RESID || EPI == EPI_BJAC) bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
+  if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
+  if (EPI == EPI_BJAC) w = W[node];
   double o0, o1;
   if (EPI == EPI_Y) {
     o0 = s0; o1 = s1;
@@ -476,26 +476,22 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_SELL       0 disables the SELL-64 storage (default 1), used for
 //                   matrices with >= MAMG_SELL_MIN_ROWS (2^20) node rows
 //   MAMG_SELL_POST  1: SELL-64-sigma for the merged [P | AP] too (default 0)
-//   MAMG_PREFETCH   0: fused post kernel loads its epilogue operands last
-//   MAMG_SELL_U     SELL blocks per chunk (4, 8, 16) / MAMG_SELL_PRE epilogue
-//                   loads before the row loop (level-0 SELL kernels)
+//   MAMG_SELL_U     SELL blocks per chunk (4, 8, 16), level-0 SELL kernels
+//   MAMG_NT         1: non-temporal matrix loads in the level-0 kernels
 int g_remap = 1;
 int g_post_lanes = 0;
 int g_sym = 1;
 int g_sell = 1;
 int g_sell_post = 0;
 int g_sell_u = 8;
-int g_sell_pre = 0;
-int g_prefetch = 1;
+int g_nt = 0;
 int64_t g_sell_min_rows = 1 << 20;
 void read_knobs() {
   const char* su = std::getenv("MAMG_SELL_U");
   g_sell_u = su ? std::atoi(su) : 8;
   if (g_sell_u != 4 && g_sell_u != 8 && g_sell_u != 16) g_sell_u = 8;
-  su = std::getenv("MAMG_SELL_PRE");
-  g_sell_pre = su ? std::atoi(su) : 0;
-  const char* pf = std::getenv("MAMG_PREFETCH");
-  g_prefetch = pf ? std::atoi(pf) : 1;
+  su = std::getenv("MAMG_NT");
+  g_nt = su ? std::atoi(su) : 0;
   const char* sp = std::getenv("MAMG_SELL_POST");
   g_sell_post = sp ? std::atoi(sp) : 0;
   const char* s = std::getenv("MAMG_SELL");
@@ -636,8 +632,9 @@ struct DeviceHandle {
 
 namespace {
 
-template <class T>
-int dalloc(DeviceHandle* h, T** p, int64_t count, std::string* err) {
+// device allocation owned by a handle (single-GPU or multi-GPU: both keep `allocs`)
+template <class HT, class T>
+int dalloc(HT* h, T** p, int64_t count, std::string* err) {
   *p = nullptr;
   if (count <= 0) return MAMG_OK;
   void* q = nullptr;
@@ -683,7 +680,8 @@ int pick_lanes_bsr(int64_t nr, int64_t nb) {
 }
 
 // SELL-64 copy of a BSR2 matrix (host packing: convert.cpp to_sell)
-int upload_sell(DeviceHandle* h, const HBsr& B, DBsr* D, std::string* err) {
+template <class HT>
+int upload_sell(HT* h, const HBsr& B, DBsr* D, std::string* err) {
   HSell S;
   const bool merged = (int64_t)B.ptr.size() == 2 * B.nr + 1;
   int rc = to_sell(B, D->sym, SELL_C, merged ? SELL_SIGMA : 1, &S, err);
@@ -710,7 +708,8 @@ int upload_sell(DeviceHandle* h, const HBsr& B, DBsr* D, std::string* err) {
 }
 
 // (also uploads a merged [P | AP] matrix: then B.ptr has 2 nr + 1 entries)
-int upload_bsr(DeviceHandle* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
+template <class HT>
+int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
                bool sym = false) {
   const int64_t np = (int64_t)B.ptr.size();
   D->nr = B.nr;
@@ -790,12 +789,11 @@ Op bsr_op(const DBsr& M, int epi, int cls, int tag, const double* x, int64_t xs,
 }
 
 // merged [P | AP] blocks + 2 nr + 1 pointers, e gathered once, x1 r1 W out
-Op post_op(const DLevel& L, int cls, int tag, const double* e, const double* x1, double* out,
-           int64_t os) {
-  const DBsr& M = L.PAb;
+Op post_op(const DBsr& M, const double* r1, const dv4* W, int cls, int tag, const double* e,
+           const double* x1, double* out, int64_t os) {
   Op o;
   o.kind = OP_POST; o.cls = cls; o.tag = tag; o.Mb = &M; o.n = M.nr;
-  o.x = e; o.y = x1; o.b = L.r; o.W = L.Wd; o.out = out; o.os = os;
+  o.x = e; o.y = x1; o.b = r1; o.W = W; o.out = out; o.os = os;
   o.bytes = 36.0 * M.nb + index_bytes(M, 2 * M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr * 3 + 32.0 * M.nr;
   return o;
 }
@@ -903,7 +901,7 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   int s0 = 0;
   if (L.PAb.nr > 0 && p.postsmooth_iter >= 1) {   // prolongation + first post sweep
     const bool last = p.postsmooth_iter == 1;
-    ops->push_back(post_op(L, clsS, tagA, C.x, X, last ? xout : X2, last ? os : 0));
+    ops->push_back(post_op(L.PAb, L.r, L.Wd, clsS, tagA, C.x, X, last ? xout : X2, last ? os : 0));
     if (!last) std::swap(X, X2);
     s0 = 1;
   } else {
@@ -997,17 +995,17 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
 #undef BSR_ARGS
 }
 
-template <bool XFM, bool SYM, int U, bool PRE, int TAG>
+template <bool XFM, bool SYM, int U, bool NT, int TAG>
 void launch_sell_u(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
   switch (o.epi) {
-    case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
-    default: sell2_kernel<EPI_BJAC, XFM, SYM, U, PRE, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    default: sell2_kernel<EPI_BJAC, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
   }
 #undef SELL_ARGS
 }
@@ -1015,7 +1013,7 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   if (TAG == 0) {   // the level-0 operator: tuning variants (bench/variants.py)
-    switch (g_sell_u * 2 + (g_sell_pre ? 1 : 0)) {
+    switch (g_sell_u * 2 + (g_nt ? 1 : 0)) {
       case 8: launch_sell_u<XFM, SYM, 4, false, TAG>(o, s); return;
       case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
       case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
@@ -1050,7 +1048,7 @@ void launch_post_vl(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-  if (g_prefetch)
+  if (g_nt && TAG == 0)
     bsr2_post_kernel<VL, true, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
                                                       o.out, o.os, remap_of(o));
   else
@@ -1449,6 +1447,7 @@ struct DDLevel {
   int64_t nv = 0, nloc = 0, ng = 0;
   bool replicated = false, coarsest = false;
   DBsr A, P, R;
+  DBsr PA;                 // post fusion: merged [P_loc | AP_loc]
   dv4* W = nullptr;
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
@@ -1499,30 +1498,6 @@ int ddalloc(DistHandle* h, T** p, int64_t count, std::string* err) {
   return MAMG_OK;
 }
 
-int dupload_bsr(DistHandle* h, const HBsr& B, DBsr* D, std::string* err, bool sym = false) {
-  D->nr = B.nr;
-  D->nc = B.nc;
-  D->nb = B.ptr.empty() ? 0 : B.ptr[B.nr];
-  D->lanes = pick_lanes_bsr(B.nr, D->nb);
-  int rc;
-  if ((rc = ddalloc(h, &D->ptr, B.nr + 1, err))) return rc;
-  if ((rc = ddalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
-  D->sym = sym && g_sym && blocks_symmetric(B);
-  const int per = D->sym ? 3 : 4;
-  if ((rc = ddalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
-  HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), (B.nr + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if (D->nb) {
-    HIPCHK(hipMemcpy(D->col, B.col.data(), D->nb * sizeof(int32_t), hipMemcpyHostToDevice));
-    if (D->sym) {
-      std::vector<double> v3;
-      pack_sym(B, &v3);
-      HIPCHK(hipMemcpy(D->val, v3.data(), D->nb * 3 * sizeof(double), hipMemcpyHostToDevice));
-    } else {
-      HIPCHK(hipMemcpy(D->val, B.val.data(), D->nb * 4 * sizeof(double), hipMemcpyHostToDevice));
-    }
-  }
-  return MAMG_OK;
-}
 
 DOp wrap(const Op& o) {
   DOp d;
@@ -1579,6 +1554,10 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   }
   dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
   if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  if (D.PA.nr > 0) {   // fused: xout = X + P e + W (r - AP e), all operands local
+    ops->push_back(wrap(post_op(D.PA, D.r, D.W, l0 ? C_L0_SMOOTH : C_COARSE, tagA, C.x, X, xout, os)));
+    return;
+  }
   ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
                              nullptr, X, 0)));
   if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
@@ -1651,7 +1630,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     return MAMG_ERR_UNSUPPORTED;
   }
   DistPlan plan;
-  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, &plan, err);
+  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err);
   if (rc) return rc;
   std::unique_ptr<DistHandle> h(new DistHandle());
   h->p = p;
@@ -1687,9 +1666,13 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else {
-      if ((rc = dupload_bsr(h.get(), P.A, &D.A, err, true))) return rc;
-      if ((rc = dupload_bsr(h.get(), P.P, &D.P, err))) return rc;
-      if ((rc = dupload_bsr(h.get(), P.Rp, &D.R, err))) return rc;
+      if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) return rc;
+      if (P.PA.nr > 0) {
+        if ((rc = upload_bsr(h.get(), P.PA, &D.PA, 0, err))) return rc;
+      } else {
+        if ((rc = upload_bsr(h.get(), P.P, &D.P, 0, err))) return rc;
+      }
+      if ((rc = upload_bsr(h.get(), P.Rp, &D.R, 0, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.W, D.nloc, err))) return rc;
       HIPCHK(hipMemcpy(D.W, P.W.data(), 4 * D.nloc * sizeof(double), hipMemcpyHostToDevice));
     }

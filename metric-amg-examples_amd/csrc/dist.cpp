@@ -17,7 +17,11 @@
 //           nodes), columns = owned fine nodes.  R r is formed as partial
 //           sums, then ghost partials are sent to their owners and added in
 //           rank order (deterministic).
+//   PA_loc: (post fusion) P_loc and AP_loc = (A P)_loc merged row by row, same
+//           columns as P_loc: the fused post sweep x1 + P e + W (r1 - AP e)
+//           needs only owned x1, r1 and e's ghosts (no fine-level halo)
 //   ghosts(l) = external columns of A_loc  U  external columns of P_{l-1} loc
+//               (U external columns of AP_{l-1} loc with post fusion)
 //   send list to q = the owned nodes that are ghosts of q, in q's order.
 // Only owned rows are converted to blocks (no global copy of A_0 per rank);
 // ghost sets of all ranks come straight from the field-major CSR.
@@ -103,11 +107,13 @@ void transpose_bsr(const HBsr& B, HBsr* T) {
 }  // namespace
 
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    DistPlan* plan, std::string* err) {
+                    bool fuse, DistPlan* plan, std::string* err) {
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
   const int nl = (int)H.levels.size();
   if (nl < 2) { *err = "multi-GPU path needs at least two levels"; return MAMG_ERR_UNSUPPORTED; }
+  for (int l = 0; l + 1 < nl && fuse; ++l)
+    if (H.levels[l].AP.n != H.levels[l].n) fuse = false;   // A P not kept by the setup
   plan->rank = rank;
   plan->nranks = nranks;
   plan->levels.assign(nl, DistLevel());
@@ -141,6 +147,8 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       if (l > 0) {
         const DistLevel& F = plan->levels[l - 1];
         external_node_cols(H.levels[l - 1].P.view(), F.nv, D.nv, F.own[q], F.own[q + 1], o0, o1, &g);
+        if (fuse)
+          external_node_cols(H.levels[l - 1].AP.view(), F.nv, D.nv, F.own[q], F.own[q + 1], o0, o1, &g);
       }
       sort_unique(&g);
       ghosts[l][q] = std::move(g);
@@ -193,6 +201,11 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
     if (D.replicated) {
       to_bsr2(Pv, D.nv, C.nv, &D.P);
       transpose_bsr(D.P, &D.Rp);
+      if (fuse) {
+        HBsr AP;
+        to_bsr2(H.levels[l].AP.view(), D.nv, C.nv, &AP);
+        merge_bsr_rows(D.P, AP, &D.PA);
+      }
       continue;
     }
     const int64_t c0 = C.o0, c1 = C.o1, cnloc = C.nloc;
@@ -200,12 +213,19 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
     const bool crep = C.replicated;
     to_bsr2_rows(Pv, D.nv, C.nv, D.o0, D.o1, &D.P);
     const int64_t ncl = crep ? C.nv : cnloc + (int64_t)cg.size();
-    remap_cols(&D.P, ncl, [&](int64_t J) -> int64_t {
+    auto cmap = [&](int64_t J) -> int64_t {
       if (crep) return J;
       if (J >= c0 && J < c1) return J - c0;
       return cnloc + (std::lower_bound(cg.begin(), cg.end(), J) - cg.begin());
-    });
+    };
+    remap_cols(&D.P, ncl, cmap);
     transpose_bsr(D.P, &D.Rp);
+    if (fuse) {
+      HBsr AP;
+      to_bsr2_rows(H.levels[l].AP.view(), D.nv, C.nv, D.o0, D.o1, &AP);
+      remap_cols(&AP, ncl, cmap);
+      merge_bsr_rows(D.P, AP, &D.PA);
+    }
   }
   return MAMG_OK;
 }

@@ -20,6 +20,7 @@ struct DistLevel {
   HBsr A;                         // owned rows x [owned | ghost] (replicated: global)
   HBsr P;                         // owned fine rows x level l+1 local (or global)
   HBsr Rp;                        // transpose of P (partial restriction)
+  HBsr PA;                        // post fusion: merged [P_loc | AP_loc] (P then empty)
   std::vector<double> W;          // 4 per owned node
 };
 
@@ -29,6 +30,6 @@ struct DistPlan {
 };
 
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    DistPlan* plan, std::string* err);
+                    bool fuse, DistPlan* plan, std::string* err);
 
 }  // namespace mamg
