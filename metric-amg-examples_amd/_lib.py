@@ -112,6 +112,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError('libmamg.so not built (%s); run __graft_entry__.build() '
                               'or make -C metric-amg-examples_amd/csrc' % LIB_PATH)
+        # One HIP runtime per process: torch's wheel ships its own
+        # libamdhip64 (soname libamdhip64.so.7, NEEDED as "libamdhip64.so").
+        # Loaded first, it also satisfies libmamg's libamdhip64.so.7; loaded
+        # after libmamg, torch would bring up a second runtime that finds no
+        # device.  So torch (when installed) is imported before the library.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

@@ -1,0 +1,5 @@
+source scripts/gpu_run.sh
+export TMPDIR=/tmp
+step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --steps 20 --warmup 3 --pcg
