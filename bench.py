@@ -62,6 +62,10 @@ def main():
     ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
     ap.add_argument('--pcg', action='store_true', help='also run one full PCG solve (N = 1)')
+    ap.add_argument('--setup', choices=('gpu', 'host'), default='gpu',
+                    help='N = 1 hierarchy construction: GPU setup (default) or host setup + upload')
+    ap.add_argument('--compare-host-setup', action='store_true',
+                    help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
 
     import torch
@@ -105,15 +109,30 @@ def main():
 
     r_full = M.problems.seeded_rhs(sysm.N)
     H = None
+    setup_info = {}
     if world == 1:
-        t0 = time.time()
-        H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
-        t_setup = time.time() - t0
-        t0 = time.time()
-        B = M.MetricAMG.from_host(H, sysm.W)
-        t_upload = time.time() - t0
-        sizes = [H.sizes(l) for l in range(H.num_levels)]
-        levels = [[s['n'], s['nnzA']] for s in sizes]
+        if args.setup == 'host':
+            t0 = time.time()
+            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+            t_setup = time.time() - t0
+            t0 = time.time()
+            B = M.MetricAMG.from_host(H, sysm.W)
+            t_upload = time.time() - t0
+            setup_info = {'path': 'host', 'host_setup_s': round(t_setup, 3), 'upload_s': round(t_upload, 3)}
+        else:
+            # GPU setup: A0 copied to HBM once, hierarchy and apply layouts
+            # built by gfx950 kernels (bitwise equal to the host setup)
+            torch.cuda.synchronize(dev)
+            t0 = time.time()
+            B = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu')
+            t_setup = time.time() - t0
+            setup_info = {'path': 'gpu', 'wall_s': round(t_setup, 3), 'phases_ms': B.setup_timings}
+            if args.compare_host_setup:
+                t0 = time.time()
+                Hc = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+                setup_info['host_setup_s'] = round(time.time() - t0, 3)
+                Hc.close()
+        levels = None
         layout = B.layout
         r = torch.as_tensor(r_full).to(dev)
     else:
@@ -123,7 +142,8 @@ def main():
         B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
                             comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local)
         t_setup = time.time() - t0
-        t_upload = 0.0
+        setup_info = {'path': 'host setup replicated on every rank + rank-local upload',
+                      'wall_s': round(t_setup, 3)}
         levels = None
         layout = 'bsr2-dist'
         r = torch.as_tensor(B.local_slice(r_full)).to(dev)
@@ -177,6 +197,8 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import cref
+        if H is None:       # same hierarchy bits, from the GPU setup copied back
+            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, gpu=True)
         lv = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
         lv[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
         ch = cref.CHierarchy(lv)
@@ -192,6 +214,8 @@ def main():
                'sample': '%d applies of the full nrefs=%d hierarchy (oracle/vcycle_ref.c, OpenMP), '
                          'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, args.nrefs, err)}
         del ch, lv
+    if H is not None and levels is None:
+        levels = [[s['n'], s['nnzA']] for s in (H.sizes(l) for l in range(H.num_levels))]
 
     # measured HBM bytes per launch of the two dominant kernels (rocprofv3
     # FETCH_SIZE + WRITE_SIZE, calibrated; profiles/traffic.json, written by
@@ -252,8 +276,7 @@ def main():
         'roofline_kernels': rooflines,
         'level0_format': fmt0,
         'cpu_baseline': cpu,
-        'setup_s': {'generate': round(t_gen, 2), 'host_setup': round(t_setup, 2),
-                    'upload': round(t_upload, 2)},
+        'setup': dict(setup_info, generate_s=round(t_gen, 2)),
         'breakdown': breakdown,
         'pcg': pcg,
     }

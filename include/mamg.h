@@ -201,6 +201,29 @@ void mamg_dist_destroy(mamg_dhandle* h);
 /* Host setup + upload.  Level-0 matrix is uploaded from A directly. */
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out);
+/* GPU setup: the same hierarchy as mamg_setup, bit
+ * for bit, built by gfx950 kernels -- strength, MIS-2 aggregation, node-block
+ * smoothers, SA prolongator, Galerkin products, coarsest inverse -- and the
+ * apply layouts built in HBM (no host round trip).  Covers the nodal 2-field
+ * profile (num_functions 2, node_block_smoother 1, sa_block_diag 1; level-0
+ * seed blocks must be node-aligned, as the bidomain's idofs are); anything
+ * else returns MAMG_ERR_UNSUPPORTED (use mamg_setup).  Replaces the setup
+ * half of metricAMG.__init__ (src/utils.py:86).  A: host CSR, copied once. */
+int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                   const mamg_params* params, mamg_handle** out);
+/* Same with A's rowptr/colind/values in device memory (read during setup
+ * only; the caller may free them afterwards).  idofs: host array. */
+int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_idofs,
+                          const mamg_params* params, mamg_handle** out);
+/* GPU setup, hierarchy copied back into a host mamg_hier (tests, multi-GPU
+ * planning); the hierarchy keeps a view of A as mamg_host_setup does. */
+int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                        const mamg_params* params, mamg_hier** out);
+/* Setup phase timings of a GPU-setup handle, ms[8]: aggregation, smoothers,
+ * prolongator, Galerkin, coarsest, apply-layout build, setup total, A upload
+ * (zeros for handles from mamg_setup / mamg_upload). */
+int mamg_setup_timings(const mamg_handle* h, double* ms8);
+
 /* Upload an existing host hierarchy (level 0 matrix taken from A). */
 int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
                 mamg_handle** out);

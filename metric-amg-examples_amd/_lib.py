@@ -87,6 +87,13 @@ SIGNATURES = {
     'mamg_dist_destroy': (None, [VP]),
     'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                              C.POINTER(VP)]),
+    'mamg_setup_gpu': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                                 C.POINTER(VP)]),
+    'mamg_setup_gpu_device': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                                        C.POINTER(VP)]),
+    'mamg_gpu_host_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                                      C.POINTER(VP)]),
+    'mamg_setup_timings': (C.c_int, [VP, P_F64]),
     'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),
     'mamg_destroy': (None, [VP]),
     'mamg_nrows': (C.c_int64, [VP]),

@@ -78,34 +78,104 @@ def _stream_ptr(stream):
     return C.c_void_p(int(stream))
 
 
+def gpu_setup_supported(p) -> bool:
+    """The GPU setup (mamg_setup_gpu) covers the nodal 2-field profile."""
+    return p.num_functions == 2 and p.node_block_smoother != 0 and \
+        (p.AMG_type == 1 or p.sa_block_diag != 0)
+
+
+def _device_csr(A):
+    """(indptr, indices, data[, shape]) of CUDA tensors -> (mamg_csr, n, m) or None."""
+    if not isinstance(A, (tuple, list)) or len(A) < 3 or not getattr(A[0], 'is_cuda', False):
+        return None
+    ip, ix, dv = A[0], A[1], A[2]
+    import torch
+    if ip.dtype != torch.int64 or ix.dtype != torch.int32 or dv.dtype != torch.float64 \
+            or not (ip.is_contiguous() and ix.is_contiguous() and dv.is_contiguous()):
+        raise TypeError('device CSR must be contiguous int64 indptr, int32 indices, float64 data')
+    n = ip.numel() - 1
+    shape = A[3] if len(A) > 3 else (n, n)
+    s = _lib.mamg_csr()
+    s.nrows, s.ncols, s.nnz = n, int(shape[1]), ix.numel()
+    s.rowptr = C.cast(C.c_void_p(ip.data_ptr()), C.POINTER(C.c_int64))
+    s.colind = C.cast(C.c_void_p(ix.data_ptr()), C.POINTER(C.c_int32))
+    s.values = C.cast(C.c_void_p(dv.data_ptr()), C.POINTER(C.c_double))
+    return s, n, int(shape[1])
+
+
 class MetricAMG:
     """One multigrid cycle per application, on the GPU.
 
-    A: CSR operator (scipy sparse, (indptr, indices, data), or System).
+    A: CSR operator (scipy sparse, (indptr, indices, data), or System), or a
+       tuple of CUDA tensors (indptr int64, indices int32, data float64) that
+       is already in HBM (GPU setup only; read during setup, not kept).
     W: list of function spaces / block sizes (only sizes are used).
     idofs: interface dofs seeding the level-0 Schwarz blocks (src/utils.py:84).
     parameters: dict with the reference's key names (see parameters.py).
+    setup: 'gpu' (mamg_setup_gpu: hierarchy built by gfx950 kernels, bitwise
+       equal to the host setup), 'host' (mamg_setup: C++/OpenMP setup, then
+       upload), or 'auto' (default): 'gpu' when the profile is one the GPU
+       setup covers, else 'host'.  ``setup_path`` records what ran and why.
     """
 
-    def __init__(self, A, W=None, idofs=None, parameters=None, **overrides):
+    def __init__(self, A, W=None, idofs=None, parameters=None, setup='auto', **overrides):
         self._L = _lib.lib()
-        indptr, indices, data, n, m = csr_arrays(A)
-        if n != m:
-            raise ValueError('A must be square')
-        self.shape = (n, n)
-        self.W = _dims(W, n)
         self.params = make_params(parameters, **overrides)
-        self._A = (indptr, indices, data)        # level 0 stays referenced
-        self._Aop = A
-        csr = _lib.as_csr_struct(indptr, indices, data, m)
         if idofs is not None:
             self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
             ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
         else:
             self.idofs, ip, ni = None, None, 0
+        if setup not in ('auto', 'gpu', 'host'):
+            raise ValueError("setup must be 'auto', 'gpu' or 'host'")
         h = C.c_void_p()
-        _lib.check(self._L.mamg_setup(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h)))
+        dev = _device_csr(A)
+        if dev is not None:                      # A already in HBM
+            csr, n, m = dev
+            if n != m:
+                raise ValueError('A must be square')
+            if setup == 'host':
+                raise ValueError("a device-resident A needs setup='gpu' (or 'auto')")
+            self.shape = (n, n)
+            self.W = _dims(W, n)
+            self._A = None
+            self._Aop = None
+            _lib.check(self._L.mamg_setup_gpu_device(C.byref(csr), ip, ni, C.byref(self.params),
+                                                     C.byref(h)))
+            self._h = h
+            self.setup_path = 'gpu'
+            return
+        indptr, indices, data, n, m = csr_arrays(A)
+        if n != m:
+            raise ValueError('A must be square')
+        self.shape = (n, n)
+        self.W = _dims(W, n)
+        self._A = (indptr, indices, data)        # level 0 stays referenced
+        self._Aop = A
+        csr = _lib.as_csr_struct(indptr, indices, data, m)
+        use_gpu = setup == 'gpu' or (setup == 'auto' and gpu_setup_supported(self.params))
+        self.setup_path = 'host'
+        if use_gpu:
+            rc = self._L.mamg_setup_gpu(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h))
+            if rc == _lib.ERR_UNSUPPORTED and setup == 'auto':
+                # e.g. seed blocks that are not node-aligned: the host setup
+                # builds the same profile; recorded, not silent
+                self.setup_path = 'host (%s)' % self._L.mamg_last_error().decode(errors='replace')
+            else:
+                _lib.check(rc)
+                self.setup_path = 'gpu'
+        if not self.setup_path == 'gpu':
+            _lib.check(self._L.mamg_setup(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h)))
         self._h = h
+
+    @property
+    def setup_timings(self) -> dict:
+        """GPU setup phase timings in ms (zeros for a host setup)."""
+        ms = (C.c_double * 8)()
+        _lib.check(self._L.mamg_setup_timings(self._h, ms))
+        names = ('aggregate', 'smoother', 'prolongator', 'galerkin', 'coarsest', 'layout',
+                 'setup_total', 'upload_A0')
+        return {k: round(ms[i], 3) for i, k in enumerate(names)}
 
     @classmethod
     def from_host(cls, H: 'HostHierarchy', W=None):
@@ -215,7 +285,7 @@ class HostHierarchy:
     uploads, exported level by level.  Used by tests and the bench's CPU
     baseline; needs no GPU."""
 
-    def __init__(self, A, idofs=None, parameters=None, **overrides):
+    def __init__(self, A, idofs=None, parameters=None, gpu=False, **overrides):
         self._L = _lib.lib()
         indptr, indices, data, n, m = csr_arrays(A)
         self._A = (indptr, indices, data)
@@ -228,8 +298,10 @@ class HostHierarchy:
         else:
             self.idofs, ip, ni = None, None, 0
         h = C.c_void_p()
-        _lib.check(self._L.mamg_host_setup(C.byref(csr), ip, ni, C.byref(self.params),
-                                           C.byref(h)))
+        # gpu=True: the same hierarchy built by the GPU setup, copied back
+        # (mamg_gpu_host_setup; bitwise-parity tests and multi-GPU planning)
+        fn = self._L.mamg_gpu_host_setup if gpu else self._L.mamg_host_setup
+        _lib.check(fn(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h)))
         self._h = h
 
     @property

@@ -336,6 +336,92 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   GUARD_END
 }
 
+int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                   const mamg_params* params, mamg_handle** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  std::string err;
+  mamg::GHier G;
+  G.device = params->device;
+  mamg::DevMat dA;
+  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, idofs, n_idofs, *params, &G, &err))) {
+    set_error(err);
+    return rc;
+  }
+  mamg::DeviceHandle* d = nullptr;
+  rc = mamg::dev_from_ghier(&G, dA, *params, &d, &err);
+  if (rc) { set_error(err); return rc; }
+  *out = new mamg_handle{d};
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_idofs,
+                          const mamg_params* params, mamg_handle** out) {
+  GUARD_BEGIN
+  if (!out || !params || !dA || !dA->rowptr || (dA->nnz > 0 && (!dA->colind || !dA->values))) {
+    set_error("null argument");
+    return MAMG_ERR_ARG;
+  }
+  *out = nullptr;
+  if (dA->nrows <= 0 || dA->ncols <= 0 || dA->nnz < 0 || dA->nrows > INT32_MAX || dA->ncols > INT32_MAX) {
+    set_error("bad CSR sizes");
+    return MAMG_ERR_ARG;
+  }
+  mamg::DevMat M;
+  M.n = dA->nrows;
+  M.m = dA->ncols;
+  M.nnz = dA->nnz;
+  M.ptr = const_cast<int64_t*>(dA->rowptr);
+  M.col = const_cast<int32_t*>(dA->colind);
+  M.val = const_cast<double*>(dA->values);
+  std::string err;
+  mamg::GHier G;
+  G.device = params->device;
+  int rc = mamg::gpu_setup(M, idofs, n_idofs, *params, &G, &err);
+  if (rc) { set_error(err); return rc; }
+  mamg::DeviceHandle* d = nullptr;
+  rc = mamg::dev_from_ghier(&G, M, *params, &d, &err);
+  if (rc) { set_error(err); return rc; }
+  *out = new mamg_handle{d};
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                        const mamg_params* params, mamg_hier** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  std::string err;
+  mamg::GHier G;
+  G.device = params->device;
+  mamg::DevMat dA;
+  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, idofs, n_idofs, *params, &G, &err))) {
+    set_error(err);
+    return rc;
+  }
+  mamg_hier* h = new mamg_hier();
+  rc = mamg::ghier_download(G, v, &h->H, &err);
+  if (rc) { set_error(err); delete h; return rc; }
+  *out = h;
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_setup_timings(const mamg_handle* h, double* ms8) {
+  if (!h || !ms8) { set_error("null argument"); return MAMG_ERR_ARG; }
+  mamg::dev_setup_ms(h->d, ms8);
+  return MAMG_OK;
+}
+
 int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
                 mamg_handle** out) {
   GUARD_BEGIN

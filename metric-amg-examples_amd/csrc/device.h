@@ -2,6 +2,7 @@
 #pragma once
 #include <string>
 
+#include "gsetup.h"
 #include "host.h"
 
 namespace mamg {
@@ -10,6 +11,12 @@ struct DeviceHandle;
 
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
                std::string* err);
+// apply handle from a GPU-setup hierarchy (everything stays in HBM); G's
+// buffers are released level by level as the apply layouts are built
+int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandle** out,
+                   std::string* err);
+// setup phase timings of a handle built by the GPU setup (ms; zeros otherwise)
+void dev_setup_ms(const DeviceHandle* h, double* ms8);
 void dev_destroy(DeviceHandle* h);
 int64_t dev_nrows(const DeviceHandle* h);
 int dev_num_levels(const DeviceHandle* h);

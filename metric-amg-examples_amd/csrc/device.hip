@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -619,6 +620,7 @@ struct DeviceHandle {
   double* dres = nullptr;
   double* hres = nullptr;          // pinned host scalar
   double apply_bytes = 0.0;
+  double setup_ms[8] = {};         // GPU setup phase timings (dev_from_ghier)
   ~DeviceHandle() {
     for (auto& g : graphs) {
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -742,11 +744,327 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
   return MAMG_OK;
 }
 
-int upload_csr_as_bsr(DeviceHandle* h, const CsrView& M, int64_t nr, int64_t nc, DBsr* D, int lanes,
-                      std::string* err, bool sym = false) {
-  HBsr B;
-  to_bsr2(M, nr, nc, &B);
-  return upload_bsr(h, B, D, lanes, err, sym);
+// ---------------------------------------------------------------------------
+// Device-side layout construction: field-major CSR already in HBM (GPU setup
+// output, or host CSR copied up) -> the BSR2 / symmetric / SELL-64 / merged
+// [P | AP] apply layouts.  Same layouts as the host conversions in
+// convert.cpp (to_bsr2, merge_bsr_rows, to_sell with sigma = 1, pack_sym);
+// pure data movement, so the apply sees identical bits either way.
+// ---------------------------------------------------------------------------
+// node I's four sorted column segments: q = 2 f + g holds the entries of row
+// f nr + I whose column lies in field g (node column = col - g nc)
+__device__ __forceinline__ void node_segs(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                          int64_t nr, int64_t nc, int64_t I, int64_t* k, int64_t* e) {
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t a = ptr[f * nr + I], b = ptr[f * nr + I + 1];
+    int64_t lo = a, hi = b;                 // first entry with col >= nc
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (col[mid] < nc) lo = mid + 1; else hi = mid;
+    }
+    k[2 * f] = a; e[2 * f] = lo; k[2 * f + 1] = lo; e[2 * f + 1] = b;
+  }
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ col,
+                                                      const double* __restrict__ val, int64_t* bptr,
+                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t k[4], e[4];
+  node_segs(ptr, col, nr, nc, I, k, e);
+  int64_t o = FILL ? bptr[I] : 0;
+  for (;;) {
+    int64_t J = INT64_MAX;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (k[q] < e[q]) J = min(J, (int64_t)col[k[q]] - (q & 1) * nc);
+    if (J == INT64_MAX) break;
+    dv4 v = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (k[q] < e[q] && (int64_t)col[k[q]] - (q & 1) * nc == J) {
+        if (FILL) v[q] = val[k[q]];
+        ++k[q];
+      }
+    if (FILL) { bcol[o] = (int32_t)J; bval[o] = v; }
+    ++o;
+  }
+  if (!FILL) bptr[I + 1] = o;
+}
+
+__global__ __launch_bounds__(256) void sym_check_kernel(int64_t nb, const dv4* __restrict__ v, int* bad) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < nb && __double_as_longlong(v[k].y) != __double_as_longlong(v[k].z)) atomicOr(bad, 1);
+}
+
+__global__ __launch_bounds__(256) void pack_sym_kernel(int64_t nb, const dv4* __restrict__ v,
+                                                       double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nb) return;
+  const dv4 a = v[k];
+  out[2 * k] = a.x;
+  out[2 * k + 1] = a.w;
+  out[2 * nb + k] = a.y;
+}
+
+// merged [P | Q] row pointers: lengths at 2I+1, 2I+2 (scanned afterwards)
+__global__ __launch_bounds__(256) void merge_len_kernel(int64_t nr, const int64_t* __restrict__ pp,
+                                                        const int64_t* __restrict__ qp, int64_t* mptr) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  mptr[2 * I + 1] = pp[I + 1] - pp[I];
+  mptr[2 * I + 2] = qp[I + 1] - qp[I];
+  if (I == 0) mptr[0] = 0;
+}
+
+__global__ __launch_bounds__(256) void merge_fill_kernel(int64_t nr, const int64_t* __restrict__ pp,
+                                                         const int32_t* __restrict__ pc, const dv4* __restrict__ pv,
+                                                         const int64_t* __restrict__ qp, const int32_t* __restrict__ qc,
+                                                         const dv4* __restrict__ qv, const int64_t* __restrict__ mptr,
+                                                         int32_t* __restrict__ mc, dv4* __restrict__ mv) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t d = mptr[2 * I];
+  for (int64_t k = pp[I]; k < pp[I + 1]; ++k, ++d) { mc[d] = pc[k]; mv[d] = pv[k]; }
+  for (int64_t k = qp[I]; k < qp[I + 1]; ++k, ++d) { mc[d] = qc[k]; mv[d] = qv[k]; }
+}
+
+// SELL-64: slice widths and per-row meta (length | first-part length << 16)
+__global__ __launch_bounds__(256) void sell_meta_kernel(int64_t nr, const int64_t* __restrict__ bptr, int merged,
+                                                        int32_t* __restrict__ meta, int64_t* __restrict__ soff,
+                                                        int* bad) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t ns = (nr + SELL_C - 1) / SELL_C;
+  if (s >= ns) return;
+  int64_t w = 0;
+  for (int64_t I = s * SELL_C; I < min(nr, (s + 1) * SELL_C); ++I) {
+    const int64_t a = merged ? bptr[2 * I] : bptr[I];
+    const int64_t m = merged ? bptr[2 * I + 1] : a;
+    const int64_t e = merged ? bptr[2 * I + 2] : bptr[I + 1];
+    if (e - a >= 0xffff) { atomicOr(bad, 1); continue; }
+    meta[I] = (int32_t)((e - a) | ((m - a) << 16));
+    w = max(w, e - a);
+  }
+  soff[s + 1] = (int64_t)SELL_C * w;
+  if (s == 0) soff[0] = 0;
+}
+
+__global__ __launch_bounds__(256) void sell_fill_kernel(int64_t nr, const int64_t* __restrict__ bptr, int merged,
+                                                        const int32_t* __restrict__ bcol, const dv4* __restrict__ bval,
+                                                        const int64_t* __restrict__ soff, int64_t nbs, int sym,
+                                                        int32_t* __restrict__ scol, double* __restrict__ sval) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  const int64_t a = merged ? bptr[2 * I] : bptr[I];
+  const int64_t e = merged ? bptr[2 * I + 2] : bptr[I + 1];
+  int64_t kk = soff[I / SELL_C] + (I % SELL_C);
+  for (int64_t k = a; k < e; ++k, kk += SELL_C) {
+    scol[kk] = bcol[k];
+    const dv4 v = bval[k];
+    if (sym) {
+      sval[2 * kk] = v.x;
+      sval[2 * kk + 1] = v.w;
+      sval[2 * nbs + kk] = v.y;
+    } else {
+      reinterpret_cast<dv4*>(sval)[kk] = v;
+    }
+  }
+}
+
+// coarsest inverse, dof order -> node-interleaved order
+__global__ __launch_bounds__(256) void permute_dense_kernel(int64_t n, const double* __restrict__ in,
+                                                            double* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * n) return;
+  const int64_t i = t / n, j = t % n, nv = n / 2;
+  out[(2 * (i % nv) + i / nv) * n + (2 * (j % nv) + j / nv)] = in[t];
+}
+
+// raw device BSR2 (4 doubles per block); merged: ptr has 2 nr + 1 entries
+struct TBsr {
+  int64_t nr = 0, nc = 0, nb = 0;
+  bool merged = false;
+  int64_t* ptr = nullptr;
+  int32_t* col = nullptr;
+  dv4* val = nullptr;
+};
+
+struct TmpPool {            // scoped temporaries of the layout builder
+  std::vector<void*> v;
+  ~TmpPool() { for (void* p : v) (void)hipFree(p); }
+  template <class T>
+  int alloc(T** p, int64_t count, std::string* err) {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+    v.push_back(q);
+    *p = (T*)q;
+    return MAMG_OK;
+  }
+  void release(void* p) {
+    for (auto& q : v)
+      if (q == p) { (void)hipFree(q); q = nullptr; }
+  }
+};
+
+int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B, std::string* err) {
+  int rc;
+  B->nr = nr; B->nc = nc; B->merged = false;
+  if ((rc = T->alloc(&B->ptr, nr + 1, err))) return rc;
+  HIPCHK(hipMemset(B->ptr, 0, sizeof(int64_t)));
+  if (nr) csr2bsr_kernel<false><<<nblocks(nr), 256>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(B->ptr, B->ptr, nr + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
+  if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
+  if (nr) csr2bsr_kernel<true><<<nblocks(nr), 256>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+int dev_merge_rows(TmpPool* T, const TBsr& P, const TBsr& Q, TBsr* M, std::string* err) {
+  int rc;
+  const int64_t nr = P.nr;
+  M->nr = nr; M->nc = P.nc; M->merged = true;
+  if ((rc = T->alloc(&M->ptr, 2 * nr + 1, err))) return rc;
+  if (nr) merge_len_kernel<<<nblocks(nr), 256>>>(nr, P.ptr, Q.ptr, M->ptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(M->ptr, M->ptr, 2 * nr + 1, nullptr, err))) return rc;
+  M->nb = P.nb + Q.nb;
+  if ((rc = T->alloc(&M->col, M->nb, err))) return rc;
+  if ((rc = T->alloc(&M->val, M->nb, err))) return rc;
+  if (nr) merge_fill_kernel<<<nblocks(nr), 256>>>(nr, P.ptr, P.col, P.val, Q.ptr, Q.col, Q.val, M->ptr, M->col, M->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+// final apply layout from a raw device BSR (the device-side counterpart of
+// upload_bsr): SELL-64 for large short-row plain matrices, symmetric-block
+// packing where every block has (0,1) == (1,0) bitwise, else 4 doubles/block
+template <class HT>
+int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, std::string* err) {
+  int rc;
+  const int64_t nr = B.nr, np = B.merged ? 2 * nr + 1 : nr + 1;
+  D->nr = nr;
+  D->nc = B.nc;
+  D->nb = B.nb;
+  D->lanes = lanes > 0 ? lanes : pick_lanes_bsr(nr, D->nb);
+  bool sym = false;
+  if (sym_ok && g_sym && !B.merged && B.nb > 0) {
+    int* bad = nullptr;
+    if ((rc = T->alloc(&bad, 1, err))) return rc;
+    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    sym_check_kernel<<<nblocks(B.nb), 256>>>(B.nb, B.val, bad);
+    int hb = 1;
+    HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
+    sym = hb == 0;
+  }
+  D->sym = sym;
+  const int per = sym ? 3 : 4;
+  if (g_sell && nr >= g_sell_min_rows && D->nb <= 40 * nr && !B.merged) {
+    const int64_t ns = (nr + SELL_C - 1) / SELL_C;
+    int* bad = nullptr;
+    if ((rc = T->alloc(&bad, 1, err))) return rc;
+    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    D->sell = true;
+    if ((rc = dalloc(h, &D->soff, ns + 1, err))) return rc;
+    if ((rc = dalloc(h, &D->meta, std::max<int64_t>(nr, 1), err))) return rc;
+    sell_meta_kernel<<<nblocks(ns), 256>>>(nr, B.ptr, 0, D->meta, D->soff, bad);
+    HIPCHK(hipGetLastError());
+    int hb = 0;
+    HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
+    if (hb) { *err = "SELL: row longer than 65534 blocks"; return MAMG_ERR_UNSUPPORTED; }
+    if ((rc = dscan_incl_i64(D->soff, D->soff, ns + 1, nullptr, err))) return rc;
+    HIPCHK(hipMemcpy(&D->nbs, D->soff + ns, sizeof(int64_t), hipMemcpyDeviceToHost));
+    if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nbs, 1), err))) return rc;
+    if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nbs, 1), err))) return rc;
+    HIPCHK(hipMemset(D->col, 0, std::max<int64_t>(D->nbs, 1) * sizeof(int32_t)));
+    HIPCHK(hipMemset(D->val, 0, std::max<int64_t>(per * D->nbs, 1) * sizeof(double)));
+    sell_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, 0, B.col, B.val, D->soff, D->nbs, sym ? 1 : 0, D->col, D->val);
+    HIPCHK(hipGetLastError());
+    return MAMG_OK;
+  }
+  if ((rc = dalloc(h, &D->ptr, np, err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, B.ptr, np * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  if (D->nb) {
+    HIPCHK(hipMemcpy(D->col, B.col, D->nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
+    if (sym) pack_sym_kernel<<<nblocks(D->nb), 256>>>(D->nb, B.val, D->val);
+    else HIPCHK(hipMemcpy(D->val, B.val, D->nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+    HIPCHK(hipGetLastError());
+  }
+  return MAMG_OK;
+}
+
+// one BSR2 level from device-resident field-major CSRs (AP.n == 0: no fusion)
+struct LevelSrc {
+  DevMat A, P, AP, R;
+  const double* W = nullptr;      // 4 nv node blocks (device)
+  const double* Ainv = nullptr;   // coarsest: n x n dof order (device)
+};
+
+int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
+  DLevel& D = h->L[l];
+  const mamg_params& p = h->p;
+  const int64_t nv = D.n / 2;
+  int rc;
+  TmpPool T;
+  if (D.coarsest) {
+    if ((rc = dalloc(h, &D.Ainv, D.n * D.n, err))) return rc;
+    permute_dense_kernel<<<nblocks(D.n * D.n), 256>>>(D.n, S.Ainv, D.Ainv);
+    HIPCHK(hipGetLastError());
+    TBsr B;
+    if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
+    return finalize_bsr(h, &T, B, &D.Ab, 0, false, err);
+  }
+  {
+    TBsr B;
+    if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err))) return rc;
+    T.release(B.ptr); T.release(B.col); T.release(B.val);
+  }
+  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n) {
+    TBsr Pb, Qb, M;
+    if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
+    if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
+    if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
+    T.release(Pb.ptr); T.release(Pb.col); T.release(Pb.val);
+    T.release(Qb.ptr); T.release(Qb.col); T.release(Qb.val);
+    if ((rc = finalize_bsr(h, &T, M, &D.PAb, g_post_lanes, false, err))) return rc;
+  } else {
+    TBsr Pb;
+    if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, Pb, &D.Pb, 0, false, err))) return rc;
+  }
+  {
+    TBsr Rb;
+    if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
+  }
+  if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
+  HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
+  HIPCHK(hipDeviceSynchronize());
+  return MAMG_OK;
+}
+
+// host CSR -> temporary device CSR
+int upload_tmp(TmpPool* T, const CsrView& M, DevMat* D, std::string* err) {
+  int rc;
+  D->n = M.n; D->m = M.m; D->nnz = M.nnz();
+  if ((rc = T->alloc(&D->ptr, M.n + 1, err))) return rc;
+  if ((rc = T->alloc(&D->col, D->nnz, err))) return rc;
+  if ((rc = T->alloc(&D->val, D->nnz, err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, M.ptr, (M.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (D->nnz) {
+    HIPCHK(hipMemcpy(D->col, M.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, M.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
 }
 
 // ---- algorithmic bytes (per layout) ------------------------------
@@ -1176,42 +1494,35 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
     D.coarsest = hl.coarsest;
     const CsrView Al = l == 0 ? A0 : H.A(l);
     const int lanesA = l == 0 ? p.spmv_lanes : 0;
-    if (D.coarsest) {
+    if (h->bsr && !(l == 0 && D.coarsest)) {
+      // copy the level's CSRs up once and build the apply layouts on the device
+      TmpPool T;
+      LevelSrc S;
+      if ((rc = upload_tmp(&T, Al, &S.A, err))) return rc;
+      if (D.coarsest) {
+        double* dA = nullptr;
+        if ((rc = T.alloc(&dA, D.n * D.n, err))) return rc;
+        HIPCHK(hipMemcpy(dA, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
+        S.Ainv = dA;
+        if ((rc = build_bsr_level(h.get(), l, S, 0, 0, err))) return rc;
+      } else {
+        const int64_t nv = D.n / 2, nvc = H.levels[l + 1].n / 2;
+        if ((rc = upload_tmp(&T, hl.P.view(), &S.P, err))) return rc;
+        if ((rc = upload_tmp(&T, hl.R.view(), &S.R, err))) return rc;
+        if (p.post_fusion && p.postsmooth_iter >= 1 && hl.AP.n == hl.n)
+          if ((rc = upload_tmp(&T, hl.AP.view(), &S.AP, err))) return rc;
+        std::vector<double> blk;
+        node_blocks_of(hl.WB.view(), nv, &blk);
+        double* dW = nullptr;
+        if ((rc = T.alloc(&dW, 4 * nv, err))) return rc;
+        HIPCHK(hipMemcpy(dW, blk.data(), 4 * nv * sizeof(double), hipMemcpyHostToDevice));
+        S.W = dW;
+        if ((rc = build_bsr_level(h.get(), l, S, nvc, lanesA, err))) return rc;
+      }
+    } else if (D.coarsest) {     // CSR layout, or a single-level hierarchy
       if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
-      if (h->bsr && l > 0) {      // node-interleaved coarsest vectors: permute
-        std::vector<double> Ap(D.n * D.n);
-        const int64_t nv = D.n / 2;
-        auto pos = [nv](int64_t i) { return 2 * (i % nv) + i / nv; };
-        for (int64_t i = 0; i < D.n; ++i)
-          for (int64_t j = 0; j < D.n; ++j) Ap[pos(i) * D.n + pos(j)] = hl.Ainv[i * D.n + j];
-        HIPCHK(hipMemcpy(D.Ainv, Ap.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
-      } else {
-        HIPCHK(hipMemcpy(D.Ainv, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
-      }
-      if (l == 0) {
-        if ((rc = upload_csr(h.get(), Al, &D.A, lanesA, err))) return rc;
-      } else if (h->bsr) {
-        if ((rc = upload_csr_as_bsr(h.get(), Al, D.n / 2, D.n / 2, &D.Ab, 0, err))) return rc;
-      } else {
-        if ((rc = upload_csr(h.get(), Al, &D.A, 0, err))) return rc;
-      }
-    } else if (h->bsr) {
-      const int64_t nv = D.n / 2, nvc = H.levels[l + 1].n / 2;
-      if ((rc = upload_csr_as_bsr(h.get(), Al, nv, nv, &D.Ab, lanesA, err, true))) return rc;
-      if (p.post_fusion && p.postsmooth_iter >= 1 && hl.AP.n == hl.n) {
-        HBsr Pn, APn, M;
-        to_bsr2(hl.P.view(), nv, nvc, &Pn);
-        to_bsr2(hl.AP.view(), nv, nvc, &APn);
-        merge_bsr_rows(Pn, APn, &M);
-        if ((rc = upload_bsr(h.get(), M, &D.PAb, g_post_lanes, err))) return rc;
-      } else {
-        if ((rc = upload_csr_as_bsr(h.get(), hl.P.view(), nv, nvc, &D.Pb, 0, err))) return rc;
-      }
-      if ((rc = upload_csr_as_bsr(h.get(), hl.R.view(), nvc, nv, &D.Rb, 0, err))) return rc;
-      std::vector<double> blk;
-      node_blocks_of(hl.WB.view(), nv, &blk);
-      if ((rc = dalloc(h.get(), &D.Wd, nv, err))) return rc;
-      HIPCHK(hipMemcpy(D.Wd, blk.data(), 4 * nv * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(D.Ainv, hl.Ainv.data(), D.n * D.n * sizeof(double), hipMemcpyHostToDevice));
+      if ((rc = upload_csr(h.get(), Al, &D.A, lanesA, err))) return rc;
     } else {
       if ((rc = upload_csr(h.get(), Al, &D.A, lanesA, err))) return rc;
       if ((rc = upload_csr(h.get(), hl.P.view(), &D.P, 0, err))) return rc;
@@ -1237,6 +1548,79 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   HIPCHK(hipDeviceSynchronize());
   *out = h.release();
   return MAMG_OK;
+}
+
+int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandle** out,
+                   std::string* err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::unique_ptr<DeviceHandle> h(new DeviceHandle());
+  h->p = p;
+  h->device = p.device;
+  HIPCHK(hipSetDevice(p.device));
+  HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
+  read_knobs();
+  h->bsr = true;
+  const int nl = (int)G->levels.size();
+  h->L.resize(nl);
+  int rc;
+  for (int l = 0; l < nl; ++l) {
+    GLevel& g = G->levels[l];
+    DLevel& D = h->L[l];
+    D.n = g.n;
+    D.coarsest = g.coarsest;
+    if (l == 0 && D.coarsest) {          // single-level hierarchy: CSR A0 + dense inverse
+      if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
+      HIPCHK(hipMemcpy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double), hipMemcpyDeviceToDevice));
+      D.A.n = A0.n; D.A.m = A0.m; D.A.nnz = A0.nnz;
+      D.A.lanes = p.spmv_lanes > 0 ? p.spmv_lanes : pick_lanes(A0.n, A0.nnz);
+      if ((rc = dalloc(h.get(), &D.A.ptr, A0.n + 1, err))) return rc;
+      if ((rc = dalloc(h.get(), &D.A.col, std::max<int64_t>(A0.nnz, 1), err))) return rc;
+      if ((rc = dalloc(h.get(), &D.A.val, std::max<int64_t>(A0.nnz, 1), err))) return rc;
+      HIPCHK(hipMemcpy(D.A.ptr, A0.ptr, (A0.n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+      if (A0.nnz) {
+        HIPCHK(hipMemcpy(D.A.col, A0.col, A0.nnz * sizeof(int32_t), hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(D.A.val, A0.val, A0.nnz * sizeof(double), hipMemcpyDeviceToDevice));
+      }
+    } else {
+      LevelSrc S;
+      S.A = l == 0 ? A0 : g.A;
+      S.P = g.P; S.R = g.R; S.AP = g.AP; S.W = g.W; S.Ainv = g.Ainv;
+      const int64_t nvc = D.coarsest ? 0 : G->levels[l + 1].n / 2;
+      if ((rc = build_bsr_level(h.get(), l, S, nvc, l == 0 ? p.spmv_lanes : 0, err))) return rc;
+    }
+    // the level's GPU-setup buffers are no longer needed (A_l stays for l+1's
+    // Galerkin product only, which is done)
+    for (void* q : {(void*)g.P.ptr, (void*)g.P.col, (void*)g.P.val, (void*)g.R.ptr, (void*)g.R.col,
+                    (void*)g.R.val, (void*)g.AP.ptr, (void*)g.AP.col, (void*)g.AP.val, (void*)g.W,
+                    (void*)g.Ainv})
+      if (q) G->release(q);
+    if (l > 0)
+      for (void* q : {(void*)g.A.ptr, (void*)g.A.col, (void*)g.A.val})
+        if (q) G->release(q);
+    g.P = g.R = g.AP = DevMat();
+    g.W = g.Ainv = nullptr;
+    if (l > 0) g.A = DevMat();
+    double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
+    for (double** v : vecs)
+      if ((rc = dalloc(h.get(), v, D.n, err))) return rc;
+  }
+  const int64_t n0 = h->L[0].n;
+  double** v0[] = {&h->hr, &h->hz};
+  for (double** v : v0)
+    if ((rc = dalloc(h.get(), v, n0, err))) return rc;
+  std::vector<Op> ops;
+  apply_ops(h.get(), h->hr, h->hz, &ops);
+  for (const Op& o : ops) h->apply_bytes += o.bytes;
+  for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
+  HIPCHK(hipDeviceSynchronize());
+  h->setup_ms[GS_LAYOUT] =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = h.release();
+  return MAMG_OK;
+}
+
+void dev_setup_ms(const DeviceHandle* h, double* ms8) {
+  for (int k = 0; k < 8; ++k) ms8[k] = h->setup_ms[k];
 }
 
 void dev_destroy(DeviceHandle* h) {

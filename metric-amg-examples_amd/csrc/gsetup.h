@@ -1,0 +1,65 @@
+// gsetup.h -- device-resident hierarchy produced by the GPU setup
+// (gsetup.hip) and consumed by the apply-layout builder (device.hip).
+// Plain pointers only (no HIP types), so host translation units can include it.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "host.h"
+
+namespace mamg {
+
+// device CSR: int64 row pointers, int32 sorted columns, fp64 values
+struct DevMat {
+  int64_t n = 0, m = 0, nnz = 0;
+  int64_t* ptr = nullptr;
+  int32_t* col = nullptr;
+  double* val = nullptr;
+};
+
+// one level of the nodal (num_functions == 2) SA hierarchy on the device;
+// every field-major CSR follows the host setup's definition bit for bit
+struct GLevel {
+  int64_t n = 0;              // dofs (2 nv)
+  bool coarsest = false;
+  DevMat A;                   // level 0: the caller's matrix (not owned)
+  DevMat P, R, AP;            // prolongation, restriction = P^T, A P
+  double* W = nullptr;        // 2x2 smoother block per node, node-major (4 nv)
+  uint8_t* joined = nullptr;  // level 0: 1 if node I's two dofs form one seed block
+  double* Ainv = nullptr;     // coarsest: dense inverse, n x n row-major, dof order
+  int64_t* agg = nullptr;     // aggregate of each node (-1 isolated)
+  int64_t nagg = 0;
+  double w_sa = 0.0;
+};
+
+struct GHier {
+  mamg_params params;
+  int device = 0;
+  std::vector<GLevel> levels;
+  std::vector<void*> allocs;  // every device buffer above (owned)
+  double phase_ms[8] = {};    // setup phase timings (see gsetup.hip)
+  ~GHier();
+  void release(void* p);      // free one owned buffer now
+};
+
+// GPU setup of the nodal smoothed-aggregation hierarchy
+// from a device CSR A0 (kept as level 0, not copied); idofs are host ints.
+int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mamg_params& p,
+              GHier* G, std::string* err);
+// copy a GPU hierarchy into a host Hierarchy (same fields the host setup
+// fills; level-0 A is the given host view)
+int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string* err);
+// host CSR -> HBM, buffers owned by G (G->device selects the GPU)
+int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err);
+
+// phase_ms slots
+enum { GS_AGGREGATE = 0, GS_SMOOTHER = 1, GS_PROLONG = 2, GS_GALERKIN = 3, GS_COARSEST = 4,
+       GS_LAYOUT = 5, GS_TOTAL = 6, GS_UPLOAD = 7 };
+
+// device primitives (dprims.hip)
+int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std::string* err);
+int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, int64_t* vout,
+                        int64_t n, int key_bits, void* stream, std::string* err);
+
+}  // namespace mamg

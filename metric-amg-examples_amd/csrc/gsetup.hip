@@ -1,0 +1,1205 @@
+// gsetup.hip -- GPU setup of the nodal smoothed-aggregation hierarchy.
+//
+// Replaces the HAZmath metric-AMG setup behind
+//   metricAMG(A, W, idofs=interface_dofs, parameters=...)   src/utils.py:86
+// for the bidomain profile (num_functions = 2, node-block smoothers, nodal SA;
+// DESIGN.md section 2.2) with gfx950 kernels, starting from A0 already in HBM.
+// It computes the same hierarchy as the host setup (setup.cpp) BIT FOR BIT:
+// every value is the same sequence of IEEE binary64 operations (this file is
+// compiled with -ffp-contract=off; device sqrt and division are correctly
+// rounded), sums run in the host's (scipy SMMP / CSR) order, exact zeros are
+// dropped by the same rules, and every integer decision (strength, MIS-2,
+// aggregation, seed blocks) follows setup.cpp exactly.
+//
+// Per level (nv nodes, 2 fields, dof f nv + I):
+//   node graph     s_IJ = ||A_IJ||_F          one thread per node: 4-way merge
+//   strength       flags on the node graph, symmetrised via the mirror entry
+//   MIS-2          round-synchronous 2-hop max of hash keys; roots by scan
+//   aggregation    distance-1 joins, then strongest aggregated neighbour
+//   smoothers      2x2 node-block (or level-0 seed-block) inverses, rho_B =
+//                  max_i sum_j |(D_B^-1 A)_ij| by a 2-row merge per dof
+//   prolongator    A T (wave-per-row hash SpGEMM), then P = T - w D_B^-1 (A T)
+//                  fused into one 2-row merge per dof
+//   Galerkin       R = P^T (stable radix sort), A P and R (A P) (hash SpGEMM)
+//   coarsest       dense Gauss-Jordan (no pivoting), one pivot per 3 launches
+//
+// Hash SpGEMM (row i of C = A B): one wavefront per row; A's entries are
+// consumed in CSR order (one step each), the 64 lanes take B's row k
+// (distinct columns, so no two lanes of a step touch one slot); the LDS table
+// accumulates sums[j] += a_ik b_kj exactly in scipy's order.  Rows are binned
+// by their product count: <= 384 into a 512-slot table (4 waves per block),
+// larger into 2048 slots (1 wave per block); a row with more distinct columns
+// than that fails loudly (MAMG_ERR_UNSUPPORTED) instead of degrading.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "gsetup.h"
+
+typedef double dv4_t __attribute__((ext_vector_type(4)));
+
+namespace mamg {
+
+GHier::~GHier() {
+  for (void* p : allocs)
+    if (p) (void)hipFree(p);
+}
+
+void GHier::release(void* p) {
+  for (auto& q : allocs)
+    if (q == p) { (void)hipFree(q); q = nullptr; }
+}
+
+namespace {
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      *err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
+      return MAMG_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
+
+#define RCHK(expr)              \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_) return rc_;        \
+  } while (0)
+
+inline unsigned nblk(int64_t work, int per = 256) { return (unsigned)std::max<int64_t>(1, (work + per - 1) / per); }
+
+constexpr uint64_t ST_OUT = 0, ST_UND = 1, ST_IN = 2;
+
+// same arithmetic as host.h hash32 / oracle hash32
+__device__ __forceinline__ uint32_t dhash32(uint64_t i, int level) {
+  uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
+  uint32_t lv = (uint32_t)(((uint64_t)(int64_t)level * 0x85EBCA77ull) & 0xFFFFFFFFull);
+  x = x * 0x9E3779B1u + lv;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ int64_t dfind(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                         int64_t i, int64_t j) {
+  int64_t lo = ptr[i], hi = ptr[i + 1];
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (col[mid] < j) lo = mid + 1; else hi = mid;
+  }
+  return (lo < ptr[i + 1] && col[lo] == j) ? lo : -1;
+}
+
+// ---------------------------------------------------------------------------
+// owned device buffers
+// ---------------------------------------------------------------------------
+struct Scratch {            // temporaries of one setup call
+  std::vector<void*> v;
+  ~Scratch() { for (void* p : v) if (p) (void)hipFree(p); }
+  template <class T>
+  int alloc(T** p, int64_t count, std::string* err) {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+    v.push_back(q);
+    *p = (T*)q;
+    return MAMG_OK;
+  }
+  void release(void* p) {
+    for (auto& q : v)
+      if (q == p) { (void)hipFree(q); q = nullptr; }
+  }
+};
+
+template <class T>
+int galloc(GHier* G, T** p, int64_t count, std::string* err) {
+  void* q = nullptr;
+  HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+  G->allocs.push_back(q);
+  *p = (T*)q;
+  return MAMG_OK;
+}
+
+template <class T>
+int to_host(T* dst, const T* src, int64_t count, std::string* err) {
+  if (count > 0) HIPCHK(hipMemcpy(dst, src, count * sizeof(T), hipMemcpyDeviceToHost));
+  return MAMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// node graph (setup.cpp node_graph, nf = 2): s_IJ = sqrt(sum of squares over
+// the 2x2 block), accumulated over rows I then nv + I, each in CSR order
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void segs2(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                      int64_t nr, int64_t nc, int64_t I, int64_t* k, int64_t* e) {
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t a = ptr[f * nr + I], b = ptr[f * nr + I + 1];
+    int64_t lo = a, hi = b;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (col[mid] < nc) lo = mid + 1; else hi = mid;
+    }
+    k[2 * f] = a; e[2 * f] = lo; k[2 * f + 1] = lo; e[2 * f + 1] = b;
+  }
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void node_graph_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val, int64_t* gptr,
+                                                         int32_t* __restrict__ gcol, double* __restrict__ gval) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  int64_t k[4], e[4];
+  segs2(ptr, col, nv, nv, I, k, e);
+  int64_t o = FILL ? gptr[I] : 0;
+  for (;;) {
+    int64_t J = INT64_MAX;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (k[q] < e[q]) J = min(J, (int64_t)col[k[q]] - (q & 1) * nv);
+    if (J == INT64_MAX) break;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)          // order (f0,g0) (f0,g1) (f1,g0) (f1,g1)
+      if (k[q] < e[q] && (int64_t)col[k[q]] - (q & 1) * nv == J) {
+        const double a = val[k[q]];
+        acc += a * a;
+        ++k[q];
+      }
+    if (FILL) { gcol[o] = (int32_t)J; gval[o] = sqrt(acc); }
+    ++o;
+  }
+  if (!FILL) gptr[I + 1] = o;
+}
+
+// |diagonal| of a square CSR (0 if absent)
+__global__ __launch_bounds__(256) void absdiag_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                      double* __restrict__ d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = dfind(ptr, col, i, i);
+  d[i] = p >= 0 ? fabs(val[p]) : 0.0;
+}
+
+// strength (setup.cpp strength): flag the entry and its mirror; a missing
+// mirror (non-symmetric pattern) is counted and rejected by the caller
+__global__ __launch_bounds__(256) void strength_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val, const double* __restrict__ d,
+                                                       double theta, uint8_t* flag, int* nextra) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+    const int64_t j = col[k];
+    if (j == i) continue;
+    const double av = fabs(val[k]);
+    const double s = sqrt(d[i] * d[j]);
+    if ((av >= theta * s) && (av > 1e-12 * s)) {
+      flag[k] = 1;
+      const int64_t q = dfind(ptr, col, j, i);
+      if (q >= 0) flag[q] = 1;
+      else atomicAdd(nextra, 1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MIS-2 aggregation (setup.cpp aggregate_mis2)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mis_init_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                       const uint8_t* __restrict__ flag, int level,
+                                                       uint64_t* __restrict__ state, uint64_t* __restrict__ low,
+                                                       uint8_t* __restrict__ nonisol) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  bool any = false;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) any |= flag[k] != 0;
+  nonisol[i] = any;
+  state[i] = any ? ST_UND : ST_OUT;
+  low[i] = ((uint64_t)(dhash32((uint64_t)i, level) & 0x7FFFFFFFu) << 31) | (uint64_t)i;
+}
+
+__global__ __launch_bounds__(256) void mis_key_kernel(int64_t n, const uint64_t* __restrict__ state,
+                                                      const uint64_t* __restrict__ low, uint64_t* __restrict__ key,
+                                                      unsigned long long* und) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool u = false;
+  if (i < n) {
+    key[i] = (state[i] << 62) | low[i];
+    u = state[i] == ST_UND;
+  }
+  const unsigned long long b = __ballot(u);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(und, (unsigned long long)__popcll(b));
+}
+
+__global__ __launch_bounds__(256) void mis_max_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ col,
+                                                      const uint8_t* __restrict__ flag,
+                                                      const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t m = in[i];
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+    if (flag[k]) m = max(m, in[col[k]]);
+  out[i] = m;
+}
+
+__global__ __launch_bounds__(256) void mis_update_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const uint8_t* __restrict__ flag,
+                                                         const uint64_t* __restrict__ m1,
+                                                         const uint64_t* __restrict__ key,
+                                                         uint64_t* __restrict__ state) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || state[i] != ST_UND) return;
+  uint64_t m = m1[i];
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+    if (flag[k]) m = max(m, m1[col[k]]);
+  if (m == key[i]) state[i] = ST_IN;
+  else if ((m >> 62) == ST_IN) state[i] = ST_OUT;
+}
+
+__global__ __launch_bounds__(256) void root_flag_kernel(int64_t n, const uint64_t* __restrict__ state,
+                                                        int64_t* __restrict__ f) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) f[i] = state[i] == ST_IN;
+}
+
+// agg = root number (inclusive scan - 1) for roots, -1 otherwise
+__global__ __launch_bounds__(256) void root_number_kernel(int64_t n, const uint64_t* __restrict__ state,
+                                                          const int64_t* __restrict__ scan, int64_t* __restrict__ agg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) agg[i] = state[i] == ST_IN ? scan[i] - 1 : -1;
+}
+
+// phase 2: a non-root joins its (unique) strong root neighbour
+__global__ __launch_bounds__(256) void agg_phase2_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const uint8_t* __restrict__ flag,
+                                                         const uint64_t* __restrict__ state,
+                                                         const int64_t* __restrict__ agg, int64_t* __restrict__ agg2) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t a = agg[i];
+  if (state[i] != ST_IN)
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+      if (flag[k] && state[col[k]] == ST_IN) a = agg[col[k]];
+  agg2[i] = a;
+}
+
+// phase 3: remaining non-isolated nodes join the strongest aggregated
+// neighbour (weight |s_IJ| * 1.0; ties: smallest aggregate id)
+__global__ __launch_bounds__(256) void agg_phase3_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val,
+                                                         const uint8_t* __restrict__ flag,
+                                                         const uint8_t* __restrict__ nonisol,
+                                                         const int64_t* __restrict__ agg2, int64_t* __restrict__ agg3,
+                                                         int* bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (!nonisol[i] || agg2[i] >= 0) { agg3[i] = agg2[i]; return; }
+  double bw = -1.0;
+  int64_t ba = -1;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+    if (!flag[k]) continue;
+    const double w = fabs(val[k]) * 1.0;
+    if (w == 0.0) continue;
+    const int64_t a = agg2[col[k]];
+    if (a < 0) continue;
+    if (w > bw || (w == bw && a < ba)) { bw = w; ba = a; }
+  }
+  if (ba < 0) atomicAdd(bad, 1);
+  agg3[i] = ba;
+}
+
+// ---------------------------------------------------------------------------
+// smoother / SA node blocks
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void seed_mark_kernel(int64_t m, const int32_t* __restrict__ idofs, int64_t n,
+                                                        uint8_t* __restrict__ isseed, int* bad) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m) return;
+  const int32_t s = idofs[t];
+  if (s < 0 || s >= n) { atomicAdd(bad, 1); return; }
+  isseed[s] = 1;
+}
+
+// strongest seed neighbour of every non-seed dof (setup.cpp block_smoother)
+__global__ __launch_bounds__(256) void best_seed_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ col,
+                                                        const double* __restrict__ val,
+                                                        const uint8_t* __restrict__ isseed, int64_t* __restrict__ best) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  int64_t bs = -1;
+  if (!isseed[j]) {
+    double bv = -1.0;
+    for (int64_t k = ptr[j]; k < ptr[j + 1]; ++k) {
+      const int64_t s = col[k];
+      if (s == j || !isseed[s]) continue;
+      const double v = fabs(val[k]);
+      if (v > bv || (v == bv && s < bs)) { bv = v; bs = s; }
+    }
+  }
+  best[j] = bs;
+}
+
+// seed blocks are node-aligned iff every joiner joins its own node's other
+// dof; joined[I]: dofs I and nv + I form one block (needs Schwarz_mmsize >= 2)
+__global__ __launch_bounds__(256) void seed_align_kernel(int64_t nv, const uint8_t* __restrict__ isseed,
+                                                         const int64_t* __restrict__ best, int mmsize,
+                                                         uint8_t* __restrict__ joined, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  bool j = false;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t d = f * nv + I, partner = (1 - f) * nv + I;
+    if (isseed[d] || best[d] < 0) continue;
+    if (best[d] != partner) { atomicAdd(bad, 1); continue; }
+    j = j || mmsize >= 2;
+  }
+  joined[I] = j;
+}
+
+// 2x2 node-block inverse by Gauss-Jordan without pivoting (setup.cpp
+// gauss_jordan on the block [[a00 a01] [a10 a11]]); a block split into two
+// singletons (joined == 0) has its coupling entries set to 0, which gives the
+// singleton inverses 1/a00, 1/a11 bit for bit
+__device__ __forceinline__ double entry(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                        const double* __restrict__ val, int64_t i, int64_t j) {
+  const int64_t p = dfind(ptr, col, i, j);
+  return p >= 0 ? val[p] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void node_inverse_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const double* __restrict__ val,
+                                                           const uint8_t* __restrict__ joined,
+                                                           dv4_t* __restrict__ Dinv, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  const bool jn = joined ? joined[I] != 0 : true;
+  double M[2][4];
+  M[0][0] = entry(ptr, col, val, I, I);
+  M[0][1] = jn ? entry(ptr, col, val, I, nv + I) : 0.0;
+  M[1][0] = jn ? entry(ptr, col, val, nv + I, I) : 0.0;
+  M[1][1] = entry(ptr, col, val, nv + I, nv + I);
+  M[0][2] = 1.0; M[0][3] = 0.0; M[1][2] = 0.0; M[1][3] = 1.0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double p = M[k][k];
+    if (!(p > 0.0)) ok = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) M[k][j] = M[k][j] / p;
+    const int i = 1 - k;
+    const double fi = M[i][k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) M[i][j] = M[i][j] - fi * M[k][j];
+  }
+  if (!ok) atomicAdd(bad, 1);
+  Dinv[I] = dv4_t{M[0][2], M[0][3], M[1][2], M[1][3]};
+}
+
+// rho_B = max over dofs of sum_j |(D_B^-1 A)_ij| (SMMP order: row I's terms
+// then row nv + I's; sorted-column abs sum of the nonzeros)
+__global__ __launch_bounds__(256) void block_rho_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ col,
+                                                        const double* __restrict__ val,
+                                                        const dv4_t* __restrict__ Dinv,
+                                                        unsigned long long* rho_bits) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * nv) return;
+  const int64_t I = i % nv, f = i / nv;
+  const dv4_t D = Dinv[I];
+  const double d0 = f ? D.z : D.x, d1 = f ? D.w : D.y;
+  int64_t a = ptr[I], ae = ptr[I + 1], b = ptr[nv + I], be = ptr[nv + I + 1];
+  double s = 0.0;
+  while (a < ae || b < be) {
+    const int64_t ja = a < ae ? col[a] : INT64_MAX, jb = b < be ? col[b] : INT64_MAX;
+    const int64_t j = min(ja, jb);
+    double v = 0.0;
+    if (ja == j) { v = v + d0 * val[a]; ++a; }
+    if (jb == j) { v = v + d1 * val[b]; ++b; }
+    if (v != 0.0) s += fabs(v) * 1.0;
+  }
+  atomicMax(rho_bits, (unsigned long long)__double_as_longlong(s));
+}
+
+__global__ __launch_bounds__(256) void scale_blocks_kernel(int64_t nv, double sc, const dv4_t* __restrict__ D,
+                                                           dv4_t* __restrict__ W) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  const dv4_t d = D[I];
+  W[I] = dv4_t{sc * d.x, sc * d.y, sc * d.z, sc * d.w};
+}
+
+// ---------------------------------------------------------------------------
+// hash SpGEMM, C = A B, one wavefront per row (see file header)
+// ---------------------------------------------------------------------------
+struct BCsr {               // B given as CSR
+  const int64_t* ptr;
+  const int32_t* col;
+  const double* val;
+  __device__ __forceinline__ int64_t len(int64_t k) const { return ptr[k + 1] - ptr[k]; }
+  __device__ __forceinline__ void get(int64_t k, int64_t t, int32_t* j, double* v) const {
+    const int64_t q = ptr[k] + t;
+    *j = col[q];
+    *v = val[q];
+  }
+};
+
+struct BTent {              // B = tentative prolongator: dof f nv + I -> f nagg + agg(I), 1.0
+  const int64_t* agg;
+  int64_t nv, nagg;
+  __device__ __forceinline__ int64_t len(int64_t k) const { return agg[k % nv] >= 0 ? 1 : 0; }
+  __device__ __forceinline__ void get(int64_t k, int64_t, int32_t* j, double* v) const {
+    *j = (int32_t)((k / nv) * nagg + agg[k % nv]);
+    *v = 1.0;
+  }
+};
+
+template <class BS>
+__global__ __launch_bounds__(256) void prod_count_kernel(int64_t n, const int64_t* __restrict__ aptr,
+                                                         const int32_t* __restrict__ acol, BS B,
+                                                         int64_t* __restrict__ ub) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t s = 0;
+  for (int64_t k = aptr[i]; k < aptr[i + 1]; ++k) s += B.len(acol[k]);
+  ub[i] = s;
+}
+
+__global__ __launch_bounds__(256) void bin_rows_kernel(int64_t n, const int64_t* __restrict__ ub, int64_t lim,
+                                                       int32_t* __restrict__ big, int* nbig) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && ub[i] > lim) big[atomicAdd(nbig, 1)] = (int32_t)i;
+}
+
+template <int TS, int WPB, bool FILL, class BS>
+__global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
+    int64_t nrows, const int32_t* __restrict__ rows, const int64_t* __restrict__ ub, int64_t lim,
+    const int64_t* __restrict__ aptr, const int32_t* __restrict__ acol, const double* __restrict__ aval,
+    BS B, int64_t* cptr, int32_t* __restrict__ ccol, double* __restrict__ cval, int* overflow) {
+  __shared__ int32_t keys[WPB][TS];
+  __shared__ double sums[WPB][TS];
+  __shared__ int32_t ck[WPB][TS];
+  __shared__ double cv[WPB][TS];
+  __shared__ int cnt[WPB];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  for (int64_t r = (int64_t)blockIdx.x * WPB + w; r < nrows; r += nw) {
+    const int64_t i = rows ? rows[r] : r;
+    if (!rows && ub[i] > lim) continue;          // binned to the large-table launch
+    for (int s = lane; s < TS; s += 64) { keys[w][s] = -1; sums[w][s] = 0.0; }
+    if (lane == 0) cnt[w] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    bool full = false;
+    for (int64_t kk = aptr[i]; kk < aptr[i + 1]; ++kk) {
+      const int64_t k = acol[kk];
+      const double a = aval[kk];
+      const int64_t len = B.len(k);
+      for (int64_t t0 = 0; t0 < len; t0 += 64) {
+        const int64_t t = t0 + lane;
+        if (t < len) {
+          int32_t j;
+          double bv;
+          B.get(k, t, &j, &bv);
+          uint32_t slot = ((uint32_t)j * 2654435761u) & (TS - 1);
+          int probes = 0;
+          for (;;) {
+            const int32_t cur = keys[w][slot];
+            if (cur == j) break;
+            if (cur == -1) {
+              const int32_t old = atomicCAS(&keys[w][slot], -1, j);
+              if (old == -1 || old == j) break;
+            }
+            slot = (slot + 1) & (TS - 1);
+            if (++probes >= TS) { full = true; break; }
+          }
+          if (!full) sums[w][slot] = sums[w][slot] + a * bv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    }
+    if (__any(full)) {
+      if (lane == 0) atomicAdd(overflow, 1);
+      continue;
+    }
+    // nonzero entries (scipy drops exact zeros), appended in any order
+    for (int s = lane; s < TS; s += 64) {
+      if (keys[w][s] != -1 && sums[w][s] != 0.0) {
+        const int q = atomicAdd(&cnt[w], 1);
+        ck[w][q] = keys[w][s];
+        cv[w][q] = sums[w][s];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int m = cnt[w];
+    if (!FILL) {
+      if (lane == 0) cptr[i + 1] = m;
+      continue;
+    }
+    const int64_t base = cptr[i];
+    for (int e = lane; e < m; e += 64) {     // rank sort by column
+      const int32_t key = ck[w][e];
+      int rank = 0;
+      for (int t = 0; t < m; ++t) rank += ck[w][t] < key;
+      ccol[base + rank] = key;
+      cval[base + rank] = cv[w][e];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// prolongator smoothing fused with the merge against T (setup.cpp
+// smooth_prolongator_block + smooth_merge): row i = f nv + I of
+// Y = D_B^-1 (A T) is the merge of (A T) rows I and nv + I (terms in that
+// order), scaled by w, then P_i = T_i - Y_i with zeros dropped
+// ---------------------------------------------------------------------------
+template <bool FILL>
+__global__ __launch_bounds__(256) void smooth_p_kernel(int64_t nv, const int64_t* __restrict__ tptr,
+                                                       const int32_t* __restrict__ tcol,
+                                                       const double* __restrict__ tval,
+                                                       const dv4_t* __restrict__ Dinv, const int64_t* __restrict__ agg,
+                                                       int64_t nagg, double w, int64_t* pptr,
+                                                       int32_t* __restrict__ pcol, double* __restrict__ pval) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * nv) return;
+  const int64_t I = i % nv, f = i / nv;
+  const dv4_t D = Dinv[I];
+  const double d0 = f ? D.z : D.x, d1 = f ? D.w : D.y;
+  const bool ht = agg[I] >= 0;
+  const int32_t tc = ht ? (int32_t)(f * nagg + agg[I]) : -1;
+  bool tdone = !ht;
+  int64_t o = FILL ? pptr[i] : 0;
+  int64_t a = tptr[I], ae = tptr[I + 1], b = tptr[nv + I], be = tptr[nv + I + 1];
+  while (a < ae || b < be) {
+    const int64_t ja = a < ae ? tcol[a] : INT64_MAX, jb = b < be ? tcol[b] : INT64_MAX;
+    const int64_t jj = min(ja, jb);
+    double y = 0.0;
+    if (ja == jj) { y = y + d0 * tval[a]; ++a; }
+    if (jb == jj) { y = y + d1 * tval[b]; ++b; }
+    if (y == 0.0) continue;                       // Y's exact zeros are dropped
+    const int32_t j = (int32_t)jj;
+    const double x = 1.0 * (w * y);
+    if (!tdone && tc < j) {
+      if (FILL) { pcol[o] = tc; pval[o] = 1.0; }
+      ++o;
+      tdone = true;
+    }
+    double r;
+    if (x == 0.0) {
+      if (!tdone && tc == j) { r = 1.0; tdone = true; } else continue;
+    } else if (!tdone && tc == j) {
+      r = 1.0 - x; tdone = true;
+    } else {
+      r = 0.0 - x;
+    }
+    if (r != 0.0) {
+      if (FILL) { pcol[o] = j; pval[o] = r; }
+      ++o;
+    }
+  }
+  if (!tdone) {
+    if (FILL) { pcol[o] = tc; pval[o] = 1.0; }
+    ++o;
+  }
+  if (!FILL) pptr[i + 1] = o;
+}
+
+// unsmoothed aggregation: P = T
+__global__ __launch_bounds__(256) void tent_kernel(int64_t n, int64_t nv, const int64_t* __restrict__ agg,
+                                                   int64_t nagg, int64_t* __restrict__ pptr,
+                                                   int32_t* __restrict__ pcol, double* __restrict__ pval, int pass) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t I = i % nv, f = i / nv;
+  if (pass == 0) { pptr[i + 1] = agg[I] >= 0 ? 1 : 0; return; }
+  if (agg[I] >= 0) { pcol[pptr[i]] = (int32_t)(f * nagg + agg[I]); pval[pptr[i]] = 1.0; }
+}
+
+// ---------------------------------------------------------------------------
+// transpose helpers: row index of every entry, column counts, gather
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void entry_rows_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         int64_t* __restrict__ idx, int64_t* __restrict__ colcnt,
+                                                         const int32_t* __restrict__ col) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+    idx[k] = k;
+    atomicAdd((unsigned long long*)&colcnt[col[k] + 1], 1ull);
+  }
+}
+
+__global__ __launch_bounds__(256) void row_of_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                     int32_t* __restrict__ rowof) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) rowof[k] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(256) void transpose_gather_kernel(int64_t nnz, const int64_t* __restrict__ perm,
+                                                               const int32_t* __restrict__ rowof,
+                                                               const double* __restrict__ val,
+                                                               int32_t* __restrict__ rcol, double* __restrict__ rval) {
+  const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (d >= nnz) return;
+  const int64_t k = perm[d];
+  rcol[d] = rowof[k];
+  rval[d] = val[k];
+}
+
+// ---------------------------------------------------------------------------
+// coarsest level: dense matrix + Gauss-Jordan (setup.cpp gauss_jordan)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dense_init_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val, double* __restrict__ M) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t w = 2 * n;
+  for (int64_t j = 0; j < w; ++j) M[i * w + j] = 0.0;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) M[i * w + col[k]] = val[k];
+  M[i * w + n + i] = 1.0;
+}
+
+// pivot p = M[k][k] into f[n], multipliers f[i] = M[i][k] (f[k] = 0); rows
+// i != k are untouched by the row-k scaling, so reading them first is exact
+__global__ __launch_bounds__(256) void gj_col_kernel(int64_t n, int64_t k, const double* M, double* f) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) f[i] = i == k ? 0.0 : M[i * 2 * n + k];
+  if (i == k) f[n] = M[k * 2 * n + k];
+}
+
+__global__ __launch_bounds__(256) void gj_scale_kernel(int64_t n, int64_t k, double* M, const double* f, int* bad) {
+  const int64_t w = 2 * n;
+  const double p = f[n];
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < w) {
+    if (j == 0 && !(p > 0.0)) atomicAdd(bad, 1);
+    M[k * w + j] = M[k * w + j] / p;
+  }
+}
+
+__global__ __launch_bounds__(256) void gj_elim_kernel(int64_t n, int64_t k, double* M, const double* f) {
+  const int64_t w = 2 * n;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * w) return;
+  const int64_t i = t / w, j = t % w;
+  if (i == k) return;
+  M[i * w + j] = M[i * w + j] - f[i] * M[k * w + j];
+}
+
+__global__ __launch_bounds__(256) void gj_extract_kernel(int64_t n, const double* __restrict__ M,
+                                                         double* __restrict__ inv) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * n) return;
+  const int64_t i = t / n, j = t % n;
+  inv[t] = M[i * 2 * n + n + j];
+}
+
+// input check (setup.cpp host_setup): monotone row pointers, columns in
+// range and strictly increasing within each row
+__global__ __launch_bounds__(256) void validate_kernel(int64_t n, int64_t m, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, int* bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t a = ptr[i], b = ptr[i + 1];
+  int nb = b < a;
+  for (int64_t k = a; k < b && !nb; ++k) {
+    const int32_t c = col[k];
+    nb |= (c < 0 || c >= m || (k > a && c <= col[k - 1]));
+  }
+  if (nb) atomicAdd(bad, 1);
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+struct Clock {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  double lap() {
+    const auto t = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(t - t0).count();
+    t0 = t;
+    return ms;
+  }
+};
+
+int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
+
+// exact output size + row pointers + entries of C = A B (hash SpGEMM)
+template <class BS>
+int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
+  constexpr int TS1 = 512, TS2 = 2048;
+  constexpr int64_t LIM1 = 384;
+  const int64_t n = A.n;
+  Scratch S;
+  int64_t* ub = nullptr;
+  int32_t* big = nullptr;
+  int* ctr = nullptr;   // [0] nbig, [1] overflow
+  RCHK(S.alloc(&ub, n, err));
+  RCHK(S.alloc(&big, n, err));
+  RCHK(S.alloc(&ctr, 2, err));
+  HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
+  prod_count_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, B, ub);
+  bin_rows_kernel<<<nblk(n), 256>>>(n, ub, LIM1, big, ctr);
+  HIPCHK(hipGetLastError());
+  int nbig = 0;
+  RCHK(read_int(ctr, &nbig, err));
+  C->n = n;
+  C->m = ncols;
+  RCHK(galloc(G, &C->ptr, n + 1, err));
+  HIPCHK(hipMemset(C->ptr, 0, (n + 1) * sizeof(int64_t)));
+  const unsigned g1 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 3) / 4), 65536);
+  const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      RCHK(dscan_incl_i64(C->ptr, C->ptr, n + 1, nullptr, err));
+      RCHK(to_host(&C->nnz, C->ptr + n, 1, err));
+      RCHK(galloc(G, &C->col, C->nnz, err));
+      RCHK(galloc(G, &C->val, C->nnz, err));
+    }
+    if (pass == 0) {
+      spgemm_kernel<TS1, 4, false><<<g1, 256>>>(n, nullptr, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
+                                                 nullptr, nullptr, ctr + 1);
+      if (nbig)
+        spgemm_kernel<TS2, 1, false><<<g2, 64>>>(nbig, big, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
+                                                  nullptr, nullptr, ctr + 1);
+    } else {
+      spgemm_kernel<TS1, 4, true><<<g1, 256>>>(n, nullptr, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
+                                                C->col, C->val, ctr + 1);
+      if (nbig)
+        spgemm_kernel<TS2, 1, true><<<g2, 64>>>(nbig, big, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
+                                                 C->col, C->val, ctr + 1);
+    }
+    HIPCHK(hipGetLastError());
+    int ovf = 0;
+    RCHK(read_int(ctr + 1, &ovf, err));
+    if (ovf) {
+      *err = "GPU SpGEMM: " + std::to_string(ovf) + " row(s) with more than 2048 distinct columns "
+             "(use the host setup, mamg_setup)";
+      return MAMG_ERR_UNSUPPORTED;
+    }
+  }
+  return MAMG_OK;
+}
+
+// R = P^T (setup.cpp transpose: counting order == stable sort by column)
+int transpose(GHier* G, const DevMat& P, DevMat* R, std::string* err) {
+  Scratch S;
+  const int64_t nnz = P.nnz;
+  R->n = P.m;
+  R->m = P.n;
+  R->nnz = nnz;
+  RCHK(galloc(G, &R->ptr, P.m + 1, err));
+  RCHK(galloc(G, &R->col, nnz, err));
+  RCHK(galloc(G, &R->val, nnz, err));
+  HIPCHK(hipMemset(R->ptr, 0, (P.m + 1) * sizeof(int64_t)));
+  int64_t *idx = nullptr, *perm = nullptr;
+  int32_t *keys = nullptr, *rowof = nullptr;
+  RCHK(S.alloc(&idx, nnz, err));
+  RCHK(S.alloc(&perm, nnz, err));
+  RCHK(S.alloc(&keys, nnz, err));
+  RCHK(S.alloc(&rowof, nnz, err));
+  entry_rows_kernel<<<nblk(P.n), 256>>>(P.n, P.ptr, idx, R->ptr, P.col);
+  row_of_kernel<<<nblk(P.n), 256>>>(P.n, P.ptr, rowof);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(R->ptr, R->ptr, P.m + 1, nullptr, err));
+  int bits = 1;
+  while ((int64_t(1) << bits) < P.m && bits < 32) ++bits;
+  RCHK(dsort_pairs_i32_i64(P.col, keys, idx, perm, nnz, bits, nullptr, err));
+  transpose_gather_kernel<<<nblk(nnz), 256>>>(nnz, perm, rowof, P.val, R->col, R->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+// W = (relax / rho_B) D_B^-1 and rho_B for node blocks D
+int block_rho(const DevMat& A, int64_t nv, const dv4_t* D, double* rho, std::string* err) {
+  Scratch S;
+  unsigned long long* rb = nullptr;
+  RCHK(S.alloc(&rb, 1, err));
+  HIPCHK(hipMemset(rb, 0, sizeof(unsigned long long)));
+  block_rho_kernel<<<nblk(2 * nv), 256>>>(nv, A.ptr, A.col, A.val, D, rb);
+  HIPCHK(hipGetLastError());
+  unsigned long long h = 0;
+  RCHK(to_host(&h, rb, 1, err));
+  std::memcpy(rho, &h, sizeof(double));
+  return MAMG_OK;
+}
+
+int node_inverse(const DevMat& A, int64_t nv, const uint8_t* joined, dv4_t* D, const char* what,
+                 std::string* err) {
+  Scratch S;
+  int* bad = nullptr;
+  RCHK(S.alloc(&bad, 1, err));
+  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  node_inverse_kernel<<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, joined, D, bad);
+  HIPCHK(hipGetLastError());
+  int hb = 0;
+  RCHK(read_int(bad, &hb, err));
+  if (hb) { *err = std::string(what) + " block not SPD (non-positive pivot)"; return MAMG_ERR_SETUP; }
+  return MAMG_OK;
+}
+
+// aggregation of the node graph of A (setup.cpp node_graph + strength + aggregate_mis2)
+int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, int64_t** agg_out,
+              int64_t* nagg_out, std::string* err) {
+  Scratch S;
+  DevMat Gr;
+  Gr.n = Gr.m = nv;
+  RCHK(S.alloc(&Gr.ptr, nv + 1, err));
+  HIPCHK(hipMemset(Gr.ptr, 0, sizeof(int64_t)));
+  node_graph_kernel<false><<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
+  RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
+  RCHK(S.alloc(&Gr.col, Gr.nnz, err));
+  RCHK(S.alloc(&Gr.val, Gr.nnz, err));
+  node_graph_kernel<true><<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+  double* d = nullptr;
+  uint8_t *flag = nullptr, *nonisol = nullptr;
+  int* ctr = nullptr;
+  RCHK(S.alloc(&d, nv, err));
+  RCHK(S.alloc(&flag, Gr.nnz, err));
+  RCHK(S.alloc(&nonisol, nv, err));
+  RCHK(S.alloc(&ctr, 2, err));
+  HIPCHK(hipMemset(flag, 0, std::max<int64_t>(Gr.nnz, 1)));
+  HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
+  absdiag_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d);
+  strength_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d, theta, flag, ctr);
+  HIPCHK(hipGetLastError());
+  int nextra = 0;
+  RCHK(read_int(ctr, &nextra, err));
+  if (nextra) {
+    *err = "GPU setup: strength graph has entries without a mirror (non-symmetric sparsity "
+           "pattern); use the host setup (mamg_setup)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  uint64_t *state = nullptr, *low = nullptr, *key = nullptr, *m1 = nullptr;
+  unsigned long long* und = nullptr;
+  RCHK(S.alloc(&state, nv, err));
+  RCHK(S.alloc(&low, nv, err));
+  RCHK(S.alloc(&key, nv, err));
+  RCHK(S.alloc(&m1, nv, err));
+  RCHK(S.alloc(&und, 1, err));
+  mis_init_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, flag, level, state, low, nonisol);
+  for (int rounds = 0;; ++rounds) {
+    if (rounds > 10000) { *err = "mis2 did not converge"; return MAMG_ERR_SETUP; }
+    HIPCHK(hipMemset(und, 0, sizeof(unsigned long long)));
+    mis_key_kernel<<<nblk(nv), 256>>>(nv, state, low, key, und);
+    HIPCHK(hipGetLastError());
+    unsigned long long hu = 0;
+    RCHK(to_host(&hu, und, 1, err));
+    if (hu == 0) break;
+    mis_max_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, key, m1);
+    mis_update_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
+  }
+  int64_t *f = nullptr, *agg = nullptr, *agg2 = nullptr, *agg3 = nullptr;
+  RCHK(S.alloc(&f, nv, err));
+  RCHK(S.alloc(&agg, nv, err));
+  RCHK(S.alloc(&agg2, nv, err));
+  RCHK(galloc(G, &agg3, nv, err));
+  root_flag_kernel<<<nblk(nv), 256>>>(nv, state, f);
+  RCHK(dscan_incl_i64(f, f, nv, nullptr, err));
+  int64_t nroots = 0;
+  RCHK(to_host(&nroots, f + nv - 1, 1, err));
+  root_number_kernel<<<nblk(nv), 256>>>(nv, state, f, agg);
+  agg_phase2_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, state, agg, agg2);
+  agg_phase3_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, flag, nonisol, agg2, agg3, ctr + 1);
+  HIPCHK(hipGetLastError());
+  int bad = 0;
+  RCHK(read_int(ctr + 1, &bad, err));
+  if (bad) { *err = "aggregation left a non-isolated node unassigned"; return MAMG_ERR_SETUP; }
+  *agg_out = agg3;
+  *nagg_out = nroots;
+  return MAMG_OK;
+}
+
+int coarsest_inverse(GHier* G, const DevMat& A, double** inv_out, std::string* err) {
+  Scratch S;
+  const int64_t n = A.n, w = 2 * n;
+  double *M = nullptr, *f = nullptr, *inv = nullptr;
+  int* bad = nullptr;
+  RCHK(S.alloc(&M, n * w, err));
+  RCHK(S.alloc(&f, n + 1, err));
+  RCHK(S.alloc(&bad, 1, err));
+  RCHK(galloc(G, &inv, n * n, err));
+  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  dense_init_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, M);
+  for (int64_t k = 0; k < n; ++k) {
+    gj_col_kernel<<<nblk(n), 256>>>(n, k, M, f);
+    gj_scale_kernel<<<nblk(w), 256>>>(n, k, M, f, bad);
+    gj_elim_kernel<<<nblk(n * w), 256>>>(n, k, M, f);
+  }
+  gj_extract_kernel<<<nblk(n * n), 256>>>(n, M, inv);
+  HIPCHK(hipGetLastError());
+  int hb = 0;
+  RCHK(read_int(bad, &hb, err));
+  if (hb) { *err = "coarsest matrix not SPD"; return MAMG_ERR_SETUP; }
+  *inv_out = inv;
+  return MAMG_OK;
+}
+
+}  // namespace
+
+int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mamg_params& p, GHier* G,
+              std::string* err) {
+  int rc = check_params(p, err);
+  if (rc) return rc;
+  if (p.num_functions != 2 || !p.node_block_smoother || (p.AMG_type == MAMG_SA_AMG && !p.sa_block_diag)) {
+    *err = "GPU setup covers the nodal 2-field profile (num_functions 2, node_block_smoother 1, "
+           "sa_block_diag 1); use the host setup (mamg_setup) for other profiles";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  if (A0.n != A0.m || A0.n <= 0 || A0.n % 2) { *err = "A must be square with an even size"; return MAMG_ERR_ARG; }
+  G->params = p;
+  G->device = p.device;
+  G->levels.clear();
+  HIPCHK(hipSetDevice(p.device));
+  Clock clk, tot;
+  {
+    Scratch S;
+    int* bad = nullptr;
+    RCHK(S.alloc(&bad, 1, err));
+    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    validate_kernel<<<nblk(A0.n), 256>>>(A0.n, A0.m, A0.ptr, A0.col, bad);
+    HIPCHK(hipGetLastError());
+    int hb = 0;
+    RCHK(read_int(bad, &hb, err));
+    if (hb) {
+      *err = "rowptr not monotone, or column index out of range or not strictly increasing within a row";
+      return MAMG_ERR_ARG;
+    }
+  }
+  DevMat cur = A0;
+  for (int l = 0; l < p.max_levels; ++l) {
+    G->levels.emplace_back();
+    GLevel& L = G->levels.back();
+    if (l > 0) L.A = cur;
+    const int64_t n = cur.n, nv = n / 2;
+    L.n = n;
+    bool last = (n <= p.coarse_dof) || (l == p.max_levels - 1);
+    int64_t* agg = nullptr;
+    int64_t nagg = 0;
+    if (n % 2) { *err = "matrix size not divisible by num_functions"; return MAMG_ERR_ARG; }
+    clk.lap();
+    if (!last) {
+      RCHK(aggregate(G, cur, nv, l, p.strong_coupled, &agg, &nagg, err));
+      if (nagg == 0 || 2 * nagg >= n) last = true;
+    }
+    G->phase_ms[0] += clk.lap();
+    if (last) {
+      if (n > p.max_coarse_dense) {
+        *err = "coarsest level " + std::to_string(n) + " too large for dense solve";
+        return MAMG_ERR_SETUP;
+      }
+      RCHK(coarsest_inverse(G, cur, &L.Ainv, err));
+      L.coarsest = true;
+      G->phase_ms[4] += clk.lap();
+      break;
+    }
+    L.agg = agg;
+    L.nagg = nagg;
+    // smoother blocks (level 0: seed blocks from idofs when node-aligned)
+    Scratch S;
+    dv4_t* Dsm = nullptr;
+    RCHK(S.alloc(&Dsm, nv, err));
+    const bool seeds = l < p.Schwarz_levels && l == 0 && idofs != nullptr && n_idofs > 0;
+    if (seeds) {
+      int32_t* di = nullptr;
+      uint8_t* isseed = nullptr;
+      int64_t* best = nullptr;
+      int* bad = nullptr;
+      RCHK(S.alloc(&di, n_idofs, err));
+      RCHK(S.alloc(&isseed, n, err));
+      RCHK(S.alloc(&best, n, err));
+      RCHK(S.alloc(&bad, 2, err));
+      RCHK(galloc(G, &L.joined, nv, err));
+      HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIPCHK(hipMemset(isseed, 0, n));
+      HIPCHK(hipMemset(bad, 0, 2 * sizeof(int)));
+      seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
+      best_seed_kernel<<<nblk(n), 256>>>(n, cur.ptr, cur.col, cur.val, isseed, best);
+      seed_align_kernel<<<nblk(nv), 256>>>(nv, isseed, best, p.Schwarz_mmsize, L.joined, bad + 1);
+      HIPCHK(hipGetLastError());
+      int hb[2] = {0, 0};
+      RCHK(to_host(hb, bad, 2, err));
+      if (hb[0]) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+      if (hb[1]) {
+        *err = "GPU setup: the idofs seed blocks are not node-aligned (a dof joins another node's "
+               "seed); use the host setup (mamg_setup)";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+      RCHK(node_inverse(cur, nv, L.joined, Dsm, "smoother", err));
+    } else {
+      RCHK(node_inverse(cur, nv, nullptr, Dsm, "smoother", err));
+    }
+    double rho_sm = 0.0;
+    RCHK(block_rho(cur, nv, Dsm, &rho_sm, err));
+    RCHK(galloc(G, (dv4_t**)&L.W, nv, err));
+    scale_blocks_kernel<<<nblk(nv), 256>>>(nv, p.relaxation / rho_sm, Dsm, (dv4_t*)L.W);
+    HIPCHK(hipGetLastError());
+    G->phase_ms[1] += clk.lap();
+    // prolongator
+    if (p.AMG_type == MAMG_SA_AMG) {
+      dv4_t* Dsa = Dsm;
+      double rho_sa = rho_sm;
+      if (seeds) {                  // SA always smooths with the full node blocks
+        RCHK(S.alloc(&Dsa, nv, err));
+        RCHK(node_inverse(cur, nv, nullptr, Dsa, "SA node", err));
+        RCHK(block_rho(cur, nv, Dsa, &rho_sa, err));
+      }
+      const double w = p.sa_omega / rho_sa;
+      L.w_sa = w;
+      GHier tmp;                    // A T lives only until P is built
+      DevMat AT;
+      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, 2 * nagg, &AT, err));
+      L.P.n = n;
+      L.P.m = 2 * nagg;
+      RCHK(galloc(G, &L.P.ptr, n + 1, err));
+      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      smooth_p_kernel<false><<<nblk(n), 256>>>(nv, AT.ptr, AT.col, AT.val, Dsa, agg, nagg, w, L.P.ptr,
+                                               nullptr, nullptr);
+      HIPCHK(hipGetLastError());
+      RCHK(dscan_incl_i64(L.P.ptr, L.P.ptr, n + 1, nullptr, err));
+      RCHK(to_host(&L.P.nnz, L.P.ptr + n, 1, err));
+      RCHK(galloc(G, &L.P.col, L.P.nnz, err));
+      RCHK(galloc(G, &L.P.val, L.P.nnz, err));
+      smooth_p_kernel<true><<<nblk(n), 256>>>(nv, AT.ptr, AT.col, AT.val, Dsa, agg, nagg, w, L.P.ptr,
+                                              L.P.col, L.P.val);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipDeviceSynchronize());
+    } else {
+      L.P.n = n;
+      L.P.m = 2 * nagg;
+      RCHK(galloc(G, &L.P.ptr, n + 1, err));
+      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      tent_kernel<<<nblk(n), 256>>>(n, nv, agg, nagg, L.P.ptr, nullptr, nullptr, 0);
+      RCHK(dscan_incl_i64(L.P.ptr, L.P.ptr, n + 1, nullptr, err));
+      RCHK(to_host(&L.P.nnz, L.P.ptr + n, 1, err));
+      RCHK(galloc(G, &L.P.col, L.P.nnz, err));
+      RCHK(galloc(G, &L.P.val, L.P.nnz, err));
+      tent_kernel<<<nblk(n), 256>>>(n, nv, agg, nagg, L.P.ptr, L.P.col, L.P.val, 1);
+      HIPCHK(hipGetLastError());
+    }
+    G->phase_ms[2] += clk.lap();
+    // Galerkin: R = P^T, A P, A_c = R (A P)
+    RCHK(transpose(G, L.P, &L.R, err));
+    RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err));
+    DevMat next;
+    RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err));
+    if (!p.post_fusion) {
+      for (void* q : {(void*)L.AP.ptr, (void*)L.AP.col, (void*)L.AP.val}) G->release(q);
+      L.AP = DevMat();
+    }
+    HIPCHK(hipDeviceSynchronize());
+    G->phase_ms[3] += clk.lap();
+    if (p.print_level > 0)
+      std::fprintf(stderr, "[mamg gpu] level %d: n=%lld nnz=%lld nagg=%lld nnzP=%lld\n", l, (long long)n,
+                   (long long)cur.nnz, (long long)nagg, (long long)L.P.nnz);
+    cur = next;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  G->phase_ms[6] = tot.lap();
+  return MAMG_OK;
+}
+
+int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
+  HIPCHK(hipSetDevice(G->device));
+  Clock clk;
+  D->n = A.n;
+  D->m = A.m;
+  D->nnz = A.nnz();
+  RCHK(galloc(G, &D->ptr, A.n + 1, err));
+  RCHK(galloc(G, &D->col, D->nnz, err));
+  RCHK(galloc(G, &D->val, D->nnz, err));
+  HIPCHK(hipMemcpy(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (D->nnz) {
+    HIPCHK(hipMemcpy(D->col, A.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, A.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
+  }
+  G->phase_ms[GS_UPLOAD] = clk.lap();
+  return MAMG_OK;
+}
+
+int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string* err) {
+  H->params = G.params;
+  H->A0 = A0;
+  H->levels.clear();
+  auto dl = [&](const DevMat& M, Csr* C) -> int {
+    C->n = M.n;
+    C->m = M.m;
+    C->ptr.resize(M.n + 1);
+    C->col.resize(M.nnz);
+    C->val.resize(M.nnz);
+    RCHK(to_host(C->ptr.data(), M.ptr, M.n + 1, err));
+    RCHK(to_host(C->col.data(), M.col, M.nnz, err));
+    RCHK(to_host(C->val.data(), M.val, M.nnz, err));
+    return MAMG_OK;
+  };
+  for (size_t l = 0; l < G.levels.size(); ++l) {
+    const GLevel& g = G.levels[l];
+    H->levels.emplace_back();
+    HostLevel& h = H->levels.back();
+    h.n = g.n;
+    h.coarsest = g.coarsest;
+    if (l > 0) RCHK(dl(g.A, &h.A));
+    if (g.coarsest) {
+      h.Ainv.resize(g.n * g.n);
+      RCHK(to_host(h.Ainv.data(), g.Ainv, g.n * g.n, err));
+      break;
+    }
+    const int64_t nv = g.n / 2;
+    RCHK(dl(g.P, &h.P));
+    RCHK(dl(g.R, &h.R));
+    if (g.AP.n) RCHK(dl(g.AP, &h.AP));
+    h.agg.resize(nv);
+    RCHK(to_host(h.agg.data(), g.agg, nv, err));
+    h.nagg = g.nagg;
+    h.w_sa = g.w_sa;
+    // smoother as the host's block CSR: node blocks {I, nv + I} (2 entries per
+    // row), or singletons where level-0 seed blocks split a node
+    std::vector<double> W(4 * nv);
+    std::vector<uint8_t> jn(nv, 1);
+    RCHK(to_host(W.data(), g.W, 4 * nv, err));
+    if (g.joined) RCHK(to_host(jn.data(), g.joined, nv, err));
+    Csr& B = h.WB;
+    B.n = B.m = g.n;
+    B.ptr.assign(g.n + 1, 0);
+    for (int64_t i = 0; i < g.n; ++i) B.ptr[i + 1] = B.ptr[i] + (jn[i % nv] ? 2 : 1);
+    B.col.resize(B.ptr[g.n]);
+    B.val.resize(B.ptr[g.n]);
+    for (int64_t i = 0; i < g.n; ++i) {
+      const int64_t I = i % nv, f = i / nv;
+      int64_t o = B.ptr[i];
+      if (jn[I]) {
+        B.col[o] = (int32_t)I; B.val[o] = W[4 * I + 2 * f];
+        B.col[o + 1] = (int32_t)(nv + I); B.val[o + 1] = W[4 * I + 2 * f + 1];
+      } else {
+        B.col[o] = (int32_t)i; B.val[o] = W[4 * I + 3 * f];
+      }
+    }
+  }
+  return MAMG_OK;
+}
+
+}  // namespace mamg

@@ -1,0 +1,145 @@
+"""GPU setup (mamg_setup_gpu, csrc/gsetup.hip) against the host setup.
+
+Contract: for the nodal 2-field profile the GPU
+builds the SAME hierarchy as the C++ host setup, bit for bit -- node graph,
+strength, MIS-2 aggregates, smoother blocks, SA prolongator, R = P^T,
+Galerkin coarse operators, coarsest inverse -- and the host setup is itself
+bitwise equal to the oracle (tests/test_host_setup.py, tests/test_golden.py).
+So: every exported level array is np.array_equal, and an apply through a
+GPU-setup handle equals the host-setup handle's apply exactly (same device
+kernels on identical bits), hence the oracle's to 1e-10.
+"""
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+
+def _mamg():
+    import metric_amg_examples_amd as M
+    return M
+
+
+CASES = [
+    (2, 32, 1.0, dict()),
+    (2, 64, 1e6, dict()),
+    (3, 8, 1e6, dict()),
+    (3, 16, 1e4, dict()),
+    (3, 16, 1e10, dict()),
+    (3, 16, 1e2, dict(strong_coupled=0.08)),
+    (2, 32, 1e3, dict(AMG_type=1)),                 # UA: P = T
+    (3, 16, 1e6, dict(post_fusion=0)),
+    (2, 32, 1e3, dict(Schwarz_mmsize=1)),           # level-0 seed blocks split into singletons
+    (2, 64, 1e4, dict(coarse_dof=400, max_levels=3)),
+]
+
+
+def hierarchies_equal(Hh, Hg):
+    assert Hh.num_levels == Hg.num_levels
+    for l in range(Hh.num_levels):
+        a, b = Hh.level(l, with_A=(l > 0)), Hg.level(l, with_A=(l > 0))
+        assert a.keys() == b.keys(), (l, a.keys(), b.keys())
+        for k in a:
+            if k == 'n':
+                assert a[k] == b[k]
+                continue
+            x, y = a[k], b[k]
+            if isinstance(x, tuple):
+                for u, v in zip(x[:3], y[:3]):
+                    assert np.array_equal(u, v), (l, k)
+                assert x[3] == y[3]
+            else:
+                assert np.array_equal(x, y), (l, k)
+
+
+@pytest.mark.parametrize('dim,n,g,kw', CASES)
+def test_gpu_hierarchy_bitwise_equals_host(lib_built, dim, n, g, kw):
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    Hh = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **kw)
+    Hg = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True, **kw)
+    hierarchies_equal(Hh, Hg)
+    Hh.close()
+    Hg.close()
+
+
+@pytest.mark.parametrize('dim,n,g,kw', CASES)
+def test_gpu_setup_apply_bitwise_equals_host_setup(lib_built, dim, n, g, kw):
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    Bg = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu', **kw)
+    Bh = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='host', **kw)
+    assert Bg.setup_path == 'gpu' and Bh.setup_path == 'host'
+    assert Bg.num_levels == Bh.num_levels
+    for lv in range(Bg.num_levels):
+        assert Bg.level_format(lv) == Bh.level_format(lv)
+    for seed in (1234, 7):
+        r = mo.seeded_rhs(s.N, seed)
+        assert np.array_equal(Bg * r, Bh * r)
+    oracle_kw = {k: v for k, v in kw.items() if k != 'post_fusion'}
+    if 'AMG_type' in oracle_kw:
+        oracle_kw['AMG_type'] = {1: 'UA', 2: 'SA'}[oracle_kw['AMG_type']]
+    h = mo.setup(A, mo.Params(num_functions=2, **oracle_kw), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    tol = 1e-10 if g < 1e8 else 1e-8
+    assert np.linalg.norm(Bg * r - zo) / np.linalg.norm(zo) < tol
+    t = Bg.setup_timings
+    assert t['setup_total'] > 0 and t['layout'] > 0
+
+
+def test_gpu_setup_device_input_and_pcg(lib_built):
+    """A handed over in HBM (torch tensors): same handle bits; PCG through it
+    takes the oracle's iteration count."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    dA = (torch.as_tensor(s.indptr).cuda(), torch.as_tensor(s.indices).cuda(),
+          torch.as_tensor(s.data).cuda())
+    Bd = M.MetricAMG(dA, s.W, idofs=s.idofs, num_functions=2)
+    Bh = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='host')
+    r = mo.seeded_rhs(s.N)
+    assert np.array_equal(Bd * r, Bh * r)
+    Bd._Aop = A
+    solver = M.ConjGrad(A, precond=Bd, tolerance=1e-8, maxiter=500)
+    solver * r
+    ref = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs), r, 1e-8, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+
+
+def test_gpu_setup_rejects_unsupported_and_bad_input(lib_built):
+    M = _mamg()
+    s = M.problems.bidomain(2, 16, 1e3)
+    A = s.scipy()
+    with pytest.raises(M._lib.MamgError) as ei:           # scalar profile
+        M.MetricAMG(A, setup='gpu')
+    assert ei.value.code == -4
+    # 'auto' picks the host setup for it (recorded)
+    B = M.MetricAMG(A)
+    assert B.setup_path == 'host'
+    # seeds that are not node-aligned (every 3rd dof): GPU refuses, auto records why
+    idofs = np.arange(0, s.N, 3, dtype=np.int32)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.MetricAMG(A, s.W, idofs=idofs, num_functions=2, setup='gpu')
+    assert ei.value.code == -4
+    B = M.MetricAMG(A, s.W, idofs=idofs, num_functions=2)
+    assert B.setup_path.startswith('host (') and 'node-aligned' in B.setup_path
+    # unsorted columns in a row
+    ip, ix, dv = s.indptr.copy(), s.indices.copy(), s.data.copy()
+    ix[ip[5]], ix[ip[5] + 1] = ix[ip[5] + 1], ix[ip[5]]
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.MetricAMG((ip, ix, dv), s.W, idofs=s.idofs, num_functions=2, setup='gpu')
+    assert ei.value.code == -1
+
+
+def test_gpu_setup_large_3d_bitwise(lib_built):
+    """bidomain_3d n=64 (N = 550k): the whole hierarchy bitwise equal."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 64, 1e6)
+    Hh = M.HostHierarchy(s, idofs=s.idofs, num_functions=2)
+    Hg = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True)
+    hierarchies_equal(Hh, Hg)
