@@ -5,10 +5,12 @@ Drop-in for the reference's `metric_mono` hot path:
     BB = metricAMG(AA_, W, idofs=interface_dofs, parameters=parameters.parameters_metric_mi355x)
     AAinv = ConjGrad(AA_, precond=BB, tolerance=1e-8, maxiter=500)
     xx = AAinv * bb_
+Block form (src/utils.py:45-53): precond.get_hazmath_metric_precond -> R.T * Minv * R.
+File boundary (src/utils.py:304-333, src/run_solver_3d1d.py): fileio, drivers.
 """
-from . import _lib, parameters, problems
+from . import _lib, fileio, parameters, precond, problems
 from .amg import DistMetricAMG, DistPlan, HostHierarchy, MetricAMG, metricAMG
 from .krylov import ConjGrad, lanczos_eigenvalues
 
-__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'ConjGrad', 'lanczos_eigenvalues',
-           'parameters', 'problems', '_lib']
+__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'ConjGrad',
+           'lanczos_eigenvalues', 'parameters', 'problems', 'precond', 'fileio', '_lib']

@@ -252,6 +252,9 @@ class MetricAMG:
         return y
 
     def __mul__(self, r):
+        if getattr(r, '_mamg_operator', False):      # Minv * R (block form, src/utils.py:53)
+            from .precond import _Product
+            return _Product([self, r])
         return self.matvec(r)
 
     __call__ = matvec

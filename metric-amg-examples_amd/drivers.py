@@ -1,0 +1,240 @@
+"""Problem drivers: the reference's command lines on this framework.
+
+    python -m metric_amg_examples_amd.drivers bidomain_3d -nrefs 6 -gamma 1e6 -precond metric_mono
+    python -m metric_amg_examples_amd.drivers emi_3d -nrefs 5 -gamma 1e6 -precond metric
+    python -m metric_amg_examples_amd.drivers emi_3d1d -gamma 1e4 -radius 1.0 -dump 1 -outdir D/
+    python -m metric_amg_examples_amd.drivers run_solver_3d1d -infile input_metric.dat -indir D/ -outdir O/
+
+Each mirrors a reference script's CLI and output:
+  bidomain_2d / bidomain_3d   src/bidomain_2d.py:105-278, src/bidomain_3d.py:52-220
+  emi_2d / emi_3d             src/emi_2d.py:133-263, src/emi_3d.py:60-196
+  emi_3d1d                    src/emi_3d1d.py:99-167 (dump / solve)
+  run_solver_3d1d             src/run_solver_3d1d.py:17-38 (HAZmath file-based solve)
+Mesh loops: n = 2^i for i in [5, 5+nrefs) (bidomain 2-D), [3, 3+nrefs)
+(bidomain 3-D), [6, 6+nrefs) (EMI 2-D), [2, 2+nrefs) (EMI 3-D).  Every solve
+appends the reference's iters row ``ndofs niters cond timeKSP r h``
+(src/bidomain_2d.py:149,259) to results/<problem>/iters_<...>.txt; timeKSP
+spans preconditioner setup + CG, as in the reference (:176-197).
+Differences (stated, not hidden): the matrices come from the in-library
+generators (problems.py; FEniCS is absent), the right-hand side is the seeded
+uniform(-1,1) vector instead of the manufactured solution's load, so the H1
+error tables are not produced; the 3D-1D neuron mesh is the synthetic
+``problems.neuron_curve``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+from . import fileio, parameters as P, problems
+from .amg import MetricAMG
+from .krylov import ConjGrad
+from .precond import (get_block_diag_precond, get_hazmath_amg_precond, get_hazmath_metric_precond,
+                      get_hazmath_metric_precond_mono)
+
+HEADERS_KSP = ['ndofs', 'niters', 'cond', 'timeKSP', 'r', 'h']
+
+
+def _iters_path(result_dir, precond, **kv):
+    tail = '_'.join('%s%s' % (k, v) for k, v in kv.items())
+    return os.path.join(result_dir, 'iters_precond%s_%s.txt' % (precond, tail))
+
+
+def _append(path, row, first):
+    with open(path, 'w' if first else 'a') as out:
+        if first:
+            out.write('%s\n' % ' '.join(HEADERS_KSP))
+        out.write('%s\n' % ' '.join(map(str, row)))
+
+
+def _solve(A, W, b, precond, idofs, tol, maxiter, monolithic_params=None):
+    """setup + CG, timed together (the reference's timeKSP)."""
+    then = time.time()
+    Asp = A.scipy() if hasattr(A, 'scipy') else A
+    nf = 2 if W[0] == W[1] else 1
+    if precond == 'metric_mono':
+        BB = get_hazmath_metric_precond_mono(A, W, parameters=monolithic_params, interface_dofs=idofs,
+                                             num_functions=nf)
+        Aop = A                              # same object: device-resident PCG
+    elif precond == 'metric':
+        BB = get_hazmath_metric_precond(Asp, W, parameters=monolithic_params, interface_dofs=idofs,
+                                        num_functions=nf)
+        Aop = BB.Aop
+    elif precond == 'amg':
+        BB = get_hazmath_amg_precond(Asp, W)
+        Aop = BB._Aop
+    elif precond == 'diag':
+        BB = get_block_diag_precond(Asp, W)
+        Aop = Asp
+    else:
+        raise ValueError(precond)
+    solver = ConjGrad(Aop, precond=BB, tolerance=tol, maxiter=maxiter)
+    x = solver * b
+    dt = time.time() - then
+    niters = len(solver.residuals) - 1
+    eigs = solver.eigenvalue_estimates()
+    cond = float(max(eigs) / min(eigs))
+    return x, niters, cond, dt, solver.residuals[-1], BB
+
+
+def bidomain(argv, dim):
+    ap = argparse.ArgumentParser(prog='bidomain_%dd' % dim)
+    ap.add_argument('-nrefs', type=int, default=1)
+    ap.add_argument('-kappa1', type=float, default=2)
+    ap.add_argument('-kappa2', type=float, default=3)
+    ap.add_argument('-gamma', type=float, default=1)
+    ap.add_argument('-pdegree', type=int, default=1, choices=(1,))
+    ap.add_argument('-precond', type=str, default='metric_mono',
+                    choices=('metric_mono', 'metric', 'amg', 'diag'))
+    ap.add_argument('-save', type=int, default=0)
+    ap.add_argument('-results', type=str, default='./results')
+    args, _ = ap.parse_known_args(argv)
+    rdir = os.path.join(args.results, 'bidomain_%dd' % dim)
+    os.makedirs(rdir, exist_ok=True)
+    path = _iters_path(rdir, args.precond, kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma,
+                       pdegree=args.pdegree)
+    i0 = 5 if dim == 2 else 3
+    rows = []
+    for k, n in enumerate(2 ** i for i in range(i0, i0 + args.nrefs)):
+        s = problems.bidomain(dim, n, args.gamma, args.kappa1, args.kappa2)
+        b = problems.seeded_rhs(s.N)
+        x, niters, cond, dt, r, _ = _solve(s, s.W, b, args.precond, s.idofs, 1e-8, 500)
+        row = (s.N, niters, cond, dt, r, np.sqrt(dim) / n)
+        rows.append(row)
+        _append(path, row, k == 0)
+        print('bidomain_%dd n=%d ndofs=%d niters=%d cond=%.3g timeKSP=%.3fs r=%.3e'
+              % (dim, n, s.N, niters, cond, dt, r), flush=True)
+    return rows
+
+
+def emi(argv, dim):
+    ap = argparse.ArgumentParser(prog='emi_%dd' % dim)
+    ap.add_argument('-nrefs', type=int, default=1)
+    ap.add_argument('-kappa1', type=float, default=2)
+    ap.add_argument('-kappa2', type=float, default=3)
+    ap.add_argument('-gamma', type=float, default=5)
+    ap.add_argument('-pdegree', type=int, default=1, choices=(1,))
+    ap.add_argument('-precond', type=str, default='metric', choices=('metric', 'metric_mono', 'diag'))
+    ap.add_argument('-save', type=int, default=0)
+    ap.add_argument('-results', type=str, default='./results')
+    args, _ = ap.parse_known_args(argv)
+    rdir = os.path.join(args.results, 'emi_%dd' % dim)
+    os.makedirs(rdir, exist_ok=True)
+    path = _iters_path(rdir, args.precond, kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma,
+                       pdegree=args.pdegree)
+    i0 = 6 if dim == 2 else 2
+    rows = []
+    for k, n in enumerate(2 ** i for i in range(i0, i0 + args.nrefs)):
+        s = problems.emi(dim, n, args.gamma, args.kappa1, args.kappa2)
+        b = [problems.seeded_rhs(s.W[0], 1234), problems.seeded_rhs(s.W[1], 4321)]
+        then = time.time()
+        if args.precond == 'diag':
+            BB = get_block_diag_precond(s.blocks, s.W)
+        else:
+            BB = get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+        solver = ConjGrad(s, precond=BB, tolerance=1e-10, maxiter=500)   # src/emi_3d.py:143
+        solver * b
+        dt = time.time() - then
+        niters = len(solver.residuals) - 1
+        eigs = solver.eigenvalue_estimates()
+        row = (s.N, niters, float(max(eigs) / min(eigs)), dt, solver.residuals[-1], np.sqrt(dim) / n)
+        rows.append(row)
+        _append(path, row, k == 0)
+        print('emi_%dd n=%d ndofs=%d niters=%d cond=%.3g timeKSP=%.3fs' % (dim, n, s.N, niters, row[2], dt),
+              flush=True)
+    return rows
+
+
+def emi_3d1d(argv):
+    ap = argparse.ArgumentParser(prog='emi_3d1d')
+    ap.add_argument('-gamma', type=float, default=1)
+    ap.add_argument('-dump', type=int, default=0, choices=(0, 1))
+    ap.add_argument('-radius', type=float, default=1)
+    ap.add_argument('-n', type=int, default=32, help='cells per direction of the tissue cube')
+    ap.add_argument('-outdir', type=str, default='./data/emi_3d1d/')
+    args, _ = ap.parse_known_args(argv)
+    t0 = time.time()
+    s = problems.emi_3d1d(args.n, args.gamma, args.radius)
+    print('System setup and assembly time: %.3f' % (time.time() - t0), flush=True)
+    A = s.scipy()
+    b = problems.seeded_rhs(s.N)
+    if args.dump:
+        fileio.dump_system(A, b, s.W, args.outdir)
+        return None
+    # alternative solver: the file-free path of solve_haznics (src/utils.py:95-127)
+    B = MetricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_metric_mi355x)
+    solver = ConjGrad(A, precond=B, tolerance=1e-6, maxiter=1000, stop_type=1)
+    solver * b
+    print('niters %d' % (len(solver.residuals) - 1))
+    return len(solver.residuals) - 1
+
+
+def fenics_metric_solver_xd_1d(sfile: str, mdir: str, odir: str, quiet: bool = False) -> int:
+    """HAZmath's file-based 3D-1D solve (haznics.fenics_metric_solver_xd_1d,
+    called at src/run_solver_3d1d.py:38): parameters from the .dat file,
+    A / b / idofs from mdir (utils.dump_system format), CG with the file's
+    stopping rule, metric AMG seeded at the 1D dofs; writes odir/solution.txt.
+    Returns the iteration count."""
+    d = fileio.read_dat(sfile)
+    params, solver_prm, notes = fileio.dat_to_parameters(d)
+    A, b, idofs, idofs3d = fileio.load_system(mdir)
+    N = A.shape[0]
+    W = [N - len(idofs), len(idofs)] if idofs is not None else [N]
+    t0 = time.time()
+    B = MetricAMG(A, W, idofs=idofs, parameters=params)
+    t1 = time.time()
+    st = solver_prm['stop_type']
+    cg = ConjGrad(A, precond=B, tolerance=solver_prm['tol'], maxiter=solver_prm['maxit'],
+                  stop_type=1 if st == 1 else None, relativeconv=st == 2)
+    x = cg * b
+    t2 = time.time()
+    os.makedirs(odir, exist_ok=True)
+    fileio.write_solution(os.path.join(odir, 'solution.txt'), x)
+    niters = len(cg.residuals) - 1
+    if not quiet:
+        for n in notes:
+            print('[mamg] parameter substitution: %s' % n)
+        rel = cg.residual_norms[-1] / max(np.linalg.norm(b), 1e-300)
+        print('Number of iterations = %d, relative residual = %.6e' % (niters, rel))
+        print('AMG setup (%s): %.3f s, solve: %.3f s, levels: %d'
+              % (B.setup_path, t1 - t0, t2 - t1, B.num_levels), flush=True)
+    return niters
+
+
+def run_solver_3d1d(argv):
+    ap = argparse.ArgumentParser(prog='run_solver_3d1d')
+    ap.add_argument('-infile', type=str, default='./src/input_metric.dat')
+    ap.add_argument('-indir', type=str, default='./data/emi_3d1d/')
+    ap.add_argument('-outdir', type=str, default='./results/emi_3d1d/')
+    args, _ = ap.parse_known_args(argv)
+    if not os.path.exists(args.infile) or not os.path.exists(args.indir):
+        raise SystemExit('input file or matrix directory missing')
+    return fenics_metric_solver_xd_1d(os.path.abspath(args.infile), os.path.abspath(args.indir) + '/',
+                                      os.path.abspath(args.outdir) + '/')
+
+
+COMMANDS = {
+    'bidomain_2d': lambda a: bidomain(a, 2),
+    'bidomain_3d': lambda a: bidomain(a, 3),
+    'emi_2d': lambda a: emi(a, 2),
+    'emi_3d': lambda a: emi(a, 3),
+    'emi_3d1d': emi_3d1d,
+    'run_solver_3d1d': run_solver_3d1d,
+}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if not argv or argv[0] not in COMMANDS:
+        print(__doc__)
+        return 2
+    COMMANDS[argv[0]](argv[1:])
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

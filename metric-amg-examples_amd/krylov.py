@@ -46,7 +46,19 @@ def lanczos_eigenvalues(alphas, betas):
 
 class ConjGrad:
     def __init__(self, A, precond=None, tolerance=1e-5, initial_guess=None, maxiter=200,
-                 show=1, callback=None, relativeconv=False, device=None, **kwargs):
+                 show=1, callback=None, relativeconv=False, device=None, stop_type=None, **kwargs):
+        # block systems (src/emi_3d.py:143: CG on the 2x2 block matrix with
+        # precond R^T Minv R): solved on the monolithic storage, where
+        # R^T Minv R is Minv itself; block vectors in and out
+        self._block_sizes = None
+        if hasattr(A, 'blocks') or isinstance(A, (list, tuple)):
+            from .precond import to_monolithic
+            Am = getattr(precond, 'Aop', None)
+            self._block_sizes = ([int(w) for w in A.W] if hasattr(A, 'W')
+                                 else [blk[0].shape[0] for blk in A])
+            A = Am if Am is not None else to_monolithic(A)
+        if getattr(precond, 'monolithic', None) is not None:
+            precond = precond.monolithic
         self.A = A
         self.B = precond
         self.tolerance = float(tolerance)
@@ -56,20 +68,35 @@ class ConjGrad:
         self.callback = callback
         self.relativeconv = bool(relativeconv)
         self.device = device
+        # stop_type None: cbc.block (sqrt(<r,Br>) vs tolerance); 1: HAZmath
+        # linear_stop_type 1, ||r||_2 <= tolerance ||b||_2 (src/input_metric.dat:54)
+        if stop_type not in (None, 1):
+            raise ValueError('stop_type must be None (cbc.block) or 1 (||r||/||b||)')
+        self.stop_type = stop_type
         self.residuals, self.alphas, self.betas = [], [], []
+        self.residual_norms = []
         self.breakdown = False
 
     # ------------------------------------------------------------------
     def _device_ok(self):
-        if self.device is False or self.callback is not None:
+        if self.device is False or self.callback is not None or self.stop_type is not None:
             return False
         B = self.B
         return isinstance(B, MetricAMG) and B._Aop is self.A
 
     def __mul__(self, b):
+        blocks = isinstance(b, (list, tuple))
+        if blocks:
+            b = np.concatenate([np.asarray(bi, dtype=np.float64) for bi in b])
         if self._device_ok() or self.device is True:
-            return self._solve_device(b)
-        return self._solve_host(b)
+            x = self._solve_device(b)
+        else:
+            x = self._solve_host(b)
+        if blocks:
+            sizes = self._block_sizes or [len(x)]
+            off = np.concatenate([[0], np.cumsum(sizes)])
+            return [x[off[i]:off[i + 1]] for i in range(len(sizes))]
+        return x
 
     def _solve_device(self, b):
         import torch
@@ -115,8 +142,16 @@ class ConjGrad:
         residuals = [np.sqrt(rz)]
         alphas, betas = [], []
         tol = self.tolerance * residuals[0] if self.relativeconv else self.tolerance
+        norms = [float(np.linalg.norm(r))]
+        bnorm = float(np.linalg.norm(b)) or 1.0
+
+        def converged():
+            if self.stop_type == 1:
+                return norms[-1] <= self.tolerance * bnorm
+            return residuals[-1] <= tol
+
         it = 0
-        while residuals[-1] > tol and it < self.maxiter:
+        while not converged() and it < self.maxiter:
             z = A @ d
             dz = float(np.dot(d, z))
             if dz == 0:
@@ -136,12 +171,14 @@ class ConjGrad:
             beta = rz / rz_prev
             d = z + beta * d
             residuals.append(np.sqrt(rz))
+            norms.append(float(np.linalg.norm(r)))
             alphas.append(alpha)
             betas.append(beta)
             if self.callback is not None:
                 self.callback(k=it, x=x, r=r)
             it += 1
         self.residuals, self.alphas, self.betas = residuals, alphas, betas
+        self.residual_norms = norms
         return x
 
     def eigenvalue_estimates(self):

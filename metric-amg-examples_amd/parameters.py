@@ -51,7 +51,7 @@ parameters_metric_mi355x = {
     "coarse_solver": SOLVER_UMFPACK,
     "coarse_scaling": OFF,
     "aggregation_type": MIS,
-    "strong_coupled": 0.08,
+    "strong_coupled": 0.0,        # nodal strength: theta = 0 (0.08 stalls coarsening)
     "max_aggregation": 100,
     "amli_degree": 3,
     "Schwarz_levels": 1,

@@ -1,0 +1,150 @@
+"""Preconditioner factories of the reference's drivers, block form included.
+
+Reference: /root/reference/src/utils.py
+  get_block_diag_precond(A, W, bcs)                          :9-12   exact block LU
+  get_hazmath_amg_precond(A, W, bcs, parameters, ...)         :15-42  plain (non-metric) AMG
+  get_hazmath_metric_precond(A, W, bcs, parameters, idofs)    :45-53  R^T Minv R on a block system
+  get_hazmath_metric_precond_mono(A, W, bcs, parameters, idofs) :56-90 metricAMG on the monolithic CSR
+``ii_convert`` (fenics_ii) becomes ``to_monolithic``; ``ReductionOperator``
+maps a block vector [x0, x1] onto the monolithic vector (concatenation) and
+its transpose splits it back, so ``R.T * Minv * R`` applies the monolithic
+preconditioner to block vectors exactly as the reference composes it (:53).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .amg import MetricAMG
+from . import parameters as P
+
+
+def to_monolithic(A):
+    """2x2 list of scipy blocks | BlockSystem | sparse -> monolithic CSR (sorted)."""
+    import scipy.sparse as sp
+    if hasattr(A, 'blocks'):
+        A = A.blocks
+    elif hasattr(A, 'scipy'):
+        A = A.scipy()
+    if isinstance(A, (list, tuple)):
+        M = sp.bmat(A, format='csr')
+    else:
+        M = sp.csr_matrix(A)
+    M.sort_indices()
+    return M
+
+
+def _sizes(W):
+    return [int(w.dim()) if hasattr(w, 'dim') else int(w) for w in W]
+
+
+class ReductionOperator:
+    """Block vector <-> monolithic vector (xii.ReductionOperator([len(W)], W))."""
+    _mamg_operator = True      # composes with MetricAMG.__mul__ into a product
+
+    def __init__(self, W, transpose=False):
+        self.sizes = _sizes(W)
+        self.offsets = np.concatenate([[0], np.cumsum(self.sizes)])
+        self.transposed = transpose
+
+    @property
+    def T(self):
+        return ReductionOperator(self.sizes, not self.transposed)
+
+    def __call__(self, x):
+        if self.transposed:                      # monolithic -> blocks
+            x = np.asarray(x)
+            return [x[self.offsets[i]:self.offsets[i + 1]].copy() for i in range(len(self.sizes))]
+        return np.concatenate([np.asarray(xi, dtype=np.float64) for xi in x])
+
+    def __mul__(self, other):
+        if isinstance(other, (ReductionOperator, MetricAMG, _Product)):
+            return _Product([self, other])
+        return self(other)
+
+
+class _Product:
+    """Operator product applied right to left (R.T * Minv * R)."""
+    _mamg_operator = True
+
+    def __init__(self, ops):
+        self.ops = []
+        for o in ops:
+            self.ops.extend(o.ops if isinstance(o, _Product) else [o])
+
+    def __mul__(self, other):
+        if isinstance(other, (ReductionOperator, MetricAMG, _Product)):
+            return _Product([self, other])
+        x = other
+        for o in reversed(self.ops):
+            x = o(x) if isinstance(o, ReductionOperator) else o * x
+        return x
+
+    __call__ = __mul__
+
+    @property
+    def monolithic(self):
+        """the monolithic preconditioner inside (for device-resident PCG)."""
+        for o in self.ops:
+            if isinstance(o, MetricAMG):
+                return o
+        return None
+
+
+def get_hazmath_metric_precond_mono(A, W, bcs=None, parameters=None, interface_dofs=None, **kw):
+    """metricAMG(A, W, idofs=interface_dofs, parameters=parameters)  (src/utils.py:56-90).
+    ``parameters`` None -> the GPU profile (parameters_metric_mi355x); a
+    HAZmath dict is mapped with ``to_gpu_profile`` first (substitutions in
+    ``.substitutions``)."""
+    notes = []
+    if parameters is None:
+        parameters = P.parameters_metric_mi355x
+    else:
+        parameters, notes = P.to_gpu_profile(parameters)
+    B = MetricAMG(A, W, idofs=interface_dofs, parameters=parameters, **kw)
+    B.substitutions = notes
+    return B
+
+
+def get_hazmath_metric_precond(A, W, bcs=None, parameters=None, interface_dofs=None, **kw):
+    """R^T * Minv * R with Minv the monolithic metric AMG (src/utils.py:45-53)."""
+    AA = to_monolithic(A)
+    R = ReductionOperator(W)
+    Minv = get_hazmath_metric_precond_mono(AA, W, bcs, parameters=parameters,
+                                           interface_dofs=interface_dofs, **kw)
+    op = R.T * Minv * R
+    op.Aop = AA
+    return op
+
+
+def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs=None, **kw):
+    """Plain (non-metric) AMG on the monolithic matrix (src/utils.py:15-42):
+    no interface seeds, point smoothers."""
+    params = dict(P.parameters_metric_mi355x) if parameters is None else P.to_gpu_profile(parameters)[0]
+    params['Schwarz_levels'] = 0
+    return MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
+
+
+class BlockDiagLU:
+    """Exact LU of each diagonal block (src/utils.py:9-12, PETSc LU there;
+    SuperLU here).  The 'diag' option of the EMI / bidomain drivers -- a
+    reference baseline, not part of the metric-AMG hot path."""
+
+    def __init__(self, A, W):
+        from scipy.sparse.linalg import splu
+        AA = to_monolithic(A)
+        self.sizes = _sizes(W)
+        off = np.concatenate([[0], np.cumsum(self.sizes)])
+        self.off = off
+        self.lu = [splu(AA[off[i]:off[i + 1], off[i]:off[i + 1]].tocsc()) for i in range(len(self.sizes))]
+
+    def __mul__(self, r):
+        if isinstance(r, (list, tuple)):
+            return [lu.solve(np.asarray(ri)) for lu, ri in zip(self.lu, r)]
+        r = np.asarray(r)
+        return np.concatenate([lu.solve(r[self.off[i]:self.off[i + 1]]) for i, lu in enumerate(self.lu)])
+
+    __call__ = __mul__
+
+
+def get_block_diag_precond(A, W, bcs=None):
+    return BlockDiagLU(A, W)
