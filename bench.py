@@ -220,24 +220,29 @@ def main():
     # measured HBM bytes per launch of the two dominant kernels (rocprofv3
     # FETCH_SIZE + WRITE_SIZE, calibrated; profiles/traffic.json, written by
     # scripts/traffic.py from the committed PMC summaries of this config)
+    fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
+    post_mode = 'k' if fmt0.get('post_k') else 'merged'
     traffic = {}
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
     if os.path.exists(tpath) and world == 1:
         try:
             tj = json.load(open(tpath))
-            if tj.get('N') == sysm.N and tj.get('layout') == layout:
+            if tj.get('N') == sysm.N and tj.get('layout') == layout and tj.get('post', 'merged') == post_mode:
                 traffic = tj.get('kernels', {})
         except (OSError, ValueError):
             traffic = {}
 
-    fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
     if layout == 'csr':
         names = ('csr_kernel<*,RESID,0>', 'csr_kernel<*,BJAC/JACOBI,0>')
+    elif post_mode == 'k':
+        names = ('%s<RESID,...,0>' % ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel'),
+                 '%s<KPOST,...,0>' % ('sell2_kernel' if fmt0.get('post_sell') else 'bsr2_kernel'))
     else:
         names = ('%s<RESID,...,0>' % ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel'),
                  'bsr2_post_kernel<8,...,0>' if fmt0.get('post_fused', True) else 'bsr2_kernel<*,BJAC,...,0>')
     descr = ('level-0 residual r = b - A0 x', 'level-0 prolongation + post-smoothing '
-             'z = x1 + P e + W (r1 - (AP) e)')
+             + ('z = x1 + W r1 + K e, K = P - W (A P)' if post_mode == 'k'
+                else 'z = x1 + P e + W (r1 - (AP) e)'))
     rooflines = []
     for c, key in ((0, 'L0_resid'), (1, 'L0_smooth_spmv')):
         if kms[c] <= 0:

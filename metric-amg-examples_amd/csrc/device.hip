@@ -50,8 +50,10 @@ namespace {
   } while (0)
 
 // epilogues: y = s | y = y0 + s | r = b - s | x' = x + w (b - s) (point) |
-// x' = x + W_I (b_I - s_I) (2x2 block, BSR only)
-enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4 };
+// x' = x + W_I (b_I - s_I) (2x2 block, BSR only) |
+// z = x1_I + W_I r1_I + s_I with s = K e, K = P - W (A P) (BSR only: the
+// prolongation fused with the first post sweep through one operator)
+enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4, EPI_KPOST = 5 };
 
 typedef double dv4 __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -187,6 +189,11 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
       o0 = y[2 * node] + s0; o1 = y[2 * node + 1] + s1;
     } else if (EPI == EPI_RESID) {
       o0 = vget(b, bs, node, 0) - s0; o1 = vget(b, bs, node, 1) - s1;
+    } else if (EPI == EPI_KPOST) {
+      const double r0 = vget(b, bs, node, 0), r1 = vget(b, bs, node, 1);
+      const dv4 w = W[node];
+      o0 = y[2 * node] + (w.x * r0 + w.y * r1) + s0;
+      o1 = y[2 * node + 1] + (w.z * r0 + w.w * r1) + s1;
     } else {  // EPI_BJAC
       const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
       const dv4 w = W[node];
@@ -301,9 +308,10 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   // epilogue operands after the loop (measured: loading them first is slower)
   double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
   dv4 w = {0.0, 0.0, 0.0, 0.0};
-  if (EPI == EPI_RESID || EPI == EPI_BJAC) bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
-  if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
-  if (EPI == EPI_BJAC) w = W[node];
+  if (EPI == EPI_RESID || EPI == EPI_BJAC || EPI == EPI_KPOST)
+    bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
+  if (EPI == EPI_YADD || EPI == EPI_BJAC || EPI == EPI_KPOST) yy = reinterpret_cast<const double2*>(y)[node];
+  if (EPI == EPI_BJAC || EPI == EPI_KPOST) w = W[node];
   double o0, o1;
   if (EPI == EPI_Y) {
     o0 = s0; o1 = s1;
@@ -311,6 +319,9 @@ __global__ __launch_bounds__(256) void sell2_kernel(
     o0 = yy.x + s0; o1 = yy.y + s1;
   } else if (EPI == EPI_RESID) {
     o0 = bb.x - s0; o1 = bb.y - s1;
+  } else if (EPI == EPI_KPOST) {
+    o0 = yy.x + (w.x * bb.x + w.y * bb.y) + s0;
+    o1 = yy.y + (w.z * bb.x + w.w * bb.y) + s1;
   } else {  // EPI_BJAC
     const double r0 = bb.x - s0, r1 = bb.y - s1;
     o0 = yy.x + (w.x * r0 + w.y * r1);
@@ -479,6 +490,9 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_SELL_POST  1: SELL-64-sigma for the merged [P | AP] too (default 0)
 //   MAMG_SELL_U     SELL blocks per chunk (4, 8, 16), level-0 SELL kernels
 //   MAMG_NT         1: non-temporal matrix loads in the level-0 kernels
+//   MAMG_POST_K     0: fused post sweep over [P | AP] instead of K = P - W A P (default 1)
+//   MAMG_POST_SELL  0: K in lane-group BSR instead of SELL-64 (default 1)
+//   MAMG_POST_U     SELL blocks per chunk of the K kernel (4 default, 8, 16)
 int g_remap = 1;
 int g_post_lanes = 0;
 int g_sym = 1;
@@ -486,8 +500,18 @@ int g_sell = 1;
 int g_sell_post = 0;
 int g_sell_u = 8;
 int g_nt = 0;
+int g_post_k = 1;
+int g_post_u = 4;
+int g_post_sell = 1;
 int64_t g_sell_min_rows = 1 << 20;
 void read_knobs() {
+  const char* pk = std::getenv("MAMG_POST_K");
+  g_post_k = pk ? std::atoi(pk) != 0 : 1;
+  pk = std::getenv("MAMG_POST_U");
+  g_post_u = pk ? std::atoi(pk) : 4;
+  if (g_post_u != 4 && g_post_u != 8 && g_post_u != 16) g_post_u = 4;
+  pk = std::getenv("MAMG_POST_SELL");
+  g_post_sell = pk ? std::atoi(pk) != 0 : 1;
   const char* su = std::getenv("MAMG_SELL_U");
   g_sell_u = su ? std::atoi(su) : 8;
   if (g_sell_u != 4 && g_sell_u != 8 && g_sell_u != 16) g_sell_u = 8;
@@ -558,6 +582,7 @@ struct DLevel {
   DCsr A, P, R, WB;        // CSR layout
   DBsr Ab, Pb, Rb;         // BSR2 layout
   DBsr PAb;                // BSR2 post fusion: merged [P | AP] rows (ptr: 2 nr + 1)
+  DBsr KPb;                // BSR2 post fusion: K = P - W (A P), one operator (default)
   dv4* Wd = nullptr;       // BSR2 layout: 2x2 smoother block per node
   double* winv = nullptr;
   double* Ainv = nullptr;
@@ -833,6 +858,41 @@ __global__ __launch_bounds__(256) void merge_fill_kernel(int64_t nr, const int64
   for (int64_t k = qp[I]; k < qp[I + 1]; ++k, ++d) { mc[d] = qc[k]; mv[d] = qv[k]; }
 }
 
+// K = P - W_I (A P) row by row on the union of P's and AP's block patterns
+// (the fused post-smoothing operator: x1 + P e + W (r1 - AP e) = x1 + W r1 + K e);
+// a block absent from one operand contributes exact zeros
+template <bool FILL>
+__global__ __launch_bounds__(256) void kmerge_kernel(int64_t nr, const int64_t* __restrict__ pp,
+                                                     const int32_t* __restrict__ pc, const dv4* __restrict__ pv,
+                                                     const int64_t* __restrict__ qp, const int32_t* __restrict__ qc,
+                                                     const dv4* __restrict__ qv, const dv4* __restrict__ W,
+                                                     int64_t* kp, int32_t* __restrict__ kc, dv4* __restrict__ kv) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t a = pp[I], ae = pp[I + 1], b = qp[I], be = qp[I + 1];
+  int64_t o = FILL ? kp[I] : 0;
+  const dv4 w = FILL ? W[I] : dv4{0.0, 0.0, 0.0, 0.0};
+  const dv4 zero = {0.0, 0.0, 0.0, 0.0};
+  while (a < ae || b < be) {
+    const int32_t ja = a < ae ? pc[a] : INT32_MAX, jb = b < be ? qc[b] : INT32_MAX;
+    const int32_t j = min(ja, jb);
+    if (FILL) {
+      const dv4 p = ja == j ? pv[a] : zero, q = jb == j ? qv[b] : zero;
+      dv4 k;   // blocks (0,0) (0,1) (1,0) (1,1) = x y z w;  (W q)_ab = W_a0 q_0b + W_a1 q_1b
+      k.x = p.x - (w.x * q.x + w.y * q.z);
+      k.y = p.y - (w.x * q.y + w.y * q.w);
+      k.z = p.z - (w.z * q.x + w.w * q.z);
+      k.w = p.w - (w.z * q.y + w.w * q.w);
+      kc[o] = j;
+      kv[o] = k;
+    }
+    if (ja == j) ++a;
+    if (jb == j) ++b;
+    ++o;
+  }
+  if (!FILL) kp[I + 1] = o;
+}
+
 // SELL-64: slice widths and per-row meta (length | first-part length << 16)
 __global__ __launch_bounds__(256) void sell_meta_kernel(int64_t nr, const int64_t* __restrict__ bptr, int merged,
                                                         int32_t* __restrict__ meta, int64_t* __restrict__ soff,
@@ -942,11 +1002,32 @@ int dev_merge_rows(TmpPool* T, const TBsr& P, const TBsr& Q, TBsr* M, std::strin
   return MAMG_OK;
 }
 
+int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* K, std::string* err) {
+  int rc;
+  const int64_t nr = P.nr;
+  K->nr = nr; K->nc = P.nc; K->merged = false;
+  if ((rc = T->alloc(&K->ptr, nr + 1, err))) return rc;
+  HIPCHK(hipMemset(K->ptr, 0, sizeof(int64_t)));
+  const dv4* Wv = reinterpret_cast<const dv4*>(W);
+  if (nr) kmerge_kernel<false><<<nblocks(nr), 256>>>(nr, P.ptr, P.col, P.val, Q.ptr, Q.col, Q.val, Wv, K->ptr,
+                                                      nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(K->ptr, K->ptr, nr + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&K->nb, K->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = T->alloc(&K->col, K->nb, err))) return rc;
+  if ((rc = T->alloc(&K->val, K->nb, err))) return rc;
+  if (nr) kmerge_kernel<true><<<nblocks(nr), 256>>>(nr, P.ptr, P.col, P.val, Q.ptr, Q.col, Q.val, Wv, K->ptr,
+                                                     K->col, K->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
 // final apply layout from a raw device BSR (the device-side counterpart of
 // upload_bsr): SELL-64 for large short-row plain matrices, symmetric-block
 // packing where every block has (0,1) == (1,0) bitwise, else 4 doubles/block
 template <class HT>
-int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, std::string* err) {
+int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, std::string* err,
+                 bool allow_sell = true) {
   int rc;
   const int64_t nr = B.nr, np = B.merged ? 2 * nr + 1 : nr + 1;
   D->nr = nr;
@@ -965,7 +1046,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   }
   D->sym = sym;
   const int per = sym ? 3 : 4;
-  if (g_sell && nr >= g_sell_min_rows && D->nb <= 40 * nr && !B.merged) {
+  if (allow_sell && g_sell && nr >= g_sell_min_rows && D->nb <= 40 * nr && !B.merged) {
     const int64_t ns = (nr + SELL_C - 1) / SELL_C;
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
@@ -1032,10 +1113,19 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
-    if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
+    if (g_post_k) {   // one operator K = P - W (A P) on AP's pattern
+      if ((rc = dev_kmerge(&T, Pb, Qb, S.W, &M, err))) return rc;
+    } else {          // P and AP blocks side by side in one row window
+      if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
+    }
     T.release(Pb.ptr); T.release(Pb.col); T.release(Pb.val);
     T.release(Qb.ptr); T.release(Qb.col); T.release(Qb.val);
-    if ((rc = finalize_bsr(h, &T, M, &D.PAb, g_post_lanes, false, err))) return rc;
+    // K: SELL-64 with 4-block chunks (K rows hold ~9 blocks at level 0; A/B in
+    // DESIGN.md section 4), lane-group BSR if MAMG_POST_SELL=0; the merged
+    // window is never SELL on this path
+    if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, g_post_lanes, false, err,
+                           g_post_k && g_post_sell)))
+      return rc;
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -1084,7 +1174,7 @@ double bsr_bytes(const DBsr& M, int epi) {
   double b = (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;  // A, x, out
   if (epi == EPI_YADD) b += 16.0 * M.nr;
   if (epi == EPI_RESID) b += 16.0 * M.nr;
-  if (epi == EPI_BJAC) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;       // y, b, W
+  if (epi == EPI_BJAC || epi == EPI_KPOST) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;   // y, b, W
   return b;
 }
 
@@ -1217,7 +1307,13 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     ops->push_back(axpy_op(C.n, C.e, C.x));
   }
   int s0 = 0;
-  if (L.PAb.nr > 0 && p.postsmooth_iter >= 1) {   // prolongation + first post sweep
+  if (L.KPb.nr > 0 && p.postsmooth_iter >= 1) {   // z = x1 + W r1 + K e (one operator)
+    const bool last = p.postsmooth_iter == 1;
+    ops->push_back(bsr_op(L.KPb, EPI_KPOST, clsS, tagA, C.x, 0, X, L.r, 0, L.Wd, last ? xout : X2,
+                          last ? os : 0));
+    if (!last) std::swap(X, X2);
+    s0 = 1;
+  } else if (L.PAb.nr > 0 && p.postsmooth_iter >= 1) {   // prolongation + first post sweep
     const bool last = p.postsmooth_iter == 1;
     ops->push_back(post_op(L.PAb, L.r, L.Wd, clsS, tagA, C.x, X, last ? xout : X2, last ? os : 0));
     if (!last) std::swap(X, X2);
@@ -1308,6 +1404,9 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
     case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_KPOST:   // K is never symmetric and e is node-major
+      if constexpr (!XFM && !SYM) bsr2_kernel<VL, EPI_KPOST, false, false, TAG><<<g, 256, 0, s>>>(BSR_ARGS);
+      break;
     default: bsr2_kernel<VL, EPI_BJAC, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
   }
 #undef BSR_ARGS
@@ -1323,6 +1422,9 @@ void launch_sell_u(const Op& o, hipStream_t s) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_RESID: sell2_kernel<EPI_RESID, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
+    case EPI_KPOST:
+      if constexpr (!XFM && !SYM) sell2_kernel<EPI_KPOST, false, false, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS);
+      break;
     default: sell2_kernel<EPI_BJAC, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
   }
 #undef SELL_ARGS
@@ -1331,7 +1433,8 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   if (TAG == 0) {   // the level-0 operator: tuning variants (bench/variants.py)
-    switch (g_sell_u * 2 + (g_nt ? 1 : 0)) {
+    const int u = o.epi == EPI_KPOST ? g_post_u : g_sell_u;
+    switch (u * 2 + (g_nt ? 1 : 0)) {
       case 8: launch_sell_u<XFM, SYM, 4, false, TAG>(o, s); return;
       case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
       case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
@@ -1637,7 +1740,8 @@ int dev_layout(const DeviceHandle* h) { return h->bsr ? 1 : 0; }
 int dev_level_format(const DeviceHandle* h, int level) {
   const DLevel& L = h->L[level];
   return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) |
-         (L.PAb.nr > 0 ? MAMG_FMT_POST_FUSED : 0);
+         (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
+         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0);
 }
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {

@@ -13,10 +13,13 @@ selected at src/bidomain_3d.py:144-145):
 HAZmath's source is not in /root/reference and not installable here, so every
 component below is a restatement of its published algorithm family [ext,
 recalled], not a pinned copy:
-  * HEM: one greedy heavy-edge matching pass per level over the strength
-    graph (|a_ij| >= theta sqrt(|a_ii a_jj|)), vertices in index order, each
+  * HEM: greedy heavy-edge matching over the strength graph
+    (|a_ij| >= theta sqrt(|a_ii a_jj|)), vertices in index order, each
     unmatched vertex pairs with its heaviest unmatched strong neighbour (ties:
-    smallest index); unmatched vertices are singleton aggregates;
+    smallest index); unmatched vertices are singletons.  Two passes per level
+    (the second matches the pairs on their Galerkin graph), so aggregates hold
+    up to 4 dofs -- one pass alone coarsens by < 2 and the W-cycle's work
+    then grows without bound with the number of levels;
   * UA: piecewise-constant P, Galerkin A_c = P^T A P;
   * SGS: forward then backward Gauss-Seidel (exact triangular solves);
   * level-0 symmetric multiplicative Schwarz: one block per seed = the seed and
@@ -53,6 +56,7 @@ class RefParams:
     Schwarz_maxlvl: int = 1
     presmooth_iter: int = 1
     postsmooth_iter: int = 1
+    hem_passes: int = 2          # matching passes per level (aggregates of <= 2^passes)
 
 
 def hem_aggregate(A: sp.csr_matrix, theta: float):
@@ -131,7 +135,13 @@ class RefHierarchy:
                 lev.Ainv = sla.lu_factor(cur.toarray())
                 break
             agg, nagg = hem_aggregate(cur, p.strong_coupled)
-            if nagg >= n:
+            for _ in range(p.hem_passes - 1):       # aggregates of matched pairs
+                T1 = sp.csr_matrix((np.ones(n), (np.arange(n), agg)), shape=(n, nagg))
+                A1 = (T1.T @ cur @ T1).tocsr()
+                A1.sort_indices()
+                a2, nagg = hem_aggregate(A1, p.strong_coupled)
+                agg = a2[agg]
+            if nagg > 0.9 * n:                  # coarsening stalled: solve directly here
                 lev.Ainv = sla.lu_factor(cur.toarray())
                 break
             lev.P = sp.csr_matrix((np.ones(n), (np.arange(n), agg)), shape=(n, nagg))

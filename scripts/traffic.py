@@ -31,10 +31,14 @@ def classify(name):
     kind, targs = m.group(1), [t.strip() for t in m.group(2).split(',')]
     if kind == 'bsr2_post_kernel':
         return 'L0_smooth_spmv' if targs[-1] == '0' else None
-    if kind == 'sell2_kernel':          # <EPI, XFM, SYM, U, PRE, TAG>
-        return 'L0_resid' if targs[0] == '2' and targs[1] == 'false' and targs[-1] == '0' else None
-    # bsr2_kernel<VL, EPI, XFM, SYM, TAG>
-    return 'L0_resid' if targs[1] == '2' and targs[2] == 'false' and targs[-1] == '0' else None
+    epi, xfm = (targs[0], targs[1]) if kind == 'sell2_kernel' else (targs[1], targs[2])
+    if targs[-1] != '0':
+        return None
+    if epi == '2' and xfm == 'false':   # EPI_RESID on the internal vectors
+        return 'L0_resid'
+    if epi == '5':                      # EPI_KPOST: z = x1 + W r1 + K e
+        return 'L0_smooth_spmv'
+    return None
 
 
 def collect(path, counter):
@@ -60,6 +64,8 @@ def main():
     ap.add_argument('write_csv')
     ap.add_argument('--N', type=int, required=True)
     ap.add_argument('--layout', default='bsr2')
+    ap.add_argument('--post', default='k', choices=('k', 'merged'),
+                    help='post-smoothing operator the profiled run used (MAMG_POST_K)')
     ap.add_argument('--out', default='profiles/traffic.json')
     a = ap.parse_args()
     f = collect(a.fetch_csv, 'FETCH_SIZE')
@@ -71,7 +77,7 @@ def main():
         kernels[c] = round(fb + wb, 1)
         detail[c] = {'grid': f[c][0], 'launches': f[c][2], 'fetch_bytes': round(fb, 1),
                      'write_bytes': round(wb, 1)}
-    out = {'layout': a.layout, 'N': a.N, 'kernels': kernels, 'detail': detail,
+    out = {'layout': a.layout, 'N': a.N, 'post': a.post, 'kernels': kernels, 'detail': detail,
            'calibration': 'bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (profiles/r01_pmc_calibration.txt)'}
     json.dump(out, open(a.out, 'w'), indent=1)
     print(json.dumps(out))

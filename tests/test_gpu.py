@@ -180,6 +180,30 @@ def test_post_fusion_equals_unfused(lib_built, dim, n, g, kw):
         assert rel(Bf * r, Bu * r) < 1e-12
 
 
+@pytest.mark.parametrize('sell', ['0', '1'])
+def test_post_operator_k_equals_merged(lib_built, monkeypatch, sell):
+    """K = P - W (A P) stored as one operator (z = x1 + W r1 + K e, default)
+    and the merged [P | AP] window (z = x1 + P e + W (r1 - AP e)) are the
+    same cycle up to summation order."""
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1' if sell == '1' else str(1 << 20))
+    monkeypatch.setenv('MAMG_POST_SELL', sell)
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    zs, fmts = [], []
+    for k in ('1', '0'):
+        monkeypatch.setenv('MAMG_POST_K', k)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        fmts.append(B.level_format(0))
+        zs.append(B * mo.seeded_rhs(s.N))
+        B.close()
+    assert fmts[0]['post_k'] and not fmts[1]['post_k'] and fmts[0]['post_fused'] and fmts[1]['post_fused']
+    assert fmts[0]['post_sell'] == (sell == '1')
+    assert rel(zs[0], zs[1]) < 1e-12
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    assert rel(zs[0], h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
+
+
 @pytest.mark.parametrize('remap', ['0', '1', '2'])
 def test_symmetric_blocks_and_xcd_remap_bitwise(lib_built, monkeypatch, remap):
     """The symmetric-block format (3 doubles per 2x2 block, chosen at upload
