@@ -298,7 +298,20 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   mamg::Hierarchy H;
   std::string err;
   Seeds S(idofs, n_idofs, v.n, params);
-  rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
+  // every rank builds the same hierarchy: on its own GPU when the profile is
+  // the GPU setup's (bitwise equal to the host setup), else on the host
+  rc = MAMG_ERR_UNSUPPORTED;
+  if (params->num_functions == 2 && params->node_block_smoother &&
+      (params->AMG_type == MAMG_UA_AMG || params->sa_block_diag)) {
+    mamg::GHier G;
+    G.device = params->device;
+    mamg::DevMat dA;
+    rc = mamg::upload_a0(v, &G, &dA, &err);
+    if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
+    if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
+    if (rc && rc != MAMG_ERR_UNSUPPORTED) { set_error(err); return rc; }
+  }
+  if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
   if (rc) { set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
   rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err);

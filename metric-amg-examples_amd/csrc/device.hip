@@ -1936,6 +1936,7 @@ struct DDLevel {
   bool replicated = false, coarsest = false;
   DBsr A, P, R;
   DBsr PA;                 // post fusion: merged [P_loc | AP_loc]
+  DBsr K;                  // post fusion: K_loc = P_loc - W (AP)_loc (default)
   dv4* W = nullptr;
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
@@ -2042,6 +2043,11 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   }
   dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
   if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  if (D.K.nr > 0) {    // fused: xout = X + W r + K e, all operands local
+    ops->push_back(wrap(bsr_op(D.K, EPI_KPOST, l0 ? C_L0_SMOOTH : C_COARSE, tagA, C.x, 0, X, D.r, 0, D.W,
+                               xout, os)));
+    return;
+  }
   if (D.PA.nr > 0) {   // fused: xout = X + P e + W (r - AP e), all operands local
     ops->push_back(wrap(post_op(D.PA, D.r, D.W, l0 ? C_L0_SMOOTH : C_COARSE, tagA, C.x, X, xout, os)));
     return;
@@ -2117,15 +2123,15 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
   }
+  read_knobs();
   DistPlan plan;
-  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err);
+  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0);
   if (rc) return rc;
   std::unique_ptr<DistHandle> h(new DistHandle());
   h->p = p;
   h->rank = rank;
   h->nranks = nranks;
   h->device = p.device;
-  read_knobs();
   HIPCHK(hipSetDevice(p.device));
   if (comm_id) {                         // RCCL communicator; NULL = virtual (tests)
     ncclUniqueId uid;
@@ -2155,7 +2161,9 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else {
       if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) return rc;
-      if (P.PA.nr > 0) {
+      if (P.K.nr > 0) {
+        if ((rc = upload_bsr(h.get(), P.K, &D.K, g_post_lanes, err))) return rc;
+      } else if (P.PA.nr > 0) {
         if ((rc = upload_bsr(h.get(), P.PA, &D.PA, 0, err))) return rc;
       } else {
         if ((rc = upload_bsr(h.get(), P.P, &D.P, 0, err))) return rc;

@@ -106,8 +106,47 @@ void transpose_bsr(const HBsr& B, HBsr* T) {
 
 }  // namespace
 
+void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K) {
+  const int64_t nr = P.nr;
+  K->nr = nr;
+  K->nc = P.nc;
+  K->ptr.assign(nr + 1, 0);
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      for (int64_t I = 0; I < nr; ++I) K->ptr[I + 1] += K->ptr[I];
+      K->col.resize(K->ptr[nr]);
+      K->val.resize(4 * K->ptr[nr]);
+    }
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t I = 0; I < nr; ++I) {
+      int64_t a = P.ptr[I], ae = P.ptr[I + 1], b = AP.ptr[I], be = AP.ptr[I + 1];
+      int64_t o = pass ? K->ptr[I] : 0;
+      const double* w = &W[4 * I];
+      const double zero[4] = {0.0, 0.0, 0.0, 0.0};
+      while (a < ae || b < be) {
+        const int32_t ja = a < ae ? P.col[a] : INT32_MAX, jb = b < be ? AP.col[b] : INT32_MAX;
+        const int32_t j = std::min(ja, jb);
+        if (pass) {   // same operation order as device.hip kmerge_kernel
+          const double* p = ja == j ? &P.val[4 * a] : zero;
+          const double* q = jb == j ? &AP.val[4 * b] : zero;
+          double* k = &K->val[4 * o];
+          k[0] = p[0] - (w[0] * q[0] + w[1] * q[2]);
+          k[1] = p[1] - (w[0] * q[1] + w[1] * q[3]);
+          k[2] = p[2] - (w[2] * q[0] + w[3] * q[2]);
+          k[3] = p[3] - (w[2] * q[1] + w[3] * q[3]);
+          K->col[o] = j;
+        }
+        if (ja == j) ++a;
+        if (jb == j) ++b;
+        ++o;
+      }
+      if (!pass) K->ptr[I + 1] = o;
+    }
+  }
+}
+
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err) {
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost) {
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
   const int nl = (int)H.levels.size();
@@ -204,7 +243,8 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       if (fuse) {
         HBsr AP;
         to_bsr2(H.levels[l].AP.view(), D.nv, C.nv, &AP);
-        merge_bsr_rows(D.P, AP, &D.PA);
+        if (kpost) kmerge_rows(D.P, AP, D.W, &D.K);
+        else merge_bsr_rows(D.P, AP, &D.PA);
       }
       continue;
     }
@@ -224,7 +264,8 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       HBsr AP;
       to_bsr2_rows(H.levels[l].AP.view(), D.nv, C.nv, D.o0, D.o1, &AP);
       remap_cols(&AP, ncl, cmap);
-      merge_bsr_rows(D.P, AP, &D.PA);
+      if (kpost) kmerge_rows(D.P, AP, D.W, &D.K);
+      else merge_bsr_rows(D.P, AP, &D.PA);
     }
   }
   return MAMG_OK;

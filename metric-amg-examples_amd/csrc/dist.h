@@ -20,7 +20,8 @@ struct DistLevel {
   HBsr A;                         // owned rows x [owned | ghost] (replicated: global)
   HBsr P;                         // owned fine rows x level l+1 local (or global)
   HBsr Rp;                        // transpose of P (partial restriction)
-  HBsr PA;                        // post fusion: merged [P_loc | AP_loc] (P then empty)
+  HBsr PA;                        // post fusion: merged [P_loc | AP_loc] (kpost == false)
+  HBsr K;                         // post fusion: K_loc = P_loc - W (AP)_loc (kpost == true)
   std::vector<double> W;          // 4 per owned node
 };
 
@@ -29,7 +30,11 @@ struct DistPlan {
   std::vector<DistLevel> levels;
 };
 
+// fuse: prolongation fused into the post sweep (needs A P from the setup);
+// kpost: through K = P - W (A P) (one operator), else through [P | AP]
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err);
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost = true);
+// K rows = P rows - W_I (AP rows), block-column union (both sorted, same columns)
+void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K);
 
 }  // namespace mamg

@@ -471,28 +471,12 @@ struct BTent {              // B = tentative prolongator: dof f nv + I -> f nagg
   }
 };
 
-template <class BS>
-__global__ __launch_bounds__(256) void prod_count_kernel(int64_t n, const int64_t* __restrict__ aptr,
-                                                         const int32_t* __restrict__ acol, BS B,
-                                                         int64_t* __restrict__ ub) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  int64_t s = 0;
-  for (int64_t k = aptr[i]; k < aptr[i + 1]; ++k) s += B.len(acol[k]);
-  ub[i] = s;
-}
-
-__global__ __launch_bounds__(256) void bin_rows_kernel(int64_t n, const int64_t* __restrict__ ub, int64_t lim,
-                                                       int32_t* __restrict__ big, int* nbig) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n && ub[i] > lim) big[atomicAdd(nbig, 1)] = (int32_t)i;
-}
-
 template <int TS, int WPB, bool FILL, class BS>
 __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
     int64_t nrows, const int32_t* __restrict__ rows, const int64_t* __restrict__ ub, int64_t lim,
     const int64_t* __restrict__ aptr, const int32_t* __restrict__ acol, const double* __restrict__ aval,
-    BS B, int64_t* cptr, int32_t* __restrict__ ccol, double* __restrict__ cval, int* overflow) {
+    BS B, int64_t* cptr, int32_t* __restrict__ ccol, double* __restrict__ cval, int* overflow,
+    int32_t* spill) {
   __shared__ int32_t keys[WPB][TS];
   __shared__ double sums[WPB][TS];
   __shared__ int32_t ck[WPB][TS];
@@ -502,7 +486,7 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
   const int64_t nw = (int64_t)gridDim.x * WPB;
   for (int64_t r = (int64_t)blockIdx.x * WPB + w; r < nrows; r += nw) {
     const int64_t i = rows ? rows[r] : r;
-    if (!rows && ub[i] > lim) continue;          // binned to the large-table launch
+    if (!rows && ub && ub[i] > lim) continue;    // binned to the large-table launch
     for (int s = lane; s < TS; s += 64) { keys[w][s] = -1; sums[w][s] = 0.0; }
     if (lane == 0) cnt[w] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -535,9 +519,16 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       }
+      if (__any(full)) break;
     }
     if (__any(full)) {
-      if (lane == 0) atomicAdd(overflow, 1);
+      // table full: the row spills to the large-table launch (count pass) or
+      // is skipped here because that launch fills it (fill pass); in the
+      // large-table launch itself it is an error
+      if (lane == 0) {
+        if (!rows && spill && !FILL) spill[atomicAdd(overflow, 1)] = (int32_t)i;
+        else if (rows || !spill) atomicAdd(overflow + 1, 1);
+      }
       continue;
     }
     // nonzero entries (scipy drops exact zeros), appended in any order
@@ -746,31 +737,30 @@ struct Clock {
 
 int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
 
-// exact output size + row pointers + entries of C = A B (hash SpGEMM)
+// exact output size + row pointers + entries of C = A B (hash SpGEMM).
+// Optimistic tiering: every row first runs in a 512-slot table (4 waves per
+// block); a row whose distinct columns overflow it spills to a list that the
+// 2048-slot launch (1 wave per block) redoes.  Each slot accumulates its
+// products in A-row order whatever the table size, so both tiers give the
+// same bits.  (Binning by the product-count upper bound sent most Galerkin
+// rows, whose product counts far exceed their distinct counts, to the slow
+// large-table launch.)
 template <class BS>
 int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
   constexpr int TS1 = 512, TS2 = 2048;
-  constexpr int64_t LIM1 = 384;
   const int64_t n = A.n;
   Scratch S;
-  int64_t* ub = nullptr;
   int32_t* big = nullptr;
-  int* ctr = nullptr;   // [0] nbig, [1] overflow
-  RCHK(S.alloc(&ub, n, err));
+  int* ctr = nullptr;   // [0] spilled rows, [1] rows over the large table
   RCHK(S.alloc(&big, n, err));
   RCHK(S.alloc(&ctr, 2, err));
   HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
-  prod_count_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, B, ub);
-  bin_rows_kernel<<<nblk(n), 256>>>(n, ub, LIM1, big, ctr);
-  HIPCHK(hipGetLastError());
-  int nbig = 0;
-  RCHK(read_int(ctr, &nbig, err));
   C->n = n;
   C->m = ncols;
   RCHK(galloc(G, &C->ptr, n + 1, err));
   HIPCHK(hipMemset(C->ptr, 0, (n + 1) * sizeof(int64_t)));
   const unsigned g1 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 3) / 4), 65536);
-  const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
+  int nbig = 0;
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1) {
       RCHK(dscan_incl_i64(C->ptr, C->ptr, n + 1, nullptr, err));
@@ -779,17 +769,21 @@ int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::strin
       RCHK(galloc(G, &C->val, C->nnz, err));
     }
     if (pass == 0) {
-      spgemm_kernel<TS1, 4, false><<<g1, 256>>>(n, nullptr, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
-                                                 nullptr, nullptr, ctr + 1);
+      spgemm_kernel<TS1, 4, false><<<g1, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
+                                                 nullptr, nullptr, ctr, big);
+      HIPCHK(hipGetLastError());
+      RCHK(read_int(ctr, &nbig, err));
+      const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
       if (nbig)
-        spgemm_kernel<TS2, 1, false><<<g2, 64>>>(nbig, big, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
-                                                  nullptr, nullptr, ctr + 1);
+        spgemm_kernel<TS2, 1, false><<<g2, 64>>>(nbig, big, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
+                                                  nullptr, nullptr, ctr, nullptr);
     } else {
-      spgemm_kernel<TS1, 4, true><<<g1, 256>>>(n, nullptr, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
-                                                C->col, C->val, ctr + 1);
+      const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
+      spgemm_kernel<TS1, 4, true><<<g1, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
+                                                C->col, C->val, ctr, big);
       if (nbig)
-        spgemm_kernel<TS2, 1, true><<<g2, 64>>>(nbig, big, ub, LIM1, A.ptr, A.col, A.val, B, C->ptr,
-                                                 C->col, C->val, ctr + 1);
+        spgemm_kernel<TS2, 1, true><<<g2, 64>>>(nbig, big, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
+                                                 C->col, C->val, ctr, nullptr);
     }
     HIPCHK(hipGetLastError());
     int ovf = 0;

@@ -45,16 +45,19 @@ def test_virtual_ranks_match_oracle(lib_built, dim, n, g, P, rep):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('mode', ['unfused', 'sell'])
+@pytest.mark.parametrize('mode', ['unfused', 'sell', 'merged'])
 def test_virtual_ranks_storage_variants(lib_built, monkeypatch, mode):
     """Distributed cycle without post fusion (prolongation, fine halo,
-    block-Jacobi sweep) and with SELL-64 storage forced onto the rank-local
-    operators: both equal the single-rank oracle apply."""
+    block-Jacobi sweep), with SELL-64 storage forced onto the rank-local
+    operators (K included), and with the [P | AP] post window instead of
+    K = P - W AP: all equal the single-rank oracle apply."""
     import torch
     import metric_amg_examples_amd as M
     kw = {}
     if mode == 'sell':
         monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    elif mode == 'merged':
+        monkeypatch.setenv('MAMG_POST_K', '0')
     else:
         kw['post_fusion'] = 0
     s = M.problems.bidomain(3, 16, 1e6)
