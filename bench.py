@@ -222,23 +222,26 @@ def main():
     # scripts/traffic.py from the committed PMC summaries of this config)
     fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
     post_mode = 'k' if fmt0.get('post_k') else 'merged'
+    a0_mode = 'half' if fmt0.get('half') else 'sell'
     traffic = {}
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
     if os.path.exists(tpath) and world == 1:
         try:
             tj = json.load(open(tpath))
-            if tj.get('N') == sysm.N and tj.get('layout') == layout and tj.get('post', 'merged') == post_mode:
+            if (tj.get('N') == sysm.N and tj.get('layout') == layout and tj.get('post', 'merged') == post_mode
+                    and tj.get('a0', 'sell') == a0_mode):
                 traffic = tj.get('kernels', {})
         except (OSError, ValueError):
             traffic = {}
 
+    rk = 'hsell2_kernel' if fmt0.get('half') else ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel')
     if layout == 'csr':
         names = ('csr_kernel<*,RESID,0>', 'csr_kernel<*,BJAC/JACOBI,0>')
     elif post_mode == 'k':
-        names = ('%s<RESID,...,0>' % ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel'),
+        names = ('%s<RESID,...,0>' % rk,
                  '%s<KPOST,...,0>' % ('sell2_kernel' if fmt0.get('post_sell') else 'bsr2_kernel'))
     else:
-        names = ('%s<RESID,...,0>' % ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel'),
+        names = ('%s<RESID,...,0>' % rk,
                  'bsr2_post_kernel<8,...,0>' if fmt0.get('post_fused', True) else 'bsr2_kernel<*,BJAC,...,0>')
     descr = ('level-0 residual r = b - A0 x', 'level-0 prolongation + post-smoothing '
              + ('z = x1 + W r1 + K e, K = P - W (A P)' if post_mode == 'k'

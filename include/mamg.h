@@ -239,9 +239,11 @@ int mamg_device_layout(const mamg_handle* h);
  * per symmetric 2x2 block), MAMG_FMT_POST_FUSED (prolongation fused with the
  * first post sweep), MAMG_FMT_POST_K (... through one stored operator
  * K = P - W (A P): z = x1 + W r1 + K e; else through [P | AP]),
- * MAMG_FMT_POST_SELL (K stored sliced-ELL).  Returns flags >= 0, or < 0. */
+ * MAMG_FMT_POST_SELL (K stored sliced-ELL), MAMG_FMT_HALF (A stored as its
+ * upper half, ELL-64, lower blocks read through their mirrors).
+ * Returns flags >= 0, or < 0. */
 enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_POST_K = 8,
-       MAMG_FMT_POST_SELL = 16 };
+       MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32 };
 int mamg_level_format(const mamg_handle* h, int level);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */

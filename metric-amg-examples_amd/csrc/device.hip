@@ -277,8 +277,8 @@ __global__ __launch_bounds__(256) void sell2_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
-    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os) {
-  const int64_t node = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
+  const int64_t node = row_block(remap) * 256 + threadIdx.x;
   if (node >= nr) return;
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int len = meta[node] & 0xffff;
@@ -322,6 +322,98 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   } else if (EPI == EPI_KPOST) {
     o0 = yy.x + (w.x * bb.x + w.y * bb.y) + s0;
     o1 = yy.y + (w.z * bb.x + w.w * bb.y) + s1;
+  } else {  // EPI_BJAC
+    const double r0 = bb.x - s0, r1 = bb.y - s1;
+    o0 = yy.x + (w.x * r0 + w.y * r1);
+    o1 = yy.y + (w.z * r0 + w.w * r1);
+  }
+  vset(out, os, node, 0, o0);
+  vset(out, os, node, 1, o1);
+}
+
+// ---------------------------------------------------------------------------
+// Half-symmetric ELL-64 for a symmetric A0 (A_JI = A_IJ^T bitwise and every
+// block symmetric, so A_JI = A_IJ): only the upper part J >= I is streamed
+// (28 B per block with its column); a lower entry J < I is a 4-byte slot
+// pointer to its mirror (J, I) in the upper part, whose row J the sweep
+// streamed a few MB earlier, so the re-read is served by L2 / the 256 MB
+// MALL instead of HBM.  The ELL slot p of upper block j of row J is
+// (J / 64) 64 hwu + 64 j + J % 64, so J = 64 (p / (64 hwu)) + p % 64 needs no
+// column.  For a translation-invariant stencil the 64 lanes' mirror slots
+// are 64 consecutive rows of one slot: the gathers are coalesced too.
+// Sums run lower part then upper part, each in column order: the full row's
+// block order, so the result is bitwise that of sell2_kernel.
+// ---------------------------------------------------------------------------
+template <int EPI, bool XFM, int U, int TAG>
+__global__ __launch_bounds__(256) void hsell2_kernel(
+    int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
+    const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
+    const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
+  const int64_t node = row_block(remap) * 256 + threadIdx.x;
+  if (node >= nr) return;
+  const double* offd = uval + 2 * nbs;
+  const int m = meta[node];
+  const int ulen = m & 0xffff, llen = m >> 16;
+  const uint32_t urow = 64u * (uint32_t)hwu;
+  double s0 = 0.0, s1 = 0.0;
+  {
+    const int64_t k = (node >> 6) * (int64_t)(64 * hwl) + (node & 63);
+    for (int j = 0; j < llen; j += U) {
+      uint32_t p[U];
+      dv4 v[U];
+      double2 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) p[u] = (uint32_t)lptr[k + (int64_t)SELL_C * (j + u < llen ? j + u : llen - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t c = (int32_t)((p[u] / urow) * 64u + (p[u] & 63u));
+        v[u] = blk<true>(uval, offd, p[u]);
+        a[u] = xget<XFM>(x, xs, c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j + u < llen;
+        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+      }
+    }
+  }
+  {
+    const int64_t k = (node >> 6) * (int64_t)urow + (node & 63);
+    for (int j = 0; j < ulen; j += U) {
+      int32_t c[U];
+      dv4 v[U];
+      double2 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t kk = k + (int64_t)SELL_C * (j + u < ulen ? j + u : ulen - 1);
+        c[u] = ucol[kk];
+        v[u] = blk<true>(uval, offd, kk);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j + u < ulen;
+        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+      }
+    }
+  }
+  double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
+  dv4 w = {0.0, 0.0, 0.0, 0.0};
+  if (EPI == EPI_RESID || EPI == EPI_BJAC)
+    bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
+  if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
+  if (EPI == EPI_BJAC) w = W[node];
+  double o0, o1;
+  if (EPI == EPI_Y) {
+    o0 = s0; o1 = s1;
+  } else if (EPI == EPI_YADD) {
+    o0 = yy.x + s0; o1 = yy.y + s1;
+  } else if (EPI == EPI_RESID) {
+    o0 = bb.x - s0; o1 = bb.y - s1;
   } else {  // EPI_BJAC
     const double r0 = bb.x - s0, r1 = bb.y - s1;
     o0 = yy.x + (w.x * r0 + w.y * r1);
@@ -493,7 +585,17 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_POST_K     0: fused post sweep over [P | AP] instead of K = P - W A P (default 1)
 //   MAMG_POST_SELL  0: K in lane-group BSR instead of SELL-64 (default 1)
 //   MAMG_POST_U     SELL blocks per chunk of the K kernel (4 default, 8, 16)
+//   MAMG_SELL_REMAP 1: XCD-contiguous row order for the level-0 SELL kernels
+//   MAMG_SELL_MAX_LEN SELL only for matrices with <= this many blocks per row (40)
+//   MAMG_HALF       0: full SELL-64 instead of the half-symmetric ELL-64 for A0 (default 1)
+//   MAMG_HALF_U     blocks per chunk of the half-symmetric kernel (4 default, 8)
+//   MAMG_HALF_REMAP XCD-contiguous row order for the half-symmetric kernel (default 1:
+//                   the mirror re-reads then hit the XCD's own L2)
 int g_remap = 1;
+int g_sell_remap = 0;
+int g_half = 1;
+int g_half_u = 4;
+int g_half_remap = 1;
 int g_post_lanes = 0;
 int g_sym = 1;
 int g_sell = 1;
@@ -504,6 +606,7 @@ int g_post_k = 1;
 int g_post_u = 4;
 int g_post_sell = 1;
 int64_t g_sell_min_rows = 1 << 20;
+int64_t g_sell_max_len = 40;
 void read_knobs() {
   const char* pk = std::getenv("MAMG_POST_K");
   g_post_k = pk ? std::atoi(pk) != 0 : 1;
@@ -523,6 +626,17 @@ void read_knobs() {
   g_sell = s ? std::atoi(s) : 1;
   s = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = s ? std::atoll(s) : (1 << 20);
+  s = std::getenv("MAMG_SELL_MAX_LEN");
+  g_sell_max_len = s ? std::atoll(s) : 40;
+  su = std::getenv("MAMG_HALF");
+  g_half = su ? std::atoi(su) != 0 : 1;
+  su = std::getenv("MAMG_HALF_U");
+  g_half_u = su ? std::atoi(su) : 4;
+  if (g_half_u != 4 && g_half_u != 8) g_half_u = 4;
+  su = std::getenv("MAMG_HALF_REMAP");
+  g_half_remap = su ? std::atoi(su) != 0 : 1;
+  su = std::getenv("MAMG_SELL_REMAP");
+  g_sell_remap = su ? std::atoi(su) != 0 : 0;
   const char* e = std::getenv("MAMG_XCD_REMAP");
   g_remap = e ? std::atoi(e) : 1;
   e = std::getenv("MAMG_POST_LANES");
@@ -574,6 +688,14 @@ struct DBsr {              // 2x2 blocks, node-major
   int64_t* soff = nullptr;
   int32_t* meta = nullptr;
   int32_t* perm = nullptr;  // SELL-C-sigma: row held by each slot (merged matrices)
+  // half-symmetric ELL-64 (half == true, A symmetric bitwise): col / val hold
+  // the upper part J >= I, hwu slots per row; lptr holds, per lower entry
+  // J < I, the slot of the mirror block (J, I) in the upper part, hwl slots
+  // per row; meta = upper length | lower length << 16
+  bool half = false;
+  int hwu = 0, hwl = 0;
+  int64_t nlo = 0;          // lower entries (nb = upper entries + nlo)
+  int32_t* lptr = nullptr;
 };
 
 struct DLevel {
@@ -746,7 +868,7 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
   int rc;
   // SELL-64 for many short rows (one lane per row needs >> 256 CUs x 64 rows)
   const bool merged_rows = np == 2 * B.nr + 1;
-  if (g_sell && B.nr >= g_sell_min_rows && D->nb <= 40 * B.nr && (!merged_rows || g_sell_post)) {
+  if (g_sell && B.nr >= g_sell_min_rows && D->nb <= g_sell_max_len * B.nr && (!merged_rows || g_sell_post)) {
     D->sym = sym && g_sym && np == B.nr + 1 && blocks_symmetric(B);
     return upload_sell(h, B, D, err);
   }
@@ -935,6 +1057,71 @@ __global__ __launch_bounds__(256) void sell_fill_kernel(int64_t nr, const int64_
   }
 }
 
+// half-symmetric ELL-64: lower counts, row meta, widths (atomicMax)
+__global__ __launch_bounds__(256) void half_meta_kernel(int64_t nr, const int64_t* __restrict__ bptr,
+                                                        const int32_t* __restrict__ bcol, int32_t* __restrict__ lcnt,
+                                                        int32_t* __restrict__ meta, int* wmax,
+                                                        unsigned long long* nlo) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t lo = bptr[I], hi = bptr[I + 1];
+  const int64_t len = hi - lo;
+  while (lo < hi) {            // first column >= I
+    const int64_t mid = (lo + hi) >> 1;
+    if (bcol[mid] < I) lo = mid + 1; else hi = mid;
+  }
+  const int64_t nl = lo - bptr[I], nu = len - nl;
+  if (len >= 0x7fff) { atomicOr(wmax + 2, 1); return; }
+  atomicAdd(nlo, (unsigned long long)nl);
+  lcnt[I] = (int32_t)nl;
+  meta[I] = (int32_t)(nu | (nl << 16));
+  atomicMax(wmax, (int)nu);
+  atomicMax(wmax + 1, (int)nl);
+}
+
+// upper blocks into their ELL slots (symmetric-block packing); every lower
+// block (I, J) must have a bitwise-equal mirror (J, I), whose upper slot it
+// records
+__global__ __launch_bounds__(256) void half_fill_kernel(int64_t nr, const int64_t* __restrict__ bptr,
+                                                        const int32_t* __restrict__ bcol, const dv4* __restrict__ bval,
+                                                        const int32_t* __restrict__ lcnt, int hwu, int hwl, int64_t nbs,
+                                                        int32_t* __restrict__ ucol, double* __restrict__ uval,
+                                                        int32_t* __restrict__ lptr, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  const int64_t a = bptr[I], e = bptr[I + 1], nl = lcnt[I];
+  const int64_t ubase = (I >> 6) * (int64_t)(64 * hwu) + (I & 63);
+  for (int64_t k = a + nl, j = 0; k < e; ++k, ++j) {
+    const int64_t kk = ubase + 64 * j;
+    const dv4 v = bval[k];
+    ucol[kk] = bcol[k];
+    uval[2 * kk] = v.x;
+    uval[2 * kk + 1] = v.w;
+    uval[2 * nbs + kk] = v.y;
+  }
+  const int64_t lbase = (I >> 6) * (int64_t)(64 * hwl) + (I & 63);
+  for (int64_t k = a, j = 0; k < a + nl; ++k, ++j) {
+    const int64_t J = bcol[k];
+    int64_t lo = bptr[J] + lcnt[J], hi = bptr[J + 1];
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (bcol[mid] < I) lo = mid + 1; else hi = mid;
+    }
+    const dv4 v = bval[k];
+    bool ok = lo < bptr[J + 1] && bcol[lo] == I;
+    if (ok) {
+      const dv4 t = bval[lo];
+      ok = __double_as_longlong(v.x) == __double_as_longlong(t.x) &&
+           __double_as_longlong(v.y) == __double_as_longlong(t.z) &&
+           __double_as_longlong(v.z) == __double_as_longlong(t.y) &&
+           __double_as_longlong(v.w) == __double_as_longlong(t.w);
+    }
+    if (!ok) { atomicOr(bad, 1); return; }
+    const int64_t jj = lo - bptr[J] - lcnt[J];
+    lptr[lbase + 64 * j] = (int32_t)((J >> 6) * (int64_t)(64 * hwu) + 64 * jj + (J & 63));
+  }
+}
+
 // coarsest inverse, dof order -> node-interleaved order
 __global__ __launch_bounds__(256) void permute_dense_kernel(int64_t n, const double* __restrict__ in,
                                                             double* __restrict__ out) {
@@ -1022,12 +1209,71 @@ int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* 
   return MAMG_OK;
 }
 
+// half-symmetric ELL-64 for a square symmetric-block A (hsell2_kernel).
+// Returns MAMG_OK with D->half set, or MAMG_OK with D->half false when A is
+// not symmetric bitwise or the ELL padding would exceed ~30 % (then the
+// caller builds SELL-64); device arrays of a rejected attempt are freed.
+template <class HT>
+int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
+  int rc;
+  const int64_t nr = B.nr, ns = (nr + SELL_C - 1) / SELL_C;
+  int32_t* lcnt = nullptr;
+  int* wm = nullptr;   // [0] max upper, [1] max lower, [2] too long, [3] not symmetric
+  if ((rc = T->alloc(&lcnt, nr, err))) return rc;
+  if ((rc = T->alloc(&wm, 4, err))) return rc;
+  HIPCHK(hipMemset(wm, 0, 4 * sizeof(int)));
+  int32_t* meta = nullptr;
+  unsigned long long* nlod = nullptr;
+  if ((rc = T->alloc(&meta, nr, err))) return rc;
+  if ((rc = T->alloc(&nlod, 1, err))) return rc;
+  HIPCHK(hipMemset(nlod, 0, sizeof(unsigned long long)));
+  half_meta_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, lcnt, meta, wm, nlod);
+  HIPCHK(hipGetLastError());
+  int hw[4] = {0, 0, 0, 0};
+  unsigned long long nloh = 0;
+  HIPCHK(hipMemcpy(hw, wm, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&nloh, nlod, sizeof(nloh), hipMemcpyDeviceToHost));
+  if (hw[2]) return MAMG_OK;
+  const int64_t nlo = (int64_t)nloh, nup = B.nb - nlo;
+  const int64_t su = 64 * ns * (int64_t)hw[0], sl = 64 * ns * (int64_t)hw[1];
+  if (su >= (int64_t)1 << 31 || (double)su > 1.3 * nup + 4096 || (double)sl > 1.3 * nlo + 4096) return MAMG_OK;
+  int32_t *ucol = nullptr, *lptr = nullptr;
+  double* uval = nullptr;
+  if ((rc = T->alloc(&ucol, su, err))) return rc;
+  if ((rc = T->alloc(&uval, 3 * su, err))) return rc;
+  if ((rc = T->alloc(&lptr, sl, err))) return rc;
+  HIPCHK(hipMemset(ucol, 0, std::max<int64_t>(su, 1) * sizeof(int32_t)));
+  HIPCHK(hipMemset(uval, 0, std::max<int64_t>(3 * su, 1) * sizeof(double)));
+  HIPCHK(hipMemset(lptr, 0, std::max<int64_t>(sl, 1) * sizeof(int32_t)));
+  half_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, B.val, lcnt, hw[0], hw[1], su, ucol, uval, lptr,
+                                         wm + 3);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(&hw[3], wm + 3, sizeof(int), hipMemcpyDeviceToHost));
+  if (hw[3]) return MAMG_OK;
+  // accepted: move into handle-owned memory
+  if ((rc = dalloc(h, &D->meta, std::max<int64_t>(nr, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(su, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(3 * su, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->lptr, std::max<int64_t>(sl, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->meta, meta, nr * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->col, ucol, std::max<int64_t>(su, 1) * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->val, uval, std::max<int64_t>(3 * su, 1) * sizeof(double), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->lptr, lptr, std::max<int64_t>(sl, 1) * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  T->release(ucol); T->release(uval); T->release(lptr);
+  D->half = true;
+  D->hwu = hw[0];
+  D->hwl = hw[1];
+  D->nbs = su;
+  D->nlo = nlo;
+  return MAMG_OK;
+}
+
 // final apply layout from a raw device BSR (the device-side counterpart of
 // upload_bsr): SELL-64 for large short-row plain matrices, symmetric-block
 // packing where every block has (0,1) == (1,0) bitwise, else 4 doubles/block
 template <class HT>
 int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, std::string* err,
-                 bool allow_sell = true) {
+                 bool allow_sell = true, bool allow_half = false) {
   int rc;
   const int64_t nr = B.nr, np = B.merged ? 2 * nr + 1 : nr + 1;
   D->nr = nr;
@@ -1046,7 +1292,11 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   }
   D->sym = sym;
   const int per = sym ? 3 : 4;
-  if (allow_sell && g_sell && nr >= g_sell_min_rows && D->nb <= 40 * nr && !B.merged) {
+  if (allow_sell && g_sell && nr >= g_sell_min_rows && D->nb <= g_sell_max_len * nr && !B.merged) {
+    if (allow_half && g_half && sym && nr == B.nc) {
+      if ((rc = try_half(h, T, B, D, err))) return rc;
+      if (D->half) return MAMG_OK;
+    }
     const int64_t ns = (nr + SELL_C - 1) / SELL_C;
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
@@ -1106,7 +1356,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr B;
     if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true, l == 0))) return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
   if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n) {
@@ -1171,7 +1421,10 @@ double index_bytes(const DBsr& M, int64_t ptr_entries) {
 }
 
 double bsr_bytes(const DBsr& M, int epi) {
-  double b = (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;  // A, x, out
+  // half-symmetric: upper blocks (28 B with column) + 4-byte mirror slot per
+  // lower block + row meta; the mirrors' values are re-reads, not counted
+  double b = M.half ? 28.0 * (M.nb - M.nlo) + 4.0 * M.nlo + 4.0 * M.nr + 16.0 * M.nc + 16.0 * M.nr
+                    : (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;
   if (epi == EPI_YADD) b += 16.0 * M.nr;
   if (epi == EPI_RESID) b += 16.0 * M.nr;
   if (epi == EPI_BJAC || epi == EPI_KPOST) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;   // y, b, W
@@ -1417,7 +1670,8 @@ void launch_sell_u(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
-#define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os
+#define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
+    (TAG == 0 ? g_sell_remap : 0)
   switch (o.epi) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
@@ -1496,8 +1750,35 @@ void launch_post_tag(const Op& o, hipStream_t s) {
   }
 }
 
+template <bool XFM, int U, int TAG>
+void launch_half_u(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const unsigned g = nblocks(M.nr);
+  if (g == 0) return;
+#define HALF_ARGS M.nr, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, o.x, o.xs, o.y, o.b, o.bs, o.W, \
+    o.out, o.os, (TAG == 0 ? g_half_remap : 0)
+  switch (o.epi) {
+    case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_RESID: hsell2_kernel<EPI_RESID, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_KPOST: break;   // A is never the K operator
+    default: hsell2_kernel<EPI_BJAC, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+  }
+#undef HALF_ARGS
+}
+
+template <int TAG>
+void launch_half(const Op& o, hipStream_t s) {
+  if (o.xfm) {
+    if (g_half_u == 4) launch_half_u<true, 4, TAG>(o, s); else launch_half_u<true, 8, TAG>(o, s);
+  } else {
+    if (g_half_u == 4) launch_half_u<false, 4, TAG>(o, s); else launch_half_u<false, 8, TAG>(o, s);
+  }
+}
+
 template <int TAG>
 void launch_bsr_tag(const Op& o, hipStream_t s) {
+  if (o.Mb->half) { launch_half<TAG>(o, s); return; }
   if (o.Mb->sell) { launch_sell<TAG>(o, s); return; }
   switch (o.Mb->lanes) {
     case 2: launch_bsr_vl<2, TAG>(o, s); break;
@@ -1739,7 +2020,7 @@ double dev_apply_bytes(const DeviceHandle* h) { return h->apply_bytes; }
 int dev_layout(const DeviceHandle* h) { return h->bsr ? 1 : 0; }
 int dev_level_format(const DeviceHandle* h, int level) {
   const DLevel& L = h->L[level];
-  return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) |
+  return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) | (L.Ab.half ? MAMG_FMT_HALF : 0) |
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
          (L.KPb.sell ? MAMG_FMT_POST_SELL : 0);
 }

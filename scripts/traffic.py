@@ -25,13 +25,13 @@ WRITE_SCALE = 1024
 
 
 def classify(name):
-    m = re.search(r'(sell2_kernel|bsr2_kernel|bsr2_post_kernel)<([^>]*)>', name)
+    m = re.search(r'(hsell2_kernel|sell2_kernel|bsr2_kernel|bsr2_post_kernel)<([^>]*)>', name)
     if not m:
         return None
     kind, targs = m.group(1), [t.strip() for t in m.group(2).split(',')]
     if kind == 'bsr2_post_kernel':
         return 'L0_smooth_spmv' if targs[-1] == '0' else None
-    epi, xfm = (targs[0], targs[1]) if kind == 'sell2_kernel' else (targs[1], targs[2])
+    epi, xfm = (targs[0], targs[1]) if kind in ('sell2_kernel', 'hsell2_kernel') else (targs[1], targs[2])
     if targs[-1] != '0':
         return None
     if epi == '2' and xfm == 'false':   # EPI_RESID on the internal vectors
@@ -66,6 +66,8 @@ def main():
     ap.add_argument('--layout', default='bsr2')
     ap.add_argument('--post', default='k', choices=('k', 'merged'),
                     help='post-smoothing operator the profiled run used (MAMG_POST_K)')
+    ap.add_argument('--a0', default='half', choices=('half', 'sell'),
+                    help='level-0 operator storage of the profiled run')
     ap.add_argument('--out', default='profiles/traffic.json')
     a = ap.parse_args()
     f = collect(a.fetch_csv, 'FETCH_SIZE')
@@ -77,7 +79,7 @@ def main():
         kernels[c] = round(fb + wb, 1)
         detail[c] = {'grid': f[c][0], 'launches': f[c][2], 'fetch_bytes': round(fb, 1),
                      'write_bytes': round(wb, 1)}
-    out = {'layout': a.layout, 'N': a.N, 'post': a.post, 'kernels': kernels, 'detail': detail,
+    out = {'layout': a.layout, 'N': a.N, 'post': a.post, 'a0': a.a0, 'kernels': kernels, 'detail': detail,
            'calibration': 'bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (profiles/r01_pmc_calibration.txt)'}
     json.dump(out, open(a.out, 'w'), indent=1)
     print(json.dumps(out))

@@ -224,6 +224,59 @@ def test_symmetric_blocks_and_xcd_remap_bitwise(lib_built, monkeypatch, remap):
     assert np.array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e3, dict(maxit=2, presmooth_iter=2,
+                                                                                   postsmooth_iter=2)),
+                                        (3, 16, 1e4, dict(post_fusion=0))])
+@pytest.mark.parametrize('env', [dict(), dict(MAMG_HALF_U='8'), dict(MAMG_HALF_REMAP='0')])
+def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw, env):
+    """Half-symmetric ELL-64 A_0 (upper blocks streamed, lower blocks read
+    through their mirrors) sums every row in the full row's block order: the
+    apply and the device PCG are bitwise those of full SELL-64 storage."""
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    outs, its = [], []
+    for half in ('1', '0'):
+        monkeypatch.setenv('MAMG_HALF', half)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+        f = B.level_format(0)
+        assert f['sell'] != (half == '1') and f['half'] == (half == '1') and f['sym']
+        outs.append(B * r)
+        solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        solver * r
+        its.append(solver.residuals)
+        B.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert its[0] == its[1]
+    h = mo.setup(A, mo.Params(num_functions=2, **oracle_kw(kw)), idofs=s.idofs)
+    assert rel(outs[0], h.apply(r)) < APPLY_TOL
+
+
+def test_half_symmetric_rejects_nonsymmetric(lib_built, monkeypatch):
+    """A_0 whose 2x2 blocks are symmetric but A_IJ != A_JI in one ulp: the
+    mirror check rejects the half format (full SELL-64 is used) and the apply
+    still matches the oracle."""
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 8, 1e2)
+    A = s.scipy().tocsr().copy()
+    row = int(np.argmax(np.diff(A.indptr)[:s.nv]))      # an interior field-0 row
+    k = next(k for k in range(A.indptr[row], A.indptr[row + 1]) if A.indices[k] != row
+             and A.indices[k] < s.nv)
+    A.data[k] = np.nextafter(A.data[k], np.inf)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    f = B.level_format(0)
+    assert f['sell'] and not f['half']
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    assert rel(B * r, h.apply(r)) < APPLY_TOL
+    B.close()
+
+
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (3, 16, 1e10, dict()),
                                         (2, 64, 1e3, dict(maxit=2, presmooth_iter=2, postsmooth_iter=2)),
                                         (3, 16, 1e4, dict(cycle_type='W')),
