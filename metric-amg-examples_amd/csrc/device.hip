@@ -344,17 +344,18 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 // Sums run lower part then upper part, each in column order: the full row's
 // block order, so the result is bitwise that of sell2_kernel.
 // ---------------------------------------------------------------------------
-template <int EPI, bool XFM, int U, int TAG>
+template <int EPI, bool XFM, int U, bool GH, int TAG>
 __global__ __launch_bounds__(256) void hsell2_kernel(
     int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
     const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
-    const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
+    const int64_t* __restrict__ gsoff, const int32_t* __restrict__ gcol, const double* __restrict__ gval,
+    int64_t ngs, const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
     int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
   const int64_t node = row_block(remap) * 256 + threadIdx.x;
   if (node >= nr) return;
   const double* offd = uval + 2 * nbs;
   const int m = meta[node];
-  const int ulen = m & 0xffff, llen = m >> 16;
+  const int ulen = m & 0xff, llen = (m >> 8) & 0xff;
   const uint32_t urow = 64u * (uint32_t)hwu;
   double s0 = 0.0, s1 = 0.0;
   {
@@ -396,6 +397,30 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const bool ok = j + u < ulen;
+        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+      }
+    }
+  }
+  if (GH) {   // ghost columns (after every owned column in the row's order)
+    const int glen = m >> 16;
+    const int64_t k = gsoff[node >> 6] + (node & 63);
+    const double* goff = gval + 2 * ngs;
+    for (int j = 0; j < glen; j += U) {
+      int32_t c[U];
+      dv4 v[U];
+      double2 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t kk = k + (int64_t)SELL_C * (j + u < glen ? j + u : glen - 1);
+        c[u] = gcol[kk];
+        v[u] = blk<true>(gval, goff, kk);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j + u < glen;
         s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
         s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
       }
@@ -689,13 +714,19 @@ struct DBsr {              // 2x2 blocks, node-major
   int32_t* meta = nullptr;
   int32_t* perm = nullptr;  // SELL-C-sigma: row held by each slot (merged matrices)
   // half-symmetric ELL-64 (half == true, A symmetric bitwise): col / val hold
-  // the upper part J >= I, hwu slots per row; lptr holds, per lower entry
-  // J < I, the slot of the mirror block (J, I) in the upper part, hwl slots
-  // per row; meta = upper length | lower length << 16
+  // the upper part I <= J < nr, hwu slots per row; lptr holds,
+  // per lower entry J < I, the slot of the mirror block (J, I) in the upper
+  // part, hwl slots per row; ghost columns (>= nr, multi-GPU rank-local A)
+  // in their own SELL-64 part (gsoff per slice, zero width where a slice has
+  // none); meta = upper length | lower length << 8 | ghost length << 16
   bool half = false;
   int hwu = 0, hwl = 0;
-  int64_t nlo = 0;          // lower entries (nb = upper entries + nlo)
+  int64_t nlo = 0;          // lower entries (nb = upper + ghost entries + nlo)
   int32_t* lptr = nullptr;
+  int64_t ngs = 0;          // ghost-part slots (0: no ghost part)
+  int64_t* gsoff = nullptr;
+  int32_t* gcol = nullptr;
+  double* gval = nullptr;
 };
 
 struct DLevel {
@@ -1057,41 +1088,62 @@ __global__ __launch_bounds__(256) void sell_fill_kernel(int64_t nr, const int64_
   }
 }
 
-// half-symmetric ELL-64: lower counts, row meta, widths (atomicMax)
+// half-symmetric ELL-64: per-row lower / upper / ghost counts (meta),
+// widths (atomicMax), lower-entry total
 __global__ __launch_bounds__(256) void half_meta_kernel(int64_t nr, const int64_t* __restrict__ bptr,
-                                                        const int32_t* __restrict__ bcol, int32_t* __restrict__ lcnt,
+                                                        const int32_t* __restrict__ bcol,
                                                         int32_t* __restrict__ meta, int* wmax,
                                                         unsigned long long* nlo) {
   const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (I >= nr) return;
-  int64_t lo = bptr[I], hi = bptr[I + 1];
-  const int64_t len = hi - lo;
+  const int64_t a = bptr[I], e = bptr[I + 1];
+  int64_t lo = a, hi = e;
   while (lo < hi) {            // first column >= I
     const int64_t mid = (lo + hi) >> 1;
     if (bcol[mid] < I) lo = mid + 1; else hi = mid;
   }
-  const int64_t nl = lo - bptr[I], nu = len - nl;
-  if (len >= 0x7fff) { atomicOr(wmax + 2, 1); return; }
+  const int64_t nl = lo - a;
+  hi = e;
+  while (lo < hi) {            // first column >= nr (ghosts)
+    const int64_t mid = (lo + hi) >> 1;
+    if (bcol[mid] < nr) lo = mid + 1; else hi = mid;
+  }
+  const int64_t ng = e - lo, nu = e - a - nl - ng;
+  if (nu > 0xff || nl > 0xff || ng > 0x7fff) { atomicOr(wmax + 2, 1); return; }
   atomicAdd(nlo, (unsigned long long)nl);
-  lcnt[I] = (int32_t)nl;
-  meta[I] = (int32_t)(nu | (nl << 16));
+  meta[I] = (int32_t)(nu | (nl << 8) | (ng << 16));
   atomicMax(wmax, (int)nu);
   atomicMax(wmax + 1, (int)nl);
 }
 
-// upper blocks into their ELL slots (symmetric-block packing); every lower
-// block (I, J) must have a bitwise-equal mirror (J, I), whose upper slot it
-// records
+// ghost-part slice widths (slot counts, scanned into gsoff afterwards)
+__global__ __launch_bounds__(256) void half_gwidth_kernel(int64_t nr, const int32_t* __restrict__ meta,
+                                                          int64_t* __restrict__ gsoff) {
+  const int64_t sl = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t ns = (nr + SELL_C - 1) / SELL_C;
+  if (sl >= ns) return;
+  int w = 0;
+  for (int64_t I = sl * SELL_C; I < min(nr, (sl + 1) * SELL_C); ++I) w = max(w, meta[I] >> 16);
+  gsoff[sl + 1] = (int64_t)SELL_C * w;
+  if (sl == 0) gsoff[0] = 0;
+}
+
+// upper blocks into their ELL slots, ghost blocks into the ghost SELL part
+// (symmetric-block packing); every lower block (I, J) must have a
+// bitwise-equal mirror (J, I), whose upper slot it records
 __global__ __launch_bounds__(256) void half_fill_kernel(int64_t nr, const int64_t* __restrict__ bptr,
                                                         const int32_t* __restrict__ bcol, const dv4* __restrict__ bval,
-                                                        const int32_t* __restrict__ lcnt, int hwu, int hwl, int64_t nbs,
+                                                        const int32_t* __restrict__ meta, int hwu, int hwl, int64_t nbs,
                                                         int32_t* __restrict__ ucol, double* __restrict__ uval,
-                                                        int32_t* __restrict__ lptr, int* bad) {
+                                                        int32_t* __restrict__ lptr, const int64_t* __restrict__ gsoff,
+                                                        int64_t ngs, int32_t* __restrict__ gcol,
+                                                        double* __restrict__ gval, int* bad, int check_only) {
   const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (I >= nr) return;
-  const int64_t a = bptr[I], e = bptr[I + 1], nl = lcnt[I];
+  const int mI = meta[I];
+  const int64_t a = bptr[I], e = bptr[I + 1], nl = (mI >> 8) & 0xff, ng = mI >> 16;
   const int64_t ubase = (I >> 6) * (int64_t)(64 * hwu) + (I & 63);
-  for (int64_t k = a + nl, j = 0; k < e; ++k, ++j) {
+  for (int64_t k = a + nl, j = 0; k < e - ng && !check_only; ++k, ++j) {
     const int64_t kk = ubase + 64 * j;
     const dv4 v = bval[k];
     ucol[kk] = bcol[k];
@@ -1099,16 +1151,29 @@ __global__ __launch_bounds__(256) void half_fill_kernel(int64_t nr, const int64_
     uval[2 * kk + 1] = v.w;
     uval[2 * nbs + kk] = v.y;
   }
+  if (ng && !check_only) {
+    const int64_t gbase = gsoff[I >> 6] + (I & 63);
+    for (int64_t k = e - ng, j = 0; k < e; ++k, ++j) {
+      const int64_t kk = gbase + 64 * j;
+      const dv4 v = bval[k];
+      gcol[kk] = bcol[k];
+      gval[2 * kk] = v.x;
+      gval[2 * kk + 1] = v.w;
+      gval[2 * ngs + kk] = v.y;
+    }
+  }
   const int64_t lbase = (I >> 6) * (int64_t)(64 * hwl) + (I & 63);
   for (int64_t k = a, j = 0; k < a + nl; ++k, ++j) {
     const int64_t J = bcol[k];
-    int64_t lo = bptr[J] + lcnt[J], hi = bptr[J + 1];
+    const int mJ = meta[J];
+    const int64_t uJ = bptr[J] + ((mJ >> 8) & 0xff), eJ = uJ + (mJ & 0xff);
+    int64_t lo = uJ, hi = eJ;
     while (lo < hi) {
       const int64_t mid = (lo + hi) >> 1;
       if (bcol[mid] < I) lo = mid + 1; else hi = mid;
     }
     const dv4 v = bval[k];
-    bool ok = lo < bptr[J + 1] && bcol[lo] == I;
+    bool ok = lo < eJ && bcol[lo] == I;
     if (ok) {
       const dv4 t = bval[lo];
       ok = __double_as_longlong(v.x) == __double_as_longlong(t.x) &&
@@ -1117,7 +1182,8 @@ __global__ __launch_bounds__(256) void half_fill_kernel(int64_t nr, const int64_
            __double_as_longlong(v.w) == __double_as_longlong(t.w);
     }
     if (!ok) { atomicOr(bad, 1); return; }
-    const int64_t jj = lo - bptr[J] - lcnt[J];
+    if (check_only) continue;
+    const int64_t jj = lo - uJ;
     lptr[lbase + 64 * j] = (int32_t)((J >> 6) * (int64_t)(64 * hwu) + 64 * jj + (J & 63));
   }
 }
@@ -1209,63 +1275,105 @@ int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* 
   return MAMG_OK;
 }
 
-// half-symmetric ELL-64 for a square symmetric-block A (hsell2_kernel).
-// Returns MAMG_OK with D->half set, or MAMG_OK with D->half false when A is
-// not symmetric bitwise or the ELL padding would exceed ~30 % (then the
-// caller builds SELL-64); device arrays of a rejected attempt are freed.
+// half-symmetric ELL-64 for a symmetric-block A whose owned part (columns
+// < nr) is symmetric bitwise; columns >= nr (ghosts of a rank-local A) go to
+// the ghost part (hsell2_kernel).  Returns MAMG_OK with D->half set, or
+// MAMG_OK with D->half false when a mirror is missing or differs, a row part
+// is too long, or the ELL padding would exceed ~30 % (the caller then builds
+// SELL-64); temporaries of a rejected attempt are freed with the pool.
 template <class HT>
 int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
   int rc;
   const int64_t nr = B.nr, ns = (nr + SELL_C - 1) / SELL_C;
-  int32_t* lcnt = nullptr;
-  int* wm = nullptr;   // [0] max upper, [1] max lower, [2] too long, [3] not symmetric
-  if ((rc = T->alloc(&lcnt, nr, err))) return rc;
-  if ((rc = T->alloc(&wm, 4, err))) return rc;
-  HIPCHK(hipMemset(wm, 0, 4 * sizeof(int)));
+  int* wm = nullptr;   // [0] max upper, [1] max lower, [2] part too long, [3] not symmetric
   int32_t* meta = nullptr;
   unsigned long long* nlod = nullptr;
+  int64_t* gsoff = nullptr;
+  if ((rc = T->alloc(&wm, 4, err))) return rc;
   if ((rc = T->alloc(&meta, nr, err))) return rc;
   if ((rc = T->alloc(&nlod, 1, err))) return rc;
+  if ((rc = T->alloc(&gsoff, ns + 1, err))) return rc;
+  HIPCHK(hipMemset(wm, 0, 4 * sizeof(int)));
   HIPCHK(hipMemset(nlod, 0, sizeof(unsigned long long)));
-  half_meta_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, lcnt, meta, wm, nlod);
+  half_meta_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, meta, wm, nlod);
   HIPCHK(hipGetLastError());
   int hw[4] = {0, 0, 0, 0};
   unsigned long long nloh = 0;
   HIPCHK(hipMemcpy(hw, wm, 4 * sizeof(int), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(&nloh, nlod, sizeof(nloh), hipMemcpyDeviceToHost));
   if (hw[2]) return MAMG_OK;
-  const int64_t nlo = (int64_t)nloh, nup = B.nb - nlo;
+  half_gwidth_kernel<<<nblocks(ns), 256>>>(nr, meta, gsoff);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(gsoff, gsoff, ns + 1, nullptr, err))) return rc;
+  int64_t ngs = 0;
+  HIPCHK(hipMemcpy(&ngs, gsoff + ns, sizeof(int64_t), hipMemcpyDeviceToHost));
+  const int64_t nlo = (int64_t)nloh;
   const int64_t su = 64 * ns * (int64_t)hw[0], sl = 64 * ns * (int64_t)hw[1];
-  if (su >= (int64_t)1 << 31 || (double)su > 1.3 * nup + 4096 || (double)sl > 1.3 * nlo + 4096) return MAMG_OK;
-  int32_t *ucol = nullptr, *lptr = nullptr;
-  double* uval = nullptr;
-  if ((rc = T->alloc(&ucol, su, err))) return rc;
-  if ((rc = T->alloc(&uval, 3 * su, err))) return rc;
-  if ((rc = T->alloc(&lptr, sl, err))) return rc;
-  HIPCHK(hipMemset(ucol, 0, std::max<int64_t>(su, 1) * sizeof(int32_t)));
-  HIPCHK(hipMemset(uval, 0, std::max<int64_t>(3 * su, 1) * sizeof(double)));
-  HIPCHK(hipMemset(lptr, 0, std::max<int64_t>(sl, 1) * sizeof(int32_t)));
-  half_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, B.val, lcnt, hw[0], hw[1], su, ucol, uval, lptr,
-                                         wm + 3);
+  const int64_t nup = B.nb - nlo;   // upper + ghost entries
+  if (su >= (int64_t)1 << 31 || (double)(su + ngs) > 1.3 * nup + 4096 || (double)sl > 1.3 * nlo + 4096)
+    return MAMG_OK;
+  half_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, B.val, meta, hw[0], hw[1], su, nullptr, nullptr,
+                                         nullptr, nullptr, 0, nullptr, nullptr, wm + 3, 1);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(&hw[3], wm + 3, sizeof(int), hipMemcpyDeviceToHost));
-  if (hw[3]) return MAMG_OK;
-  // accepted: move into handle-owned memory
+  if (hw[3]) return MAMG_OK;   // a mirror is missing or differs
   if ((rc = dalloc(h, &D->meta, std::max<int64_t>(nr, 1), err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(su, 1), err))) return rc;
   if ((rc = dalloc(h, &D->val, std::max<int64_t>(3 * su, 1), err))) return rc;
   if ((rc = dalloc(h, &D->lptr, std::max<int64_t>(sl, 1), err))) return rc;
+  if (ngs) {
+    if ((rc = dalloc(h, &D->gsoff, ns + 1, err))) return rc;
+    if ((rc = dalloc(h, &D->gcol, ngs, err))) return rc;
+    if ((rc = dalloc(h, &D->gval, 3 * ngs, err))) return rc;
+    HIPCHK(hipMemcpy(D->gsoff, gsoff, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+    HIPCHK(hipMemset(D->gcol, 0, ngs * sizeof(int32_t)));
+    HIPCHK(hipMemset(D->gval, 0, 3 * ngs * sizeof(double)));
+  }
   HIPCHK(hipMemcpy(D->meta, meta, nr * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->col, ucol, std::max<int64_t>(su, 1) * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->val, uval, std::max<int64_t>(3 * su, 1) * sizeof(double), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->lptr, lptr, std::max<int64_t>(sl, 1) * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  T->release(ucol); T->release(uval); T->release(lptr);
+  HIPCHK(hipMemset(D->col, 0, std::max<int64_t>(su, 1) * sizeof(int32_t)));
+  HIPCHK(hipMemset(D->val, 0, std::max<int64_t>(3 * su, 1) * sizeof(double)));
+  HIPCHK(hipMemset(D->lptr, 0, std::max<int64_t>(sl, 1) * sizeof(int32_t)));
+  half_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, B.val, meta, hw[0], hw[1], su, D->col, D->val, D->lptr,
+                                         D->gsoff, ngs, D->gcol, D->gval, wm + 3, 0);
+  HIPCHK(hipGetLastError());
   D->half = true;
   D->hwu = hw[0];
   D->hwl = hw[1];
   D->nbs = su;
   D->nlo = nlo;
+  D->ngs = ngs;
   return MAMG_OK;
+}
+
+// host BSR2 (multi-GPU rank-local level-0 A: owned rows, [owned | ghost]
+// columns) -> half-symmetric ELL-64 when its owned part is symmetric bitwise,
+// else upload_bsr (SELL-64 / lane groups)
+template <class HT>
+int upload_half_or_bsr(HT* h, const HBsr& B, DBsr* D, std::string* err) {
+  const int64_t np = (int64_t)B.ptr.size();
+  if (g_half && g_sell && g_sym && B.nr >= g_sell_min_rows && np == B.nr + 1 && blocks_symmetric(B)) {
+    int rc;
+    TmpPool T;
+    TBsr tb;
+    tb.nr = B.nr; tb.nc = B.nc; tb.nb = B.ptr[B.nr];
+    if ((rc = T.alloc(&tb.ptr, np, err))) return rc;
+    if ((rc = T.alloc(&tb.col, tb.nb, err))) return rc;
+    if ((rc = T.alloc(&tb.val, tb.nb, err))) return rc;
+    HIPCHK(hipMemcpy(tb.ptr, B.ptr.data(), np * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (tb.nb) {
+      HIPCHK(hipMemcpy(tb.col, B.col.data(), tb.nb * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(tb.val, B.val.data(), tb.nb * sizeof(dv4), hipMemcpyHostToDevice));
+    }
+    D->nr = B.nr;
+    D->nc = B.nc;
+    D->nb = tb.nb;
+    D->lanes = pick_lanes_bsr(B.nr, D->nb);
+    D->sym = true;
+    if ((rc = try_half(h, &T, tb, D, err))) return rc;
+    HIPCHK(hipDeviceSynchronize());
+    if (D->half) return MAMG_OK;
+  }
+  return upload_bsr(h, B, D, 0, err, true);
 }
 
 // final apply layout from a raw device BSR (the device-side counterpart of
@@ -1423,7 +1531,8 @@ double index_bytes(const DBsr& M, int64_t ptr_entries) {
 double bsr_bytes(const DBsr& M, int epi) {
   // half-symmetric: upper blocks (28 B with column) + 4-byte mirror slot per
   // lower block + row meta; the mirrors' values are re-reads, not counted
-  double b = M.half ? 28.0 * (M.nb - M.nlo) + 4.0 * M.nlo + 4.0 * M.nr + 16.0 * M.nc + 16.0 * M.nr
+  double b = M.half ? 28.0 * (M.nb - M.nlo) + 4.0 * M.nlo + 4.0 * M.nr + (M.ngs ? 8.0 * (M.nr / SELL_C + 2) : 0.0) +
+                          16.0 * M.nc + 16.0 * M.nr
                     : (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;
   if (epi == EPI_YADD) b += 16.0 * M.nr;
   if (epi == EPI_RESID) b += 16.0 * M.nr;
@@ -1750,29 +1859,35 @@ void launch_post_tag(const Op& o, hipStream_t s) {
   }
 }
 
-template <bool XFM, int U, int TAG>
+template <bool XFM, int U, bool GH, int TAG>
 void launch_half_u(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
-#define HALF_ARGS M.nr, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, o.x, o.xs, o.y, o.b, o.bs, o.W, \
-    o.out, o.os, (TAG == 0 ? g_half_remap : 0)
+#define HALF_ARGS M.nr, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
+    o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap
   switch (o.epi) {
-    case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
-    case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
-    case EPI_RESID: hsell2_kernel<EPI_RESID, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_RESID: hsell2_kernel<EPI_RESID, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_KPOST: break;   // A is never the K operator
-    default: hsell2_kernel<EPI_BJAC, XFM, U, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    default: hsell2_kernel<EPI_BJAC, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
   }
 #undef HALF_ARGS
 }
 
+template <bool XFM, bool GH, int TAG>
+void launch_half_x(const Op& o, hipStream_t s) {
+  if (g_half_u == 8) launch_half_u<XFM, 8, GH, TAG>(o, s); else launch_half_u<XFM, 4, GH, TAG>(o, s);
+}
+
 template <int TAG>
 void launch_half(const Op& o, hipStream_t s) {
+  const bool gh = o.Mb->ngs > 0;
   if (o.xfm) {
-    if (g_half_u == 4) launch_half_u<true, 4, TAG>(o, s); else launch_half_u<true, 8, TAG>(o, s);
+    if (gh) launch_half_x<true, true, TAG>(o, s); else launch_half_x<true, false, TAG>(o, s);
   } else {
-    if (g_half_u == 4) launch_half_u<false, 4, TAG>(o, s); else launch_half_u<false, 8, TAG>(o, s);
+    if (gh) launch_half_x<false, true, TAG>(o, s); else launch_half_x<false, false, TAG>(o, s);
   }
 }
 
@@ -2441,7 +2556,11 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else {
-      if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) return rc;
+      if (l == 0) {
+        if ((rc = upload_half_or_bsr(h.get(), P.A, &D.A, err))) return rc;
+      } else if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) {
+        return rc;
+      }
       if (P.K.nr > 0) {
         if ((rc = upload_bsr(h.get(), P.K, &D.K, g_post_lanes, err))) return rc;
       } else if (P.PA.nr > 0) {

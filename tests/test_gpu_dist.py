@@ -45,17 +45,19 @@ def test_virtual_ranks_match_oracle(lib_built, dim, n, g, P, rep):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('mode', ['unfused', 'sell', 'merged'])
+@pytest.mark.parametrize('mode', ['unfused', 'sell', 'nohalf', 'merged'])
 def test_virtual_ranks_storage_variants(lib_built, monkeypatch, mode):
     """Distributed cycle without post fusion (prolongation, fine halo,
     block-Jacobi sweep), with SELL-64 storage forced onto the rank-local
-    operators (K included), and with the [P | AP] post window instead of
-    K = P - W AP: all equal the single-rank oracle apply."""
+    operators (K included; the level-0 A then half-symmetric with a ghost
+    part), SELL-64 A without the half format, and with the [P | AP] post
+    window instead of K = P - W AP: all equal the single-rank oracle apply."""
     import torch
     import metric_amg_examples_amd as M
     kw = {}
-    if mode == 'sell':
+    if mode in ('sell', 'nohalf'):
         monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+        monkeypatch.setenv('MAMG_HALF', '1' if mode == 'sell' else '0')
     elif mode == 'merged':
         monkeypatch.setenv('MAMG_POST_K', '0')
     else:
@@ -96,3 +98,31 @@ def test_single_rank_rccl(lib_built):
     assert np.linalg.norm(zt.cpu().numpy() - zo) / np.linalg.norm(zo) < 1e-10
     assert ms > 0 and d.apply_bytes > 0
     d.close()
+
+
+@pytest.mark.parametrize('P', [2, 4])
+def test_virtual_ranks_half_bitwise(lib_built, monkeypatch, P):
+    """Rank-local level-0 A in the half-symmetric format (owned part through
+    mirrors, ghost columns in their own part) sums each row in its local
+    column order: bitwise the SELL-64 result, with fewer bytes per apply."""
+    import torch
+    import metric_amg_examples_amd as M
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 16, 1e6)
+    r = mo.seeded_rhs(s.N)
+    out, nbytes = [], []
+    for half in ('1', '0'):
+        monkeypatch.setenv('MAMG_HALF', half)
+        hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                              num_functions=2) for p in range(P)]
+        rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+        zs = [torch.zeros_like(x) for x in rs]
+        M.DistMetricAMG.virtual_apply(hs, rs, zs)
+        torch.cuda.synchronize()
+        out.append([z.cpu().numpy() for z in zs])
+        nbytes.append(sum(hh.apply_bytes for hh in hs))
+        for hh in hs:
+            hh.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    assert nbytes[0] < nbytes[1]
