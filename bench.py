@@ -61,7 +61,8 @@ def main():
                     help='multi-GPU: replicate levels with <= this many nodes')
     ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
-    ap.add_argument('--pcg', action='store_true', help='also run one full PCG solve (N = 1)')
+    ap.add_argument('--pcg', action='store_true',
+                    help='also run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL)')
     ap.add_argument('--setup', choices=('gpu', 'host'), default='gpu',
                     help='N = 1 hierarchy construction: GPU setup (default) or host setup + upload')
     ap.add_argument('--compare-host-setup', action='store_true',
@@ -142,7 +143,8 @@ def main():
         B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
                             comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local)
         t_setup = time.time() - t0
-        setup_info = {'path': 'host setup replicated on every rank + rank-local upload',
+        setup_info = {'path': 'deterministic setup replicated on every rank (GPU setup; host setup if the '
+                              'profile is unsupported) + rank-local upload',
                       'wall_s': round(t_setup, 3)}
         levels = None
         layout = 'bsr2-dist'
@@ -191,6 +193,14 @@ def main():
         solver * r_full
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
                'seconds': round(time.time() - t0, 3)}
+    elif args.pcg:
+        solver = M.DistConjGrad.for_handles(B, stream=stream, tolerance=1e-8, maxiter=500)
+        barrier()
+        t0 = time.perf_counter()
+        solver.solve([r.clone()])
+        barrier()
+        pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
+               'seconds': round(allmax(time.perf_counter() - t0), 3)}
 
     # ---- CPU baseline: oracle C restatement on the same hierarchy, host cores
     cpu = None

@@ -188,6 +188,10 @@ int mamg_dist_range(const mamg_dhandle* h, int64_t* o0, int64_t* o1, int64_t* nv
 int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes);
 int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r_local, double* d_z_local,
                            void* stream);
+/* y = A x on the rank's rows (the PCG operator; x, y local field-major
+ * slices): forward halo of x, then the rank-local A.  Replaces the A * d
+ * product inside cbc.block ConjGrad (src/bidomain_3d.py:149) on N GPUs. */
+int mamg_dist_spmv_device(mamg_dhandle* h, const double* d_x_local, double* d_y_local, void* stream);
 int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int reps, int mode,
                          double* ms_per_apply, double* kernel_ms, double* class_bytes,
                          void* stream);
@@ -195,6 +199,7 @@ int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int re
  * apply all n ranks in lockstep, exchanges as device copies. */
 int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double** d_z,
                             void* stream);
+int mamg_dist_virtual_spmv(mamg_dhandle** hs, int n, const double** d_x, double** d_y, void* stream);
 void mamg_dist_destroy(mamg_dhandle* h);
 
 /* ---- device hierarchy ------------------------------------------------- */

@@ -10,7 +10,7 @@ File boundary (src/utils.py:304-333, src/run_solver_3d1d.py): fileio, drivers.
 """
 from . import _lib, fileio, parameters, precond, problems
 from .amg import DistMetricAMG, DistPlan, HostHierarchy, MetricAMG, metricAMG
-from .krylov import ConjGrad, lanczos_eigenvalues
+from .krylov import ConjGrad, DistConjGrad, lanczos_eigenvalues
 
-__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'ConjGrad',
+__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'ConjGrad', 'DistConjGrad',
            'lanczos_eigenvalues', 'parameters', 'problems', 'precond', 'fileio', '_lib']

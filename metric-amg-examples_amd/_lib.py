@@ -84,6 +84,8 @@ SIGNATURES = {
     'mamg_dist_apply_device': (C.c_int, [VP, VP, VP, VP]),
     'mamg_dist_time_apply': (C.c_int, [VP, VP, VP, C.c_int, C.c_int, P_F64, P_F64, P_F64, VP]),
     'mamg_dist_virtual_apply': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
+    'mamg_dist_spmv_device': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_dist_virtual_spmv': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
     'mamg_dist_destroy': (None, [VP]),
     'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                              C.POINTER(VP)]),

@@ -499,6 +499,21 @@ class DistMetricAMG:
                                                 int(mode), C.byref(ms), kms, cb, _stream_ptr(stream)))
         return ms.value, list(kms), list(cb)
 
+    def spmv_device(self, x, y, stream=None):
+        """y = A x on this rank's rows (local field-major slices; one halo
+        exchange of x)."""
+        _lib.check(self._L.mamg_dist_spmv_device(self._h, _device_ptr(x), _device_ptr(y),
+                                                 _stream_ptr(stream)))
+        return y
+
+    @staticmethod
+    def virtual_spmv(handles, xs, ys, stream=None):
+        n = len(handles)
+        H = (C.c_void_p * n)(*[h._h.value for h in handles])
+        X = (C.c_void_p * n)(*[_device_ptr(x).value for x in xs])
+        Y = (C.c_void_p * n)(*[_device_ptr(y).value for y in ys])
+        _lib.check(_lib.lib().mamg_dist_virtual_spmv(H, n, X, Y, _stream_ptr(stream)))
+
     @staticmethod
     def virtual_apply(handles, rs, zs, stream=None):
         n = len(handles)

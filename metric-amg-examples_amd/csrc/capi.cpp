@@ -337,6 +337,24 @@ int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r, double* d_z, void
   DEV_CALL(mamg::dist_apply(h->d, d_r, d_z, stream, &err))
 }
 
+int mamg_dist_spmv_device(mamg_dhandle* h, const double* d_x, double* d_y, void* stream) {
+  DEV_CALL(mamg::dist_spmv(h->d, d_x, d_y, stream, &err))
+}
+
+int mamg_dist_virtual_spmv(mamg_dhandle** hs, int n, const double** d_x, double** d_y, void* stream) {
+  GUARD_BEGIN
+  if (!hs || n < 1 || !d_x || !d_y) { set_error("null argument"); return MAMG_ERR_ARG; }
+  std::vector<mamg::DistHandle*> H(n);
+  std::vector<const double*> X(d_x, d_x + n);
+  std::vector<double*> Y(d_y, d_y + n);
+  for (int i = 0; i < n; ++i) H[i] = hs[i]->d;
+  std::string err;
+  int rc = mamg::dist_virtual_spmv(H, X, Y, stream, &err);
+  if (rc) set_error(err);
+  return rc;
+  GUARD_END
+}
+
 int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int reps, int mode,
                          double* ms, double* kernel_ms, double* class_bytes, void* stream) {
   DEV_CALL(mamg::dist_time_apply(h->d, d_r, d_z, reps, mode, ms, kernel_ms, class_bytes, stream, &err))

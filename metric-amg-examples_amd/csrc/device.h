@@ -42,6 +42,9 @@ void dist_destroy(DistHandle* h);
 void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
 double dist_apply_bytes(const DistHandle* h);
 int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
+int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::string* err);
+int dist_virtual_spmv(const std::vector<DistHandle*>& hs, const std::vector<const double*>& x,
+                      const std::vector<double*>& y, void* stream, std::string* err);
 int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
                     double* kernel_ms, double* class_bytes, void* stream, std::string* err);
 int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,

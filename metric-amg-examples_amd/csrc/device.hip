@@ -596,6 +596,13 @@ __global__ __launch_bounds__(256) void cg_undo_kernel(int64_t n, double alpha,
   if (i < n) x[i] = x[i] - alpha * d[i];
 }
 
+// field-major [v0; v1] (stride bs) -> node-interleaved pairs
+__global__ __launch_bounds__(256) void interleave2_kernel(int64_t n, const double* __restrict__ in, int64_t bs,
+                                                          double* __restrict__ out) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < n) reinterpret_cast<double2*>(out)[I] = double2{in[I], in[bs + I]};
+}
+
 inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 
 // tuning knobs, read at upload (bench/variants.py):
@@ -743,7 +750,7 @@ struct DLevel {
          *c = nullptr, *e = nullptr;
 };
 
-enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6 };
+enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -1928,6 +1935,9 @@ void launch(const Op& o, hipStream_t s) {
     case OP_GEMV:
       if (o.n) gemv_kernel<<<(unsigned)((o.n + 3) / 4), 256, 0, s>>>(o.n, o.w, o.x, o.out);
       break;
+    case OP_ILV:
+      if (o.n) interleave2_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.b, o.bs, o.out);
+      break;
   }
 }
 
@@ -2336,6 +2346,7 @@ struct DDLevel {
   dv4* W = nullptr;
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
+  double* spx = nullptr;   // level 0: [owned | ghost] operand of the standalone SpMV
   int64_t* send_idx = nullptr;
   double *sendbuf = nullptr, *recvbuf = nullptr;
   std::vector<int64_t> send_off, ghost_off;
@@ -2460,6 +2471,11 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     launch(d.op, s);
     return MAMG_OK;
   }
+  if (h->nranks == 1) return MAMG_OK;   // no peers: halos empty, sums over one rank
+  if (!h->comm) {
+    *err = "virtual rank handle (no communicator): use mamg_dist_virtual_apply / _spmv";
+    return MAMG_ERR_ARG;
+  }
   if (d.dk == D_ALLREDUCE) {
     NCCLCHK(ncclAllReduce(d.buf, d.buf, d.count, ncclDouble, ncclSum, h->comm, s));
     return MAMG_OK;
@@ -2502,6 +2518,19 @@ void dapply_ops(const DistHandle* h, const double* r, double* z, std::vector<DOp
   ops->clear();
   const int64_t nloc = h->L[0].nloc;
   dcycle_ops(h, 0, r, nloc, z, nloc, ops);
+}
+
+// y = A x on the rank's rows (field-major local slices): interleave x into
+// the [owned | ghost] buffer, forward halo, SpMV with A_loc (PCG operator)
+void dspmv_ops(const DistHandle* h, const double* x, double* y, std::vector<DOp>* ops) {
+  ops->clear();
+  const DDLevel& D = h->L[0];
+  Op o;
+  o.kind = OP_ILV; o.cls = C_MISC; o.n = D.nloc; o.b = x; o.bs = D.nloc; o.out = D.spx;
+  o.bytes = 32.0 * D.nloc;
+  ops->push_back(wrap(o));
+  if (!D.replicated) ops->push_back(halo_op(0, D.spx, D, C_COMM));
+  ops->push_back(wrap(bsr_op(D.A, EPI_Y, C_L0_RESID, 0, D.spx, 0, nullptr, nullptr, 0, nullptr, y, D.nloc)));
 }
 
 }  // namespace
@@ -2577,6 +2606,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     if ((rc = ddalloc(h.get(), &D.x, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.t, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
+    if (l == 0 && !D.coarsest && (rc = ddalloc(h.get(), &D.spx, 2 * full, err))) return rc;
     const int64_t ns = P.send_idx.size();
     if (ns) {
       if ((rc = ddalloc(h.get(), &D.send_idx, ns, err))) return rc;
@@ -2613,6 +2643,19 @@ int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std:
   HIPCHK(hipSetDevice(h->device));
   std::vector<DOp> ops;
   dapply_ops(h, d_r, d_z, &ops);
+  for (const DOp& d : ops) {
+    int rc = run_dop(h, d, (hipStream_t)stream, err);
+    if (rc) return rc;
+  }
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  if (h->L.empty() || h->L[0].coarsest) { *err = "single-level hierarchy: no distributed operator"; return MAMG_ERR_ARG; }
+  std::vector<DOp> ops;
+  dspmv_ops(h, d_x, d_y, &ops);
   for (const DOp& d : ops) {
     int rc = run_dop(h, d, (hipStream_t)stream, err);
     if (rc) return rc;
@@ -2685,13 +2728,10 @@ __global__ __launch_bounds__(256) void vsum_kernel(int64_t n, const double* __re
   if (i < n) acc[i] = acc[i] + a[i];
 }
 
-int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
-                       const std::vector<double*>& z, void* stream, std::string* err) {
+// P ranks' op lists in lockstep on one stream
+int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vector<DOp>>& ops, hipStream_t s,
+                std::string* err) {
   const int P = (int)hs.size();
-  hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipSetDevice(hs[0]->device));
-  std::vector<std::vector<DOp>> ops(P);
-  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
   for (int p = 1; p < P; ++p)
     if (ops[p].size() != ops[0].size()) { *err = "rank schedules differ"; return MAMG_ERR_SETUP; }
   for (size_t k = 0; k < ops[0].size(); ++k) {
@@ -2753,6 +2793,27 @@ int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<con
   }
   HIPCHK(hipGetLastError());
   return MAMG_OK;
+}
+
+int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
+                       const std::vector<double*>& z, void* stream, std::string* err) {
+  const int P = (int)hs.size();
+  HIPCHK(hipSetDevice(hs[0]->device));
+  std::vector<std::vector<DOp>> ops(P);
+  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
+  return virtual_run(hs, ops, (hipStream_t)stream, err);
+}
+
+int dist_virtual_spmv(const std::vector<DistHandle*>& hs, const std::vector<const double*>& x,
+                      const std::vector<double*>& y, void* stream, std::string* err) {
+  const int P = (int)hs.size();
+  HIPCHK(hipSetDevice(hs[0]->device));
+  std::vector<std::vector<DOp>> ops(P);
+  for (int p = 0; p < P; ++p) {
+    if (hs[p]->L.empty() || hs[p]->L[0].coarsest) { *err = "single-level hierarchy"; return MAMG_ERR_ARG; }
+    dspmv_ops(hs[p], x[p], y[p], &ops[p]);
+  }
+  return virtual_run(hs, ops, (hipStream_t)stream, err);
 }
 
 }  // namespace mamg

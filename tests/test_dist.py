@@ -141,3 +141,83 @@ def test_dist_cycle_gloo_world2(lib_built):
         z[o0:o1] = zl[:nloc]
         z[s.nv + o0:s.nv + o1] = zl[nloc:]
     assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-13
+
+
+def _gloo_pcg_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, 'oracle')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import dist_ref
+        import mamg_oracle
+        import metric_amg_examples_amd as M
+        s = M.problems.bidomain(3, 16, 1e4)
+        A = s.scipy().tocsr()
+        H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2)
+        plan = M.DistPlan(H, rank, world, 100)
+        lv = [plan.level(l) for l in range(plan.num_levels)]
+        Ainv = dist_ref.nodemajor_Ainv(H.level(H.num_levels - 1)['Ainv'])
+        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm())
+        o0, o1, nv = lv[0]['o0'], lv[0]['o1'], s.nv
+        nloc = o1 - o0
+        rows = np.r_[o0:o1, nv + o0:nv + o1]
+        Aloc = A[rows]
+
+        def spmv(xs, ys):        # gather x (sum of zero-padded slices), multiply owned rows
+            full = torch.zeros(s.N, dtype=torch.float64)
+            full[o0:o1] = xs[0][:nloc]
+            full[nv + o0:nv + o1] = xs[0][nloc:]
+            dist.all_reduce(full)
+            ys[0].copy_(torch.from_numpy(Aloc @ full.numpy()))
+
+        def precond(rs, zs):
+            zs[0].copy_(torch.from_numpy(dc.apply_local(rs[0].numpy())))
+
+        def allreduce(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t.item())
+
+        b = torch.from_numpy(dist_ref.local_slice(mamg_oracle.seeded_rhs(s.N), nv, o0, o1))
+        cg = M.DistConjGrad(spmv, precond, allreduce, tolerance=1e-8, maxiter=500)
+        x = cg.solve([b])[0].numpy()
+        q.put((rank, o0, o1, x, cg.residuals))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_pcg_gloo_world2(lib_built):
+    """DistConjGrad over two gloo ranks (rank-local operator rows, the
+    distributed cycle as preconditioner, dots all-reduced): the iteration
+    count and residual history of the single-process oracle PCG."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_pcg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e4)
+    A = s.scipy()
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    b = mo.seeded_rhs(s.N)
+    ref = mo.pcg(A, h.apply, b, 1e-8, 500)
+    x = np.zeros(s.N)
+    for rank, o0, o1, xl, resid in res:
+        assert len(resid) == len(ref.residuals)
+        assert np.allclose(resid, ref.residuals, rtol=1e-8, atol=0)
+        nloc = o1 - o0
+        x[o0:o1] = xl[:nloc]
+        x[s.nv + o0:s.nv + o1] = xl[nloc:]
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-8

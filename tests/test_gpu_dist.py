@@ -126,3 +126,36 @@ def test_virtual_ranks_half_bitwise(lib_built, monkeypatch, P):
     for a, b in zip(out[0], out[1]):
         assert np.array_equal(a, b)
     assert nbytes[0] < nbytes[1]
+
+
+@pytest.mark.parametrize('P', [1, 3])
+def test_dist_pcg_virtual_ranks(lib_built, P):
+    """DistConjGrad on P virtual ranks (rank-local SpMV with halo, distributed
+    V-cycle, dots summed over ranks): iteration count and residual history of
+    the oracle PCG; the rank SpMV equals the global SpMV's rows."""
+    import torch
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e4)
+    A = s.scipy()
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    b = mo.seeded_rhs(s.N)
+    ref = mo.pcg(A, h.apply, b, 1e-8, 500)
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                          num_functions=2) for p in range(P)]
+    xs = [torch.as_tensor(hh.local_slice(b)).cuda() for hh in hs]
+    ys = [torch.zeros_like(x) for x in xs]
+    if P > 1:
+        M.DistMetricAMG.virtual_spmv(hs, xs, ys)
+    else:
+        hs[0].spmv_device(xs[0], ys[0])
+    torch.cuda.synchronize()
+    yo = A @ b
+    for hh, y in zip(hs, ys):
+        assert np.allclose(y.cpu().numpy(), hh.local_slice(yo), rtol=1e-13, atol=1e-13 * np.abs(yo).max())
+    cg = M.DistConjGrad.for_handles(hs if P > 1 else hs[0], tolerance=1e-8, maxiter=500)
+    x = _gather(s, hs, cg.solve([torch.as_tensor(hh.local_slice(b)).cuda() for hh in hs]))
+    assert len(cg.residuals) == len(ref.residuals)
+    assert np.allclose(cg.residuals, ref.residuals, rtol=1e-6, atol=0)
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-6
+    for hh in hs:
+        hh.close()
