@@ -346,12 +346,12 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 // ---------------------------------------------------------------------------
 template <int EPI, bool XFM, int U, bool GH, int TAG>
 __global__ __launch_bounds__(256) void hsell2_kernel(
-    int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
+    int64_t row0, int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
     const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
     const int64_t* __restrict__ gsoff, const int32_t* __restrict__ gcol, const double* __restrict__ gval,
     int64_t ngs, const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
     int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
-  const int64_t node = row_block(remap) * 256 + threadIdx.x;
+  const int64_t node = row0 + row_block(remap) * 256 + threadIdx.x;   // rows [row0, nr)
   if (node >= nr) return;
   const double* offd = uval + 2 * nbs;
   const int m = meta[node];
@@ -776,6 +776,7 @@ struct Op {
   int64_t xs = 0, bs = 0, os = 0;   // BSR2 field strides (0 = node-major)
   bool xfm = false;
   int remap = 0;                    // XCD-contiguous row order (restriction ops)
+  int64_t r0 = 0, r1 = -1;          // row range [r0, r1) (half-symmetric ops; r1 < 0: all rows)
   double bytes = 0.0;
 };
 
@@ -1869,9 +1870,10 @@ void launch_post_tag(const Op& o, hipStream_t s) {
 template <bool XFM, int U, bool GH, int TAG>
 void launch_half_u(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
-  const unsigned g = nblocks(M.nr);
-  if (g == 0) return;
-#define HALF_ARGS M.nr, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
+  const int64_t r0 = o.r1 < 0 ? 0 : o.r0, r1 = o.r1 < 0 ? M.nr : o.r1;
+  const unsigned g = nblocks(r1 - r0);
+  if (r1 <= r0) return;
+#define HALF_ARGS r0, r1, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
     o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap
   switch (o.epi) {
     case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
@@ -2347,12 +2349,13 @@ struct DDLevel {
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
   double* spx = nullptr;   // level 0: [owned | ghost] operand of the standalone SpMV
+  int64_t ib0 = 0, ib1 = 0;  // longest run of A_loc rows without ghost columns
   int64_t* send_idx = nullptr;
   double *sendbuf = nullptr, *recvbuf = nullptr;
   std::vector<int64_t> send_off, ghost_off;
 };
 
-enum DKind { D_OP = 0, D_HALO = 1, D_REVERSE = 2, D_ALLREDUCE = 3 };
+enum DKind { D_OP = 0, D_HALO = 1, D_REVERSE = 2, D_ALLREDUCE = 3, D_OVERLAP = 4 };
 
 struct DOp {
   int dk = D_OP;
@@ -2374,7 +2377,13 @@ struct DistHandle {
   std::vector<void*> allocs;
   double apply_bytes = 0.0;
   int64_t nv0 = 0, o0 = 0, o1 = 0;
+  bool overlap = true;                 // MAMG_OVERLAP: interior rows during the forward halo
+  hipStream_t side = nullptr;          // stream of the interior rows
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   ~DistHandle() {
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (side) (void)hipStreamDestroy(side);
     for (void* a : allocs) (void)hipFree(a);
     if (comm) (void)ncclCommDestroy(comm);
   }
@@ -2409,6 +2418,36 @@ DOp halo_op(int level, double* x, const DDLevel& D, int cls) {
   return d;
 }
 
+// forward halo of x followed by the SpMV `op` on A_loc: with the
+// half-symmetric A, the ghost-free row run [ib0, ib1) (maybe empty) runs on the
+// side stream while the halo is in flight (one D_OVERLAP), the rest after it.
+// Every row is computed by the same kernel code either way (same bits).
+void halo_residual(const DistHandle* h, int l, double* x, const Op& op, std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[l];
+  if (!(h->overlap && D.A.half)) {
+    ops->push_back(halo_op(l, x, D, C_COMM));
+    ops->push_back(wrap(op));
+    return;
+  }
+  const double f = (double)(D.ib1 - D.ib0) / (double)std::max<int64_t>(D.nloc, 1);
+  DOp ov = halo_op(l, x, D, op.cls);   // timed and counted with the SpMV's class
+  ov.dk = D_OVERLAP;
+  ov.op = op;
+  ov.op.r0 = D.ib0;
+  ov.op.r1 = D.ib1;
+  ov.op.bytes = op.bytes * f;
+  ov.bytes += ov.op.bytes;
+  ops->push_back(ov);
+  const int64_t lo[2] = {0, D.ib1}, hi[2] = {D.ib0, D.nloc};
+  for (int k = 0; k < 2; ++k) {   // both always emitted (possibly empty): one schedule on every rank
+    Op b = op;
+    b.r0 = lo[k];
+    b.r1 = hi[k];
+    b.bytes = op.bytes * (double)std::max<int64_t>(hi[k] - lo[k], 0) / (double)std::max<int64_t>(D.nloc, 1);
+    ops->push_back(wrap(b));
+  }
+}
+
 // multi-GPU cycle from x = 0 (V-cycle, nu1 = nu2 = 1): see dist.cpp / dist_ref.py
 void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
                 std::vector<DOp>* ops) {
@@ -2430,9 +2469,14 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
     o.out = X; o.bytes = 64.0 * D.nloc;
     ops->push_back(wrap(o));
   }
-  if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
-  ops->push_back(wrap(bsr_op(D.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs,
-                             nullptr, D.r, 0)));
+  {
+    const Op res = bsr_op(D.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs, nullptr, D.r, 0);
+    if (D.replicated) {
+      ops->push_back(wrap(res));
+    } else {
+      halo_residual(h, l, X, res, ops);
+    }
+  }
   ops->push_back(wrap(bsr_op(D.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, D.r, 0, nullptr, nullptr, 0,
                              nullptr, C.b, 0)));
   ops->back().op.remap = 1;
@@ -2471,7 +2515,10 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     launch(d.op, s);
     return MAMG_OK;
   }
-  if (h->nranks == 1) return MAMG_OK;   // no peers: halos empty, sums over one rank
+  if (h->nranks == 1) {                 // no peers: halos empty, sums over one rank
+    if (d.dk == D_OVERLAP) launch(d.op, s);
+    return MAMG_OK;
+  }
   if (!h->comm) {
     *err = "virtual rank handle (no communicator): use mamg_dist_virtual_apply / _spmv";
     return MAMG_ERR_ARG;
@@ -2482,6 +2529,17 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
   }
   const DDLevel& D = h->L[d.level];
   const int64_t ns = D.send_off.back();
+  if (d.dk == D_OVERLAP) {   // interior rows on the side stream, halo on s, join
+    HIPCHK(hipEventRecord(h->ev_in, s));
+    HIPCHK(hipStreamWaitEvent(h->side, h->ev_in, 0));
+    launch(d.op, h->side);
+    HIPCHK(hipEventRecord(h->ev_out, h->side));
+    DOp hd = d;
+    hd.dk = D_HALO;
+    int rc = run_dop(h, hd, s, err);
+    HIPCHK(hipStreamWaitEvent(s, h->ev_out, 0));
+    return rc;
+  }
   if (d.dk == D_HALO) {
     if (ns) pack2_kernel<<<nblocks(ns), 256, 0, s>>>(ns, D.send_idx, d.buf, D.sendbuf);
     NCCLCHK(ncclGroupStart());
@@ -2529,8 +2587,8 @@ void dspmv_ops(const DistHandle* h, const double* x, double* y, std::vector<DOp>
   o.kind = OP_ILV; o.cls = C_MISC; o.n = D.nloc; o.b = x; o.bs = D.nloc; o.out = D.spx;
   o.bytes = 32.0 * D.nloc;
   ops->push_back(wrap(o));
-  if (!D.replicated) ops->push_back(halo_op(0, D.spx, D, C_COMM));
-  ops->push_back(wrap(bsr_op(D.A, EPI_Y, C_L0_RESID, 0, D.spx, 0, nullptr, nullptr, 0, nullptr, y, D.nloc)));
+  const Op mv = bsr_op(D.A, EPI_Y, C_L0_RESID, 0, D.spx, 0, nullptr, nullptr, 0, nullptr, y, D.nloc);
+  if (D.replicated) ops->push_back(wrap(mv)); else halo_residual(h, 0, D.spx, mv, ops);
 }
 
 }  // namespace
@@ -2563,6 +2621,13 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     std::memcpy(&uid, comm_id, sizeof(uid));
     NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
   }
+  {
+    const char* e = std::getenv("MAMG_OVERLAP");
+    h->overlap = e ? std::atoi(e) != 0 : true;
+  }
+  HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
   const int nl = (int)plan.levels.size();
   h->L.resize(nl);
   for (int l = 0; l < nl; ++l) {
@@ -2585,6 +2650,20 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else {
+      if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
+        int64_t best0 = 0, best1 = 0, run0 = 0;
+        for (int64_t I = 0; I <= P.A.nr; ++I) {
+          bool ghost = I == P.A.nr;
+          for (int64_t k = I < P.A.nr ? P.A.ptr[I] : 0; !ghost && k < P.A.ptr[I + 1]; ++k)
+            ghost = P.A.col[k] >= P.A.nr;
+          if (ghost) {
+            if (I - run0 > best1 - best0) { best0 = run0; best1 = I; }
+            run0 = I + 1;
+          }
+        }
+        D.ib0 = best0;
+        D.ib1 = best1;
+      }
       if (l == 0) {
         if ((rc = upload_half_or_bsr(h.get(), P.A, &D.A, err))) return rc;
       } else if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) {
@@ -2738,7 +2817,9 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
     const int dk = ops[0][k].dk;
     if (dk == D_OP) {
       for (int p = 0; p < P; ++p) launch(ops[p][k].op, s);
-    } else if (dk == D_HALO) {
+    } else if (dk == D_HALO || dk == D_OVERLAP) {
+      if (dk == D_OVERLAP)
+        for (int p = 0; p < P; ++p) launch(ops[p][k].op, s);
       for (int p = 0; p < P; ++p) {
         const DDLevel& D = hs[p]->L[ops[p][k].level];
         const int64_t ns = D.send_off.back();

@@ -159,3 +159,31 @@ def test_dist_pcg_virtual_ranks(lib_built, P):
     assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-6
     for hh in hs:
         hh.close()
+
+
+def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch):
+    """Residual split into the ghost-free row window (run while the halo is
+    in flight) and the boundary rows (after it): bitwise the unsplit apply,
+    for the cycle and the rank SpMV."""
+    import torch
+    import metric_amg_examples_amd as M
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 16, 1e6)
+    r = mo.seeded_rhs(s.N)
+    P = 3
+    out = []
+    for ov in ('1', '0'):
+        monkeypatch.setenv('MAMG_OVERLAP', ov)
+        hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                              num_functions=2) for p in range(P)]
+        rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+        zs = [torch.zeros_like(x) for x in rs]
+        ys = [torch.zeros_like(x) for x in rs]
+        M.DistMetricAMG.virtual_apply(hs, rs, zs)
+        M.DistMetricAMG.virtual_spmv(hs, rs, ys)
+        torch.cuda.synchronize()
+        out.append([z.cpu().numpy() for z in zs] + [y.cpu().numpy() for y in ys])
+        for hh in hs:
+            hh.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
