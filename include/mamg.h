@@ -245,10 +245,12 @@ int mamg_device_layout(const mamg_handle* h);
  * first post sweep), MAMG_FMT_POST_K (... through one stored operator
  * K = P - W (A P): z = x1 + W r1 + K e; else through [P | AP]),
  * MAMG_FMT_POST_SELL (K stored sliced-ELL), MAMG_FMT_HALF (A stored as its
- * upper half, ELL-64, lower blocks read through their mirrors).
+ * upper half, ELL-64, lower blocks read through their mirrors), MAMG_FMT_BANDS
+ * (the half-symmetric kernel walks the rows in plane bands per XCD; order
+ * only, results are bitwise those of row order).
  * Returns flags >= 0, or < 0. */
 enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_POST_K = 8,
-       MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32 };
+       MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32, MAMG_FMT_BANDS = 64 };
 int mamg_level_format(const mamg_handle* h, int level);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */

@@ -217,7 +217,8 @@ class MetricAMG:
         f = self._L.mamg_level_format(self._h, int(level))
         _lib.check(min(f, 0))
         return {'sell': bool(f & 1), 'sym': bool(f & 2), 'post_fused': bool(f & 4),
-                'post_k': bool(f & 8), 'post_sell': bool(f & 16), 'half': bool(f & 32)}
+                'post_k': bool(f & 8), 'post_sell': bool(f & 16), 'half': bool(f & 32),
+                'bands': bool(f & 64)}
 
     @property
     def apply_bytes(self) -> float:

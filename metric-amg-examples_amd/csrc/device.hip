@@ -350,8 +350,10 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
     const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
     const int64_t* __restrict__ gsoff, const int32_t* __restrict__ gcol, const double* __restrict__ gval,
     int64_t ngs, const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
-    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
-  const int64_t node = row0 + row_block(remap) * 256 + threadIdx.x;   // rows [row0, nr)
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap,
+    const int32_t* __restrict__ sched) {
+  const int64_t blk0 = sched ? (int64_t)sched[blockIdx.x] : row_block(remap);
+  const int64_t node = row0 + blk0 * 256 + threadIdx.x;   // rows [row0, nr)
   if (node >= nr) return;
   const double* offd = uval + 2 * nbs;
   const int m = meta[node];
@@ -623,11 +625,14 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_HALF_U     blocks per chunk of the half-symmetric kernel (4 default, 8)
 //   MAMG_HALF_REMAP XCD-contiguous row order for the half-symmetric kernel (default 1:
 //                   the mirror re-reads then hit the XCD's own L2)
+//   MAMG_HALF_BANDS band schedule of the half-symmetric kernel: sub-bands per XCD
+//                   (default 1; 0 = off, row order by MAMG_HALF_REMAP)
 int g_remap = 1;
 int g_sell_remap = 0;
 int g_half = 1;
 int g_half_u = 4;
 int g_half_remap = 1;
+int g_half_bands = 1;
 int g_post_lanes = 0;
 int g_sym = 1;
 int g_sell = 1;
@@ -667,6 +672,8 @@ void read_knobs() {
   if (g_half_u != 4 && g_half_u != 8) g_half_u = 4;
   su = std::getenv("MAMG_HALF_REMAP");
   g_half_remap = su ? std::atoi(su) != 0 : 1;
+  su = std::getenv("MAMG_HALF_BANDS");
+  g_half_bands = su ? std::atoi(su) : 1;
   su = std::getenv("MAMG_SELL_REMAP");
   g_sell_remap = su ? std::atoi(su) != 0 : 0;
   const char* e = std::getenv("MAMG_XCD_REMAP");
@@ -734,6 +741,10 @@ struct DBsr {              // 2x2 blocks, node-major
   int64_t* gsoff = nullptr;
   int32_t* gcol = nullptr;
   double* gval = nullptr;
+  // band schedule of the half-symmetric kernel (full-range launches):
+  // workgroup b processes 256-row block sched[b] (nullptr: row_block order)
+  int32_t* sched = nullptr;
+  int64_t nsched = 0;
 };
 
 struct DLevel {
@@ -1283,6 +1294,73 @@ int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* 
   return MAMG_OK;
 }
 
+// Band schedule for the half-symmetric kernel.  A lower block (I, J < I) is
+// re-read from row J's upper part; with the rows of a structured 3-D mesh in
+// lexicographic order the farthest mirror sits one plane (stride S rows)
+// back.  Row order alone puts a whole plane (~16 MB at n = 256) between the
+// two reads, more than an XCD's 4 MB L2.  The schedule cuts each plane of
+// 256-row blocks into 8 x nsub bands, gives XCD x (workgroups b = x mod 8)
+// the bands x nsub .. x nsub + nsub - 1 and walks each band plane by plane,
+// so the mirror was streamed one band (S / (8 nsub) rows) earlier on the same
+// XCD.  S = the median, over sampled rows, of the distance to the row's first
+// (smallest) column.  The schedule only permutes which workgroup computes
+// which rows: every row is still summed by one lane in its own order, so the
+// result is bitwise that of any other order.  Unstructured or narrow-band
+// matrices (< 4 blocks per band) keep the row_block order.
+template <class HT>
+int build_band_sched(HT* h, const TBsr& B, DBsr* D, std::string* err) {
+  const int nsub = g_half_bands;
+  const int64_t nr = B.nr, G = (nr + 255) / 256;
+  if (nsub <= 0 || G < 64) return MAMG_OK;
+  const int ns = 257;
+  std::vector<int64_t> off;
+  for (int i = 0; i < ns; ++i) {
+    const int64_t I = nr / 4 + (nr / 2) * i / ns;
+    int64_t p = 0;
+    int32_t c = 0;
+    HIPCHK(hipMemcpy(&p, B.ptr + I, sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&c, B.col + p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (c < I) off.push_back(I - c);
+  }
+  if (off.size() < ns / 2) return MAMG_OK;
+  std::nth_element(off.begin(), off.begin() + off.size() / 2, off.end());
+  const int64_t S = off[off.size() / 2];
+  const int64_t Pb = std::max<int64_t>(1, (S + 128) / 256), nb = 8 * (int64_t)nsub;
+  if (Pb < 4 * nb) return MAMG_OK;
+  std::vector<std::vector<int32_t>> L(8);
+  for (int x = 0; x < 8; ++x)
+    for (int sb = 0; sb < nsub; ++sb) {
+      const int64_t band = (int64_t)x * nsub + sb, c0 = band * Pb / nb, c1 = (band + 1) * Pb / nb;
+      for (int64_t p0 = 0; p0 < G; p0 += Pb)
+        for (int64_t c = c0; c < c1 && p0 + c < G; ++c) L[x].push_back((int32_t)(p0 + c));
+    }
+  // balance to the round-robin dispatch: XCD x runs ceil / floor(G / 8)
+  // workgroups; surplus tails move to the short lists
+  std::vector<int32_t> spill;
+  for (int x = 0; x < 8; ++x) {
+    const size_t want = (size_t)(G / 8 + (x < G % 8 ? 1 : 0));
+    while (L[x].size() > want) { spill.push_back(L[x].back()); L[x].pop_back(); }
+  }
+  for (int x = 0; x < 8; ++x) {
+    const size_t want = (size_t)(G / 8 + (x < G % 8 ? 1 : 0));
+    while (L[x].size() < want) { L[x].push_back(spill.back()); spill.pop_back(); }
+  }
+  std::vector<int32_t> sched(G);
+  std::vector<char> seen(G, 0);
+  for (int64_t b = 0; b < G; ++b) {
+    sched[b] = L[b % 8][b / 8];
+    if (sched[b] < 0 || sched[b] >= G || seen[sched[b]]++) {
+      *err = "band schedule is not a permutation of the row blocks";
+      return MAMG_ERR_SETUP;
+    }
+  }
+  int rc;
+  if ((rc = dalloc(h, &D->sched, G, err))) return rc;
+  HIPCHK(hipMemcpy(D->sched, sched.data(), G * sizeof(int32_t), hipMemcpyHostToDevice));
+  D->nsched = G;
+  return MAMG_OK;
+}
+
 // half-symmetric ELL-64 for a symmetric-block A whose owned part (columns
 // < nr) is symmetric bitwise; columns >= nr (ghosts of a rank-local A) go to
 // the ghost part (hsell2_kernel).  Returns MAMG_OK with D->half set, or
@@ -1350,7 +1428,7 @@ int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
   D->nbs = su;
   D->nlo = nlo;
   D->ngs = ngs;
-  return MAMG_OK;
+  return build_band_sched(h, B, D, err);
 }
 
 // host BSR2 (multi-GPU rank-local level-0 A: owned rows, [owned | ghost]
@@ -1874,7 +1952,8 @@ void launch_half_u(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(r1 - r0);
   if (r1 <= r0) return;
 #define HALF_ARGS r0, r1, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
-    o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap
+    o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap, \
+    (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched : nullptr
   switch (o.epi) {
     case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
@@ -2149,7 +2228,7 @@ int dev_level_format(const DeviceHandle* h, int level) {
   const DLevel& L = h->L[level];
   return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) | (L.Ab.half ? MAMG_FMT_HALF : 0) |
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
-         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0);
+         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 ? MAMG_FMT_BANDS : 0);
 }
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {

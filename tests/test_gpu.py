@@ -256,6 +256,30 @@ def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw, env):
     assert rel(outs[0], h.apply(r)) < APPLY_TOL
 
 
+@pytest.mark.parametrize('bands', ['1', '2'])
+def test_half_band_schedule_bitwise(lib_built, monkeypatch, bands):
+    """The band schedule of the half-symmetric kernel (rows walked plane band
+    by plane band on each XCD) only reorders workgroups: at 3-D n=128 (where
+    it engages) the apply and the device PCG are bitwise those of row order."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 128, 1e6)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    outs, its = [], []
+    for b in (bands, '0'):
+        monkeypatch.setenv('MAMG_HALF_BANDS', b)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        f = B.level_format(0)
+        assert f['half'] and f['bands'] == (b != '0')
+        outs.append(B * r)
+        solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        solver * r
+        its.append(solver.residuals)
+        B.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert its[0] == its[1]
+
+
 def test_half_symmetric_rejects_nonsymmetric(lib_built, monkeypatch):
     """A_0 whose 2x2 blocks are symmetric but A_IJ != A_JI in one ulp: the
     mirror check rejects the half format (full SELL-64 is used) and the apply
