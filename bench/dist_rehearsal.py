@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Full-size rehearsal of the N-rank path on one GPU (virtual ranks).
+
+    python bench/dist_rehearsal.py [--nrefs 6] [--ranks 8]
+
+Builds the P rank-local handles of bidomain_3d (each runs the same
+deterministic setup as a real rank would, then keeps its rows), reports per
+rank the setup wall time, device bytes held and the process's peak host RSS,
+then runs one virtual distributed apply (device copies stand in for RCCL,
+same counts/offsets) and compares it with the single-GPU apply.  This is what
+each process of `bench.py --gpus P` does before its timed region.
+"""
+import argparse
+import json
+import os
+import resource
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--nrefs', type=int, default=6)
+    ap.add_argument('--gamma', type=float, default=1e6)
+    ap.add_argument('--ranks', type=int, default=8)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import metric_amg_examples_amd as M
+    n = M.problems.finest_n(3, args.nrefs)
+    s = M.problems.bidomain(3, n, args.gamma)
+    r = M.problems.seeded_rhs(s.N)
+    out = {'N': s.N, 'ranks': args.ranks, 'per_rank': []}
+    hs = []
+    for p in range(args.ranks):
+        torch.cuda.synchronize()
+        m0 = torch.cuda.mem_get_info()[0]
+        t0 = time.time()
+        hs.append(M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=args.ranks, comm_id=None,
+                                  num_functions=2))
+        torch.cuda.synchronize()
+        t = time.time() - t0
+        held = m0 - torch.cuda.mem_get_info()[0]
+        rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20
+        out['per_rank'].append({'rank': p, 'setup_s': round(t, 2), 'device_GB': round(held / 1e9, 2),
+                                'peak_rss_GB': round(rss, 1), 'nodes': [hs[-1].o0, hs[-1].o1]})
+        print('rank %d: setup %.1fs, device %.2f GB, peak RSS %.1f GB' % (p, t, held / 1e9, rss), flush=True)
+    rs = [torch.as_tensor(h.local_slice(r)).cuda() for h in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    nv = s.N // 2
+    z = np.zeros(s.N)
+    for h, zz in zip(hs, zs):
+        zz = zz.cpu().numpy()
+        k = h.o1 - h.o0
+        z[h.o0:h.o1] = zz[:k]
+        z[nv + h.o0:nv + h.o1] = zz[k:]
+    for h in hs:
+        h.close()
+    B = M.MetricAMG(s, s.W, idofs=s.idofs, num_functions=2, setup='gpu')
+    z1 = B * r
+    out['rel_diff_vs_single_gpu'] = float(np.linalg.norm(z - z1) / np.linalg.norm(z1))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -620,6 +620,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_POST_SELL  0: K in lane-group BSR instead of SELL-64 (default 1)
 //   MAMG_POST_U     SELL blocks per chunk of the K kernel (4 default, 8, 16)
 //   MAMG_SELL_REMAP 1: XCD-contiguous row order for the level-0 SELL kernels
+//   MAMG_POST_REMAP 1: XCD-contiguous row order for the level-0 K (post) kernel
 //   MAMG_SELL_MAX_LEN SELL only for matrices with <= this many blocks per row (40)
 //   MAMG_HALF       0: full SELL-64 instead of the half-symmetric ELL-64 for A0 (default 1)
 //   MAMG_HALF_U     blocks per chunk of the half-symmetric kernel (4 default, 8)
@@ -629,6 +630,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //                   (default 1; 0 = off, row order by MAMG_HALF_REMAP)
 int g_remap = 1;
 int g_sell_remap = 0;
+int g_post_remap = 0;
 int g_half = 1;
 int g_half_u = 4;
 int g_half_remap = 1;
@@ -674,6 +676,8 @@ void read_knobs() {
   g_half_remap = su ? std::atoi(su) != 0 : 1;
   su = std::getenv("MAMG_HALF_BANDS");
   g_half_bands = su ? std::atoi(su) : 1;
+  su = std::getenv("MAMG_POST_REMAP");
+  g_post_remap = su ? std::atoi(su) != 0 : 0;
   su = std::getenv("MAMG_SELL_REMAP");
   g_sell_remap = su ? std::atoi(su) != 0 : 0;
   const char* e = std::getenv("MAMG_XCD_REMAP");
@@ -1866,7 +1870,7 @@ void launch_sell_u(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 ? g_sell_remap : 0)
+    (TAG == 0 ? (o.epi == EPI_KPOST ? g_post_remap : g_sell_remap) : 0)
   switch (o.epi) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
