@@ -23,13 +23,18 @@
 //   Galerkin       R = P^T (stable radix sort), A P and R (A P) (hash SpGEMM)
 //   coarsest       dense Gauss-Jordan (no pivoting), one pivot per 3 launches
 //
-// Hash SpGEMM (row i of C = A B): one wavefront per row; A's entries are
-// consumed in CSR order (one step each), the 64 lanes take B's row k
-// (distinct columns, so no two lanes of a step touch one slot); the LDS table
-// accumulates sums[j] += a_ik b_kj exactly in scipy's order.  Rows are binned
-// by their product count: <= 384 into a 512-slot table (4 waves per block),
-// larger into 2048 slots (1 wave per block); a row with more distinct columns
-// than that fails loudly (MAMG_ERR_UNSUPPORTED) instead of degrading.
+// Hash SpGEMM (row i of C = A B): one wavefront per row; the LDS table
+// accumulates sums[j] += a_ik b_kj exactly in scipy's order (A's entries in
+// CSR order, each B row's entries once).  The wave takes A's entries in
+// batches of 64 / GL: lane group g (GL lanes) loads entry kb + g and its B row,
+// all groups insert their columns into the table at once, then the groups add
+// their products one group after another (g ascending = CSR order; within a
+// group the columns are distinct, so no two lanes touch one slot).  A batch
+// with a B row longer than GL falls back to one entry at a time, 64 lanes over
+// its B row.  GL is chosen per product from B's mean row length.  Rows run
+// first in a 128-slot table, overflowing rows in 512 and then 2048 slots; a
+// row with more distinct columns than that fails loudly
+// (MAMG_ERR_UNSUPPORTED) instead of degrading.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -471,18 +476,36 @@ struct BTent {              // B = tentative prolongator: dof f nv + I -> f nagg
   }
 };
 
-template <int TS, int WPB, bool FILL, class BS>
+// insert column j into a wave's table: its slot, or full = true
+template <int TS>
+__device__ __forceinline__ uint32_t hash_insert(int32_t* keys, int32_t j, bool* full) {
+  uint32_t slot = ((uint32_t)j * 2654435761u) & (TS - 1);
+  for (int probes = 0;;) {
+    const int32_t cur = keys[slot];
+    if (cur == j) return slot;
+    if (cur == -1) {
+      const int32_t old = atomicCAS(&keys[slot], -1, j);
+      if (old == -1 || old == j) return slot;
+    }
+    slot = (slot + 1) & (TS - 1);
+    if (++probes >= TS) { *full = true; return 0; }
+  }
+}
+
+template <int TS, int WPB, bool FILL, int GL, class BS>
 __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
     int64_t nrows, const int32_t* __restrict__ rows, const int64_t* __restrict__ ub, int64_t lim,
     const int64_t* __restrict__ aptr, const int32_t* __restrict__ acol, const double* __restrict__ aval,
     BS B, int64_t* cptr, int32_t* __restrict__ ccol, double* __restrict__ cval, int* overflow,
     int32_t* spill) {
+  constexpr int NG = 64 / GL;
   __shared__ int32_t keys[WPB][TS];
   __shared__ double sums[WPB][TS];
   __shared__ int32_t ck[WPB][TS];
   __shared__ double cv[WPB][TS];
   __shared__ int cnt[WPB];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane / GL, sub = lane % GL;
   const int64_t nw = (int64_t)gridDim.x * WPB;
   for (int64_t r = (int64_t)blockIdx.x * WPB + w; r < nrows; r += nw) {
     const int64_t i = rows ? rows[r] : r;
@@ -492,42 +515,57 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     bool full = false;
-    for (int64_t kk = aptr[i]; kk < aptr[i + 1]; ++kk) {
-      const int64_t k = acol[kk];
-      const double a = aval[kk];
-      const int64_t len = B.len(k);
-      for (int64_t t0 = 0; t0 < len; t0 += 64) {
-        const int64_t t = t0 + lane;
-        if (t < len) {
-          int32_t j;
-          double bv;
-          B.get(k, t, &j, &bv);
-          uint32_t slot = ((uint32_t)j * 2654435761u) & (TS - 1);
-          int probes = 0;
-          for (;;) {
-            const int32_t cur = keys[w][slot];
-            if (cur == j) break;
-            if (cur == -1) {
-              const int32_t old = atomicCAS(&keys[w][slot], -1, j);
-              if (old == -1 || old == j) break;
-            }
-            slot = (slot + 1) & (TS - 1);
-            if (++probes >= TS) { full = true; break; }
-          }
-          if (!full) sums[w][slot] = sums[w][slot] + a * bv;
+    const int64_t a1 = aptr[i + 1];
+    for (int64_t kb = aptr[i]; kb < a1; kb += NG) {
+      int64_t k = 0, len = 0;
+      double a = 0.0;
+      if (kb + g < a1) { k = acol[kb + g]; a = aval[kb + g]; len = B.len(k); }
+      if (NG > 1 && !__any(len > GL)) {
+        const bool act = sub < len;
+        int32_t j = 0;
+        double bv = 0.0;
+        uint32_t slot = 0;
+        if (act) {
+          B.get(k, sub, &j, &bv);
+          slot = hash_insert<TS>(keys[w], j, &full);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (__any(full)) break;
+        for (int gg = 0; gg < NG; ++gg) {       // groups add in CSR order
+          if (g == gg && act) sums[w][slot] = sums[w][slot] + a * bv;
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        continue;
+      }
+      for (int gg = 0; gg < NG && kb + gg < a1; ++gg) {   // one entry at a time
+        const int64_t k1 = acol[kb + gg];
+        const double a2 = aval[kb + gg];
+        const int64_t len1 = B.len(k1);
+        for (int64_t t0 = 0; t0 < len1; t0 += 64) {
+          const int64_t t = t0 + lane;
+          if (t < len1) {
+            int32_t j;
+            double bv;
+            B.get(k1, t, &j, &bv);
+            const uint32_t slot = hash_insert<TS>(keys[w], j, &full);
+            if (!full) sums[w][slot] = sums[w][slot] + a2 * bv;
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        if (__any(full)) break;
       }
       if (__any(full)) break;
     }
     if (__any(full)) {
-      // table full: the row spills to the large-table launch (count pass) or
-      // is skipped here because that launch fills it (fill pass); in the
-      // large-table launch itself it is an error
+      // table full: the row spills to the next tier's list (count pass) or
+      // is skipped here because that tier fills it (fill pass); in the last
+      // tier (no spill list) it is an error
       if (lane == 0) {
-        if (!rows && spill && !FILL) spill[atomicAdd(overflow, 1)] = (int32_t)i;
-        else if (rows || !spill) atomicAdd(overflow + 1, 1);
+        if (!spill) atomicAdd(overflow + 1, 1);
+        else if (!FILL) spill[atomicAdd(overflow, 1)] = (int32_t)i;
       }
       continue;
     }
@@ -738,29 +776,32 @@ struct Clock {
 int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
 
 // exact output size + row pointers + entries of C = A B (hash SpGEMM).
-// Optimistic tiering: every row first runs in a 512-slot table (4 waves per
-// block); a row whose distinct columns overflow it spills to a list that the
-// 2048-slot launch (1 wave per block) redoes.  Each slot accumulates its
-// products in A-row order whatever the table size, so both tiers give the
-// same bits.  (Binning by the product-count upper bound sent most Galerkin
-// rows, whose product counts far exceed their distinct counts, to the slow
-// large-table launch.)
-template <class BS>
-int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
-  constexpr int TS1 = 512, TS2 = 2048;
+// Optimistic tiering: every row first runs in a 128-slot table (4 waves per
+// block, 12 KB of LDS, so LDS no longer caps the waves per CU); a row whose
+// distinct columns overflow it spills to a list that the 512-slot launch
+// redoes, whose overflow the 2048-slot launch (1 wave per block) redoes.  A
+// row's tier depends only on its distinct-column count, so the count and fill
+// passes agree.  Each slot accumulates its products in A-row order whatever
+// the table size, so every tier gives the same bits.  (Binning by the
+// product-count upper bound sent most Galerkin rows, whose product counts far
+// exceed their distinct counts, to the slow large-table launch.)
+template <int GL, class BS>
+int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
+  constexpr int TS0 = 128, TS1 = 512, TS2 = 2048;
   const int64_t n = A.n;
   Scratch S;
-  int32_t* big = nullptr;
-  int* ctr = nullptr;   // [0] spilled rows, [1] rows over the large table
-  RCHK(S.alloc(&big, n, err));
-  RCHK(S.alloc(&ctr, 2, err));
-  HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
+  int32_t *l1 = nullptr, *l2 = nullptr;
+  int* ctr = nullptr;   // [0] rows spilled by tier 0, [1] tier-2 overflow, [2] rows spilled by tier 1
+  RCHK(S.alloc(&l1, n, err));
+  RCHK(S.alloc(&l2, n, err));
+  RCHK(S.alloc(&ctr, 4, err));
+  HIPCHK(hipMemset(ctr, 0, 4 * sizeof(int)));
   C->n = n;
   C->m = ncols;
   RCHK(galloc(G, &C->ptr, n + 1, err));
   HIPCHK(hipMemset(C->ptr, 0, (n + 1) * sizeof(int64_t)));
-  const unsigned g1 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 3) / 4), 65536);
-  int nbig = 0;
+  const unsigned g0 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 3) / 4), 65536);
+  int n1 = 0, n2 = 0;
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1) {
       RCHK(dscan_incl_i64(C->ptr, C->ptr, n + 1, nullptr, err));
@@ -768,22 +809,33 @@ int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::strin
       RCHK(galloc(G, &C->col, C->nnz, err));
       RCHK(galloc(G, &C->val, C->nnz, err));
     }
+    int64_t* cp = C->ptr;
+    int32_t* cc = pass ? C->col : nullptr;
+    double* cv = pass ? C->val : nullptr;
     if (pass == 0) {
-      spgemm_kernel<TS1, 4, false><<<g1, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
-                                                 nullptr, nullptr, ctr, big);
+      spgemm_kernel<TS0, 4, false, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
+                                                ctr, l1);
       HIPCHK(hipGetLastError());
-      RCHK(read_int(ctr, &nbig, err));
-      const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
-      if (nbig)
-        spgemm_kernel<TS2, 1, false><<<g2, 64>>>(nbig, big, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
-                                                  nullptr, nullptr, ctr, nullptr);
+      RCHK(read_int(ctr, &n1, err));
+      if (n1) {
+        const unsigned g1 = (unsigned)std::min<int64_t>((n1 + 3) / 4, 65536);
+        spgemm_kernel<TS1, 4, false, GL><<<g1, 256>>>(n1, l1, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
+                                                  ctr + 2, l2);
+        HIPCHK(hipGetLastError());
+        RCHK(read_int(ctr + 2, &n2, err));
+      }
+      if (n2)
+        spgemm_kernel<TS2, 1, false, GL><<<(unsigned)std::min<int64_t>(n2, 65536), 64>>>(
+            n2, l2, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr, nullptr);
     } else {
-      const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, nbig), 65536);
-      spgemm_kernel<TS1, 4, true><<<g1, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
-                                                C->col, C->val, ctr, big);
-      if (nbig)
-        spgemm_kernel<TS2, 1, true><<<g2, 64>>>(nbig, big, nullptr, 0, A.ptr, A.col, A.val, B, C->ptr,
-                                                 C->col, C->val, ctr, nullptr);
+      spgemm_kernel<TS0, 4, true, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
+                                               ctr + 3, l1);
+      if (n1)
+        spgemm_kernel<TS1, 4, true, GL><<<(unsigned)std::min<int64_t>((n1 + 3) / 4, 65536), 256>>>(
+            n1, l1, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr + 3, l2);
+      if (n2)
+        spgemm_kernel<TS2, 1, true, GL><<<(unsigned)std::min<int64_t>(n2, 65536), 64>>>(
+            n2, l2, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr, nullptr);
     }
     HIPCHK(hipGetLastError());
     int ovf = 0;
@@ -795,6 +847,14 @@ int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::strin
     }
   }
   return MAMG_OK;
+}
+
+// lane-group width from B's mean row length (most B rows fit one group)
+template <class BS>
+int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, double blen) {
+  if (blen <= 1.5) return spgemm_gl<2>(G, A, B, ncols, C, err);
+  if (blen <= 6.0) return spgemm_gl<8>(G, A, B, ncols, C, err);
+  return spgemm_gl<32>(G, A, B, ncols, C, err);
 }
 
 // R = P^T (setup.cpp transpose: counting order == stable sort by column)
@@ -1066,7 +1126,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       L.w_sa = w;
       GHier tmp;                    // A T lives only until P is built
       DevMat AT;
-      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, 2 * nagg, &AT, err));
+      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, 2 * nagg, &AT, err, 1.0));
       L.P.n = n;
       L.P.m = 2 * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
@@ -1098,9 +1158,9 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     G->phase_ms[2] += clk.lap();
     // Galerkin: R = P^T, A P, A_c = R (A P)
     RCHK(transpose(G, L.P, &L.R, err));
-    RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err));
+    RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err, (double)L.P.nnz / std::max<int64_t>(1, L.P.n)));
     DevMat next;
-    RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err));
+    RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err, (double)L.AP.nnz / std::max<int64_t>(1, L.AP.n)));
     if (!p.post_fusion) {
       for (void* q : {(void*)L.AP.ptr, (void*)L.AP.col, (void*)L.AP.val}) G->release(q);
       L.AP = DevMat();
