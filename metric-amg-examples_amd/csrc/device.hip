@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "device.h"
+#include "rowstage.h"
 
 namespace mamg {
 namespace {
@@ -952,43 +953,33 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
 // convert.cpp (to_bsr2, merge_bsr_rows, to_sell with sigma = 1, pack_sym);
 // pure data movement, so the apply sees identical bits either way.
 // ---------------------------------------------------------------------------
-// node I's four sorted column segments: q = 2 f + g holds the entries of row
-// f nr + I whose column lies in field g (node column = col - g nc)
-__device__ __forceinline__ void node_segs(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
-                                          int64_t nr, int64_t nc, int64_t I, int64_t* k, int64_t* e) {
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int64_t a = ptr[f * nr + I], b = ptr[f * nr + I + 1];
-    int64_t lo = a, hi = b;                 // first entry with col >= nc
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (col[mid] < nc) lo = mid + 1; else hi = mid;
-    }
-    k[2 * f] = a; e[2 * f] = lo; k[2 * f + 1] = lo; e[2 * f + 1] = b;
-  }
-}
-
+// node I's four sorted column segments (rowstage.h stage_segs): q = 2 f + g
+// holds the entries of row f nr + I whose column lies in field g (node
+// column = col - g nc)
 template <bool FILL>
-__global__ __launch_bounds__(256) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
-                                                      const int32_t* __restrict__ col,
-                                                      const double* __restrict__ val, int64_t* bptr,
-                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
+                                                     const int32_t* __restrict__ col,
+                                                     const double* __restrict__ val, int64_t* bptr,
+                                                     int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
+  __shared__ RowStage S;     // rowstage.h: the wave's rows staged through LDS
+  const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
+  RowView vw[2];
+  stage_rows<FILL>(S, ptr, col, val, nr, I0, vw);
   if (I >= nr) return;
   int64_t k[4], e[4];
-  node_segs(ptr, col, nr, nc, I, k, e);
+  stage_segs(ptr, vw, nr, nc, I, k, e);
   int64_t o = FILL ? bptr[I] : 0;
   for (;;) {
     int64_t J = INT64_MAX;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q]) J = min(J, (int64_t)col[k[q]] - (q & 1) * nc);
+      if (k[q] < e[q]) J = min(J, (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nc);
     if (J == INT64_MAX) break;
     dv4 v = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q] && (int64_t)col[k[q]] - (q & 1) * nc == J) {
-        if (FILL) v[q] = val[k[q]];
+      if (k[q] < e[q] && (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nc == J) {
+        if (FILL) v[q] = vw[q >> 1].val(k[q]);
         ++k[q];
       }
     if (FILL) { bcol[o] = (int32_t)J; bval[o] = v; }
@@ -1251,13 +1242,13 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   B->nr = nr; B->nc = nc; B->merged = false;
   if ((rc = T->alloc(&B->ptr, nr + 1, err))) return rc;
   HIPCHK(hipMemset(B->ptr, 0, sizeof(int64_t)));
-  if (nr) csr2bsr_kernel<false><<<nblocks(nr), 256>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
+  if (nr) csr2bsr_kernel<false><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(B->ptr, B->ptr, nr + 1, nullptr, err))) return rc;
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
-  if (nr) csr2bsr_kernel<true><<<nblocks(nr), 256>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
 }

@@ -44,6 +44,7 @@
 #include <cstring>
 
 #include "gsetup.h"
+#include "rowstage.h"
 
 typedef double dv4_t __attribute__((ext_vector_type(4)));
 
@@ -142,42 +143,33 @@ int to_host(T* dst, const T* src, int64_t count, std::string* err) {
 // node graph (setup.cpp node_graph, nf = 2): s_IJ = sqrt(sum of squares over
 // the 2x2 block), accumulated over rows I then nv + I, each in CSR order
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void segs2(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
-                                      int64_t nr, int64_t nc, int64_t I, int64_t* k, int64_t* e) {
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int64_t a = ptr[f * nr + I], b = ptr[f * nr + I + 1];
-    int64_t lo = a, hi = b;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (col[mid] < nc) lo = mid + 1; else hi = mid;
-    }
-    k[2 * f] = a; e[2 * f] = lo; k[2 * f + 1] = lo; e[2 * f + 1] = b;
-  }
-}
-
 template <bool FILL>
-__global__ __launch_bounds__(256) void node_graph_kernel(int64_t nv, const int64_t* __restrict__ ptr,
-                                                         const int32_t* __restrict__ col,
-                                                         const double* __restrict__ val, int64_t* gptr,
-                                                         int32_t* __restrict__ gcol, double* __restrict__ gval) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ col,
+                                                        const double* __restrict__ val, int64_t* gptr,
+                                                        int32_t* __restrict__ gcol, double* __restrict__ gval) {
+  __shared__ RowStage S;
+  const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
+  RowView vw[2];
+  stage_rows<FILL>(S, ptr, col, val, nv, I0, vw);
   if (I >= nv) return;
   int64_t k[4], e[4];
-  segs2(ptr, col, nv, nv, I, k, e);
+  stage_segs(ptr, vw, nv, nv, I, k, e);
   int64_t o = FILL ? gptr[I] : 0;
   for (;;) {
     int64_t J = INT64_MAX;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q]) J = min(J, (int64_t)col[k[q]] - (q & 1) * nv);
+      if (k[q] < e[q]) J = min(J, (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nv);
     if (J == INT64_MAX) break;
     double acc = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)          // order (f0,g0) (f0,g1) (f1,g0) (f1,g1)
-      if (k[q] < e[q] && (int64_t)col[k[q]] - (q & 1) * nv == J) {
-        const double a = val[k[q]];
-        acc += a * a;
+      if (k[q] < e[q] && (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nv == J) {
+        if (FILL) {
+          const double a = vw[q >> 1].val(k[q]);
+          acc += a * a;
+        }
         ++k[q];
       }
     if (FILL) { gcol[o] = (int32_t)J; gval[o] = sqrt(acc); }
@@ -420,27 +412,37 @@ __global__ __launch_bounds__(256) void node_inverse_kernel(int64_t nv, const int
 
 // rho_B = max over dofs of sum_j |(D_B^-1 A)_ij| (SMMP order: row I's terms
 // then row nv + I's; sorted-column abs sum of the nonzeros)
-__global__ __launch_bounds__(256) void block_rho_kernel(int64_t nv, const int64_t* __restrict__ ptr,
-                                                        const int32_t* __restrict__ col,
-                                                        const double* __restrict__ val,
-                                                        const dv4_t* __restrict__ Dinv,
-                                                        unsigned long long* rho_bits) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= 2 * nv) return;
-  const int64_t I = i % nv, f = i / nv;
-  const dv4_t D = Dinv[I];
-  const double d0 = f ? D.z : D.x, d1 = f ? D.w : D.y;
-  int64_t a = ptr[I], ae = ptr[I + 1], b = ptr[nv + I], be = ptr[nv + I + 1];
+__global__ __launch_bounds__(64) void block_rho_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const dv4_t* __restrict__ Dinv,
+                                                       unsigned long long* rho_bits) {
+  __shared__ RowStage S;
+  const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
+  RowView vw[2];
+  stage_rows<true>(S, ptr, col, val, nv, I0, vw);
   double s = 0.0;
-  while (a < ae || b < be) {
-    const int64_t ja = a < ae ? col[a] : INT64_MAX, jb = b < be ? col[b] : INT64_MAX;
-    const int64_t j = min(ja, jb);
-    double v = 0.0;
-    if (ja == j) { v = v + d0 * val[a]; ++a; }
-    if (jb == j) { v = v + d1 * val[b]; ++b; }
-    if (v != 0.0) s += fabs(v) * 1.0;
+  if (I < nv) {
+    const dv4_t D = Dinv[I];
+    for (int f = 0; f < 2; ++f) {          // dof f nv + I
+      const double d0 = f ? D.z : D.x, d1 = f ? D.w : D.y;
+      int64_t a = ptr[I], ae = ptr[I + 1], b = ptr[nv + I], be = ptr[nv + I + 1];
+      double sf = 0.0;
+      while (a < ae || b < be) {
+        const int64_t ja = a < ae ? vw[0].col(a) : INT64_MAX, jb = b < be ? vw[1].col(b) : INT64_MAX;
+        const int64_t j = min(ja, jb);
+        double v = 0.0;
+        if (ja == j) { v = v + d0 * vw[0].val(a); ++a; }
+        if (jb == j) { v = v + d1 * vw[1].val(b); ++b; }
+        if (v != 0.0) sf += fabs(v) * 1.0;
+      }
+      s = fmax(s, sf);
+    }
   }
-  atomicMax(rho_bits, (unsigned long long)__double_as_longlong(s));
+  // wave max first (the sums are >= +0, so the max is exact in any order),
+  // then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(rho_bits, (unsigned long long)__double_as_longlong(s));
 }
 
 __global__ __launch_bounds__(256) void scale_blocks_kernel(int64_t nv, double sc, const dv4_t* __restrict__ D,
@@ -853,7 +855,8 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
 template <class BS>
 int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, double blen) {
   if (blen <= 1.5) return spgemm_gl<2>(G, A, B, ncols, C, err);
-  if (blen <= 6.0) return spgemm_gl<8>(G, A, B, ncols, C, err);
+  if (blen <= 5.0) return spgemm_gl<8>(G, A, B, ncols, C, err);
+  if (blen <= 11.0) return spgemm_gl<16>(G, A, B, ncols, C, err);
   return spgemm_gl<32>(G, A, B, ncols, C, err);
 }
 
@@ -892,7 +895,7 @@ int block_rho(const DevMat& A, int64_t nv, const dv4_t* D, double* rho, std::str
   unsigned long long* rb = nullptr;
   RCHK(S.alloc(&rb, 1, err));
   HIPCHK(hipMemset(rb, 0, sizeof(unsigned long long)));
-  block_rho_kernel<<<nblk(2 * nv), 256>>>(nv, A.ptr, A.col, A.val, D, rb);
+  block_rho_kernel<<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, D, rb);
   HIPCHK(hipGetLastError());
   unsigned long long h = 0;
   RCHK(to_host(&h, rb, 1, err));
@@ -922,13 +925,13 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, in
   Gr.n = Gr.m = nv;
   RCHK(S.alloc(&Gr.ptr, nv + 1, err));
   HIPCHK(hipMemset(Gr.ptr, 0, sizeof(int64_t)));
-  node_graph_kernel<false><<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
+  node_graph_kernel<false><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
   RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
   RCHK(S.alloc(&Gr.col, Gr.nnz, err));
   RCHK(S.alloc(&Gr.val, Gr.nnz, err));
-  node_graph_kernel<true><<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+  node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
   double* d = nullptr;
   uint8_t *flag = nullptr, *nonisol = nullptr;
   int* ctr = nullptr;

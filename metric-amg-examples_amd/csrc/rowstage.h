@@ -1,0 +1,86 @@
+// rowstage.h -- LDS staging of a wave's node rows for the setup/layout merges.
+//
+// The node-wise merges of the field-major CSR (node graph, block rho, CSR ->
+// BSR2) give each lane one node I and walk rows I and nr + I sequentially, in
+// column order (their sums must keep that order to stay bitwise equal to the
+// host setup).  Read straight from HBM, the 64 lanes of a load instruction
+// touch 64 different rows: every instruction splits into ~64 cache-line
+// requests and the merges ran at ~0.1 TB/s.  Here the wave first copies the
+// contiguous entry ranges of its 64 nodes' rows -- ptr[I0] .. ptr[I0 + 64] of
+// field 0 and the same of field 1 -- into LDS with coalesced loads, then each
+// lane merges from LDS in the same order as before.  Ranges longer than CAP
+// (coarse Galerkin rows) are read from global memory exactly as before.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mamg {
+
+constexpr int RS_NODES = 64;     // nodes per wave (= workgroup)
+constexpr int RS_CAP = 2048;     // staged entries per field (A0: ~1900)
+
+struct RowStage {
+  int32_t c[2][RS_CAP];
+  double v[2][RS_CAP];
+};
+
+// Row view of one field: entry k of the field's rows is C[k - off], V[k - off]
+struct RowView {
+  const int32_t* C;
+  const double* V;
+  int64_t off;
+  __device__ __forceinline__ int32_t col(int64_t k) const { return C[k - off]; }
+  __device__ __forceinline__ double val(int64_t k) const { return V[k - off]; }
+};
+
+// Stage the rows of nodes [I0, I0 + RS_NODES) (clipped to nr) of both fields;
+// fills view[2] (LDS when the ranges fit, else global).  Every lane of the
+// wave must call it (the loads and the barrier are wave-wide).
+template <bool VALS>
+__device__ __forceinline__ void stage_rows(RowStage& S, const int64_t* __restrict__ ptr,
+                                           const int32_t* __restrict__ col, const double* __restrict__ val,
+                                           int64_t nr, int64_t I0, RowView* view) {
+  const int lane = threadIdx.x & 63;
+  const int64_t I1 = I0 + RS_NODES < nr ? I0 + RS_NODES : nr;
+  int64_t b[2], n[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    b[f] = ptr[f * nr + I0];
+    n[f] = ptr[f * nr + I1] - b[f];
+  }
+  const bool fits = n[0] <= RS_CAP && n[1] <= RS_CAP;
+  if (fits) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      for (int64_t t = lane; t < n[f]; t += 64) {
+        S.c[f][t] = col[b[f] + t];
+        if (VALS) S.v[f][t] = val[b[f] + t];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < 2; ++f) view[f] = RowView{S.c[f], S.v[f], b[f]};
+  } else {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) view[f] = RowView{col, val, 0};
+  }
+}
+
+// node I's four sorted column segments (q = 2 f + g: the entries of row
+// f nr + I whose column lies in field g, node column = col - g nc)
+__device__ __forceinline__ void stage_segs(const int64_t* __restrict__ ptr, const RowView* view, int64_t nr,
+                                           int64_t nc, int64_t I, int64_t* k, int64_t* e) {
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t a = ptr[f * nr + I], b = ptr[f * nr + I + 1];
+    int64_t lo = a, hi = b;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (view[f].col(mid) < nc) lo = mid + 1; else hi = mid;
+    }
+    k[2 * f] = a; e[2 * f] = lo; k[2 * f + 1] = lo; e[2 * f + 1] = b;
+  }
+}
+
+}  // namespace mamg
