@@ -619,7 +619,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_NT         1: non-temporal matrix loads in the level-0 kernels
 //   MAMG_POST_K     0: fused post sweep over [P | AP] instead of K = P - W A P (default 1)
 //   MAMG_POST_SELL  0: K in lane-group BSR instead of SELL-64 (default 1)
-//   MAMG_POST_U     SELL blocks per chunk of the K kernel (4 default, 8, 16)
+//   MAMG_POST_U     SELL blocks per chunk of the K kernel (6 default, 4, 5, 8, 16)
 //   MAMG_SELL_REMAP 1: XCD-contiguous row order for the level-0 SELL kernels
 //   MAMG_POST_REMAP 1: XCD-contiguous row order for the level-0 K (post) kernel
 //   MAMG_SELL_MAX_LEN SELL only for matrices with <= this many blocks per row (40)
@@ -643,7 +643,7 @@ int g_sell_post = 0;
 int g_sell_u = 8;
 int g_nt = 0;
 int g_post_k = 1;
-int g_post_u = 4;
+int g_post_u = 6;
 int g_post_sell = 1;
 int64_t g_sell_min_rows = 1 << 20;
 int64_t g_sell_max_len = 40;
@@ -651,8 +651,8 @@ void read_knobs() {
   const char* pk = std::getenv("MAMG_POST_K");
   g_post_k = pk ? std::atoi(pk) != 0 : 1;
   pk = std::getenv("MAMG_POST_U");
-  g_post_u = pk ? std::atoi(pk) : 4;
-  if (g_post_u != 4 && g_post_u != 8 && g_post_u != 16) g_post_u = 4;
+  g_post_u = pk ? std::atoi(pk) : 6;
+  if (g_post_u != 4 && g_post_u != 5 && g_post_u != 6 && g_post_u != 8 && g_post_u != 16) g_post_u = 6;
   pk = std::getenv("MAMG_POST_SELL");
   g_post_sell = pk ? std::atoi(pk) != 0 : 1;
   const char* su = std::getenv("MAMG_SELL_U");
@@ -1881,6 +1881,8 @@ void launch_sell_x(const Op& o, hipStream_t s) {
     switch (u * 2 + (g_nt ? 1 : 0)) {
       case 8: launch_sell_u<XFM, SYM, 4, false, TAG>(o, s); return;
       case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
+      case 10: launch_sell_u<XFM, SYM, 5, false, TAG>(o, s); return;
+      case 12: launch_sell_u<XFM, SYM, 6, false, TAG>(o, s); return;
       case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
       case 17: launch_sell_u<XFM, SYM, 8, true, TAG>(o, s); return;
       case 32: launch_sell_u<XFM, SYM, 16, false, TAG>(o, s); return;
