@@ -9,6 +9,9 @@ rank the setup wall time, device bytes held and the process's peak host RSS,
 then runs one virtual distributed apply (device copies stand in for RCCL,
 same counts/offsets) and compares it with the single-GPU apply.  This is what
 each process of `bench.py --gpus P` does before its timed region.
+
+With MAMG_DIST_DRY=1 it instead times each rank's cycle with the exchanges
+skipped: the compute part of the P-GPU apply (RCCL latency not included).
 """
 import argparse
 import json
@@ -50,6 +53,21 @@ def main():
         print('rank %d: setup %.1fs, device %.2f GB, peak RSS %.1f GB' % (p, t, held / 1e9, rss), flush=True)
     rs = [torch.as_tensor(h.local_slice(r)).cuda() for h in hs]
     zs = [torch.zeros_like(x) for x in rs]
+    if os.environ.get('MAMG_DIST_DRY') == '1':
+        # compute-only time of each rank's cycle (exchanges skipped; the
+        # numbers exclude RCCL latency, the results are not used)
+        names = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_prolong',
+                 'coarse_levels', 'coarsest_dense', 'misc', 'comm']
+        for p, h in enumerate(hs):
+            h.time_apply(rs[p], zs[p], 3, 0)
+            ms, _, _ = h.time_apply(rs[p], zs[p], 20, 0)
+            ms1, kms, _ = h.time_apply(rs[p], zs[p], 5, 1)
+            out['per_rank'][p]['compute_ms_per_apply'] = round(ms, 4)
+            out['per_rank'][p]['classes_ms'] = {k: round(v, 4) for k, v in zip(names, kms) if v}
+            print('rank %d: compute-only %.3f ms/apply %s' % (p, ms, out['per_rank'][p]['classes_ms']),
+                  flush=True)
+        print(json.dumps(out), flush=True)
+        return
     M.DistMetricAMG.virtual_apply(hs, rs, zs)
     torch.cuda.synchronize()
     nv = s.N // 2

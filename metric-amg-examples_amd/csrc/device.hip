@@ -2454,6 +2454,7 @@ struct DistHandle {
   double apply_bytes = 0.0;
   int64_t nv0 = 0, o0 = 0, o1 = 0;
   bool overlap = true;                 // MAMG_OVERLAP: interior rows during the forward halo
+  bool dry = false;                    // MAMG_DIST_DRY: virtual rank skips its exchanges (timing only)
   hipStream_t side = nullptr;          // stream of the interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   ~DistHandle() {
@@ -2595,6 +2596,10 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     if (d.dk == D_OVERLAP) launch(d.op, s);
     return MAMG_OK;
   }
+  if (!h->comm && h->dry) {            // compute-only timing of one rank (results meaningless)
+    if (d.dk == D_OVERLAP) launch(d.op, s);
+    return MAMG_OK;
+  }
   if (!h->comm) {
     *err = "virtual rank handle (no communicator): use mamg_dist_virtual_apply / _spmv";
     return MAMG_ERR_ARG;
@@ -2700,6 +2705,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   {
     const char* e = std::getenv("MAMG_OVERLAP");
     h->overlap = e ? std::atoi(e) != 0 : true;
+    e = std::getenv("MAMG_DIST_DRY");
+    h->dry = !comm_id && e && std::atoi(e) != 0;
   }
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
