@@ -750,6 +750,10 @@ struct DBsr {              // 2x2 blocks, node-major
   // workgroup b processes 256-row block sched[b] (nullptr: row_block order)
   int32_t* sched = nullptr;
   int64_t nsched = 0;
+  int64_t band_stride = 0;  // plane stride S in rows (0: no band schedule)
+  // band schedule of one sub-range launch [sr0, sr1) (multi-GPU interior rows)
+  int32_t* sched_r = nullptr;
+  int64_t nsched_r = 0, sr0 = 0, sr1 = 0;
 };
 
 struct DLevel {
@@ -1289,39 +1293,11 @@ int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* 
   return MAMG_OK;
 }
 
-// Band schedule for the half-symmetric kernel.  A lower block (I, J < I) is
-// re-read from row J's upper part; with the rows of a structured 3-D mesh in
-// lexicographic order the farthest mirror sits one plane (stride S rows)
-// back.  Row order alone puts a whole plane (~16 MB at n = 256) between the
-// two reads, more than an XCD's 4 MB L2.  The schedule cuts each plane of
-// 256-row blocks into 8 x nsub bands, gives XCD x (workgroups b = x mod 8)
-// the bands x nsub .. x nsub + nsub - 1 and walks each band plane by plane,
-// so the mirror was streamed one band (S / (8 nsub) rows) earlier on the same
-// XCD.  S = the median, over sampled rows, of the distance to the row's first
-// (smallest) column.  The schedule only permutes which workgroup computes
-// which rows: every row is still summed by one lane in its own order, so the
-// result is bitwise that of any other order.  Unstructured or narrow-band
-// matrices (< 4 blocks per band) keep the row_block order.
-template <class HT>
-int build_band_sched(HT* h, const TBsr& B, DBsr* D, std::string* err) {
-  const int nsub = g_half_bands;
-  const int64_t nr = B.nr, G = (nr + 255) / 256;
-  if (nsub <= 0 || G < 64) return MAMG_OK;
-  const int ns = 257;
-  std::vector<int64_t> off;
-  for (int i = 0; i < ns; ++i) {
-    const int64_t I = nr / 4 + (nr / 2) * i / ns;
-    int64_t p = 0;
-    int32_t c = 0;
-    HIPCHK(hipMemcpy(&p, B.ptr + I, sizeof(int64_t), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&c, B.col + p, sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (c < I) off.push_back(I - c);
-  }
-  if (off.size() < ns / 2) return MAMG_OK;
-  std::nth_element(off.begin(), off.begin() + off.size() / 2, off.end());
-  const int64_t S = off[off.size() / 2];
+// the schedule of G 256-row blocks for plane stride S (empty: keep row order)
+std::vector<int32_t> band_sched(int64_t G, int64_t S, int nsub) {
+  std::vector<int32_t> sched;
   const int64_t Pb = std::max<int64_t>(1, (S + 128) / 256), nb = 8 * (int64_t)nsub;
-  if (Pb < 4 * nb) return MAMG_OK;
+  if (nsub <= 0 || G < 64 || Pb < 4 * nb) return sched;
   std::vector<std::vector<int32_t>> L(8);
   for (int x = 0; x < 8; ++x)
     for (int sb = 0; sb < nsub; ++sb) {
@@ -1340,20 +1316,69 @@ int build_band_sched(HT* h, const TBsr& B, DBsr* D, std::string* err) {
     const size_t want = (size_t)(G / 8 + (x < G % 8 ? 1 : 0));
     while (L[x].size() < want) { L[x].push_back(spill.back()); spill.pop_back(); }
   }
-  std::vector<int32_t> sched(G);
+  sched.resize(G);
   std::vector<char> seen(G, 0);
   for (int64_t b = 0; b < G; ++b) {
     sched[b] = L[b % 8][b / 8];
-    if (sched[b] < 0 || sched[b] >= G || seen[sched[b]]++) {
-      *err = "band schedule is not a permutation of the row blocks";
-      return MAMG_ERR_SETUP;
-    }
+    if (sched[b] < 0 || sched[b] >= G || seen[sched[b]]++) return std::vector<int32_t>();
   }
+  return sched;
+}
+
+template <class HT>
+int upload_sched(HT* h, const std::vector<int32_t>& sched, int32_t** d, int64_t* n, std::string* err) {
   int rc;
-  if ((rc = dalloc(h, &D->sched, G, err))) return rc;
-  HIPCHK(hipMemcpy(D->sched, sched.data(), G * sizeof(int32_t), hipMemcpyHostToDevice));
-  D->nsched = G;
+  if ((rc = dalloc(h, d, (int64_t)sched.size(), err))) return rc;
+  HIPCHK(hipMemcpy(*d, sched.data(), sched.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  *n = (int64_t)sched.size();
   return MAMG_OK;
+}
+
+// Band schedule for the half-symmetric kernel.  A lower block (I, J < I) is
+// re-read from row J's upper part; with the rows of a structured 3-D mesh in
+// lexicographic order the farthest mirror sits one plane (stride S rows)
+// back.  Row order alone puts a whole plane (~16 MB at n = 256) between the
+// two reads, more than an XCD's 4 MB L2.  The schedule cuts each plane of
+// 256-row blocks into 8 x nsub bands, gives XCD x (workgroups b = x mod 8)
+// the bands x nsub .. x nsub + nsub - 1 and walks each band plane by plane,
+// so the mirror was streamed one band (S / (8 nsub) rows) earlier on the same
+// XCD.  S = the median, over sampled rows, of the distance to the row's first
+// (smallest) column.  The schedule only permutes which workgroup computes
+// which rows: every row is still summed by one lane in its own order, so the
+// result is bitwise that of any other order.  Unstructured or narrow-band
+// matrices (< 4 blocks per band) keep the row_block order.
+template <class HT>
+int build_band_sched(HT* h, const TBsr& B, DBsr* D, std::string* err) {
+  const int64_t nr = B.nr, G = (nr + 255) / 256;
+  if (g_half_bands <= 0 || G < 64) return MAMG_OK;
+  const int ns = 257;
+  std::vector<int64_t> off;
+  for (int i = 0; i < ns; ++i) {
+    const int64_t I = nr / 4 + (nr / 2) * i / ns;
+    int64_t p = 0;
+    int32_t c = 0;
+    HIPCHK(hipMemcpy(&p, B.ptr + I, sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&c, B.col + p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (c < I) off.push_back(I - c);
+  }
+  if (off.size() < ns / 2) return MAMG_OK;
+  std::nth_element(off.begin(), off.begin() + off.size() / 2, off.end());
+  const std::vector<int32_t> sched = band_sched(G, off[off.size() / 2], g_half_bands);
+  if (sched.empty()) return MAMG_OK;
+  D->band_stride = off[off.size() / 2];
+  return upload_sched(h, sched, &D->sched, &D->nsched, err);
+}
+
+// the same for the launch over rows [r0, r1) only (block b covers rows
+// r0 + 256 b ..): the multi-GPU interior run
+template <class HT>
+int build_band_sched_range(HT* h, DBsr* D, int64_t r0, int64_t r1, std::string* err) {
+  if (!D->half || D->band_stride <= 0 || r1 <= r0) return MAMG_OK;
+  const std::vector<int32_t> sched = band_sched((r1 - r0 + 255) / 256, D->band_stride, g_half_bands);
+  if (sched.empty()) return MAMG_OK;
+  D->sr0 = r0;
+  D->sr1 = r1;
+  return upload_sched(h, sched, &D->sched_r, &D->nsched_r, err);
 }
 
 // half-symmetric ELL-64 for a symmetric-block A whose owned part (columns
@@ -1950,7 +1975,8 @@ void launch_half_u(const Op& o, hipStream_t s) {
   if (r1 <= r0) return;
 #define HALF_ARGS r0, r1, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
     o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap, \
-    (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched : nullptr
+    (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched \
+    : (r0 == M.sr0 && r1 == M.sr1 && (int64_t)g == M.nsched_r) ? M.sched_r : nullptr
   switch (o.epi) {
     case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
@@ -2225,7 +2251,7 @@ int dev_level_format(const DeviceHandle* h, int level) {
   const DLevel& L = h->L[level];
   return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) | (L.Ab.half ? MAMG_FMT_HALF : 0) |
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
-         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 ? MAMG_FMT_BANDS : 0);
+         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0);
 }
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
@@ -2749,6 +2775,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       }
       if (l == 0) {
         if ((rc = upload_half_or_bsr(h.get(), P.A, &D.A, err))) return rc;
+        if ((rc = build_band_sched_range(h.get(), &D.A, D.ib0, D.ib1, err))) return rc;
       } else if ((rc = upload_bsr(h.get(), P.A, &D.A, 0, err, true))) {
         return rc;
       }

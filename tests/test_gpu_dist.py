@@ -187,3 +187,31 @@ def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch):
             hh.close()
     for a, b in zip(out[0], out[1]):
         assert np.array_equal(a, b)
+
+
+def test_virtual_ranks_band_schedule_bitwise(lib_built, monkeypatch):
+    """Band schedule on the rank-local half-symmetric A (full-range launch
+    and the ghost-free interior run launched during the halo) at 3-D n=128 on
+    2 ranks, where it engages: cycle and rank SpMV bitwise equal to row
+    order."""
+    import torch
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 128, 1e6)
+    r = mo.seeded_rhs(s.N)
+    P = 2
+    out = []
+    for bands in ('1', '0'):
+        monkeypatch.setenv('MAMG_HALF_BANDS', bands)
+        hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None,
+                              num_functions=2) for p in range(P)]
+        rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+        zs = [torch.zeros_like(x) for x in rs]
+        ys = [torch.zeros_like(x) for x in rs]
+        M.DistMetricAMG.virtual_apply(hs, rs, zs)
+        M.DistMetricAMG.virtual_spmv(hs, rs, ys)
+        torch.cuda.synchronize()
+        out.append([z.cpu().numpy() for z in zs] + [y.cpu().numpy() for y in ys])
+        for hh in hs:
+            hh.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
