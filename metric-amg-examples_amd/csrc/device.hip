@@ -629,6 +629,9 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //                   the mirror re-reads then hit the XCD's own L2)
 //   MAMG_HALF_BANDS band schedule of the half-symmetric kernel: sub-bands per XCD
 //                   (default 1; 0 = off, row order by MAMG_HALF_REMAP)
+//   multi-GPU (read at mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch
+//   during the forward halo (default 1); MAMG_DIST_DRY 1 = a virtual rank skips its
+//   exchanges (compute-only timing, bench/dist_rehearsal.py; results meaningless)
 int g_remap = 1;
 int g_sell_remap = 0;
 int g_post_remap = 0;
