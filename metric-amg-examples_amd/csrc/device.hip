@@ -629,12 +629,16 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //                   the mirror re-reads then hit the XCD's own L2)
 //   MAMG_HALF_BANDS band schedule of the half-symmetric kernel: sub-bands per XCD
 //                   (default 1; 0 = off, row order by MAMG_HALF_REMAP)
+//   MAMG_R_LANES / MAMG_A1_LANES  lanes per row of the level-0 restriction / the
+//                   level-1 operator (0 = auto from the mean row length)
 //   multi-GPU (read at mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch
 //   during the forward halo (default 1); MAMG_DIST_DRY 1 = a virtual rank skips its
 //   exchanges (compute-only timing, bench/dist_rehearsal.py; results meaningless)
 int g_remap = 1;
 int g_sell_remap = 0;
 int g_post_remap = 0;
+int g_r_lanes = 0;
+int g_a1_lanes = 0;
 int g_half = 1;
 int g_half_u = 4;
 int g_half_remap = 1;
@@ -688,6 +692,10 @@ void read_knobs() {
   g_remap = e ? std::atoi(e) : 1;
   e = std::getenv("MAMG_POST_LANES");
   g_post_lanes = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_R_LANES");
+  g_r_lanes = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_A1_LANES");
+  g_a1_lanes = e ? std::atoi(e) : 0;
   e = std::getenv("MAMG_SYM_BLOCKS");
   g_sym = e ? std::atoi(e) != 0 : 1;
 }
@@ -1573,7 +1581,9 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr B;
     if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true, l == 0))) return rc;
+    if ((rc = finalize_bsr(h, &T, B, &D.Ab, l == 1 && g_a1_lanes ? g_a1_lanes : lanesA, true, err, true,
+                           l == 0)))
+      return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
   if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n) {
@@ -1601,7 +1611,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr Rb;
     if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, l == 0 ? g_r_lanes : 0, false, err))) return rc;
   }
   if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
   HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
