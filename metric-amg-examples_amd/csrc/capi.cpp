@@ -306,15 +306,17 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     mamg::GHier G;
     G.device = params->device;
     mamg::DevMat dA;
+    mamg::dev_prereserve(params->device, v.nnz(), nranks);   // rank-local layout memory first
     rc = mamg::upload_a0(v, &G, &dA, &err);
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
     if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
-    if (rc && rc != MAMG_ERR_UNSUPPORTED) { set_error(err); return rc; }
+    if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
   if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
-  if (rc) { set_error(err); return rc; }
+  if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
   rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err);
+  mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_dhandle{d};
   return MAMG_OK;
@@ -415,12 +417,15 @@ int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   G.device = params->device;
   mamg::DevMat dA;
   Seeds S(idofs, n_idofs, v.n, params);
+  mamg::dev_prereserve(params->device, v.nnz(), 1);   // layout memory before the setup churn
   if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err))) {
+    mamg::dev_prereserve_release();
     set_error(err);
     return rc;
   }
   mamg::DeviceHandle* d = nullptr;
   rc = mamg::dev_from_ghier(&G, dA, *params, &d, &err);
+  mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
   return MAMG_OK;
@@ -450,10 +455,12 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
   mamg::GHier G;
   G.device = params->device;
   Seeds S(idofs, n_idofs, M.n, params);
+  mamg::dev_prereserve(params->device, M.nnz, 1);   // layout memory before the setup churn
   int rc = mamg::gpu_setup(M, S.ptr, S.n, *params, &G, &err);
-  if (rc) { set_error(err); return rc; }
+  if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DeviceHandle* d = nullptr;
   rc = mamg::dev_from_ghier(&G, M, *params, &d, &err);
+  mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
   return MAMG_OK;

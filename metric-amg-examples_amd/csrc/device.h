@@ -13,6 +13,8 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
                std::string* err);
 // apply handle from a GPU-setup hierarchy (everything stays in HBM); G's
 // buffers are released level by level as the apply layouts are built
+void dev_prereserve(int device, int64_t nnz, int nranks);
+void dev_prereserve_release();
 int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandle** out,
                    std::string* err);
 // setup phase timings of a handle built by the GPU setup (ms; zeros otherwise)

@@ -828,6 +828,8 @@ struct DeviceHandle {
   bool bsr = false;
   std::vector<DLevel> L;
   std::vector<void*> allocs;
+  char* arena = nullptr;           // pre-reserved HBM, bump-allocated (dev_prereserve)
+  size_t arena_left = 0;
   hipStream_t cap = nullptr;
   std::vector<Graph> graphs;
   double* hr = nullptr;            // host-apply staging (device)
@@ -856,6 +858,13 @@ template <class HT, class T>
 int dalloc(HT* h, T** p, int64_t count, std::string* err) {
   *p = nullptr;
   if (count <= 0) return MAMG_OK;
+  const size_t bytes = ((size_t)count * sizeof(T) + 4095) & ~(size_t)4095;
+  if (h->arena && bytes <= h->arena_left) {
+    *p = (T*)h->arena;
+    h->arena += bytes;
+    h->arena_left -= bytes;
+    return MAMG_OK;
+  }
   void* q = nullptr;
   HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
@@ -2176,10 +2185,46 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   return MAMG_OK;
 }
 
+// HBM reserved before the GPU setup churns memory: the apply layout is then
+// bump-allocated from it (dev_from_ghier / dist_upload adopt it).  Measured at
+// nrefs=6, fresh processes: K kernel 1.47-1.50 ms from the reservation vs
+// 1.61-1.71 ms from hipMallocs made after the setup's alloc/free churn
+// (profiles/r01_bench_prereserve_ab.log).  Bytes per A0
+// entry: MAMG_PRERESERVE_B_PER_NNZ (default 20, ~16.5 used at nrefs=6; 0 = off);
+// a rank of N reserves 1.25 x that / N + 0.5.
+static void* g_pre = nullptr;
+static size_t g_pre_bytes = 0;
+void dev_prereserve(int device, int64_t nnz, int nranks) {
+  const char* e = std::getenv("MAMG_PRERESERVE_B_PER_NNZ");
+  double b = e ? std::atof(e) : 20.0;
+  if (nranks > 1) b = 1.25 * b / nranks + 0.5;
+  dev_prereserve_release();
+  if (b <= 0 || nnz <= 0) return;
+  if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return; }
+  const size_t bytes = ((size_t)(b * (double)nnz) + (1 << 21)) & ~(size_t)((1 << 21) - 1);
+  if (hipMalloc(&g_pre, bytes) == hipSuccess) g_pre_bytes = bytes;
+  else { (void)hipGetLastError(); g_pre = nullptr; }
+}
+void dev_prereserve_release() {
+  if (g_pre) (void)hipFree(g_pre);
+  g_pre = nullptr;
+  g_pre_bytes = 0;
+}
+template <class HT>
+void adopt_prereserve(HT* h) {
+  if (!g_pre) return;
+  h->allocs.push_back(g_pre);
+  h->arena = (char*)g_pre;
+  h->arena_left = g_pre_bytes;
+  g_pre = nullptr;
+  g_pre_bytes = 0;
+}
+
 int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandle** out,
                    std::string* err) {
   const auto t0 = std::chrono::steady_clock::now();
   std::unique_ptr<DeviceHandle> h(new DeviceHandle());
+  adopt_prereserve(h.get());
   h->p = p;
   h->device = p.device;
   HIPCHK(hipSetDevice(p.device));
@@ -2490,6 +2535,8 @@ struct DistHandle {
   ncclComm_t comm = nullptr;
   std::vector<DDLevel> L;
   std::vector<void*> allocs;
+  char* arena = nullptr;
+  size_t arena_left = 0;
   double apply_bytes = 0.0;
   int64_t nv0 = 0, o0 = 0, o1 = 0;
   bool overlap = true;                 // MAMG_OVERLAP: interior rows during the forward halo
@@ -2731,6 +2778,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0);
   if (rc) return rc;
   std::unique_ptr<DistHandle> h(new DistHandle());
+  adopt_prereserve(h.get());
   h->p = p;
   h->rank = rank;
   h->nranks = nranks;
