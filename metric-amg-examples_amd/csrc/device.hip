@@ -1930,6 +1930,7 @@ void launch_sell_x(const Op& o, hipStream_t s) {
       case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
       case 10: launch_sell_u<XFM, SYM, 5, false, TAG>(o, s); return;
       case 12: launch_sell_u<XFM, SYM, 6, false, TAG>(o, s); return;
+      case 13: launch_sell_u<XFM, SYM, 6, true, TAG>(o, s); return;
       case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
       case 17: launch_sell_u<XFM, SYM, 8, true, TAG>(o, s); return;
       case 32: launch_sell_u<XFM, SYM, 16, false, TAG>(o, s); return;
