@@ -278,8 +278,9 @@ __global__ __launch_bounds__(256) void sell2_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
-    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap) {
-  const int64_t node = row_block(remap) * 256 + threadIdx.x;
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap,
+    const int32_t* __restrict__ sched) {
+  const int64_t node = (sched ? (int64_t)sched[blockIdx.x] : row_block(remap)) * 256 + threadIdx.x;
   if (node >= nr) return;
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int len = meta[node] & 0xffff;
@@ -622,6 +623,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_POST_U     SELL blocks per chunk of the K kernel (6 default, 4, 5, 8, 16)
 //   MAMG_SELL_REMAP 1: XCD-contiguous row order for the level-0 SELL kernels
 //   MAMG_POST_REMAP 1: XCD-contiguous row order for the level-0 K (post) kernel
+//   MAMG_POST_BANDS 1: the K kernel walks A0's band schedule (default 0)
 //   MAMG_SELL_MAX_LEN SELL only for matrices with <= this many blocks per row (40)
 //   MAMG_HALF       0: full SELL-64 instead of the half-symmetric ELL-64 for A0 (default 1)
 //   MAMG_HALF_U     blocks per chunk of the half-symmetric kernel (4 default, 8)
@@ -637,6 +639,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 int g_remap = 1;
 int g_sell_remap = 0;
 int g_post_remap = 0;
+int g_post_bands = 0;
 int g_r_lanes = 0;
 int g_a1_lanes = 0;
 int g_half = 1;
@@ -684,6 +687,8 @@ void read_knobs() {
   g_half_remap = su ? std::atoi(su) != 0 : 1;
   su = std::getenv("MAMG_HALF_BANDS");
   g_half_bands = su ? std::atoi(su) : 1;
+  su = std::getenv("MAMG_POST_BANDS");
+  g_post_bands = su ? std::atoi(su) != 0 : 0;
   su = std::getenv("MAMG_POST_REMAP");
   g_post_remap = su ? std::atoi(su) != 0 : 0;
   su = std::getenv("MAMG_SELL_REMAP");
@@ -1612,6 +1617,10 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, g_post_lanes, false, err,
                            g_post_k && g_post_sell)))
       return rc;
+    if (g_post_bands && g_post_k && D.KPb.sell && D.Ab.nsched > 0 && D.KPb.nr == D.Ab.nr) {
+      D.KPb.sched = D.Ab.sched;      // K's rows are A0's rows: walk them in the same bands
+      D.KPb.nsched = D.Ab.nsched;    // (owned by the handle through D.Ab)
+    }
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -1908,7 +1917,8 @@ void launch_sell_u(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 ? (o.epi == EPI_KPOST ? g_post_remap : g_sell_remap) : 0)
+    (TAG == 0 ? (o.epi == EPI_KPOST ? g_post_remap : g_sell_remap) : 0), \
+    ((int64_t)g == M.nsched ? M.sched : nullptr)
   switch (o.epi) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
