@@ -607,6 +607,252 @@ __global__ __launch_bounds__(256) void interleave2_kernel(int64_t n, const doubl
   if (I < n) reinterpret_cast<double2*>(out)[I] = double2{in[I], in[bs + I]};
 }
 
+// node-interleaved pairs -> out (field stride os, or node-interleaved if os == 0)
+__global__ __launch_bounds__(256) void deinterleave2_kernel(int64_t n, const double* __restrict__ in,
+                                                            double* __restrict__ out, int64_t os) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= n) return;
+  const double2 v = reinterpret_cast<const double2*>(in)[I];
+  vset(out, os, I, 0, v.x);
+  vset(out, os, I, 1, v.y);
+}
+
+// ---------------------------------------------------------------------------
+// Multicolour node-block Gauss-Seidel (SMOOTHER_SGS / SMOOTHER_GS): the
+// reference's SGS (src/amg_parameters.py:72) and its level-0 multiplicative
+// Schwarz on the seed blocks (src/utils.py:84) in a parallel order.  The
+// nodes are coloured (jp_round_kernel) so that no two nodes of a colour are
+// adjacent; G = A_l with its node rows permuted colour by colour, so one
+// colour is one contiguous row range [c0, c1) and one launch:
+//   x(I) <- x(I) + D_i (b(I) - (A x)(I)),   I = perm[i],
+// in place (a lane never reads an x(J) another lane of the launch writes).
+// D_i = the unscaled inverse of node I's smoother block (permuted order).
+// Lane groups of VL per row as bsr2_kernel; x node-interleaved; b with field
+// stride bs (the caller's [u1; u2] r on level 0).  Oracle:
+// mamg_oracle.Level.gs_sweep.
+// ---------------------------------------------------------------------------
+template <int VL, bool SYM>
+__global__ __launch_bounds__(256) void gs2_kernel(
+    int64_t c0, int64_t c1, const int32_t* __restrict__ perm, const int64_t* __restrict__ bptr,
+    const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbt,
+    const dv4* __restrict__ D, double* x, const double* __restrict__ b, int64_t bs) {
+  const int lane = threadIdx.x & (VL - 1);
+  const int64_t i = c0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) / VL;
+  const double* offd = SYM ? bval + 2 * nbt : nullptr;
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+  if (i < c1) {
+    const int64_t p0 = bptr[i], p1 = bptr[i + 1];
+    for (int64_t base = p0; base < p1; base += 2 * VL) {
+      const int64_t ka = base + lane, kb = ka + VL;
+      const bool ha = ka < p1, hb = kb < p1;
+      const int64_t la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
+      const int32_t ca = bcol[la], cb = bcol[lb];
+      const dv4 v0 = blk<SYM>(bval, offd, la), v1 = blk<SYM>(bval, offd, lb);
+      const double2 a = x2[ca], e = x2[cb];
+      s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
+      s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
+      t0 += hb ? v1.x * e.x + v1.y * e.y : 0.0;
+      t1 += hb ? v1.z * e.x + v1.w * e.y : 0.0;
+    }
+  }
+  s0 += t0;
+  s1 += t1;
+#pragma unroll
+  for (int off = VL / 2; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off, VL);
+    s1 += __shfl_xor(s1, off, VL);
+  }
+  if (i < c1 && lane == 0) {
+    const int64_t I = perm[i];
+    const double r0 = vget(b, bs, I, 0) - s0, r1 = vget(b, bs, I, 1) - s1;
+    const dv4 d = D[i];
+    const double2 xi = x2[I];
+    reinterpret_cast<double2*>(x)[I] = double2{xi.x + (d.x * r0 + d.y * r1), xi.y + (d.z * r0 + d.w * r1)};
+  }
+}
+
+__device__ __forceinline__ uint32_t hash32_dev(uint64_t i, int level) {   // = host.h hash32
+  uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
+  const uint32_t lv = (uint32_t)(((uint64_t)(int64_t)level * 0x85EBCA77ull) & 0xFFFFFFFFull);
+  x = x * 0x9E3779B1u + lv;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint64_t colour_key(int64_t I, int level) {
+  return ((uint64_t)hash32_dev((uint64_t)I, level + 0x4000) << 32) | (uint64_t)(uint32_t)I;
+}
+
+// one round of the Jones-Plassmann colouring (mamg_oracle.jp_colouring): an
+// uncoloured node whose key beats every uncoloured neighbour's takes the
+// smallest colour no coloured neighbour holds.  Reads the previous round's
+// colours (cin), writes the next (cout): winners of a round are never
+// adjacent, so the result is independent of the visiting order.
+__global__ __launch_bounds__(256) void jp_round_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, int level,
+                                                       const int8_t* __restrict__ cin, int8_t* __restrict__ cout,
+                                                       unsigned long long* nleft, int* toomany) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  const int8_t ci = cin[I];
+  if (ci >= 0) { cout[I] = ci; return; }
+  const uint64_t key = colour_key(I, level);
+  uint64_t nbmax = 0, mask = 0;
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+    const int32_t J = col[k];
+    if (J == I) continue;
+    const int8_t cj = cin[J];
+    if (cj < 0) {
+      const uint64_t kj = colour_key(J, level);
+      nbmax = kj > nbmax ? kj : nbmax;
+    } else {
+      mask |= 1ull << cj;
+    }
+  }
+  if (key > nbmax) {
+    if (~mask == 0ull) { *toomany = 1; cout[I] = 0; }
+    else cout[I] = (int8_t)(__ffsll((long long)~mask) - 1);
+  } else {
+    cout[I] = -1;
+    atomicAdd(nleft, 1ull);
+  }
+}
+
+// the colouring needs an undirected node graph: every block (I, J) must have
+// its mirror (J, I) (binary search in row J)
+__global__ __launch_bounds__(256) void pattern_sym_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ col, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+    const int32_t J = col[k];
+    int64_t lo = ptr[J], hi = ptr[J + 1];
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (col[m] < I) lo = m + 1; else hi = m;
+    }
+    if (lo >= ptr[J + 1] || col[lo] != I) { *bad = 1; return; }
+  }
+}
+
+__global__ __launch_bounds__(256) void colour_count_kernel(int64_t nr, const int8_t* __restrict__ c,
+                                                           int32_t* __restrict__ ci, int64_t* __restrict__ iota,
+                                                           unsigned long long* cnt) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  ci[I] = c[I];
+  iota[I] = I;
+  atomicAdd(cnt + c[I], 1ull);
+}
+
+__global__ __launch_bounds__(256) void perm_len_kernel(int64_t nr, const int64_t* __restrict__ sorted,
+                                                       const int64_t* __restrict__ ptr, int32_t* __restrict__ perm,
+                                                       int64_t* __restrict__ gptr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nr) return;
+  const int64_t I = sorted[i];
+  perm[i] = (int32_t)I;
+  gptr[i + 1] = ptr[I + 1] - ptr[I];
+}
+
+// 2x2 Gauss-Jordan without pivoting in mamg_oracle.batched_inverse's
+// operation order (no contraction), on node I's diagonal block; the
+// off-diagonals are dropped when I's two dofs are separate smoother blocks
+// (W_I diagonal), which gives exactly the two 1x1 inverses
+__device__ dv4 gj2_inverse(double a00, double a01, double a10, double a11, int* bad) {
+#pragma clang fp contract(off)
+  if (!(a00 > 0.0)) { *bad = 1; return dv4{0.0, 0.0, 0.0, 0.0}; }
+  const double p = a00;
+  const double r01 = a01 / p, r02 = 1.0 / p, r03 = 0.0 / p;
+  const double f1 = a10;
+  double m11 = a11 - f1 * r01, m12 = 0.0 - f1 * r02, m13 = 1.0 - f1 * r03;
+  if (!(m11 > 0.0)) { *bad = 1; return dv4{0.0, 0.0, 0.0, 0.0}; }
+  const double q = m11;
+  m12 = m12 / q;
+  m13 = m13 / q;
+  const double f0 = r01;
+  const double n02 = r02 - f0 * m12, n03 = r03 - f0 * m13;
+  return dv4{n02, n03, m12, m13};
+}
+
+__global__ __launch_bounds__(256) void perm_fill_kernel(int64_t nr, const int32_t* __restrict__ perm,
+                                                        const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                        const dv4* __restrict__ val, const dv4* __restrict__ W,
+                                                        const int64_t* __restrict__ gptr, int32_t* __restrict__ gcol,
+                                                        dv4* __restrict__ gval, dv4* __restrict__ Dg, int* bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nr) return;
+  const int64_t I = perm[i];
+  int64_t o = gptr[i];
+  dv4 dg = {0.0, 0.0, 0.0, 0.0};
+  bool has = false;
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k, ++o) {
+    gcol[o] = col[k];
+    gval[o] = val[k];
+    if (col[k] == I) { dg = val[k]; has = true; }
+  }
+  if (!has) { *bad = 1; return; }
+  const dv4 w = W[I];
+  const bool split = w.y == 0.0 && w.z == 0.0;
+  Dg[i] = gj2_inverse(dg.x, split ? 0.0 : dg.y, split ? 0.0 : dg.z, dg.w, bad);
+}
+
+// coarse-grid correction scaling (coarse_scaling ON, src/amg_parameters.py:78):
+// alpha = <b_c, e> / <A_c e, e> (= <r, P e> / <A P e, P e> for A_c = P^T A P),
+// e <- alpha e; alpha = 1 if the denominator is not positive.  Partial sums
+// per block, then every block of the scaling launch reduces the partials in
+// the same fixed order (so all agree on alpha).  Oracle: mamg_oracle.coarse_scale.
+constexpr int SCALE_BLOCKS = 256;
+__global__ __launch_bounds__(256) void dot2_partial_kernel(int64_t n, const double* __restrict__ bc,
+                                                           const double* __restrict__ e,
+                                                           const double* __restrict__ q,
+                                                           double* __restrict__ part) {
+  __shared__ double red[8];
+  double s = 0.0, t = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    s += bc[i] * e[i];
+    t += q[i] * e[i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    t += __shfl_xor(t, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; red[4 + (threadIdx.x >> 6)] = t; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    part[2 * blockIdx.x + 1] = (red[4] + red[5]) + (red[6] + red[7]);
+  }
+}
+
+__global__ __launch_bounds__(256) void cscale_kernel(int64_t n, int nb, const double* __restrict__ part,
+                                                     double* __restrict__ e) {
+  __shared__ double red[8];
+  __shared__ double alpha;
+  double s = 0.0, t = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) { s += part[2 * i]; t += part[2 * i + 1]; }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    t += __shfl_xor(t, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; red[4 + (threadIdx.x >> 6)] = t; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double num = (red[0] + red[1]) + (red[2] + red[3]);
+    const double den = (red[4] + red[5]) + (red[6] + red[7]);
+    alpha = den > 0.0 ? num / den : 1.0;
+  }
+  __syncthreads();
+  const double a = alpha;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) e[i] = a * e[i];
+}
+
 inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 
 // tuning knobs, read at upload (bench/variants.py):
@@ -784,9 +1030,22 @@ struct DLevel {
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr,
          *c = nullptr, *e = nullptr;
+  // multicolour Gauss-Seidel (SMOOTHER_SGS / SMOOTHER_GS, BSR2 layout): A_l's
+  // node rows permuted colour by colour (Gb, lane groups), the node of each
+  // permuted row (gperm), the unscaled smoother-block inverses in that order
+  // (Gd), colour c = permuted rows [gcs[c], gcs[c + 1])
+  DBsr Gb;
+  int32_t* gperm = nullptr;
+  dv4* Gd = nullptr;
+  std::vector<int64_t> gcs, gbk;     // colour row starts / block starts (+ end)
+  // coarse-grid correction scaling of the correction computed ON this level:
+  // q = A_l e, partial sums of <b, e>, <q, e>
+  double* q = nullptr;
+  double* part2 = nullptr;
 };
 
-enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7 };
+enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7,
+              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -812,7 +1071,9 @@ struct Op {
   int64_t xs = 0, bs = 0, os = 0;   // BSR2 field strides (0 = node-major)
   bool xfm = false;
   int remap = 0;                    // XCD-contiguous row order (restriction ops)
-  int64_t r0 = 0, r1 = -1;          // row range [r0, r1) (half-symmetric ops; r1 < 0: all rows)
+  int64_t r0 = 0, r1 = -1;          // row range [r0, r1) (half-symmetric ops, GS colours; r1 < 0: all rows)
+  const int32_t* perm = nullptr;    // GS: node of each permuted row
+  double* part = nullptr;           // DOT2 / CSCALE partial sums
   double bytes = 0.0;
 };
 
@@ -1578,6 +1839,90 @@ struct LevelSrc {
   const double* Ainv = nullptr;   // coarsest: n x n dof order (device)
 };
 
+inline bool gs_smoother(const mamg_params& p) {
+  return p.smoother == MAMG_SMOOTHER_SGS || p.smoother == MAMG_SMOOTHER_GS;
+}
+
+// Multicolour GS layout of one level from A_l's device BSR2 B and the
+// level's (scaled) smoother blocks W (only their pattern is used: a node
+// whose W block is diagonal has two 1x1 smoother blocks).  Colouring:
+// jp_round_kernel rounds (one 8-byte readback each); permutation: stable
+// radix sort of the nodes by colour (ascending node id within a colour);
+// then the permuted BSR2 copy, its block inverses, and the colour ranges.
+template <class HT>
+int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLevel* D, std::string* err) {
+  int rc;
+  const int64_t nr = B.nr;
+  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 64 colours, [2] bad block
+  unsigned long long* left = nullptr;
+  unsigned long long* cnt = nullptr;
+  int8_t *ca = nullptr, *cb = nullptr;
+  if ((rc = T->alloc(&flags, 4, err))) return rc;
+  if ((rc = T->alloc(&left, 1, err))) return rc;
+  if ((rc = T->alloc(&cnt, 64, err))) return rc;
+  if ((rc = T->alloc(&ca, nr, err))) return rc;
+  if ((rc = T->alloc(&cb, nr, err))) return rc;
+  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(hipMemset(cnt, 0, 64 * sizeof(unsigned long long)));
+  pattern_sym_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, flags);
+  HIPCHK(hipGetLastError());
+  int hf[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[0]) { *err = "multicolour GS: node pattern of level " + std::to_string(level) + " not symmetric"; return MAMG_ERR_UNSUPPORTED; }
+  HIPCHK(hipMemset(ca, 0xff, nr));
+  for (int round = 0;; ++round) {
+    unsigned long long nl = 0;
+    HIPCHK(hipMemset(left, 0, sizeof(unsigned long long)));
+    jp_round_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, level, ca, cb, left, flags + 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(&nl, left, sizeof(nl), hipMemcpyDeviceToHost));
+    std::swap(ca, cb);
+    if (nl == 0) break;
+    if (round > 100000) { *err = "multicolour GS: colouring did not finish"; return MAMG_ERR_SETUP; }
+  }
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[1]) { *err = "multicolour GS: more than 64 colours on level " + std::to_string(level); return MAMG_ERR_UNSUPPORTED; }
+  int32_t *ci = nullptr, *cs = nullptr;
+  int64_t *iota = nullptr, *sorted = nullptr;
+  if ((rc = T->alloc(&ci, nr, err))) return rc;
+  if ((rc = T->alloc(&cs, nr, err))) return rc;
+  if ((rc = T->alloc(&iota, nr, err))) return rc;
+  if ((rc = T->alloc(&sorted, nr, err))) return rc;
+  colour_count_kernel<<<nblocks(nr), 256>>>(nr, ca, ci, iota, cnt);
+  HIPCHK(hipGetLastError());
+  if ((rc = dsort_pairs_i32_i64(ci, cs, iota, sorted, nr, 6, nullptr, err))) return rc;
+  unsigned long long hc[64];
+  HIPCHK(hipMemcpy(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost));
+  int ncol = 0;
+  for (int c = 0; c < 64; ++c)
+    if (hc[c]) ncol = c + 1;
+  D->gcs.assign(ncol + 1, 0);
+  for (int c = 0; c < ncol; ++c) D->gcs[c + 1] = D->gcs[c] + (int64_t)hc[c];
+  TBsr G;
+  G.nr = nr; G.nc = B.nc; G.nb = B.nb;
+  if ((rc = T->alloc(&G.ptr, nr + 1, err))) return rc;
+  HIPCHK(hipMemset(G.ptr, 0, sizeof(int64_t)));
+  if ((rc = dalloc(h, &D->gperm, nr, err))) return rc;
+  if ((rc = dalloc(h, &D->Gd, nr, err))) return rc;
+  perm_len_kernel<<<nblocks(nr), 256>>>(nr, sorted, B.ptr, D->gperm, G.ptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(G.ptr, G.ptr, nr + 1, nullptr, err))) return rc;
+  if ((rc = T->alloc(&G.col, G.nb, err))) return rc;
+  if ((rc = T->alloc(&G.val, G.nb, err))) return rc;
+  perm_fill_kernel<<<nblocks(nr), 256>>>(nr, D->gperm, B.ptr, B.col, B.val, reinterpret_cast<const dv4*>(W),
+                                         G.ptr, G.col, G.val, D->Gd, flags + 2);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[2]) { *err = "multicolour GS: a smoother block is missing or not SPD on level " + std::to_string(level); return MAMG_ERR_SETUP; }
+  D->gbk.assign(ncol + 1, 0);
+  for (int c = 0; c <= ncol; ++c) HIPCHK(hipMemcpy(&D->gbk[c], G.ptr + D->gcs[c], sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = finalize_bsr(h, T, G, &D->Gb, 0, true, err, false))) return rc;
+  for (void* q : {(void*)ca, (void*)cb, (void*)ci, (void*)cs, (void*)iota, (void*)sorted, (void*)G.ptr, (void*)G.col,
+                  (void*)G.val})
+    T->release(q);
+  return MAMG_OK;
+}
+
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
   DLevel& D = h->L[l];
   const mamg_params& p = h->p;
@@ -1598,9 +1943,11 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = finalize_bsr(h, &T, B, &D.Ab, l == 1 && g_a1_lanes ? g_a1_lanes : lanesA, true, err, true,
                            l == 0)))
       return rc;
+    if (gs_smoother(p))
+      if ((rc = build_gs(h, &T, B, S.W, l, &D, err))) return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
-  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n) {
+  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p)) {
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
@@ -1718,6 +2065,8 @@ Op axpy_op(int64_t n, const double* e, double* x) {
   return o;
 }
 
+void scale_ops(const DeviceHandle* h, int lc, std::vector<Op>* ops);
+
 // ---- CSR layout: cycle from zero initial guess: xout = MG_l(b) --------------
 void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
   const DLevel& L = h->L[l];
@@ -1756,6 +2105,7 @@ void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, 
     cycle_ops_csr(h, l + 1, C.c, C.e, ops);
     ops->push_back(axpy_op(C.n, C.e, C.x));
   }
+  if (p.coarse_scaling) scale_ops(h, l + 1, ops);
   ops->push_back(csr_op(L.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, X, nullptr, nullptr, X));
   for (int s = 0; s < p.postsmooth_iter; ++s) {
     double* out = (s == p.postsmooth_iter - 1) ? xout : X2;
@@ -1771,6 +2121,45 @@ void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, 
 
 // ---- BSR2 layout.  b / xout of level 0 are the caller's field-major vectors
 // (stride nv0); all other vectors are node-interleaved (stride 0).
+// one multicolour GS sweep (colours ascending if fwd, else descending) in place on x
+Op gs_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int cls) {
+  Op o;
+  o.kind = OP_GS; o.cls = cls; o.Mb = &L.Gb; o.perm = L.gperm; o.W = L.Gd;
+  o.x = x; o.out = x; o.b = b; o.bs = bs;
+  o.r0 = L.gcs[c]; o.r1 = L.gcs[c + 1]; o.n = o.r1 - o.r0;
+  const double rows = (double)o.n, ncol = (double)(L.gcs.size() - 1);
+  // blocks + pointers + perm + D + b + own x read/write + the gathered x
+  // (every node's pair once per sweep, spread over the colours)
+  o.bytes = (L.Gb.sym ? 28.0 : 36.0) * (double)(L.gbk[c + 1] - L.gbk[c]) + 8.0 * (rows + 1) + 4.0 * rows +
+            32.0 * rows + 16.0 * rows + 32.0 * rows + 16.0 * (double)L.Gb.nc / ncol;
+  return o;
+}
+
+void gs_sweep_ops(const DLevel& L, bool fwd, double* x, const double* b, int64_t bs, int cls, std::vector<Op>* ops) {
+  const int nc = (int)L.gcs.size() - 1;
+  for (int k = 0; k < nc; ++k) {
+    const int c = fwd ? k : nc - 1 - k;
+    if (L.gcs[c + 1] > L.gcs[c]) ops->push_back(gs_op(L, c, x, b, bs, cls));
+  }
+}
+
+// coarse-grid correction scaling of level lc's correction e = C.x against its
+// right-hand side C.b: q = A_c e, then alpha and e <- alpha e
+void scale_ops(const DeviceHandle* h, int lc, std::vector<Op>* ops) {
+  const DLevel& C = h->L[lc];
+  if (h->bsr) ops->push_back(bsr_op(C.Ab, EPI_Y, C_MISC, 1, C.x, 0, nullptr, nullptr, 0, nullptr, C.q, 0));
+  else ops->push_back(csr_op(C.A, EPI_Y, C_MISC, 1, C.x, nullptr, nullptr, nullptr, C.q));
+  Op d;
+  d.kind = OP_DOT2; d.cls = C_MISC; d.n = C.n; d.b = C.b; d.x = C.x; d.y = C.q; d.part = C.part2;
+  d.bytes = 24.0 * C.n;
+  ops->push_back(d);
+  Op sc;
+  sc.kind = OP_CSCALE; sc.cls = C_MISC; sc.n = C.n; sc.part = C.part2; sc.out = C.x; sc.bytes = 16.0 * C.n;
+  ops->push_back(sc);
+}
+
+// ---- BSR2 layout.  b / xout of level 0 are the caller's field-major vectors
+// (stride nv0); all other vectors are node-interleaved (stride 0).
 void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
                    int64_t os, std::vector<Op>* ops) {
   const DLevel& L = h->L[l];
@@ -1782,17 +2171,27 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   const int tagA = l0 ? 0 : 1;
   const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
   const int clsW = l0 ? C_L0_WB : C_COARSE;
-  double* X = L.t;
+  const bool gs = L.gcs.size() > 1;                       // multicolour GS on this level
+  const bool sgs = p.smoother == MAMG_SMOOTHER_SGS;
+  double* X = (gs && os == 0) ? xout : L.t;               // GS sweeps in place
   double* X2 = L.t2;
-  {   // first sweep from x = 0: X = W b
+  if (gs) {   // pre: from x = 0, forward (SGS: then backward) sweeps
+    Op z;
+    z.kind = OP_ZERO; z.cls = clsW; z.n = L.n; z.out = X; z.bytes = 8.0 * L.n;
+    ops->push_back(z);
+    for (int s = 0; s < p.presmooth_iter; ++s) {
+      gs_sweep_ops(L, true, X, b, bs, clsS, ops);
+      if (sgs) gs_sweep_ops(L, false, X, b, bs, clsS, ops);
+    }
+  } else {    // first sweep from x = 0: X = W b
     Op o;
     o.kind = OP_BD; o.cls = clsW; o.n = nv; o.W = L.Wd; o.b = b; o.bs = bs; o.out = X;
     o.bytes = 32.0 * nv + 16.0 * nv + 16.0 * nv;
     ops->push_back(o);
-  }
-  for (int s = 1; s < p.presmooth_iter; ++s) {
-    ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, X2, 0));
-    std::swap(X, X2);
+    for (int s = 1; s < p.presmooth_iter; ++s) {
+      ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, X2, 0));
+      std::swap(X, X2);
+    }
   }
   ops->push_back(bsr_op(L.Ab, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs,
                         nullptr, L.r, 0));
@@ -1804,6 +2203,21 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     ops->push_back(bsr_op(C.Ab, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0));
     cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops);
     ops->push_back(axpy_op(C.n, C.e, C.x));
+  }
+  if (p.coarse_scaling) scale_ops(h, l + 1, ops);
+  if (gs) {   // prolongate, then backward (SGS: forward then backward) sweeps
+    ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0, nullptr, X, 0));
+    for (int s = 0; s < p.postsmooth_iter; ++s) {
+      if (sgs) gs_sweep_ops(L, true, X, b, bs, clsS, ops);
+      gs_sweep_ops(L, false, X, b, bs, clsS, ops);
+    }
+    if (X != xout) {
+      Op o;
+      o.kind = OP_ILV; o.epi = 1; o.cls = clsW; o.n = nv; o.b = X; o.out = xout; o.os = os;
+      o.bytes = 32.0 * nv;
+      ops->push_back(o);
+    }
+    return;
   }
   int s0 = 0;
   if (L.KPb.nr > 0 && p.postsmooth_iter >= 1) {   // z = x1 + W r1 + K e (one operator)
@@ -2049,6 +2463,27 @@ void launch_bsr_tag(const Op& o, hipStream_t s) {
   }
 }
 
+template <int VL>
+void launch_gs_vl(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const unsigned g = nblocks(o.n * (int64_t)VL);
+  if (M.sym)
+    gs2_kernel<VL, true><<<g, 256, 0, s>>>(o.r0, o.r1, o.perm, M.ptr, M.col, M.val, M.nb, o.W, o.out, o.b, o.bs);
+  else
+    gs2_kernel<VL, false><<<g, 256, 0, s>>>(o.r0, o.r1, o.perm, M.ptr, M.col, M.val, M.nb, o.W, o.out, o.b, o.bs);
+}
+
+void launch_gs(const Op& o, hipStream_t s) {
+  switch (o.Mb->lanes) {
+    case 2: launch_gs_vl<2>(o, s); break;
+    case 4: launch_gs_vl<4>(o, s); break;
+    case 8: launch_gs_vl<8>(o, s); break;
+    case 16: launch_gs_vl<16>(o, s); break;
+    case 32: launch_gs_vl<32>(o, s); break;
+    default: launch_gs_vl<64>(o, s); break;
+  }
+}
+
 void launch(const Op& o, hipStream_t s) {
   switch (o.kind) {
     case OP_CSR:
@@ -2073,7 +2508,20 @@ void launch(const Op& o, hipStream_t s) {
       if (o.n) gemv_kernel<<<(unsigned)((o.n + 3) / 4), 256, 0, s>>>(o.n, o.w, o.x, o.out);
       break;
     case OP_ILV:
-      if (o.n) interleave2_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.b, o.bs, o.out);
+      if (o.n && o.epi == 1) deinterleave2_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.b, o.out, o.os);
+      else if (o.n) interleave2_kernel<<<nblocks(o.n), 256, 0, s>>>(o.n, o.b, o.bs, o.out);
+      break;
+    case OP_GS:
+      if (o.n > 0) launch_gs(o, s);
+      break;
+    case OP_ZERO:
+      if (o.n) (void)hipMemsetAsync(o.out, 0, o.n * sizeof(double), s);
+      break;
+    case OP_DOT2:
+      if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
+      break;
+    case OP_CSCALE:
+      if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
       break;
   }
 }
@@ -2132,6 +2580,10 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   h->L.resize(nl);
   h->bsr = bsr_eligible(H, A0, p);
   read_knobs();
+  if (gs_smoother(p) && !h->bsr) {
+    *err = "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned smoother blocks)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   int rc;
   for (int l = 0; l < nl; ++l) {
     const HostLevel& hl = H.levels[l];
@@ -2183,6 +2635,10 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
     double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
     for (double** v : vecs)
       if ((rc = dalloc(h.get(), v, D.n, err))) return rc;
+    if (p.coarse_scaling) {
+      if ((rc = dalloc(h.get(), &D.q, D.n, err))) return rc;
+      if ((rc = dalloc(h.get(), &D.part2, 2 * SCALE_BLOCKS, err))) return rc;
+    }
   }
   const int64_t n0 = h->L[0].n;
   double** v0[] = {&h->hr, &h->hz};
@@ -2285,6 +2741,10 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
     double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
     for (double** v : vecs)
       if ((rc = dalloc(h.get(), v, D.n, err))) return rc;
+    if (p.coarse_scaling) {
+      if ((rc = dalloc(h.get(), &D.q, D.n, err))) return rc;
+      if ((rc = dalloc(h.get(), &D.part2, 2 * SCALE_BLOCKS, err))) return rc;
+    }
   }
   const int64_t n0 = h->L[0].n;
   double** v0[] = {&h->hr, &h->hz};
@@ -2782,6 +3242,10 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
                 const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err) {
   if (p.cycle_type != MAMG_V_CYCLE || p.maxit != 1 || p.presmooth_iter != 1 || p.postsmooth_iter != 1) {
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  if (gs_smoother(p) || p.coarse_scaling) {
+    *err = "multi-GPU apply supports the block-Jacobi smoothers without coarse scaling";
     return MAMG_ERR_UNSUPPORTED;
   }
   read_knobs();

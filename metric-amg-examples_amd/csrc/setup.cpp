@@ -663,12 +663,18 @@ int check_params(const mamg_params& p, std::string* err) {
   if (p.abi_version != MAMG_ABI_VERSION) { *err = "mamg_params.abi_version mismatch"; return MAMG_ERR_ARG; }
   if (p.AMG_type != MAMG_SA_AMG && p.AMG_type != MAMG_UA_AMG) { *err = "AMG_type must be SA_AMG or UA_AMG"; return MAMG_ERR_UNSUPPORTED; }
   if (p.cycle_type != MAMG_V_CYCLE && p.cycle_type != MAMG_W_CYCLE) { *err = "cycle_type must be V_CYCLE or W_CYCLE (AMLI/NL_AMLI/ADD not implemented)"; return MAMG_ERR_UNSUPPORTED; }
-  if (p.smoother != MAMG_SMOOTHER_JACOBI && p.smoother != MAMG_SMOOTHER_L1DIAG && p.smoother != MAMG_SMOOTHER_JACOBI_RHO) {
-    *err = "smoother must be SMOOTHER_JACOBI, SMOOTHER_L1DIAG or SMOOTHER_JACOBI_RHO (sequential GS/SGS are not reproducible on the GPU)";
+  if (p.smoother != MAMG_SMOOTHER_JACOBI && p.smoother != MAMG_SMOOTHER_L1DIAG && p.smoother != MAMG_SMOOTHER_JACOBI_RHO &&
+      p.smoother != MAMG_SMOOTHER_GS && p.smoother != MAMG_SMOOTHER_SGS) {
+    *err = "smoother must be SMOOTHER_JACOBI, SMOOTHER_L1DIAG, SMOOTHER_JACOBI_RHO, SMOOTHER_GS or SMOOTHER_SGS";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  if ((p.smoother == MAMG_SMOOTHER_GS || p.smoother == MAMG_SMOOTHER_SGS) &&
+      (p.num_functions != 2 || !p.node_block_smoother)) {
+    *err = "multicolour GS/SGS smoothers are node-block smoothers: num_functions 2 and node_block_smoother 1";
     return MAMG_ERR_UNSUPPORTED;
   }
   if (p.aggregation_type != MAMG_MIS) { *err = "aggregation_type must be MIS (deterministic parallel MIS-2); VMB/HEM/HEC/MWM not implemented"; return MAMG_ERR_UNSUPPORTED; }
-  if (p.coarse_scaling != MAMG_OFF) { *err = "coarse_scaling ON not supported (it makes the cycle non-linear)"; return MAMG_ERR_UNSUPPORTED; }
+  if (p.coarse_scaling != MAMG_OFF && p.coarse_scaling != MAMG_ON) { *err = "coarse_scaling must be OFF or ON"; return MAMG_ERR_ARG; }
   if (p.coarse_solver != MAMG_COARSE_DENSE) { *err = "coarse_solver must be 32 (direct)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels > 1) { *err = "Schwarz_levels > 1 not supported (seeds exist on level 0 only)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels == 1 && p.Schwarz_type != MAMG_SCHWARZ_BLOCK_JACOBI) {

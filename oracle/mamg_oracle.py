@@ -224,6 +224,8 @@ class Params:
     num_functions: int = 1        # >1: nodal aggregation over field-major dofs
     node_block_smoother: int = 1  # nodal: node-block Jacobi where no seed blocks
     sa_block_diag: int = 1        # nodal: smooth P with node-block D^-1
+    coarse_scaling: int = 0       # 1: e <- alpha e, alpha = <b_c, e> / <A_c e, e>
+
 
 
 def _rowsum_seq(A: sp.csr_matrix, x: np.ndarray) -> np.ndarray:
@@ -588,6 +590,98 @@ def block_smoother(A: sp.csr_matrix, seeds, p: Params, blocks=None) -> sp.csr_ma
     return W, bid, nb
 
 
+# --------------------------------------------------------------------------
+# multicolour node-block Gauss-Seidel (the reference's SGS smoother,
+# src/amg_parameters.py:72, and its level-0 multiplicative Schwarz on the seed
+# blocks, src/utils.py:84 / amg_parameters.py:83-86, in a GPU-parallel order)
+# --------------------------------------------------------------------------
+GS_MAX_COLOURS = 64
+
+
+def node_pattern(A: sp.csr_matrix, nf: int) -> sp.csr_matrix:
+    """Node graph of a field-major dof matrix: block (I, J) present iff any
+    entry of rows f*nv+I lies in columns g*nv+J; diagonal excluded.  Raises if
+    the pattern is not symmetric (the colouring needs an undirected graph)."""
+    n = A.shape[0]
+    nv = n // nf
+    r = np.repeat(np.arange(n), np.diff(A.indptr)) % nv
+    c = A.indices % nv
+    m = r != c
+    G = sp.csr_matrix((np.ones(int(m.sum()), np.int8), (r[m], c[m])), shape=(nv, nv))
+    G.sum_duplicates()
+    G.data[:] = 1
+    G.sort_indices()
+    if (G != G.T).nnz:
+        raise RuntimeError('node pattern not symmetric: multicolour GS unsupported')
+    return G
+
+
+def colour_key(nv: int, level: int) -> np.ndarray:
+    """priority of node I: hash32(I, level + 0x4000) in the high word, I in
+    the low word (unique)."""
+    I = np.arange(nv, dtype=np.uint64)
+    return (hash32(np.arange(nv), level + 0x4000).astype(np.uint64) << np.uint64(32)) | I
+
+
+def jp_colouring(G: sp.csr_matrix, level: int) -> np.ndarray:
+    """Round-synchronous Jones-Plassmann colouring.  Per round every
+    uncoloured node whose key exceeds the keys of all its uncoloured
+    neighbours takes the smallest colour held by none of its (previously)
+    coloured neighbours.  Winners of one round are never adjacent, so the
+    result does not depend on the order nodes are visited (the GPU kernel
+    runs the same rounds).  Returns int32 colour per node."""
+    nv = G.shape[0]
+    key = colour_key(nv, level)
+    col = np.full(nv, -1, np.int64)
+    ip, ix = G.indptr, G.indices
+    rr = np.repeat(np.arange(nv), np.diff(ip))
+    rounds = 0
+    while (col < 0).any():
+        unc = col < 0
+        kk = np.where(unc, key, np.uint64(0))
+        nbmax = np.zeros(nv, np.uint64)
+        if len(ix):
+            nz = np.flatnonzero(np.diff(ip) > 0)
+            nbmax[nz] = np.maximum.reduceat(kk[ix], ip[nz])
+        win = unc & (key > nbmax)
+        bits = np.where(col[ix] >= 0, np.left_shift(np.uint64(1), np.maximum(col[ix], 0).astype(np.uint64)),
+                        np.uint64(0))
+        mask = np.zeros(nv, np.uint64)
+        if len(ix):
+            mask[nz] = np.bitwise_or.reduceat(bits, ip[nz])
+        w = np.flatnonzero(win)
+        m = mask[w]
+        if np.any(m == np.uint64(0xFFFFFFFFFFFFFFFF)):
+            raise RuntimeError('more than %d colours' % GS_MAX_COLOURS)
+        free = (~m) & (m + np.uint64(1))            # lowest zero bit
+        c = np.zeros(len(w), np.int64)
+        for b in range(GS_MAX_COLOURS):
+            c[free == (np.uint64(1) << np.uint64(b))] = b
+        col[w] = c
+        rounds += 1
+    return col.astype(np.int32)
+
+
+def node_block_inverse(A: sp.csr_matrix, bid: np.ndarray, nb: int, nf: int = 2) -> np.ndarray:
+    """Unscaled inverse of the smoother blocks as one nf x nf block per node
+    (nv, nf, nf); blocks must be node-aligned (both dofs of a node in one
+    block, or each alone).  Same Gauss-Jordan as block_inverse_csr."""
+    n = A.shape[0]
+    nv = n // nf
+    Dinv = block_inverse_csr(A, bid, nb)
+    out = np.zeros((nv, nf, nf))
+    for f in range(nf):
+        for g in range(nf):
+            rows = f * nv + np.arange(nv)
+            cols = g * nv + np.arange(nv)
+            out[:, f, g] = np.asarray(Dinv[rows, cols]).ravel()
+    same = np.all([bid[f * nv:(f + 1) * nv] == bid[:nv] for f in range(nf)], axis=0)
+    sizes = np.bincount(bid, minlength=nb)
+    if not np.all(same | (sizes[bid[:nv]] == 1)):
+        raise RuntimeError('smoother blocks not node-aligned: multicolour GS unsupported')
+    return out
+
+
 @dataclasses.dataclass
 class Level:
     A: sp.csr_matrix
@@ -600,9 +694,29 @@ class Level:
     w_sa: float = 0.0
     Ainv: np.ndarray = None
     bid: np.ndarray = None
+    colour: np.ndarray = None        # multicolour GS: colour per node
+    ncolours: int = 0
+    Dn: np.ndarray = None            # multicolour GS: (nv, 2, 2) block inverses
+    crows: list = None               # node ids of each colour (ascending)
 
     def smooth_apply(self, r):
         return self.WB @ r if self.WB is not None else self.winv * r
+
+    def gs_sweep(self, x, b, forward=True):
+        """x <- x + D_I^-1 (b - A x)_I for the nodes I of each colour in turn
+        (colours ascending if forward, else descending); nodes of one colour
+        are never adjacent, so each colour step is one parallel update."""
+        nv = self.A.shape[0] // 2
+        order = range(self.ncolours) if forward else range(self.ncolours - 1, -1, -1)
+        for c in order:
+            I = self.crows[c]
+            rows = np.concatenate([I, nv + I])
+            res = b[rows] - self.A[rows] @ x
+            r0, r1 = res[:len(I)], res[len(I):]
+            D = self.Dn[I]
+            x[I] = x[I] + (D[:, 0, 0] * r0 + D[:, 0, 1] * r1)
+            x[nv + I] = x[nv + I] + (D[:, 1, 0] * r0 + D[:, 1, 1] * r1)
+        return x
 
 
 class Hierarchy:
@@ -619,17 +733,33 @@ class Hierarchy:
         if lev.Ainv is not None:
             return lev.Ainv @ b
         A = lev.A
-        x = lev.smooth_apply(b)                      # first sweep from x = 0
-        for _ in range(p.presmooth_iter - 1):
-            x = x + lev.smooth_apply(b - A @ x)
+        gs = lev.colour is not None
+        if gs:                                       # SGS: forward + backward; GS: forward
+            x = np.zeros_like(b)
+            for _ in range(p.presmooth_iter):
+                x = lev.gs_sweep(x, b, True)
+                if p.smoother == 'SGS':
+                    x = lev.gs_sweep(x, b, False)
+        else:
+            x = lev.smooth_apply(b)                  # first sweep from x = 0
+            for _ in range(p.presmooth_iter - 1):
+                x = x + lev.smooth_apply(b - A @ x)
         r = b - A @ x
         bc = lev.R @ r
+        C = self.levels[l + 1]
         e = self.cycle(l + 1, bc)
-        if p.cycle_type == 'W' and self.levels[l + 1].Ainv is None:
-            e = e + self.cycle(l + 1, bc - self.levels[l + 1].A @ e)
+        if p.cycle_type == 'W' and C.Ainv is None:
+            e = e + self.cycle(l + 1, bc - C.A @ e)
+        if p.coarse_scaling:                         # src/amg_parameters.py:78
+            e = coarse_scale(C.A, bc, e)
         x = x + lev.P @ e
         for _ in range(p.postsmooth_iter):
-            x = x + lev.smooth_apply(b - A @ x)
+            if gs:                                   # SGS: forward + backward; GS: backward
+                if p.smoother == 'SGS':
+                    x = lev.gs_sweep(x, b, True)
+                x = lev.gs_sweep(x, b, False)
+            else:
+                x = x + lev.smooth_apply(b - A @ x)
         return x
 
     def apply(self, r: np.ndarray) -> np.ndarray:
@@ -646,6 +776,18 @@ class Hierarchy:
     def info(self):
         return [(lv.A.shape[0], lv.A.nnz, 0 if lv.P is None else lv.P.nnz)
                 for lv in self.levels]
+
+
+def coarse_scale(Ac, bc, e):
+    """Coarse-grid correction scaling (HAZmath `coarse_scaling: ON`,
+    src/amg_parameters.py:78): the fine correction P e is scaled by
+    alpha = <r, P e> / <A P e, P e>.  With R = P^T and A_c = R A P (Galerkin)
+    this is <b_c, e> / <A_c e, e>, computed on the coarse level; alpha = 1 if
+    the denominator is not positive."""
+    q = Ac @ e
+    den = float(np.dot(e, q))
+    alpha = float(np.dot(bc, e)) / den if den > 0 else 1.0
+    return alpha * e
 
 
 def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarchy:
@@ -674,12 +816,21 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
                 raise RuntimeError('coarsest level %d too large for dense solve' % n)
             lev.Ainv = dense_inverse(cur.toarray())
             break
+        gs = p.smoother in ('SGS', 'GS')
+        if gs and (nf != 2 or not p.node_block_smoother):
+            raise ValueError('multicolour GS needs num_functions = 2 and node-block smoothers')
+        pj = dataclasses.replace(p, smoother='JACOBI_RHO') if gs else p
         if l < p.Schwarz_levels and idofs is not None and l == 0:
-            lev.WB, lev.bid, _ = block_smoother(cur, idofs, p)
+            lev.WB, lev.bid, nbk = block_smoother(cur, idofs, pj)
         elif nf > 1 and p.node_block_smoother:
-            lev.WB, lev.bid, _ = block_smoother(cur, None, p, node_blocks(n, nf))
+            lev.WB, lev.bid, nbk = block_smoother(cur, None, pj, node_blocks(n, nf))
         else:
             lev.winv = smoother_weights(cur, p)
+        if gs:
+            lev.Dn = node_block_inverse(cur, lev.bid, nbk)
+            lev.colour = jp_colouring(node_pattern(cur, 2), l)
+            lev.ncolours = int(lev.colour.max()) + 1 if len(lev.colour) else 0
+            lev.crows = [np.flatnonzero(lev.colour == c) for c in range(lev.ncolours)]
         lev.agg, lev.nagg = agg, nagg
         T = tentative_nodal(agg, nagg, nf) if nf > 1 else tentative(agg, nagg)
         if p.AMG_type == 'SA':

@@ -162,3 +162,65 @@ def test_pcg_amg_gamma_robust():
         res = mo.pcg(s['A'], h, mo.seeded_rhs(s['A'].shape[0]), 1e-8, 500)
         its.append(res.niters)
     assert max(its) < 60, its
+
+
+# ---- multicolour GS / coarse scaling (round 2) ------------------------------
+@pytest.mark.parametrize('dim,n', [(2, 16), (3, 8)])
+def test_jp_colouring_is_proper_and_deterministic(dim, n):
+    s = mo.bidomain_system(dim, n, 1e4)
+    G = mo.node_pattern(s['A'], 2)
+    c = mo.jp_colouring(G, 0)
+    r = np.repeat(np.arange(G.shape[0]), np.diff(G.indptr))
+    assert np.all(c[r] != c[G.indices])                 # no edge inside a colour
+    assert np.array_equal(c, mo.jp_colouring(G, 0))
+    assert c.min() == 0 and c.max() < mo.GS_MAX_COLOURS
+    # every node with colour k > 0 has a neighbour of each smaller colour (greedy)
+    for I in np.flatnonzero(c > 0)[:200]:
+        nb = set(c[G.indices[G.indptr[I]:G.indptr[I + 1]]])
+        assert set(range(c[I])) <= nb
+
+
+def test_sgs_cycle_symmetric_and_stronger():
+    s = mo.bidomain_system(3, 8, 1e6)
+    A = s['A']
+    h = mo.setup(A, mo.Params(num_functions=2, smoother='SGS'), idofs=s['idofs'])
+    r1, r2 = mo.seeded_rhs(A.shape[0], 1), mo.seeded_rhs(A.shape[0], 2)
+    a, b = r2 @ h(r1), r1 @ h(r2)
+    assert abs(a - b) < 1e-12 * abs(a)
+    hj = mo.setup(A, mo.Params(num_functions=2), idofs=s['idofs'])
+    b0 = mo.seeded_rhs(A.shape[0])
+    assert mo.pcg(A, h, b0).niters < mo.pcg(A, hj, b0).niters
+
+
+def test_gs_sweep_equals_sequential_block_gs_in_colour_order():
+    """One forward colour sweep = sequential node-block Gauss-Seidel over the
+    nodes sorted by (colour, index)."""
+    s = mo.bidomain_system(2, 8, 1e2)
+    A = s['A']
+    h = mo.setup(A, mo.Params(num_functions=2, smoother='GS'), idofs=s['idofs'])
+    lev = h.levels[0]
+    nv = A.shape[0] // 2
+    b = mo.seeded_rhs(A.shape[0])
+    x = lev.gs_sweep(np.zeros_like(b), b.copy(), True)
+    y = np.zeros_like(b)
+    Ad = A.toarray()
+    for I in np.lexsort((np.arange(nv), lev.colour)):
+        rows = [I, nv + I]
+        res = b[rows] - Ad[rows] @ y
+        y[rows] += lev.Dn[I] @ res
+    assert np.allclose(x, y, rtol=1e-13, atol=1e-13)
+
+
+def test_coarse_scale_equals_fine_formula():
+    """alpha on the coarse level = <r, P e> / <A P e, P e> on the fine level."""
+    s = mo.bidomain_system(2, 16, 1e3)
+    A = s['A']
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s['idofs'])
+    lev, C = h.levels[0], h.levels[1]
+    r = mo.seeded_rhs(A.shape[0])
+    bc = lev.R @ r
+    e = np.random.default_rng(5).standard_normal(C.A.shape[0])
+    Pe = lev.P @ e
+    alpha_f = (r @ Pe) / (Pe @ (A @ Pe))
+    es = mo.coarse_scale(C.A, bc, e)
+    assert np.allclose(es, alpha_f * e, rtol=1e-10)
