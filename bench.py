@@ -65,9 +65,15 @@ def main():
                     help='also run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL)')
     ap.add_argument('--setup', choices=('gpu', 'host'), default='gpu',
                     help='N = 1 hierarchy construction: GPU setup (default) or host setup + upload')
+    ap.add_argument('--smoother', choices=('jacobi', 'sgs', 'gs'), default='jacobi',
+                    help='level smoother: node-block Jacobi (mi355x_sa_v) or multicolour node-block SGS / GS')
+    ap.add_argument('--scaling', type=int, default=0, help='coarse-grid correction scaling (coarse_scaling ON)')
+    ap.add_argument('--cycle', choices=('V', 'W'), default='V')
     ap.add_argument('--compare-host-setup', action='store_true',
                     help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
+    prof = dict(smoother={'jacobi': 3, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
+                cycle_type={'V': 1, 'W': 2}[args.cycle])
 
     import torch
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -114,7 +120,7 @@ def main():
     if world == 1:
         if args.setup == 'host':
             t0 = time.time()
-            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, **prof)
             t_setup = time.time() - t0
             t0 = time.time()
             B = M.MetricAMG.from_host(H, sysm.W)
@@ -125,7 +131,7 @@ def main():
             # built by gfx950 kernels (bitwise equal to the host setup)
             torch.cuda.synchronize(dev)
             t0 = time.time()
-            B = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu')
+            B = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu', **prof)
             t_setup = time.time() - t0
             setup_info = {'path': 'gpu', 'wall_s': round(t_setup, 3), 'phases_ms': B.setup_timings}
             if args.compare_host_setup:
@@ -189,10 +195,13 @@ def main():
     if args.pcg and world == 1:
         B._Aop = sysm
         solver = M.ConjGrad(sysm, precond=B, tolerance=1e-8, maxiter=500)
+        torch.cuda.synchronize(dev)
         t0 = time.time()
         solver * r_full
+        torch.cuda.synchronize(dev)
+        tp = time.time() - t0
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
-               'seconds': round(time.time() - t0, 3)}
+               'seconds': round(tp, 4), 'setup_plus_pcg_s': round(tp + t_setup, 4)}
     elif args.pcg:
         solver = M.DistConjGrad.for_handles(B, stream=stream, tolerance=1e-8, maxiter=500)
         barrier()

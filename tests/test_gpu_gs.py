@@ -108,3 +108,4 @@ def test_sgs_symmetric_and_deterministic(lib_built):
     c = float(torch.dot(r1, z2))
     assert abs(a - c) <= 1e-12 * abs(a)
     assert torch.equal(z1, z1b)
+
