@@ -49,6 +49,22 @@ def breakdown_dict(kms, cbytes, ms_all):
     return out
 
 
+def device_src_sha():
+    import hashlib
+    with open(os.path.join(ROOT, 'metric-amg-examples_amd', 'csrc', 'device.hip'), 'rb') as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -61,8 +77,14 @@ def main():
                     help='multi-GPU: replicate levels with <= this many nodes')
     ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
-    ap.add_argument('--pcg', action='store_true',
-                    help='also run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL)')
+    ap.add_argument('--pcg', type=int, default=-1,
+                    help='run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL); '
+                         'default: on for N = 1, off for N > 1')
+    ap.add_argument('--cpu-pcg', type=int, default=1,
+                    help='N = 1: also run the CPU PCG (oracle C cycle + SpMV, host cores) on the same '
+                         'hierarchy and report its iteration count next to the GPU one')
+    ap.add_argument('--compare-profiles', type=int, default=1,
+                    help='N = 1: also set up and solve with the multicolour-SGS profile (iterations, seconds)')
     ap.add_argument('--setup', choices=('gpu', 'host'), default='gpu',
                     help='N = 1 hierarchy construction: GPU setup (default) or host setup + upload')
     ap.add_argument('--smoother', choices=('jacobi', 'sgs', 'gs'), default='jacobi',
@@ -72,6 +94,8 @@ def main():
     ap.add_argument('--compare-host-setup', action='store_true',
                     help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
+    if args.pcg < 0:
+        args.pcg = 1 if int(os.environ.get('WORLD_SIZE', '1')) == 1 else 0
     prof = dict(smoother={'jacobi': 3, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
                 cycle_type={'V': 1, 'W': 2}[args.cycle])
 
@@ -192,6 +216,7 @@ def main():
         breakdown = breakdown_dict(kms_all, cbytes, ms_all)
 
     pcg = None
+    gpu_res = None
     if args.pcg and world == 1:
         B._Aop = sysm
         solver = M.ConjGrad(sysm, precond=B, tolerance=1e-8, maxiter=500)
@@ -200,8 +225,12 @@ def main():
         solver * r_full
         torch.cuda.synchronize(dev)
         tp = time.time() - t0
+        gpu_res = list(solver.residuals)
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
-               'seconds': round(tp, 4), 'setup_plus_pcg_s': round(tp + t_setup, 4)}
+               'seconds': round(tp, 4), 'setup_s': round(t_setup, 4),
+               'setup_plus_pcg_s': round(tp + t_setup, 4),
+               'note': 'cbc.block ConjGrad, tolerance 1e-8 absolute on sqrt(<r,Br>), maxiter 500 '
+                       '(src/bidomain_3d.py:149); timeKSP-style: setup + solve'}
     elif args.pcg:
         solver = M.DistConjGrad.for_handles(B, stream=stream, tolerance=1e-8, maxiter=500)
         barrier()
@@ -210,6 +239,32 @@ def main():
         barrier()
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
                'seconds': round(allmax(time.perf_counter() - t0), 3)}
+
+    # ---- the reference's smoother family on the GPU (multicolour SGS +
+    # coarse-grid scaling): iterations and time to solution next to the default
+    profiles = None
+    if args.compare_profiles and world == 1 and args.pcg:
+        profiles = []
+        for name, kw in (('mi355x_sgs (multicolour node-block SGS, coarse scaling ON)',
+                          dict(smoother=11, coarse_scaling=1)),):
+            torch.cuda.synchronize(dev)
+            t0 = time.time()
+            B2 = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu', **kw)
+            torch.cuda.synchronize(dev)
+            ts = time.time() - t0
+            ms2, _, _ = B2.time_apply(r, z, 5, 0, stream)
+            s2 = M.ConjGrad(sysm, precond=B2, tolerance=1e-8, maxiter=500)
+            B2._Aop = sysm
+            torch.cuda.synchronize(dev)
+            t0 = time.time()
+            s2 * r_full
+            torch.cuda.synchronize(dev)
+            tp2 = time.time() - t0
+            profiles.append({'profile': name, 'niters': len(s2.residuals) - 1, 'pcg_s': round(tp2, 4),
+                             'setup_s': round(ts, 4), 'setup_plus_pcg_s': round(ts + tp2, 4),
+                             'ms_per_apply': round(ms2, 4)})
+            B2.close()
+            del s2
 
     # ---- CPU baseline: oracle C restatement on the same hierarchy, host cores
     cpu = None
@@ -229,27 +284,47 @@ def main():
         zg = z.cpu().numpy()
         err = float(np.linalg.norm(zc - zg) / np.linalg.norm(zc))
         cpu = {'value': round(1.0 / tc, 4), 'unit': 'V-cycle applies/s', 'cores': ch.threads(),
-               'kind': 'port',
+               'kind': 'port', 'nproc': os.cpu_count(),
+               'affinity': len(os.sched_getaffinity(0)), 'cpu_model': cpu_model(),
                'sample': '%d applies of the full nrefs=%d hierarchy (oracle/vcycle_ref.c, OpenMP), '
                          'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, args.nrefs, err)}
+        if args.cpu_pcg and pcg is not None:
+            # N1: PCG iteration count of the CPU path (same hierarchy bits,
+            # C cycle + C SpMV) against the GPU's (src/bidomain_3d.py:149-157)
+            t0 = time.time()
+            _, cres = ch.pcg(r_full, 1e-8, 500)
+            pcg['cpu_pcg'] = {'niters': len(cres) - 1, 'seconds': round(time.time() - t0, 2),
+                              'max_rel_residual_diff': float(max(abs(a - b) / b for a, b in
+                                                                 zip(gpu_res, cres))) if len(cres) == len(gpu_res)
+                              else None,
+                              'threads': ch.threads()}
         del ch, lv
     if H is not None and levels is None:
         levels = [[s['n'], s['nnzA']] for s in (H.sizes(l) for l in range(H.num_levels))]
 
     # measured HBM bytes per launch of the two dominant kernels (rocprofv3
-    # FETCH_SIZE + WRITE_SIZE, calibrated; profiles/traffic.json, written by
-    # scripts/traffic.py from the committed PMC summaries of this config)
+    # FETCH_SIZE + WRITE_SIZE passes, calibrated; profiles/traffic.json,
+    # written by scripts/traffic.py from the PMC CSVs of this config).  Used
+    # only when it was measured on this kernel source (device.hip sha256)
+    # and this layout; the line carries its provenance either way.
     fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
     post_mode = 'k' if fmt0.get('post_k') else 'merged'
     a0_mode = 'half' if fmt0.get('half') else 'sell'
-    traffic = {}
+    traffic, traffic_src = {}, None
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
+    src_sha = device_src_sha()
     if os.path.exists(tpath) and world == 1:
         try:
             tj = json.load(open(tpath))
-            if (tj.get('N') == sysm.N and tj.get('layout') == layout and tj.get('post', 'merged') == post_mode
-                    and tj.get('a0', 'sell') == a0_mode):
+            ok = (tj.get('N') == sysm.N and tj.get('layout') == layout and tj.get('post', 'merged') == post_mode
+                  and tj.get('a0', 'sell') == a0_mode)
+            if ok and tj.get('device_src_sha256') == src_sha:
                 traffic = tj.get('kernels', {})
+                traffic_src = 'profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of ' \
+                              'this kernel source, device.hip sha256 %s)' % src_sha[:16]
+            else:
+                traffic_src = 'not used: profiles/traffic.json was measured on another kernel source or config ' \
+                              '(device.hip sha256 %s vs %s)' % (str(tj.get('device_src_sha256'))[:16], src_sha[:16])
         except (OSError, ValueError):
             traffic = {}
 
@@ -273,7 +348,7 @@ def main():
         rooflines.append({
             'bound': 'hbm', 'kernel': '%s (%s)%s' % (descr[c], names[c], '' if world == 1 else ', rank 0 slice'),
             'achieved': round(ach, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
-            'frac': round(ach / HBM_PEAK_GBPS, 4), 'traffic': traffic.get(key),
+            'frac': round(ach / HBM_PEAK_GBPS, 4), 'traffic': traffic.get(key), 'traffic_source': traffic_src,
             'bytes_per_launch': cbytes[c], 'ms_per_launch': round(kms[c], 4)})
     roofline = max(rooflines, key=lambda r: r['ms_per_launch']) if rooflines else None
     out = {
@@ -306,6 +381,7 @@ def main():
         'setup': dict(setup_info, generate_s=round(t_gen, 2)),
         'breakdown': breakdown,
         'pcg': pcg,
+        'pcg_profiles': profiles,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

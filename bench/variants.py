@@ -4,7 +4,7 @@
     python bench/variants.py [--nrefs 6] [--reps 20] VAR=VAL,VAR=VAL ...
 
 Each argument is one variant: environment knobs read at upload
-(MAMG_XCD_REMAP, MAMG_POST_LANES) plus optional parameter overrides given as
+(MAMG_HALF, MAMG_HALF_BANDS, MAMG_POST_K) plus optional parameter overrides given as
 p.<name>=<int> (e.g. p.post_fusion=0).  The setup runs once; every variant
 re-uploads it, runs `reps` graph applies (ms per apply) and one instrumented
 pass (per-class kernel ms).  One JSON line per variant.
@@ -26,7 +26,7 @@ def main():
     ap.add_argument('--nrefs', type=int, default=6)
     ap.add_argument('--gamma', type=float, default=1e6)
     ap.add_argument('--reps', type=int, default=20)
-    ap.add_argument('variants', nargs='*', default=['MAMG_XCD_REMAP=1'])
+    ap.add_argument('variants', nargs='*', default=['MAMG_HALF=1'])
     args = ap.parse_args()
     import torch
     import metric_amg_examples_amd as M

@@ -871,100 +871,39 @@ __global__ __launch_bounds__(256) void cscale_kernel(int64_t n, int nb, const do
 
 inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 
-// tuning knobs, read at upload (bench/variants.py):
-//   MAMG_XCD_REMAP  0 off, 1 restriction ops only (default), 2 every BSR op
-//   MAMG_POST_LANES lanes per row of the fused post kernel (0 = auto)
-//   MAMG_SYM_BLOCKS 0 disables the symmetric-block format (default 1)
-//   MAMG_SELL       0 disables the SELL-64 storage (default 1), used for
-//                   matrices with >= MAMG_SELL_MIN_ROWS (2^20) node rows
-//   MAMG_SELL_POST  1: SELL-64-sigma for the merged [P | AP] too (default 0)
-//   MAMG_SELL_U     SELL blocks per chunk (4, 8, 16), level-0 SELL kernels
-//   MAMG_NT         1: non-temporal matrix loads in the level-0 kernels
-//   MAMG_POST_K     0: fused post sweep over [P | AP] instead of K = P - W A P (default 1)
-//   MAMG_POST_SELL  0: K in lane-group BSR instead of SELL-64 (default 1)
-//   MAMG_POST_U     SELL blocks per chunk of the K kernel (6 default, 4, 5, 8, 16)
-//   MAMG_SELL_REMAP 1: XCD-contiguous row order for the level-0 SELL kernels
-//   MAMG_POST_REMAP 1: XCD-contiguous row order for the level-0 K (post) kernel
-//   MAMG_POST_BANDS 1: the K kernel walks A0's band schedule (default 0)
-//   MAMG_SELL_MAX_LEN SELL only for matrices with <= this many blocks per row (40)
-//   MAMG_HALF       0: full SELL-64 instead of the half-symmetric ELL-64 for A0 (default 1)
-//   MAMG_HALF_U     blocks per chunk of the half-symmetric kernel (4 default, 8)
-//   MAMG_HALF_REMAP XCD-contiguous row order for the half-symmetric kernel (default 1:
-//                   the mirror re-reads then hit the XCD's own L2)
-//   MAMG_HALF_BANDS band schedule of the half-symmetric kernel: sub-bands per XCD
-//                   (default 1; 0 = off, row order by MAMG_HALF_REMAP)
-//   MAMG_R_LANES / MAMG_A1_LANES  lanes per row of the level-0 restriction / the
-//                   level-1 operator (0 = auto from the mean row length)
-//   multi-GPU (read at mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch
-//   during the forward halo (default 1); MAMG_DIST_DRY 1 = a virtual rank skips its
-//   exchanges (compute-only timing, bench/dist_rehearsal.py; results meaningless)
-int g_remap = 1;
-int g_sell_remap = 0;
-int g_post_remap = 0;
-int g_post_bands = 0;
-int g_r_lanes = 0;
-int g_a1_lanes = 0;
+// Tuning knobs (environment, read at upload), kept
+// because a test or an A/B needs them:
+//   MAMG_SELL_MIN_ROWS  node rows from which a level-0-class operator is stored
+//                       SELL-64 / half-symmetric (default 2^20; tests lower it
+//                       to exercise those formats on small problems)
+//   MAMG_HALF           0: SELL-64 instead of the half-symmetric ELL-64 A0 (1)
+//   MAMG_HALF_BANDS     band schedule of the half-symmetric kernel: sub-bands per
+//                       XCD (1; 0 = row order)
+//   MAMG_POST_K         0: fused post sweep over [P | AP] instead of K = P - W A P (1)
+//   multi-GPU (mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch during
+//   the forward halo (1); MAMG_DIST_DRY 1 = a virtual rank skips its exchanges
+//   (compute-only timing; results meaningless); setup: MAMG_PRERESERVE_B_PER_NNZ
+// Fixed by measurement (round 1 A/Bs; the variants
+// measured slower were removed in round 2): XCD-contiguous restriction rows,
+// SELL chunks of 8 blocks (K: 6), half-symmetric chunks of 4 with
+// XCD-contiguous rows, symmetric-block packing, lane counts from the mean row
+// length.
+constexpr int g_sell_u = 8;
+constexpr int g_post_u = 6;
+constexpr int64_t g_sell_max_len = 40;
 int g_half = 1;
-int g_half_u = 4;
-int g_half_remap = 1;
 int g_half_bands = 1;
-int g_post_lanes = 0;
-int g_sym = 1;
-int g_sell = 1;
-int g_sell_post = 0;
-int g_sell_u = 8;
-int g_nt = 0;
 int g_post_k = 1;
-int g_post_u = 6;
-int g_post_sell = 1;
 int64_t g_sell_min_rows = 1 << 20;
-int64_t g_sell_max_len = 40;
 void read_knobs() {
-  const char* pk = std::getenv("MAMG_POST_K");
-  g_post_k = pk ? std::atoi(pk) != 0 : 1;
-  pk = std::getenv("MAMG_POST_U");
-  g_post_u = pk ? std::atoi(pk) : 6;
-  if (g_post_u != 4 && g_post_u != 5 && g_post_u != 6 && g_post_u != 8 && g_post_u != 16) g_post_u = 6;
-  pk = std::getenv("MAMG_POST_SELL");
-  g_post_sell = pk ? std::atoi(pk) != 0 : 1;
-  const char* su = std::getenv("MAMG_SELL_U");
-  g_sell_u = su ? std::atoi(su) : 8;
-  if (g_sell_u != 4 && g_sell_u != 8 && g_sell_u != 16) g_sell_u = 8;
-  su = std::getenv("MAMG_NT");
-  g_nt = su ? std::atoi(su) : 0;
-  const char* sp = std::getenv("MAMG_SELL_POST");
-  g_sell_post = sp ? std::atoi(sp) : 0;
-  const char* s = std::getenv("MAMG_SELL");
-  g_sell = s ? std::atoi(s) : 1;
-  s = std::getenv("MAMG_SELL_MIN_ROWS");
-  g_sell_min_rows = s ? std::atoll(s) : (1 << 20);
-  s = std::getenv("MAMG_SELL_MAX_LEN");
-  g_sell_max_len = s ? std::atoll(s) : 40;
-  su = std::getenv("MAMG_HALF");
-  g_half = su ? std::atoi(su) != 0 : 1;
-  su = std::getenv("MAMG_HALF_U");
-  g_half_u = su ? std::atoi(su) : 4;
-  if (g_half_u != 4 && g_half_u != 8) g_half_u = 4;
-  su = std::getenv("MAMG_HALF_REMAP");
-  g_half_remap = su ? std::atoi(su) != 0 : 1;
-  su = std::getenv("MAMG_HALF_BANDS");
-  g_half_bands = su ? std::atoi(su) : 1;
-  su = std::getenv("MAMG_POST_BANDS");
-  g_post_bands = su ? std::atoi(su) != 0 : 0;
-  su = std::getenv("MAMG_POST_REMAP");
-  g_post_remap = su ? std::atoi(su) != 0 : 0;
-  su = std::getenv("MAMG_SELL_REMAP");
-  g_sell_remap = su ? std::atoi(su) != 0 : 0;
-  const char* e = std::getenv("MAMG_XCD_REMAP");
-  g_remap = e ? std::atoi(e) : 1;
-  e = std::getenv("MAMG_POST_LANES");
-  g_post_lanes = e ? std::atoi(e) : 0;
-  e = std::getenv("MAMG_R_LANES");
-  g_r_lanes = e ? std::atoi(e) : 0;
-  e = std::getenv("MAMG_A1_LANES");
-  g_a1_lanes = e ? std::atoi(e) : 0;
-  e = std::getenv("MAMG_SYM_BLOCKS");
-  g_sym = e ? std::atoi(e) != 0 : 1;
+  const char* e = std::getenv("MAMG_POST_K");
+  g_post_k = e ? std::atoi(e) != 0 : 1;
+  e = std::getenv("MAMG_SELL_MIN_ROWS");
+  g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
+  e = std::getenv("MAMG_HALF");
+  g_half = e ? std::atoi(e) != 0 : 1;
+  e = std::getenv("MAMG_HALF_BANDS");
+  g_half_bands = e ? std::atoi(e) : 1;
 }
 
 // every block symmetric (bitwise): then 3 doubles per block carry it exactly
@@ -1093,7 +1032,7 @@ struct Op {
   double bytes = 0.0;
 };
 
-inline int remap_of(const Op& o) { return g_remap == 2 ? 1 : (g_remap == 1 ? o.remap : 0); }
+inline int remap_of(const Op& o) { return o.remap; }
 
 struct Graph {
   const double* r = nullptr;
@@ -1122,7 +1061,12 @@ struct DeviceHandle {
   double* hres = nullptr;          // pinned host scalar
   double apply_bytes = 0.0;
   double setup_ms[8] = {};         // GPU setup phase timings (dev_from_ghier)
+  // every piece of work on the handle's scratch buffers (apply, host apply,
+  // spmv, PCG, timing) waits for this event on its stream and re-records it
+  // afterwards: work on one handle is serialized across streams
+  hipEvent_t last = nullptr;
   ~DeviceHandle() {
+    if (last) (void)hipEventDestroy(last);
     for (auto& g : graphs) {
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
       if (g.graph) (void)hipGraphDestroy(g.graph);
@@ -1229,13 +1173,13 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
   int rc;
   // SELL-64 for many short rows (one lane per row needs >> 256 CUs x 64 rows)
   const bool merged_rows = np == 2 * B.nr + 1;
-  if (g_sell && B.nr >= g_sell_min_rows && D->nb <= g_sell_max_len * B.nr && (!merged_rows || g_sell_post)) {
-    D->sym = sym && g_sym && np == B.nr + 1 && blocks_symmetric(B);
+  if (B.nr >= g_sell_min_rows && D->nb <= g_sell_max_len * B.nr && !merged_rows) {
+    D->sym = sym && np == B.nr + 1 && blocks_symmetric(B);
     return upload_sell(h, B, D, err);
   }
   if ((rc = dalloc(h, &D->ptr, np, err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
-  D->sym = sym && g_sym && np == B.nr + 1 && blocks_symmetric(B);
+  D->sym = sym && np == B.nr + 1 && blocks_symmetric(B);
   const int per = D->sym ? 3 : 4;
   if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
   HIPCHK(hipMemcpy(D->ptr, B.ptr.data(), np * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -1759,7 +1703,7 @@ int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
 template <class HT>
 int upload_half_or_bsr(HT* h, const HBsr& B, DBsr* D, std::string* err) {
   const int64_t np = (int64_t)B.ptr.size();
-  if (g_half && g_sell && g_sym && B.nr >= g_sell_min_rows && np == B.nr + 1 && blocks_symmetric(B)) {
+  if (g_half && B.nr >= g_sell_min_rows && np == B.nr + 1 && blocks_symmetric(B)) {
     int rc;
     TmpPool T;
     TBsr tb;
@@ -1797,7 +1741,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   D->nb = B.nb;
   D->lanes = lanes > 0 ? lanes : pick_lanes_bsr(nr, D->nb);
   bool sym = false;
-  if (sym_ok && g_sym && !B.merged && B.nb > 0) {
+  if (sym_ok && !B.merged && B.nb > 0) {
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
     HIPCHK(hipMemset(bad, 0, sizeof(int)));
@@ -1808,7 +1752,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   }
   D->sym = sym;
   const int per = sym ? 3 : 4;
-  if (allow_sell && g_sell && nr >= g_sell_min_rows && D->nb <= g_sell_max_len * nr && !B.merged) {
+  if (allow_sell && nr >= g_sell_min_rows && D->nb <= g_sell_max_len * nr && !B.merged) {
     if (allow_half && g_half && sym && nr == B.nc) {
       if ((rc = try_half(h, T, B, D, err))) return rc;
       if (D->half) return MAMG_OK;
@@ -1973,7 +1917,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr B;
     if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, B, &D.Ab, l == 1 && g_a1_lanes ? g_a1_lanes : lanesA, true, err, true,
+    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true,
                            l == 0)))
       return rc;
     if (gs_smoother(p))
@@ -1994,13 +1938,8 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     // K: SELL-64 with 4-block chunks (K rows hold ~9 blocks at level 0; A/B in
     // DESIGN.md section 4), lane-group BSR if MAMG_POST_SELL=0; the merged
     // window is never SELL on this path
-    if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, g_post_lanes, false, err,
-                           g_post_k && g_post_sell)))
+    if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0)))
       return rc;
-    if (g_post_bands && g_post_k && D.KPb.sell && D.Ab.nsched > 0 && D.KPb.nr == D.Ab.nr) {
-      D.KPb.sched = D.Ab.sched;      // K's rows are A0's rows: walk them in the same bands
-      D.KPb.nsched = D.Ab.nsched;    // (owned by the handle through D.Ab)
-    }
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -2009,7 +1948,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr Rb;
     if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, l == 0 ? g_r_lanes : 0, false, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
   }
   if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
   HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
@@ -2364,7 +2303,7 @@ void launch_sell_u(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(M.nr);
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 ? (o.epi == EPI_KPOST ? g_post_remap : g_sell_remap) : 0), \
+    0, \
     ((int64_t)g == M.nsched ? M.sched : nullptr)
   switch (o.epi) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
@@ -2380,21 +2319,10 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
-  if (TAG == 0) {   // the level-0 operator: tuning variants (bench/variants.py)
-    const int u = o.epi == EPI_KPOST ? g_post_u : g_sell_u;
-    switch (u * 2 + (g_nt ? 1 : 0)) {
-      case 8: launch_sell_u<XFM, SYM, 4, false, TAG>(o, s); return;
-      case 9: launch_sell_u<XFM, SYM, 4, true, TAG>(o, s); return;
-      case 10: launch_sell_u<XFM, SYM, 5, false, TAG>(o, s); return;
-      case 12: launch_sell_u<XFM, SYM, 6, false, TAG>(o, s); return;
-      case 13: launch_sell_u<XFM, SYM, 6, true, TAG>(o, s); return;
-      case 16: launch_sell_u<XFM, SYM, 8, false, TAG>(o, s); return;
-      case 17: launch_sell_u<XFM, SYM, 8, true, TAG>(o, s); return;
-      case 32: launch_sell_u<XFM, SYM, 16, false, TAG>(o, s); return;
-      default: launch_sell_u<XFM, SYM, 16, true, TAG>(o, s); return;
-    }
-  }
-  launch_sell_u<XFM, SYM, 8, false, TAG>(o, s);
+  // level-0 K operator: chunks of 6 blocks (two chunks cover its ~9-block
+  // rows); everything else 8
+  if (TAG == 0 && o.epi == EPI_KPOST) launch_sell_u<XFM, SYM, g_post_u, false, TAG>(o, s);
+  else launch_sell_u<XFM, SYM, g_sell_u, false, TAG>(o, s);
 }
 
 template <int TAG>
@@ -2420,11 +2348,7 @@ void launch_post_vl(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-  if (g_nt && TAG == 0)
-    bsr2_post_kernel<VL, true, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
-                                                      o.out, o.os, remap_of(o));
-  else
-    bsr2_post_kernel<VL, false, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
+  bsr2_post_kernel<VL, false, TAG><<<g, 256, 0, s>>>(M.nr, M.ptr, M.col, M.val, o.x, o.y, o.b, o.W,
                                                        o.out, o.os, remap_of(o));
 }
 
@@ -2454,7 +2378,7 @@ void launch_half_u(const Op& o, hipStream_t s) {
   const unsigned g = nblocks(r1 - r0);
   if (r1 <= r0) return;
 #define HALF_ARGS r0, r1, M.meta, M.col, M.val, M.nbs, M.hwu, M.lptr, M.hwl, M.gsoff, M.gcol, M.gval, M.ngs, \
-    o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, g_half_remap, \
+    o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, 1, \
     (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched \
     : (r0 == M.sr0 && r1 == M.sr1 && (int64_t)g == M.nsched_r) ? M.sched_r : nullptr
   switch (o.epi) {
@@ -2469,7 +2393,7 @@ void launch_half_u(const Op& o, hipStream_t s) {
 
 template <bool XFM, bool GH, int TAG>
 void launch_half_x(const Op& o, hipStream_t s) {
-  if (g_half_u == 8) launch_half_u<XFM, 8, GH, TAG>(o, s); else launch_half_u<XFM, 4, GH, TAG>(o, s);
+  launch_half_u<XFM, 4, GH, TAG>(o, s);
 }
 
 template <int TAG>
@@ -2559,10 +2483,22 @@ void launch(const Op& o, hipStream_t s) {
   }
 }
 
+// handle ordering (DeviceHandle::last)
+int order_begin(DeviceHandle* h, hipStream_t s, std::string* err) {
+  if (!h->last) HIPCHK(hipEventCreateWithFlags(&h->last, hipEventDisableTiming));
+  HIPCHK(hipStreamWaitEvent(s, h->last, 0));
+  return MAMG_OK;
+}
+int order_end(DeviceHandle* h, hipStream_t s, std::string* err) {
+  HIPCHK(hipEventRecord(h->last, s));
+  return MAMG_OK;
+}
+
 int get_graph(DeviceHandle* h, const double* r, double* z, hipGraphExec_t* exec, std::string* err) {
   for (auto& g : h->graphs)
     if (g.r == r && g.z == z) { *exec = g.exec; return MAMG_OK; }
-  if (h->graphs.size() >= 16) {   // evict oldest
+  if (h->graphs.size() >= 16) {   // evict oldest, after every launch on the handle finished
+    if (h->last) HIPCHK(hipEventSynchronize(h->last));
     auto& g = h->graphs.front();
     (void)hipGraphExecDestroy(g.exec);
     (void)hipGraphDestroy(g.graph);
@@ -2692,8 +2628,12 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
 // (profiles/r01_bench_prereserve_ab.log).  Bytes per A0
 // entry: MAMG_PRERESERVE_B_PER_NNZ (default 20, ~16.5 used at nrefs=6; 0 = off);
 // a rank of N reserves 1.25 x that / N + 0.5.
-static void* g_pre = nullptr;
-static size_t g_pre_bytes = 0;
+// one pending reservation per host thread (setups in different threads, e.g.
+// virtual ranks or several devices, never see each other's), tagged with its
+// device: a handle on another device does not adopt it
+static thread_local void* g_pre = nullptr;
+static thread_local size_t g_pre_bytes = 0;
+static thread_local int g_pre_dev = -1;
 void dev_prereserve(int device, int64_t nnz, int nranks) {
   const char* e = std::getenv("MAMG_PRERESERVE_B_PER_NNZ");
   double b = e ? std::atof(e) : 20.0;
@@ -2702,31 +2642,39 @@ void dev_prereserve(int device, int64_t nnz, int nranks) {
   if (b <= 0 || nnz <= 0) return;
   if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return; }
   const size_t bytes = ((size_t)(b * (double)nnz) + (1 << 21)) & ~(size_t)((1 << 21) - 1);
-  if (hipMalloc(&g_pre, bytes) == hipSuccess) g_pre_bytes = bytes;
+  if (hipMalloc(&g_pre, bytes) == hipSuccess) { g_pre_bytes = bytes; g_pre_dev = device; }
   else { (void)hipGetLastError(); g_pre = nullptr; }
 }
 void dev_prereserve_release() {
-  if (g_pre) (void)hipFree(g_pre);
+  if (g_pre) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(g_pre_dev);
+    (void)hipFree(g_pre);
+    (void)hipSetDevice(cur);
+  }
   g_pre = nullptr;
   g_pre_bytes = 0;
+  g_pre_dev = -1;
 }
 template <class HT>
 void adopt_prereserve(HT* h) {
-  if (!g_pre) return;
+  if (!g_pre || g_pre_dev != h->device) { dev_prereserve_release(); return; }
   h->allocs.push_back(g_pre);
   h->arena = (char*)g_pre;
   h->arena_left = g_pre_bytes;
   g_pre = nullptr;
   g_pre_bytes = 0;
+  g_pre_dev = -1;
 }
 
 int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandle** out,
                    std::string* err) {
   const auto t0 = std::chrono::steady_clock::now();
   std::unique_ptr<DeviceHandle> h(new DeviceHandle());
-  adopt_prereserve(h.get());
   h->p = p;
   h->device = p.device;
+  adopt_prereserve(h.get());
   HIPCHK(hipSetDevice(p.device));
   HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
   read_knobs();
@@ -2822,28 +2770,33 @@ int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std
   hipGraphExec_t exec;
   int rc = get_graph(h, d_r, d_z, &exec, err);
   if (rc) return rc;
+  if ((rc = order_begin(h, (hipStream_t)stream, err))) return rc;
   HIPCHK(hipGraphLaunch(exec, (hipStream_t)stream));
-  return MAMG_OK;
+  return order_end(h, (hipStream_t)stream, err);
 }
 
 int dev_apply_host(DeviceHandle* h, const double* r, double* z, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
   const int64_t n = h->L[0].n;
-  HIPCHK(hipMemcpyAsync(h->hr, r, n * sizeof(double), hipMemcpyHostToDevice, h->cap));
   hipGraphExec_t exec;
   int rc = get_graph(h, h->hr, h->hz, &exec, err);
   if (rc) return rc;
+  if ((rc = order_begin(h, h->cap, err))) return rc;   // after queued device-pointer applies
+  HIPCHK(hipMemcpyAsync(h->hr, r, n * sizeof(double), hipMemcpyHostToDevice, h->cap));
   HIPCHK(hipGraphLaunch(exec, h->cap));
   HIPCHK(hipMemcpyAsync(z, h->hz, n * sizeof(double), hipMemcpyDeviceToHost, h->cap));
+  if ((rc = order_end(h, h->cap, err))) return rc;
   HIPCHK(hipStreamSynchronize(h->cap));
   return MAMG_OK;
 }
 
 int dev_spmv(DeviceHandle* h, const double* d_x, double* d_y, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
+  int rc = order_begin(h, (hipStream_t)stream, err);
+  if (rc) return rc;
   launch(a0_op(h, EPI_Y, d_x, nullptr, d_y), (hipStream_t)stream);
   HIPCHK(hipGetLastError());
-  return MAMG_OK;
+  return order_end(h, (hipStream_t)stream, err);
 }
 
 namespace {
@@ -2874,6 +2827,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     HIPCHK(hipHostMalloc((void**)&h->hres, sizeof(double), hipHostMallocDefault));
   }
   const unsigned g = nblocks(n);
+  if ((rc = order_begin(h, s, err))) return rc;
   launch(a0_op(h, EPI_RESID, d_x, d_b, h->cr), s);                 // r = b - A x
   if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;         // z = B r
   HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -2888,7 +2842,11 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), s);              // q = A d
     double dz;
     if ((rc = dot(h, n, h->cd, h->cq, s, &dz, err))) return rc;
-    if (dz == 0.0) break;
+    if (dz == 0.0) {   // the host loop's breakdown flag (krylov.py): same status here
+      *err = "ConjGrad stopped: <d,Ad> = 0";
+      status = MAMG_ERR_BREAKDOWN;
+      break;
+    }
     const double alpha = rz / dz;
     cg_xr_kernel<<<g, 256, 0, s>>>(n, alpha, h->cd, h->cq, d_x, h->cr);
     if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;
@@ -2907,6 +2865,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     betas[it] = beta;
     ++it;
   }
+  if ((rc = order_end(h, s, err))) return rc;
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipGetLastError());
   *niters = it;
@@ -2917,6 +2876,8 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
                    double* kernel_ms, double* class_bytes, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
+  int rc = order_begin(h, s, err);
+  if (rc) return rc;
   std::vector<Op> ops;
   apply_ops(h, d_r, d_z, &ops);
   if (class_bytes) {
@@ -2942,6 +2903,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
     }
   }
   HIPCHK(hipEventRecord(ev[1], s));
+  if ((rc = order_end(h, s, err))) return rc;
   HIPCHK(hipEventSynchronize(ev[1]));
   HIPCHK(hipGetLastError());
   float tot = 0.f;
@@ -3286,11 +3248,11 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0);
   if (rc) return rc;
   std::unique_ptr<DistHandle> h(new DistHandle());
-  adopt_prereserve(h.get());
   h->p = p;
   h->rank = rank;
   h->nranks = nranks;
   h->device = p.device;
+  adopt_prereserve(h.get());
   HIPCHK(hipSetDevice(p.device));
   if (comm_id) {                         // RCCL communicator; NULL = virtual (tests)
     ncclUniqueId uid;
@@ -3349,7 +3311,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
         return rc;
       }
       if (P.K.nr > 0) {
-        if ((rc = upload_bsr(h.get(), P.K, &D.K, g_post_lanes, err))) return rc;
+        if ((rc = upload_bsr(h.get(), P.K, &D.K, 0, err))) return rc;
       } else if (P.PA.nr > 0) {
         if ((rc = upload_bsr(h.get(), P.PA, &D.PA, 0, err))) return rc;
       } else {

@@ -673,13 +673,31 @@ int check_params(const mamg_params& p, std::string* err) {
     *err = "multicolour GS/SGS smoothers are node-block smoothers: num_functions 2 and node_block_smoother 1";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (p.aggregation_type != MAMG_MIS) { *err = "aggregation_type must be MIS (deterministic parallel MIS-2); VMB/HEM/HEC/MWM not implemented"; return MAMG_ERR_UNSUPPORTED; }
+  if (p.aggregation_type != MAMG_MIS) {
+    *err = "aggregation_type must be MIS (deterministic parallel MIS-2): VMB/HEM/HEC/MWM are not implemented "
+           "(parameters.to_gpu_profile maps a HAZmath dict explicitly)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   if (p.coarse_scaling != MAMG_OFF && p.coarse_scaling != MAMG_ON) { *err = "coarse_scaling must be OFF or ON"; return MAMG_ERR_ARG; }
   if (p.coarse_solver != MAMG_COARSE_DENSE) { *err = "coarse_solver must be 32 (direct)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels > 1) { *err = "Schwarz_levels > 1 not supported (seeds exist on level 0 only)"; return MAMG_ERR_UNSUPPORTED; }
-  if (p.Schwarz_levels == 1 && p.Schwarz_type != MAMG_SCHWARZ_BLOCK_JACOBI) {
-    *err = "Schwarz_type must be SCHWARZ_BLOCK_JACOBI (multiplicative Schwarz is sequential)";
-    return MAMG_ERR_UNSUPPORTED;
+  if (p.Schwarz_levels == 1) {
+    // the level-0 seed blocks are smoothed by the level smoother: additive
+    // (block Jacobi) with the Jacobi smoothers, multiplicative in colour order
+    // with GS (forward) / SGS (symmetric)
+    const bool gsm = p.smoother == MAMG_SMOOTHER_GS || p.smoother == MAMG_SMOOTHER_SGS;
+    const int want = p.smoother == MAMG_SMOOTHER_SGS ? MAMG_SCHWARZ_SYMMETRIC
+                     : p.smoother == MAMG_SMOOTHER_GS ? MAMG_SCHWARZ_FORWARD : MAMG_SCHWARZ_BLOCK_JACOBI;
+    if (p.Schwarz_type != want) {
+      *err = std::string("Schwarz_type must match the smoother: SCHWARZ_BLOCK_JACOBI with the Jacobi smoothers, ") +
+             "SCHWARZ_SYMMETRIC with SMOOTHER_SGS, SCHWARZ_FORWARD with SMOOTHER_GS" + (gsm ? "" : "");
+      return MAMG_ERR_UNSUPPORTED;
+    }
+    if (p.Schwarz_maxlvl > 1) {
+      *err = "Schwarz_maxlvl > 1 (overlapping seed + ring blocks) not implemented; 1 = non-overlapping "
+             "partition of the seeds' 1-rings";
+      return MAMG_ERR_UNSUPPORTED;
+    }
   }
   if (p.Schwarz_levels == 1 && p.Schwarz_mmsize < 1) { *err = "Schwarz_mmsize must be >= 1"; return MAMG_ERR_ARG; }
   if (p.max_levels < 1 || p.maxit < 1 || p.presmooth_iter < 1 || p.postsmooth_iter < 1 || p.coarse_dof < 1) {

@@ -135,9 +135,16 @@ def dat_to_parameters(d: dict):
     if 'AMG_aggregation_type' in d:
         prm['aggregation_type'] = _AGG.get(int(d['AMG_aggregation_type']), P.VMB)
     mapped, n2 = P.to_gpu_profile(prm)
-    # HAZmath's relaxation is an SOR weight; the Jacobi smoother here takes
-    # the profile's spectral weight when the file asked for GS/SGS/SOR
-    if prm.get('smoother') in (P.SMOOTHER_GS, P.SMOOTHER_SGS):
+    # the file-based 3D-1D solve seeds the 1-D dofs: its seed blocks are not
+    # node-aligned, so it runs the CSR layout, where the multicolour GS
+    # smoothers (node-block) do not exist; HAZmath's relaxation is an SOR
+    # weight, the Jacobi smoother takes the profile's spectral weight
+    if mapped.get('smoother') in (P.SMOOTHER_GS, P.SMOOTHER_SGS):
+        notes.append('smoother GS/SGS -> SMOOTHER_JACOBI_RHO (seeds not node-aligned: CSR layout, '
+                     'no node-block multicolour GS)')
+        mapped['smoother'] = P.SMOOTHER_JACOBI_RHO
+        mapped['Schwarz_type'] = P.SCHWARZ_BLOCK_JACOBI
+        mapped.pop('num_functions', None)
         mapped['relaxation'] = 4.0 / 3.0
         notes.append('relaxation %s -> 4/3 (weight of the relaxation/rho Jacobi smoother)'
                      % prm.get('relaxation', 1.0))

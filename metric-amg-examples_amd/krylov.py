@@ -88,7 +88,10 @@ class ConjGrad:
         blocks = isinstance(b, (list, tuple))
         if blocks:
             b = np.concatenate([np.asarray(bi, dtype=np.float64) for bi in b])
-        if self._device_ok() or self.device is True:
+        if self.device is True and not self._device_ok():
+            raise ValueError('ConjGrad(device=True) needs precond = a MetricAMG built on this A (the '
+                             'device PCG uses its level-0 operator), no callback and the cbc.block stopping rule')
+        if self._device_ok():
             x = self._solve_device(b)
         else:
             x = self._solve_host(b)
@@ -118,7 +121,9 @@ class ConjGrad:
         k = it.value
         if rc == _lib.ERR_BREAKDOWN:
             self.breakdown = True
-            warnings.warn('ConjGrad breakdown: ' + B._L.mamg_last_error().decode())
+            msg = B._L.mamg_last_error().decode()
+            if '<d,Ad> = 0' not in msg:        # the host loop stops silently on <d,Ad> = 0 too
+                warnings.warn('ConjGrad breakdown: ' + msg)
             if k == 0 and res[0] == 0.0:
                 raise ValueError('Matrix is not positive')
         else:

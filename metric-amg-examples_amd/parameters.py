@@ -4,13 +4,20 @@ Keys and enum *names* follow /root/reference/src/amg_parameters.py:3-89 and
 /root/reference/src/utils.py:20-38,60-82 (haznics constants).  Numeric enum
 values are build-defined (HAZmath's are not available here).
 
-The reference's presets select sequential HAZmath components (SGS smoother,
-multiplicative Schwarz, VMB/HEM aggregation, coarse scaling) that cannot be
-reproduced on a GPU.  ``MetricAMG`` rejects them with MAMG_ERR_UNSUPPORTED
-(no silent fallback).  ``to_gpu_profile`` maps such a dict to the nearest
-GPU-parallel components and reports every substitution; the presets below
-with the reference's names are those mapped versions, so a driver that does
-``amgparams = parameters.parameters_metric_schwarz`` runs unchanged.
+* ``parameters_standard``, ``parameters_standard_schwarz``,
+  ``parameters_metric``, ``parameters_metric_schwarz``: the reference's
+  presets with their values verbatim.  ``MetricAMG`` runs what they select or
+  raises MAMG_ERR_UNSUPPORTED naming the component it lacks (VMB / HEM
+  aggregation); there is no silent substitution under these names.
+* ``parameters_metric_mi355x``: the GPU profile "mi355x_sa_v" (nodal SA,
+  V-cycle, node-block Jacobi) -- the fastest time to solution measured
+  (DESIGN.md section 2.8), the drivers' and the bench's default.
+* ``parameters_metric_mi355x_sgs``: the reference's smoother family on the
+  GPU: multicolour node-block SGS on every level (level 0: multiplicative
+  Schwarz on the seed blocks), coarse-grid correction scaling ON.
+* ``to_gpu_profile(d)``: explicit opt-in mapping of a HAZmath dict onto
+  implemented components; returns the mapped dict and every substitution.
+  ``*_gpu_mapped`` are the reference presets passed through it.
 """
 from __future__ import annotations
 
@@ -56,66 +63,81 @@ parameters_metric_mi355x = {
     "amli_degree": 3,
     "Schwarz_levels": 1,
     "Schwarz_mmsize": 100,
-    "Schwarz_maxlvl": 1,
+    "Schwarz_maxlvl": 1,          # non-overlapping partition of the seeds' 1-rings
     "Schwarz_type": SCHWARZ_BLOCK_JACOBI,
     "Schwarz_blksolver": SOLVER_UMFPACK,
     "print_level": 0,
+    "num_functions": 2,
 }
 
+# the reference's smoothers on the GPU: multicolour
+# node-block SGS (level 0: symmetric multiplicative Schwarz on the seed blocks)
+# and coarse-grid correction scaling, on the nodal SA V-cycle
+parameters_metric_mi355x_sgs = dict(
+    parameters_metric_mi355x, smoother=SMOOTHER_SGS, coarse_scaling=ON,
+    Schwarz_type=SCHWARZ_SYMMETRIC)
+
 # ---- the reference's presets, verbatim values (src/amg_parameters.py) ------
-hazmath_parameters_standard = {
+parameters_standard = {
     "prectype": 2, "AMG_type": UA_AMG, "cycle_type": W_CYCLE, "max_levels": 20, "maxit": 1,
     "smoother": SMOOTHER_SGS, "relaxation": 1.2, "presmooth_iter": 1, "postsmooth_iter": 1,
     "coarse_dof": 100, "coarse_solver": 32, "coarse_scaling": ON, "aggregation_type": VMB,
     "strong_coupled": 0.1, "max_aggregation": 100, "Schwarz_levels": 0, "print_level": 10,
 }
-hazmath_parameters_standard_schwarz = dict(
-    hazmath_parameters_standard, Schwarz_levels=1, Schwarz_mmsize=100, Schwarz_maxlvl=1,
+parameters_standard_schwarz = dict(
+    parameters_standard, Schwarz_levels=1, Schwarz_mmsize=100, Schwarz_maxlvl=1,
     Schwarz_type=SCHWARZ_SYMMETRIC, Schwarz_blksolver=32, print_level=5)
-hazmath_parameters_metric = {
+parameters_metric = {
     "AMG_type": UA_AMG, "cycle_type": W_CYCLE, "max_levels": 20, "maxit": 1,
     "smoother": SMOOTHER_SGS, "relaxation": 1.2, "presmooth_iter": 1, "postsmooth_iter": 1,
     "coarse_dof": 100, "coarse_solver": 32, "coarse_scaling": ON, "aggregation_type": HEM,
     "strong_coupled": 0.1, "max_aggregation": 100, "amli_degree": 3, "Schwarz_levels": 0,
     "print_level": 5,
 }
-hazmath_parameters_metric_schwarz = dict(
-    hazmath_parameters_metric, Schwarz_levels=1, Schwarz_mmsize=100, Schwarz_maxlvl=1,
+parameters_metric_schwarz = dict(
+    parameters_metric, Schwarz_levels=1, Schwarz_mmsize=100, Schwarz_maxlvl=1,
     Schwarz_type=SCHWARZ_SYMMETRIC, Schwarz_blksolver=32)
+# round-1 names of the same verbatim dicts
+hazmath_parameters_standard = parameters_standard
+hazmath_parameters_standard_schwarz = parameters_standard_schwarz
+hazmath_parameters_metric = parameters_metric
+hazmath_parameters_metric_schwarz = parameters_metric_schwarz
 
 
 def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
-    """Map a HAZmath parameter dict onto GPU-parallel components.
-
-    Returns (mapped dict, list of human-readable substitutions)."""
+    """Map a HAZmath parameter dict onto implemented components (explicit
+    opt-in).  Returns (mapped dict, list of human-readable substitutions)."""
     out = dict(params)
     notes = []
-    if out.get('smoother') in (SMOOTHER_GS, SMOOTHER_SGS):
-        notes.append('smoother SGS/GS -> SMOOTHER_JACOBI_RHO (relaxation/rho(D^-1A) Jacobi)')
-        out['smoother'] = SMOOTHER_JACOBI_RHO
     if out.get('aggregation_type', MIS) != MIS:
         notes.append('aggregation_type %r -> MIS (deterministic parallel MIS-2)'
                      % out.get('aggregation_type'))
         out['aggregation_type'] = MIS
-    if out.get('coarse_scaling', OFF) == ON:
-        notes.append('coarse_scaling ON -> OFF (keeps the cycle linear/symmetric for CG)')
-        out['coarse_scaling'] = OFF
-    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type') != SCHWARZ_BLOCK_JACOBI:
-        notes.append('Schwarz_type %r -> SCHWARZ_BLOCK_JACOBI (additive seed blocks)'
-                     % out.get('Schwarz_type'))
-        out['Schwarz_type'] = SCHWARZ_BLOCK_JACOBI
+    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_maxlvl', 1) > 1:
+        notes.append('Schwarz_maxlvl %d -> 1 (non-overlapping partition of the seeds\' 1-rings)'
+                     % out['Schwarz_maxlvl'])
+        out['Schwarz_maxlvl'] = 1
     if out.get('Schwarz_levels', 0) > 1:
         notes.append('Schwarz_levels %d -> 1' % out['Schwarz_levels'])
         out['Schwarz_levels'] = 1
+    smo = out.get('smoother', SMOOTHER_JACOBI_RHO)
+    want = {SMOOTHER_SGS: SCHWARZ_SYMMETRIC, SMOOTHER_GS: SCHWARZ_FORWARD}.get(smo, SCHWARZ_BLOCK_JACOBI)
+    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type', want) != want:
+        notes.append('Schwarz_type %r -> %r (the level-0 seed blocks use the level smoother)'
+                     % (out.get('Schwarz_type'), want))
+        out['Schwarz_type'] = want
+    if smo in (SMOOTHER_GS, SMOOTHER_SGS) and out.get('num_functions', 1) != 2:
+        notes.append('num_functions -> 2 (the multicolour GS smoothers are node-block smoothers)')
+        out['num_functions'] = 2
     out.pop('prectype', None)
     return out, notes
 
 
-# reference names -> GPU-mapped presets (drop-in for src/amg_parameters.py)
-parameters_standard = to_gpu_profile(hazmath_parameters_standard)[0]
-parameters_standard_schwarz = to_gpu_profile(hazmath_parameters_standard_schwarz)[0]
-parameters_metric = to_gpu_profile(hazmath_parameters_metric)[0]
-parameters_metric_schwarz = to_gpu_profile(hazmath_parameters_metric_schwarz)[0]
+# the reference presets through to_gpu_profile
+parameters_standard_gpu_mapped = to_gpu_profile(parameters_standard)[0]
+parameters_standard_schwarz_gpu_mapped = to_gpu_profile(parameters_standard_schwarz)[0]
+parameters_metric_gpu_mapped = to_gpu_profile(parameters_metric)[0]
+parameters_metric_schwarz_gpu_mapped = to_gpu_profile(parameters_metric_schwarz)[0]
 
 
 def make_params(parameters: dict | None = None, **overrides) -> _lib.mamg_params:

@@ -92,16 +92,14 @@ class _Product:
 
 def get_hazmath_metric_precond_mono(A, W, bcs=None, parameters=None, interface_dofs=None, **kw):
     """metricAMG(A, W, idofs=interface_dofs, parameters=parameters)  (src/utils.py:56-90).
-    ``parameters`` None -> the GPU profile (parameters_metric_mi355x); a
-    HAZmath dict is mapped with ``to_gpu_profile`` first (substitutions in
-    ``.substitutions``)."""
-    notes = []
+    ``parameters`` None -> the GPU profile (parameters_metric_mi355x).  A dict
+    is used as given: a HAZmath preset with a component this build lacks
+    (e.g. HEM aggregation) raises MamgError; ``parameters.to_gpu_profile``
+    is the explicit opt-in mapping."""
     if parameters is None:
         parameters = P.parameters_metric_mi355x
-    else:
-        parameters, notes = P.to_gpu_profile(parameters)
     B = MetricAMG(A, W, idofs=interface_dofs, parameters=parameters, **kw)
-    B.substitutions = notes
+    B.substitutions = []
     return B
 
 
@@ -119,7 +117,7 @@ def get_hazmath_metric_precond(A, W, bcs=None, parameters=None, interface_dofs=N
 def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs=None, **kw):
     """Plain (non-metric) AMG on the monolithic matrix (src/utils.py:15-42):
     no interface seeds, point smoothers."""
-    params = dict(P.parameters_metric_mi355x) if parameters is None else P.to_gpu_profile(parameters)[0]
+    params = dict(P.parameters_metric_mi355x) if parameters is None else dict(parameters)
     params['Schwarz_levels'] = 0
     return MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
 

@@ -37,6 +37,9 @@ def _lib():
     L.oracle_apply.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_void_p, C.c_void_p]
     L.oracle_num_threads.restype = C.c_int
+    L.oracle_pcg.restype = C.c_int
+    L.oracle_pcg.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                             C.c_void_p, C.c_double, C.c_int, C.c_void_p, C.c_void_p]
     return L
 
 
@@ -84,6 +87,21 @@ class CHierarchy:
         return z
 
     __call__ = apply
+
+    def pcg(self, b, tolerance=1e-8, maxiter=500):
+        """cbc.block ConjGrad on level 0's A with this cycle as B (C, OpenMP):
+        returns (x, residuals)."""
+        b = np.ascontiguousarray(b, np.float64)
+        n = len(b)
+        x = np.zeros(n)
+        res = np.zeros(maxiter + 1)
+        w = np.empty(4 * n)
+        it = self.L.oracle_pcg(C.cast(self.arr, C.c_void_p), len(self.levels), self.wcycle, self.nu1,
+                               self.nu2, self.maxit, b.ctypes.data, x.ctypes.data, float(tolerance),
+                               int(maxiter), res.ctypes.data, w.ctypes.data)
+        if it < 0:
+            raise ValueError('Matrix is not positive')
+        return x, list(res[:it + 1])
 
     def threads(self):
         return self.L.oracle_num_threads()

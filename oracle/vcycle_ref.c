@@ -127,3 +127,53 @@ int oracle_num_threads(void) {
   }
   return n;
 }
+
+int oracle_spmv(const ocsr* A, const double* x, double* y) {
+  spmv(A, x, y);
+  return 0;
+}
+
+static double dotp(int64_t n, const double* a, const double* b) {
+  double s = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : s)
+  for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
+  return s;
+}
+
+/*
+ * cbc.block ConjGrad (mamg_oracle.pcg, krylov.ConjGrad) with B = oracle_apply
+ * on L and the operator L[0].A: x from 0, residuals[k] = sqrt(<r_k, B r_k>),
+ * absolute tolerance.  Work: 5 vectors of L[0].n (caller-owned in w).
+ * Returns the iteration count (-1: <r,Br> < 0 at the start).
+ */
+int oracle_pcg(olevel* L, int nlev, int wcyc, int nu1, int nu2, int maxit, const double* b,
+               double* x, double tol, int maxiter, double* residuals, double* w) {
+  const int64_t n = L[0].n;
+  double *r = w, *z = w + n, *d = w + 2 * n, *q = w + 3 * n;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) { x[i] = 0.0; r[i] = b[i]; }
+  oracle_apply(L, nlev, wcyc, nu1, nu2, maxit, r, z);
+  memcpy(d, z, n * sizeof(double));
+  double rz = dotp(n, r, z);
+  if (rz < 0) return -1;
+  residuals[0] = __builtin_sqrt(rz);
+  int it = 0;
+  while (residuals[it] > tol && it < maxiter) {
+    spmv(&L[0].A, d, q);
+    const double dq = dotp(n, d, q);
+    if (dq == 0.0) break;
+    const double alpha = rz / dq;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) { x[i] = x[i] + alpha * d[i]; r[i] = r[i] - alpha * q[i]; }
+    oracle_apply(L, nlev, wcyc, nu1, nu2, maxit, r, z);
+    const double rz_prev = rz;
+    rz = dotp(n, r, z);
+    if (rz < 0) break;
+    const double beta = rz / rz_prev;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) d[i] = z[i] + beta * d[i];
+    residuals[it + 1] = __builtin_sqrt(rz);
+    ++it;
+  }
+  return it;
+}

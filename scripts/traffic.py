@@ -79,7 +79,13 @@ def main():
         kernels[c] = round(fb + wb, 1)
         detail[c] = {'grid': f[c][0], 'launches': f[c][2], 'fetch_bytes': round(fb, 1),
                      'write_bytes': round(wb, 1)}
-    out = {'layout': a.layout, 'N': a.N, 'post': a.post, 'a0': a.a0, 'kernels': kernels, 'detail': detail,
+    import hashlib
+    import os
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'metric-amg-examples_amd',
+                       'csrc', 'device.hip')
+    sha = hashlib.sha256(open(src, 'rb').read()).hexdigest()
+    out = {'layout': a.layout, 'N': a.N, 'post': a.post, 'a0': a.a0, 'device_src_sha256': sha,
+           'kernels': kernels, 'detail': detail,
            'calibration': 'bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (profiles/r01_pmc_calibration.txt)'}
     json.dump(out, open(a.out, 'w'), indent=1)
     print(json.dumps(out))

@@ -33,15 +33,18 @@ def test_params_struct_layout(lib_built):
     assert p.abi_version == 2 and p.post_fusion == 1 and p.AMG_type == 2 and p.cycle_type == 1
     assert abs(p.relaxation - 4.0 / 3.0) < 1e-15 and p.coarse_dof == 100
     assert p.num_functions == 1 and p.node_block_smoother == 1
+    assert M.parameters.make_params(M.parameters.parameters_metric_mi355x).num_functions == 2
     d = M.parameters.params_to_dict(p)
     assert set(M.parameters.KEYS) - {'prectype'} <= set(d)
 
 
 @pytest.mark.parametrize('bad,code', [
-    (dict(smoother=11), -4),                 # SGS rejected
+    (dict(smoother=11), -4),                 # SGS is a node-block smoother: num_functions 2
     (dict(aggregation_type=5), -4),          # HEM rejected
-    (dict(coarse_scaling=1), -4),
-    (dict(Schwarz_type=3), -4),              # multiplicative Schwarz rejected
+    (dict(coarse_scaling=2), -1),
+    (dict(Schwarz_type=3), -4),              # multiplicative seed blocks need the SGS smoother
+    (dict(num_functions=2, smoother=11, Schwarz_type=4), -4),
+    (dict(Schwarz_maxlvl=2), -4),            # overlapping seed + ring blocks
     (dict(cycle_type=3), -4),
     (dict(max_levels=0), -1),
     (dict(spmv_lanes=3), -1),
@@ -59,16 +62,23 @@ def test_rejects_unsupported(lib_built, bad, code):
 def test_reference_presets_map_and_report(lib_built):
     import metric_amg_examples_amd as M
     P = M.parameters
-    mapped, notes = P.to_gpu_profile(P.hazmath_parameters_metric_schwarz)
-    assert mapped['smoother'] == P.SMOOTHER_JACOBI_RHO and mapped['aggregation_type'] == P.MIS
-    assert mapped['Schwarz_type'] == P.SCHWARZ_BLOCK_JACOBI and mapped['coarse_scaling'] == P.OFF
-    assert len(notes) >= 3
-    # the raw reference preset is rejected loudly
+    # the reference's names carry the reference's values and are rejected
+    # loudly where a component is missing (HEM aggregation), never remapped
+    assert P.parameters_metric_schwarz['aggregation_type'] == P.HEM
+    assert P.parameters_metric_schwarz['smoother'] == P.SMOOTHER_SGS
     from mamg_oracle import laplace1d
-    with pytest.raises(M._lib.MamgError):
-        M.HostHierarchy(laplace1d(30), parameters=P.hazmath_parameters_metric_schwarz)
-    # the mapped one builds (UA + W-cycle)
-    H = M.HostHierarchy(laplace1d(300), parameters=P.parameters_metric_schwarz)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy(laplace1d(30), parameters=P.parameters_metric_schwarz)
+    assert ei.value.code == -4 and len(str(ei.value)) > 20
+    # explicit mapping keeps what is implemented (UA, W, SGS, coarse scaling,
+    # symmetric multiplicative seed blocks) and reports what it changes
+    mapped, notes = P.to_gpu_profile(P.parameters_metric_schwarz)
+    assert mapped['smoother'] == P.SMOOTHER_SGS and mapped['aggregation_type'] == P.MIS
+    assert mapped['Schwarz_type'] == P.SCHWARZ_SYMMETRIC and mapped['coarse_scaling'] == P.ON
+    assert mapped['num_functions'] == 2 and any('HEM' in n or '5' in n for n in notes)
+    assert P.parameters_metric_schwarz_gpu_mapped == mapped
+    H = M.HostHierarchy(laplace1d(300), parameters=P.parameters_standard_gpu_mapped,
+                        num_functions=1, smoother=P.SMOOTHER_JACOBI_RHO)
     assert H.num_levels >= 2
     with pytest.raises(KeyError):
         P.make_params({'no_such_key': 1})

@@ -187,7 +187,6 @@ def test_post_operator_k_equals_merged(lib_built, monkeypatch, sell):
     same cycle up to summation order."""
     M = _mamg()
     monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1' if sell == '1' else str(1 << 20))
-    monkeypatch.setenv('MAMG_POST_SELL', sell)
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
     zs, fmts = [], []
@@ -204,38 +203,15 @@ def test_post_operator_k_equals_merged(lib_built, monkeypatch, sell):
     assert rel(zs[0], h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
 
 
-@pytest.mark.parametrize('remap', ['0', '1', '2'])
-def test_symmetric_blocks_and_xcd_remap_bitwise(lib_built, monkeypatch, remap):
-    """The symmetric-block format (3 doubles per 2x2 block, chosen at upload
-    when every block of A_l has (0,1) == (1,0) bitwise -- the bidomain A_0)
-    and the XCD row order change only where data lives and which workgroup
-    computes a row: the apply is bitwise identical to the plain layout."""
-    M = _mamg()
-    s = M.problems.bidomain(3, 16, 1e6)
-    A = s.scipy()
-    r = mo.seeded_rhs(s.N)
-    outs = []
-    for sym in ('1', '0'):
-        monkeypatch.setenv('MAMG_SYM_BLOCKS', sym)
-        monkeypatch.setenv('MAMG_XCD_REMAP', remap if sym == '1' else '0')
-        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
-        outs.append(B * r)
-        B.close()
-    assert np.array_equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e3, dict(maxit=2, presmooth_iter=2,
                                                                                    postsmooth_iter=2)),
                                         (3, 16, 1e4, dict(post_fusion=0))])
-@pytest.mark.parametrize('env', [dict(), dict(MAMG_HALF_U='8'), dict(MAMG_HALF_REMAP='0')])
-def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw, env):
+def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw):
     """Half-symmetric ELL-64 A_0 (upper blocks streamed, lower blocks read
     through their mirrors) sums every row in the full row's block order: the
     apply and the device PCG are bitwise those of full SELL-64 storage."""
     M = _mamg()
     monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
     r = mo.seeded_rhs(s.N)
@@ -310,7 +286,6 @@ def test_sell_layout_matches_oracle(lib_built, monkeypatch, dim, n, g, kw):
     at benchmark size) forced onto every short-row level of small problems:
     all epilogues, field-major x (maxit > 1, PCG), the fused post kernel."""
     monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
-    monkeypatch.setenv('MAMG_SELL_POST', '1')
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
@@ -404,3 +379,49 @@ def test_large_properties_3d(lib_built):
     lin = B.matvec(2.0 * r + q)
     assert (torch.linalg.norm(lin - (2.0 * Br + Bq)) / torch.linalg.norm(lin)).item() < 1e-12
     assert torch.equal(B.matvec(r), Br)
+
+
+def test_host_apply_after_queued_device_apply(lib_built):
+    """A device-pointer apply queued on torch's stream and a host-pointer
+    apply (handle stream) right after it share the handle's scratch vectors:
+    the handle serializes them, both equal the oracle."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    r1, r2 = mo.seeded_rhs(s.N, 1), mo.seeded_rhs(s.N, 2)
+    big = torch.randn(4096, 4096, device='cuda')
+    for _ in range(3):
+        big = big @ big * 1e-3                  # keep torch's stream busy first
+    zt = B.matvec(torch.as_tensor(r1).cuda())
+    z2 = B * r2                                 # host apply, immediately
+    torch.cuda.synchronize()
+    assert rel(zt.cpu().numpy(), h.apply(r1)) < APPLY_TOL
+    assert rel(z2, h.apply(r2)) < APPLY_TOL
+
+
+def test_graph_cache_eviction(lib_built):
+    """More than 16 distinct (r, z) buffer pairs: the graph cache evicts
+    (after the handle's queued work finished) and every result is right."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(2, 32, 1e3)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    rs = [mo.seeded_rhs(s.N, k) for k in range(24)]
+    outs = [B.matvec(torch.as_tensor(r).cuda()) for r in rs]      # fresh z each time
+    torch.cuda.synchronize()
+    for r, z in zip(rs, outs):
+        assert rel(z.cpu().numpy(), h.apply(r)) < APPLY_TOL
+
+
+def test_device_conjgrad_requires_own_operator(lib_built):
+    M = _mamg()
+    s = M.problems.bidomain(2, 16, 1e2)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    with pytest.raises(ValueError):
+        M.ConjGrad(A.copy(), precond=B, device=True) * mo.seeded_rhs(s.N)

@@ -1,0 +1,108 @@
+"""Every BASELINE.json configuration on the GPU, at its full size (VERDICT r1
+items N1 / 'untested configs'):
+
+* bidomain_2d nrefs=6 gamma=1e6 (2-D n=1024, N=2.1M) and bidomain_3d nrefs=6
+  gamma=1e6 (3-D n=256, N=34M, the north-star config): one GPU apply against
+  the oracle's C cycle (oracle/vcycle_ref.c) on the same hierarchy (the GPU
+  setup's, copied back; the setup is bitwise the oracle's, tests/
+  test_gpu_setup.py) to 1e-10, and the PCG iteration count of the device PCG
+  equal to the CPU PCG's (oracle_pcg: the C cycle + C SpMV, cbc.block
+  ConjGrad, tolerance 1e-8 absolute, src/bidomain_3d.py:149-157), residual
+  histories within 1e-6.
+* bidomain_3d nrefs=5 (N=4.3M): the same.
+* emi_3d nrefs=5 gamma=1e6 (n=64, N=278,850; src/emi_3d.py:119-143, tolerance
+  1e-10): block-form preconditioner R^T Minv R, device apply and PCG against
+  the C cycle on the host-setup hierarchy (CSR layout).
+The bench's own line repeats the 3-D nrefs=6 PCG check (pcg.cpu_pcg).
+"""
+import sys
+import time
+
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+
+def _M():
+    import metric_amg_examples_amd as M
+    return M
+
+
+def say(*a):
+    print('[configs]', *a, file=sys.stderr, flush=True)
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def c_hierarchy(H, sysm_or_A):
+    import cref
+    M = _M()
+    ip, ix, dv, n, _ = M.amg.csr_arrays(sysm_or_A)
+    lv = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
+    lv[0]['A'] = (ip, ix, dv, (n, n))
+    p = H.params
+    return cref.CHierarchy(lv, p.cycle_type == 2, p.presmooth_iter, p.postsmooth_iter, p.maxit)
+
+
+@pytest.mark.parametrize('dim,nrefs', [(2, 6), (3, 5), (3, 6)])
+def test_bidomain_baseline_config_apply_and_pcg(lib_built, dim, nrefs):
+    import torch
+    M = _M()
+    n = M.problems.finest_n(dim, nrefs)
+    t0 = time.time()
+    s = M.problems.bidomain(dim, n, 1e6)
+    say('%dD n=%d N=%d generated in %.1fs' % (dim, n, s.N, time.time() - t0))
+    B = M.MetricAMG(s, s.W, idofs=s.idofs, num_functions=2, setup='gpu')
+    r = M.problems.seeded_rhs(s.N)
+    rt = torch.as_tensor(r).cuda()
+    z = B.matvec(rt).cpu().numpy()
+    H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True)
+    assert H.num_levels == B.num_levels
+    ch = c_hierarchy(H, s)
+    zc = ch.apply(r)
+    say('apply rel diff GPU vs C cycle: %.2e' % rel(z, zc))
+    assert rel(z, zc) < 1e-10
+    solver = M.ConjGrad(s, precond=B, tolerance=1e-8, maxiter=500)       # device PCG
+    B._Aop = s
+    solver * r
+    t0 = time.time()
+    _, cres = ch.pcg(r, 1e-8, 500)
+    say('PCG iterations GPU %d, CPU %d (CPU %.1fs, %d threads)'
+        % (len(solver.residuals) - 1, len(cres) - 1, time.time() - t0, ch.threads()))
+    assert len(solver.residuals) == len(cres)
+    assert np.allclose(solver.residuals, cres, rtol=1e-6, atol=0)
+    H.close()
+    B.close()
+
+
+def test_emi_3d_nrefs5_block_form(lib_built):
+    import torch
+    M = _M()
+    n = 2 ** (2 + 5 - 1)                                   # src/emi_3d.py:119, nrefs=5
+    s = M.problems.emi(3, n, 1e6)
+    assert s.N == 278850
+    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+    Bm = BB.monolithic
+    A = s.scipy()
+    b = [M.problems.seeded_rhs(s.W[0], 1234), M.problems.seeded_rhs(s.W[1], 4321)]
+    bb = np.concatenate(b)
+    # the same hierarchy on the host (setup = the product's host setup, which
+    # tests/test_host_setup.py pins bitwise to the Python oracle)
+    seeds = Bm.idofs
+    H = M.HostHierarchy(A, idofs=seeds, num_functions=2)
+    ch = c_hierarchy(H, A)
+    z = (Bm.matvec(torch.as_tensor(bb).cuda())).cpu().numpy()
+    assert rel(z, ch.apply(bb)) < 1e-10
+    solver = M.ConjGrad(s, precond=BB, tolerance=1e-10, maxiter=500)     # src/emi_3d.py:143
+    solver * b
+    _, cres = ch.pcg(bb, 1e-10, 500)
+    say('EMI 3-D nrefs=5: PCG iterations GPU %d, CPU %d' % (len(solver.residuals) - 1, len(cres) - 1))
+    assert len(solver.residuals) == len(cres)
+    assert np.allclose(solver.residuals, cres, rtol=1e-6, atol=0)
+    assert len(solver.residuals) < 120
+    H.close()
