@@ -37,6 +37,12 @@ CLASS_NAMES = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_p
                'coarse_levels', 'coarsest_dense', 'misc', 'comm']
 
 
+PROFILE_NAMES = {'jacobi': 'mi355x_sa_v: nodal SA V-cycle, node-block Jacobi',
+                 'poly': 'mi355x_poly: nodal SA V-cycle, Chebyshev steps of node-block Jacobi',
+                 'sgs': 'mi355x_sgs: nodal SA V-cycle, multicolour node-block SGS',
+                 'gs': 'nodal SA V-cycle, multicolour node-block GS'}
+
+
 def log(*a):
     print('[bench]', *a, file=sys.stderr, flush=True)
 
@@ -87,8 +93,10 @@ def main():
                     help='N = 1: also set up and solve with the multicolour-SGS profile (iterations, seconds)')
     ap.add_argument('--setup', choices=('gpu', 'host'), default='gpu',
                     help='N = 1 hierarchy construction: GPU setup (default) or host setup + upload')
-    ap.add_argument('--smoother', choices=('jacobi', 'sgs', 'gs'), default='jacobi',
-                    help='level smoother: node-block Jacobi (mi355x_sa_v) or multicolour node-block SGS / GS')
+    ap.add_argument('--smoother', choices=('jacobi', 'poly', 'sgs', 'gs'), default='jacobi',
+                    help='level smoother: node-block Jacobi (mi355x_sa_v), Chebyshev steps of it (poly), '
+                         'or multicolour node-block SGS / GS')
+    ap.add_argument('--poly-degree', type=int, default=2)
     ap.add_argument('--scaling', type=int, default=0, help='coarse-grid correction scaling (coarse_scaling ON)')
     ap.add_argument('--cycle', choices=('V', 'W'), default='V')
     ap.add_argument('--compare-host-setup', action='store_true',
@@ -96,8 +104,9 @@ def main():
     args = ap.parse_args()
     if args.pcg < 0:
         args.pcg = 1 if int(os.environ.get('WORLD_SIZE', '1')) == 1 else 0
-    prof = dict(smoother={'jacobi': 3, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
-                cycle_type={'V': 1, 'W': 2}[args.cycle])
+    prof = dict(smoother={'jacobi': 3, 'poly': 12, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
+                cycle_type={'V': 1, 'W': 2}[args.cycle], poly_degree=args.poly_degree,
+                Schwarz_type={'sgs': 3, 'gs': 1}.get(args.smoother, 4))
 
     import torch
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -245,14 +254,19 @@ def main():
     profiles = None
     if args.compare_profiles and world == 1 and args.pcg:
         profiles = []
-        for name, kw in (('mi355x_sgs (multicolour node-block SGS, coarse scaling ON)',
-                          dict(smoother=11, coarse_scaling=1)),):
+        for name, kw in (('mi355x_poly (Chebyshev degree 2 of node-block Jacobi)', dict(smoother=12)),
+                         ('mi355x_sa_v (node-block Jacobi)', dict(smoother=3)),
+                         ('mi355x_sgs (multicolour node-block SGS, coarse scaling ON)',
+                          dict(smoother=11, coarse_scaling=1, Schwarz_type=3)),):
+            if kw['smoother'] == prof['smoother'] and kw.get('coarse_scaling', 0) == prof['coarse_scaling']:
+                continue
             torch.cuda.synchronize(dev)
             t0 = time.time()
             B2 = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu', **kw)
             torch.cuda.synchronize(dev)
             ts = time.time() - t0
-            ms2, _, _ = B2.time_apply(r, z, 5, 0, stream)
+            z2 = torch.zeros_like(r)              # z keeps the default profile's apply (CPU check)
+            ms2, _, _ = B2.time_apply(r, z2, 5, 0, stream)
             s2 = M.ConjGrad(sysm, precond=B2, tolerance=1e-8, maxiter=500)
             B2._Aop = sysm
             torch.cuda.synchronize(dev)
@@ -264,18 +278,24 @@ def main():
                              'setup_s': round(ts, 4), 'setup_plus_pcg_s': round(ts + tp2, 4),
                              'ms_per_apply': round(ms2, 4)})
             B2.close()
-            del s2
+            del s2, z2
 
     # ---- CPU baseline: oracle C restatement on the same hierarchy, host cores
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    c_cycle = args.smoother in ('jacobi', 'poly') and not args.scaling   # what vcycle_ref.c restates
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and c_cycle:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import cref
+        import mamg_oracle as mo
         if H is None:       # same hierarchy bits, from the GPU setup copied back
             H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, gpu=True)
         lv = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
         lv[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
-        ch = cref.CHierarchy(lv)
+        poly = None
+        if args.smoother == 'poly':
+            poly = mo.poly_weights(mo.Params(smoother='POLY', poly_degree=args.poly_degree,
+                                             relaxation=B.params.relaxation, poly_ratio=B.params.poly_ratio))
+        ch = cref.CHierarchy(lv, wcycle=args.cycle == 'W', poly=poly)
         ch.apply(r_full)                                     # warm (page-in)
         t0 = time.time()
         for _ in range(args.cpu_sample):
@@ -365,8 +385,9 @@ def main():
         'dtype': 'f64',
         'data': 'synthetic (P1 bidomain matrix generated in-library; r = uniform(-1,1), seed 1234)',
         'config': {
-            'workload': 'bidomain_%dd nrefs=%d gamma=%g metric_mono (profile mi355x_sa_v, nodal SA V-cycle)'
-                        % (args.dim, args.nrefs, args.gamma),
+            'workload': 'bidomain_%dd nrefs=%d gamma=%g metric_mono (profile %s)'
+                        % (args.dim, args.nrefs, args.gamma, PROFILE_NAMES[args.smoother]
+                           + (', W-cycle' if args.cycle == 'W' else '') + (', coarse scaling' if args.scaling else '')),
             'n': n, 'N': sysm.N, 'nnz': sysm.nnz, 'levels': levels,
             'parallelism': 'single' if world == 1 else 'row-partition x%d (RCCL halo)' % world,
             'device_layout': layout,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MAMG_ABI_VERSION 2
+#define MAMG_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------- */
 enum {
@@ -48,9 +48,16 @@ enum { MAMG_V_CYCLE = 1, MAMG_W_CYCLE = 2 };                     /* cycle_type *
 enum {                                                          /* smoother   */
   MAMG_SMOOTHER_JACOBI = 1,      /* x += w D^-1 r, w = relaxation             */
   MAMG_SMOOTHER_L1DIAG = 2,      /* x += w L1^-1 r, L1_ii = sum_j |a_ij|      */
-  MAMG_SMOOTHER_JACOBI_RHO = 3,  /* x += (w/rho(D^-1A)) D^-1 r  (default)     */
-  MAMG_SMOOTHER_GS = 10,         /* HAZmath sequential smoothers: rejected    */
-  MAMG_SMOOTHER_SGS = 11
+  MAMG_SMOOTHER_JACOBI_RHO = 3,  /* x += (w/rho(D^-1A)) D^-1 r                */
+  /* HAZmath's GS / SGS in a GPU-parallel order: multicolour node-block
+   * Gauss-Seidel (forward / forward+backward), BSR2 layout only */
+  MAMG_SMOOTHER_GS = 10,
+  MAMG_SMOOTHER_SGS = 11,
+  /* polynomial smoother (HAZmath/FASP SMOOTHER_POLY): Chebyshev of degree
+   * poly_degree in W A on [relaxation/poly_ratio, relaxation], W the
+   * JACOBI_RHO (block) smoother, applied as poly_degree weighted steps
+   * x += w_k W (b - A x); pre steps k = 1..m, post m..1 (default profile) */
+  MAMG_SMOOTHER_POLY = 12
 };
 enum {                                                   /* aggregation_type  */
   MAMG_VMB = 1, MAMG_MIS = 2, MAMG_MWM = 3, MAMG_HEC = 4, MAMG_HEM = 5
@@ -70,13 +77,13 @@ typedef struct mamg_params {
   int32_t cycle_type;        /* MAMG_V_CYCLE (default) | MAMG_W_CYCLE        */
   int32_t max_levels;        /* 20                                           */
   int32_t maxit;             /* cycles per apply, 1                          */
-  int32_t smoother;          /* MAMG_SMOOTHER_JACOBI_RHO                     */
+  int32_t smoother;          /* MAMG_SMOOTHER_JACOBI_RHO (mamg_params_default) */
   double relaxation;         /* 4/3                                          */
   int32_t presmooth_iter;    /* 1                                            */
   int32_t postsmooth_iter;   /* 1                                            */
   int32_t coarse_dof;        /* 100                                          */
   int32_t coarse_solver;     /* 32 -> dense direct                           */
-  int32_t coarse_scaling;    /* MAMG_OFF (ON unsupported: non-linear cycle)  */
+  int32_t coarse_scaling;    /* MAMG_OFF | MAMG_ON: e <- <b_c,e>/<A_c e,e> e  */
   int32_t aggregation_type;  /* MAMG_MIS (deterministic parallel MIS-2)      */
   double strong_coupled;     /* SoC threshold theta, 0.0                     */
   int32_t max_aggregation;   /* accepted, unused by MIS-2 (documented)       */
@@ -103,6 +110,9 @@ typedef struct mamg_params {
    * x = x1 + P e + W (r1 - (A P) e), with A P kept from the Galerkin product
    * (one pass over [P | AP] instead of P then A).  1 */
   int32_t post_fusion;
+  /* MAMG_SMOOTHER_POLY: Chebyshev degree (1..8, 2) and interval ratio (16) */
+  int32_t poly_degree;
+  double poly_ratio;
 } mamg_params;
 
 /* Host CSR view (caller-owned). */

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('MAMG_LIB', os.path.join(_HERE, 'libmamg.so'))
 
-MAMG_ABI_VERSION = 2
+MAMG_ABI_VERSION = 3
 OK, ERR_ARG, ERR_HIP, ERR_SETUP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_BREAKDOWN = 0, -1, -2, -3, -4, -5, -6
 
 
@@ -40,6 +40,7 @@ class mamg_params(C.Structure):
         ('max_coarse_dense', C.c_int32), ('device', C.c_int32), ('spmv_lanes', C.c_int32),
         ('num_functions', C.c_int32), ('node_block_smoother', C.c_int32),
         ('sa_block_diag', C.c_int32), ('post_fusion', C.c_int32),
+        ('poly_degree', C.c_int32), ('poly_ratio', C.c_double),
     ]
 
 

@@ -149,6 +149,8 @@ void mamg_params_default(mamg_params* p) {
   p->node_block_smoother = 1;
   p->sa_block_diag = 1;
   p->post_fusion = 1;
+  p->poly_degree = 2;
+  p->poly_ratio = 16.0;
 }
 
 int mamg_gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz) {

@@ -523,6 +523,13 @@ __global__ __launch_bounds__(256) void scale_kernel(int64_t n, const double* __r
   if (i < n) x[i] = w[i] * b[i];
 }
 
+// out = w * in (SMOOTHER_POLY step smoothers w_k W, built once at upload)
+__global__ __launch_bounds__(256) void wscale_kernel(int64_t n, double w, const double* __restrict__ in,
+                                                     double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = w * in[i];
+}
+
 __global__ __launch_bounds__(256) void axpy_kernel(int64_t n, const double* __restrict__ e,
                                                    double* x) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -982,6 +989,11 @@ struct DLevel {
   DBsr KPb;                // BSR2 post fusion: K = P - W (A P), one operator (default)
   dv4* Wd = nullptr;       // BSR2 layout: 2x2 smoother block per node
   double* winv = nullptr;
+  // SMOOTHER_POLY: the step smoothers w_k W, k = 1..m (BSR2: Wk; CSR: WBk
+  // sharing WB's pattern, or winvk); empty for the Jacobi smoothers
+  std::vector<dv4*> Wk;
+  std::vector<DCsr> WBk;
+  std::vector<double*> winvk;
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr,
          *c = nullptr, *e = nullptr;
@@ -1803,6 +1815,38 @@ inline bool gs_smoother(const mamg_params& p) {
   return p.smoother == MAMG_SMOOTHER_SGS || p.smoother == MAMG_SMOOTHER_GS;
 }
 
+// smoothing step s of a sweep sequence: the Jacobi smoothers take W every
+// step; SMOOTHER_POLY takes w_1 W .. w_m W before the coarse correction and
+// w_m W .. w_1 W after it (mamg_oracle.Hierarchy.cycle), repeated per sweep
+inline int step_index(int m, int s, bool pre) {
+  const int k = s % m;
+  return pre ? k : m - 1 - k;
+}
+const dv4* step_wd(const DLevel& L, int s, bool pre) {
+  return L.Wk.empty() ? L.Wd : L.Wk[step_index((int)L.Wk.size(), s, pre)];
+}
+const DCsr& step_wb(const DLevel& L, int s, bool pre) {
+  return L.WBk.empty() ? L.WB : L.WBk[step_index((int)L.WBk.size(), s, pre)];
+}
+const double* step_winv(const DLevel& L, int s, bool pre) {
+  return L.winvk.empty() ? L.winv : L.winvk[step_index((int)L.winvk.size(), s, pre)];
+}
+
+// SMOOTHER_POLY step smoothers w_k W of n doubles each (device copies)
+int poly_scaled(DeviceHandle* h, const double* W, int64_t n, std::vector<double*>* out, std::string* err) {
+  double w[MAMG_POLY_MAX];
+  const int m = poly_weights(h->p, w);
+  for (int k = 0; k < m; ++k) {
+    double* o = nullptr;
+    int rc = dalloc(h, &o, n, err);
+    if (rc) return rc;
+    if (n) wscale_kernel<<<nblocks(n), 256>>>(n, w[k], W, o);
+    HIPCHK(hipGetLastError());
+    out->push_back(o);
+  }
+  return MAMG_OK;
+}
+
 // Multicolour GS layout of one level from A_l's device BSR2 B and the
 // level's (scaled) smoother blocks W (only their pattern is used: a node
 // whose W block is diagonal has two 1x1 smoother blocks).  Colouring:
@@ -1924,12 +1968,21 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
       if ((rc = build_gs(h, &T, B, S.W, l, &D, err))) return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
+  if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
+  HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
+  if (p.smoother == MAMG_SMOOTHER_POLY) {
+    std::vector<double*> wk;
+    if ((rc = poly_scaled(h, S.W, 4 * nv, &wk, err))) return rc;
+    for (double* q : wk) D.Wk.push_back(reinterpret_cast<dv4*>(q));
+  }
   if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p)) {
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
-    if (g_post_k) {   // one operator K = P - W (A P) on AP's pattern
-      if ((rc = dev_kmerge(&T, Pb, Qb, S.W, &M, err))) return rc;
+    if (g_post_k) {   // one operator K = P - W (A P) on AP's pattern,
+                      // W = the first post-smoothing step's smoother
+      const double* Wpost = reinterpret_cast<const double*>(step_wd(D, 0, false));
+      if ((rc = dev_kmerge(&T, Pb, Qb, Wpost, &M, err))) return rc;
     } else {          // P and AP blocks side by side in one row window
       if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
     }
@@ -1950,8 +2003,6 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
     if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
   }
-  if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
-  HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
   HIPCHK(hipDeviceSynchronize());
   return MAMG_OK;
 }
@@ -2052,20 +2103,22 @@ void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, 
   const int clsW = l0 ? C_L0_WB : C_COARSE;
   double* X = L.t;
   double* X2 = L.t2;
+  const int steps = smoother_steps(p);
+  const int npre = p.presmooth_iter * steps, npost = p.postsmooth_iter * steps;
   if (blk) {
-    ops->push_back(csr_op(L.WB, EPI_Y, clsW, tagA, b, nullptr, nullptr, nullptr, X));
+    ops->push_back(csr_op(step_wb(L, 0, true), EPI_Y, clsW, tagA, b, nullptr, nullptr, nullptr, X));
   } else {
     Op o;
-    o.kind = OP_SCALE; o.cls = clsW; o.n = L.n; o.w = L.winv; o.x = b; o.out = X;
+    o.kind = OP_SCALE; o.cls = clsW; o.n = L.n; o.w = step_winv(L, 0, true); o.x = b; o.out = X;
     o.bytes = 24.0 * L.n;
     ops->push_back(o);
   }
-  for (int s = 1; s < p.presmooth_iter; ++s) {
+  for (int s = 1; s < npre; ++s) {
     if (blk) {
       ops->push_back(csr_op(L.A, EPI_RESID, clsS, tagA, X, nullptr, b, nullptr, L.r));
-      ops->push_back(csr_op(L.WB, EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, X2));
+      ops->push_back(csr_op(step_wb(L, s, true), EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, X2));
     } else {
-      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, L.winv, X2));
+      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, step_winv(L, s, true), X2));
     }
     std::swap(X, X2);
   }
@@ -2079,13 +2132,13 @@ void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, 
   }
   if (p.coarse_scaling) scale_ops(h, l + 1, ops);
   ops->push_back(csr_op(L.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, X, nullptr, nullptr, X));
-  for (int s = 0; s < p.postsmooth_iter; ++s) {
-    double* out = (s == p.postsmooth_iter - 1) ? xout : X2;
+  for (int s = 0; s < npost; ++s) {
+    double* out = (s == npost - 1) ? xout : X2;
     if (blk) {
       ops->push_back(csr_op(L.A, EPI_RESID, clsS, tagA, X, nullptr, b, nullptr, L.r));
-      ops->push_back(csr_op(L.WB, EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, out));
+      ops->push_back(csr_op(step_wb(L, s, false), EPI_YADD, clsW, tagA, L.r, X, nullptr, nullptr, out));
     } else {
-      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, L.winv, out));
+      ops->push_back(csr_op(L.A, EPI_JACOBI, clsS, tagA, X, X, b, step_winv(L, s, false), out));
     }
     if (out == X2) std::swap(X, X2);
   }
@@ -2145,6 +2198,8 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   const int clsW = l0 ? C_L0_WB : C_COARSE;
   const bool gs = L.gcs.size() > 1;                       // multicolour GS on this level
   const bool sgs = p.smoother == MAMG_SMOOTHER_SGS;
+  const int steps = smoother_steps(p);
+  const int npre = p.presmooth_iter * steps, npost = p.postsmooth_iter * steps;
   double* X = (gs && os == 0) ? xout : L.t;               // GS sweeps in place
   double* X2 = L.t2;
   if (gs) {   // pre: from x = 0, forward (SGS: then backward) sweeps
@@ -2155,13 +2210,13 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
       gs_sweep_ops(L, true, X, b, bs, clsS, ops);
       if (sgs) gs_sweep_ops(L, false, X, b, bs, clsS, ops);
     }
-  } else {    // first sweep from x = 0: X = W b
+  } else {    // first sweep from x = 0: X = W b (POLY: w_1 W b)
     Op o;
-    o.kind = OP_BD; o.cls = clsW; o.n = nv; o.W = L.Wd; o.b = b; o.bs = bs; o.out = X;
+    o.kind = OP_BD; o.cls = clsW; o.n = nv; o.W = step_wd(L, 0, true); o.b = b; o.bs = bs; o.out = X;
     o.bytes = 32.0 * nv + 16.0 * nv + 16.0 * nv;
     ops->push_back(o);
-    for (int s = 1; s < p.presmooth_iter; ++s) {
-      ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, X2, 0));
+    for (int s = 1; s < npre; ++s) {
+      ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, step_wd(L, s, true), X2, 0));
       std::swap(X, X2);
     }
   }
@@ -2192,25 +2247,27 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     return;
   }
   int s0 = 0;
-  if (L.KPb.nr > 0 && p.postsmooth_iter >= 1) {   // z = x1 + W r1 + K e (one operator)
-    const bool last = p.postsmooth_iter == 1;
-    ops->push_back(bsr_op(L.KPb, EPI_KPOST, clsS, tagA, C.x, 0, X, L.r, 0, L.Wd, last ? xout : X2,
-                          last ? os : 0));
+  if (L.KPb.nr > 0 && npost >= 1) {   // z = x1 + W r1 + K e (one operator, K built with this W)
+    const bool last = npost == 1;
+    ops->push_back(bsr_op(L.KPb, EPI_KPOST, clsS, tagA, C.x, 0, X, L.r, 0, step_wd(L, 0, false),
+                          last ? xout : X2, last ? os : 0));
     if (!last) std::swap(X, X2);
     s0 = 1;
-  } else if (L.PAb.nr > 0 && p.postsmooth_iter >= 1) {   // prolongation + first post sweep
-    const bool last = p.postsmooth_iter == 1;
-    ops->push_back(post_op(L.PAb, L.r, L.Wd, clsS, tagA, C.x, X, last ? xout : X2, last ? os : 0));
+  } else if (L.PAb.nr > 0 && npost >= 1) {   // prolongation + first post sweep
+    const bool last = npost == 1;
+    ops->push_back(post_op(L.PAb, L.r, step_wd(L, 0, false), clsS, tagA, C.x, X, last ? xout : X2,
+                           last ? os : 0));
     if (!last) std::swap(X, X2);
     s0 = 1;
   } else {
     ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
                           nullptr, X, 0));
   }
-  for (int s = s0; s < p.postsmooth_iter; ++s) {
-    const bool last = s == p.postsmooth_iter - 1;
+  for (int s = s0; s < npost; ++s) {
+    const bool last = s == npost - 1;
     double* out = last ? xout : X2;
-    ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, L.Wd, out, last ? os : 0));
+    ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, step_wd(L, s, false), out,
+                          last ? os : 0));
     if (!last) std::swap(X, X2);
   }
 }
@@ -2599,6 +2656,21 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
       } else {
         if ((rc = dalloc(h.get(), &D.winv, D.n, err))) return rc;
         HIPCHK(hipMemcpy(D.winv, hl.winv.data(), D.n * sizeof(double), hipMemcpyHostToDevice));
+      }
+      if (p.smoother == MAMG_SMOOTHER_POLY) {   // step smoothers w_k W (values only)
+        std::vector<double*> wk;
+        if ((rc = poly_scaled(h.get(), hl.WB.n > 0 ? D.WB.val : D.winv, hl.WB.n > 0 ? D.WB.nnz : D.n, &wk,
+                              err)))
+          return rc;
+        for (double* q : wk) {
+          if (hl.WB.n > 0) {
+            DCsr c = D.WB;
+            c.val = q;
+            D.WBk.push_back(c);
+          } else {
+            D.winvk.push_back(q);
+          }
+        }
       }
     }
     double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
@@ -3239,7 +3311,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (gs_smoother(p) || p.coarse_scaling) {
+  if (gs_smoother(p) || p.coarse_scaling || p.smoother == MAMG_SMOOTHER_POLY) {
     *err = "multi-GPU apply supports the block-Jacobi smoothers without coarse scaling";
     return MAMG_ERR_UNSUPPORTED;
   }

@@ -59,6 +59,14 @@ struct Hierarchy {
 int host_setup(const CsrView& A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* out, std::string* err);
 int check_params(const mamg_params& p, std::string* err);
+// SMOOTHER_POLY step weights w[0..poly_degree) (oracle mamg_oracle.poly_weights)
+constexpr int MAMG_POLY_MAX = 8;
+int poly_weights(const mamg_params& p, double* w);
+// smoothing steps per sweep and their weights, pre order (1 step of weight 1
+// for the Jacobi smoothers)
+inline int smoother_steps(const mamg_params& p) {
+  return p.smoother == MAMG_SMOOTHER_POLY ? p.poly_degree : 1;
+}
 
 // gen.cpp
 int gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz);

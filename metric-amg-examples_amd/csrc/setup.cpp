@@ -659,14 +659,33 @@ int smooth_prolongator_block(const CsrView& A, const Csr& T, int nf, const mamg_
 
 }  // namespace
 
+// Chebyshev polynomial of degree m in W A on [hi / poly_ratio, hi], hi =
+// relaxation (a bound of lambda_max(W A): W = (relaxation / rho_B) D^-1 with
+// rho_B a Gershgorin bound), as m Richardson steps with w_k = 1 / tau_k, tau_k
+// the polynomial's roots theta + delta cos((2k - 1) pi / (2m)), k = 1..m
+int poly_weights(const mamg_params& p, double* w) {
+  const int m = smoother_steps(p);
+  if (p.smoother != MAMG_SMOOTHER_POLY) { w[0] = 1.0; return 1; }
+  const double hi = p.relaxation, lo = hi / p.poly_ratio;
+  const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo);
+  const double pi = 3.14159265358979323846;
+  for (int k = 1; k <= m; ++k) w[k - 1] = 1.0 / (theta + delta * std::cos((2 * k - 1) * pi / (2 * m)));
+  return m;
+}
+
 int check_params(const mamg_params& p, std::string* err) {
   if (p.abi_version != MAMG_ABI_VERSION) { *err = "mamg_params.abi_version mismatch"; return MAMG_ERR_ARG; }
   if (p.AMG_type != MAMG_SA_AMG && p.AMG_type != MAMG_UA_AMG) { *err = "AMG_type must be SA_AMG or UA_AMG"; return MAMG_ERR_UNSUPPORTED; }
   if (p.cycle_type != MAMG_V_CYCLE && p.cycle_type != MAMG_W_CYCLE) { *err = "cycle_type must be V_CYCLE or W_CYCLE (AMLI/NL_AMLI/ADD not implemented)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.smoother != MAMG_SMOOTHER_JACOBI && p.smoother != MAMG_SMOOTHER_L1DIAG && p.smoother != MAMG_SMOOTHER_JACOBI_RHO &&
-      p.smoother != MAMG_SMOOTHER_GS && p.smoother != MAMG_SMOOTHER_SGS) {
-    *err = "smoother must be SMOOTHER_JACOBI, SMOOTHER_L1DIAG, SMOOTHER_JACOBI_RHO, SMOOTHER_GS or SMOOTHER_SGS";
+      p.smoother != MAMG_SMOOTHER_GS && p.smoother != MAMG_SMOOTHER_SGS && p.smoother != MAMG_SMOOTHER_POLY) {
+    *err = "smoother must be SMOOTHER_JACOBI, SMOOTHER_L1DIAG, SMOOTHER_JACOBI_RHO, SMOOTHER_GS, SMOOTHER_SGS or SMOOTHER_POLY";
     return MAMG_ERR_UNSUPPORTED;
+  }
+  if (p.smoother == MAMG_SMOOTHER_POLY &&
+      (p.poly_degree < 1 || p.poly_degree > MAMG_POLY_MAX || !(p.poly_ratio > 1.0))) {
+    *err = "SMOOTHER_POLY needs poly_degree in [1, 8] and poly_ratio > 1";
+    return MAMG_ERR_ARG;
   }
   if ((p.smoother == MAMG_SMOOTHER_GS || p.smoother == MAMG_SMOOTHER_SGS) &&
       (p.num_functions != 2 || !p.node_block_smoother)) {
@@ -779,7 +798,8 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
     for (int64_t i = 0; i < n; ++i) { dg[i] = diag_of(cur, i); dinv[i] = 1.0 / dg[i]; }
     const std::vector<double> rs = abs_rowsum(cur);
     const bool blockP = nf > 1 && p.sa_block_diag;
-    const bool need_rho = (p.AMG_type == MAMG_SA_AMG && !blockP) || p.smoother == MAMG_SMOOTHER_JACOBI_RHO;
+    const bool need_rho = (p.AMG_type == MAMG_SA_AMG && !blockP) || p.smoother == MAMG_SMOOTHER_JACOBI_RHO ||
+                          p.smoother == MAMG_SMOOTHER_POLY;
     const double rho = need_rho ? rho_estimate(cur, dinv, rs, p.rho_iters) : 0.0;
     if (l < p.Schwarz_levels && l == 0 && idofs != nullptr && n_idofs > 0) {
       rc = block_smoother(cur, idofs, n_idofs, p, &lev.WB, err);

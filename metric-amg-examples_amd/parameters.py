@@ -30,6 +30,7 @@ UA_AMG, SA_AMG = 1, 2
 V_CYCLE, W_CYCLE = 1, 2
 SMOOTHER_JACOBI, SMOOTHER_L1DIAG, SMOOTHER_JACOBI_RHO = 1, 2, 3
 SMOOTHER_GS, SMOOTHER_SGS = 10, 11
+SMOOTHER_POLY = 12            # Chebyshev polynomial in W A (HAZmath/FASP SMOOTHER_POLY)
 VMB, MIS, MWM, HEC, HEM = 1, 2, 3, 4, 5
 SCHWARZ_FORWARD, SCHWARZ_BACKWARD, SCHWARZ_SYMMETRIC, SCHWARZ_BLOCK_JACOBI = 1, 2, 3, 4
 OFF, ON = 0, 1
@@ -42,7 +43,8 @@ KEYS = ('prectype', 'AMG_type', 'cycle_type', 'max_levels', 'maxit', 'smoother',
         'Schwarz_maxlvl', 'Schwarz_type', 'Schwarz_blksolver', 'print_level',
         # build-defined extensions
         'sa_omega', 'rho_iters', 'max_coarse_dense', 'device', 'spmv_lanes',
-        'num_functions', 'node_block_smoother', 'sa_block_diag', 'post_fusion')
+        'num_functions', 'node_block_smoother', 'sa_block_diag', 'post_fusion',
+        'poly_degree', 'poly_ratio')
 
 # ---- the GPU profile "mi355x_sa_v"  -------------------
 parameters_metric_mi355x = {
@@ -69,6 +71,12 @@ parameters_metric_mi355x = {
     "print_level": 0,
     "num_functions": 2,
 }
+
+# the same hierarchy with the Chebyshev smoother (SMOOTHER_POLY, degree 2 on
+# [relaxation / 16, relaxation] of W A): half the PCG iterations of node-block
+# Jacobi for two extra level-0 SpMVs per cycle
+parameters_metric_mi355x_poly = dict(
+    parameters_metric_mi355x, smoother=SMOOTHER_POLY, poly_degree=2, poly_ratio=16.0)
 
 # the reference's smoothers on the GPU: multicolour
 # node-block SGS (level 0: symmetric multiplicative Schwarz on the seed blocks)

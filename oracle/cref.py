@@ -36,6 +36,8 @@ def _lib():
     L.oracle_apply.restype = C.c_int
     L.oracle_apply.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_void_p, C.c_void_p]
+    L.oracle_set_poly.restype = C.c_int
+    L.oracle_set_poly.argtypes = [C.c_int, C.c_void_p]
     L.oracle_num_threads.restype = C.c_int
     L.oracle_pcg.restype = C.c_int
     L.oracle_pcg.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
@@ -47,9 +49,10 @@ class CHierarchy:
     """levels: list of dicts with keys A, P, R, WB as (indptr, indices, data,
     shape) tuples, winv, Ainv, n; params: cycle info."""
 
-    def __init__(self, levels, wcycle=False, nu1=1, nu2=1, maxit=1):
+    def __init__(self, levels, wcycle=False, nu1=1, nu2=1, maxit=1, poly=None):
         self.L = _lib()
         self.keep = []
+        self.poly = np.ascontiguousarray(poly if poly is not None else [], np.float64)
         self.levels = levels
         nl = len(levels)
         self.arr = (olevel * nl)()
@@ -77,7 +80,11 @@ class CHierarchy:
                 self.keep.append(a)
                 setattr(o, w, a.ctypes.data)
 
+    def _set_poly(self):   # the C oracle keeps the POLY weights in a global
+        self.L.oracle_set_poly(len(self.poly), self.poly.ctypes.data)
+
     def apply(self, r):
+        self._set_poly()
         r = np.ascontiguousarray(r, np.float64)
         z = np.zeros_like(r)
         rc = self.L.oracle_apply(C.cast(self.arr, C.c_void_p), len(self.levels), self.wcycle,
@@ -91,6 +98,7 @@ class CHierarchy:
     def pcg(self, b, tolerance=1e-8, maxiter=500):
         """cbc.block ConjGrad on level 0's A with this cycle as B (C, OpenMP):
         returns (x, residuals)."""
+        self._set_poly()
         b = np.ascontiguousarray(b, np.float64)
         n = len(b)
         x = np.zeros(n)
@@ -126,4 +134,8 @@ def from_oracle(h):
                 d['winv'] = lv.winv
         levels.append(d)
     p = h.params
-    return CHierarchy(levels, p.cycle_type == 'W', p.presmooth_iter, p.postsmooth_iter, p.maxit)
+    poly = None
+    if p.smoother == 'POLY':
+        from mamg_oracle import poly_weights
+        poly = poly_weights(p)
+    return CHierarchy(levels, p.cycle_type == 'W', p.presmooth_iter, p.postsmooth_iter, p.maxit, poly)

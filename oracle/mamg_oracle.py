@@ -40,6 +40,7 @@ rule), row entries kept sorted by column.
 from __future__ import annotations
 
 import dataclasses
+import math
 import numpy as np
 import scipy.sparse as sp
 
@@ -210,7 +211,7 @@ class Params:
     cycle_type: str = 'V'         # 'V' | 'W'
     max_levels: int = 20
     maxit: int = 1
-    smoother: str = 'JACOBI_RHO'  # 'L1DIAG' | 'JACOBI' | 'JACOBI_RHO'
+    smoother: str = 'JACOBI_RHO'  # 'L1DIAG' | 'JACOBI' | 'JACOBI_RHO' | 'POLY' | 'GS' | 'SGS'
     relaxation: float = 4.0 / 3.0
     presmooth_iter: int = 1
     postsmooth_iter: int = 1
@@ -225,6 +226,8 @@ class Params:
     node_block_smoother: int = 1  # nodal: node-block Jacobi where no seed blocks
     sa_block_diag: int = 1        # nodal: smooth P with node-block D^-1
     coarse_scaling: int = 0       # 1: e <- alpha e, alpha = <b_c, e> / <A_c e, e>
+    poly_degree: int = 2          # POLY: Chebyshev degree (steps per smoothing)
+    poly_ratio: float = 16.0      # POLY: interval [hi / poly_ratio, hi] of W A
 
 
 
@@ -470,7 +473,7 @@ def smoother_weights(A, p: Params):
     (spectrally scaled Jacobi, same rho estimate as prolongator smoothing)."""
     if p.smoother == 'JACOBI':
         d = A.diagonal().copy()
-    elif p.smoother == 'JACOBI_RHO':
+    elif p.smoother in ('JACOBI_RHO', 'POLY'):
         dg = A.diagonal().copy()
         rho = rho_estimate(A, 1.0 / dg, p.rho_iters)
         d = dg * rho
@@ -479,6 +482,33 @@ def smoother_weights(A, p: Params):
     else:
         raise ValueError(p.smoother)
     return p.relaxation / d
+
+
+def poly_weights(p: Params) -> list:
+    """POLY smoother step weights (product form of the Chebyshev polynomial).
+
+    The block smoother W = (relaxation / rho_B) D^-1 bounds the spectrum of
+    W A by hi = relaxation (rho_B is a Gershgorin bound of rho(D^-1 A)).  The
+    degree-m Chebyshev polynomial on [hi / poly_ratio, hi] is the product of
+    m Richardson steps x += w_k W (b - A x) with w_k = 1 / tau_k, tau_k its
+    roots theta + delta cos((2k - 1) pi / (2m)), k = 1..m (ascending k =
+    descending tau).  Pre-smoothing takes the steps in order 1..m,
+    post-smoothing m..1, so the cycle stays symmetric.  Same formula as
+    device.hip poly_weights (C, libm cos)."""
+    m = int(p.poly_degree)
+    hi = float(p.relaxation)
+    lo = hi / float(p.poly_ratio)
+    theta, delta = 0.5 * (hi + lo), 0.5 * (hi - lo)
+    return [1.0 / (theta + delta * math.cos((2 * k - 1) * math.pi / (2 * m))) for k in range(1, m + 1)]
+
+
+def scaled_smoother(lev, w: float):
+    """w * W of a level (block CSR or point weights), scaled value by value."""
+    if lev.WB is not None:
+        W = lev.WB.copy()
+        W.data = w * W.data
+        return W
+    return w * lev.winv
 
 
 def dense_inverse(Ad: np.ndarray) -> np.ndarray:
@@ -698,9 +728,15 @@ class Level:
     ncolours: int = 0
     Dn: np.ndarray = None            # multicolour GS: (nv, 2, 2) block inverses
     crows: list = None               # node ids of each colour (ascending)
+    polyW: list = None               # POLY: w_k W per Chebyshev step (poly_weights)
 
-    def smooth_apply(self, r):
-        return self.WB @ r if self.WB is not None else self.winv * r
+    def step_smoother(self, k):
+        return None if self.polyW is None else self.polyW[k]
+
+    def smooth_apply(self, r, S=None):
+        if S is None:
+            return self.WB @ r if self.WB is not None else self.winv * r
+        return S @ r if sp.issparse(S) else S * r
 
     def gs_sweep(self, x, b, forward=True):
         """x <- x + D_I^-1 (b - A x)_I for the nodes I of each colour in turn
@@ -741,9 +777,13 @@ class Hierarchy:
                 if p.smoother == 'SGS':
                     x = lev.gs_sweep(x, b, False)
         else:
-            x = lev.smooth_apply(b)                  # first sweep from x = 0
-            for _ in range(p.presmooth_iter - 1):
-                x = x + lev.smooth_apply(b - A @ x)
+            # step smoothers: [W] * nu1 (Jacobi), [w_1 W .. w_m W] * nu1 (POLY)
+            pre = [None] * p.presmooth_iter
+            if lev.polyW is not None:
+                pre = lev.polyW * p.presmooth_iter
+            x = lev.smooth_apply(b, pre[0])          # first sweep from x = 0
+            for S in pre[1:]:
+                x = x + lev.smooth_apply(b - A @ x, S)
         r = b - A @ x
         bc = lev.R @ r
         C = self.levels[l + 1]
@@ -753,13 +793,17 @@ class Hierarchy:
         if p.coarse_scaling:                         # src/amg_parameters.py:78
             e = coarse_scale(C.A, bc, e)
         x = x + lev.P @ e
+        post = [None]
+        if lev.polyW is not None:
+            post = lev.polyW[::-1]                   # POLY: steps m..1
         for _ in range(p.postsmooth_iter):
             if gs:                                   # SGS: forward + backward; GS: backward
                 if p.smoother == 'SGS':
                     x = lev.gs_sweep(x, b, True)
                 x = lev.gs_sweep(x, b, False)
             else:
-                x = x + lev.smooth_apply(b - A @ x)
+                for S in post:
+                    x = x + lev.smooth_apply(b - A @ x, S)
         return x
 
     def apply(self, r: np.ndarray) -> np.ndarray:
@@ -826,6 +870,8 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
             lev.WB, lev.bid, nbk = block_smoother(cur, None, pj, node_blocks(n, nf))
         else:
             lev.winv = smoother_weights(cur, p)
+        if p.smoother == 'POLY':
+            lev.polyW = [scaled_smoother(lev, w) for w in poly_weights(p)]
         if gs:
             lev.Dn = node_block_inverse(cur, lev.bid, nbk)
             lev.colour = jp_colouring(node_pattern(cur, 2), l)

@@ -9,6 +9,9 @@
  * residual):  x = S b ; (nu1-1) x += S (b - A x) ; r = b - A x ; bc = R r ;
  * e = cycle(l+1, bc) [; e += cycle(l+1, bc - Ac e)] ; x += P e ;
  * nu2 times x += S (b - A x).   S = W_B (block) or diag(winv) (point).
+ * POLY smoother (oracle_set_poly, mamg_oracle.poly_weights): every smoothing
+ * is m steps x += w_k S (b - A x), k = 1..m before the coarse correction and
+ * k = m..1 after it (the first pre step from x = 0 is x = w_1 S b).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -49,6 +52,17 @@ static void resid(const ocsr* A, const double* x, const double* b, double* r) {
   }
 }
 
+/* POLY step weights (0 steps: one unweighted step per sweep) */
+static int g_poly_m = 0;
+static double g_poly_w[16];
+
+int oracle_set_poly(int m, const double* w) {
+  if (m < 0 || m > 16) return -1;
+  g_poly_m = m;
+  for (int k = 0; k < m; ++k) g_poly_w[k] = w[k];
+  return 0;
+}
+
 /* y = S v (smoother application) */
 static void smooth_apply(const olevel* L, const double* v, double* y) {
   if (L->W.n > 0) {
@@ -57,6 +71,22 @@ static void smooth_apply(const olevel* L, const double* v, double* y) {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < L->n; ++i) y[i] = L->winv[i] * v[i];
   }
+}
+
+/* y = w S v */
+static void smooth_apply_w(const olevel* L, double w, const double* v, double* y) {
+  smooth_apply(L, v, y);
+  if (w != 1.0) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < L->n; ++i) y[i] = w * y[i];
+  }
+}
+
+/* step weight of smoothing step s of a sweep sequence (pre: 1..m, post: m..1) */
+static double step_w(int s, int pre) {
+  if (g_poly_m == 0) return 1.0;
+  const int k = s % g_poly_m;
+  return g_poly_w[pre ? k : g_poly_m - 1 - k];
 }
 
 static void axpy1(int64_t n, const double* a, double* y) {
@@ -77,10 +107,11 @@ static void cycle(olevel* L, int l, int wcyc, int nu1, int nu2, const double* b,
     return;
   }
   olevel* C = &L[l + 1];
-  smooth_apply(lv, b, x);
-  for (int s = 1; s < nu1; ++s) {
+  const int steps = g_poly_m > 0 ? g_poly_m : 1;
+  smooth_apply_w(lv, step_w(0, 1), b, x);
+  for (int s = 1; s < nu1 * steps; ++s) {
     resid(&lv->A, x, b, lv->r);
-    smooth_apply(lv, lv->r, lv->u);
+    smooth_apply_w(lv, step_w(s, 1), lv->r, lv->u);
     axpy1(n, lv->u, x);
   }
   resid(&lv->A, x, b, lv->r);
@@ -93,9 +124,9 @@ static void cycle(olevel* L, int l, int wcyc, int nu1, int nu2, const double* b,
   }
   spmv(&lv->P, C->x, lv->t);
   axpy1(n, lv->t, x);
-  for (int s = 0; s < nu2; ++s) {
+  for (int s = 0; s < nu2 * steps; ++s) {
     resid(&lv->A, x, b, lv->r);
-    smooth_apply(lv, lv->r, lv->u);
+    smooth_apply_w(lv, step_w(s, 0), lv->r, lv->u);
     axpy1(n, lv->u, x);
   }
 }

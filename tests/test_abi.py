@@ -30,7 +30,8 @@ def test_exports_every_declared_symbol(lib_built):
 def test_params_struct_layout(lib_built):
     import metric_amg_examples_amd as M
     p = M.parameters.make_params()
-    assert p.abi_version == 2 and p.post_fusion == 1 and p.AMG_type == 2 and p.cycle_type == 1
+    assert p.abi_version == 3 and p.post_fusion == 1 and p.AMG_type == 2 and p.cycle_type == 1
+    assert p.poly_degree == 2 and p.poly_ratio == 16.0     # last fields: struct tail matches mamg.h
     assert abs(p.relaxation - 4.0 / 3.0) < 1e-15 and p.coarse_dof == 100
     assert p.num_functions == 1 and p.node_block_smoother == 1
     assert M.parameters.make_params(M.parameters.parameters_metric_mi355x).num_functions == 2

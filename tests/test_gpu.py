@@ -28,6 +28,9 @@ def to_c(kw):
         c['AMG_type'] = {'SA': 2, 'UA': 1}[c['AMG_type']]
     if 'cycle_type' in c:
         c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    if 'smoother' in c:
+        c['smoother'] = {'JACOBI': 1, 'L1DIAG': 2, 'JACOBI_RHO': 3, 'GS': 10, 'SGS': 11,
+                         'POLY': 12}[c['smoother']]
     return c
 
 
@@ -48,6 +51,16 @@ APPLY_CASES = [
     (2, 32, 1e3, dict(num_functions=2, node_block_smoother=0, sa_block_diag=0)),
     (3, 16, 1e6, dict(num_functions=2, post_fusion=0)),
     (2, 32, 1e3, dict(num_functions=2, post_fusion=0, cycle_type='W')),
+    # SMOOTHER_POLY (Chebyshev steps w_k W): BSR2 with K built for w_m W, the
+    # [P | AP] and unfused posts, sweeps > 1, W-cycle, and the CSR layout
+    (3, 16, 1e6, dict(num_functions=2, smoother='POLY')),
+    (2, 64, 1e6, dict(num_functions=2, smoother='POLY', poly_degree=3)),
+    (3, 8, 1e2, dict(num_functions=2, smoother='POLY', post_fusion=0)),
+    (2, 32, 1e3, dict(num_functions=2, smoother='POLY', presmooth_iter=2, postsmooth_iter=2,
+                      cycle_type='W', maxit=2)),
+    (3, 16, 1.0, dict(smoother='POLY')),
+    (2, 32, 1e3, dict(num_functions=2, smoother='POLY', node_block_smoother=0, sa_block_diag=0,
+                      poly_ratio=8.0)),
 ]
 DEVICE_ONLY = ('post_fusion',)       # schedule knobs: same cycle, no oracle counterpart
 
@@ -78,16 +91,19 @@ def test_apply_matches_oracle(lib_built, dim, n, g, kw):
         assert rel(zt.cpu().numpy(), zo) < tol
 
 
-@pytest.mark.parametrize('dim,n,g', [(2, 64, 1.0), (3, 16, 1e6), (3, 16, 1e10), (2, 128, 1e4)])
-def test_pcg_iterations_match_oracle(lib_built, dim, n, g):
+@pytest.mark.parametrize('dim,n,g,kw', [(2, 64, 1.0, {}), (3, 16, 1e6, {}), (3, 16, 1e10, {}), (2, 128, 1e4, {}),
+                                        (3, 16, 1e6, dict(smoother='POLY')),
+                                        (3, 32, 1e6, dict(smoother='POLY')),
+                                        (2, 128, 1e4, dict(smoother='POLY'))])
+def test_pcg_iterations_match_oracle(lib_built, dim, n, g, kw):
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
     b = mo.seeded_rhs(s.N)
-    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
     solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)   # device PCG
     x = solver * b
-    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    h = mo.setup(A, mo.Params(num_functions=2, **kw), idofs=s.idofs)
     ref = mo.pcg(A, h, b, 1e-8, 500)
     assert len(solver.residuals) == len(ref.residuals)
     assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)

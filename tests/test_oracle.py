@@ -224,3 +224,47 @@ def test_coarse_scale_equals_fine_formula():
     alpha_f = (r @ Pe) / (Pe @ (A @ Pe))
     es = mo.coarse_scale(C.A, bc, e)
     assert np.allclose(es, alpha_f * e, rtol=1e-10)
+
+
+# ---- Chebyshev (POLY) smoother (round 2) -----------------------------------
+def test_poly_weights_are_chebyshev_roots():
+    """prod_k (1 - w_k t) is the degree-m Chebyshev polynomial on [hi/ratio, hi]
+    normalised to 1 at t = 0: it equioscillates with |p| <= 1/T_m(sigma)."""
+    for m, ratio in ((1, 16.0), (2, 16.0), (3, 8.0)):
+        p = mo.Params(smoother='POLY', poly_degree=m, poly_ratio=ratio)
+        w = mo.poly_weights(p)
+        hi = p.relaxation
+        lo = hi / ratio
+        t = np.linspace(lo, hi, 2001)
+        val = np.prod([1.0 - wk * t for wk in w], axis=0)
+        sigma = (hi + lo) / (hi - lo)
+        bound = 1.0 / np.cosh(m * np.arccosh(sigma))
+        assert np.max(np.abs(val)) <= bound * (1 + 1e-9)
+        assert np.max(np.abs(val)) >= bound * (1 - 1e-3)
+
+
+@pytest.mark.parametrize('kw', [dict(num_functions=2), dict(num_functions=2, poly_degree=3, cycle_type='W'),
+                                dict(), dict(num_functions=2, presmooth_iter=2, postsmooth_iter=2)])
+def test_poly_cycle_symmetric_and_matches_c_restatement(kw):
+    import cref
+    s = mo.bidomain_system(3, 8, 1e6)
+    A = s['A']
+    h = mo.setup(A, mo.Params(smoother='POLY', **kw), idofs=s['idofs'])
+    r1, r2 = mo.seeded_rhs(A.shape[0], 1), mo.seeded_rhs(A.shape[0], 2)
+    a, b = r2 @ h(r1), r1 @ h(r2)
+    assert abs(a - b) < 1e-11 * abs(a)
+    assert r1 @ h(r1) > 0
+    c = cref.from_oracle(h)
+    z, zc = h(r1), c(r1)
+    assert np.linalg.norm(z - zc) <= 1e-12 * np.linalg.norm(z)
+    _, res = c.pcg(r1, 1e-8, 500)
+    assert len(res) - 1 == mo.pcg(A, h, r1).niters
+
+
+def test_poly_halves_jacobi_iterations():
+    s = mo.bidomain_system(3, 16, 1e6)
+    A = s['A']
+    b = mo.seeded_rhs(A.shape[0])
+    nj = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2), idofs=s['idofs']), b).niters
+    npoly = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2, smoother='POLY'), idofs=s['idofs']), b).niters
+    assert npoly <= 0.6 * nj, (npoly, nj)
