@@ -569,23 +569,59 @@ __global__ __launch_bounds__(256) void dot_partial_kernel(int64_t n, const doubl
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void dot_final_kernel(int nb, const double* __restrict__ part,
-                                                        double* __restrict__ out) {
+// ---- device-resident PCG state (dev_pcg): the scalars of cbc.block's
+// ConjGrad live in HBM, so an iteration is one replayable hipGraph and the
+// host only polls the state one iteration behind the GPU
+struct PcgState {
+  double rz, dq, alpha, beta, tol;
+  int it, maxiter, active, run, status;   // status: PCG_* below
+};
+enum { PCG_RUNNING = 0, PCG_STOPPED = 1, PCG_DQ_ZERO = 2, PCG_RZ_NEG = 3, PCG_NOT_POS = 4 };
+
+__device__ double block_sum256(double s) {   // 256 threads -> thread 0
   __shared__ double red[4];
-  double s = 0.0;
-  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+  return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void cg_xr_kernel(int64_t n, double alpha,
-                                                    const double* __restrict__ d,
-                                                    const double* __restrict__ q,
-                                                    double* __restrict__ x,
-                                                    double* __restrict__ r) {
+// rz = <r, z> (partials) -> residuals[0], tolerance, first active flag
+__global__ __launch_bounds__(256) void pcg_init_kernel(int nb, const double* __restrict__ part, PcgState* st,
+                                                       double tol, int relconv, int maxiter, double* res) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+  s = block_sum256(s);
+  if (threadIdx.x) return;
+  st->it = 0; st->maxiter = maxiter; st->run = 0; st->alpha = 0.0; st->beta = 0.0; st->dq = 0.0;
+  st->rz = s;
+  if (s < 0.0) { st->active = 0; st->status = PCG_NOT_POS; st->tol = tol; res[0] = 0.0; return; }
+  const double r0 = sqrt(s);
+  res[0] = r0;
+  st->tol = relconv ? tol * r0 : tol;
+  st->active = (r0 > st->tol && maxiter > 0) ? 1 : 0;
+  st->status = st->active ? PCG_RUNNING : PCG_STOPPED;
+}
+
+// dq = <d, A d>; alpha = rz / dq (the host loop's breakdown on dq == 0)
+__global__ __launch_bounds__(256) void pcg_alpha_kernel(int nb, const double* __restrict__ part, PcgState* st) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+  s = block_sum256(s);
+  if (threadIdx.x) return;
+  st->run = st->active;
+  if (!st->active) return;
+  st->dq = s;
+  if (s == 0.0) { st->active = 0; st->status = PCG_DQ_ZERO; return; }
+  st->alpha = st->rz / s;
+}
+
+__global__ __launch_bounds__(256) void pcg_xr_kernel(int64_t n, const PcgState* __restrict__ st,
+                                                     const double* __restrict__ d, const double* __restrict__ q,
+                                                     double* __restrict__ x, double* __restrict__ r) {
+  if (!st->active) return;
+  const double alpha = st->alpha;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) {
     x[i] = x[i] + alpha * d[i];
@@ -593,18 +629,36 @@ __global__ __launch_bounds__(256) void cg_xr_kernel(int64_t n, double alpha,
   }
 }
 
-__global__ __launch_bounds__(256) void cg_d_kernel(int64_t n, double beta,
-                                                   const double* __restrict__ z,
-                                                   double* __restrict__ d) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) d[i] = z[i] + beta * d[i];
+// rz' = <r, B r>: beta, residuals[it + 1], stop test (tolerance / maxiter)
+__global__ __launch_bounds__(256) void pcg_beta_kernel(int nb, const double* __restrict__ part, PcgState* st,
+                                                       double* res, double* alphas, double* betas) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+  s = block_sum256(s);
+  if (threadIdx.x) return;
+  if (!st->active) return;
+  if (s < 0.0) { st->active = 0; st->status = PCG_RZ_NEG; return; }
+  const double beta = s / st->rz;
+  const int k = st->it;
+  st->beta = beta;
+  st->rz = s;
+  res[k + 1] = sqrt(s);
+  alphas[k] = st->alpha;
+  betas[k] = beta;
+  st->it = k + 1;
+  if (!(res[k + 1] > st->tol) || k + 1 >= st->maxiter) { st->active = 0; st->status = PCG_STOPPED; }
 }
 
-__global__ __launch_bounds__(256) void cg_undo_kernel(int64_t n, double alpha,
-                                                      const double* __restrict__ d,
-                                                      double* __restrict__ x) {
+// d = z + beta d; on <r, Br> < 0 this iteration's x update is undone instead
+// (cbc.block restores x before breaking)
+__global__ __launch_bounds__(256) void pcg_d_kernel(int64_t n, const PcgState* __restrict__ st,
+                                                    const double* __restrict__ z, double* __restrict__ d,
+                                                    double* __restrict__ x) {
+  if (!st->run || st->status == PCG_DQ_ZERO) return;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) x[i] = x[i] - alpha * d[i];
+  if (i >= n) return;
+  if (st->status == PCG_RZ_NEG) x[i] = x[i] - st->alpha * d[i];
+  else d[i] = z[i] + st->beta * d[i];
 }
 
 // field-major [v0; v1] (stride bs) -> node-interleaved pairs
@@ -2871,77 +2925,106 @@ int dev_spmv(DeviceHandle* h, const double* d_x, double* d_y, void* stream, std:
   return order_end(h, (hipStream_t)stream, err);
 }
 
-namespace {
-int dot(DeviceHandle* h, int64_t n, const double* a, const double* b, hipStream_t s, double* out,
-        std::string* err) {
-  dot_partial_kernel<<<DOT_BLOCKS, 256, 0, s>>>(n, a, b, h->part);
-  dot_final_kernel<<<1, 256, 0, s>>>(DOT_BLOCKS, h->part, h->dres);
-  HIPCHK(hipMemcpyAsync(h->hres, h->dres, sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  *out = *h->hres;
-  return MAMG_OK;
-}
-}  // namespace
 
 int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int maxiter,
             int relativeconv, double* residuals, double* alphas, double* betas, int* niters,
             void* stream, std::string* err) {
+  // cbc.block ConjGrad (mamg_oracle.pcg) with every scalar in HBM: one
+  // iteration = one hipGraph (q = A d, <d,q>, alpha, x/r update, z = B r,
+  // <r,z>, beta, stop test, d update).  The host keeps one iteration queued
+  // ahead and polls the state of the previous one, so the GPU never waits
+  // for a host round trip; the queued iteration after the stopping one
+  // finds the state inactive and leaves x untouched.
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
   const int64_t n = h->L[0].n;
   int rc;
+  if (maxiter < 0) { *err = "maxiter must be >= 0"; return MAMG_ERR_ARG; }
   if (!h->cr) {
     double** v[] = {&h->cr, &h->cz, &h->cd, &h->cq};
     for (double** q : v)
       if ((rc = dalloc(h, q, n, err))) return rc;
     if ((rc = dalloc(h, &h->part, DOT_BLOCKS, err))) return rc;
-    if ((rc = dalloc(h, &h->dres, 1, err))) return rc;
-    HIPCHK(hipHostMalloc((void**)&h->hres, sizeof(double), hipHostMallocDefault));
+    if ((rc = dalloc(h, &h->dres, (int64_t)((sizeof(PcgState) + 7) / 8), err))) return rc;
+    HIPCHK(hipHostMalloc((void**)&h->hres, 2 * sizeof(PcgState), hipHostMallocDefault));
   }
+  PcgState* st = reinterpret_cast<PcgState*>(h->dres);
+  PcgState* hst = reinterpret_cast<PcgState*>(h->hres);
+  double* dhist = nullptr;   // residuals[maxiter + 1], alphas[maxiter], betas[maxiter]
+  HIPCHK(hipMalloc(&dhist, (3 * (size_t)maxiter + 1) * sizeof(double)));
+  double *dres = dhist, *dal = dhist + maxiter + 1, *dbe = dal + maxiter;
+  struct Cleanup {
+    double* p; hipGraphExec_t e; hipGraph_t g; hipEvent_t ev[2];
+    ~Cleanup() {
+      if (e) (void)hipGraphExecDestroy(e);
+      if (g) (void)hipGraphDestroy(g);
+      for (hipEvent_t x : ev) if (x) (void)hipEventDestroy(x);
+      if (p) (void)hipFree(p);
+    }
+  } cl{dhist, nullptr, nullptr, {nullptr, nullptr}};
   const unsigned g = nblocks(n);
   if ((rc = order_begin(h, s, err))) return rc;
   launch(a0_op(h, EPI_RESID, d_x, d_b, h->cr), s);                 // r = b - A x
   if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;         // z = B r
   HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
-  double rz;
-  if ((rc = dot(h, n, h->cr, h->cz, s, &rz, err))) return rc;
-  if (rz < 0) { *err = "Matrix is not positive"; *niters = 0; return MAMG_ERR_BREAKDOWN; }
-  residuals[0] = std::sqrt(rz);
-  const double tol_eff = relativeconv ? tol * residuals[0] : tol;
-  int it = 0;
-  int status = MAMG_OK;
-  while (residuals[it] > tol_eff && it < maxiter) {
-    launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), s);              // q = A d
-    double dz;
-    if ((rc = dot(h, n, h->cd, h->cq, s, &dz, err))) return rc;
-    if (dz == 0.0) {   // the host loop's breakdown flag (krylov.py): same status here
-      *err = "ConjGrad stopped: <d,Ad> = 0";
-      status = MAMG_ERR_BREAKDOWN;
-      break;
-    }
-    const double alpha = rz / dz;
-    cg_xr_kernel<<<g, 256, 0, s>>>(n, alpha, h->cd, h->cq, d_x, h->cr);
-    if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;
-    const double rz_prev = rz;
-    if ((rc = dot(h, n, h->cr, h->cz, s, &rz, err))) return rc;
-    if (rz < 0) {
-      cg_undo_kernel<<<g, 256, 0, s>>>(n, alpha, h->cd, d_x);
-      *err = "ConjGrad breakdown (<r,Br> < 0)";
-      status = MAMG_ERR_BREAKDOWN;
-      break;
-    }
-    const double beta = rz / rz_prev;
-    cg_d_kernel<<<g, 256, 0, s>>>(n, beta, h->cz, h->cd);
-    residuals[it + 1] = std::sqrt(rz);
-    alphas[it] = alpha;
-    betas[it] = beta;
-    ++it;
+  dot_partial_kernel<<<DOT_BLOCKS, 256, 0, s>>>(n, h->cr, h->cz, h->part);
+  pcg_init_kernel<<<1, 256, 0, s>>>(DOT_BLOCKS, h->part, st, tol, relativeconv, maxiter, dres);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(&hst[0], st, sizeof(PcgState), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (hst[0].status == PCG_NOT_POS) {
+    *err = "Matrix is not positive";
+    *niters = 0;
+    (void)order_end(h, s, err);
+    return MAMG_ERR_BREAKDOWN;
   }
+  if (hst[0].active) {
+    std::vector<Op> ops;
+    apply_ops(h, h->cr, h->cz, &ops);
+    HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
+    launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), h->cap);           // q = A d
+    dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cd, h->cq, h->part);
+    pcg_alpha_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st);
+    pcg_xr_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cd, h->cq, d_x, h->cr);
+    for (const Op& o : ops) launch(o, h->cap);                          // z = B r
+    dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cr, h->cz, h->part);
+    pcg_beta_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st, dres, dal, dbe);
+    pcg_d_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cz, h->cd, d_x);
+    HIPCHK(hipStreamEndCapture(h->cap, &cl.g));
+    HIPCHK(hipGraphInstantiate(&cl.e, cl.g, nullptr, nullptr, 0));
+    for (hipEvent_t& x : cl.ev) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    // iteration k's state lands in hst[k & 1]; iteration k + 1 is queued
+    // before the host waits for iteration k
+    for (int k = 0; k < maxiter; ++k) {
+      HIPCHK(hipGraphLaunch(cl.e, s));
+      HIPCHK(hipMemcpyAsync(&hst[k & 1], st, sizeof(PcgState), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(cl.ev[k & 1], s));
+      if (k == 0) continue;
+      HIPCHK(hipEventSynchronize(cl.ev[(k - 1) & 1]));
+      if (!hst[(k - 1) & 1].active) break;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(&hst[0], st, sizeof(PcgState), hipMemcpyDeviceToHost, s));
   if ((rc = order_end(h, s, err))) return rc;
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipGetLastError());
+  const PcgState fin = hst[0];
+  const int it = fin.it;
+  HIPCHK(hipMemcpy(residuals, dres, (it + 1) * sizeof(double), hipMemcpyDeviceToHost));
+  if (it > 0) {
+    HIPCHK(hipMemcpy(alphas, dal, it * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(betas, dbe, it * sizeof(double), hipMemcpyDeviceToHost));
+  }
   *niters = it;
-  return status;
+  if (fin.status == PCG_DQ_ZERO) {   // the host loop's breakdown flag (krylov.py): same status here
+    *err = "ConjGrad stopped: <d,Ad> = 0";
+    return MAMG_ERR_BREAKDOWN;
+  }
+  if (fin.status == PCG_RZ_NEG) {
+    *err = "ConjGrad breakdown (<r,Br> < 0)";
+    return MAMG_ERR_BREAKDOWN;
+  }
+  return MAMG_OK;
 }
 
 int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,

@@ -85,6 +85,8 @@ class ConjGrad:
         return isinstance(B, MetricAMG) and B._Aop is self.A
 
     def __mul__(self, b):
+        if hasattr(b, 'data_ptr') and getattr(b, 'is_cuda', False):   # torch tensor in HBM
+            return self.solve_device(b)
         blocks = isinstance(b, (list, tuple))
         if blocks:
             b = np.concatenate([np.asarray(bi, dtype=np.float64) for bi in b])
@@ -103,11 +105,28 @@ class ConjGrad:
 
     def _solve_device(self, b):
         import torch
+        bt = torch.as_tensor(np.ascontiguousarray(b, dtype=np.float64)).cuda()
+        xt = self.solve_device(bt)
+        torch.cuda.synchronize()
+        return xt.cpu().numpy()
+
+    def solve_device(self, bt, xt=None):
+        """Device-resident solve: b (and x0 / the result) are float64 torch
+        tensors in HBM; runs on torch's current stream, returns x (no host
+        copies of the vectors; the residual history comes back to the host)."""
+        import torch
+        if not self._device_ok():
+            raise ValueError('device solve needs precond = a MetricAMG built on this A, no callback and '
+                             'the cbc.block stopping rule')
         B = self.B
         n = B.shape[0]
-        bt = torch.as_tensor(np.ascontiguousarray(b, dtype=np.float64)).cuda()
-        x0 = np.zeros(n) if self.initial_guess is None else np.asarray(self.initial_guess, np.float64)
-        xt = torch.as_tensor(np.ascontiguousarray(x0)).cuda()
+        if bt.dtype != torch.float64 or bt.numel() != n or not bt.is_contiguous():
+            raise ValueError('b must be a contiguous float64 tensor of length %d' % n)
+        if xt is None:
+            if self.initial_guess is None:
+                xt = torch.zeros_like(bt)
+            else:
+                xt = torch.as_tensor(np.ascontiguousarray(self.initial_guess, np.float64)).to(bt.device)
         res = np.zeros(self.maxiter + 1)
         al = np.zeros(max(self.maxiter, 1))
         be = np.zeros(max(self.maxiter, 1))
@@ -131,8 +150,7 @@ class ConjGrad:
         self.residuals = list(res[:k + 1])
         self.alphas = list(al[:k])
         self.betas = list(be[:k])
-        torch.cuda.synchronize()
-        return xt.cpu().numpy()
+        return xt
 
     def _solve_host(self, b):
         A, B = self.A, self.B
