@@ -79,6 +79,9 @@ def main():
     ap.add_argument('--dim', type=int, default=3)
     ap.add_argument('--nrefs', type=int, default=6)
     ap.add_argument('--gamma', type=float, default=1e6)
+    ap.add_argument('--problem', choices=('bidomain', 'emi'), default='bidomain',
+                    help='bidomain (BASELINE configs 1-3) or emi (config 4: emi_3d nrefs=5, interface seeds '
+                         'with node-aligned blocks, Schwarz_maxlvl 0)')
     ap.add_argument('--rep-nodes', type=int, default=32768,
                     help='multi-GPU: replicate levels with <= this many nodes')
     ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
@@ -122,7 +125,11 @@ def main():
 
     n = M.problems.finest_n(args.dim, args.nrefs)
     t0 = time.time()
-    sysm = M.problems.bidomain(args.dim, n, args.gamma)
+    if args.problem == 'emi':      # src/emi_3d.py:119-144 (split cube, trace coupling, interface seeds)
+        sysm = M.problems.emi(args.dim, n, args.gamma)
+        prof['Schwarz_maxlvl'] = 0
+    else:
+        sysm = M.problems.bidomain(args.dim, n, args.gamma)
     t_gen = time.time() - t0
     log('rank %d: generated %dD n=%d N=%d nnz=%d in %.1fs' % (rank, args.dim, n, sysm.N, sysm.nnz, t_gen))
     stream = torch.cuda.current_stream(dev)
@@ -169,7 +176,7 @@ def main():
             setup_info = {'path': 'gpu', 'wall_s': round(t_setup, 3), 'phases_ms': B.setup_timings}
             if args.compare_host_setup:
                 t0 = time.time()
-                Hc = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local)
+                Hc = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, **prof)
                 setup_info['host_setup_s'] = round(time.time() - t0, 3)
                 Hc.close()
         levels = None
@@ -180,7 +187,7 @@ def main():
         torch.distributed.broadcast_object_list(uid, src=0)
         t0 = time.time()
         B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
-                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local)
+                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local, **prof)
         t_setup = time.time() - t0
         setup_info = {'path': 'deterministic setup replicated on every rank (GPU setup; host setup if the '
                               'profile is unsupported) + rank-local upload',
@@ -263,6 +270,7 @@ def main():
                 continue
             torch.cuda.synchronize(dev)
             t0 = time.time()
+            kw = dict(kw, Schwarz_maxlvl=prof.get('Schwarz_maxlvl', 1))
             B2 = M.MetricAMG(sysm, sysm.W, idofs=sysm.idofs, num_functions=2, device=local, setup='gpu', **kw)
             torch.cuda.synchronize(dev)
             ts = time.time() - t0
@@ -289,7 +297,7 @@ def main():
         import cref
         import mamg_oracle as mo
         if H is None:       # same hierarchy bits, from the GPU setup copied back
-            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, gpu=True)
+            H = M.HostHierarchy(sysm, idofs=sysm.idofs, num_functions=2, device=local, gpu=True, **prof)
         lv = [H.level(l, with_A=(l > 0)) for l in range(H.num_levels)]
         lv[0]['A'] = (sysm.indptr, sysm.indices, sysm.data, (sysm.N, sysm.N))
         poly = None
@@ -386,8 +394,8 @@ def main():
         'dtype': 'f64',
         'data': 'synthetic (P1 bidomain matrix generated in-library; r = uniform(-1,1), seed 1234)',
         'config': {
-            'workload': 'bidomain_%dd nrefs=%d gamma=%g metric_mono (profile %s)'
-                        % (args.dim, args.nrefs, args.gamma, PROFILE_NAMES[args.smoother]
+            'workload': '%s_%dd nrefs=%d gamma=%g metric_mono (profile %s)'
+                        % (args.problem, args.dim, args.nrefs, args.gamma, PROFILE_NAMES[args.smoother]
                            + (', W-cycle' if args.cycle == 'W' else '') + (', coarse scaling' if args.scaling else '')),
             'n': n, 'N': sysm.N, 'nnz': sysm.nnz, 'levels': levels,
             'parallelism': 'single' if world == 1 else 'row-partition x%d (RCCL halo)' % world,

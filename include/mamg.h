@@ -90,7 +90,7 @@ typedef struct mamg_params {
   int32_t amli_degree;       /* accepted, unused (no AMLI cycle)             */
   int32_t Schwarz_levels;    /* 1: seed-block Jacobi on level 0 if idofs     */
   int32_t Schwarz_mmsize;    /* max dofs per seed block, 100                 */
-  int32_t Schwarz_maxlvl;    /* accepted; blocks are distance-1 (see DESIGN) */
+  int32_t Schwarz_maxlvl;    /* 1: seed + joined 1-ring; 0: seed node only   */
   int32_t Schwarz_type;      /* MAMG_SCHWARZ_BLOCK_JACOBI                    */
   int32_t Schwarz_blksolver; /* 32 -> dense block inverse                    */
   int32_t print_level;       /* 0 silent                                     */

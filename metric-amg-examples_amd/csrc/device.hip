@@ -3127,8 +3127,9 @@ struct DDLevel {
   DBsr PA;                 // post fusion: merged [P_loc | AP_loc]
   DBsr K;                  // post fusion: K_loc = P_loc - W (AP)_loc (default)
   dv4* W = nullptr;
+  std::vector<dv4*> Wk;    // SMOOTHER_POLY step smoothers w_k W (empty: Jacobi)
   double* Ainv = nullptr;
-  double *b = nullptr, *x = nullptr, *t = nullptr, *r = nullptr;
+  double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr;
   double* spx = nullptr;   // level 0: [owned | ghost] operand of the standalone SpMV
   int64_t ib0 = 0, ib1 = 0;  // longest run of A_loc rows without ghost columns
   int64_t* send_idx = nullptr;
@@ -3246,12 +3247,21 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
     return;
   }
   const DDLevel& C = h->L[l + 1];
+  const int m = smoother_steps(h->p);   // steps per smoothing (POLY: Chebyshev degree)
+  auto wk = [&](int s, bool pre) -> const dv4* { return D.Wk.empty() ? D.W : D.Wk[step_index(m, s, pre)]; };
+  const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
   double* X = D.t;
+  double* X2 = D.t2;
   {
     Op o;
-    o.kind = OP_BD; o.cls = l0 ? C_L0_WB : C_COARSE; o.n = D.nloc; o.W = D.W; o.b = b; o.bs = bs;
+    o.kind = OP_BD; o.cls = l0 ? C_L0_WB : C_COARSE; o.n = D.nloc; o.W = wk(0, true); o.b = b; o.bs = bs;
     o.out = X; o.bytes = 64.0 * D.nloc;
     ops->push_back(wrap(o));
+  }
+  for (int s = 1; s < m; ++s) {   // further pre steps: halo of X, then x + w_s W (b - A x)
+    const Op bj = bsr_op(D.A, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, wk(s, true), X2, 0);
+    if (D.replicated) ops->push_back(wrap(bj)); else halo_residual(h, l, X, bj, ops);
+    std::swap(X, X2);
   }
   {
     const Op res = bsr_op(D.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs, nullptr, D.r, 0);
@@ -3278,20 +3288,29 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   }
   dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
   if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
-  if (D.K.nr > 0) {    // fused: xout = X + W r + K e, all operands local
-    ops->push_back(wrap(bsr_op(D.K, EPI_KPOST, l0 ? C_L0_SMOOTH : C_COARSE, tagA, C.x, 0, X, D.r, 0, D.W,
-                               xout, os)));
-    return;
+  int s0 = 0;
+  if (D.K.nr > 0 || D.PA.nr > 0) {   // fused first post step (K built with its smoother), operands local
+    const bool last = m == 1;
+    if (D.K.nr > 0)   // X + W r + K e
+      ops->push_back(wrap(bsr_op(D.K, EPI_KPOST, clsS, tagA, C.x, 0, X, D.r, 0, wk(0, false),
+                                 last ? xout : X2, last ? os : 0)));
+    else              // X + P e + W (r - AP e)
+      ops->push_back(wrap(post_op(D.PA, D.r, wk(0, false), clsS, tagA, C.x, X, last ? xout : X2,
+                                  last ? os : 0)));
+    if (last) return;
+    std::swap(X, X2);
+    s0 = 1;
+  } else {
+    ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
+                               nullptr, X, 0)));
   }
-  if (D.PA.nr > 0) {   // fused: xout = X + P e + W (r - AP e), all operands local
-    ops->push_back(wrap(post_op(D.PA, D.r, D.W, l0 ? C_L0_SMOOTH : C_COARSE, tagA, C.x, X, xout, os)));
-    return;
+  for (int s = s0; s < m; ++s) {   // halo of the iterate, then x + w W (b - A x)
+    const bool last = s == m - 1;
+    const Op bj = bsr_op(D.A, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, wk(s, false), last ? xout : X2,
+                         last ? os : 0);
+    if (D.replicated) ops->push_back(wrap(bj)); else halo_residual(h, l, X, bj, ops);
+    std::swap(X, X2);
   }
-  ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
-                             nullptr, X, 0)));
-  if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
-  ops->push_back(wrap(bsr_op(D.A, EPI_BJAC, l0 ? C_L0_SMOOTH : C_COARSE, tagA, X, 0, X, b, bs, D.W,
-                             xout, os)));
 }
 
 int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
@@ -3394,13 +3413,16 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (gs_smoother(p) || p.coarse_scaling || p.smoother == MAMG_SMOOTHER_POLY) {
-    *err = "multi-GPU apply supports the block-Jacobi smoothers without coarse scaling";
+  if (gs_smoother(p) || p.coarse_scaling) {
+    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers without coarse scaling";
     return MAMG_ERR_UNSUPPORTED;
   }
   read_knobs();
+  double pw[MAMG_POLY_MAX];
+  const int pm = poly_weights(p, pw);
   DistPlan plan;
-  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0);
+  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0,
+                           p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0);
   if (rc) return rc;
   std::unique_ptr<DistHandle> h(new DistHandle());
   h->p = p;
@@ -3475,11 +3497,23 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = upload_bsr(h.get(), P.Rp, &D.R, 0, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.W, D.nloc, err))) return rc;
       HIPCHK(hipMemcpy(D.W, P.W.data(), 4 * D.nloc * sizeof(double), hipMemcpyHostToDevice));
+      if (p.smoother == MAMG_SMOOTHER_POLY) {   // w_k W as on one GPU (poly_scaled)
+        for (int k = 0; k < pm; ++k) {
+          dv4* q = nullptr;
+          if ((rc = ddalloc(h.get(), &q, D.nloc, err))) return rc;
+          if (D.nloc)
+            wscale_kernel<<<nblocks(4 * D.nloc), 256>>>(4 * D.nloc, pw[k], reinterpret_cast<const double*>(D.W),
+                                                         reinterpret_cast<double*>(q));
+          HIPCHK(hipGetLastError());
+          D.Wk.push_back(q);
+        }
+      }
     }
     const int64_t full = D.nloc + D.ng;
     if ((rc = ddalloc(h.get(), &D.b, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.x, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.t, 2 * full, err))) return rc;
+    if ((rc = ddalloc(h.get(), &D.t2, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
     if (l == 0 && !D.coarsest && (rc = ddalloc(h.get(), &D.spx, 2 * full, err))) return rc;
     const int64_t ns = P.send_idx.size();

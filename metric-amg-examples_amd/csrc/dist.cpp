@@ -146,7 +146,15 @@ void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HB
 }
 
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err, bool kpost) {
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost, double kw) {
+  // K = P - (kw W) AP: the first post-smoothing step's smoother (device.hip
+  // poly_scaled: kw W elementwise, then the merge; bitwise the single-GPU K)
+  auto kmerge_kw = [kw](const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K) {
+    if (kw == 1.0) { kmerge_rows(P, AP, W, K); return; }
+    std::vector<double> Ws(W.size());
+    for (size_t i = 0; i < W.size(); ++i) Ws[i] = kw * W[i];
+    kmerge_rows(P, AP, Ws, K);
+  };
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
   const int nl = (int)H.levels.size();
@@ -243,7 +251,7 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       if (fuse) {
         HBsr AP;
         to_bsr2(H.levels[l].AP.view(), D.nv, C.nv, &AP);
-        if (kpost) kmerge_rows(D.P, AP, D.W, &D.K);
+        if (kpost) kmerge_kw(D.P, AP, D.W, &D.K);
         else merge_bsr_rows(D.P, AP, &D.PA);
       }
       continue;
@@ -264,7 +272,7 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       HBsr AP;
       to_bsr2_rows(H.levels[l].AP.view(), D.nv, C.nv, D.o0, D.o1, &AP);
       remap_cols(&AP, ncl, cmap);
-      if (kpost) kmerge_rows(D.P, AP, D.W, &D.K);
+      if (kpost) kmerge_kw(D.P, AP, D.W, &D.K);
       else merge_bsr_rows(D.P, AP, &D.PA);
     }
   }

@@ -31,9 +31,9 @@ struct DistPlan {
 };
 
 // fuse: prolongation fused into the post sweep (needs A P from the setup);
-// kpost: through K = P - W (A P) (one operator), else through [P | AP]
+// kpost: through K = P - kw W (A P) (one operator), else through [P | AP]
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err, bool kpost = true);
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost = true, double kw = 1.0);
 // K rows = P rows - W_I (AP rows), block-column union (both sorted, same columns)
 void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K);
 

@@ -1080,7 +1080,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     Scratch S;
     dv4_t* Dsm = nullptr;
     RCHK(S.alloc(&Dsm, nv, err));
-    const bool seeds = l < p.Schwarz_levels && l == 0 && idofs != nullptr && n_idofs > 0;
+    const bool seeds = seed_blocks_on(p, l, idofs, n_idofs);
     if (seeds) {
       int32_t* di = nullptr;
       uint8_t* isseed = nullptr;

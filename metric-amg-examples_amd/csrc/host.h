@@ -62,6 +62,13 @@ int check_params(const mamg_params& p, std::string* err);
 // SMOOTHER_POLY step weights w[0..poly_degree) (oracle mamg_oracle.poly_weights)
 constexpr int MAMG_POLY_MAX = 8;
 int poly_weights(const mamg_params& p, double* w);
+// level-0 seed (Schwarz) blocks from idofs (src/utils.py:84-86).  Schwarz_maxlvl
+// 0 = a seed's block is its own node without a ring, which with node-block
+// smoothers is the node block: the seeds then change nothing and every level
+// is node-aligned (BSR2 layout, GPU setup, multi-GPU; EMI's interface pairs)
+inline bool seed_blocks_on(const mamg_params& p, int l, const int32_t* idofs, int64_t n_idofs) {
+  return l == 0 && l < p.Schwarz_levels && idofs != nullptr && n_idofs > 0 && p.Schwarz_maxlvl >= 1;
+}
 // smoothing steps per sweep and their weights, pre order (1 step of weight 1
 // for the Jacobi smoothers)
 inline int smoother_steps(const mamg_params& p) {

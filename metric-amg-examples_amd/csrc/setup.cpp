@@ -719,6 +719,11 @@ int check_params(const mamg_params& p, std::string* err) {
     }
   }
   if (p.Schwarz_levels == 1 && p.Schwarz_mmsize < 1) { *err = "Schwarz_mmsize must be >= 1"; return MAMG_ERR_ARG; }
+  if (p.Schwarz_maxlvl < 0) { *err = "Schwarz_maxlvl must be >= 0"; return MAMG_ERR_ARG; }
+  if (p.Schwarz_maxlvl == 0 && (p.num_functions < 2 || !p.node_block_smoother)) {
+    *err = "Schwarz_maxlvl 0 (seed blocks = the seeds' nodes) needs num_functions >= 2 and node_block_smoother 1";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   if (p.max_levels < 1 || p.maxit < 1 || p.presmooth_iter < 1 || p.postsmooth_iter < 1 || p.coarse_dof < 1) {
     *err = "max_levels, maxit, presmooth_iter, postsmooth_iter, coarse_dof must be >= 1";
     return MAMG_ERR_ARG;
@@ -801,7 +806,7 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
     const bool need_rho = (p.AMG_type == MAMG_SA_AMG && !blockP) || p.smoother == MAMG_SMOOTHER_JACOBI_RHO ||
                           p.smoother == MAMG_SMOOTHER_POLY;
     const double rho = need_rho ? rho_estimate(cur, dinv, rs, p.rho_iters) : 0.0;
-    if (l < p.Schwarz_levels && l == 0 && idofs != nullptr && n_idofs > 0) {
+    if (seed_blocks_on(p, l, idofs, n_idofs)) {
       rc = block_smoother(cur, idofs, n_idofs, p, &lev.WB, err);
       if (rc) return rc;
     } else if (nf > 1 && p.node_block_smoother) {

@@ -140,6 +140,23 @@ class BlockSystem:
     def N(self):
         return int(sum(self.W))
 
+    @property
+    def nv(self):
+        """dofs per field when both blocks have the same size (EMI: mirror-image
+        numbering, so dof I of each side forms node I of a 2-field system)."""
+        if self.W[0] != self.W[1]:
+            raise ValueError('blocks of different sizes: no node pairing')
+        return int(self.W[0])
+
+    def tocsr(self):
+        if self.info.get('_csr') is None:
+            self.info['_csr'] = self.scipy()
+        return self.info['_csr']
+
+    @property
+    def nnz(self):
+        return int(self.tocsr().nnz)
+
 
 def _eliminate(A, dofs):
     """Symmetric Dirichlet elimination (rows and columns of `dofs` -> unit diagonal)."""

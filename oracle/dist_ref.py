@@ -8,8 +8,8 @@ Tests compare the gathered result with the single-rank oracle
 (mamg_oracle.Hierarchy.apply): the partition must not change the cycle beyond
 summation order.
 
-Per distributed level (V-cycle, nu1 = nu2 = 1):
-  X = W b ; halo(X) ; r = b - A X ;
+Per distributed level (V-cycle, nu1 = nu2 = 1; POLY: the step weights w_k):
+  X = W b [; halo(X) ; X += w_k W (b - A X)] ; halo(X) ; r = b - A X ;
   part = Rp r ; [next distributed: reverse-add ghost partials to owners |
                  next replicated: all-reduce] ; xc = cycle(l+1, bc) ;
   [next distributed: halo(xc)] ; X += P xc ; halo(X) ; z = X + W (b - A X)
@@ -102,10 +102,15 @@ class GlooComm:
 
 
 class DistCycle:
-    def __init__(self, plan_levels, Ainv_nodemajor, comm):
+    """poly: the POLY step weights (mamg_oracle.poly_weights): pre-smoothing
+    takes x = w_1 W b then x += w_k W (b - A x) for k = 2..m (a halo before
+    each), post-smoothing the steps m..1; None = one Jacobi step each."""
+
+    def __init__(self, plan_levels, Ainv_nodemajor, comm, poly=None):
         self.L = plan_levels
         self.Ainv = Ainv_nodemajor
         self.comm = comm
+        self.ws = list(poly) if poly else [1.0]
 
     # forward halo: fill ghost rows of x2 (nloc+ng, 2)
     def halo(self, lv, x2):
@@ -136,15 +141,23 @@ class DistCycle:
         if lv['coarsest']:
             return (self.Ainv @ b2.ravel()).reshape(-1, 2)
         C = self.L[l + 1]
+        ws = self.ws
         if lv['replicated']:
-            X = bd_mv(lv['W'], b2)
+            X = ws[0] * bd_mv(lv['W'], b2)
+            for w in ws[1:]:
+                X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
             r = b2 - bsr_mv(lv['A'], X)
             xc = self.cycle(l + 1, bsr_mv(lv['R'], r))
             X = X + bsr_mv(lv['P'], xc)
-            return X + bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
+            for w in ws[::-1]:
+                X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
+            return X
         nloc, ng = lv['nloc'], len(lv['ghosts'])
         Xg = np.zeros((nloc + ng, 2))
-        Xg[:nloc] = bd_mv(lv['W'], b2)
+        Xg[:nloc] = ws[0] * bd_mv(lv['W'], b2)
+        for w in ws[1:]:
+            self.halo(lv, Xg)
+            Xg[:nloc] = Xg[:nloc] + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
         self.halo(lv, Xg)
         r = b2 - bsr_mv(lv['A'], Xg)
         part = bsr_mv(lv['R'], r)
@@ -160,8 +173,10 @@ class DistCycle:
         else:
             xcg = xc
         Xg[:nloc] = Xg[:nloc] + bsr_mv(lv['P'], xcg)
-        self.halo(lv, Xg)
-        return Xg[:nloc] + bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
+        for w in ws[::-1]:
+            self.halo(lv, Xg)
+            Xg[:nloc] = Xg[:nloc] + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
+        return Xg[:nloc]
 
     def apply_local(self, r_local_fieldmajor):
         """r_local: [u1 owned ; u2 owned] (length 2*nloc) -> z_local, same layout."""

@@ -219,6 +219,7 @@ class Params:
     strong_coupled: float = 0.0   # SoC threshold theta
     Schwarz_levels: int = 1       # 1: seed-block Jacobi on level 0 (needs idofs)
     Schwarz_mmsize: int = 100     # max dofs per seed block
+    Schwarz_maxlvl: int = 1       # 1: seed + joined 1-ring neighbours; 0: the seed's node (node blocks)
     sa_omega: float = 4.0 / 3.0   # prolongator smoothing  w = sa_omega / rho
     rho_iters: int = 0            # 0: Gershgorin bound; >0: inf-norm power its
     max_coarse_dense: int = 8192
@@ -864,7 +865,7 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         if gs and (nf != 2 or not p.node_block_smoother):
             raise ValueError('multicolour GS needs num_functions = 2 and node-block smoothers')
         pj = dataclasses.replace(p, smoother='JACOBI_RHO') if gs else p
-        if l < p.Schwarz_levels and idofs is not None and l == 0:
+        if l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1:
             lev.WB, lev.bid, nbk = block_smoother(cur, idofs, pj)
         elif nf > 1 and p.node_block_smoother:
             lev.WB, lev.bid, nbk = block_smoother(cur, None, pj, node_blocks(n, nf))

@@ -54,6 +54,30 @@ def test_emi_block_form_pcg_matches_oracle(lib_built, dim, n, g):
     assert isinstance(x, list) and len(x[0]) == s.W[0]
 
 
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, {}), (3, 32, 1e6, dict(smoother=12)),
+                                        (2, 128, 1e6, dict(smoother=12)), (3, 8, 1e10, {})])
+def test_emi_node_aligned_seeds_gpu_setup(lib_built, dim, n, g, kw):
+    """Schwarz_maxlvl 0: the interface seeds' blocks are their nodes (u0_I,
+    u1_I mirror pairs), so every level is node-aligned: GPU setup, BSR2 layout
+    (the multi-GPU path's format), and the PCG history of the oracle."""
+    M = _M()
+    s = M.problems.emi(dim, n, g)
+    B = M.MetricAMG(s, s.W, idofs=s.idofs, num_functions=2, Schwarz_maxlvl=0, **kw)
+    assert B.setup_path == 'gpu' and B.layout == 'bsr2'
+    b = M.problems.seeded_rhs(s.N, 1234)
+    solver = M.ConjGrad(s, precond=B, tolerance=1e-10, maxiter=500)     # src/emi_3d.py:143
+    B._Aop = s
+    solver * b
+    okw = dict(smoother='POLY') if kw.get('smoother') == 12 else {}
+    A = s.scipy()
+    h = mo.setup(A, mo.Params(num_functions=2, Schwarz_maxlvl=0, **okw), idofs=s.idofs)
+    ref = mo.pcg(A, h, b, 1e-10, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    # gamma >= 1e8: conditioning amplifies the summation-order difference
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6 if g < 1e8 else 1e-4, atol=0)
+    assert len(solver.residuals) < 80
+
+
 def _oracle_pcg_relres(A, h, b, tol, maxit):
     """PCG stopped on ||r||/||b|| (HAZmath linear_stop_type 1)."""
     x = np.zeros_like(b)

@@ -45,6 +45,40 @@ def test_virtual_ranks_match_oracle(lib_built, dim, n, g, P, rep):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('problem,kw,P', [
+    ('bidomain', dict(smoother='POLY'), 3), ('bidomain', dict(smoother='POLY', poly_degree=3), 8),
+    ('emi', {}, 2), ('emi', {}, 3), ('emi', dict(smoother='POLY'), 8), ('emi2d', dict(smoother='POLY'), 4)])
+def test_virtual_ranks_poly_and_emi(lib_built, problem, kw, P):
+    """The Chebyshev smoother (halo before every extra step; K built with the
+    first post step's smoother) and EMI (interface seeds with node-aligned
+    blocks, Schwarz_maxlvl 0: BSR2 + GPU setup on every rank) on P virtual
+    ranks equal the single-rank oracle apply (BASELINE config 4's operator)."""
+    import torch
+    import metric_amg_examples_amd as M
+    ckw = dict(kw)
+    if problem.startswith('emi'):
+        s = M.problems.emi(3, 16, 1e6) if problem == 'emi' else M.problems.emi(2, 64, 1e6)
+        kw = dict(kw, Schwarz_maxlvl=0)
+        ckw['Schwarz_maxlvl'] = 0
+    else:
+        s = M.problems.bidomain(3, 16, 1e6)
+    if ckw.get('smoother') == 'POLY':
+        ckw['smoother'] = 12
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                          num_functions=2, **ckw) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    z = _gather(s, hs, zs)
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
+    for hh in hs:
+        hh.close()
+
+
 @pytest.mark.parametrize('mode', ['unfused', 'sell', 'nohalf', 'merged'])
 def test_virtual_ranks_storage_variants(lib_built, monkeypatch, mode):
     """Distributed cycle without post fusion (prolongation, fine halo,
