@@ -48,8 +48,12 @@ class System:
         return A
 
 
-def finest_n(dim: int, nrefs: int) -> int:
-    return 2 ** ((5 if dim == 2 else 3) + nrefs - 1)
+def finest_n(dim: int, nrefs: int, problem: str = 'bidomain') -> int:
+    """Finest mesh of the drivers' refinement loops: bidomain_2d/3d
+    2**(5|3 + nrefs - 1) (src/bidomain_2d.py:168, src/bidomain_3d.py:113),
+    emi_2d/3d 2**(6|2 + nrefs - 1) (src/emi_2d.py:190, src/emi_3d.py:119)."""
+    first = {('bidomain', 2): 5, ('bidomain', 3): 3, ('emi', 2): 6, ('emi', 3): 2}[(problem, dim)]
+    return 2 ** (first + nrefs - 1)
 
 
 def bidomain(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0) -> System:

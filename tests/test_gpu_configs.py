@@ -106,3 +106,42 @@ def test_emi_3d_nrefs5_block_form(lib_built):
     assert np.allclose(solver.residuals, cres, rtol=1e-6, atol=0)
     assert len(solver.residuals) < 120
     H.close()
+
+
+def test_emi_3d_nrefs5_node_aligned_8_virtual_ranks(lib_built):
+    """BASELINE config 4 (emi_3d nrefs=5 gamma=1e6 row-partitioned over 8
+    GPUs): the interface seeds with node-aligned blocks (Schwarz_maxlvl 0),
+    GPU setup; one GPU against the C cycle on the same hierarchy, and the
+    8-rank row partition (virtual ranks: the RCCL path's counts, offsets and
+    kernels, device copies for the exchanges) against the one-GPU apply."""
+    import torch
+    M = _M()
+    n = M.problems.finest_n(3, 5, 'emi')
+    s = M.problems.emi(3, n, 1e6)
+    assert s.N == 278850
+    A = s.tocsr()
+    kw = dict(num_functions=2, Schwarz_maxlvl=0)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, setup='gpu', **kw)
+    r = M.problems.seeded_rhs(s.N)
+    z = B.matvec(torch.as_tensor(r).cuda()).cpu().numpy()
+    H = M.HostHierarchy(A, idofs=s.idofs, gpu=True, **kw)
+    ch = c_hierarchy(H, A)
+    assert rel(z, ch.apply(r)) < 1e-10
+    P = 8
+    hs = [M.DistMetricAMG(A, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=4096, **kw)
+          for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    zd = np.zeros(s.N)
+    for hh, zl in zip(hs, zs):
+        zl = zl.cpu().numpy()
+        zd[hh.o0:hh.o1] = zl[:hh.nloc]
+        zd[s.nv + hh.o0:s.nv + hh.o1] = zl[hh.nloc:]
+    say('EMI 3-D nrefs=5, 8 virtual ranks vs one GPU: %.2e' % rel(zd, z))
+    assert rel(zd, z) < 1e-10
+    for hh in hs:
+        hh.close()
+    H.close()
+    B.close()
