@@ -211,6 +211,23 @@ int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double
                             void* stream);
 int mamg_dist_virtual_spmv(mamg_dhandle** hs, int n, const double** d_x, double** d_y, void* stream);
 void mamg_dist_destroy(mamg_dhandle* h);
+/* Host-staged exchange backend: a pluggable transport for a handle made
+ * with comm_id == NULL (one process per rank, e.g. torch.distributed gloo).
+ * The pack / unpack kernels, the reverse-add in rank order and the op
+ * schedule are the RCCL path's; only the transport differs: payloads are
+ * staged through pinned host buffers and handed to the callbacks (0 = ok).
+ * Arrays are indexed by rank; entries for this rank and zero counts are
+ * unused.  Replaces RCCL where it cannot run (two ranks on one GPU). */
+typedef struct mamg_exchange {
+  void* ctx;
+  /* send scount[q] doubles from send[q] to every rank q, receive rcount[q]
+     doubles from q into recv[q] */
+  int (*sendrecv)(void* ctx, int nranks, double* const* send, const int64_t* scount,
+                  double* const* recv, const int64_t* rcount);
+  /* in-place sum of buf[count] over all ranks (the same result on every rank) */
+  int (*allreduce)(void* ctx, double* buf, int64_t count);
+} mamg_exchange;
+int mamg_dist_set_exchange(mamg_dhandle* h, const mamg_exchange* ex);
 
 /* ---- device hierarchy ------------------------------------------------- */
 /* Host setup + upload.  Level-0 matrix is uploaded from A directly. */

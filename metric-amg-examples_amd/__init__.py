@@ -9,8 +9,8 @@ Block form (src/utils.py:45-53): precond.get_hazmath_metric_precond -> R.T * Min
 File boundary (src/utils.py:304-333, src/run_solver_3d1d.py): fileio, drivers.
 """
 from . import _lib, fileio, parameters, precond, problems
-from .amg import DistMetricAMG, DistPlan, HostHierarchy, MetricAMG, metricAMG
+from .amg import DistMetricAMG, DistPlan, GlooExchange, HostHierarchy, MetricAMG, metricAMG
 from .krylov import ConjGrad, DistConjGrad, lanczos_eigenvalues
 
-__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'ConjGrad', 'DistConjGrad',
+__all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'GlooExchange', 'ConjGrad', 'DistConjGrad',
            'lanczos_eigenvalues', 'parameters', 'problems', 'precond', 'fileio', '_lib']

@@ -55,6 +55,14 @@ P_I32 = C.POINTER(C.c_int32)
 P_F64 = C.POINTER(C.c_double)
 VP = C.c_void_p
 
+# mamg_exchange (host-staged transport of a multi-GPU handle)
+SENDRECV_FN = C.CFUNCTYPE(C.c_int, VP, C.c_int, C.POINTER(P_F64), P_I64, C.POINTER(P_F64), P_I64)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, VP, P_F64, C.c_int64)
+
+
+class mamg_exchange(C.Structure):
+    _fields_ = [('ctx', VP), ('sendrecv', SENDRECV_FN), ('allreduce', ALLREDUCE_FN)]
+
 # every symbol include/mamg.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     'mamg_abi_version': (C.c_int, []),
@@ -88,6 +96,7 @@ SIGNATURES = {
     'mamg_dist_spmv_device': (C.c_int, [VP, VP, VP, VP]),
     'mamg_dist_virtual_spmv': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
     'mamg_dist_destroy': (None, [VP]),
+    'mamg_dist_set_exchange': (C.c_int, [VP, C.POINTER(mamg_exchange)]),
     'mamg_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                              C.POINTER(VP)]),
     'mamg_setup_gpu': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),

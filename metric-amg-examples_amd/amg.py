@@ -435,6 +435,38 @@ class DistPlan:
             pass
 
 
+class GlooExchange:
+    """mamg_exchange over the initialised torch.distributed group (gloo, CPU
+    tensors): point-to-point isend/irecv per peer, all-reduce as an
+    all-gather summed in rank order (deterministic, like the reverse-add)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.d, self.group = dist, group
+
+    def sendrecv(self, sends, counts):
+        import torch
+        reqs, bufs = [], {}
+        for q, n in counts.items():
+            bufs[q] = torch.empty(int(n), dtype=torch.float64)
+            reqs.append(self.d.irecv(bufs[q], src=q, group=self.group))
+        for q, a in sends.items():
+            reqs.append(self.d.isend(torch.from_numpy(np.ascontiguousarray(a)), dst=q, group=self.group))
+        for r in reqs:
+            r.wait()
+        return {q: b.numpy() for q, b in bufs.items()}
+
+    def allreduce(self, a):
+        import torch
+        n = self.d.get_world_size(self.group)
+        parts = [torch.empty(a.size, dtype=torch.float64) for _ in range(n)]
+        self.d.all_gather(parts, torch.from_numpy(np.ascontiguousarray(a)), group=self.group)
+        out = parts[0].numpy().copy()
+        for p in parts[1:]:
+            out += p.numpy()
+        return out
+
+
 class DistMetricAMG:
     """Multi-GPU preconditioner: one process per GPU (``mamg_setup_dist``).
 
@@ -445,7 +477,7 @@ class DistMetricAMG:
     builds a virtual (single-GPU, no RCCL) rank for tests."""
 
     def __init__(self, A, W=None, idofs=None, parameters=None, rank=0, nranks=1, comm_id=None,
-                 rep_nodes=32768, **overrides):
+                 rep_nodes=32768, exchange=None, **overrides):
         self._L = _lib.lib()
         indptr, indices, data, n, m = csr_arrays(A)
         self.shape = (n, n)
@@ -463,9 +495,52 @@ class DistMetricAMG:
                                            comm_id, int(rep_nodes), C.byref(h)))
         self._h = h
         self.rank, self.nranks = rank, nranks
+        self._exchange = None
+        if exchange is not None:
+            if comm_id is not None:
+                raise ValueError('exchange= replaces the RCCL communicator: pass comm_id=None')
+            self.set_exchange(exchange)
         o0, o1, nv = C.c_int64(), C.c_int64(), C.c_int64()
         _lib.check(self._L.mamg_dist_range(h, C.byref(o0), C.byref(o1), C.byref(nv)))
         self.o0, self.o1, self.nv = o0.value, o1.value, nv.value
+
+    def set_exchange(self, exchange):
+        """Host-staged transport (mamg_dist_set_exchange): 'gloo' = the
+        initialised torch.distributed process group (CPU tensors), or an
+        object with sendrecv(sends, recv_counts) -> {q: ndarray} and
+        allreduce(ndarray) -> ndarray.  The device kernels and the exchange
+        schedule are the RCCL path's."""
+        ex = GlooExchange() if exchange == 'gloo' else exchange
+        me, P = self.rank, self.nranks
+
+        def sendrecv(ctx, n, send, scount, recv, rcount):
+            try:
+                sends = {q: np.ctypeslib.as_array(send[q], (scount[q],)) for q in range(n)
+                         if q != me and scount[q] > 0}
+                counts = {q: rcount[q] for q in range(n) if q != me and rcount[q] > 0}
+                got = ex.sendrecv(sends, counts)
+                for q, a in got.items():
+                    np.ctypeslib.as_array(recv[q], (counts[q],))[:] = a
+                return 0
+            except Exception:          # noqa: BLE001 -- reported through the status code
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def allreduce(ctx, buf, count):
+            try:
+                a = np.ctypeslib.as_array(buf, (count,))
+                a[:] = ex.allreduce(a.copy())
+                return 0
+            except Exception:          # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+        fns = (_lib.SENDRECV_FN(sendrecv), _lib.ALLREDUCE_FN(allreduce))
+        st = _lib.mamg_exchange(None, fns[0], fns[1])
+        _lib.check(self._L.mamg_dist_set_exchange(self._h, C.byref(st)))
+        self._exchange = (ex, fns, st)          # the callbacks must outlive the handle's use
+        assert P == self.nranks
 
     @staticmethod
     def unique_id() -> bytes:

@@ -379,6 +379,16 @@ int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double
   GUARD_END
 }
 
+int mamg_dist_set_exchange(mamg_dhandle* h, const mamg_exchange* ex) {
+  GUARD_BEGIN
+  if (!h || !ex || !ex->sendrecv || !ex->allreduce) { set_error("null argument"); return MAMG_ERR_ARG; }
+  std::string err;
+  int rc = mamg::dist_set_exchange(h->d, *ex, &err);
+  if (rc) set_error(err);
+  return rc;
+  GUARD_END
+}
+
 void mamg_dist_destroy(mamg_dhandle* h) {
   if (!h) return;
   mamg::dist_destroy(h->d);

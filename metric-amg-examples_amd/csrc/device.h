@@ -49,6 +49,7 @@ int dist_virtual_spmv(const std::vector<DistHandle*>& hs, const std::vector<cons
                       const std::vector<double*>& y, void* stream, std::string* err);
 int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
                     double* kernel_ms, double* class_bytes, void* stream, std::string* err);
+int dist_set_exchange(DistHandle* h, const mamg_exchange& ex, std::string* err);
 int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
                        const std::vector<double*>& z, void* stream, std::string* err);
 

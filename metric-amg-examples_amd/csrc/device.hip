@@ -3165,7 +3165,16 @@ struct DistHandle {
   bool dry = false;                    // MAMG_DIST_DRY: virtual rank skips its exchanges (timing only)
   hipStream_t side = nullptr;          // stream of the interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  // host-staged exchange backend (mamg_dist_set_exchange): pinned staging
+  // per level (sends, ghost payloads, receives of the reverse-add) and one
+  // all-reduce buffer
+  bool host_ex = false;
+  mamg_exchange ex{};
+  std::vector<double*> hsend, hghost, hrecv;
+  double* hred = nullptr;
+  std::vector<void*> pinned;
   ~DistHandle() {
+    for (void* q : pinned) (void)hipHostFree(q);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (side) (void)hipStreamDestroy(side);
@@ -3313,6 +3322,77 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   }
 }
 
+// one exchange through the host callbacks: device payloads staged in pinned
+// memory around the callback (stream synchronised first), the same pack /
+// unpack / rank-ordered reverse-add kernels as the RCCL branch of run_dop
+int run_dop_host(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
+  const int P = h->nranks;
+  std::vector<double*> snd(P, nullptr), rcv(P, nullptr);
+  std::vector<int64_t> sc(P, 0), rc(P, 0);
+  if (d.dk == D_ALLREDUCE) {
+    HIPCHK(hipMemcpyAsync(h->hred, d.buf, d.count * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h->ex.allreduce(h->ex.ctx, h->hred, d.count)) { *err = "exchange allreduce callback failed"; return MAMG_ERR_HIP; }
+    HIPCHK(hipMemcpyAsync(d.buf, h->hred, d.count * sizeof(double), hipMemcpyHostToDevice, s));
+    return MAMG_OK;
+  }
+  const DDLevel& D = h->L[d.level];
+  const int64_t ns = D.send_off.back();
+  if (d.dk == D_OVERLAP) {   // interior rows on the side stream, host halo on s, join
+    HIPCHK(hipEventRecord(h->ev_in, s));
+    HIPCHK(hipStreamWaitEvent(h->side, h->ev_in, 0));
+    launch(d.op, h->side);
+    HIPCHK(hipEventRecord(h->ev_out, h->side));
+    DOp hd = d;
+    hd.dk = D_HALO;
+    int r = run_dop_host(h, hd, s, err);
+    HIPCHK(hipStreamWaitEvent(s, h->ev_out, 0));
+    return r;
+  }
+  double* hs = h->hsend[d.level];
+  double* hg = h->hghost[d.level];
+  double* hr = h->hrecv[d.level];
+  for (int q = 0; q < P; ++q) {
+    if (q == h->rank) continue;
+    const int64_t sq = D.send_off[q + 1] - D.send_off[q], gq = D.ghost_off[q + 1] - D.ghost_off[q];
+    if (d.dk == D_HALO) {   // my owned values they ghost -> their ghosts of mine
+      snd[q] = hs + 2 * D.send_off[q]; sc[q] = 2 * sq;
+      rcv[q] = hg + 2 * D.ghost_off[q]; rc[q] = 2 * gq;
+    } else {                // D_REVERSE: my ghost partials -> their owned rows
+      snd[q] = hg + 2 * D.ghost_off[q]; sc[q] = 2 * gq;
+      rcv[q] = hr + 2 * D.send_off[q]; rc[q] = 2 * sq;
+    }
+  }
+  if (d.dk == D_HALO) {
+    if (ns) {
+      pack2_kernel<<<nblocks(ns), 256, 0, s>>>(ns, D.send_idx, d.buf, D.sendbuf);
+      HIPCHK(hipMemcpyAsync(hs, D.sendbuf, 2 * ns * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (h->ex.sendrecv(h->ex.ctx, P, snd.data(), sc.data(), rcv.data(), rc.data())) {
+      *err = "exchange sendrecv callback failed";
+      return MAMG_ERR_HIP;
+    }
+    if (D.ng)
+      HIPCHK(hipMemcpyAsync(d.buf + 2 * D.nloc, hg, 2 * D.ng * sizeof(double), hipMemcpyHostToDevice, s));
+    return MAMG_OK;
+  }
+  // D_REVERSE
+  if (D.ng) HIPCHK(hipMemcpyAsync(hg, d.buf + 2 * D.nloc, 2 * D.ng * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (h->ex.sendrecv(h->ex.ctx, P, snd.data(), sc.data(), rcv.data(), rc.data())) {
+    *err = "exchange sendrecv callback failed";
+    return MAMG_ERR_HIP;
+  }
+  if (ns) HIPCHK(hipMemcpyAsync(D.recvbuf, hr, 2 * ns * sizeof(double), hipMemcpyHostToDevice, s));
+  for (int q = 0; q < P; ++q) {
+    const int64_t sq = D.send_off[q + 1] - D.send_off[q];
+    if (q == h->rank || !sq) continue;
+    addidx2_kernel<<<nblocks(sq), 256, 0, s>>>(sq, D.send_idx + D.send_off[q], D.recvbuf + 2 * D.send_off[q], d.buf);
+  }
+  return MAMG_OK;
+}
+
 int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
   if (d.dk == D_OP) {
     launch(d.op, s);
@@ -3326,6 +3406,7 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     if (d.dk == D_OVERLAP) launch(d.op, s);
     return MAMG_OK;
   }
+  if (!h->comm && h->host_ex) return run_dop_host(h, d, s, err);
   if (!h->comm) {
     *err = "virtual rank handle (no communicator): use mamg_dist_virtual_apply / _spmv";
     return MAMG_ERR_ARG;
@@ -3703,6 +3784,40 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
     }
   }
   HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+int dist_set_exchange(DistHandle* h, const mamg_exchange& ex, std::string* err) {
+  if (h->comm) { *err = "handle has an RCCL communicator; the host exchange is for comm_id == NULL"; return MAMG_ERR_ARG; }
+  HIPCHK(hipSetDevice(h->device));
+  auto pin = [&](double** p, int64_t n) -> int {
+    *p = nullptr;
+    if (n <= 0) return MAMG_OK;
+    void* q = nullptr;
+    HIPCHK(hipHostMalloc(&q, n * sizeof(double), hipHostMallocDefault));
+    h->pinned.push_back(q);
+    *p = (double*)q;
+    return MAMG_OK;
+  };
+  if (!h->host_ex) {
+    int64_t red = 0;
+    const int nl = (int)h->L.size();
+    h->hsend.assign(nl, nullptr);
+    h->hghost.assign(nl, nullptr);
+    h->hrecv.assign(nl, nullptr);
+    for (int l = 0; l < nl; ++l) {
+      const DDLevel& D = h->L[l];
+      const int64_t ns = D.send_off.empty() ? 0 : D.send_off.back();
+      int rc;
+      if ((rc = pin(&h->hsend[l], 2 * ns)) || (rc = pin(&h->hghost[l], 2 * D.ng)) || (rc = pin(&h->hrecv[l], 2 * ns)))
+        return rc;
+      red = std::max(red, 2 * D.nv);
+    }
+    int rc = pin(&h->hred, red);
+    if (rc) return rc;
+  }
+  h->ex = ex;
+  h->host_ex = true;
   return MAMG_OK;
 }
 

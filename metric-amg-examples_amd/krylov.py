@@ -248,8 +248,10 @@ class DistConjGrad:
         import torch.distributed as dist
         h = hs[0]
 
+        dev = 'cpu' if dist.get_backend(group) == 'gloo' else 'cuda'   # gloo: host-staged ranks
+
         def allreduce(v):
-            t = torch.tensor([v], dtype=torch.float64, device='cuda')
+            t = torch.tensor([v], dtype=torch.float64, device=dev)
             dist.all_reduce(t, group=group)
             return float(t.item())
         return cls(lambda xs, ys: h.spmv_device(xs[0], ys[0], stream),

@@ -249,3 +249,83 @@ def test_virtual_ranks_band_schedule_bitwise(lib_built, monkeypatch):
             hh.close()
     for a, b in zip(out[0], out[1]):
         assert np.array_equal(a, b)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _host_exchange_worker(rank, world, port, q, problem, kw):
+    """one rank process: the product's rank-local handle on the (shared) GPU,
+    its exchanges through the host-staged gloo transport"""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, 'oracle')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import metric_amg_examples_amd as M
+        import mamg_oracle
+        s = M.problems.emi(3, 16, 1e6) if problem == 'emi' else M.problems.bidomain(3, 16, 1e6)
+        A = s.tocsr() if problem == 'emi' else s
+        h = M.DistMetricAMG(A, s.W, idofs=s.idofs, rank=rank, nranks=world, comm_id=None, rep_nodes=100,
+                            exchange='gloo', num_functions=2, **kw)
+        r = torch.as_tensor(h.local_slice(mamg_oracle.seeded_rhs(s.N))).cuda()
+        z = torch.zeros_like(r)
+        h.apply_device(r, z)
+        torch.cuda.synchronize()
+        cg = M.DistConjGrad.for_handles(h, tolerance=1e-8, maxiter=500)
+        x = cg.solve([r.clone()])[0]
+        torch.cuda.synchronize()
+        q.put((rank, h.o0, h.o1, z.cpu().numpy(), x.cpu().numpy(), list(cg.residuals)))
+        h.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother=12, Schwarz_maxlvl=0))])
+def test_two_processes_host_exchange(lib_built, problem, kw):
+    """Two rank processes on the one GPU of the box, exchanging through the
+    host-staged gloo transport (RCCL refuses two ranks on one GPU): each
+    builds its plan and rank-local operators in its own process and runs the
+    product's pack / halo / reverse-add / all-reduce schedule; the gathered
+    apply equals the oracle's, and DistConjGrad (dots all-reduced over gloo)
+    has the oracle PCG's iteration count and residuals."""
+    import torch.multiprocessing as mp
+    import metric_amg_examples_amd as M
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_exchange_worker, args=(r, 2, port, q, problem, kw)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s = M.problems.emi(3, 16, 1e6) if problem == 'emi' else M.problems.bidomain(3, 16, 1e6)
+    okw = {'smoother': 'POLY', 'Schwarz_maxlvl': 0} if kw else {}
+    A = s.scipy()
+    h = mo.setup(A, mo.Params(num_functions=2, **okw), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    ref = mo.pcg(A, h, r, 1e-8, 500)
+    z, x = np.zeros(s.N), np.zeros(s.N)
+    for rank, o0, o1, zl, xl, resid in res:
+        nloc = o1 - o0
+        z[o0:o1], z[s.nv + o0:s.nv + o1] = zl[:nloc], zl[nloc:]
+        x[o0:o1], x[s.nv + o0:s.nv + o1] = xl[:nloc], xl[nloc:]
+        assert len(resid) == len(ref.residuals)
+        assert np.allclose(resid, ref.residuals, rtol=1e-6, atol=0)
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-6
