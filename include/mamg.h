@@ -64,7 +64,9 @@ enum {                                                   /* aggregation_type  */
 };                                                       /* only MIS accepted */
 enum {                                                   /* Schwarz_type      */
   MAMG_SCHWARZ_FORWARD = 1, MAMG_SCHWARZ_BACKWARD = 2, MAMG_SCHWARZ_SYMMETRIC = 3,
-  MAMG_SCHWARZ_BLOCK_JACOBI = 4  /* additive non-overlapping seed blocks (GPU) */
+  MAMG_SCHWARZ_BLOCK_JACOBI = 4, /* additive non-overlapping seed blocks (GPU) */
+  MAMG_SCHWARZ_ADDITIVE = 5      /* additive overlapping seed + maxlvl-ring blocks
+                                    (sparse seed sets, e.g. 3D-1D; CSR layout) */
 };
 enum { MAMG_OFF = 0, MAMG_ON = 1 };
 enum { MAMG_COARSE_DENSE = 32 };  /* coarse_solver: 32 (UMFPACK in HAZmath)  */

@@ -1081,6 +1081,10 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     dv4_t* Dsm = nullptr;
     RCHK(S.alloc(&Dsm, nv, err));
     const bool seeds = seed_blocks_on(p, l, idofs, n_idofs);
+    if (seeds && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
+      *err = "GPU setup: SCHWARZ_ADDITIVE (overlapping seed rings) is built by the host setup (mamg_setup)";
+      return MAMG_ERR_UNSUPPORTED;
+    }
     if (seeds) {
       int32_t* di = nullptr;
       uint8_t* isseed = nullptr;

@@ -516,6 +516,108 @@ int block_smoother_from(const CsrView& A, const std::vector<int64_t>& bid, int64
   return MAMG_OK;
 }
 
+// additive overlapping Schwarz on the seeds' rings (Schwarz_type ADDITIVE,
+// oracle overlap_smoother): blocks = seed + breadth-first neighbours up to
+// distance Schwarz_maxlvl (ascending columns, at most Schwarz_mmsize dofs),
+// S = sum_k R_k^T A_k^-1 R_k (+ 1/a_ii on uncovered dofs) accumulated block by
+// block in seed order, W = (relaxation / lambda) S with lambda from
+// max(rho_iters, 30) power iterations of S A
+int overlap_smoother(const CsrView& A, const int32_t* seeds, int64_t ns, const mamg_params& p, Csr* W,
+                     std::string* err) {
+  const int64_t n = A.n;
+  const int maxlvl = p.Schwarz_maxlvl, mm = p.Schwarz_mmsize;
+  if (ns > std::max<int64_t>(n / 8, 1) || (double)ns * mm * mm > 4e9) {
+    *err = "SCHWARZ_ADDITIVE (dense overlapping seed blocks) is for sparse seed sets: " + std::to_string(ns) +
+           " seeds of up to " + std::to_string(mm) + " dofs";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  std::vector<std::vector<int64_t>> blocks(ns);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t k = 0; k < ns; ++k) {
+    const int64_t s0 = seeds[k];
+    std::vector<int64_t> order{s0};
+    std::vector<int> depth{0};
+    auto seen = [&](int64_t j) { return std::find(order.begin(), order.end(), j) != order.end(); };
+    size_t head = 0;
+    while (head < order.size() && (int64_t)order.size() < mm) {
+      const int64_t v = order[head];
+      const int dv = depth[head];
+      ++head;
+      if (dv == maxlvl) continue;
+      for (int64_t q = A.ptr[v]; q < A.ptr[v + 1]; ++q) {
+        const int64_t j = A.col[q];
+        if (!seen(j)) {
+          order.push_back(j);
+          depth.push_back(dv + 1);
+          if ((int64_t)order.size() >= mm) break;
+        }
+      }
+    }
+    std::sort(order.begin(), order.end());
+    blocks[k] = std::move(order);
+  }
+  // sorted pattern: every block's dense square, plus the uncovered diagonal
+  std::vector<char> cov(n, 0);
+  for (const auto& b : blocks)
+    for (int64_t i : b) cov[i] = 1;
+  std::vector<std::vector<int32_t>> rc(n);
+  for (const auto& b : blocks)
+    for (int64_t i : b)
+      for (int64_t j : b) rc[i].push_back((int32_t)j);
+  W->n = W->m = n;
+  W->ptr.assign(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (!cov[i]) rc[i].push_back((int32_t)i);
+    std::sort(rc[i].begin(), rc[i].end());
+    rc[i].erase(std::unique(rc[i].begin(), rc[i].end()), rc[i].end());
+    W->ptr[i + 1] = W->ptr[i] + (int64_t)rc[i].size();
+  }
+  W->col.resize(W->ptr[n]);
+  W->val.assign(W->ptr[n], 0.0);
+  for (int64_t i = 0; i < n; ++i) std::copy(rc[i].begin(), rc[i].end(), W->col.begin() + W->ptr[i]);
+  std::vector<std::vector<int32_t>>().swap(rc);
+  const CsrView Wv = W->view();
+  for (const auto& b : blocks) {   // block order: the oracle's accumulation order
+    const int64_t m = (int64_t)b.size();
+    std::vector<double> dense(m * m, 0.0), inv(m * m);
+    for (int64_t a = 0; a < m; ++a)
+      for (int64_t c = 0; c < m; ++c) {
+        const int64_t q = find_pos(A, b[a], b[c]);
+        if (q >= 0) dense[a * m + c] = A.val[q];
+      }
+    if (!gauss_jordan(m, dense.data(), inv.data())) { *err = "Schwarz block not SPD"; return MAMG_ERR_SETUP; }
+    for (int64_t a = 0; a < m; ++a)
+      for (int64_t c = 0; c < m; ++c) W->val[find_pos(Wv, b[a], b[c])] += inv[a * m + c];
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (!cov[i]) W->val[find_pos(Wv, i, i)] = 1.0 / diag_of(A, i);
+  // lambda_max(S A): inf-norm power iterations (rho_estimate's start vector)
+  std::vector<double> v(n), t(n), w(n);
+  for (int64_t i = 0; i < n; ++i) v[i] = ((double)hash32((uint64_t)i, 977) / 4294967296.0) * 2.0 - 1.0;
+  double lam = 0.0;
+  for (int it = 0; it < std::max(p.rho_iters, 30); ++it) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      double s = 0.0;
+      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) s += A.val[k] * v[A.col[k]];
+      t[i] = s;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      double s = 0.0;
+      for (int64_t k = W->ptr[i]; k < W->ptr[i + 1]; ++k) s += W->val[k] * t[W->col[k]];
+      w[i] = s;
+    }
+    double mv = 0.0, mw = 0.0;
+    for (int64_t i = 0; i < n; ++i) { mv = std::max(mv, std::fabs(v[i])); mw = std::max(mw, std::fabs(w[i])); }
+    lam = mw / mv;
+    for (int64_t i = 0; i < n; ++i) v[i] = w[i] / mw;
+  }
+  const double sc = p.relaxation / lam;
+  for (double& x : W->val) x = sc * x;
+  return MAMG_OK;
+}
+
 // node blocks: bid(f*nv + I) = I
 void node_blocks(int64_t n, int nf, std::vector<int64_t>* bid, int64_t* nb) {
   const int64_t nv = n / nf;
@@ -707,14 +809,16 @@ int check_params(const mamg_params& p, std::string* err) {
     const bool gsm = p.smoother == MAMG_SMOOTHER_GS || p.smoother == MAMG_SMOOTHER_SGS;
     const int want = p.smoother == MAMG_SMOOTHER_SGS ? MAMG_SCHWARZ_SYMMETRIC
                      : p.smoother == MAMG_SMOOTHER_GS ? MAMG_SCHWARZ_FORWARD : MAMG_SCHWARZ_BLOCK_JACOBI;
-    if (p.Schwarz_type != want) {
+    const bool additive_ok = !gsm && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE;
+    if (p.Schwarz_type != want && !additive_ok) {
       *err = std::string("Schwarz_type must match the smoother: SCHWARZ_BLOCK_JACOBI with the Jacobi smoothers, ") +
-             "SCHWARZ_SYMMETRIC with SMOOTHER_SGS, SCHWARZ_FORWARD with SMOOTHER_GS" + (gsm ? "" : "");
+             "SCHWARZ_SYMMETRIC with SMOOTHER_SGS, SCHWARZ_FORWARD with SMOOTHER_GS (SCHWARZ_ADDITIVE: overlapping "
+             "seed rings with the Jacobi-family smoothers)";
       return MAMG_ERR_UNSUPPORTED;
     }
-    if (p.Schwarz_maxlvl > 1) {
-      *err = "Schwarz_maxlvl > 1 (overlapping seed + ring blocks) not implemented; 1 = non-overlapping "
-             "partition of the seeds' 1-rings";
+    if (p.Schwarz_maxlvl > 1 && p.Schwarz_type != MAMG_SCHWARZ_ADDITIVE) {
+      *err = "Schwarz_maxlvl > 1 needs SCHWARZ_ADDITIVE (overlapping seed + ring blocks); the non-overlapping "
+             "seed blocks are the seeds' 1-rings";
       return MAMG_ERR_UNSUPPORTED;
     }
   }
@@ -806,7 +910,10 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
     const bool need_rho = (p.AMG_type == MAMG_SA_AMG && !blockP) || p.smoother == MAMG_SMOOTHER_JACOBI_RHO ||
                           p.smoother == MAMG_SMOOTHER_POLY;
     const double rho = need_rho ? rho_estimate(cur, dinv, rs, p.rho_iters) : 0.0;
-    if (seed_blocks_on(p, l, idofs, n_idofs)) {
+    if (seed_blocks_on(p, l, idofs, n_idofs) && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
+      rc = overlap_smoother(cur, idofs, n_idofs, p, &lev.WB, err);
+      if (rc) return rc;
+    } else if (seed_blocks_on(p, l, idofs, n_idofs)) {
       rc = block_smoother(cur, idofs, n_idofs, p, &lev.WB, err);
       if (rc) return rc;
     } else if (nf > 1 && p.node_block_smoother) {

@@ -166,7 +166,7 @@ def emi_3d1d(argv):
         fileio.dump_system(A, b, s.W, args.outdir)
         return None
     # alternative solver: the file-free path of solve_haznics (src/utils.py:95-127)
-    B = MetricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_metric_mi355x)
+    B = MetricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_metric_3d1d)
     solver = ConjGrad(A, precond=B, tolerance=1e-6, maxiter=1000, stop_type=1)
     solver * b
     print('niters %d' % (len(solver.residuals) - 1))

@@ -134,7 +134,17 @@ def dat_to_parameters(d: dict):
         prm['coarse_scaling'] = P.ON if str(d['AMG_coarse_scaling']).upper() == 'ON' else P.OFF
     if 'AMG_aggregation_type' in d:
         prm['aggregation_type'] = _AGG.get(int(d['AMG_aggregation_type']), P.VMB)
+    maxlvl = prm.get('Schwarz_maxlvl', 1)
     mapped, n2 = P.to_gpu_profile(prm)
+    # the file-based 3D-1D solve seeds the sparse 1-D dofs: HAZmath's
+    # multiplicative Schwarz on their maxlvl-rings becomes the additive
+    # overlapping Schwarz on the same blocks (all blocks in parallel)
+    if mapped.get('Schwarz_levels', 0) >= 1 and maxlvl >= 1:
+        n2 = [m for m in n2 if not m.startswith('Schwarz_maxlvl') and not m.startswith('Schwarz_type')]
+        notes.append('Schwarz_type %r (multiplicative) -> SCHWARZ_ADDITIVE on the same seed + %d-ring blocks '
+                     '(overlapping, parallel)' % (prm.get('Schwarz_type'), maxlvl))
+        mapped['Schwarz_maxlvl'] = maxlvl
+        mapped['Schwarz_type'] = P.SCHWARZ_ADDITIVE
     # the file-based 3D-1D solve seeds the 1-D dofs: its seed blocks are not
     # node-aligned, so it runs the CSR layout, where the multicolour GS
     # smoothers (node-block) do not exist; HAZmath's relaxation is an SOR
@@ -143,7 +153,8 @@ def dat_to_parameters(d: dict):
         notes.append('smoother GS/SGS -> SMOOTHER_JACOBI_RHO (seeds not node-aligned: CSR layout, '
                      'no node-block multicolour GS)')
         mapped['smoother'] = P.SMOOTHER_JACOBI_RHO
-        mapped['Schwarz_type'] = P.SCHWARZ_BLOCK_JACOBI
+        if mapped.get('Schwarz_type') != P.SCHWARZ_ADDITIVE:
+            mapped['Schwarz_type'] = P.SCHWARZ_BLOCK_JACOBI
         mapped.pop('num_functions', None)
         mapped['relaxation'] = 4.0 / 3.0
         notes.append('relaxation %s -> 4/3 (weight of the relaxation/rho Jacobi smoother)'

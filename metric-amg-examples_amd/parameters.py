@@ -33,6 +33,7 @@ SMOOTHER_GS, SMOOTHER_SGS = 10, 11
 SMOOTHER_POLY = 12            # Chebyshev polynomial in W A (HAZmath/FASP SMOOTHER_POLY)
 VMB, MIS, MWM, HEC, HEM = 1, 2, 3, 4, 5
 SCHWARZ_FORWARD, SCHWARZ_BACKWARD, SCHWARZ_SYMMETRIC, SCHWARZ_BLOCK_JACOBI = 1, 2, 3, 4
+SCHWARZ_ADDITIVE = 5          # overlapping seed + Schwarz_maxlvl-ring blocks, additive (sparse seed sets)
 OFF, ON = 0, 1
 SOLVER_UMFPACK = 32          # coarse_solver / Schwarz_blksolver: dense direct here
 
@@ -77,6 +78,14 @@ parameters_metric_mi355x = {
 # Jacobi for two extra level-0 SpMVs per cycle
 parameters_metric_mi355x_poly = dict(
     parameters_metric_mi355x, smoother=SMOOTHER_POLY, poly_degree=2, poly_ratio=16.0)
+
+# 3D-1D (sparse 1-D seeds, scalar hierarchy, CSR layout): the seeds' 2-ring
+# blocks (src/input_metric.dat:96-100) overlapping, smoothed additively --
+# the parallel counterpart of HAZmath's multiplicative Schwarz there, which
+# is what makes the averaged coupling gamma-robust
+parameters_metric_3d1d = dict(
+    parameters_metric_mi355x, num_functions=1, Schwarz_type=SCHWARZ_ADDITIVE, Schwarz_maxlvl=2,
+    Schwarz_mmsize=200, coarse_dof=300, max_levels=30)
 
 # the reference's smoothers on the GPU: multicolour
 # node-block SGS (level 0: symmetric multiplicative Schwarz on the seed blocks)

@@ -220,6 +220,7 @@ class Params:
     Schwarz_levels: int = 1       # 1: seed-block Jacobi on level 0 (needs idofs)
     Schwarz_mmsize: int = 100     # max dofs per seed block
     Schwarz_maxlvl: int = 1       # 1: seed + joined 1-ring neighbours; 0: the seed's node (node blocks)
+    Schwarz_type: int = 4         # 4: non-overlapping seed blocks (block Jacobi); 5: additive overlapping rings
     sa_omega: float = 4.0 / 3.0   # prolongator smoothing  w = sa_omega / rho
     rho_iters: int = 0            # 0: Gershgorin bound; >0: inf-norm power its
     max_coarse_dense: int = 8192
@@ -622,6 +623,92 @@ def block_smoother(A: sp.csr_matrix, seeds, p: Params, blocks=None) -> sp.csr_ma
 
 
 # --------------------------------------------------------------------------
+# additive overlapping Schwarz on the seeds' rings (Schwarz_type ADDITIVE):
+# the reference's seed + Schwarz_maxlvl-ring blocks (src/amg_parameters.py:
+# 83-86, src/input_metric.dat:96-100) smoothed additively, so the blocks can
+# overlap and every block works in parallel; dofs in no block take 1/a_ii
+# --------------------------------------------------------------------------
+SCHWARZ_ADDITIVE = 5
+
+
+def seed_ring_blocks(A: sp.csr_matrix, seeds, maxlvl: int, mmsize: int):
+    """Per seed (in the given order): the seed, then breadth-first its graph
+    neighbours up to distance maxlvl, each vertex's neighbours in ascending
+    order, stopping at mmsize dofs; members sorted."""
+    ip, ix = A.indptr, A.indices
+    blocks = []
+    for s0 in np.asarray(seeds, dtype=np.int64):
+        s0 = int(s0)
+        seen = {s0}
+        order = [s0]
+        head = 0
+        depth = {s0: 0}
+        while head < len(order) and len(order) < mmsize:
+            v = order[head]
+            head += 1
+            if depth[v] == maxlvl:
+                continue
+            for j in ix[ip[v]:ip[v + 1]]:
+                j = int(j)
+                if j not in seen:
+                    seen.add(j)
+                    order.append(j)
+                    depth[j] = depth[v] + 1
+                    if len(order) >= mmsize:
+                        break
+        blocks.append(np.array(sorted(order), dtype=np.int64))
+    return blocks
+
+
+def overlap_smoother(A: sp.csr_matrix, seeds, p: 'Params'):
+    """W = (relaxation / lambda) S,  S = sum_k R_k^T A_k^-1 R_k (+ 1/a_ii on
+    dofs in no block).  A_k^-1 by Gauss-Jordan; S accumulated block by block
+    (k ascending, rows then columns of each block) on its sorted pattern from
+    0.0; lambda = max(rho_iters, 30) inf-norm power iterations of S A from
+    the hash start vector (the spectrum of an overlapping sum is far below
+    its Gershgorin bound).  Returns (W, blocks)."""
+    A = A.tocsr()
+    n = A.shape[0]
+    blocks = seed_ring_blocks(A, seeds, p.Schwarz_maxlvl, p.Schwarz_mmsize)
+    cov = np.zeros(n, dtype=bool)
+    rows, cols = [], []
+    for b in blocks:
+        cov[b] = True
+        rows.append(np.repeat(b, len(b)))
+        cols.append(np.tile(b, len(b)))
+    unc = np.flatnonzero(~cov)
+    rows.append(unc)
+    cols.append(unc)
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    key = np.unique(r * n + c)
+    pr, pc = key // n, key % n
+    indptr = np.concatenate([[0], np.cumsum(np.bincount(pr, minlength=n))]).astype(np.int64)
+    data = np.zeros(len(key))
+    for b in blocks:
+        dense = A[b][:, b].toarray()
+        Ki = batched_inverse(dense[None, :, :])[0]
+        pos = np.searchsorted(key, (np.repeat(b, len(b)) * n + np.tile(b, len(b))))
+        for t in range(len(pos)):          # sequential: duplicates in block order
+            data[pos[t]] += Ki.ravel()[t]
+    if len(unc):
+        pos = np.searchsorted(key, unc * n + unc)
+        data[pos] = 1.0 / A.diagonal()[unc]
+    S = sp.csr_matrix((data, pc.astype(np.int64), indptr), shape=(n, n))
+    S.has_sorted_indices = True
+    v = (hash32(np.arange(n), 977).astype(np.float64) / 4294967296.0) * 2.0 - 1.0
+    lam = 0.0
+    for _ in range(max(int(p.rho_iters), 30)):
+        w = _rowsum_seq(S, _rowsum_seq(A, v))
+        mv, mw = float(np.max(np.abs(v))), float(np.max(np.abs(w)))
+        lam = mw / mv
+        v = w / mw
+    W = S.copy()
+    W.data = (p.relaxation / lam) * W.data
+    return W, blocks
+
+
+# --------------------------------------------------------------------------
 # multicolour node-block Gauss-Seidel (the reference's SGS smoother,
 # src/amg_parameters.py:72, and its level-0 multiplicative Schwarz on the seed
 # blocks, src/utils.py:84 / amg_parameters.py:83-86, in a GPU-parallel order)
@@ -865,7 +952,11 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         if gs and (nf != 2 or not p.node_block_smoother):
             raise ValueError('multicolour GS needs num_functions = 2 and node-block smoothers')
         pj = dataclasses.replace(p, smoother='JACOBI_RHO') if gs else p
-        if l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1:
+        if l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1 \
+                and p.Schwarz_type == SCHWARZ_ADDITIVE:
+            lev.WB, _ = overlap_smoother(cur, idofs, pj)
+            nbk = 0
+        elif l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1:
             lev.WB, lev.bid, nbk = block_smoother(cur, idofs, pj)
         elif nf > 1 and p.node_block_smoother:
             lev.WB, lev.bid, nbk = block_smoother(cur, None, pj, node_blocks(n, nf))

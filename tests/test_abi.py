@@ -45,7 +45,9 @@ def test_params_struct_layout(lib_built):
     (dict(coarse_scaling=2), -1),
     (dict(Schwarz_type=3), -4),              # multiplicative seed blocks need the SGS smoother
     (dict(num_functions=2, smoother=11, Schwarz_type=4), -4),
-    (dict(Schwarz_maxlvl=2), -4),            # overlapping seed + ring blocks
+    (dict(Schwarz_maxlvl=2), -4),            # overlapping seed + ring blocks need SCHWARZ_ADDITIVE
+    (dict(Schwarz_maxlvl=0), -4),            # seed-node blocks need num_functions >= 2
+    (dict(num_functions=2, smoother=11, Schwarz_type=5), -4),   # ADDITIVE is for Jacobi-family smoothers
     (dict(cycle_type=3), -4),
     (dict(max_levels=0), -1),
     (dict(spmv_lanes=3), -1),

@@ -104,7 +104,7 @@ def _oracle_pcg_relres(A, h, b, tol, maxit):
     return x, it
 
 
-@pytest.mark.parametrize('radius,g', [(0.0, 1e2), (0.0, 1e8), (1.0, 1e4), (2.5, 1e2)])
+@pytest.mark.parametrize('radius,g', [(0.0, 1e2), (0.0, 1e8), (1.0, 1e4), (2.5, 1e2), (1.0, 1e6), (2.5, 1e8)])
 def test_file_based_3d1d_solve(lib_built, tmp_path, radius, g):
     """emi_3d1d -dump 1 -> run_solver_3d1d (haznics.fenics_metric_solver_xd_1d
     restated) -> solution.txt; iteration count = the oracle's with the same
@@ -120,10 +120,12 @@ def test_file_based_3d1d_solve(lib_built, tmp_path, radius, g):
     niters = drivers.fenics_metric_solver_xd_1d(dat, str(mdir) + '/', str(odir) + '/', quiet=True)
     x = M.fileio.read_solution(str(odir / 'solution.txt'))
     assert np.linalg.norm(b - A @ x) <= 1e-6 * np.linalg.norm(b) * (1 + 1e-9)
-    prm = mo.Params(coarse_dof=300, max_levels=30, Schwarz_mmsize=200)
+    # the file's Schwarz (maxlvl 2, mmsize 200) -> additive overlapping rings
+    prm = mo.Params(coarse_dof=300, max_levels=30, Schwarz_mmsize=200, Schwarz_type=5, Schwarz_maxlvl=2)
     h = mo.setup(A, prm, idofs=s.idofs)
     xo, it = _oracle_pcg_relres(A, h, b, 1e-6, 1000)
     assert niters == it
+    assert niters < 120            # gamma-robust with the averaged coupling too
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
 
 

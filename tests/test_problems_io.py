@@ -111,7 +111,10 @@ def test_dat_reader_and_mapping():
     P = M.parameters
     assert prm['AMG_type'] == P.SA_AMG and prm['cycle_type'] == P.V_CYCLE
     assert prm['smoother'] == P.SMOOTHER_JACOBI_RHO and prm['aggregation_type'] == P.MIS
-    assert prm['Schwarz_type'] == P.SCHWARZ_BLOCK_JACOBI and prm['Schwarz_mmsize'] == 200
+    # HAZmath's multiplicative Schwarz on the 1-D seeds' 2-rings -> the
+    # additive overlapping Schwarz on the same blocks
+    assert prm['Schwarz_type'] == P.SCHWARZ_ADDITIVE and prm['Schwarz_mmsize'] == 200
+    assert prm['Schwarz_maxlvl'] == 2 and any('SCHWARZ_ADDITIVE' in n for n in notes)
     assert prm['coarse_dof'] == 300 and prm['max_levels'] == 30
     assert solver == dict(type=1, maxit=1000, tol=1e-6, stop_type=1, precond_type=16)
     assert len(notes) >= 3
