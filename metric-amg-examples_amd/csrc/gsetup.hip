@@ -321,6 +321,160 @@ __global__ __launch_bounds__(256) void agg_phase3_kernel(int64_t n, const int64_
 }
 
 // ---------------------------------------------------------------------------
+// parallel heavy-edge matching (setup.cpp aggregate_hem / hem_match)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dedge_hash(int64_t i, int64_t j, int lvl) {
+  const int64_t a = i < j ? i : j, b = i < j ? j : i;
+  return dhash32((uint64_t)a, 0x5000 + lvl) ^ dhash32((uint64_t)b, 0x6000 + lvl);
+}
+
+// compacted copy of a CSR: entries with flag (if given), off the diagonal
+// (if nodiag), weight |v| * 1.0 (if absval) that is not 0.0; count / fill
+template <bool FILL>
+__global__ __launch_bounds__(256) void wgraph_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                     const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                     const uint8_t* __restrict__ flag, int absval,
+                                                     int64_t* __restrict__ optr, int32_t* __restrict__ ocol,
+                                                     double* __restrict__ oval) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t o = FILL ? optr[i] : 0;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+    if (flag && !flag[k]) continue;
+    if (col[k] == i) continue;
+    const double w = absval ? fabs(val[k]) * 1.0 : val[k];
+    if (w == 0.0) continue;
+    if (FILL) { ocol[o] = col[k]; oval[o] = w; }
+    ++o;
+  }
+  if (!FILL) optr[i + 1] = o;
+}
+
+__global__ __launch_bounds__(256) void hem_pick_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const uint8_t* __restrict__ act,
+                                                       const int64_t* __restrict__ mate, int lvl,
+                                                       int64_t* __restrict__ choice) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t best = -1;
+  double bw = 0.0;
+  uint32_t bh = 0;
+  if (act[i] && mate[i] < 0)
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+      const int64_t j = col[k];
+      if (j == i || !act[j] || mate[j] >= 0) continue;
+      const double w = val[k];
+      const uint32_t h = dedge_hash(i, j, lvl);
+      if (best < 0 || w > bw || (w == bw && (h > bh || (h == bh && j < best)))) {
+        best = j; bw = w; bh = h;
+      }
+    }
+  choice[i] = best;
+}
+
+__global__ __launch_bounds__(256) void hem_mutual_kernel(int64_t n, const int64_t* __restrict__ choice,
+                                                         int64_t* __restrict__ mate, unsigned long long* got) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool m = false;
+  if (i < n) {
+    const int64_t c = choice[i];
+    if (c >= 0 && choice[c] == i) { mate[i] = c; m = true; }
+  }
+  const unsigned long long b = __ballot(m);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(got, (unsigned long long)__popcll(b));
+}
+
+// root = smallest member of a pair (or the unmatched node itself)
+__global__ __launch_bounds__(256) void hem_root_kernel(int64_t n, const uint8_t* __restrict__ act,
+                                                       const int64_t* __restrict__ mate, int64_t* __restrict__ f) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) f[i] = act[i] && (mate[i] < 0 || i < mate[i]);
+}
+
+__global__ __launch_bounds__(256) void hem_number_kernel(int64_t n, const uint8_t* __restrict__ act,
+                                                         const int64_t* __restrict__ mate,
+                                                         const int64_t* __restrict__ scan, int64_t* __restrict__ a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (!act[i]) { a[i] = -1; return; }
+  const int64_t r = (mate[i] >= 0 && mate[i] < i) ? mate[i] : i;
+  a[i] = scan[r] - 1;
+}
+
+__global__ __launch_bounds__(256) void hem_compose_kernel(int64_t n, const int64_t* __restrict__ a,
+                                                          int64_t* __restrict__ agg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && agg[i] >= 0) agg[i] = a[agg[i]];
+}
+
+// T of one pass: row i -> a[i] (value 1) where act[i]; ptr = inclusive scan of act
+__global__ __launch_bounds__(256) void hem_t_kernel(int64_t n, const uint8_t* __restrict__ act,
+                                                    const int64_t* __restrict__ a, int64_t* __restrict__ tptr,
+                                                    int32_t* __restrict__ tcol, double* __restrict__ tval, int fill) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (!fill) { tptr[i + 1] = act[i] ? 1 : 0; return; }
+  if (act[i]) { tcol[tptr[i]] = (int32_t)a[i]; tval[tptr[i]] = 1.0; }
+}
+
+__global__ __launch_bounds__(256) void agg_size_kernel(int64_t n, const int64_t* __restrict__ agg,
+                                                       unsigned long long* __restrict__ size) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n && agg[i] >= 0) atomicAdd(size + agg[i], 1ull);
+}
+
+// a node alone in its aggregate joins the heaviest strong neighbour's
+// aggregate of >= 2 members (ties: smallest id; setup.cpp aggregate_hem)
+__global__ __launch_bounds__(256) void hem_absorb_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val,
+                                                         const int64_t* __restrict__ agg,
+                                                         const unsigned long long* __restrict__ size,
+                                                         int64_t* __restrict__ agg2, int64_t* __restrict__ used) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t a0 = agg[i];
+  if (a0 >= 0 && size[a0] == 1) {
+    double bw = 0.0;
+    int64_t ba = -1;
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+      const int64_t a = agg[col[k]];
+      if (a < 0 || size[a] < 2) continue;
+      const double w = val[k];
+      if (ba < 0 || w > bw || (w == bw && a < ba)) { bw = w; ba = a; }
+    }
+    if (ba >= 0) a0 = ba;
+  }
+  agg2[i] = a0;
+  if (a0 >= 0) used[a0] = 1;   // benign race: every writer stores 1
+}
+
+__global__ __launch_bounds__(256) void agg_remap_kernel(int64_t n, const int64_t* __restrict__ agg2,
+                                                        const int64_t* __restrict__ scan, int64_t* __restrict__ agg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) agg[i] = agg2[i] >= 0 ? scan[agg2[i]] - 1 : -1;
+}
+
+__global__ __launch_bounds__(256) void nonzero_flag_kernel(int64_t n, const int64_t* __restrict__ cnt,
+                                                           uint8_t* __restrict__ act) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) act[i] = cnt[i + 1] > 0;
+}
+
+__global__ __launch_bounds__(256) void u8_fill_kernel(int64_t n, uint8_t v, uint8_t* __restrict__ p) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ __launch_bounds__(256) void iota_nonisol_kernel(int64_t n, const uint8_t* __restrict__ act,
+                                                           int64_t* __restrict__ agg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) agg[i] = act[i] ? i : -1;
+}
+
+// ---------------------------------------------------------------------------
 // smoother / SA node blocks
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void seed_mark_kernel(int64_t m, const int32_t* __restrict__ idofs, int64_t n,
@@ -917,6 +1071,121 @@ int node_inverse(const DevMat& A, int64_t nv, const uint8_t* joined, dv4_t* D, c
   return MAMG_OK;
 }
 
+// compacted weighted graph of M (flagged, off-diagonal, non-zero entries)
+int wgraph(const DevMat& M, const uint8_t* flag, int absval, Scratch* S, DevMat* W, std::string* err) {
+  const int64_t n = M.n;
+  W->n = W->m = n;
+  RCHK(S->alloc(&W->ptr, n + 1, err));
+  HIPCHK(hipMemset(W->ptr, 0, sizeof(int64_t)));
+  wgraph_kernel<false><<<nblk(n), 256>>>(n, M.ptr, M.col, M.val, flag, absval, W->ptr, nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(W->ptr, W->ptr, n + 1, nullptr, err));
+  RCHK(to_host(&W->nnz, W->ptr + n, 1, err));
+  RCHK(S->alloc(&W->col, W->nnz, err));
+  RCHK(S->alloc(&W->val, W->nnz, err));
+  wgraph_kernel<true><<<nblk(n), 256>>>(n, M.ptr, M.col, M.val, flag, absval, W->ptr, W->col, W->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+// parallel heavy-edge matching on the strong node graph (setup.cpp
+// aggregate_hem): HEM passes of handshake rounds; pass k + 1 on T^T W T
+int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level, int64_t** agg_out,
+                      int64_t* nagg_out, std::string* err) {
+  constexpr int PASSES = 2, MAX_ROUNDS = 64;
+  Scratch S;
+  const int64_t n = Gr.n;
+  DevMat W;
+  RCHK(wgraph(Gr, flag, 1, &S, &W, err));
+  const DevMat W1 = W;   // pass-1 graph (Scratch-owned until return)
+  uint8_t* act = nullptr;
+  RCHK(S.alloc(&act, n, err));
+  {   // active = any strong neighbour
+    int64_t* cnt = nullptr;
+    RCHK(S.alloc(&cnt, n + 1, err));
+    HIPCHK(hipMemset(cnt, 0, sizeof(int64_t)));
+    wgraph_kernel<false><<<nblk(n), 256>>>(n, Gr.ptr, Gr.col, Gr.val, flag, 2, cnt, nullptr, nullptr);
+    nonzero_flag_kernel<<<nblk(n), 256>>>(n, cnt, act);
+    HIPCHK(hipGetLastError());
+  }
+  int64_t* agg = nullptr;
+  RCHK(galloc(G, &agg, n, err));
+  iota_nonisol_kernel<<<nblk(n), 256>>>(n, act, agg);
+  int64_t nagg = n;
+  unsigned long long* got = nullptr;
+  RCHK(S.alloc(&got, 1, err));
+  for (int ps = 0; ps < PASSES; ++ps) {
+    const int64_t m = W.n;
+    int64_t *mate = nullptr, *choice = nullptr, *f = nullptr, *a = nullptr;
+    RCHK(S.alloc(&mate, m, err));
+    RCHK(S.alloc(&choice, m, err));
+    RCHK(S.alloc(&f, m, err));
+    RCHK(S.alloc(&a, m, err));
+    HIPCHK(hipMemset(mate, 0xff, m * sizeof(int64_t)));
+    for (int round = 0; round < MAX_ROUNDS; ++round) {
+      HIPCHK(hipMemset(got, 0, sizeof(unsigned long long)));
+      hem_pick_kernel<<<nblk(m), 256>>>(m, W.ptr, W.col, W.val, act, mate, 16 * level + ps, choice);
+      hem_mutual_kernel<<<nblk(m), 256>>>(m, choice, mate, got);
+      HIPCHK(hipGetLastError());
+      unsigned long long hg = 0;
+      RCHK(to_host(&hg, got, 1, err));
+      if (!hg) break;
+    }
+    hem_root_kernel<<<nblk(m), 256>>>(m, act, mate, f);
+    RCHK(dscan_incl_i64(f, f, m, nullptr, err));
+    RCHK(to_host(&nagg, f + m - 1, 1, err));
+    hem_number_kernel<<<nblk(m), 256>>>(m, act, mate, f, a);
+    hem_compose_kernel<<<nblk(n), 256>>>(n, a, agg);
+    HIPCHK(hipGetLastError());
+    if (ps + 1 == PASSES) break;
+    DevMat T, Tt, WT, C;   // W_next = T^T W T without its diagonal
+    T.n = m; T.m = nagg;
+    RCHK(S.alloc(&T.ptr, m + 1, err));
+    HIPCHK(hipMemset(T.ptr, 0, sizeof(int64_t)));
+    hem_t_kernel<<<nblk(m), 256>>>(m, act, a, T.ptr, nullptr, nullptr, 0);
+    RCHK(dscan_incl_i64(T.ptr, T.ptr, m + 1, nullptr, err));
+    RCHK(to_host(&T.nnz, T.ptr + m, 1, err));
+    RCHK(S.alloc(&T.col, T.nnz, err));
+    RCHK(S.alloc(&T.val, T.nnz, err));
+    hem_t_kernel<<<nblk(m), 256>>>(m, act, a, T.ptr, T.col, T.val, 1);
+    HIPCHK(hipGetLastError());
+    RCHK(spgemm(G, W, BTent{a, m, nagg}, nagg, &WT, err, 1.0));
+    RCHK(transpose(G, T, &Tt, err));
+    RCHK(spgemm(G, Tt, BCsr{WT.ptr, WT.col, WT.val}, nagg, &C, err,
+                WT.n ? (double)WT.nnz / (double)WT.n : 1.0));
+    for (void* q : {(void*)WT.ptr, (void*)WT.col, (void*)WT.val, (void*)Tt.ptr, (void*)Tt.col, (void*)Tt.val})
+      G->release(q);
+    DevMat W2;
+    RCHK(wgraph(C, nullptr, 0, &S, &W2, err));
+    for (void* q : {(void*)C.ptr, (void*)C.col, (void*)C.val}) G->release(q);
+    W = W2;
+    RCHK(S.alloc(&act, nagg, err));
+    u8_fill_kernel<<<nblk(nagg), 256>>>(nagg, 1, act);
+    HIPCHK(hipGetLastError());
+  }
+  {   // absorption of the nodes left alone, then compact ids
+    unsigned long long* size = nullptr;
+    int64_t *agg2 = nullptr, *used = nullptr;
+    RCHK(S.alloc(&size, nagg, err));
+    RCHK(S.alloc(&agg2, n, err));
+    RCHK(S.alloc(&used, nagg, err));
+    HIPCHK(hipMemset(size, 0, std::max<int64_t>(nagg, 1) * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(used, 0, std::max<int64_t>(nagg, 1) * sizeof(int64_t)));
+    agg_size_kernel<<<nblk(n), 256>>>(n, agg, size);
+    hem_absorb_kernel<<<nblk(n), 256>>>(n, W1.ptr, W1.col, W1.val, agg, size, agg2, used);
+    HIPCHK(hipGetLastError());
+    RCHK(dscan_incl_i64(used, used, nagg, nullptr, err));
+    int64_t nused = 0;
+    if (nagg) RCHK(to_host(&nused, used + nagg - 1, 1, err));
+    agg_remap_kernel<<<nblk(n), 256>>>(n, agg2, used, agg);
+    HIPCHK(hipGetLastError());
+    nagg = nused;
+  }
+  *agg_out = agg;
+  *nagg_out = nagg;
+  return MAMG_OK;
+}
+
 // aggregation of the node graph of A (setup.cpp node_graph + strength + aggregate_mis2)
 int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, int64_t** agg_out,
               int64_t* nagg_out, std::string* err) {
@@ -951,6 +1220,7 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, in
            "pattern); use the host setup (mamg_setup)";
     return MAMG_ERR_UNSUPPORTED;
   }
+  if (G->params.aggregation_type == MAMG_HEM) return aggregate_hem_dev(G, Gr, flag, level, agg_out, nagg_out, err);
   uint64_t *state = nullptr, *low = nullptr, *key = nullptr, *m1 = nullptr;
   unsigned long long* und = nullptr;
   RCHK(S.alloc(&state, nv, err));

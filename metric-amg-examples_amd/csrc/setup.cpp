@@ -288,6 +288,144 @@ int aggregate_mis2(const CsrView& A, const Strength& S, int level,
   return MAMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// parallel heavy-edge matching aggregation (oracle aggregate_hem / hem_match)
+// ---------------------------------------------------------------------------
+constexpr int HEM_PASSES = 2, HEM_MAX_ROUNDS = 64;
+
+inline uint32_t edge_hash(int64_t i, int64_t j, int lvl) {
+  const int64_t a = std::min(i, j), b = std::max(i, j);
+  return hash32((uint64_t)a, 0x5000 + lvl) ^ hash32((uint64_t)b, 0x6000 + lvl);
+}
+
+// handshake rounds: a free active node picks the free neighbour with the
+// largest (weight, edge hash), smallest index on ties; mutual picks match
+void hem_match(const CsrView& W, const std::vector<uint8_t>& act, int lvl, std::vector<int64_t>* mate_out) {
+  const int64_t n = W.n;
+  std::vector<int64_t>& mate = *mate_out;
+  mate.assign(n, -1);
+  std::vector<int64_t> choice(n);
+  for (int round = 0; round < HEM_MAX_ROUNDS; ++round) {
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t best = -1;
+      double bw = 0.0;
+      uint32_t bh = 0;
+      if (act[i] && mate[i] < 0)
+        for (int64_t k = W.ptr[i]; k < W.ptr[i + 1]; ++k) {
+          const int64_t j = W.col[k];
+          if (j == i || !act[j] || mate[j] >= 0) continue;
+          const double w = W.val[k];
+          const uint32_t h = edge_hash(i, j, lvl);
+          if (best < 0 || w > bw || (w == bw && (h > bh || (h == bh && j < best)))) {
+            best = j; bw = w; bh = h;
+          }
+        }
+      choice[i] = best;
+    }
+    int64_t got = 0;
+#pragma omp parallel for schedule(static) reduction(+ : got)
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t c = choice[i];
+      if (c >= 0 && choice[c] == i) { mate[i] = c; ++got; }
+    }
+    if (!got) break;
+  }
+}
+
+int aggregate_hem(const CsrView& A, const Strength& S, int level, std::vector<int64_t>* agg_out,
+                  int64_t* nagg_out, std::string* err) {
+  const int64_t n = A.n;
+  Csr W;   // strong graph weighted by |a_ij| (zeros dropped)
+  W.n = W.m = n;
+  W.ptr.assign(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+      if (S.flag[k] && A.col[k] != i && std::fabs(A.val[k]) * 1.0 != 0.0) {
+        W.col.push_back(A.col[k]);
+        W.val.push_back(std::fabs(A.val[k]) * 1.0);
+      }
+    W.ptr[i + 1] = (int64_t)W.col.size();
+  }
+  const Csr W1 = W;   // the pass-1 graph (absorption of the nodes left alone)
+  std::vector<uint8_t> act(n);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int64_t i = 0; i < n; ++i) {
+    bool any = false;
+    for_strong(A, S, i, [&](int64_t) { any = true; });
+    act[i] = any;
+  }
+  std::vector<int64_t>& agg = *agg_out;
+  agg.assign(n, -1);
+  for (int64_t i = 0; i < n; ++i)
+    if (act[i]) agg[i] = i;
+  int64_t nagg = n;
+  for (int ps = 0; ps < HEM_PASSES; ++ps) {
+    const int64_t m = W.n;
+    std::vector<int64_t> mate;
+    hem_match(W.view(), act, 16 * level + ps, &mate);
+    std::vector<int64_t> a(m, -1);
+    nagg = 0;
+    for (int64_t i = 0; i < m; ++i) {   // roots (smallest member) numbered in index order
+      if (!act[i]) continue;
+      const int64_t r = mate[i] >= 0 ? std::min(i, mate[i]) : i;
+      if (r == i) a[i] = nagg++;
+    }
+    for (int64_t i = 0; i < m; ++i)
+      if (act[i] && mate[i] >= 0 && mate[i] < i) a[i] = a[mate[i]];
+    for (int64_t i = 0; i < n; ++i)
+      if (agg[i] >= 0) agg[i] = a[agg[i]];
+    if (ps + 1 == HEM_PASSES) break;
+    Csr T, Tt, WT, C;   // W_next = T^T W T, diagonal dropped
+    T.n = m; T.m = nagg;
+    T.ptr.assign(m + 1, 0);
+    for (int64_t i = 0; i < m; ++i) {
+      if (act[i]) { T.col.push_back((int32_t)a[i]); T.val.push_back(1.0); }
+      T.ptr[i + 1] = (int64_t)T.col.size();
+    }
+    spgemm(W.view(), T.view(), &WT);
+    transpose(T.view(), &Tt);
+    spgemm(Tt.view(), WT.view(), &C);
+    W = Csr();
+    W.n = W.m = nagg;
+    W.ptr.assign(nagg + 1, 0);
+    for (int64_t i = 0; i < nagg; ++i) {
+      for (int64_t k = C.ptr[i]; k < C.ptr[i + 1]; ++k)
+        if (C.col[k] != i && C.val[k] != 0.0) { W.col.push_back(C.col[k]); W.val.push_back(C.val[k]); }
+      W.ptr[i + 1] = (int64_t)W.col.size();
+    }
+    act.assign(nagg, 1);
+  }
+  // nodes left alone by every pass join the heaviest strong neighbour's
+  // aggregate of >= 2 members (ties: smallest id); ids then compacted
+  std::vector<int64_t> size(nagg, 0);
+  for (int64_t i = 0; i < n; ++i)
+    if (agg[i] >= 0) size[agg[i]]++;
+  std::vector<int64_t> agg2(agg);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int64_t i = 0; i < n; ++i) {
+    if (agg[i] < 0 || size[agg[i]] != 1) continue;
+    double bw = 0.0;
+    int64_t ba = -1;
+    for (int64_t k = W1.ptr[i]; k < W1.ptr[i + 1]; ++k) {
+      const int64_t a = agg[W1.col[k]];
+      if (a < 0 || size[a] < 2) continue;
+      const double w = W1.val[k];
+      if (ba < 0 || w > bw || (w == bw && a < ba)) { bw = w; ba = a; }
+    }
+    if (ba >= 0) agg2[i] = ba;
+  }
+  std::vector<int64_t> newid(nagg, 0);
+  for (int64_t i = 0; i < n; ++i)
+    if (agg2[i] >= 0) newid[agg2[i]] = 1;
+  int64_t used = 0;
+  for (int64_t a = 0; a < nagg; ++a) newid[a] = newid[a] ? used++ : -1;
+  for (int64_t i = 0; i < n; ++i) agg[i] = agg2[i] >= 0 ? newid[agg2[i]] : -1;
+  *nagg_out = used;
+  (void)err;
+  return MAMG_OK;
+}
+
 void tentative(const std::vector<int64_t>& agg, int64_t nagg, Csr* T) {
   const int64_t n = (int64_t)agg.size();
   T->n = n;
@@ -794,9 +932,9 @@ int check_params(const mamg_params& p, std::string* err) {
     *err = "multicolour GS/SGS smoothers are node-block smoothers: num_functions 2 and node_block_smoother 1";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (p.aggregation_type != MAMG_MIS) {
-    *err = "aggregation_type must be MIS (deterministic parallel MIS-2): VMB/HEM/HEC/MWM are not implemented "
-           "(parameters.to_gpu_profile maps a HAZmath dict explicitly)";
+  if (p.aggregation_type != MAMG_MIS && p.aggregation_type != MAMG_HEM) {
+    *err = "aggregation_type must be MIS (deterministic parallel MIS-2) or HEM (parallel heavy-edge matching): "
+           "VMB/HEC/MWM are not implemented (parameters.to_gpu_profile maps a HAZmath dict explicitly)";
     return MAMG_ERR_UNSUPPORTED;
   }
   if (p.coarse_scaling != MAMG_OFF && p.coarse_scaling != MAMG_ON) { *err = "coarse_scaling must be OFF or ON"; return MAMG_ERR_ARG; }
@@ -878,13 +1016,15 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
         node_graph(cur, nf, &G);
         Strength S;
         strength(G.view(), p.strong_coupled, &S);
-        rc = aggregate_mis2(G.view(), S, l, &agg, &nagg, err);
+        rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(G.view(), S, l, &agg, &nagg, err)
+                                            : aggregate_mis2(G.view(), S, l, &agg, &nagg, err);
         if (rc) return rc;
         if (nagg == 0 || nf * nagg >= n) last = true;
       } else {
         Strength S;
         strength(cur, p.strong_coupled, &S);
-        rc = aggregate_mis2(cur, S, l, &agg, &nagg, err);
+        rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(cur, S, l, &agg, &nagg, err)
+                                            : aggregate_mis2(cur, S, l, &agg, &nagg, err);
         if (rc) return rc;
         if (nagg == 0 || nagg >= n) last = true;
       }

@@ -6,15 +6,21 @@ values are build-defined (HAZmath's are not available here).
 
 * ``parameters_standard``, ``parameters_standard_schwarz``,
   ``parameters_metric``, ``parameters_metric_schwarz``: the reference's
-  presets with their values verbatim.  ``MetricAMG`` runs what they select or
-  raises MAMG_ERR_UNSUPPORTED naming the component it lacks (VMB / HEM
-  aggregation); there is no silent substitution under these names.
+  presets with their values verbatim.  ``MetricAMG`` runs what they select
+  (parameters_metric(_schwarz): UA + parallel HEM + W-cycle + multicolour SGS
+  + coarse scaling, on nodal systems) or raises MAMG_ERR_UNSUPPORTED naming
+  the component it lacks (VMB aggregation; SGS on scalar systems); there is
+  no silent substitution under these names.
 * ``parameters_metric_mi355x``: the GPU profile "mi355x_sa_v" (nodal SA,
-  V-cycle, node-block Jacobi) -- the fastest time to solution measured
-  (DESIGN.md section 2.8), the drivers' and the bench's default.
+  V-cycle, node-block Jacobi): the north star's profile, the drivers' and
+  the bench's default.
+* ``parameters_metric_mi355x_poly``: the same with the Chebyshev smoother --
+  the shortest time to solution measured.
 * ``parameters_metric_mi355x_sgs``: the reference's smoother family on the
   GPU: multicolour node-block SGS on every level (level 0: multiplicative
   Schwarz on the seed blocks), coarse-grid correction scaling ON.
+* ``parameters_metric_3d1d``: additive overlapping Schwarz on the 1-D seeds'
+  rings.
 * ``to_gpu_profile(d)``: explicit opt-in mapping of a HAZmath dict onto
   implemented components; returns the mapped dict and every substitution.
   ``*_gpu_mapped`` are the reference presets passed through it.
@@ -126,7 +132,7 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
     opt-in).  Returns (mapped dict, list of human-readable substitutions)."""
     out = dict(params)
     notes = []
-    if out.get('aggregation_type', MIS) != MIS:
+    if out.get('aggregation_type', MIS) not in (MIS, HEM):
         notes.append('aggregation_type %r -> MIS (deterministic parallel MIS-2)'
                      % out.get('aggregation_type'))
         out['aggregation_type'] = MIS

@@ -209,6 +209,7 @@ class Params:
     """Algorithm profile; keys mirror src/amg_parameters.py:67-89 names."""
     AMG_type: str = 'SA'          # 'SA' | 'UA'
     cycle_type: str = 'V'         # 'V' | 'W'
+    aggregation_type: str = 'MIS'  # 'MIS' (MIS-2) | 'HEM' (parallel heavy-edge matching, 2 passes)
     max_levels: int = 20
     maxit: int = 1
     smoother: str = 'JACOBI_RHO'  # 'L1DIAG' | 'JACOBI' | 'JACOBI_RHO' | 'POLY' | 'GS' | 'SGS'
@@ -393,6 +394,111 @@ def aggregate_mis2(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
             raise RuntimeError('aggregation left a non-isolated node unassigned')
         agg2 = agg3
     return agg2, len(roots)
+
+
+# --------------------------------------------------------------------------
+# parallel heavy-edge matching aggregation (aggregation_type HEM,
+# src/amg_parameters.py:79): HAZmath matches greedily in index order; here
+# every pass is a round-synchronous handshake (locally dominant edges), so
+# the GPU reproduces it exactly.  Two passes -> aggregates of <= 4 nodes.
+# --------------------------------------------------------------------------
+HEM_PASSES = 2
+HEM_MAX_ROUNDS = 64
+
+
+def edge_hash(i: np.ndarray, j: np.ndarray, level: int) -> np.ndarray:
+    """symmetric 32-bit edge priority: hash32(min) ^ hash32(max) (host.h hash32)"""
+    a, b = np.minimum(i, j), np.maximum(i, j)
+    return hash32(a, 0x5000 + level) ^ hash32(b, 0x6000 + level)
+
+
+def hem_match(W: sp.csr_matrix, active: np.ndarray, level: int):
+    """Handshake matching on the weighted graph W (symmetric, no diagonal):
+    per round every free active node picks the free neighbour with the
+    largest (weight, edge hash, -index); mutual picks are matched.  Rounds
+    until none is matched (at most HEM_MAX_ROUNDS).  Returns mate (-1 free)."""
+    n = W.shape[0]
+    r = np.repeat(np.arange(n), np.diff(W.indptr))
+    c = W.indices.astype(np.int64)
+    w = W.data
+    h = edge_hash(r, c, level).astype(np.int64)
+    mate = np.full(n, -1, dtype=np.int64)
+    for _ in range(HEM_MAX_ROUNDS):
+        free = active & (mate < 0)
+        m = free[r] & free[c] & (r != c)
+        rr, cc, ww, hh = r[m], c[m], w[m], h[m]
+        order = np.lexsort((cc, -hh, -ww, rr))          # row asc; weight, hash desc; col asc
+        rr, cc = rr[order], cc[order]
+        first = np.ones(len(rr), dtype=bool)
+        first[1:] = rr[1:] != rr[:-1]
+        choice = np.full(n, -1, dtype=np.int64)
+        choice[rr[first]] = cc[first]
+        i = np.flatnonzero(choice >= 0)
+        mutual = i[choice[choice[i]] == i]
+        if len(mutual) == 0:
+            break
+        mate[mutual] = choice[mutual]
+    return mate
+
+
+def aggregate_hem(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
+    """HEM_PASSES handshake passes on the strong graph weighted by |a_ij| /
+    s_IJ; pass k+1 matches the aggregates of pass k on W_k+1 = T_k^T W_k T_k
+    (SMMP products, diagonal and zeros dropped).  Aggregates are numbered by
+    their smallest member in index order; isolated nodes: -1."""
+    n = Wabs.shape[0]
+    W = Wabs.multiply(S).tocsr()
+    W.eliminate_zeros()
+    W.sort_indices()
+    active = np.diff(S.indptr) > 0
+    agg = np.where(active, np.arange(n), -1)
+    cur, act = W, active
+    nagg = n
+    for ps in range(HEM_PASSES):
+        m = cur.shape[0]
+        mate = hem_match(cur, act, 16 * level + ps)
+        idx = np.arange(m)
+        root = np.where(mate >= 0, np.minimum(idx, mate), idx)
+        isroot = act & (root == idx)
+        num = np.cumsum(isroot) - 1
+        a = np.where(act, num[root], -1)
+        nagg = int(isroot.sum())
+        agg = np.where(agg >= 0, a[np.maximum(agg, 0)], -1)
+        if ps + 1 == HEM_PASSES:
+            break
+        rows = np.flatnonzero(act)
+        T = sp.csr_matrix((np.ones(len(rows)), (rows, a[rows])), shape=(m, nagg))
+        T.sort_indices()
+        WT = (cur @ T).tocsr()
+        WT.sort_indices()
+        C = (T.T.tocsr() @ WT).tocsr()
+        C.sort_indices()
+        C.setdiag(0.0)
+        C.eliminate_zeros()
+        C.sort_indices()
+        cur = C
+        act = np.ones(nagg, dtype=bool)   # every aggregate may match (no external edge: stays alone)
+    # a node left alone by every pass joins the aggregate of its heaviest
+    # strong neighbour that has >= 2 members (ties: smallest aggregate id);
+    # the aggregates are then renumbered in order (matching alone leaves the
+    # leaves of star-like coarse graphs unmatched and coarsening stalls)
+    size = np.bincount(agg[agg >= 0], minlength=nagg)
+    r = np.repeat(np.arange(n), np.diff(W.indptr))
+    c = W.indices
+    single = (agg >= 0) & (size[np.maximum(agg, 0)] == 1)
+    m = single[r] & (agg[c] >= 0) & (size[np.maximum(agg[c], 0)] >= 2)
+    rr, ww, aa = r[m], W.data[m], agg[c[m]]
+    order = np.lexsort((aa, -ww, rr))
+    rr, aa = rr[order], aa[order]
+    first = np.ones(len(rr), dtype=bool)
+    first[1:] = rr[1:] != rr[:-1]
+    agg2 = agg.copy()
+    agg2[rr[first]] = aa[first]
+    used = np.zeros(nagg, dtype=bool)
+    used[agg2[agg2 >= 0]] = True
+    newid = np.cumsum(used) - 1
+    agg2 = np.where(agg2 >= 0, newid[np.maximum(agg2, 0)], -1)
+    return agg2, int(used.sum())
 
 
 def tentative(agg: np.ndarray, nagg: int) -> sp.csr_matrix:
@@ -937,11 +1043,11 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         if not last:
             if nf > 1:
                 S, Wn = node_strength(cur, nf, p.strong_coupled)
-                agg, nagg = aggregate_mis2(Wn, S, l)
+                agg, nagg = (aggregate_hem if p.aggregation_type == 'HEM' else aggregate_mis2)(Wn, S, l)
                 last = nagg == 0 or nf * nagg >= n
             else:
                 S = strength(cur, p.strong_coupled)
-                agg, nagg = aggregate_mis2(abs(cur), S, l)
+                agg, nagg = (aggregate_hem if p.aggregation_type == 'HEM' else aggregate_mis2)(abs(cur), S, l)
                 last = nagg == 0 or nagg >= n
         if last:
             if n > p.max_coarse_dense:

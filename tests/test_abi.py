@@ -41,7 +41,7 @@ def test_params_struct_layout(lib_built):
 
 @pytest.mark.parametrize('bad,code', [
     (dict(smoother=11), -4),                 # SGS is a node-block smoother: num_functions 2
-    (dict(aggregation_type=5), -4),          # HEM rejected
+    (dict(aggregation_type=1), -4),          # VMB rejected (HEM runs: parallel matching)
     (dict(coarse_scaling=2), -1),
     (dict(Schwarz_type=3), -4),              # multiplicative seed blocks need the SGS smoother
     (dict(num_functions=2, smoother=11, Schwarz_type=4), -4),
@@ -65,20 +65,28 @@ def test_rejects_unsupported(lib_built, bad, code):
 def test_reference_presets_map_and_report(lib_built):
     import metric_amg_examples_amd as M
     P = M.parameters
-    # the reference's names carry the reference's values and are rejected
-    # loudly where a component is missing (HEM aggregation), never remapped
+    # the reference's names carry the reference's values; every component of
+    # parameters_metric_schwarz now exists (UA, parallel HEM, W, SGS as
+    # multicolour node-block SGS, coarse scaling, symmetric seed blocks), so it
+    # runs as given on a nodal system, and is rejected loudly where a
+    # component is missing (SGS on a scalar system)
     assert P.parameters_metric_schwarz['aggregation_type'] == P.HEM
     assert P.parameters_metric_schwarz['smoother'] == P.SMOOTHER_SGS
     from mamg_oracle import laplace1d
     with pytest.raises(M._lib.MamgError) as ei:
         M.HostHierarchy(laplace1d(30), parameters=P.parameters_metric_schwarz)
     assert ei.value.code == -4 and len(str(ei.value)) > 20
-    # explicit mapping keeps what is implemented (UA, W, SGS, coarse scaling,
-    # symmetric multiplicative seed blocks) and reports what it changes
+    s = M.problems.bidomain(2, 16, 1e4)
+    H = M.HostHierarchy(s, idofs=s.idofs, parameters=P.parameters_metric_schwarz, num_functions=2)
+    assert H.num_levels >= 2
+    H.close()
+    # explicit mapping keeps what is implemented and reports what it changes
+    mapped, notes = P.to_gpu_profile(P.parameters_standard)
+    assert mapped['aggregation_type'] == P.MIS and any('VMB' in n or '1' in n for n in notes)
     mapped, notes = P.to_gpu_profile(P.parameters_metric_schwarz)
-    assert mapped['smoother'] == P.SMOOTHER_SGS and mapped['aggregation_type'] == P.MIS
+    assert mapped['smoother'] == P.SMOOTHER_SGS and mapped['aggregation_type'] == P.HEM
     assert mapped['Schwarz_type'] == P.SCHWARZ_SYMMETRIC and mapped['coarse_scaling'] == P.ON
-    assert mapped['num_functions'] == 2 and any('HEM' in n or '5' in n for n in notes)
+    assert mapped['num_functions'] == 2
     assert P.parameters_metric_schwarz_gpu_mapped == mapped
     H = M.HostHierarchy(laplace1d(300), parameters=P.parameters_standard_gpu_mapped,
                         num_functions=1, smoother=P.SMOOTHER_JACOBI_RHO)

@@ -30,6 +30,10 @@ def to_c(kw):
         c['smoother'] = SMO[c['smoother']]
     if 'cycle_type' in c:
         c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    if 'AMG_type' in c:
+        c['AMG_type'] = {'SA': 2, 'UA': 1}[c['AMG_type']]
+    if 'aggregation_type' in c:
+        c['aggregation_type'] = {'MIS': 2, 'HEM': 5}[c['aggregation_type']]
     return c
 
 
@@ -47,6 +51,10 @@ CASES = [
     (3, 16, 1e2, dict(smoother='GS', presmooth_iter=2, postsmooth_iter=2)),
     (3, 16, 1e4, dict(coarse_scaling=1)),                      # Jacobi + scaling (K post)
     (2, 32, 1e3, dict(coarse_scaling=1, cycle_type='W')),
+    # the reference's metric_mono family (src/amg_parameters.py:67-89) on the GPU:
+    # UA + parallel HEM + W-cycle + SGS + coarse scaling
+    (3, 16, 1e6, dict(smoother='SGS', coarse_scaling=1, cycle_type='W', AMG_type='UA', aggregation_type='HEM')),
+    (2, 64, 1e4, dict(smoother='SGS', coarse_scaling=1, cycle_type='W', AMG_type='UA', aggregation_type='HEM')),
 ]
 
 

@@ -33,6 +33,10 @@ CASES = [
     (3, 16, 1e6, dict(post_fusion=0)),
     (2, 32, 1e3, dict(Schwarz_mmsize=1)),           # level-0 seed blocks split into singletons
     (2, 64, 1e4, dict(coarse_dof=400, max_levels=3)),
+    # parallel heavy-edge matching (aggregation_type HEM), UA and SA
+    (3, 16, 1e6, dict(aggregation_type=5, AMG_type=1)),
+    (2, 64, 1e2, dict(aggregation_type=5)),
+    (3, 16, 1e10, dict(aggregation_type=5, AMG_type=1)),
 ]
 
 
@@ -82,6 +86,8 @@ def test_gpu_setup_apply_bitwise_equals_host_setup(lib_built, dim, n, g, kw):
     oracle_kw = {k: v for k, v in kw.items() if k != 'post_fusion'}
     if 'AMG_type' in oracle_kw:
         oracle_kw['AMG_type'] = {1: 'UA', 2: 'SA'}[oracle_kw['AMG_type']]
+    if 'aggregation_type' in oracle_kw:
+        oracle_kw['aggregation_type'] = {2: 'MIS', 5: 'HEM'}[oracle_kw['aggregation_type']]
     h = mo.setup(A, mo.Params(num_functions=2, **oracle_kw), idofs=s.idofs)
     r = mo.seeded_rhs(s.N)
     zo = h.apply(r)

@@ -19,6 +19,10 @@ CASES = [
     (3, 8, 1e2, dict(num_functions=2, smoother='L1DIAG', node_block_smoother=0)),
     (3, 8, 1e2, dict(num_functions=2, smoother='JACOBI', relaxation=0.5, node_block_smoother=0)),
     (2, 16, 1e2, dict(rho_iters=10, node_block_smoother=0)),
+    # parallel heavy-edge matching (aggregation_type HEM): nodal and scalar, UA and SA
+    (3, 16, 1e6, dict(num_functions=2, aggregation_type='HEM', AMG_type='UA')),
+    (3, 8, 1e4, dict(num_functions=2, aggregation_type='HEM')),
+    (2, 32, 1e3, dict(aggregation_type='HEM', AMG_type='UA')),
 ]
 
 
@@ -30,6 +34,8 @@ def to_c(kw):
         c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
     if 'smoother' in c:
         c['smoother'] = {'JACOBI': 1, 'L1DIAG': 2, 'JACOBI_RHO': 3}[c['smoother']]
+    if 'aggregation_type' in c:
+        c['aggregation_type'] = {'MIS': 2, 'HEM': 5}[c['aggregation_type']]
     return c
 
 
