@@ -270,7 +270,10 @@ def main():
                          ('reference family: UA + parallel HEM + W-cycle + multicolour SGS + coarse scaling '
                           '(src/amg_parameters.py:67-89)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=3)),):
+                               Schwarz_type=3)),
+                         ('reference family, coarse_dof 2048 (dense solve instead of the launch-bound W bottom)',
+                          dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
+                               Schwarz_type=3, coarse_dof=2048)),):
             if (kw['smoother'] == prof['smoother'] and kw.get('coarse_scaling', 0) == prof['coarse_scaling']
                     and kw.get('aggregation_type', 2) == 2):
                 continue

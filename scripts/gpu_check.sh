@@ -12,7 +12,7 @@
 # the summaries to be kept into profiles/ afterwards.
 TAG=${1:-check}
 STEPS=${2:-smoke,tests,bench,trace,pmc}
-OUT=gpurun_out/$TAG
+OUT=$(pwd)/gpurun_out/$TAG
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -34,13 +34,13 @@ if want bench; then
   step bench 600 python -u bench.py && tail -1 $OUT/bench.log > $OUT/bench.json
 fi
 if want trace; then
-  cd /tmp && step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/trace -o bench \
+  cd /tmp && step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench \
       -- python3 $ROOT/bench.py $LIGHT; cd $ROOT
 fi
 if want pmc; then
-  cd /tmp && step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/$OUT/pmc_fetch -o bench \
+  cd /tmp && step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench \
       -- python3 $ROOT/bench.py $LIGHT; cd $ROOT
-  cd /tmp && step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/$OUT/pmc_write -o bench \
+  cd /tmp && step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench \
       -- python3 $ROOT/bench.py $LIGHT; cd $ROOT
   F=$(find $OUT/pmc_fetch -name '*counter_collection.csv' | head -1)
   W=$(find $OUT/pmc_write -name '*counter_collection.csv' | head -1)
