@@ -102,6 +102,9 @@ def main():
     ap.add_argument('--poly-degree', type=int, default=2)
     ap.add_argument('--scaling', type=int, default=0, help='coarse-grid correction scaling (coarse_scaling ON)')
     ap.add_argument('--cycle', choices=('V', 'W'), default='V')
+    ap.add_argument('--exchange', choices=('rccl', 'gloo'), default='rccl',
+                    help='N > 1 transport: RCCL (default), or the host-staged gloo exchange '
+                         '(mamg_dist_set_exchange; runs several ranks on one GPU, for rehearsals)')
     ap.add_argument('--compare-host-setup', action='store_true',
                     help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
@@ -115,11 +118,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.exchange == 'gloo' and torch.cuda.device_count() > 0:
+        local %= torch.cuda.device_count()      # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    gloo = world > 1 and args.exchange == 'gloo'
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if gloo:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=dev)
+    rdev = torch.device('cpu') if gloo else dev        # device of the timing reductions
 
     import metric_amg_examples_amd as M
 
@@ -144,14 +154,14 @@ def main():
     def allmax(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=rdev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         return t.item()
 
     def allsum(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=rdev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
         return t.item()
 
@@ -184,11 +194,12 @@ def main():
         layout = B.layout
         r = torch.as_tensor(r_full).to(dev)
     else:
-        uid = [M.DistMetricAMG.unique_id() if rank == 0 else None]
+        uid = [M.DistMetricAMG.unique_id() if (rank == 0 and not gloo) else None]
         torch.distributed.broadcast_object_list(uid, src=0)
         t0 = time.time()
         B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
-                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local, **prof)
+                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local,
+                            exchange='gloo' if gloo else None, **prof)
         t_setup = time.time() - t0
         setup_info = {'path': 'deterministic setup replicated on every rank (GPU setup; host setup if the '
                               'profile is unsupported) + rank-local upload',
@@ -412,7 +423,8 @@ def main():
                         % (args.problem, args.dim, args.nrefs, args.gamma, PROFILE_NAMES[args.smoother]
                            + (', W-cycle' if args.cycle == 'W' else '') + (', coarse scaling' if args.scaling else '')),
             'n': n, 'N': sysm.N, 'nnz': sysm.nnz, 'levels': levels,
-            'parallelism': 'single' if world == 1 else 'row-partition x%d (RCCL halo)' % world,
+            'parallelism': 'single' if world == 1 else 'row-partition x%d (%s halo)' % (
+                world, 'host-staged gloo' if gloo else 'RCCL'),
             'device_layout': layout,
         },
         'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),

@@ -43,7 +43,7 @@ def main():
         m0 = torch.cuda.mem_get_info()[0]
         t0 = time.time()
         hs.append(M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=args.ranks, comm_id=None,
-                                  num_functions=2))
+                                  num_functions=2, print_level=2))
         torch.cuda.synchronize()
         t = time.time() - t0
         held = m0 - torch.cuda.mem_get_info()[0]

@@ -1,6 +1,8 @@
 // capi.cpp -- extern "C" boundary (include/mamg.h).  No exceptions cross it:
 // every entry point catches, records a thread-local message and returns a
 // negative status.
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -300,6 +302,15 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   mamg::Hierarchy H;
   std::string err;
   Seeds S(idofs, n_idofs, v.n, params);
+  // setup phases to stderr with print_level >= 2 (HAZmath's setup printing)
+  auto t_0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (params->print_level < 2) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[mamg] rank %d/%d setup: %-24s %.3f s\n", rank, nranks, what,
+                 std::chrono::duration<double>(t - t_0).count());
+    t_0 = t;
+  };
   // every rank builds the same hierarchy: on its own GPU when the profile is
   // the GPU setup's (bitwise equal to the host setup), else on the host
   rc = MAMG_ERR_UNSUPPORTED;
@@ -310,14 +321,18 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     mamg::DevMat dA;
     mamg::dev_prereserve(params->device, v.nnz(), nranks);   // rank-local layout memory first
     rc = mamg::upload_a0(v, &G, &dA, &err);
+    lap("A0 upload");
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
+    lap("GPU setup");
     if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
+    lap("hierarchy download");
     if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
   if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
   rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err);
+  lap("plan + rank-local upload");
   mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_dhandle{d};

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -3502,9 +3503,13 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   double pw[MAMG_POLY_MAX];
   const int pm = poly_weights(p, pw);
   DistPlan plan;
+  const auto tp0 = std::chrono::steady_clock::now();
   int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0,
                            p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0);
   if (rc) return rc;
+  if (p.print_level >= 2)
+    std::fprintf(stderr, "[mamg] rank %d/%d setup:   of which host plan    %.3f s\n", rank, nranks,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count());
   std::unique_ptr<DistHandle> h(new DistHandle());
   h->p = p;
   h->rank = rank;
