@@ -362,7 +362,7 @@ def main():
     # only when it was measured on this kernel source (device.hip sha256)
     # and this layout; the line carries its provenance either way.
     fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
-    post_mode = 'k' if fmt0.get('post_k') else 'merged'
+    post_mode = 'k' if (fmt0.get('post_k') or world > 1) else 'merged'   # rank-local K by default
     a0_mode = 'half' if fmt0.get('half') else 'sell'
     traffic, traffic_src = {}, None
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
@@ -382,12 +382,12 @@ def main():
         except (OSError, ValueError):
             traffic = {}
 
-    rk = 'hsell2_kernel' if fmt0.get('half') else ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel')
+    rk = 'hsell2_kernel' if (fmt0.get('half') or world > 1) else ('sell2_kernel' if fmt0.get('sell') else 'bsr2_kernel')
     if layout == 'csr':
         names = ('csr_kernel<*,RESID,0>', 'csr_kernel<*,BJAC/JACOBI,0>')
     elif post_mode == 'k':
         names = ('%s<RESID,...,0>' % rk,
-                 '%s<KPOST,...,0>' % ('sell2_kernel' if fmt0.get('post_sell') else 'bsr2_kernel'))
+                 '%s<KPOST,...,0>' % ('sell2_kernel' if (fmt0.get('post_sell') or world > 1) else 'bsr2_kernel'))
     else:
         names = ('%s<RESID,...,0>' % rk,
                  'bsr2_post_kernel<8,...,0>' if fmt0.get('post_fused', True) else 'bsr2_kernel<*,BJAC,...,0>')
