@@ -3,6 +3,7 @@
 // negative status.
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -311,6 +312,8 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                  std::chrono::duration<double>(t - t_0).count());
     t_0 = t;
   };
+  mamg::GhostLists ghosts;
+  bool pre = false;
   // every rank builds the same hierarchy: on its own GPU when the profile is
   // the GPU setup's (bitwise equal to the host setup), else on the host
   rc = MAMG_ERR_UNSUPPORTED;
@@ -324,14 +327,23 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     lap("A0 upload");
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
     lap("GPU setup");
-    if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
+    // each rank downloads only the rows it keeps, ghost lists computed on the
+    // GPU (MAMG_DIST_FULL_DOWNLOAD=1: the whole hierarchy, ghosts on the host)
+    const char* full = std::getenv("MAMG_DIST_FULL_DOWNLOAD");
+    if (full && std::atoi(full)) {
+      if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
+    } else if (!rc) {
+      rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, params->post_fusion != 0, &H,
+                                     &ghosts, &err);
+      pre = !rc;
+    }
     lap("hierarchy download");
     if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
   if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
-  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err);
+  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err, pre ? &ghosts : nullptr);
   lap("plan + rank-local upload");
   mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }

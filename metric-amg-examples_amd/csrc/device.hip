@@ -3490,7 +3490,8 @@ int dist_get_unique_id(void* id, std::string* err) {
 }
 
 int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
-                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err) {
+                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
+                const GhostLists* ghosts) {
   if (p.cycle_type != MAMG_V_CYCLE || p.maxit != 1 || p.presmooth_iter != 1 || p.postsmooth_iter != 1) {
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
@@ -3505,7 +3506,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   DistPlan plan;
   const auto tp0 = std::chrono::steady_clock::now();
   int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0,
-                           p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0);
+                           p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0, ghosts);
   if (rc) return rc;
   if (p.print_level >= 2)
     std::fprintf(stderr, "[mamg] rank %d/%d setup:   of which host plan    %.3f s\n", rank, nranks,

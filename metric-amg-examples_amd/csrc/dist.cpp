@@ -145,8 +145,22 @@ void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HB
   }
 }
 
+void dist_ranges(const std::vector<int64_t>& nv, const std::vector<char>& coarsest, int nranks,
+                 int64_t rep_nodes, std::vector<std::vector<int64_t>>* own, std::vector<char>* rep) {
+  const size_t nl = nv.size();
+  own->assign(nl, std::vector<int64_t>(nranks + 1));
+  rep->assign(nl, 0);
+  bool r = false;
+  for (size_t l = 0; l < nl; ++l) {
+    if (l > 0 && (nv[l] <= rep_nodes || coarsest[l])) r = true;
+    (*rep)[l] = r;
+    for (int q = 0; q <= nranks; ++q) (*own)[l][q] = r ? (q == 0 ? 0 : nv[l]) : (nv[l] * q) / nranks;
+  }
+}
+
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err, bool kpost, double kw) {
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost, double kw,
+                    const GhostLists* pre) {
   // K = P - (kw W) AP: the first post-smoothing step's smoother (device.hip
   // poly_scaled: kw W elementwise, then the merge; bitwise the single-GPU K)
   auto kmerge_kw = [kw](const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K) {
@@ -165,29 +179,38 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
   plan->nranks = nranks;
   plan->levels.assign(nl, DistLevel());
   auto Aview = [&](int l) { return l == 0 ? A0 : H.A(l); };
-  // replication: from the first small level down; coarsest always; level 0 never
-  bool rep = false;
-  for (int l = 0; l < nl; ++l) {
-    const HostLevel& hl = H.levels[l];
-    DistLevel& D = plan->levels[l];
-    D.nv = hl.n / 2;
-    D.coarsest = hl.coarsest;
-    if (l > 0 && (D.nv <= rep_nodes || D.coarsest)) rep = true;
-    D.replicated = rep;
-    D.own.resize(nranks + 1);
-    for (int q = 0; q <= nranks; ++q) D.own[q] = rep ? (q == 0 ? 0 : D.nv) : (D.nv * q) / nranks;
-    if (!hl.coarsest && hl.WB.n == 0) {
-      *err = "multi-GPU path needs node-block smoothers on every level";
-      return MAMG_ERR_UNSUPPORTED;
+  {
+    std::vector<int64_t> nv(nl);
+    std::vector<char> co(nl), rep;
+    std::vector<std::vector<int64_t>> own;
+    for (int l = 0; l < nl; ++l) { nv[l] = H.levels[l].n / 2; co[l] = H.levels[l].coarsest; }
+    dist_ranges(nv, co, nranks, rep_nodes, &own, &rep);
+    for (int l = 0; l < nl; ++l) {
+      const HostLevel& hl = H.levels[l];
+      DistLevel& D = plan->levels[l];
+      D.nv = nv[l];
+      D.coarsest = hl.coarsest;
+      D.replicated = rep[l];
+      D.own = own[l];
+      if (!hl.coarsest && hl.WB.n == 0 && hl.Wn.empty()) {
+        *err = "multi-GPU path needs node-block smoothers on every level";
+        return MAMG_ERR_UNSUPPORTED;
+      }
     }
   }
   // ghost lists of every rank on distributed levels (send lists need them)
-  std::vector<std::vector<std::vector<int64_t>>> ghosts(nl, std::vector<std::vector<int64_t>>(nranks));
+  GhostLists ghosts_here;
+  if (!pre) ghosts_here.assign(nl, std::vector<std::vector<int64_t>>(nranks));
+  const GhostLists& ghosts = pre ? *pre : ghosts_here;
+  if (pre && ((int)pre->size() != nl || (*pre)[0].size() != (size_t)nranks)) {
+    *err = "precomputed ghost lists do not match the hierarchy";
+    return MAMG_ERR_ARG;
+  }
 #pragma omp parallel for collapse(2) schedule(dynamic, 1)
   for (int l = 0; l < nl; ++l)
     for (int q = 0; q < nranks; ++q) {
       const DistLevel& D = plan->levels[l];
-      if (D.replicated) continue;
+      if (pre || D.replicated) continue;
       const int64_t o0 = D.own[q], o1 = D.own[q + 1];
       std::vector<int64_t> g;
       external_node_cols(Aview(l), D.nv, D.nv, o0, o1, o0, o1, &g);
@@ -198,18 +221,28 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
           external_node_cols(H.levels[l - 1].AP.view(), F.nv, D.nv, F.own[q], F.own[q + 1], o0, o1, &g);
       }
       sort_unique(&g);
-      ghosts[l][q] = std::move(g);
+      ghosts_here[l][q] = std::move(g);
     }
   for (int l = 0; l < nl; ++l) {
     DistLevel& D = plan->levels[l];
     const HostLevel& hl = H.levels[l];
+    // smoother blocks: Wfull holds nodes [w0, w0 + Wfull.size()/4)
     std::vector<double> Wfull;
-    if (!hl.coarsest && !node_blocks_of(hl.WB.view(), D.nv, &Wfull)) {
+    int64_t w0 = 0;
+    if (!hl.Wn.empty()) {
+      Wfull = hl.Wn;
+      w0 = hl.wn0;
+    } else if (!hl.coarsest && !node_blocks_of(hl.WB.view(), D.nv, &Wfull)) {
       *err = "multi-GPU path needs node-block smoothers on every level";
       return MAMG_ERR_UNSUPPORTED;
     }
+    const int64_t w1 = w0 + (int64_t)Wfull.size() / 4;
     if (D.replicated) {
       D.o0 = 0; D.o1 = D.nv; D.nloc = D.nv;
+      if (!hl.coarsest && (w0 != 0 || w1 != D.nv)) {
+        *err = "smoother slice does not cover a replicated level";
+        return MAMG_ERR_ARG;
+      }
       to_bsr2(Aview(l), D.nv, D.nv, &D.A);
       D.W = std::move(Wfull);
       D.ghost_off.assign(nranks + 1, 0);
@@ -238,7 +271,11 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       if (J >= o0 && J < o1) return J - o0;
       return nloc + (std::lower_bound(gl.begin(), gl.end(), J) - gl.begin());
     });
-    D.W.assign(Wfull.begin() + 4 * o0, Wfull.begin() + 4 * o1);
+    if (o0 < w0 || o1 > w1) {
+      *err = "smoother slice does not cover the owned nodes";
+      return MAMG_ERR_ARG;
+    }
+    D.W.assign(Wfull.begin() + 4 * (o0 - w0), Wfull.begin() + 4 * (o1 - w0));
   }
   // P_loc / Rp_loc (need the level l+1 numbering)
   for (int l = 0; l + 1 < nl; ++l) {

@@ -30,10 +30,25 @@ struct DistPlan {
   std::vector<DistLevel> levels;
 };
 
+// ghost node lists [level][rank] (global ids, sorted).  build_dist_plan reads
+// the own rank's list whole and the other ranks' lists only inside the own
+// node range (the send lists), so a precomputed set may hold just that.
+using GhostLists = std::vector<std::vector<std::vector<int64_t>>>;
+
+// node ranges [level][nranks+1] and replication of every level, identical on
+// all ranks: replicated from the first level with <= rep_nodes nodes (or the
+// coarsest) down; level 0 never
+void dist_ranges(const std::vector<int64_t>& nv, const std::vector<char>& coarsest, int nranks,
+                 int64_t rep_nodes, std::vector<std::vector<int64_t>>* own, std::vector<char>* rep);
+
 // fuse: prolongation fused into the post sweep (needs A P from the setup);
-// kpost: through K = P - kw W (A P) (one operator), else through [P | AP]
+// kpost: through K = P - kw W (A P) (one operator), else through [P | AP].
+// pre: ghost lists computed elsewhere (ghier_download_rank: then H holds only
+// the rows this rank reads, and node-major smoother slices in HostLevel::Wn);
+// nullptr = computed here from the full hierarchy.
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
-                    bool fuse, DistPlan* plan, std::string* err, bool kpost = true, double kw = 1.0);
+                    bool fuse, DistPlan* plan, std::string* err, bool kpost = true, double kw = 1.0,
+                    const GhostLists* pre = nullptr);
 // K rows = P rows - W_I (AP rows), block-column union (both sorted, same columns)
 void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K);
 

@@ -50,6 +50,13 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
 // copy a GPU hierarchy into a host Hierarchy (same fields the host setup
 // fills; level-0 A is the given host view)
 int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string* err);
+// multi-GPU: download only what rank `rank` of `nranks` reads (its node rows
+// of every distributed level, replicated levels whole, no R / aggregates) and
+// compute the ghost lists on the device (build_dist_plan's `pre`); A0d is the
+// device copy of the host A0
+int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
+                        int64_t rep_nodes, bool post_fusion, Hierarchy* H,
+                        std::vector<std::vector<std::vector<int64_t>>>* ghosts, std::string* err);
 // host CSR -> HBM, buffers owned by G (G->device selects the GPU)
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err);
 

@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "dist.h"
 #include "gsetup.h"
 #include "rowstage.h"
 
@@ -1528,6 +1529,169 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
       } else {
         B.col[o] = (int32_t)i; B.val[o] = W[4 * I + 3 * f];
       }
+    }
+  }
+  return MAMG_OK;
+}
+
+namespace {
+
+// ghost marks of one field-major matrix for every rank: row i (node I = i mod
+// nr) belongs to the rank q whose range rown[q..q+1) holds I; a column node
+// J = col mod nc outside coln[q..q+1) is a ghost of q: mark[q nc + J] = 1
+// (dist.cpp external_node_cols, all ranks in one pass)
+__global__ void ghost_mark_kernel(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                  int64_t n, int64_t nr, int64_t nc, const int64_t* __restrict__ rown,
+                                  const int64_t* __restrict__ coln, int nranks,
+                                  uint8_t* __restrict__ mark) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t I = i % nr;
+  int lo = 0, hi = nranks - 1;   // last q with rown[q] <= I (empty ranges skipped)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (rown[mid] <= I) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t c0 = coln[lo], c1 = coln[lo + 1];
+  uint8_t* m = mark + (int64_t)lo * nc;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+    const int64_t J = col[k] % nc;
+    if (J < c0 || J >= c1) m[J] = 1;
+  }
+}
+
+struct DevScratch {             // plain hipMalloc buffer, freed on scope exit
+  void* p = nullptr;
+  ~DevScratch() { if (p) (void)hipFree(p); }
+};
+
+}  // namespace
+
+int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
+                        int64_t rep_nodes, bool post_fusion, Hierarchy* H, GhostLists* ghosts,
+                        std::string* err) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
+  H->params = G.params;
+  H->A0 = A0;
+  H->levels.clear();
+  int nl = 0;
+  while (nl < (int)G.levels.size())
+    if (G.levels[nl++].coarsest) break;
+  // same ranges, replication and fusion decision as build_dist_plan
+  std::vector<int64_t> nv(nl);
+  std::vector<char> co(nl), rep;
+  std::vector<std::vector<int64_t>> own;
+  for (int l = 0; l < nl; ++l) { nv[l] = G.levels[l].n / 2; co[l] = G.levels[l].coarsest; }
+  dist_ranges(nv, co, nranks, rep_nodes, &own, &rep);
+  bool fuse = post_fusion;
+  for (int l = 0; l + 1 < nl && fuse; ++l)
+    if (G.levels[l].AP.n != G.levels[l].n) fuse = false;
+
+  // full download of a matrix, or of the node rows [r0, r1) of both fields
+  // (other rows empty: build_dist_plan reads no others)
+  auto dl = [&](const DevMat& M, bool all, int64_t r0, int64_t r1, Csr* C) -> int {
+    C->n = M.n;
+    C->m = M.m;
+    if (all) {
+      C->ptr.resize(M.n + 1);
+      C->col.resize(M.nnz);
+      C->val.resize(M.nnz);
+      RCHK(to_host(C->ptr.data(), M.ptr, M.n + 1, err));
+      RCHK(to_host(C->col.data(), M.col, M.nnz, err));
+      RCHK(to_host(C->val.data(), M.val, M.nnz, err));
+      return MAMG_OK;
+    }
+    const int64_t nr = M.n / 2, w = r1 - r0;
+    std::vector<int64_t> p0(w + 1), p1(w + 1);
+    RCHK(to_host(p0.data(), M.ptr + r0, w + 1, err));
+    RCHK(to_host(p1.data(), M.ptr + nr + r0, w + 1, err));
+    const int64_t n0 = p0[w] - p0[0], n1 = p1[w] - p1[0];
+    C->col.resize(n0 + n1);
+    C->val.resize(n0 + n1);
+    RCHK(to_host(C->col.data(), M.col + p0[0], n0, err));
+    RCHK(to_host(C->val.data(), M.val + p0[0], n0, err));
+    RCHK(to_host(C->col.data() + n0, M.col + p1[0], n1, err));
+    RCHK(to_host(C->val.data() + n0, M.val + p1[0], n1, err));
+    C->ptr.resize(M.n + 1);
+    std::fill(C->ptr.begin(), C->ptr.begin() + r0, 0);
+    for (int64_t t = 0; t <= w; ++t) C->ptr[r0 + t] = p0[t] - p0[0];
+    std::fill(C->ptr.begin() + r1, C->ptr.begin() + nr + r0, n0);
+    for (int64_t t = 0; t <= w; ++t) C->ptr[nr + r0 + t] = n0 + p1[t] - p1[0];
+    std::fill(C->ptr.begin() + nr + r1, C->ptr.end(), n0 + n1);
+    return MAMG_OK;
+  };
+
+  // ghost lists: the own rank's whole list, the others' inside the own range
+  ghosts->assign(nl, std::vector<std::vector<int64_t>>(nranks));
+  int64_t mark_bytes = 0;
+  for (int l = 0; l < nl; ++l)
+    if (!rep[l]) mark_bytes = std::max<int64_t>(mark_bytes, (int64_t)nranks * nv[l]);
+  if (mark_bytes) {
+    DevScratch rng, mk;
+    HIPCHK(hipMalloc(&rng.p, (size_t)nl * (nranks + 1) * sizeof(int64_t)));
+    HIPCHK(hipMalloc(&mk.p, (size_t)mark_bytes));
+    int64_t* drng = (int64_t*)rng.p;
+    uint8_t* mark = (uint8_t*)mk.p;
+    for (int l = 0; l < nl; ++l)
+      HIPCHK(hipMemcpy(drng + (size_t)l * (nranks + 1), own[l].data(), (nranks + 1) * sizeof(int64_t),
+                       hipMemcpyHostToDevice));
+    std::vector<uint8_t> hm;
+    for (int l = 0; l < nl; ++l) {
+      if (rep[l]) continue;
+      HIPCHK(hipMemset(mark, 0, (size_t)nranks * nv[l]));
+      auto marks = [&](const DevMat& M, int rl) {
+        if (M.n == 0) return;
+        ghost_mark_kernel<<<nblk(M.n), 256>>>(M.ptr, M.col, M.n, nv[rl], nv[l], drng + (size_t)rl * (nranks + 1),
+                                              drng + (size_t)l * (nranks + 1), nranks, mark);
+      };
+      marks(l == 0 ? A0d : G.levels[l].A, l);
+      if (l > 0) {
+        marks(G.levels[l - 1].P, l - 1);
+        if (fuse) marks(G.levels[l - 1].AP, l - 1);
+      }
+      HIPCHK(hipGetLastError());
+      const int64_t o0 = own[l][rank], o1 = own[l][rank + 1];
+      for (int q = 0; q < nranks; ++q) {
+        const int64_t a = q == rank ? 0 : o0, b = q == rank ? nv[l] : o1;
+        hm.resize(b - a);
+        RCHK(to_host(hm.data(), mark + (size_t)q * nv[l] + a, b - a, err));
+        std::vector<int64_t>& g = (*ghosts)[l][q];
+        for (int64_t t = 0; t < b - a; ++t)
+          if (hm[t]) g.push_back(a + t);
+      }
+    }
+  }
+
+  for (int l = 0; l < nl; ++l) {
+    const GLevel& g = G.levels[l];
+    H->levels.emplace_back();
+    HostLevel& h = H->levels.back();
+    h.n = g.n;
+    h.coarsest = g.coarsest;
+    const bool all = rep[l];
+    const int64_t o0 = own[l][rank], o1 = own[l][rank + 1];
+    if (l > 0) RCHK(dl(g.A, all, o0, o1, &h.A));
+    if (g.coarsest) {
+      h.Ainv.resize(g.n * g.n);
+      RCHK(to_host(h.Ainv.data(), g.Ainv, g.n * g.n, err));
+      break;
+    }
+    RCHK(dl(g.P, all, o0, o1, &h.P));
+    if (fuse) RCHK(dl(g.AP, all, o0, o1, &h.AP));
+    h.nagg = g.nagg;
+    h.w_sa = g.w_sa;
+    // node blocks of the owned nodes (ghier_download's WB: a node split by
+    // seed blocks keeps its two diagonal entries only)
+    const int64_t w0 = all ? 0 : o0, w1 = all ? nv[l] : o1;
+    h.wn0 = w0;
+    h.Wn.resize(4 * (w1 - w0));
+    RCHK(to_host(h.Wn.data(), g.W + 4 * w0, 4 * (w1 - w0), err));
+    if (g.joined) {
+      std::vector<uint8_t> jn(w1 - w0);
+      RCHK(to_host(jn.data(), g.joined + w0, w1 - w0, err));
+      for (int64_t t = 0; t < w1 - w0; ++t)
+        if (!jn[t]) h.Wn[4 * t + 1] = h.Wn[4 * t + 2] = 0.0;
     }
   }
   return MAMG_OK;

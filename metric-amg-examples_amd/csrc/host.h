@@ -38,6 +38,8 @@ struct HostLevel {
   Csr A;                    // level 0: empty (the caller's matrix is used)
   std::vector<double> winv; // point smoother weights (empty if WB used)
   Csr WB;                   // seed-block smoother (level 0 with idofs)
+  std::vector<double> Wn;   // or: 2x2 node blocks of nodes [wn0, wn0 + Wn.size()/4)
+  int64_t wn0 = 0;          //     (multi-GPU rank slice, gsetup.hip ghier_download_rank)
   Csr P, R;                 // prolongation / restriction (R = P^T)
   Csr AP;                   // A P (Galerkin intermediate; kept for post fusion)
   std::vector<int64_t> agg; // aggregate id per row (-1 isolated)

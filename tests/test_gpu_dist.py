@@ -79,6 +79,46 @@ def test_virtual_ranks_poly_and_emi(lib_built, problem, kw, P):
         hh.close()
 
 
+@pytest.mark.parametrize('case,P,rep', [('bidomain', 3, 100), ('bidomain', 8, 1), ('unfused', 2, 100),
+                                         ('emi_poly', 4, 100), ('bidomain2d', 5, 10)])
+def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
+    """Each rank downloads only its rows of the GPU hierarchy, with the ghost
+    lists marked on the device (gsetup.hip ghier_download_rank): the same
+    rank-local operators as the whole-hierarchy download with host ghost
+    lists -- bitwise equal applies and byte counts, also with every level
+    above the coarsest distributed (rep_nodes 1, 8 ranks), without post
+    fusion and with the seed-split EMI smoother."""
+    import torch
+    import metric_amg_examples_amd as M
+    kw = {}
+    if case == 'emi_poly':
+        s = M.problems.emi(3, 16, 1e6)
+        kw = dict(smoother=12, Schwarz_maxlvl=0)
+    elif case == 'bidomain2d':
+        s = M.problems.bidomain(2, 64, 1.0)
+    else:
+        s = M.problems.bidomain(3, 16, 1e6)
+    if case == 'unfused':
+        kw['post_fusion'] = 0
+    r = mo.seeded_rhs(s.N)
+    out, nbytes = [], []
+    for full in ('1', '0'):
+        monkeypatch.setenv('MAMG_DIST_FULL_DOWNLOAD', full)
+        hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
+                              num_functions=2, **kw) for p in range(P)]
+        rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+        zs = [torch.zeros_like(x) for x in rs]
+        M.DistMetricAMG.virtual_apply(hs, rs, zs)
+        torch.cuda.synchronize()
+        out.append([z.cpu().numpy() for z in zs])
+        nbytes.append([hh.apply_bytes for hh in hs])
+        for hh in hs:
+            hh.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    assert nbytes[0] == nbytes[1]
+
+
 @pytest.mark.parametrize('mode', ['unfused', 'sell', 'nohalf', 'merged'])
 def test_virtual_ranks_storage_variants(lib_built, monkeypatch, mode):
     """Distributed cycle without post fusion (prolongation, fine halo,
