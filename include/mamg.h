@@ -142,6 +142,17 @@ int mamg_gen_bidomain(int dim, int64_t n, double gamma, double kappa1,
                       double kappa2, int64_t* rowptr, int32_t* colind,
                       double* values);
 
+/* Manufactured solution of the bidomain drivers (src/bidomain_2d.py:7-99,
+ * src/bidomain_3d.py:7-49): b[nrows] = the right-hand side of the system
+ * mamg_gen_bidomain builds (loads, full-flux terms on tags 3/4, Dirichlet
+ * lifting; exact values on the Dirichlet rows). */
+int mamg_gen_bidomain_mms(int dim, int64_t n, double gamma, double kappa1,
+                          double kappa2, double* b);
+/* H1 errors err[2] = |u1 - u1h|_1, |u2 - u2h|_1 of a solution x[nrows]
+ * (errornorm(u, uh, 'H1'), src/bidomain_2d.py:239-240). */
+int mamg_bidomain_mms_error(int dim, int64_t n, double gamma, double kappa1,
+                            double kappa2, const double* x, double* err);
+
 /* ---- host setup (no GPU needed).  The hierarchy keeps a VIEW of A (level
  *      0): the caller keeps A alive until mamg_hier_free. ------------------ */
 /* Replaces metricAMG.__init__'s HAZmath setup (src/utils.py:86).  idofs may

@@ -71,6 +71,9 @@ SIGNATURES = {
     'mamg_gen_bidomain_size': (C.c_int, [C.c_int, C.c_int64, P_I64, P_I64]),
     'mamg_gen_bidomain': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double,
                                     P_I64, P_I32, P_F64]),
+    'mamg_gen_bidomain_mms': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, P_F64]),
+    'mamg_bidomain_mms_error': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                          P_F64, P_F64]),
     'mamg_host_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64,
                                   C.POINTER(mamg_params), C.POINTER(VP)]),
     'mamg_hier_free': (None, [VP]),

@@ -174,6 +174,25 @@ int mamg_gen_bidomain(int dim, int64_t n, double gamma, double kappa1, double ka
   GUARD_END
 }
 
+int mamg_gen_bidomain_mms(int dim, int64_t n, double gamma, double kappa1, double kappa2, double* b) {
+  GUARD_BEGIN
+  if (!b) { set_error("null output buffer"); return MAMG_ERR_ARG; }
+  int rc = mamg::gen_bidomain_mms(dim, n, gamma, kappa1, kappa2, b);
+  if (rc) set_error("gen_bidomain_mms: dim must be 2 or 3 and n >= 1");
+  return rc;
+  GUARD_END
+}
+
+int mamg_bidomain_mms_error(int dim, int64_t n, double gamma, double kappa1, double kappa2,
+                            const double* x, double* err) {
+  GUARD_BEGIN
+  if (!x || !err) { set_error("null argument"); return MAMG_ERR_ARG; }
+  int rc = mamg::bidomain_mms_error(dim, n, gamma, kappa1, kappa2, x, err);
+  if (rc) set_error("bidomain_mms_error: dim must be 2 or 3 and n >= 1");
+  return rc;
+  GUARD_END
+}
+
 int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN

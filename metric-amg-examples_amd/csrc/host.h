@@ -81,6 +81,10 @@ inline int smoother_steps(const mamg_params& p) {
 int gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz);
 int gen_bidomain(int dim, int64_t n, double gamma, double k1, double k2,
                  int64_t* rowptr, int32_t* colind, double* values);
+// mms.cpp: manufactured-solution right-hand side and H1 errors
+int gen_bidomain_mms(int dim, int64_t n, double gamma, double k1, double k2, double* b);
+int bidomain_mms_error(int dim, int64_t n, double gamma, double k1, double k2, const double* x,
+                       double* err);
 
 // convert.cpp: field-major CSR (rows f*nr+I, cols g*nc+J, 2 fields) -> 2x2 BSR
 struct HBsr {

@@ -15,11 +15,15 @@ Mesh loops: n = 2^i for i in [5, 5+nrefs) (bidomain 2-D), [3, 3+nrefs)
 appends the reference's iters row ``ndofs niters cond timeKSP r h``
 (src/bidomain_2d.py:149,259) to results/<problem>/iters_<...>.txt; timeKSP
 spans preconditioner setup + CG, as in the reference (:176-197).
+The bidomain drivers solve against the reference's manufactured solution
+(csrc/mms.cpp, src/bidomain_2d.py:7-99) and append its error row
+``ndofs h |eu1|_1 r|eu1|_1 |eu2|_1 r|eu2|_1`` (H1 errors and rates,
+src/bidomain_2d.py:150,239-270) to results/<problem>/error_<...>.txt;
+``-rhs random`` uses the bench's seeded uniform(-1,1) vector instead.
 Differences (stated, not hidden): the matrices come from the in-library
-generators (problems.py; FEniCS is absent), the right-hand side is the seeded
-uniform(-1,1) vector instead of the manufactured solution's load, so the H1
-error tables are not produced; the 3D-1D neuron mesh is the synthetic
-``problems.neuron_curve``.
+generators (problems.py; FEniCS is absent); the EMI drivers use seeded random
+right-hand sides (their manufactured solutions are not restated); the 3D-1D
+neuron mesh is the synthetic ``problems.neuron_curve``.
 """
 from __future__ import annotations
 
@@ -37,17 +41,18 @@ from .precond import (get_block_diag_precond, get_hazmath_amg_precond, get_hazma
                       get_hazmath_metric_precond_mono)
 
 HEADERS_KSP = ['ndofs', 'niters', 'cond', 'timeKSP', 'r', 'h']
+HEADERS_ERROR = ['ndofs', 'h', '|eu1|_1', 'r|eu1|_1', '|eu2|_1', 'r|eu2|_1']
 
 
-def _iters_path(result_dir, precond, **kv):
+def _iters_path(result_dir, precond, what='iters', **kv):
     tail = '_'.join('%s%s' % (k, v) for k, v in kv.items())
-    return os.path.join(result_dir, 'iters_precond%s_%s.txt' % (precond, tail))
+    return os.path.join(result_dir, '%s_precond%s_%s.txt' % (what, precond, tail))
 
 
-def _append(path, row, first):
+def _append(path, row, first, headers=HEADERS_KSP):
     with open(path, 'w' if first else 'a') as out:
         if first:
-            out.write('%s\n' % ' '.join(HEADERS_KSP))
+            out.write('%s\n' % ' '.join(headers))
         out.write('%s\n' % ' '.join(map(str, row)))
 
 
@@ -92,22 +97,39 @@ def bidomain(argv, dim):
                     choices=('metric_mono', 'metric', 'amg', 'diag'))
     ap.add_argument('-save', type=int, default=0)
     ap.add_argument('-results', type=str, default='./results')
+    ap.add_argument('-rhs', type=str, default='mms', choices=('mms', 'random'))
     args, _ = ap.parse_known_args(argv)
     rdir = os.path.join(args.results, 'bidomain_%dd' % dim)
     os.makedirs(rdir, exist_ok=True)
-    path = _iters_path(rdir, args.precond, kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma,
-                       pdegree=args.pdegree)
+    tags = dict(kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma, pdegree=args.pdegree)
+    path = _iters_path(rdir, args.precond, **tags)
+    epath = _iters_path(rdir, args.precond, 'error', **tags)
     i0 = 5 if dim == 2 else 3
     rows = []
+    errors0 = h0 = None
     for k, n in enumerate(2 ** i for i in range(i0, i0 + args.nrefs)):
         s = problems.bidomain(dim, n, args.gamma, args.kappa1, args.kappa2)
-        b = problems.seeded_rhs(s.N)
+        if args.rhs == 'mms':
+            b = problems.bidomain_mms_rhs(dim, n, args.gamma, args.kappa1, args.kappa2)
+        else:
+            b = problems.seeded_rhs(s.N)
         x, niters, cond, dt, r, _ = _solve(s, s.W, b, args.precond, s.idofs, 1e-8, 500)
-        row = (s.N, niters, cond, dt, r, np.sqrt(dim) / n)
+        h = np.sqrt(dim) / n            # dolfin hmin: the simplices' longest edge
+        row = (s.N, niters, cond, dt, r, h)
         rows.append(row)
         _append(path, row, k == 0)
         print('bidomain_%dd n=%d ndofs=%d niters=%d cond=%.3g timeKSP=%.3fs r=%.3e'
               % (dim, n, s.N, niters, cond, dt, r), flush=True)
+        if args.rhs != 'mms':
+            continue
+        xs = x.cpu().numpy() if hasattr(x, 'cpu') else np.asarray(x)
+        errors = np.array(problems.bidomain_mms_errors(dim, n, xs, args.gamma, args.kappa1, args.kappa2))
+        rates = [np.nan] * 2 if errors0 is None else np.log(errors / errors0) / np.log(h / h0)
+        errors0, h0 = errors, h
+        erow = (s.N, h) + tuple(v for pair in zip(errors, rates) for v in pair)
+        _append(epath, erow, k == 0, HEADERS_ERROR)
+        print('    |eu1|_1=%.4e (rate %.3f)  |eu2|_1=%.4e (rate %.3f)'
+              % (errors[0], rates[0], errors[1], rates[1]), flush=True)
     return rows
 
 

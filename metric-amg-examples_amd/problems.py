@@ -70,6 +70,32 @@ def bidomain(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float 
     return System(indptr, indices, data, int(N.value), int(N.value) // 2, dim, n, float(gamma))
 
 
+def bidomain_mms_rhs(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0) -> np.ndarray:
+    """Right-hand side of bidomain(dim, n, ...) for the reference's manufactured
+    solution (src/bidomain_2d.py:7-99, src/bidomain_3d.py:7-49; csrc/mms.cpp)."""
+    L = _lib.lib()
+    N, nnz = C.c_int64(), C.c_int64()
+    _lib.check(L.mamg_gen_bidomain_size(dim, n, C.byref(N), C.byref(nnz)))
+    b = np.empty(N.value, dtype=np.float64)
+    _lib.check(L.mamg_gen_bidomain_mms(dim, n, float(gamma), float(kappa1), float(kappa2),
+                                       _lib.ptr(b, C.c_double)))
+    return b
+
+
+def bidomain_mms_errors(dim: int, n: int, x, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0):
+    """(|u1 - u1h|_H1, |u2 - u2h|_H1) of a solution x of the manufactured problem
+    (errornorm(u, uh, 'H1'), src/bidomain_2d.py:239-240)."""
+    L = _lib.lib()
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    nv = (n + 1) ** dim
+    if x.shape != (2 * nv,):
+        raise ValueError('x must have 2 (n+1)^dim entries')
+    err = np.zeros(2)
+    _lib.check(L.mamg_bidomain_mms_error(dim, n, float(gamma), float(kappa1), float(kappa2),
+                                         _lib.ptr(x, C.c_double), _lib.ptr(err, C.c_double)))
+    return float(err[0]), float(err[1])
+
+
 def seeded_rhs(N: int, seed: int = 1234) -> np.ndarray:
     """uniform(-1, 1) fp64, numpy default_rng(seed)."""
     return np.random.default_rng(seed).uniform(-1.0, 1.0, N)

@@ -137,6 +137,19 @@ def test_drivers_write_reference_iters_schema(lib_built, tmp_path):
     f = [p for p in os.listdir(tmp_path / 'bidomain_2d') if p.startswith('iters_precondmetric_mono')]
     lines = open(tmp_path / 'bidomain_2d' / f[0]).read().split('\n')
     assert lines[0] == 'ndofs niters cond timeKSP r h' and len(lines[1].split()) == 6
+    # manufactured solution (the default right-hand side): the reference's
+    # error table with H1 rate ~1, errors equal to the direct solve's
+    f = [p for p in os.listdir(tmp_path / 'bidomain_2d') if p.startswith('error_precondmetric_mono')]
+    lines = open(tmp_path / 'bidomain_2d' / f[0]).read().strip().split('\n')
+    assert lines[0] == 'ndofs h |eu1|_1 r|eu1|_1 |eu2|_1 r|eu2|_1' and len(lines) == 3
+    last = [float(v) for v in lines[2].split()]
+    assert 0.97 < last[3] < 1.03 and 0.97 < last[5] < 1.03
+    import scipy.sparse.linalg as spla
+    from metric_amg_examples_amd import problems
+    s = problems.bidomain(2, 64, 1e6)
+    xd = spla.spsolve(s.scipy().tocsc(), problems.bidomain_mms_rhs(2, 64, 1e6))
+    ed = problems.bidomain_mms_errors(2, 64, xd, 1e6)
+    assert np.allclose([last[2], last[4]], ed, rtol=1e-6, atol=0)
     rows = drivers.emi(['-nrefs', '1', '-gamma', '1e4', '-results', str(tmp_path)], 3)
     assert rows[0][1] < 80
     rows = drivers.bidomain(['-nrefs', '1', '-gamma', '1e2', '-precond', 'metric',
