@@ -15,15 +15,16 @@ Mesh loops: n = 2^i for i in [5, 5+nrefs) (bidomain 2-D), [3, 3+nrefs)
 appends the reference's iters row ``ndofs niters cond timeKSP r h``
 (src/bidomain_2d.py:149,259) to results/<problem>/iters_<...>.txt; timeKSP
 spans preconditioner setup + CG, as in the reference (:176-197).
-The bidomain drivers solve against the reference's manufactured solution
-(csrc/mms.cpp, src/bidomain_2d.py:7-99) and append its error row
+The bidomain and EMI drivers solve against the reference's manufactured
+solutions (csrc/mms.cpp, mms.py; src/bidomain_2d.py:7-99, src/emi_2d.py:8-128)
+and append the error row
 ``ndofs h |eu1|_1 r|eu1|_1 |eu2|_1 r|eu2|_1`` (H1 errors and rates,
 src/bidomain_2d.py:150,239-270) to results/<problem>/error_<...>.txt;
 ``-rhs random`` uses the bench's seeded uniform(-1,1) vector instead.
 Differences (stated, not hidden): the matrices come from the in-library
-generators (problems.py; FEniCS is absent); the EMI drivers use seeded random
-right-hand sides (their manufactured solutions are not restated); the 3D-1D
-neuron mesh is the synthetic ``problems.neuron_curve``.
+generators (problems.py; FEniCS is absent); the EMI drivers' manufactured
+solutions are restated in mms.py (src/emi_2d.py:8-128); the 3D-1D neuron mesh
+is the synthetic ``problems.neuron_curve``.
 """
 from __future__ import annotations
 
@@ -34,7 +35,7 @@ import time
 
 import numpy as np
 
-from . import fileio, parameters as P, problems
+from . import fileio, mms, parameters as P, problems
 from .amg import MetricAMG
 from .krylov import ConjGrad
 from .precond import (get_block_diag_precond, get_hazmath_amg_precond, get_hazmath_metric_precond,
@@ -143,31 +144,49 @@ def emi(argv, dim):
     ap.add_argument('-precond', type=str, default='metric', choices=('metric', 'metric_mono', 'diag'))
     ap.add_argument('-save', type=int, default=0)
     ap.add_argument('-results', type=str, default='./results')
+    ap.add_argument('-rhs', type=str, default='mms', choices=('mms', 'random'))
     args, _ = ap.parse_known_args(argv)
     rdir = os.path.join(args.results, 'emi_%dd' % dim)
     os.makedirs(rdir, exist_ok=True)
-    path = _iters_path(rdir, args.precond, kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma,
-                       pdegree=args.pdegree)
+    tags = dict(kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma, pdegree=args.pdegree)
+    path = _iters_path(rdir, args.precond, **tags)
+    epath = _iters_path(rdir, args.precond, 'error', **tags)
     i0 = 6 if dim == 2 else 2
     rows = []
+    errors0 = h0 = None
     for k, n in enumerate(2 ** i for i in range(i0, i0 + args.nrefs)):
         s = problems.emi(dim, n, args.gamma, args.kappa1, args.kappa2)
-        b = [problems.seeded_rhs(s.W[0], 1234), problems.seeded_rhs(s.W[1], 4321)]
+        if args.rhs == 'mms':
+            b = mms.emi_mms_rhs(dim, n, args.gamma, args.kappa1, args.kappa2)
+        else:
+            b = [problems.seeded_rhs(s.W[0], 1234), problems.seeded_rhs(s.W[1], 4321)]
         then = time.time()
         if args.precond == 'diag':
             BB = get_block_diag_precond(s.blocks, s.W)
         else:
             BB = get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
         solver = ConjGrad(s, precond=BB, tolerance=1e-10, maxiter=500)   # src/emi_3d.py:143
-        solver * b
+        x = solver * b
         dt = time.time() - then
         niters = len(solver.residuals) - 1
         eigs = solver.eigenvalue_estimates()
-        row = (s.N, niters, float(max(eigs) / min(eigs)), dt, solver.residuals[-1], np.sqrt(dim) / n)
+        h = np.sqrt(dim) / n
+        row = (s.N, niters, float(max(eigs) / min(eigs)), dt, solver.residuals[-1], h)
         rows.append(row)
         _append(path, row, k == 0)
         print('emi_%dd n=%d ndofs=%d niters=%d cond=%.3g timeKSP=%.3fs' % (dim, n, s.N, niters, row[2], dt),
               flush=True)
+        if args.rhs != 'mms':
+            continue
+        xs = [xi.cpu().numpy() if hasattr(xi, 'cpu') else np.asarray(xi) for xi in x] \
+            if isinstance(x, (list, tuple)) else (x.cpu().numpy() if hasattr(x, 'cpu') else np.asarray(x))
+        errors = np.array(mms.emi_mms_errors(dim, n, xs, args.gamma, args.kappa1, args.kappa2))
+        rates = [np.nan] * 2 if errors0 is None else np.log(errors / errors0) / np.log(h / h0)
+        errors0, h0 = errors, h
+        _append(epath, (s.N, h) + tuple(v for pair in zip(errors, rates) for v in pair), k == 0,
+                HEADERS_ERROR)
+        print('    |eu1|_1=%.4e (rate %.3f)  |eu2|_1=%.4e (rate %.3f)'
+              % (errors[0], rates[0], errors[1], rates[1]), flush=True)
     return rows
 
 

@@ -221,23 +221,11 @@ def emi(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0
         raise ValueError('n must be even and >= 4')
     h = 1.0 / n
     m = n // 2
-    cell_shape = [n] * (dim - 1) + [m]
     vert_shape = [n + 1] * (dim - 1) + [m + 1]
     nv = int(np.prod(vert_shape))
-    grids = np.meshgrid(*[np.arange(s) for s in cell_shape], indexing='ij')
-    lc = np.stack([g.ravel() for g in grids], axis=1).astype(np.int64)
 
     def half(top: bool):
-        cells = lc.copy()
-        cells[:, dim - 1] += m if top else 0     # global lattice layer of the cell's lower corner
-
-        def index(v):
-            layer = v[:, dim - 1] - m if top else m - v[:, dim - 1]
-            idx = layer
-            for d in range(dim - 2, -1, -1):
-                idx = idx * (n + 1) + v[:, d]
-            return idx
-
+        cells, index = emi_half(dim, n, top)
         Kloc = _PATH_K[dim] * (h if dim == 3 else 1.0)
         Mloc = _mass_loc(dim, h ** dim / (2 if dim == 2 else 6))
         return _assemble(_simplices(cells, dim), index, nv, Kloc, Mloc)[0]
@@ -270,6 +258,24 @@ def emi(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0
     idofs = np.concatenate([gam, nv + gam]) if both_sides else gam
     return BlockSystem(blocks, [nv, nv], idofs.astype(np.int32), 'emi_%dd' % dim,
                        dict(dim=dim, n=n, gamma=gamma, kappa1=kappa1, kappa2=kappa2, n_interface=ng))
+
+
+def emi_half(dim: int, n: int, top: bool):
+    """(lower-corner lattice coordinates of the half's cells, vertex -> dof
+    index) of Omega_1 (top, x_d > 1/2) or Omega_2: dofs numbered by layer
+    distance from Gamma, then lattice order (problems.emi)."""
+    m = n // 2
+    grids = np.meshgrid(*[np.arange(s) for s in [n] * (dim - 1) + [m]], indexing='ij')
+    cells = np.stack([g.ravel() for g in grids], axis=1).astype(np.int64)
+    cells[:, dim - 1] += m if top else 0         # global lattice layer of the cell's lower corner
+
+    def index(v):
+        layer = v[:, dim - 1] - m if top else m - v[:, dim - 1]
+        idx = layer
+        for d in range(dim - 2, -1, -1):
+            idx = idx * (n + 1) + v[:, d]
+        return idx
+    return cells, index
 
 
 def _assemble_simplices_flat(ids, nv, Mloc):

@@ -49,3 +49,21 @@ def test_mms_rejects_bad_arguments(lib_built):
         problems.bidomain_mms_rhs(4, 8, 1.0)
     with pytest.raises(ValueError):
         problems.bidomain_mms_errors(2, 8, np.zeros(5), 1.0)
+
+
+@pytest.mark.parametrize('dim,ns,gamma,lo', [(2, (16, 32, 64), 1.0, 0.98), (2, (16, 32, 64), 1e6, 0.98),
+                                              (3, (4, 8, 16), 5.0, 0.9)])
+def test_emi_mms_h1_rate_is_one(lib_built, dim, ns, gamma, lo):
+    """EMI manufactured solution (src/emi_2d.py:8-128: interface terms g_r, g_n,
+    full flux on the sides, Dirichlet on the outer faces): H1 rate ~1 with
+    direct solves of problems.emi -- a sign or normal error would stall it."""
+    from metric_amg_examples_amd import mms, problems
+    errs = []
+    for n in ns:
+        s = problems.emi(dim, n, gamma)
+        b = np.concatenate(mms.emi_mms_rhs(dim, n, gamma))
+        x = spla.spsolve(s.scipy().tocsc(), b)
+        errs.append(mms.emi_mms_errors(dim, n, x, gamma))
+    errs = np.array(errs)
+    rates = np.log(errs[1:] / errs[:-1]) / np.log(0.5)
+    assert np.all(rates[-1] > lo) and np.all(rates[-1] < 1.1), rates
