@@ -5,6 +5,7 @@ Reference: /root/reference/src/utils.py
   get_hazmath_amg_precond(A, W, bcs, parameters, ...)         :15-42  plain (non-metric) AMG
   get_hazmath_metric_precond(A, W, bcs, parameters, idofs)    :45-53  R^T Minv R on a block system
   get_hazmath_metric_precond_mono(A, W, bcs, parameters, idofs) :56-90 metricAMG on the monolithic CSR
+  solve_haznics(A, b, W, interface_dofs)                    :95-132 the whole solve in the library
 ``ii_convert`` (fenics_ii) becomes ``to_monolithic``; ``ReductionOperator``
 maps a block vector [x0, x1] onto the monolithic vector (concatenation) and
 its transpose splits it back, so ``R.T * Minv * R`` applies the monolithic
@@ -120,6 +121,31 @@ def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs
     params = dict(P.parameters_metric_mi355x) if parameters is None else dict(parameters)
     params['Schwarz_levels'] = 0
     return MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
+
+
+def solve_haznics(A, b, W, interface_dofs=None, parameters=None, tolerance=1e-8, maxiter=500):
+    """The whole solve in the library (src/utils.py:95-132: haznics'
+    fenics_metric_amg_solver_dcsr on the monolithic matrix): metric AMG seeded
+    at interface_dofs + PCG, both on the device.  HAZmath's solver reads its
+    own defaults, which are not in the reference tree; here ``parameters``
+    (default: the GPU profile) and the drivers' CG tolerance apply.
+    Returns (niters, [x0, x1], solve seconds) -- x split by W like the
+    reference's ii_Function."""
+    import time
+    from .krylov import ConjGrad
+    AA = to_monolithic(A)
+    sizes = _sizes(W)
+    t0 = time.time()
+    B = get_hazmath_metric_precond_mono(AA, sizes, parameters=parameters, interface_dofs=interface_dofs,
+                                        num_functions=2 if len(sizes) == 2 and sizes[0] == sizes[1] else 1)
+    cg = ConjGrad(AA, precond=B, tolerance=tolerance, maxiter=maxiter)   # same A: device PCG
+    bb = np.concatenate([np.asarray(v, np.float64) for v in b]) if isinstance(b, (list, tuple)) \
+        else np.asarray(b, np.float64)
+    x = cg * bb
+    x = x.cpu().numpy() if hasattr(x, 'cpu') else np.asarray(x)
+    dt = time.time() - t0
+    offs = np.cumsum([0] + list(sizes))
+    return len(cg.residuals) - 1, [x[offs[i]:offs[i + 1]] for i in range(len(sizes))], dt
 
 
 class BlockDiagLU:

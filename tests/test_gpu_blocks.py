@@ -150,6 +150,11 @@ def test_drivers_write_reference_iters_schema(lib_built, tmp_path):
     xd = spla.spsolve(s.scipy().tocsc(), problems.bidomain_mms_rhs(2, 64, 1e6))
     ed = problems.bidomain_mms_errors(2, 64, xd, 1e6)
     assert np.allclose([last[2], last[4]], ed, rtol=1e-6, atol=0)
+    # -precond metric_hazmath: the whole solve in the library (solve_haznics), the same
+    # preconditioner and CG as metric_mono here, so the same iteration count
+    hz = drivers.bidomain(['-nrefs', '1', '-gamma', '1e6', '-precond', 'metric_hazmath',
+                           '-results', str(tmp_path)], 2)
+    assert hz[0][1] == rows[0][1] and hz[0][2] == -1
     rows = drivers.emi(['-nrefs', '1', '-gamma', '1e4', '-results', str(tmp_path)], 3)
     assert rows[0][1] < 80
     rows = drivers.bidomain(['-nrefs', '1', '-gamma', '1e2', '-precond', 'metric',
