@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Profile the reference family (UA + HEM + W-cycle + multicolour SGS + coarse
+scaling) on one GPU: level sizes, colours per level and the apply's launch
+count / time, for rocprofv3 --kernel-trace --stats.
+
+    python bench/prof_ref_family.py [--nrefs 5] [--reps 5] [--coarse-dof 100]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--nrefs', type=int, default=5)
+    ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--coarse-dof', type=int, default=100)
+    args = ap.parse_args()
+    import torch
+    import metric_amg_examples_amd as M
+    n = M.problems.finest_n(3, args.nrefs)
+    s = M.problems.bidomain(3, n, 1e6)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu', AMG_type=1, aggregation_type=5,
+                    cycle_type=2, smoother=11, coarse_scaling=1, Schwarz_type=3, coarse_dof=args.coarse_dof,
+                    print_level=1)
+    print('levels', B.num_levels, flush=True)
+    r = torch.as_tensor(M.problems.seeded_rhs(s.N)).cuda()
+    z = torch.zeros_like(r)
+    B.apply_device(r, z)
+    torch.cuda.synchronize()
+    t = time.time()
+    for _ in range(args.reps):
+        B.apply_device(r, z)
+    torch.cuda.synchronize()
+    print('ms/apply %.3f' % ((time.time() - t) / args.reps * 1e3), flush=True)
+
+
+if __name__ == '__main__':
+    main()
