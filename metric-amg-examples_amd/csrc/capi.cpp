@@ -336,33 +336,40 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   // every rank builds the same hierarchy: on its own GPU when the profile is
   // the GPU setup's (bitwise equal to the host setup), else on the host
   rc = MAMG_ERR_UNSUPPORTED;
+  mamg::GHier G;
+  mamg::DevMat dA;
+  bool on_device = false;   // rank-local operators built from G in HBM
   if (params->num_functions == 2 && params->node_block_smoother &&
       (params->AMG_type == MAMG_UA_AMG || params->sa_block_diag)) {
-    mamg::GHier G;
     G.device = params->device;
-    mamg::DevMat dA;
     mamg::dev_prereserve(params->device, v.nnz(), nranks);   // rank-local layout memory first
     rc = mamg::upload_a0(v, &G, &dA, &err);
     lap("A0 upload");
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
     lap("GPU setup");
-    // each rank downloads only the rows it keeps, ghost lists computed on the
-    // GPU (MAMG_DIST_FULL_DOWNLOAD=1: the whole hierarchy, ghosts on the host)
-    const char* full = std::getenv("MAMG_DIST_FULL_DOWNLOAD");
-    if (full && std::atoi(full)) {
-      if (!rc) rc = mamg::ghier_download(G, v, &H, &err);
-    } else if (!rc) {
+    // default: ghost lists marked on the GPU, the rank's operators cut out of
+    // G in HBM.  MAMG_DIST_FULL_DOWNLOAD=1: the whole hierarchy downloaded and
+    // planned on the host; =2: the rank's rows downloaded, planned on the host
+    // (both bitwise the default; tests)
+    const char* e = std::getenv("MAMG_DIST_FULL_DOWNLOAD");
+    const int mode = e ? std::atoi(e) : 0;
+    if (rc) {
+    } else if (mode == 1) {
+      rc = mamg::ghier_download(G, v, &H, &err);
+    } else {
       rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, params->post_fusion != 0, &H,
-                                     &ghosts, &err);
+                                     &ghosts, &err, mode == 2);
       pre = !rc;
+      on_device = !rc && mode != 2;
     }
-    lap("hierarchy download");
+    lap(on_device ? "ghost lists" : "hierarchy download");
     if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
   if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
-  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err, pre ? &ghosts : nullptr);
+  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err, pre ? &ghosts : nullptr,
+                         on_device ? &G : nullptr, on_device ? &dA : nullptr);
   lap("plan + rank-local upload");
   mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }

@@ -38,10 +38,13 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
 // multi-GPU (device.hip, second half)
 struct DistHandle;
 int dist_get_unique_id(void* id, std::string* err);
-// ghosts: precomputed ghost lists (ghier_download_rank), else nullptr
+// ghosts: precomputed ghost lists (ghier_download_rank), else nullptr; G / A0d:
+// build the rank-local operators on the device from this GPU hierarchy (H then
+// holds only level sizes and the coarsest inverse)
 int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
                 const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
-                const std::vector<std::vector<std::vector<int64_t>>>* ghosts = nullptr);
+                const std::vector<std::vector<std::vector<int64_t>>>* ghosts = nullptr,
+                const GHier* G = nullptr, const DevMat* A0d = nullptr);
 void dist_destroy(DistHandle* h);
 void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
 double dist_apply_bytes(const DistHandle* h);

@@ -1351,6 +1351,7 @@ __global__ __launch_bounds__(256) void kmerge_kernel(int64_t nr, const int64_t* 
                                                      const int64_t* __restrict__ qp, const int32_t* __restrict__ qc,
                                                      const dv4* __restrict__ qv, const dv4* __restrict__ W,
                                                      int64_t* kp, int32_t* __restrict__ kc, dv4* __restrict__ kv) {
+#pragma clang fp contract(off)   // the host's kmerge_rows (dist.cpp, -ffp-contract=off) bit for bit
   const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (I >= nr) return;
   int64_t a = pp[I], ae = pp[I + 1], b = qp[I], be = qp[I + 1];
@@ -3489,9 +3490,301 @@ int dist_get_unique_id(void* id, std::string* err) {
   return MAMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Rank-local operators built in HBM from the GPU hierarchy (mamg_setup_dist's
+// default): the device restatement of build_dist_plan's conversions, so no
+// matrix of the hierarchy crosses PCIe.  Row slices are gathered from the
+// field-major CSRs, converted by the single-GPU csr2bsr kernel, and their
+// columns renumbered [owned | ghost] (owned first, each part in global order:
+// dist.cpp remap_cols); K by kmerge_kernel, the partial restriction from R's
+// rows (R = P^T exactly, so its blocks are transpose_bsr's).  Bitwise the
+// host plan's operators (tests/test_gpu_dist.py::test_rank_slice_download_bitwise).
+// ---------------------------------------------------------------------------
+namespace {
+
+// rows f m + i of the gathered CSR = rows f nvr + row(i) of M, row(i) =
+// rows[i] or r0 + i
+__global__ __launch_bounds__(256) void rowlen_gather_kernel(int64_t m, int64_t nvr, const int64_t* __restrict__ rows,
+                                                            int64_t r0, const int64_t* __restrict__ ptr,
+                                                            int64_t* __restrict__ len) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * m) return;
+  const int64_t f = i / m, k = i - f * m;
+  const int64_t src = f * nvr + (rows ? rows[k] : r0 + k);
+  len[i + 1] = ptr[src + 1] - ptr[src];
+}
+
+__global__ __launch_bounds__(256) void rowcopy_gather_kernel(int64_t m, int64_t nvr, const int64_t* __restrict__ rows,
+                                                             int64_t r0, const int64_t* __restrict__ ptr,
+                                                             const int32_t* __restrict__ col,
+                                                             const double* __restrict__ val,
+                                                             const int64_t* __restrict__ optr,
+                                                             int32_t* __restrict__ ocol, double* __restrict__ oval) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * m) return;
+  const int64_t f = i / m, k = i - f * m;
+  const int64_t src = f * nvr + (rows ? rows[k] : r0 + k);
+  int64_t o = optr[i];
+  for (int64_t q = ptr[src]; q < ptr[src + 1]; ++q, ++o) {
+    ocol[o] = col[q];
+    oval[o] = val[q];
+  }
+}
+
+// node columns -> local [owned | ghost] numbering: owned blocks first, then
+// ghosts, each in the row's (global) order
+__global__ __launch_bounds__(256) void map_part_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, const dv4* __restrict__ val,
+                                                       const int32_t* __restrict__ map, int32_t nown,
+                                                       int32_t* __restrict__ ocol, dv4* __restrict__ oval) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t o = ptr[I];
+  for (int part = 0; part < 2; ++part)
+    for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+      const int32_t c = map[col[k]];
+      if ((c < nown) == (part == 0)) { ocol[o] = c; oval[o] = val[k]; ++o; }
+    }
+}
+
+// keep the blocks whose column lies in [w0, w1), renumbered from w0
+__global__ __launch_bounds__(256) void window_len_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col, int64_t w0, int64_t w1,
+                                                         int64_t* __restrict__ len) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t c = 0;
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) c += col[k] >= w0 && col[k] < w1;
+  len[I + 1] = c;
+}
+
+__global__ __launch_bounds__(256) void window_fill_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const dv4* __restrict__ val, int64_t w0, int64_t w1,
+                                                          const int64_t* __restrict__ optr,
+                                                          int32_t* __restrict__ ocol, dv4* __restrict__ oval) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  int64_t o = optr[I];
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k)
+    if (col[k] >= w0 && col[k] < w1) { ocol[o] = (int32_t)(col[k] - w0); oval[o] = val[k]; ++o; }
+}
+
+__global__ __launch_bounds__(256) void map_fill_kernel(int64_t n, int64_t first, int32_t base,
+                                                       const int64_t* __restrict__ ids, int32_t* __restrict__ map) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  map[ids ? ids[k] : first + k] = base + (int32_t)k;
+}
+
+__global__ __launch_bounds__(256) void ghost_row_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ col, int32_t nown,
+                                                        uint8_t* __restrict__ flag) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  uint8_t g = 0;
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) g |= col[k] >= nown;
+  flag[I] = g;
+}
+
+// a node split by seed blocks keeps the two diagonal entries of its block
+__global__ __launch_bounds__(256) void unjoin_kernel(int64_t n, const uint8_t* __restrict__ joined, dv4* W) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < n && !joined[I]) { W[I].y = 0.0; W[I].z = 0.0; }
+}
+
+// rows of a field-major CSR (node rows r0 + i, or rows[i]) as a BSR2 with
+// global node columns
+int dev_rows_to_bsr(TmpPool* T, const DevMat& M, int64_t nvr, int64_t nvc, int64_t m, const int64_t* rows,
+                    int64_t r0, TBsr* B, std::string* err) {
+  int rc;
+  DevMat S;
+  S.n = 2 * m;
+  S.m = M.m;
+  if ((rc = T->alloc(&S.ptr, 2 * m + 1, err))) return rc;
+  HIPCHK(hipMemset(S.ptr, 0, sizeof(int64_t)));
+  if (m) rowlen_gather_kernel<<<nblocks(2 * m), 256>>>(m, nvr, rows, r0, M.ptr, S.ptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(S.ptr, S.ptr, 2 * m + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&S.nnz, S.ptr + 2 * m, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = T->alloc(&S.col, S.nnz, err))) return rc;
+  if ((rc = T->alloc(&S.val, S.nnz, err))) return rc;
+  if (m) rowcopy_gather_kernel<<<nblocks(2 * m), 256>>>(m, nvr, rows, r0, M.ptr, M.col, M.val, S.ptr, S.col, S.val);
+  HIPCHK(hipGetLastError());
+  return dev_csr_to_bsr(T, S, m, nvc, B, err);
+}
+
+// column map of a distributed level: owned J -> J - o0, ghost g_k -> nloc + k
+int dev_col_map(TmpPool* T, const DistLevel& L, int32_t** map, std::string* err) {
+  int rc;
+  if ((rc = T->alloc(map, L.nv, err))) return rc;
+  HIPCHK(hipMemset(*map, 0xff, L.nv * sizeof(int32_t)));
+  if (L.nloc) map_fill_kernel<<<nblocks(L.nloc), 256>>>(L.nloc, L.o0, 0, nullptr, *map);
+  const int64_t ng = (int64_t)L.ghosts.size();
+  if (ng) {
+    int64_t* g = nullptr;
+    if ((rc = T->alloc(&g, ng, err))) return rc;
+    HIPCHK(hipMemcpy(g, L.ghosts.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice));
+    map_fill_kernel<<<nblocks(ng), 256>>>(ng, 0, (int32_t)L.nloc, g, *map);
+  }
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+// BSR2 columns renumbered by map, [owned | ghost] order; nc = local columns
+int dev_map_cols(TmpPool* T, const TBsr& B, const int32_t* map, int64_t nown, int64_t nc, TBsr* O,
+                 std::string* err) {
+  int rc;
+  *O = B;
+  O->nc = nc;
+  if ((rc = T->alloc(&O->col, B.nb, err))) return rc;
+  if ((rc = T->alloc(&O->val, B.nb, err))) return rc;
+  if (B.nr) map_part_kernel<<<nblocks(B.nr), 256>>>(B.nr, B.ptr, B.col, B.val, map, (int32_t)nown, O->col, O->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+int dev_window_cols(TmpPool* T, const TBsr& B, int64_t w0, int64_t w1, TBsr* O, std::string* err) {
+  int rc;
+  O->nr = B.nr; O->nc = w1 - w0; O->merged = false;
+  if ((rc = T->alloc(&O->ptr, B.nr + 1, err))) return rc;
+  HIPCHK(hipMemset(O->ptr, 0, sizeof(int64_t)));
+  if (B.nr) window_len_kernel<<<nblocks(B.nr), 256>>>(B.nr, B.ptr, B.col, w0, w1, O->ptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(O->ptr, O->ptr, B.nr + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&O->nb, O->ptr + B.nr, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = T->alloc(&O->col, O->nb, err))) return rc;
+  if ((rc = T->alloc(&O->val, O->nb, err))) return rc;
+  if (B.nr) window_fill_kernel<<<nblocks(B.nr), 256>>>(B.nr, B.ptr, B.col, B.val, w0, w1, O->ptr, O->col, O->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
+// level l's A_loc (+ overlap window, band schedule), K / [P | AP] / P, R_loc
+// and W from the GPU hierarchy (the operator block of dist_upload)
+int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPlan& plan, int l, double kw,
+                 std::string* err) {
+  int rc;
+  const DistLevel& P = plan.levels[l];
+  const GLevel& g = G.levels[l];
+  DDLevel& D = h->L[l];
+  const int64_t nv = P.nv, nloc = P.nloc, nc = nloc + (int64_t)P.ghosts.size();
+  TmpPool T;
+  int32_t* map = nullptr;
+  if (!P.replicated && (rc = dev_col_map(&T, P, &map, err))) return rc;
+  // A_loc
+  {
+    TBsr raw, tA;
+    const DevMat& Am = l == 0 ? A0d : g.A;
+    if ((rc = dev_rows_to_bsr(&T, Am, nv, nv, nloc, nullptr, P.o0, &raw, err))) return rc;
+    if (P.replicated) tA = raw;
+    else if ((rc = dev_map_cols(&T, raw, map, nloc, nc, &tA, err))) return rc;
+    if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
+      uint8_t* fl = nullptr;
+      if ((rc = T.alloc(&fl, nloc, err))) return rc;
+      if (nloc) ghost_row_kernel<<<nblocks(nloc), 256>>>(nloc, tA.ptr, tA.col, (int32_t)nloc, fl);
+      HIPCHK(hipGetLastError());
+      std::vector<uint8_t> hf(nloc);
+      if (nloc) HIPCHK(hipMemcpy(hf.data(), fl, nloc, hipMemcpyDeviceToHost));
+      int64_t best0 = 0, best1 = 0, run0 = 0;
+      for (int64_t I = 0; I <= nloc; ++I)
+        if (I == nloc || hf[I]) {
+          if (I - run0 > best1 - best0) { best0 = run0; best1 = I; }
+          run0 = I + 1;
+        }
+      D.ib0 = best0;
+      D.ib1 = best1;
+    }
+    bool half = false;
+    if (l == 0 && g_half && tA.nr >= g_sell_min_rows && tA.nb > 0) {   // upload_half_or_bsr
+      int* bad = nullptr;
+      if ((rc = T.alloc(&bad, 1, err))) return rc;
+      HIPCHK(hipMemset(bad, 0, sizeof(int)));
+      sym_check_kernel<<<nblocks(tA.nb), 256>>>(tA.nb, tA.val, bad);
+      int hb = 1;
+      HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
+      if (hb == 0) {
+        D.A.nr = tA.nr; D.A.nc = tA.nc; D.A.nb = tA.nb;
+        D.A.lanes = pick_lanes_bsr(tA.nr, tA.nb);
+        D.A.sym = true;
+        if ((rc = try_half(h, &T, tA, &D.A, err))) return rc;
+        HIPCHK(hipDeviceSynchronize());
+        half = D.A.half;
+      }
+    }
+    if (!half && (rc = finalize_bsr(h, &T, tA, &D.A, 0, true, err))) return rc;
+    if (l == 0 && (rc = build_band_sched_range(h, &D.A, D.ib0, D.ib1, err))) return rc;
+  }
+  // W (node blocks of the owned rows)
+  if ((rc = ddalloc(h, &D.W, nloc, err))) return rc;
+  if (nloc) {
+    HIPCHK(hipMemcpy(D.W, reinterpret_cast<const dv4*>(g.W) + P.o0, nloc * sizeof(dv4), hipMemcpyDeviceToDevice));
+    if (g.joined) unjoin_kernel<<<nblocks(nloc), 256>>>(nloc, g.joined + P.o0, D.W);
+    HIPCHK(hipGetLastError());
+  }
+  // prolongation side (level l+1 numbering)
+  const DistLevel& C = plan.levels[l + 1];
+  const int64_t cnc = C.replicated ? C.nv : C.nloc + (int64_t)C.ghosts.size();
+  int32_t* cmap = nullptr;
+  if (!C.replicated && (rc = dev_col_map(&T, C, &cmap, err))) return rc;
+  auto rows_c = [&](const DevMat& M, TBsr* O) -> int {   // rows [o0, o1) of a fine x coarse CSR
+    TBsr raw;
+    int r = dev_rows_to_bsr(&T, M, nv, C.nv, nloc, nullptr, P.o0, &raw, err);
+    if (r) return r;
+    if (C.replicated) { *O = raw; return MAMG_OK; }
+    return dev_map_cols(&T, raw, cmap, C.nloc, cnc, O, err);
+  };
+  TBsr tP;
+  if ((rc = rows_c(g.P, &tP))) return rc;
+  if (plan.fuse) {
+    TBsr tAP, tK;
+    if ((rc = rows_c(g.AP, &tAP))) return rc;
+    if (plan.kpost) {
+      const double* Wk = reinterpret_cast<const double*>(D.W);
+      if (kw != 1.0 && nloc) {
+        double* q = nullptr;
+        if ((rc = T.alloc(&q, 4 * nloc, err))) return rc;
+        wscale_kernel<<<nblocks(4 * nloc), 256>>>(4 * nloc, kw, Wk, q);
+        HIPCHK(hipGetLastError());
+        Wk = q;
+      }
+      if ((rc = dev_kmerge(&T, tP, tAP, Wk, &tK, err))) return rc;
+      if ((rc = finalize_bsr(h, &T, tK, &D.K, 0, false, err))) return rc;
+    } else {
+      if ((rc = dev_merge_rows(&T, tP, tAP, &tK, err))) return rc;
+      if ((rc = finalize_bsr(h, &T, tK, &D.PA, 0, false, err))) return rc;
+    }
+  } else if ((rc = finalize_bsr(h, &T, tP, &D.P, 0, false, err))) {
+    return rc;
+  }
+  // partial restriction R_loc = P_loc^T: R's rows of the local coarse nodes
+  // ([owned | ghost], or all when replicated), columns in [o0, o1)
+  {
+    std::vector<int64_t> rows;
+    rows.reserve(cnc);
+    if (C.replicated) {
+      for (int64_t J = 0; J < C.nv; ++J) rows.push_back(J);
+    } else {
+      for (int64_t J = C.o0; J < C.o1; ++J) rows.push_back(J);
+      rows.insert(rows.end(), C.ghosts.begin(), C.ghosts.end());
+    }
+    int64_t* drows = nullptr;
+    if ((rc = T.alloc(&drows, cnc, err))) return rc;
+    if (cnc) HIPCHK(hipMemcpy(drows, rows.data(), cnc * sizeof(int64_t), hipMemcpyHostToDevice));
+    TBsr raw, tR;
+    if ((rc = dev_rows_to_bsr(&T, g.R, C.nv, nv, cnc, drows, 0, &raw, err))) return rc;
+    if ((rc = dev_window_cols(&T, raw, P.o0, P.o1, &tR, err))) return rc;
+    if ((rc = finalize_bsr(h, &T, tR, &D.R, 0, false, err))) return rc;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return MAMG_OK;
+}
+
+}  // namespace
+
 int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
                 const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
-                const GhostLists* ghosts) {
+                const GhostLists* ghosts, const GHier* G, const DevMat* A0d) {
   if (p.cycle_type != MAMG_V_CYCLE || p.maxit != 1 || p.presmooth_iter != 1 || p.postsmooth_iter != 1) {
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
@@ -3505,8 +3798,13 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   const int pm = poly_weights(p, pw);
   DistPlan plan;
   const auto tp0 = std::chrono::steady_clock::now();
-  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, p.post_fusion != 0, &plan, err, g_post_k != 0,
-                           p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0, ghosts);
+  const double kw = p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0;
+  bool fuse = p.post_fusion != 0;
+  if (G)                   // operators from the GPU hierarchy: fusion needs its A P on every level
+    for (size_t l = 0; l + 1 < G->levels.size() && fuse; ++l)
+      if (!G->levels[l].coarsest && G->levels[l].AP.n != G->levels[l].n) fuse = false;
+  int rc = build_dist_plan(H, A0, rank, nranks, rep_nodes, fuse, &plan, err, g_post_k != 0, kw, ghosts,
+                           G != nullptr);
   if (rc) return rc;
   if (p.print_level >= 2)
     std::fprintf(stderr, "[mamg] rank %d/%d setup:   of which host plan    %.3f s\n", rank, nranks,
@@ -3553,6 +3851,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
         for (int64_t j = 0; j < n; ++j) Ap[pos(i) * n + pos(j)] = hl.Ainv[i * n + j];
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
+    } else if (G) {
+      if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, err))) return rc;
     } else {
       if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
         int64_t best0 = 0, best1 = 0, run0 = 0;
@@ -3584,6 +3884,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = upload_bsr(h.get(), P.Rp, &D.R, 0, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.W, D.nloc, err))) return rc;
       HIPCHK(hipMemcpy(D.W, P.W.data(), 4 * D.nloc * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (!D.coarsest) {
       if (p.smoother == MAMG_SMOOTHER_POLY) {   // w_k W as on one GPU (poly_scaled)
         for (int k = 0; k < pm; ++k) {
           dv4* q = nullptr;

@@ -160,7 +160,7 @@ void dist_ranges(const std::vector<int64_t>& nv, const std::vector<char>& coarse
 
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
                     bool fuse, DistPlan* plan, std::string* err, bool kpost, double kw,
-                    const GhostLists* pre) {
+                    const GhostLists* pre, bool meta_only) {
   // K = P - (kw W) AP: the first post-smoothing step's smoother (device.hip
   // poly_scaled: kw W elementwise, then the merge; bitwise the single-GPU K)
   auto kmerge_kw = [kw](const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K) {
@@ -173,10 +173,13 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
   if (H.params.num_functions != 2) { *err = "multi-GPU path needs num_functions == 2 (BSR2 layout)"; return MAMG_ERR_UNSUPPORTED; }
   const int nl = (int)H.levels.size();
   if (nl < 2) { *err = "multi-GPU path needs at least two levels"; return MAMG_ERR_UNSUPPORTED; }
-  for (int l = 0; l + 1 < nl && fuse; ++l)
+  if (meta_only && !pre) { *err = "meta-only plan needs precomputed ghost lists"; return MAMG_ERR_ARG; }
+  for (int l = 0; l + 1 < nl && fuse && !meta_only; ++l)
     if (H.levels[l].AP.n != H.levels[l].n) fuse = false;   // A P not kept by the setup
   plan->rank = rank;
   plan->nranks = nranks;
+  plan->fuse = fuse;
+  plan->kpost = kpost;
   plan->levels.assign(nl, DistLevel());
   auto Aview = [&](int l) { return l == 0 ? A0 : H.A(l); };
   {
@@ -192,7 +195,7 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
       D.coarsest = hl.coarsest;
       D.replicated = rep[l];
       D.own = own[l];
-      if (!hl.coarsest && hl.WB.n == 0 && hl.Wn.empty()) {
+      if (!meta_only && !hl.coarsest && hl.WB.n == 0 && hl.Wn.empty()) {
         *err = "multi-GPU path needs node-block smoothers on every level";
         return MAMG_ERR_UNSUPPORTED;
       }
@@ -226,15 +229,23 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
   for (int l = 0; l < nl; ++l) {
     DistLevel& D = plan->levels[l];
     const HostLevel& hl = H.levels[l];
+    if (meta_only && D.replicated) {   // ranges and lists only
+      D.o0 = 0; D.o1 = D.nv; D.nloc = D.nv;
+      D.ghost_off.assign(nranks + 1, 0);
+      D.send_off.assign(nranks + 1, 0);
+      continue;
+    }
     // smoother blocks: Wfull holds nodes [w0, w0 + Wfull.size()/4)
     std::vector<double> Wfull;
     int64_t w0 = 0;
-    if (!hl.Wn.empty()) {
-      Wfull = hl.Wn;
-      w0 = hl.wn0;
-    } else if (!hl.coarsest && !node_blocks_of(hl.WB.view(), D.nv, &Wfull)) {
-      *err = "multi-GPU path needs node-block smoothers on every level";
-      return MAMG_ERR_UNSUPPORTED;
+    if (!meta_only) {
+      if (!hl.Wn.empty()) {
+        Wfull = hl.Wn;
+        w0 = hl.wn0;
+      } else if (!hl.coarsest && !node_blocks_of(hl.WB.view(), D.nv, &Wfull)) {
+        *err = "multi-GPU path needs node-block smoothers on every level";
+        return MAMG_ERR_UNSUPPORTED;
+      }
     }
     const int64_t w1 = w0 + (int64_t)Wfull.size() / 4;
     if (D.replicated) {
@@ -264,6 +275,7 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
           if (g >= D.o0 && g < D.o1) D.send_idx.push_back(g - D.o0);
       D.send_off[q + 1] = (int64_t)D.send_idx.size();
     }
+    if (meta_only) continue;
     const int64_t o0 = D.o0, o1 = D.o1, nloc = D.nloc;
     const std::vector<int64_t>& gl = D.ghosts;
     to_bsr2_rows(Aview(l), D.nv, D.nv, o0, o1, &D.A);
@@ -278,7 +290,7 @@ int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks,
     D.W.assign(Wfull.begin() + 4 * (o0 - w0), Wfull.begin() + 4 * (o1 - w0));
   }
   // P_loc / Rp_loc (need the level l+1 numbering)
-  for (int l = 0; l + 1 < nl; ++l) {
+  for (int l = 0; l + 1 < nl && !meta_only; ++l) {
     DistLevel& D = plan->levels[l];
     const DistLevel& C = plan->levels[l + 1];
     const CsrView Pv = H.levels[l].P.view();

@@ -27,6 +27,7 @@ struct DistLevel {
 
 struct DistPlan {
   int rank = 0, nranks = 1;
+  bool fuse = false, kpost = true;   // post fusion taken; through K (else [P | AP])
   std::vector<DistLevel> levels;
 };
 
@@ -46,9 +47,12 @@ void dist_ranges(const std::vector<int64_t>& nv, const std::vector<char>& coarse
 // pre: ghost lists computed elsewhere (ghier_download_rank: then H holds only
 // the rows this rank reads, and node-major smoother slices in HostLevel::Wn);
 // nullptr = computed here from the full hierarchy.
+// meta_only: ranges, ghosts and send lists only (the operators are built on
+// the device from the GPU hierarchy, device.hip dev_rank_ops); H then needs
+// only each level's n / coarsest (and the coarsest Ainv), `pre` is required.
 int build_dist_plan(const Hierarchy& H, const CsrView& A0, int rank, int nranks, int64_t rep_nodes,
                     bool fuse, DistPlan* plan, std::string* err, bool kpost = true, double kw = 1.0,
-                    const GhostLists* pre = nullptr);
+                    const GhostLists* pre = nullptr, bool meta_only = false);
 // K rows = P rows - W_I (AP rows), block-column union (both sorted, same columns)
 void kmerge_rows(const HBsr& P, const HBsr& AP, const std::vector<double>& W, HBsr* K);
 

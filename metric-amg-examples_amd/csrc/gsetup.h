@@ -53,10 +53,12 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
 // multi-GPU: download only what rank `rank` of `nranks` reads (its node rows
 // of every distributed level, replicated levels whole, no R / aggregates) and
 // compute the ghost lists on the device (build_dist_plan's `pre`); A0d is the
-// device copy of the host A0
+// device copy of the host A0.  matrices = false: level sizes, the coarsest
+// inverse and the ghost lists only (the operators are then built on the device)
 int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H,
-                        std::vector<std::vector<std::vector<int64_t>>>* ghosts, std::string* err);
+                        std::vector<std::vector<std::vector<int64_t>>>* ghosts, std::string* err,
+                        bool matrices = true);
 // host CSR -> HBM, buffers owned by G (G->device selects the GPU)
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err);
 

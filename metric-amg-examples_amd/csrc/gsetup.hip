@@ -1570,7 +1570,7 @@ struct DevScratch {             // plain hipMalloc buffer, freed on scope exit
 
 int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H, GhostLists* ghosts,
-                        std::string* err) {
+                        std::string* err, bool matrices) {
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   H->params = G.params;
   H->A0 = A0;
@@ -1671,12 +1671,13 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
     h.coarsest = g.coarsest;
     const bool all = rep[l];
     const int64_t o0 = own[l][rank], o1 = own[l][rank + 1];
-    if (l > 0) RCHK(dl(g.A, all, o0, o1, &h.A));
+    if (l > 0 && matrices) RCHK(dl(g.A, all, o0, o1, &h.A));
     if (g.coarsest) {
       h.Ainv.resize(g.n * g.n);
       RCHK(to_host(h.Ainv.data(), g.Ainv, g.n * g.n, err));
       break;
     }
+    if (!matrices) continue;
     RCHK(dl(g.P, all, o0, o1, &h.P));
     if (fuse) RCHK(dl(g.AP, all, o0, o1, &h.AP));
     h.nagg = g.nagg;

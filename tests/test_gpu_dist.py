@@ -80,14 +80,16 @@ def test_virtual_ranks_poly_and_emi(lib_built, problem, kw, P):
 
 
 @pytest.mark.parametrize('case,P,rep', [('bidomain', 3, 100), ('bidomain', 8, 1), ('unfused', 2, 100),
-                                         ('emi_poly', 4, 100), ('bidomain2d', 5, 10)])
+                                         ('emi_poly', 4, 100), ('bidomain2d', 5, 10), ('sell', 3, 100),
+                                         ('merged', 2, 100)])
 def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
-    """Each rank downloads only its rows of the GPU hierarchy, with the ghost
-    lists marked on the device (gsetup.hip ghier_download_rank): the same
-    rank-local operators as the whole-hierarchy download with host ghost
-    lists -- bitwise equal applies and byte counts, also with every level
-    above the coarsest distributed (rep_nodes 1, 8 ranks), without post
-    fusion and with the seed-split EMI smoother."""
+    """The rank-local operators built in HBM from the GPU hierarchy (default;
+    ghost lists marked on the device, device.hip dev_rank_ops), from the
+    rank's downloaded rows planned on the host, and from the whole
+    downloaded hierarchy planned on the host: bitwise equal applies and byte
+    counts, also with every level above the coarsest distributed (rep_nodes
+    1, 8 ranks), without post fusion, with the seed-split EMI smoother and
+    with SELL / [P | AP] storage forced."""
     import torch
     import metric_amg_examples_amd as M
     kw = {}
@@ -100,9 +102,13 @@ def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
         s = M.problems.bidomain(3, 16, 1e6)
     if case == 'unfused':
         kw['post_fusion'] = 0
+    elif case == 'sell':
+        monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')     # SELL / half-symmetric rank-local A with ghosts
+    elif case == 'merged':
+        monkeypatch.setenv('MAMG_POST_K', '0')
     r = mo.seeded_rhs(s.N)
     out, nbytes = [], []
-    for full in ('1', '0'):
+    for full in ('1', '2', '0'):   # whole download + host plan, rank rows + host plan, built in HBM
         monkeypatch.setenv('MAMG_DIST_FULL_DOWNLOAD', full)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
                               num_functions=2, **kw) for p in range(P)]
@@ -114,9 +120,10 @@ def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
         nbytes.append([hh.apply_bytes for hh in hs])
         for hh in hs:
             hh.close()
-    for a, b in zip(out[0], out[1]):
-        assert np.array_equal(a, b)
-    assert nbytes[0] == nbytes[1]
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert np.array_equal(a, b)
+    assert nbytes[0] == nbytes[1] == nbytes[2]
 
 
 @pytest.mark.parametrize('mode', ['unfused', 'sell', 'nohalf', 'merged'])
