@@ -284,9 +284,16 @@ def main():
                                Schwarz_type=3)),
                          ('reference family, coarse_dof 2048 (dense solve instead of the launch-bound W bottom)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=3, coarse_dof=2048)),):
+                               Schwarz_type=3, coarse_dof=2048)),
+                         ('mi355x_patch: the reference\'s level-0 smoother (symmetric multiplicative Schwarz on '
+                          'the overlapping 1-ring node patches, SCHWARZ_PATCHES), node-block Jacobi below',
+                          dict(smoother=3, Schwarz_type=6)),
+                         ('reference family with its level-0 node-patch Schwarz: UA + parallel HEM + W-cycle + '
+                          'SGS + coarse scaling + SCHWARZ_PATCHES, coarse_dof 2048',
+                          dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
+                               Schwarz_type=6, coarse_dof=2048)),):
             if (kw['smoother'] == prof['smoother'] and kw.get('coarse_scaling', 0) == prof['coarse_scaling']
-                    and kw.get('aggregation_type', 2) == 2):
+                    and kw.get('aggregation_type', 2) == 2 and kw.get('Schwarz_type', 4) == prof['Schwarz_type']):
                 continue
             torch.cuda.synchronize(dev)
             t0 = time.time()

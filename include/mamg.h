@@ -65,8 +65,14 @@ enum {                                                   /* aggregation_type  */
 enum {                                                   /* Schwarz_type      */
   MAMG_SCHWARZ_FORWARD = 1, MAMG_SCHWARZ_BACKWARD = 2, MAMG_SCHWARZ_SYMMETRIC = 3,
   MAMG_SCHWARZ_BLOCK_JACOBI = 4, /* additive non-overlapping seed blocks (GPU) */
-  MAMG_SCHWARZ_ADDITIVE = 5      /* additive overlapping seed + maxlvl-ring blocks
+  MAMG_SCHWARZ_ADDITIVE = 5,     /* additive overlapping seed + maxlvl-ring blocks
                                     (sparse seed sets, e.g. 3D-1D; CSR layout) */
+  /* symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
+     (the reference's SCHWARZ_SYMMETRIC with Schwarz_maxlvl 1): one patch per
+     node = both fields of its closed neighbourhood, exact local solves, in a
+     distance-3 multicolour order; level 0, BSR2 layout, single GPU; needs a
+     seed dof on every node (the bidomain's idofs) */
+  MAMG_SCHWARZ_PATCHES = 6
 };
 enum { MAMG_OFF = 0, MAMG_ON = 1 };
 enum { MAMG_COARSE_DENSE = 32 };  /* coarse_solver: 32 (UMFPACK in HAZmath)  */

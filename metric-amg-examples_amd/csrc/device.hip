@@ -836,6 +836,238 @@ __global__ __launch_bounds__(256) void perm_len_kernel(int64_t nrp, const int32_
   gptr[i + 1] = I < 0 ? 0 : ptr[I + 1] - ptr[I];
 }
 
+// ---------------------------------------------------------------------------
+// Multiplicative node-patch Schwarz on level 0 (Schwarz_type PATCHES): the
+// reference's level-0 smoother, symmetric multiplicative Schwarz on one block
+// per seed = seed + its 1-ring (src/amg_parameters.py:83-87, src/utils.py:84)
+// with exact local solves.  With a seed on every node (the bidomain's u2
+// dofs, src/bidomain_3d.py:138) the block of node I is both fields of the
+// closed neighbourhood N[I] = row I of A_0's node pattern.  Parallel order:
+// patches coloured at distance 3 (two patch centres of one colour are >= 4
+// hops apart: no patch of a launch reads an x another one writes).
+// Oracle: mamg_oracle.Patches (colouring, inverses, sweep).
+// ---------------------------------------------------------------------------
+constexpr int PATCH_MAX_NODES = 16;
+constexpr int PATCH_WORDS = 4;          // 256 colours
+
+__device__ __forceinline__ uint64_t patch_key_dev(int64_t I) {
+  return ((uint64_t)hash32_dev((uint64_t)I, 0x5000) << 32) | (uint64_t)(uint32_t)I;
+}
+
+// k[I] = key(I) while I is uncoloured, else 0
+__global__ __launch_bounds__(256) void pkey_init_kernel(int64_t nr, const int16_t* __restrict__ c, uint64_t* __restrict__ k) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < nr) k[I] = c[I] < 0 ? patch_key_dev(I) : 0ull;
+}
+
+// out[I] = max of in over row I's node columns and I itself (one hop)
+__global__ __launch_bounds__(256) void pkey_max_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, const uint64_t* __restrict__ in,
+                                                       uint64_t* __restrict__ out) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  uint64_t m = in[I];
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+    const uint64_t v = in[col[k]];
+    m = v > m ? v : m;
+  }
+  out[I] = m;
+}
+
+// colour bit of every coloured node (256-bit, PATCH_WORDS words per node)
+__global__ __launch_bounds__(256) void pmask_init_kernel(int64_t nr, const int16_t* __restrict__ c, uint64_t* __restrict__ m) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  const int ci = c[I];
+#pragma unroll
+  for (int w = 0; w < PATCH_WORDS; ++w)
+    m[PATCH_WORDS * I + w] = (ci >= 0 && ci / 64 == w) ? (1ull << (ci % 64)) : 0ull;
+}
+
+// out[I] = OR of in over row I's node columns and I itself (one hop)
+__global__ __launch_bounds__(256) void pmask_or_kernel(int64_t nr, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, const uint64_t* __restrict__ in,
+                                                       uint64_t* __restrict__ out) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr) return;
+  uint64_t m[PATCH_WORDS];
+#pragma unroll
+  for (int w = 0; w < PATCH_WORDS; ++w) m[w] = in[PATCH_WORDS * I + w];
+  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+    const int64_t J = col[k];
+#pragma unroll
+    for (int w = 0; w < PATCH_WORDS; ++w) m[w] |= in[PATCH_WORDS * J + w];
+  }
+#pragma unroll
+  for (int w = 0; w < PATCH_WORDS; ++w) out[PATCH_WORDS * I + w] = m[w];
+}
+
+// one distance-3 Jones-Plassmann round (mamg_oracle.patch_colouring): an
+// uncoloured node whose key is the 3-hop maximum (k3) takes the lowest colour
+// absent from the 3-hop colour mask (m3); two winners are > 3 hops apart
+__global__ __launch_bounds__(256) void patch_assign_kernel(int64_t nr, int16_t* __restrict__ c,
+                                                           const uint64_t* __restrict__ k3, const uint64_t* __restrict__ m3,
+                                                           unsigned long long* nleft, int* toomany) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nr || c[I] >= 0) return;
+  if (k3[I] != patch_key_dev(I)) { atomicAdd(nleft, 1ull); return; }
+  int cc = -1;
+  for (int w = 0; w < PATCH_WORDS && cc < 0; ++w) {
+    const uint64_t m = m3[PATCH_WORDS * I + w];
+    if (~m) cc = 64 * w + __ffsll((long long)~m) - 1;
+  }
+  if (cc < 0) { *toomany = 1; cc = 0; }
+  c[I] = (int16_t)cc;
+}
+
+__global__ __launch_bounds__(256) void pcolour_count_kernel(int64_t nr, const int16_t* __restrict__ c,
+                                                            int32_t* __restrict__ ci, int64_t* __restrict__ iota,
+                                                            unsigned long long* cnt) {
+  __shared__ unsigned int hist[64 * PATCH_WORDS];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < nr) {
+    ci[I] = c[I];
+    iota[I] = I;
+    atomicAdd(&hist[c[I]], 1u);
+  }
+  __syncthreads();
+  if (hist[threadIdx.x]) atomicAdd(cnt + threadIdx.x, (unsigned long long)hist[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void patch_rowlen_kernel(int64_t nr, const int64_t* __restrict__ ptr, int* maxlen) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < nr) atomicMax(maxlen, (int)(ptr[I + 1] - ptr[I]));
+}
+
+__global__ __launch_bounds__(256) void i64_to_i32_kernel(int64_t n, const int64_t* __restrict__ a, int32_t* __restrict__ b) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) b[i] = (int32_t)a[i];
+}
+
+// column-packed upper triangle: U(i, j), i <= j, at j (j + 1) / 2 + i
+__device__ __forceinline__ int upk(int i, int j) { return i <= j ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j; }
+
+// Patch inverses, one wave per patch (4 per workgroup).  Lane j < 2d holds
+// column j of the augmented [A_p | I] (d = 2 m <= 32 rows in registers; local
+// dof i = 2 a + f, a = the node's position in row I, f = field).  Gauss-Jordan
+// without pivoting in mamg_oracle.batched_inverse's operation order (row k
+// divided by the pivot, then M_i -= M_ik M_k, no contraction); the packed
+// upper triangle of the inverse is stored (the oracle symmetrises the same).
+__global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_t* __restrict__ perm,
+                                                        const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                        const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
+                                                        int* bad) {
+#pragma clang fp contract(off)
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wv;
+  if (i >= np) return;
+  const int32_t I = perm[i];
+  const int64_t q0 = ptr[I];
+  const int m = (int)(ptr[I + 1] - q0);
+  const int d = 2 * m;
+  double M[2 * PATCH_MAX_NODES];
+#pragma unroll
+  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = 0.0;
+  if (lane < d) {
+    const int32_t Jb = col[q0 + (lane >> 1)];
+    const int g = lane & 1;
+#pragma unroll
+    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
+      if (a < m) {
+        const int32_t Ja = col[q0 + a];
+        int64_t lo = ptr[Ja], hi = ptr[Ja + 1];
+        while (lo < hi) {
+          const int64_t md = (lo + hi) >> 1;
+          if (col[md] < Jb) lo = md + 1; else hi = md;
+        }
+        if (lo < ptr[Ja + 1] && col[lo] == Jb) {
+          const dv4 v = val[lo];
+          M[2 * a] = g ? v.y : v.x;
+          M[2 * a + 1] = g ? v.w : v.z;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = (lane - d == r) ? 1.0 : 0.0;
+  }
+  for (int k = 0; k < d; ++k) {
+    double mk = 0.0;
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) mk = r == k ? M[r] : mk;
+    const double p = __shfl(mk, k);
+    if (!(p > 0.0)) { if (lane == 0) atomicOr(bad, 1); return; }
+    mk = mk / p;
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) {
+      const double f = __shfl(M[r], k);
+      const double t = f * mk;
+      M[r] = r == k ? mk : M[r] - t;
+    }
+  }
+  if (lane >= d && lane < 2 * d) {
+    const int jj = lane - d;
+    double* Up = U + i * ustride + jj * (jj + 1) / 2;
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r)
+      if (r <= jj) Up[r] = M[r];
+  }
+}
+
+// One colour of a patch sweep, one wave per patch (4 per workgroup), in place
+// on x (node-interleaved):  x|_p += Minv_p (b - A x)|_p.  The patch's node rows
+// are reduced by 4 lanes each (lanes 4a..4a+3 = node a); lane i < d then forms
+// delta_i = sum_j U(min, max) r_j and updates its own dof.  b has field stride
+// bs (the caller's [u1; u2] r on level 0).
+__global__ __launch_bounds__(256) void patch_kernel(int64_t c0, int64_t c1, const int32_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                    const dv4* __restrict__ val, const double* __restrict__ U,
+                                                    int64_t ustride, double* x, const double* __restrict__ b, int64_t bs) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = c0 + (int64_t)blockIdx.x * 4 + wv;
+  if (i >= c1) return;
+  const int32_t I = perm[i];
+  const int64_t q0 = ptr[I];
+  const int m = (int)(ptr[I + 1] - q0);
+  const int a = lane >> 2, q = lane & 3;
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  double s0 = 0.0, s1 = 0.0;
+  int32_t J = 0;
+  if (a < m) {
+    J = col[q0 + a];
+    const int64_t p1 = ptr[J + 1];
+    for (int64_t k = ptr[J] + q; k < p1; k += 4) {
+      const int32_t c = col[k];
+      const dv4 v = val[k];
+      const double2 xc = x2[c];
+      s0 += v.x * xc.x + v.y * xc.y;
+      s1 += v.z * xc.x + v.w * xc.y;
+    }
+  }
+  s0 += __shfl_xor(s0, 1);
+  s1 += __shfl_xor(s1, 1);
+  s0 += __shfl_xor(s0, 2);
+  s1 += __shfl_xor(s1, 2);
+  double r0 = 0.0, r1 = 0.0;
+  if (a < m) {
+    r0 = vget(b, bs, J, 0) - s0;
+    r1 = vget(b, bs, J, 1) - s1;
+  }
+  const double* Up = U + i * ustride;
+  const int li = lane < 2 * m ? lane : 0;
+  double delta = 0.0;
+  for (int jn = 0; jn < m; ++jn) {
+    const double a0 = __shfl(r0, 4 * jn), a1 = __shfl(r1, 4 * jn);
+    delta += Up[upk(li, 2 * jn)] * a0 + Up[upk(li, 2 * jn + 1)] * a1;
+  }
+  if (lane < 2 * m) {
+    const int64_t Ji = col[q0 + (lane >> 1)];
+    x[2 * Ji + (lane & 1)] += delta;
+  }
+}
+
 // 2x2 Gauss-Jordan without pivoting in mamg_oracle.batched_inverse's
 // operation order (no contraction), on node I's diagonal block; the
 // off-diagonals are dropped when I's two dofs are separate smoother blocks
@@ -1060,6 +1292,18 @@ struct DLevel {
   int32_t* gperm = nullptr;
   dv4* Gd = nullptr;
   std::vector<int64_t> gcs, gbk;     // colour row starts / block starts (+ end)
+  // level-0 node-patch Schwarz (Schwarz_type PATCHES): A_0 as plain BSR2 in
+  // node order (Sptr, Scol, Sval: the patch rows), the patch centres colour by
+  // colour (pperm), colour c = patches [pcs[c], pcs[c + 1]), the packed upper
+  // triangles of the patch inverses (pu, stride pus doubles per patch)
+  int64_t* Sptr = nullptr;
+  int32_t* Scol = nullptr;
+  dv4* Sval = nullptr;
+  int64_t Snb = 0;
+  int32_t* pperm = nullptr;
+  double* pu = nullptr;
+  int64_t pus = 0;
+  std::vector<int64_t> pcs;
   // coarse-grid correction scaling of the correction computed ON this level:
   // q = A_l e, partial sums of <b, e>, <q, e>
   double* q = nullptr;
@@ -1067,7 +1311,7 @@ struct DLevel {
 };
 
 enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7,
-              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11 };
+              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11, OP_PATCH = 12 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -1096,6 +1340,7 @@ struct Op {
   int64_t r0 = 0, r1 = -1;          // row range [r0, r1) (half-symmetric ops, GS colours; r1 < 0: all rows)
   const int32_t* perm = nullptr;    // GS: node of each permuted row
   double* part = nullptr;           // DOT2 / CSCALE partial sums
+  const struct DLevel* lev = nullptr;   // PATCH: the level's patch data
   double bytes = 0.0;
 };
 
@@ -2000,6 +2245,103 @@ int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLeve
   return MAMG_OK;
 }
 
+inline bool patch_schwarz(const mamg_params& p) {
+  return p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_PATCHES;
+}
+
+// Node-patch Schwarz data of level 0 from A_0's device BSR2 B: distance-3
+// colouring (rounds of three key-max and three mask-or hops, one 8-byte
+// readback each), patches sorted by colour (stable radix sort, ascending
+// centre within a colour), A_0 kept as plain BSR2 for the patch rows, and the
+// patch inverses (patch_inv_kernel).
+int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::string* err) {
+  int rc;
+  const int64_t nr = B.nr;
+  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 256 colours, [2] bad pivot, [3] max row length
+  unsigned long long* left = nullptr;
+  unsigned long long* cnt = nullptr;
+  if ((rc = T->alloc(&flags, 4, err))) return rc;
+  if ((rc = T->alloc(&left, 1, err))) return rc;
+  if ((rc = T->alloc(&cnt, 64 * PATCH_WORDS, err))) return rc;
+  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(hipMemset(cnt, 0, 64 * PATCH_WORDS * sizeof(unsigned long long)));
+  pattern_sym_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, flags);
+  patch_rowlen_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, flags + 3);
+  HIPCHK(hipGetLastError());
+  int hf[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[0]) { *err = "node patches: node pattern of level 0 not symmetric"; return MAMG_ERR_UNSUPPORTED; }
+  if (hf[3] > PATCH_MAX_NODES) {
+    *err = "node patches: a node has " + std::to_string(hf[3]) + " neighbours (at most " +
+           std::to_string(PATCH_MAX_NODES) + " nodes per patch)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  int16_t* c = nullptr;
+  uint64_t *k1 = nullptr, *k2 = nullptr, *m1 = nullptr, *m2 = nullptr;
+  if ((rc = T->alloc(&c, nr, err))) return rc;
+  if ((rc = T->alloc(&k1, nr, err))) return rc;
+  if ((rc = T->alloc(&k2, nr, err))) return rc;
+  if ((rc = T->alloc(&m1, PATCH_WORDS * nr, err))) return rc;
+  if ((rc = T->alloc(&m2, PATCH_WORDS * nr, err))) return rc;
+  HIPCHK(hipMemset(c, 0xff, nr * sizeof(int16_t)));
+  for (int round = 0;; ++round) {
+    unsigned long long nl = 0;
+    HIPCHK(hipMemset(left, 0, sizeof(unsigned long long)));
+    pkey_init_kernel<<<nblocks(nr), 256>>>(nr, c, k1);
+    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k1, k2);
+    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k2, k1);
+    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k1, k2);
+    pmask_init_kernel<<<nblocks(nr), 256>>>(nr, c, m1);
+    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m1, m2);
+    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m2, m1);
+    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m1, m2);
+    patch_assign_kernel<<<nblocks(nr), 256>>>(nr, c, k2, m2, left, flags + 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(&nl, left, sizeof(nl), hipMemcpyDeviceToHost));
+    if (nl == 0) break;
+    if (round > 100000) { *err = "node patches: colouring did not finish"; return MAMG_ERR_SETUP; }
+  }
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[1]) { *err = "node patches: more than 256 colours"; return MAMG_ERR_UNSUPPORTED; }
+  T->release(k1); T->release(k2); T->release(m1); T->release(m2);
+  int32_t *ci = nullptr, *cs = nullptr;
+  int64_t *iota = nullptr, *sorted = nullptr;
+  if ((rc = T->alloc(&ci, nr, err))) return rc;
+  if ((rc = T->alloc(&cs, nr, err))) return rc;
+  if ((rc = T->alloc(&iota, nr, err))) return rc;
+  if ((rc = T->alloc(&sorted, nr, err))) return rc;
+  pcolour_count_kernel<<<nblocks(nr), 256>>>(nr, c, ci, iota, cnt);
+  HIPCHK(hipGetLastError());
+  if ((rc = dsort_pairs_i32_i64(ci, cs, iota, sorted, nr, 8, nullptr, err))) return rc;
+  std::vector<unsigned long long> hc(64 * PATCH_WORDS);
+  HIPCHK(hipMemcpy(hc.data(), cnt, hc.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  int ncol = 0;
+  for (int k = 0; k < 64 * PATCH_WORDS; ++k)
+    if (hc[k]) ncol = k + 1;
+  D->pcs.assign(ncol + 1, 0);
+  for (int k = 0; k < ncol; ++k) D->pcs[k + 1] = D->pcs[k] + (int64_t)hc[k];
+  if ((rc = dalloc(h, &D->pperm, nr, err))) return rc;
+  i64_to_i32_kernel<<<nblocks(nr), 256>>>(nr, sorted, D->pperm);
+  HIPCHK(hipGetLastError());
+  for (void* q : {(void*)c, (void*)ci, (void*)cs, (void*)iota, (void*)sorted}) T->release(q);
+  // A_0's patch rows: plain BSR2 in node order
+  D->Snb = B.nb;
+  if ((rc = dalloc(h, &D->Sptr, nr + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->Scol, B.nb, err))) return rc;
+  if ((rc = dalloc(h, &D->Sval, B.nb, err))) return rc;
+  HIPCHK(hipMemcpy(D->Sptr, B.ptr, (nr + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->Scol, B.col, B.nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->Sval, B.val, B.nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+  const int64_t dmax = 2 * (int64_t)hf[3];
+  D->pus = dmax * (dmax + 1) / 2;
+  if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
+  patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Sval, D->pus, D->pu, flags + 2);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
+  return MAMG_OK;
+}
+
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
   DLevel& D = h->L[l];
   const mamg_params& p = h->p;
@@ -2020,8 +2362,11 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true,
                            l == 0)))
       return rc;
-    if (gs_smoother(p))
+    const bool patches = l == 0 && patch_schwarz(p);
+    if (gs_smoother(p) && !patches)
       if ((rc = build_gs(h, &T, B, S.W, l, &D, err))) return rc;
+    if (patches)
+      if ((rc = build_patches(h, &T, B, &D, err))) return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
   if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
@@ -2031,7 +2376,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = poly_scaled(h, S.W, 4 * nv, &wk, err))) return rc;
     for (double* q : wk) D.Wk.push_back(reinterpret_cast<dv4*>(q));
   }
-  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p)) {
+  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p) && !(l == 0 && patch_schwarz(p))) {
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
@@ -2216,6 +2561,27 @@ Op gs_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int cls
   return o;
 }
 
+// one colour of a node-patch sweep: per patch its packed inverse, its node
+// rows (blocks + pointers), b and x read/write for its dofs, the gathered x
+Op patch_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int cls) {
+  Op o;
+  o.kind = OP_PATCH; o.cls = cls; o.lev = &L;
+  o.out = x; o.b = b; o.bs = bs;
+  o.r0 = L.pcs[c]; o.r1 = L.pcs[c + 1]; o.n = o.r1 - o.r0;
+  const double np = (double)o.n, nv = (double)(L.n / 2);
+  const double mavg = nv > 0 ? (double)L.Snb / nv : 0.0;   // nodes per patch = blocks per row
+  o.bytes = np * (8.0 * (double)L.pus + mavg * (36.0 * mavg + 8.0) + mavg * (16.0 + 32.0) + 12.0);
+  return o;
+}
+
+void patch_sweep_ops(const DLevel& L, bool fwd, double* x, const double* b, int64_t bs, int cls, std::vector<Op>* ops) {
+  const int nc = (int)L.pcs.size() - 1;
+  for (int k = 0; k < nc; ++k) {
+    const int c = fwd ? k : nc - 1 - k;
+    if (L.pcs[c + 1] > L.pcs[c]) ops->push_back(patch_op(L, c, x, b, bs, cls));
+  }
+}
+
 void gs_sweep_ops(const DLevel& L, bool fwd, double* x, const double* b, int64_t bs, int cls, std::vector<Op>* ops) {
   const int nc = (int)L.gcs.size() - 1;
   for (int k = 0; k < nc; ++k) {
@@ -2252,8 +2618,13 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   const int tagA = l0 ? 0 : 1;
   const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
   const int clsW = l0 ? C_L0_WB : C_COARSE;
-  const bool gs = L.gcs.size() > 1;                       // multicolour GS on this level
-  const bool sgs = p.smoother == MAMG_SMOOTHER_SGS;
+  const bool pat = L.pcs.size() > 1;                      // node-patch Schwarz on this level
+  const bool gs = L.gcs.size() > 1 || pat;                // multicolour GS on this level
+  const bool sgs = p.smoother == MAMG_SMOOTHER_SGS || pat;
+  auto sweep = [&](bool fwd, double* x) {
+    if (pat) patch_sweep_ops(L, fwd, x, b, bs, clsS, ops);
+    else gs_sweep_ops(L, fwd, x, b, bs, clsS, ops);
+  };
   const int steps = smoother_steps(p);
   const int npre = p.presmooth_iter * steps, npost = p.postsmooth_iter * steps;
   double* X = (gs && os == 0) ? xout : L.t;               // GS sweeps in place
@@ -2263,8 +2634,8 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     z.kind = OP_ZERO; z.cls = clsW; z.n = L.n; z.out = X; z.bytes = 8.0 * L.n;
     ops->push_back(z);
     for (int s = 0; s < p.presmooth_iter; ++s) {
-      gs_sweep_ops(L, true, X, b, bs, clsS, ops);
-      if (sgs) gs_sweep_ops(L, false, X, b, bs, clsS, ops);
+      sweep(true, X);
+      if (sgs) sweep(false, X);
     }
   } else {    // first sweep from x = 0: X = W b (POLY: w_1 W b)
     Op o;
@@ -2291,8 +2662,8 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   if (gs) {   // prolongate, then backward (SGS: forward then backward) sweeps
     ops->push_back(bsr_op(L.Pb, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0, nullptr, X, 0));
     for (int s = 0; s < p.postsmooth_iter; ++s) {
-      if (sgs) gs_sweep_ops(L, true, X, b, bs, clsS, ops);
-      gs_sweep_ops(L, false, X, b, bs, clsS, ops);
+      if (sgs) sweep(true, X);
+      sweep(false, X);
     }
     if (X != xout) {
       Op o;
@@ -2583,6 +2954,11 @@ void launch(const Op& o, hipStream_t s) {
       break;
     case OP_GS:
       if (o.n > 0) launch_gs(o, s);
+      break;
+    case OP_PATCH:
+      if (o.n > 0)
+        patch_kernel<<<(unsigned)((o.n + 3) / 4), 256, 0, s>>>(o.r0, o.r1, o.lev->pperm, o.lev->Sptr, o.lev->Scol,
+                                                                o.lev->Sval, o.lev->pu, o.lev->pus, o.out, o.b, o.bs);
       break;
     case OP_ZERO:
       if (o.n) (void)hipMemsetAsync(o.out, 0, o.n * sizeof(double), s);
@@ -3789,8 +4165,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (gs_smoother(p) || p.coarse_scaling) {
-    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers without coarse scaling";
+  if (gs_smoother(p) || p.coarse_scaling || patch_schwarz(p)) {
+    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers without coarse scaling or node patches";
     return MAMG_ERR_UNSUPPORTED;
   }
   read_knobs();

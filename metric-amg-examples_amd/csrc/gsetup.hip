@@ -1293,6 +1293,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
               std::string* err) {
   int rc = check_params(p, err);
   if (rc) return rc;
+  if ((rc = check_patch_seeds(p, idofs, n_idofs, A0.n, err))) return rc;
   if (p.num_functions != 2 || !p.node_block_smoother || (p.AMG_type == MAMG_SA_AMG && !p.sa_block_diag)) {
     *err = "GPU setup covers the nodal 2-field profile (num_functions 2, node_block_smoother 1, "
            "sa_block_diag 1); use the host setup (mamg_setup) for other profiles";

@@ -948,7 +948,13 @@ int check_params(const mamg_params& p, std::string* err) {
     const int want = p.smoother == MAMG_SMOOTHER_SGS ? MAMG_SCHWARZ_SYMMETRIC
                      : p.smoother == MAMG_SMOOTHER_GS ? MAMG_SCHWARZ_FORWARD : MAMG_SCHWARZ_BLOCK_JACOBI;
     const bool additive_ok = !gsm && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE;
-    if (p.Schwarz_type != want && !additive_ok) {
+    if (p.Schwarz_type == MAMG_SCHWARZ_PATCHES) {
+      if (p.num_functions != 2 || !p.node_block_smoother || p.Schwarz_maxlvl != 1) {
+        *err = "SCHWARZ_PATCHES (multiplicative node-patch Schwarz) needs num_functions 2, node_block_smoother 1 "
+               "and Schwarz_maxlvl 1";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+    } else if (p.Schwarz_type != want && !additive_ok) {
       *err = std::string("Schwarz_type must match the smoother: SCHWARZ_BLOCK_JACOBI with the Jacobi smoothers, ") +
              "SCHWARZ_SYMMETRIC with SMOOTHER_SGS, SCHWARZ_FORWARD with SMOOTHER_GS (SCHWARZ_ADDITIVE: overlapping "
              "seed rings with the Jacobi-family smoothers)";
@@ -979,10 +985,27 @@ int check_params(const mamg_params& p, std::string* err) {
   return MAMG_OK;
 }
 
+// SCHWARZ_PATCHES: one patch per node, so every node must hold a seed dof
+// (the bidomain's idofs = every u2 dof, src/bidomain_3d.py:138)
+int check_patch_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err) {
+  if (p.Schwarz_levels < 1 || p.Schwarz_type != MAMG_SCHWARZ_PATCHES) return MAMG_OK;
+  const int64_t nv = n / 2;
+  std::vector<char> has(nv, 0);
+  for (int64_t i = 0; i < n_idofs; ++i)
+    if (idofs[i] >= 0 && idofs[i] < n) has[idofs[i] % nv] = 1;
+  for (int64_t I = 0; I < nv; ++I)
+    if (!has[I]) {
+      *err = "SCHWARZ_PATCHES needs a seed dof (idofs) on every node; node " + std::to_string(I) + " has none";
+      return MAMG_ERR_UNSUPPORTED;
+    }
+  return MAMG_OK;
+}
+
 int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* H, std::string* err) {
   int rc = check_params(p, err);
   if (rc) return rc;
+  if ((rc = check_patch_seeds(p, idofs, n_idofs, A0.n, err))) return rc;
   if (A0.n != A0.m || A0.n <= 0) { *err = "A must be square and non-empty"; return MAMG_ERR_ARG; }
   for (int64_t i = 0; i < A0.n; ++i)
     if (A0.ptr[i + 1] < A0.ptr[i]) { *err = "rowptr not monotone"; return MAMG_ERR_ARG; }

@@ -145,6 +145,8 @@ def dat_to_parameters(d: dict):
                      '(overlapping, parallel)' % (prm.get('Schwarz_type'), maxlvl))
         mapped['Schwarz_maxlvl'] = maxlvl
         mapped['Schwarz_type'] = P.SCHWARZ_ADDITIVE
+        if prm.get('num_functions') is None:
+            mapped.pop('num_functions', None)
     # the file-based 3D-1D solve seeds the 1-D dofs: its seed blocks are not
     # node-aligned, so it runs the CSR layout, where the multicolour GS
     # smoothers (node-block) do not exist; HAZmath's relaxation is an SOR

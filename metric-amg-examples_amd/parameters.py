@@ -19,6 +19,12 @@ values are build-defined (HAZmath's are not available here).
 * ``parameters_metric_mi355x_sgs``: the reference's smoother family on the
   GPU: multicolour node-block SGS on every level (level 0: multiplicative
   Schwarz on the seed blocks), coarse-grid correction scaling ON.
+* ``parameters_metric_mi355x_patch``: the reference's level-0 smoother --
+  symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
+  (``SCHWARZ_PATCHES``), node-block Jacobi below.
+  ``SCHWARZ_SYMMETRIC`` itself names multiplicative Schwarz on the
+  non-overlapping seed blocks (node blocks); ``to_gpu_profile`` maps the
+  reference's SYMMETRIC 1-ring blocks onto ``SCHWARZ_PATCHES``.
 * ``parameters_metric_3d1d``: additive overlapping Schwarz on the 1-D seeds'
   rings.
 * ``to_gpu_profile(d)``: explicit opt-in mapping of a HAZmath dict onto
@@ -40,6 +46,8 @@ SMOOTHER_POLY = 12            # Chebyshev polynomial in W A (HAZmath/FASP SMOOTH
 VMB, MIS, MWM, HEC, HEM = 1, 2, 3, 4, 5
 SCHWARZ_FORWARD, SCHWARZ_BACKWARD, SCHWARZ_SYMMETRIC, SCHWARZ_BLOCK_JACOBI = 1, 2, 3, 4
 SCHWARZ_ADDITIVE = 5          # overlapping seed + Schwarz_maxlvl-ring blocks, additive (sparse seed sets)
+SCHWARZ_PATCHES = 6           # the reference's overlapping seed + 1-ring blocks, symmetric multiplicative
+                              # (one patch per node, distance-3 multicolour order; level 0, nodal)
 OFF, ON = 0, 1
 SOLVER_UMFPACK = 32          # coarse_solver / Schwarz_blksolver: dense direct here
 
@@ -100,6 +108,13 @@ parameters_metric_mi355x_sgs = dict(
     parameters_metric_mi355x, smoother=SMOOTHER_SGS, coarse_scaling=ON,
     Schwarz_type=SCHWARZ_SYMMETRIC)
 
+# the reference's level-0 smoother on the GPU:
+# symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
+# (src/amg_parameters.py:83-87, src/utils.py:84) = one patch per node, exact
+# local solves; node-block Jacobi on the coarser levels of the SA V-cycle.
+# PCG iterations within 1.2x of the reference algorithm's (oracle, 3-D)
+parameters_metric_mi355x_patch = dict(parameters_metric_mi355x, Schwarz_type=SCHWARZ_PATCHES)
+
 # ---- the reference's presets, verbatim values (src/amg_parameters.py) ------
 parameters_standard = {
     "prectype": 2, "AMG_type": UA_AMG, "cycle_type": W_CYCLE, "max_levels": 20, "maxit": 1,
@@ -145,7 +160,14 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
         out['Schwarz_levels'] = 1
     smo = out.get('smoother', SMOOTHER_JACOBI_RHO)
     want = {SMOOTHER_SGS: SCHWARZ_SYMMETRIC, SMOOTHER_GS: SCHWARZ_FORWARD}.get(smo, SCHWARZ_BLOCK_JACOBI)
-    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type', want) != want:
+    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type') == SCHWARZ_SYMMETRIC \
+            and out.get('Schwarz_maxlvl', 1) == 1:
+        notes.append('Schwarz_type SCHWARZ_SYMMETRIC on the seeds\' 1-rings -> SCHWARZ_PATCHES (the same '
+                     'overlapping blocks, multiplicative in a distance-3 multicolour order; nodal systems '
+                     'with a seed on every node)')
+        out['Schwarz_type'] = SCHWARZ_PATCHES
+        out['num_functions'] = 2
+    elif out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type', want) != want:
         notes.append('Schwarz_type %r -> %r (the level-0 seed blocks use the level smoother)'
                      % (out.get('Schwarz_type'), want))
         out['Schwarz_type'] = want

@@ -221,7 +221,7 @@ class Params:
     Schwarz_levels: int = 1       # 1: seed-block Jacobi on level 0 (needs idofs)
     Schwarz_mmsize: int = 100     # max dofs per seed block
     Schwarz_maxlvl: int = 1       # 1: seed + joined 1-ring neighbours; 0: the seed's node (node blocks)
-    Schwarz_type: int = 4         # 4: non-overlapping seed blocks (block Jacobi); 5: additive overlapping rings
+    Schwarz_type: int = 4         # 4: non-overlapping seed blocks (block Jacobi); 5: additive overlapping rings; 6: node patches
     sa_omega: float = 4.0 / 3.0   # prolongator smoothing  w = sa_omega / rho
     rho_iters: int = 0            # 0: Gershgorin bound; >0: inf-norm power its
     max_coarse_dense: int = 8192
@@ -906,6 +906,126 @@ def node_block_inverse(A: sp.csr_matrix, bid: np.ndarray, nb: int, nf: int = 2) 
     return out
 
 
+# --------------------------------------------------------------------------
+# Multiplicative node-patch Schwarz on level 0 (Schwarz_type PATCHES): the
+# reference's level-0 smoother -- symmetric multiplicative Schwarz on one
+# block per seed = the seed + its Schwarz_maxlvl = 1 ring in A's graph
+# (src/amg_parameters.py:83-87, src/utils.py:84), exact local solves
+# (Schwarz_blksolver 32).  With the bidomain's seeds (every u2 dof,
+# src/bidomain_3d.py:138) the block of node I's seed is both fields of the
+# closed node neighbourhood N[I].  Parallel order: patches coloured so that
+# two patches of one colour are >= 4 node hops apart (distance-3
+# Jones-Plassmann), so no patch of a colour reads an x another one writes;
+# a sweep takes the colours in order (forward) or reversed (backward).
+# --------------------------------------------------------------------------
+SCHWARZ_PATCHES = 6
+PATCH_MAX_NODES = 16
+PATCH_MAX_COLOURS = 256
+
+
+def patch_key(nv: int) -> np.ndarray:
+    """priority of patch (centre node) I: hash32(I, 0x5000) high, I low."""
+    I = np.arange(nv, dtype=np.uint64)
+    return (hash32(np.arange(nv), 0x5000).astype(np.uint64) << np.uint64(32)) | I
+
+
+def _row_reduce(Gd: sp.csr_matrix, v: np.ndarray, op) -> np.ndarray:
+    """out[I] = op over the columns J of row I of v[J] (rows are non-empty)."""
+    return op.reduceat(v[Gd.indices], Gd.indptr[:-1], axis=0)
+
+
+def patch_colouring(Gd: sp.csr_matrix) -> np.ndarray:
+    """Distance-3 round-synchronous Jones-Plassmann on the node graph Gd
+    (diagonal included).  Per round: k3 = max over the 3-hop neighbourhood
+    of the uncoloured keys (three row-max passes), m3 = OR over the 3-hop
+    neighbourhood of the coloured nodes' colour bits (256-bit, four uint64
+    words); an uncoloured node with k3 == its own key takes the lowest colour
+    absent from m3.  Two winners of a round are > 3 hops apart, so the
+    result does not depend on the visiting order (device: patch_round)."""
+    nv = Gd.shape[0]
+    key = patch_key(nv)
+    col = np.full(nv, -1, np.int64)
+    words = PATCH_MAX_COLOURS // 64
+    while (col < 0).any():
+        unc = col < 0
+        k = np.where(unc, key, np.uint64(0))
+        for _ in range(3):
+            k = _row_reduce(Gd, k, np.maximum)
+        m = np.zeros((nv, words), np.uint64)
+        cc = np.flatnonzero(~unc)
+        m[cc, col[cc] // 64] = np.left_shift(np.uint64(1), (col[cc] % 64).astype(np.uint64))
+        for _ in range(3):
+            m = _row_reduce(Gd, m, np.bitwise_or)
+        win = np.flatnonzero(unc & (k == key))
+        c = np.full(len(win), -1, np.int64)
+        for wd in range(words - 1, -1, -1):
+            mw = m[win, wd]
+            free = (~mw) & (mw + np.uint64(1))      # lowest zero bit of the word
+            has = free != 0
+            c[has] = 64 * wd + np.log2(free[has].astype(np.float64)).astype(np.int64)
+        if (c < 0).any():
+            raise RuntimeError('more than %d patch colours' % PATCH_MAX_COLOURS)
+        col[win] = c
+    return col.astype(np.int32)
+
+
+class Patches:
+    """Level-0 node patches: centre I -> nodes = row I of the node graph with
+    its diagonal (sorted); local dof i = 2 a + f (a = position of the node,
+    f = field); Minv = the patch matrix's Gauss-Jordan inverse (no pivoting,
+    batched_inverse), symmetrised from its upper triangle."""
+
+    def __init__(self, A: sp.csr_matrix, idofs):
+        n = A.shape[0]
+        nv = n // 2
+        if idofs is None or np.unique(np.asarray(idofs, np.int64) % nv).size != nv:
+            raise ValueError('node patches need a seed dof on every node')
+        G = node_pattern(A, 2)
+        Gd = (G + sp.identity(nv, dtype=np.int8, format='csr')).tocsr()
+        Gd.data[:] = 1
+        Gd.sort_indices()
+        m = np.diff(Gd.indptr)
+        if m.max() > PATCH_MAX_NODES:
+            raise RuntimeError('a node patch holds more than %d nodes' % PATCH_MAX_NODES)
+        self.nv = nv
+        self.colour = patch_colouring(Gd)
+        self.ncolours = int(self.colour.max()) + 1
+        self.crows = [np.flatnonzero(self.colour == c) for c in range(self.ncolours)]
+        self.m = m
+        dmax = 2 * int(m.max())
+        # dofs[I, i] = global dof of local dof i (field-major order), -1 padding
+        self.dofs = np.full((nv, dmax), -1, np.int64)
+        self.Minv = np.zeros((nv, dmax, dmax))
+        A = A.tocsr()
+        for mm in np.unique(m):
+            I = np.flatnonzero(m == mm)
+            nodes = np.stack([Gd.indices[Gd.indptr[i]:Gd.indptr[i + 1]] for i in I])   # (k, mm)
+            d = 2 * mm
+            dofs = np.empty((len(I), d), np.int64)
+            dofs[:, 0::2] = nodes
+            dofs[:, 1::2] = nv + nodes
+            self.dofs[I, :d] = dofs
+            Ap = np.stack([A[dd][:, dd].toarray() for dd in dofs])
+            Mi = batched_inverse(Ap)
+            U = np.triu(Mi)
+            self.Minv[I, :d, :d] = U + np.transpose(np.triu(Mi, 1), (0, 2, 1))
+
+    def sweep(self, A: sp.csr_matrix, x: np.ndarray, b: np.ndarray, forward=True):
+        """x <- x + Minv_I (b - A x)|_patch(I) for the patches of each colour
+        in turn (ascending if forward, else descending)."""
+        order = range(self.ncolours) if forward else range(self.ncolours - 1, -1, -1)
+        for c in order:
+            I = self.crows[c]
+            D = self.dofs[I]
+            ok = D >= 0
+            dd = D[ok]
+            res = np.zeros(D.shape)
+            res[ok] = b[dd] - A[dd] @ x
+            delta = np.einsum('kij,kj->ki', self.Minv[I], res)
+            x[dd] = x[dd] + delta[ok]
+        return x
+
+
 @dataclasses.dataclass
 class Level:
     A: sp.csr_matrix
@@ -923,6 +1043,7 @@ class Level:
     Dn: np.ndarray = None            # multicolour GS: (nv, 2, 2) block inverses
     crows: list = None               # node ids of each colour (ascending)
     polyW: list = None               # POLY: w_k W per Chebyshev step (poly_weights)
+    patches: 'Patches' = None        # level 0, Schwarz_type PATCHES
 
     def step_smoother(self, k):
         return None if self.polyW is None else self.polyW[k]
@@ -964,7 +1085,12 @@ class Hierarchy:
             return lev.Ainv @ b
         A = lev.A
         gs = lev.colour is not None
-        if gs:                                       # SGS: forward + backward; GS: forward
+        if lev.patches is not None:                  # symmetric multiplicative patch Schwarz
+            x = np.zeros_like(b)
+            for _ in range(p.presmooth_iter):
+                x = lev.patches.sweep(A, x, b, True)
+                x = lev.patches.sweep(A, x, b, False)
+        elif gs:                                     # SGS: forward + backward; GS: forward
             x = np.zeros_like(b)
             for _ in range(p.presmooth_iter):
                 x = lev.gs_sweep(x, b, True)
@@ -991,7 +1117,10 @@ class Hierarchy:
         if lev.polyW is not None:
             post = lev.polyW[::-1]                   # POLY: steps m..1
         for _ in range(p.postsmooth_iter):
-            if gs:                                   # SGS: forward + backward; GS: backward
+            if lev.patches is not None:
+                x = lev.patches.sweep(A, x, b, True)
+                x = lev.patches.sweep(A, x, b, False)
+            elif gs:                                 # SGS: forward + backward; GS: backward
                 if p.smoother == 'SGS':
                     x = lev.gs_sweep(x, b, True)
                 x = lev.gs_sweep(x, b, False)
@@ -1075,6 +1204,10 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
             lev.colour = jp_colouring(node_pattern(cur, 2), l)
             lev.ncolours = int(lev.colour.max()) + 1 if len(lev.colour) else 0
             lev.crows = [np.flatnonzero(lev.colour == c) for c in range(lev.ncolours)]
+        if l == 0 and p.Schwarz_levels >= 1 and p.Schwarz_type == SCHWARZ_PATCHES:
+            if nf != 2 or p.Schwarz_maxlvl != 1:
+                raise ValueError('node patches need num_functions = 2 and Schwarz_maxlvl = 1')
+            lev.patches = Patches(cur, idofs)
         lev.agg, lev.nagg = agg, nagg
         T = tentative_nodal(agg, nagg, nf) if nf > 1 else tentative(agg, nagg)
         if p.AMG_type == 'SA':

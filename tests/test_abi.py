@@ -85,7 +85,8 @@ def test_reference_presets_map_and_report(lib_built):
     assert mapped['aggregation_type'] == P.MIS and any('VMB' in n or '1' in n for n in notes)
     mapped, notes = P.to_gpu_profile(P.parameters_metric_schwarz)
     assert mapped['smoother'] == P.SMOOTHER_SGS and mapped['aggregation_type'] == P.HEM
-    assert mapped['Schwarz_type'] == P.SCHWARZ_SYMMETRIC and mapped['coarse_scaling'] == P.ON
+    assert mapped['Schwarz_type'] == P.SCHWARZ_PATCHES and mapped['coarse_scaling'] == P.ON
+    assert any('SCHWARZ_PATCHES' in n for n in notes)
     assert mapped['num_functions'] == 2
     assert P.parameters_metric_schwarz_gpu_mapped == mapped
     H = M.HostHierarchy(laplace1d(300), parameters=P.parameters_standard_gpu_mapped,

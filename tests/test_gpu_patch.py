@@ -1,0 +1,129 @@
+"""GPU parity of the multiplicative node-patch Schwarz smoother
+(Schwarz_type SCHWARZ_PATCHES: the reference's level-0 symmetric
+multiplicative Schwarz on the seeds' overlapping 1-ring blocks,
+/root/reference/src/amg_parameters.py:83-87, src/utils.py:84) against the CPU
+oracle (mamg_oracle.Patches: distance-3 colouring, Gauss-Jordan patch
+inverses, colour-ordered sweeps).
+
+Tolerances as tests/test_gpu_gs.py: one apply to 1e-10 relative (colouring,
+order and patch inverses are exact; only the residual summation order
+differs), PCG iteration count equal to the oracle's, residuals within 1e-6.
+"""
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+PATCHES = 6
+
+
+def _mamg():
+    import metric_amg_examples_amd as M
+    return M
+
+
+def to_c(kw):
+    c = dict(kw, Schwarz_type=PATCHES)
+    if 'smoother' in c:
+        c['smoother'] = {'SGS': 11, 'GS': 10, 'POLY': 12}[c['smoother']]
+    if 'cycle_type' in c:
+        c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    if 'AMG_type' in c:
+        c['AMG_type'] = {'SA': 2, 'UA': 1}[c['AMG_type']]
+    if 'aggregation_type' in c:
+        c['aggregation_type'] = {'MIS': 2, 'HEM': 5}[c['aggregation_type']]
+    return c
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+CASES = [
+    (3, 8, 1e6, dict()),
+    (3, 16, 1e6, dict()),
+    (2, 32, 1.0, dict()),
+    (2, 64, 1e6, dict(coarse_scaling=1)),
+    (3, 16, 1e4, dict(smoother='SGS', coarse_scaling=1)),
+    (3, 8, 1e2, dict(smoother='POLY')),
+    (3, 16, 1e6, dict(cycle_type='W', presmooth_iter=2, postsmooth_iter=2)),
+    # the reference's metric_schwarz family with its own level-0 Schwarz:
+    # UA + parallel HEM + W-cycle + SGS + coarse scaling + node patches
+    (3, 16, 1e6, dict(smoother='SGS', coarse_scaling=1, cycle_type='W', AMG_type='UA', aggregation_type='HEM')),
+]
+
+
+@pytest.mark.parametrize('setup', ['host', 'gpu'])
+@pytest.mark.parametrize('dim,n,g,kw', CASES)
+def test_patch_apply_matches_oracle(lib_built, dim, n, g, kw, setup):
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup=setup, **to_c(kw))
+    assert B.setup_path == setup, B.setup_path
+    h = mo.setup(A, mo.Params(num_functions=2, Schwarz_type=PATCHES, **kw), idofs=s.idofs)
+    assert B.num_levels == len(h.levels)
+    for seed in (1234, 7):
+        r = mo.seeded_rhs(s.N, seed)
+        zo = h.apply(r)
+        z = B * r
+        assert rel(z, zo) < 1e-10
+        zt = B.matvec(torch.as_tensor(r).cuda())
+        torch.cuda.synchronize()
+        assert rel(zt.cpu().numpy(), zo) < 1e-10
+
+
+@pytest.mark.parametrize('dim,n,g', [(3, 16, 1e6), (2, 64, 1e4), (3, 8, 1e10)])
+def test_patch_pcg_matches_oracle(lib_built, dim, n, g):
+    """Device PCG with the node-patch profile: iteration count and residual
+    history equal the oracle's."""
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    b = mo.seeded_rhs(s.N)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, Schwarz_type=PATCHES)
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+    x = solver * b
+    h = mo.setup(A, mo.Params(num_functions=2, Schwarz_type=PATCHES), idofs=s.idofs)
+    ref = mo.pcg(A, h, b, 1e-8, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+    assert rel(x, ref.x) < 1e-6
+
+
+def test_patch_cycle_symmetric_and_deterministic(lib_built):
+    """Forward + backward colour sweeps make the cycle a symmetric operator;
+    two graph replays give identical bits (no races inside a colour)."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, Schwarz_type=PATCHES)
+    r1 = torch.as_tensor(mo.seeded_rhs(s.N, 1)).cuda()
+    r2 = torch.as_tensor(mo.seeded_rhs(s.N, 2)).cuda()
+    z1, z2 = B.matvec(r1), B.matvec(r2)
+    z1b = B.matvec(r1)
+    torch.cuda.synchronize()
+    a = float(torch.dot(r2, z1))
+    c = float(torch.dot(r1, z2))
+    assert abs(a - c) <= 1e-12 * abs(a)
+    assert torch.equal(z1, z1b)
+
+
+def test_patch_bidomain_3d_nrefs4(lib_built):
+    """A larger 3-D case (n = 64, 550K dofs) on the GPU setup: PCG converges
+    in the oracle-sized iteration range and the device PCG equals the host loop."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 64, 1e6)
+    A = s.scipy()
+    b = mo.seeded_rhs(s.N)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, Schwarz_type=PATCHES, setup='gpu')
+    dev = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+    dev * b
+    host = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500, device=False)
+    host * b
+    assert len(dev.residuals) == len(host.residuals) <= 12
+    assert np.allclose(dev.residuals, host.residuals, rtol=1e-6, atol=0)
