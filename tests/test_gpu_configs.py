@@ -145,3 +145,35 @@ def test_emi_3d_nrefs5_node_aligned_8_virtual_ranks(lib_built):
         hh.close()
     H.close()
     B.close()
+
+
+@pytest.mark.parametrize('radius', [0.0, 1.0])
+def test_emi_3d1d_gamma_sweep(lib_built, radius):
+    """BASELINE config 5 on one GPU: the 3D-1D system (src/emi_3d1d.py:99-167)
+    on a 49^3 tissue cube with the synthetic branched neuron, gamma swept
+    1e0..1e8 (run_bidomain-style sweep of the reference), profile
+    parameters_metric_3d1d (additive overlapping Schwarz on the 1-D seeds'
+    2-rings).  Per gamma: the device-resident PCG and the host-loop PCG over
+    the same preconditioner take the same iterations and reach the driver's
+    relative tolerance 1e-6; the counts stay gamma-robust."""
+    M = _M()
+    P = M.parameters
+    its = {}
+    for g in (1.0, 1e2, 1e4, 1e6, 1e8):
+        s = M.problems.emi_3d1d(48, g, radius)
+        A = s.scipy()
+        b = M.problems.seeded_rhs(s.N)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_metric_3d1d)
+        dev = M.ConjGrad(A, precond=B, tolerance=1e-6, maxiter=1000, stop_type=1)
+        x = dev * b
+        host = M.ConjGrad(A, precond=B, tolerance=1e-6, maxiter=1000, stop_type=1, device=False)
+        host * b
+        x = x.cpu().numpy() if hasattr(x, 'cpu') else np.asarray(x)
+        n_dev, n_host = len(dev.residuals) - 1, len(host.residuals) - 1
+        say('emi_3d1d n=48 radius', radius, 'gamma', g, 'N', s.N, 'PCG its device', n_dev, 'host', n_host)
+        assert n_dev == n_host
+        assert np.linalg.norm(b - A @ x) <= 1e-5 * np.linalg.norm(b)
+        its[g] = n_dev
+        B.close()
+    assert max(its.values()) < 200
+    assert max(its.values()) <= 3 * min(its.values()), its
