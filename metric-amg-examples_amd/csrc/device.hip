@@ -3024,6 +3024,38 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// Re-home the level-0 streams -- K values and columns (6.4 GB at nrefs=6),
+// A_0's upper values and columns (4.3 GB), R_0's values (2.3 GB) -- into fresh
+// allocations once the setup's temporaries are gone.  The kernels' DRAM rate
+// depends on where these arrays land, for the same bytes and the same PMC
+// traffic: as built in the pre-reserved arena, K ran 1.59 / 1.71 ms on two
+// boxes; copied after the setup 1.48-1.65 ms, residual 1.06-1.09 vs 1.09-1.10
+// ms, restriction 0.51 vs 0.53 ms, never slower over 15 fresh processes
+// (profiles/r02_rehome_level0.txt).  Same data: results
+// are bitwise equal.  The arena's copies stay unused.
+void rehome_level0(DeviceHandle* h) {
+  if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell) return;
+  DLevel& L = h->L[0];
+  auto mv = [&](void** ptr, size_t b) {
+    void* r = nullptr;
+    if (!*ptr || hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }   // keep the old copy
+    if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(r);
+      return;
+    }
+    h->allocs.push_back(r);
+    *ptr = r;
+  };
+  mv((void**)&L.KPb.val, (size_t)L.KPb.nbs * 4 * sizeof(double));
+  mv((void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
+  if (L.Ab.half) {
+    mv((void**)&L.Ab.val, (size_t)L.Ab.nbs * 3 * sizeof(double));
+    mv((void**)&L.Ab.col, (size_t)L.Ab.nbs * sizeof(int32_t));
+  }
+  if (!L.Rb.sell && !L.Rb.sym) mv((void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
+}
+
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
                std::string* err) {
   std::unique_ptr<DeviceHandle> h(new DeviceHandle());
@@ -3121,6 +3153,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   apply_ops(h.get(), h->hr, h->hz, &ops);
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   HIPCHK(hipDeviceSynchronize());
+  rehome_level0(h.get());
   *out = h.release();
   return MAMG_OK;
 }
@@ -3240,6 +3273,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
   HIPCHK(hipDeviceSynchronize());
+  rehome_level0(h.get());
   h->setup_ms[GS_LAYOUT] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = h.release();
