@@ -3025,7 +3025,8 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 
 // ---------------------------------------------------------------------------
 // Re-home the level-0 streams -- K values and columns (6.4 GB at nrefs=6),
-// A_0's upper values and columns (4.3 GB), R_0's values (2.3 GB) -- into fresh
+// A_0's upper values and columns (4.3 GB), R_0's values (2.3 GB) -- and the
+// coarser levels' operators into fresh
 // allocations once the setup's temporaries are gone.  The kernels' DRAM rate
 // depends on where these arrays land, for the same bytes and the same PMC
 // traffic: as built in the pre-reserved arena, K ran 1.59 / 1.71 ms on two
@@ -3033,7 +3034,7 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // ms, restriction 0.51 vs 0.53 ms, never slower over 15 fresh processes
 // (profiles/r02_rehome_level0.txt).  Same data: results
 // are bitwise equal.  The arena's copies stay unused.
-void rehome_level0(DeviceHandle* h) {
+void rehome_operators(DeviceHandle* h) {
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
   auto mv = [&](void** ptr, size_t b) {
@@ -3054,6 +3055,18 @@ void rehome_level0(DeviceHandle* h) {
     mv((void**)&L.Ab.col, (size_t)L.Ab.nbs * sizeof(int32_t));
   }
   if (!L.Rb.sell && !L.Rb.sym) mv((void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
+  // the coarser levels' operators too (coarse levels 0.41 -> 0.395 ms per apply)
+  auto mvb = [&](DBsr& M) {
+    if (M.nr == 0 || M.half) return;
+    const int64_t slots = M.sell ? M.nbs : M.nb;
+    mv((void**)&M.val, (size_t)slots * (M.sym ? 3 : 4) * sizeof(double));
+    mv((void**)&M.col, (size_t)slots * sizeof(int32_t));
+  };
+  for (size_t l = 1; l < h->L.size(); ++l) {
+    DLevel& D = h->L[l];
+    if (D.coarsest) break;
+    mvb(D.Ab); mvb(D.KPb); mvb(D.Rb); mvb(D.Pb);
+  }
 }
 
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
@@ -3153,7 +3166,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   apply_ops(h.get(), h->hr, h->hz, &ops);
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   HIPCHK(hipDeviceSynchronize());
-  rehome_level0(h.get());
+  rehome_operators(h.get());
   *out = h.release();
   return MAMG_OK;
 }
@@ -3273,7 +3286,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
   HIPCHK(hipDeviceSynchronize());
-  rehome_level0(h.get());
+  rehome_operators(h.get());
   h->setup_ms[GS_LAYOUT] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = h.release();
