@@ -3026,20 +3026,25 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // ---------------------------------------------------------------------------
 // Re-home the level-0 streams -- K values and columns (6.4 GB at nrefs=6),
 // A_0's upper values and columns (4.3 GB), R_0's values (2.3 GB) -- and the
-// coarser levels' operators into fresh
-// allocations once the setup's temporaries are gone.  The kernels' DRAM rate
-// depends on where these arrays land, for the same bytes and the same PMC
-// traffic: as built in the pre-reserved arena, K ran 1.59 / 1.71 ms on two
-// boxes; copied after the setup 1.48-1.65 ms, residual 1.06-1.09 vs 1.09-1.10
-// ms, restriction 0.51 vs 0.53 ms, never slower over 15 fresh processes
-// (profiles/r02_rehome_level0.txt).  Same data: results
-// are bitwise equal.  The arena's copies stay unused.
+// coarser levels' operators into fresh, physically contiguous allocations
+// (hipDeviceMallocContiguous; a plain allocation where the driver has none)
+// once the setup's temporaries are gone.  The kernels' DRAM rate depends on
+// where these arrays land, for the same bytes and the same PMC traffic: as
+// built in the pre-reserved arena K ran 1.59-1.71 ms; re-homed into plain
+// allocations 1.48-1.68 ms (residual 1.06-1.09 vs 1.09-1.10 ms, restriction
+// 0.51 vs 0.53 ms); re-homed contiguously 1.47-1.59 ms, 268.6-276.4 applies/s
+// against 263-264 for plain allocations on the same box (DESIGN.md section 5,
+// profiles/r02_rehome_level0.txt).  Same data: results are bitwise equal.
+// The arena's copies stay unused.
 void rehome_operators(DeviceHandle* h) {
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
   auto mv = [&](void** ptr, size_t b) {
     void* r = nullptr;
-    if (!*ptr || hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }   // keep the old copy
+    if (!*ptr) return;
+    // physically contiguous when the driver has it (K 1.47-1.50 vs 1.59-1.67 ms), else a plain allocation
+    if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+    if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }   // keep the old copy
     if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
       (void)hipGetLastError();
       (void)hipFree(r);
