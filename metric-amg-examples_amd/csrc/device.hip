@@ -3036,41 +3036,43 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // against 263-264 for plain allocations on the same box (DESIGN.md section 5,
 // profiles/r02_rehome_level0.txt).  Same data: results are bitwise equal.
 // The arena's copies stay unused.
+// move one array into a fresh, physically contiguous allocation (plain
+// hipMalloc where the driver has none; the old copy is kept if both fail)
+void rehome_array(std::vector<void*>* allocs, void** ptr, size_t b) {
+  void* r = nullptr;
+  if (!*ptr || b == 0) return;
+  if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+  if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }
+  if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(r);
+    return;
+  }
+  allocs->push_back(r);
+  *ptr = r;
+}
+
+// values and columns of one operator (half-symmetric: the upper part)
+void rehome_bsr(std::vector<void*>* allocs, DBsr& M) {
+  if (M.nr == 0) return;
+  const int64_t slots = (M.sell || M.half) ? M.nbs : M.nb;
+  rehome_array(allocs, (void**)&M.val, (size_t)slots * ((M.sym || M.half) ? 3 : 4) * sizeof(double));
+  rehome_array(allocs, (void**)&M.col, (size_t)slots * sizeof(int32_t));
+}
+
 void rehome_operators(DeviceHandle* h) {
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
-  auto mv = [&](void** ptr, size_t b) {
-    void* r = nullptr;
-    if (!*ptr) return;
-    // physically contiguous when the driver has it (K 1.47-1.50 vs 1.59-1.67 ms), else a plain allocation
-    if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
-    if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }   // keep the old copy
-    if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipFree(r);
-      return;
-    }
-    h->allocs.push_back(r);
-    *ptr = r;
-  };
-  mv((void**)&L.KPb.val, (size_t)L.KPb.nbs * 4 * sizeof(double));
-  mv((void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
-  if (L.Ab.half) {
-    mv((void**)&L.Ab.val, (size_t)L.Ab.nbs * 3 * sizeof(double));
-    mv((void**)&L.Ab.col, (size_t)L.Ab.nbs * sizeof(int32_t));
-  }
-  if (!L.Rb.sell && !L.Rb.sym) mv((void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
+  rehome_bsr(&h->allocs, L.KPb);          // the largest stream first
+  if (L.Ab.half) rehome_bsr(&h->allocs, L.Ab);
+  if (!L.Rb.sell && !L.Rb.sym)
+    rehome_array(&h->allocs, (void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
   // the coarser levels' operators too (coarse levels 0.41 -> 0.395 ms per apply)
-  auto mvb = [&](DBsr& M) {
-    if (M.nr == 0 || M.half) return;
-    const int64_t slots = M.sell ? M.nbs : M.nb;
-    mv((void**)&M.val, (size_t)slots * (M.sym ? 3 : 4) * sizeof(double));
-    mv((void**)&M.col, (size_t)slots * sizeof(int32_t));
-  };
   for (size_t l = 1; l < h->L.size(); ++l) {
     DLevel& D = h->L[l];
     if (D.coarsest) break;
-    mvb(D.Ab); mvb(D.KPb); mvb(D.Rb); mvb(D.Pb);
+    for (DBsr* M : {&D.Ab, &D.KPb, &D.Rb, &D.Pb})
+      if (!M->half) rehome_bsr(&h->allocs, *M);
   }
 }
 
@@ -4344,6 +4346,10 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   h->nv0 = plan.levels[0].nv;
   h->o0 = plan.levels[0].o0;
   h->o1 = plan.levels[0].o1;
+  // the rank-local operators re-homed as on one GPU (rehome_operators)
+  for (DDLevel& D : h->L)
+    if (!D.coarsest && !D.replicated)
+      for (DBsr* M : {&D.K, &D.A, &D.R, &D.PA, &D.P}) rehome_bsr(&h->allocs, *M);
   std::vector<DOp> ops;
   dapply_ops(h.get(), nullptr, nullptr, &ops);
   for (const DOp& d : ops) h->apply_bytes += d.bytes;
