@@ -10,7 +10,7 @@ then runs one virtual distributed apply (device copies stand in for RCCL,
 same counts/offsets) and compares it with the single-GPU apply.  This is what
 each process of `bench.py --gpus P` does before its timed region.
 
-With MAMG_DIST_DRY=1 it instead times each rank's cycle with the exchanges
+With MAMG_DIST_TEST=dry it instead times each rank's cycle with the exchanges
 skipped: the compute part of the P-GPU apply (RCCL latency not included).
 """
 import argparse
@@ -53,7 +53,7 @@ def main():
         print('rank %d: setup %.1fs, device %.2f GB, peak RSS %.1f GB' % (p, t, held / 1e9, rss), flush=True)
     rs = [torch.as_tensor(h.local_slice(r)).cuda() for h in hs]
     zs = [torch.zeros_like(x) for x in rs]
-    if os.environ.get('MAMG_DIST_DRY') == '1':
+    if os.environ.get('MAMG_DIST_TEST') == 'dry':
         # compute-only time of each rank's cycle (exchanges skipped; the
         # numbers exclude RCCL latency, the results are not used)
         names = ['L0_resid', 'L0_smooth_spmv', 'L0_smoother', 'L0_restrict', 'L0_prolong',

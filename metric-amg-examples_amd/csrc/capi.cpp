@@ -348,11 +348,12 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
     lap("GPU setup");
     // default: ghost lists marked on the GPU, the rank's operators cut out of
-    // G in HBM.  MAMG_DIST_FULL_DOWNLOAD=1: the whole hierarchy downloaded and
-    // planned on the host; =2: the rank's rows downloaded, planned on the host
-    // (both bitwise the default; tests)
-    const char* e = std::getenv("MAMG_DIST_FULL_DOWNLOAD");
-    const int mode = e ? std::atoi(e) : 0;
+    // G in HBM.  MAMG_DIST_TEST=full: the whole hierarchy downloaded and
+    // planned on the host; =rows: the rank's rows downloaded, planned on the
+    // host (both bitwise the default; tests)
+    const char* e = std::getenv("MAMG_DIST_TEST");
+    const std::string et = e ? e : "";
+    const int mode = et == "full" ? 1 : et == "rows" ? 2 : 0;
     if (rc) {
     } else if (mode == 1) {
       rc = mamg::ghier_download(G, v, &H, &err);

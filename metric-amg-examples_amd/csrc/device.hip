@@ -1175,7 +1175,7 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //                       XCD (1; 0 = row order)
 //   MAMG_POST_K         0: fused post sweep over [P | AP] instead of K = P - W A P (1)
 //   multi-GPU (mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch during
-//   the forward halo (1); MAMG_DIST_DRY 1 = a virtual rank skips its exchanges
+//   the forward halo (1); MAMG_DIST_TEST=dry: a virtual rank skips its exchanges
 //   (compute-only timing; results meaningless); setup: MAMG_PRERESERVE_B_PER_NNZ
 // Fixed by measurement (round 1 A/Bs; the variants
 // measured slower were removed in round 2): XCD-contiguous restriction rows,
@@ -3594,7 +3594,7 @@ struct DistHandle {
   double apply_bytes = 0.0;
   int64_t nv0 = 0, o0 = 0, o1 = 0;
   bool overlap = true;                 // MAMG_OVERLAP: interior rows during the forward halo
-  bool dry = false;                    // MAMG_DIST_DRY: virtual rank skips its exchanges (timing only)
+  bool dry = false;                    // MAMG_DIST_TEST=dry: virtual rank skips its exchanges (timing only)
   hipStream_t side = nullptr;          // stream of the interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   // host-staged exchange backend (mamg_dist_set_exchange): pinned staging
@@ -4254,8 +4254,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   {
     const char* e = std::getenv("MAMG_OVERLAP");
     h->overlap = e ? std::atoi(e) != 0 : true;
-    e = std::getenv("MAMG_DIST_DRY");
-    h->dry = !comm_id && e && std::atoi(e) != 0;
+    e = std::getenv("MAMG_DIST_TEST");
+    h->dry = !comm_id && e && std::string(e) == "dry";
   }
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));

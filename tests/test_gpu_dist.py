@@ -108,8 +108,8 @@ def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
         monkeypatch.setenv('MAMG_POST_K', '0')
     r = mo.seeded_rhs(s.N)
     out, nbytes = [], []
-    for full in ('1', '2', '0'):   # whole download + host plan, rank rows + host plan, built in HBM
-        monkeypatch.setenv('MAMG_DIST_FULL_DOWNLOAD', full)
+    for full in ('full', 'rows', ''):   # whole download + host plan, rank rows + host plan, built in HBM
+        monkeypatch.setenv('MAMG_DIST_TEST', full)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
                               num_functions=2, **kw) for p in range(P)]
         rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
