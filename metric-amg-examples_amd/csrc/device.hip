@@ -274,7 +274,16 @@ __global__ __launch_bounds__(256) void bsr2_post_kernel(
 constexpr int SELL_C = 64;
 constexpr int SELL_U = 4;     // blocks in flight per lane
 
-template <int EPI, bool XFM, bool SYM, int U, bool NT, int TAG>
+// SPL: general blocks stored as two 16-byte streams per slot, the (0,0)(0,1)
+// pairs at bval[2k] and the (1,0)(1,1) pairs at bval[2 nbs + 2k]: each load
+// instruction reads 1 KB contiguous instead of 16 B of every 32 B over 2 KB
+__device__ __forceinline__ dv4 blk_split(const double* __restrict__ v, int64_t nbs, int64_t k) {
+  const dv2 a = reinterpret_cast<const dv2*>(v)[k];
+  const dv2 b = reinterpret_cast<const dv2*>(v + 2 * nbs)[k];
+  return dv4{a.x, a.y, b.x, b.y};
+}
+
+template <int EPI, bool XFM, bool SYM, int U, bool SPL, int TAG>
 __global__ __launch_bounds__(256) void sell2_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
@@ -296,8 +305,8 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < len ? j + u : len - 1);
-      c[u] = ldg<NT>(bcol + kk);
-      v[u] = blk<SYM, NT>(bval, offd, kk);
+      c[u] = bcol[kk];
+      v[u] = SPL ? blk_split(bval, nbs, kk) : blk<SYM>(bval, offd, kk);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
@@ -1239,6 +1248,7 @@ struct DBsr {              // 2x2 blocks, node-major
   // SELL-64 storage (sell == true): ptr unused; soff per slice, meta per row,
   // col / val hold nbs (>= nb, padded) slots
   bool sell = false;
+  bool split = false;       // SELL general blocks as two 16-byte streams (sell2_kernel SPL)
   int64_t nbs = 0;
   int64_t* soff = nullptr;
   int32_t* meta = nullptr;
@@ -2245,6 +2255,14 @@ int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLeve
   return MAMG_OK;
 }
 
+__global__ __launch_bounds__(256) void split_blocks_kernel(int64_t nbs, const dv4* __restrict__ in, dv2* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nbs) return;
+  const dv4 v = in[k];
+  out[k] = dv2{v.x, v.y};
+  out[nbs + k] = dv2{v.z, v.w};
+}
+
 inline bool patch_schwarz(const mamg_params& p) {
   return p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_PATCHES;
 }
@@ -2394,6 +2412,17 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     // window is never SELL on this path
     if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0)))
       return rc;
+    // K's general blocks as two 16-byte streams (sell2_kernel SPL): each wave
+    // load reads 1 KB contiguous; K 1.712 -> 1.572 ms on one box, three
+    // alternating processes each (profiles/r02_ab_k_split.txt)
+    if (g_post_k && D.KPb.sell && !D.KPb.sym) {
+      dv2* q = nullptr;
+      if ((rc = dalloc(h, &q, 2 * D.KPb.nbs, err))) return rc;
+      split_blocks_kernel<<<nblocks(D.KPb.nbs), 256>>>(D.KPb.nbs, reinterpret_cast<const dv4*>(D.KPb.val), q);
+      HIPCHK(hipGetLastError());
+      D.KPb.val = reinterpret_cast<double*>(q);
+      D.KPb.split = true;
+    }
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -2805,7 +2834,8 @@ template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   // level-0 K operator: chunks of 6 blocks (two chunks cover its ~9-block
   // rows); everything else 8
-  if (TAG == 0 && o.epi == EPI_KPOST) launch_sell_u<XFM, SYM, g_post_u, false, TAG>(o, s);
+  if (TAG == 0 && o.epi == EPI_KPOST && o.Mb->split) launch_sell_u<XFM, SYM, g_post_u, true, TAG>(o, s);
+  else if (TAG == 0 && o.epi == EPI_KPOST) launch_sell_u<XFM, SYM, g_post_u, false, TAG>(o, s);
   else launch_sell_u<XFM, SYM, g_sell_u, false, TAG>(o, s);
 }
 
