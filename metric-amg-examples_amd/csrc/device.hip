@@ -2834,7 +2834,8 @@ template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   // level-0 K operator: chunks of 6 blocks (two chunks cover its ~9-block
   // rows); everything else 8
-  if (TAG == 0 && o.epi == EPI_KPOST && o.Mb->split) launch_sell_u<XFM, SYM, g_post_u, true, TAG>(o, s);
+  if (o.Mb->split && TAG == 0) launch_sell_u<XFM, SYM, g_post_u, true, TAG>(o, s);
+  else if (o.Mb->split) launch_sell_u<XFM, SYM, g_sell_u, true, TAG>(o, s);
   else if (TAG == 0 && o.epi == EPI_KPOST) launch_sell_u<XFM, SYM, g_post_u, false, TAG>(o, s);
   else launch_sell_u<XFM, SYM, g_sell_u, false, TAG>(o, s);
 }
