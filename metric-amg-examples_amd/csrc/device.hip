@@ -1200,7 +1200,7 @@ int g_post_k = 1;
 int64_t g_sell_min_rows = 1 << 20;
 void read_knobs() {
   const char* e = std::getenv("MAMG_POST_K");
-  g_post_k = e ? std::atoi(e) != 0 : 1;
+  g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K, layout timed; 2 / 3: K, split / block forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
   e = std::getenv("MAMG_HALF");
@@ -2263,6 +2263,13 @@ __global__ __launch_bounds__(256) void split_blocks_kernel(int64_t nbs, const dv
   out[nbs + k] = dv2{v.z, v.w};
 }
 
+__global__ __launch_bounds__(256) void unsplit_blocks_kernel(int64_t nbs, const dv2* __restrict__ in, dv4* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nbs) return;
+  const dv2 a = in[k], b = in[nbs + k];
+  out[k] = dv4{a.x, a.y, b.x, b.y};
+}
+
 inline bool patch_schwarz(const mamg_params& p) {
   return p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_PATCHES;
 }
@@ -2412,17 +2419,6 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     // window is never SELL on this path
     if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0)))
       return rc;
-    // K's general blocks as two 16-byte streams (sell2_kernel SPL): each wave
-    // load reads 1 KB contiguous; K 1.712 -> 1.572 ms on one box, three
-    // alternating processes each (profiles/r02_ab_k_split.txt)
-    if (g_post_k && D.KPb.sell && !D.KPb.sym) {
-      dv2* q = nullptr;
-      if ((rc = dalloc(h, &q, 2 * D.KPb.nbs, err))) return rc;
-      split_blocks_kernel<<<nblocks(D.KPb.nbs), 256>>>(D.KPb.nbs, reinterpret_cast<const dv4*>(D.KPb.val), q);
-      HIPCHK(hipGetLastError());
-      D.KPb.val = reinterpret_cast<double*>(q);
-      D.KPb.split = true;
-    }
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -3107,6 +3103,73 @@ void rehome_operators(DeviceHandle* h) {
   }
 }
 
+// Block layout of the level-0 K values, chosen on the device at hand.  One
+// 32-byte block per SELL slot, or two 16-byte streams per slot (sell2_kernel
+// SPL: each wave load 1 KB contiguous).  Which is faster depends on the box,
+// for the same bytes: K 1.712 -> 1.572 ms split on one MI355X, 1.64 -> 1.745 ms
+// on another (alternating processes, profiles/r02_ab_k_split.txt).  Both are
+// timed in the same allocation (the values are rearranged in place) over
+// whole eager applies, and the faster is kept; the arithmetic is the same, so
+// results are bitwise equal either way.
+// MAMG_POST_K=2 / =3 force the split / block layout on every SELL-stored K
+// (tests: both layouts at small sizes).
+void choose_k_layout(DeviceHandle* h) {
+  if (!h->bsr || h->L.size() < 2 || g_post_k == 3) return;
+  if (g_post_k == 2) {                       // forced split, every level stored SELL
+    for (DLevel& D : h->L) {
+      if (D.coarsest || !D.KPb.sell || D.KPb.sym || D.KPb.split) continue;
+      void* t = nullptr;
+      if (hipMalloc(&t, (size_t)D.KPb.nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
+      split_blocks_kernel<<<nblocks(D.KPb.nbs), 256>>>(D.KPb.nbs, reinterpret_cast<const dv4*>(D.KPb.val), (dv2*)t);
+      (void)hipMemcpy(D.KPb.val, t, (size_t)D.KPb.nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
+      (void)hipFree(t);
+      D.KPb.split = true;
+    }
+    return;
+  }
+  if (h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell || h->L[0].KPb.sym) return;
+  DLevel& L = h->L[0];
+  const int64_t nbs = L.KPb.nbs;
+  void* tmp = nullptr;
+  if (hipMalloc(&tmp, (size_t)nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
+  (void)hipMemset(h->hr, 0, L.n * sizeof(double));
+  std::vector<Op> ops;
+  apply_ops(h, h->hr, h->hz, &ops);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto time_apply = [&]() {
+    for (int i = 0; i < 2; ++i) for (const Op& o : ops) launch(o, nullptr);
+    (void)hipEventRecord(e0, nullptr);
+    for (int i = 0; i < 6; ++i) for (const Op& o : ops) launch(o, nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / 6;
+  };
+  auto rearrange = [&](bool to_split) {
+    if (to_split)
+      split_blocks_kernel<<<nblocks(nbs), 256>>>(nbs, reinterpret_cast<const dv4*>(L.KPb.val), (dv2*)tmp);
+    else
+      unsplit_blocks_kernel<<<nblocks(nbs), 256>>>(nbs, reinterpret_cast<const dv2*>(L.KPb.val), (dv4*)tmp);
+    (void)hipMemcpy(L.KPb.val, tmp, (size_t)nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
+    L.KPb.split = to_split;
+  };
+  const float t_block = time_apply();
+  rearrange(true);
+  const float t_split = time_apply();
+  if (t_split >= t_block) rearrange(false);
+  if (h->p.print_level >= 2)
+    std::fprintf(stderr, "[mamg] K layout: one block per slot %.4f ms/apply, split %.4f ms/apply -> %s\n", t_block,
+                 t_split, L.KPb.split ? "split" : "block");
+  (void)hipDeviceSynchronize();
+  (void)hipFree(tmp);
+  (void)hipGetLastError();
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+}
+
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
                std::string* err) {
   std::unique_ptr<DeviceHandle> h(new DeviceHandle());
@@ -3205,6 +3268,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
+  choose_k_layout(h.get());
   *out = h.release();
   return MAMG_OK;
 }
@@ -3325,6 +3389,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
+  choose_k_layout(h.get());
   h->setup_ms[GS_LAYOUT] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = h.release();

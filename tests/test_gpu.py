@@ -441,3 +441,31 @@ def test_device_conjgrad_requires_own_operator(lib_built):
     B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
     with pytest.raises(ValueError):
         M.ConjGrad(A.copy(), precond=B, device=True) * mo.seeded_rhs(s.N)
+
+
+def test_k_block_layouts_bitwise(lib_built, monkeypatch):
+    """The K values stored one 32-byte block per SELL slot (MAMG_POST_K=3) or
+    as two 16-byte streams (=2, sell2_kernel SPL): the same sums, so the apply
+    and the device PCG are bitwise equal; the default (=1) times both on large
+    problems and keeps the faster."""
+    import torch
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    zs, its = [], []
+    for mode in ('3', '2'):
+        monkeypatch.setenv('MAMG_POST_K', mode)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        assert B.level_format(0)['post_sell']
+        zs.append(B.matvec(r))
+        cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        x = cg * mo.seeded_rhs(s.N)
+        its.append((len(cg.residuals), np.asarray(x.cpu() if hasattr(x, 'cpu') else x)))
+        torch.cuda.synchronize()
+        B.close()
+    assert torch.equal(zs[0], zs[1])
+    assert its[0][0] == its[1][0] and np.array_equal(its[0][1], its[1][1])
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    assert rel(zs[1].cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
