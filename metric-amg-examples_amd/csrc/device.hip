@@ -1042,18 +1042,38 @@ __global__ __launch_bounds__(256) void patch_kernel(int64_t c0, int64_t c1, cons
   const int m = (int)(ptr[I + 1] - q0);
   const int a = lane >> 2, q = lane & 3;
   const double2* x2 = reinterpret_cast<const double2*>(x);
+  // this lane's row of the packed inverse, loaded up front: it does not
+  // depend on the residual, so its latency overlaps the row gathers
+  const double* Up = U + i * ustride;
+  const int li = lane < 2 * m ? lane : 0;
+  double u[2 * PATCH_MAX_NODES];
+#pragma unroll
+  for (int j = 0; j < 2 * PATCH_MAX_NODES; ++j) u[j] = j < 2 * m ? Up[upk(li, j)] : 0.0;
+  // node a's row, blocks q, q + 4, q + 8, q + 12 (a row has <= PATCH_MAX_NODES
+  // blocks): loads first, then gathers, then the sums in block order
   double s0 = 0.0, s1 = 0.0;
   int32_t J = 0;
   if (a < m) {
     J = col[q0 + a];
-    const int64_t p1 = ptr[J + 1];
-    for (int64_t k = ptr[J] + q; k < p1; k += 4) {
-      const int32_t c = col[k];
-      const dv4 v = val[k];
-      const double2 xc = x2[c];
-      s0 += v.x * xc.x + v.y * xc.y;
-      s1 += v.z * xc.x + v.w * xc.y;
+    const int64_t p0 = ptr[J], p1 = ptr[J + 1];
+    int32_t c[PATCH_MAX_NODES / 4];
+    dv4 v[PATCH_MAX_NODES / 4];
+    double2 xc[PATCH_MAX_NODES / 4];
+#pragma unroll
+    for (int t = 0; t < PATCH_MAX_NODES / 4; ++t) {
+      const int64_t k = p0 + q + 4 * t;
+      const int64_t kk = k < p1 ? k : p0;
+      c[t] = col[kk];
+      v[t] = val[kk];
     }
+#pragma unroll
+    for (int t = 0; t < PATCH_MAX_NODES / 4; ++t) xc[t] = x2[c[t]];
+#pragma unroll
+    for (int t = 0; t < PATCH_MAX_NODES / 4; ++t)
+      if (p0 + q + 4 * t < p1) {
+        s0 += v[t].x * xc[t].x + v[t].y * xc[t].y;
+        s1 += v[t].z * xc[t].x + v[t].w * xc[t].y;
+      }
   }
   s0 += __shfl_xor(s0, 1);
   s1 += __shfl_xor(s1, 1);
@@ -1064,12 +1084,11 @@ __global__ __launch_bounds__(256) void patch_kernel(int64_t c0, int64_t c1, cons
     r0 = vget(b, bs, J, 0) - s0;
     r1 = vget(b, bs, J, 1) - s1;
   }
-  const double* Up = U + i * ustride;
-  const int li = lane < 2 * m ? lane : 0;
   double delta = 0.0;
-  for (int jn = 0; jn < m; ++jn) {
+#pragma unroll
+  for (int jn = 0; jn < PATCH_MAX_NODES; ++jn) {
     const double a0 = __shfl(r0, 4 * jn), a1 = __shfl(r1, 4 * jn);
-    delta += Up[upk(li, 2 * jn)] * a0 + Up[upk(li, 2 * jn + 1)] * a1;
+    if (jn < m) delta += u[2 * jn] * a0 + u[2 * jn + 1] * a1;
   }
   if (lane < 2 * m) {
     const int64_t Ji = col[q0 + (lane >> 1)];
