@@ -4461,10 +4461,9 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   h->nv0 = plan.levels[0].nv;
   h->o0 = plan.levels[0].o0;
   h->o1 = plan.levels[0].o1;
-  // the rank-local operators re-homed as on one GPU (rehome_operators)
-  for (DDLevel& D : h->L)
-    if (!D.coarsest && !D.replicated)
-      for (DBsr* M : {&D.K, &D.A, &D.R, &D.PA, &D.P}) rehome_bsr(&h->allocs, *M);
+  // the rank-local operators are not re-homed: they are plain allocations
+  // made after the setup already, and a second copy measured 204-208 vs
+  // 209-214 applies/s (2 ranks, one GPU, profiles/r02_bench_2rank_rehome_ab.txt)
   std::vector<DOp> ops;
   dapply_ops(h.get(), nullptr, nullptr, &ops);
   for (const DOp& d : ops) h->apply_bytes += d.bytes;
