@@ -112,7 +112,7 @@ def main():
         args.pcg = 1 if int(os.environ.get('WORLD_SIZE', '1')) == 1 else 0
     prof = dict(smoother={'jacobi': 3, 'poly': 12, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
                 cycle_type={'V': 1, 'W': 2}[args.cycle], poly_degree=args.poly_degree,
-                Schwarz_type={'sgs': 3, 'gs': 1}.get(args.smoother, 4))
+                Schwarz_type={'sgs': 7, 'gs': 7}.get(args.smoother, 4))
 
     import torch
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -277,14 +277,14 @@ def main():
         for name, kw in (('mi355x_poly (Chebyshev degree 2 of node-block Jacobi)', dict(smoother=12)),
                          ('mi355x_sa_v (node-block Jacobi)', dict(smoother=3)),
                          ('mi355x_sgs (multicolour node-block SGS, coarse scaling ON)',
-                          dict(smoother=11, coarse_scaling=1, Schwarz_type=3)),
+                          dict(smoother=11, coarse_scaling=1, Schwarz_type=7)),
                          ('reference family: UA + parallel HEM + W-cycle + multicolour SGS + coarse scaling '
                           '(src/amg_parameters.py:67-89)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=3)),
+                               Schwarz_type=7)),
                          ('reference family, coarse_dof 2048 (dense solve instead of the launch-bound W bottom)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=3, coarse_dof=2048)),
+                               Schwarz_type=7, coarse_dof=2048)),
                          ('mi355x_patch: the reference\'s level-0 smoother (symmetric multiplicative Schwarz on '
                           'the overlapping 1-ring node patches, SCHWARZ_PATCHES), node-block Jacobi below',
                           dict(smoother=3, Schwarz_type=6)),

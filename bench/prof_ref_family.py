@@ -26,7 +26,7 @@ def main():
     s = M.problems.bidomain(3, n, 1e6)
     A = s.scipy()
     B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu', AMG_type=1, aggregation_type=5,
-                    cycle_type=2, smoother=11, coarse_scaling=1, Schwarz_type=3, coarse_dof=args.coarse_dof,
+                    cycle_type=2, smoother=11, coarse_scaling=1, Schwarz_type=7, coarse_dof=args.coarse_dof,
                     print_level=1)
     print('levels', B.num_levels, flush=True)
     r = torch.as_tensor(M.problems.seeded_rhs(s.N)).cuda()

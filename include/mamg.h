@@ -61,8 +61,16 @@ enum {                                                          /* smoother   */
 };
 enum {                                                   /* aggregation_type  */
   MAMG_VMB = 1, MAMG_MIS = 2, MAMG_MWM = 3, MAMG_HEC = 4, MAMG_HEM = 5
-};                                                       /* only MIS accepted */
+};  /* accepted: MIS (deterministic parallel MIS-2) and HEM (parallel heavy-edge
+       matching); VMB/MWM/HEC -> MAMG_ERR_UNSUPPORTED */
 enum {                                                   /* Schwarz_type      */
+  /* The reference's names (src/amg_parameters.py:83-87, src/utils.py:84):
+   * multiplicative Schwarz on the OVERLAPPING blocks seed + Schwarz_maxlvl
+   * ring.  SYMMETRIC with Schwarz_maxlvl 1 on a nodal system (num_functions
+   * 2) runs as MAMG_SCHWARZ_PATCHES (the same blocks and local solves);
+   * with Schwarz_maxlvl 0 the blocks are the seeds' nodes (no overlap) and
+   * the type must match the smoother (SYMMETRIC: SGS, FORWARD: GS).  Every
+   * other overlapping combination returns MAMG_ERR_UNSUPPORTED. */
   MAMG_SCHWARZ_FORWARD = 1, MAMG_SCHWARZ_BACKWARD = 2, MAMG_SCHWARZ_SYMMETRIC = 3,
   MAMG_SCHWARZ_BLOCK_JACOBI = 4, /* additive non-overlapping seed blocks (GPU) */
   MAMG_SCHWARZ_ADDITIVE = 5,     /* additive overlapping seed + maxlvl-ring blocks
@@ -72,7 +80,12 @@ enum {                                                   /* Schwarz_type      */
      node = both fields of its closed neighbourhood, exact local solves, in a
      distance-3 multicolour order; level 0, BSR2 layout, single GPU; needs a
      seed dof on every node (the bidomain's idofs) */
-  MAMG_SCHWARZ_PATCHES = 6
+  MAMG_SCHWARZ_PATCHES = 6,
+  /* the level smoother applied to NON-overlapping seed blocks (a seed plus
+     the non-seed dofs that join it, <= Schwarz_mmsize): additive with the
+     Jacobi family, multicolour forward with GS, symmetric with SGS (for the
+     bidomain: node-block SGS on level 0) */
+  MAMG_SCHWARZ_SEED_BLOCKS = 7
 };
 enum { MAMG_OFF = 0, MAMG_ON = 1 };
 enum { MAMG_COARSE_DENSE = 32 };  /* coarse_solver: 32 (UMFPACK in HAZmath)  */
@@ -92,7 +105,7 @@ typedef struct mamg_params {
   int32_t coarse_dof;        /* 100                                          */
   int32_t coarse_solver;     /* 32 -> dense direct                           */
   int32_t coarse_scaling;    /* MAMG_OFF | MAMG_ON: e <- <b_c,e>/<A_c e,e> e  */
-  int32_t aggregation_type;  /* MAMG_MIS (deterministic parallel MIS-2)      */
+  int32_t aggregation_type;  /* MAMG_MIS (parallel MIS-2) | MAMG_HEM          */
   double strong_coupled;     /* SoC threshold theta, 0.0                     */
   int32_t max_aggregation;   /* accepted, unused by MIS-2 (documented)       */
   int32_t amli_degree;       /* accepted, unused (no AMLI cycle)             */

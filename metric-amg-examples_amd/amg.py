@@ -59,6 +59,19 @@ def _dims(W, n):
     return dims
 
 
+def _with_functions(W, parameters, overrides):
+    """The reference's metricAMG receives the block space W (src/utils.py:86):
+    a W of k >= 2 equal-sized blocks (the bidomain's and EMI's P1 x P1) gives
+    num_functions = k unless the dict or an override sets it."""
+    if 'num_functions' in overrides or (parameters and 'num_functions' in parameters) \
+            or W is None or not isinstance(W, (list, tuple)) or len(W) < 2:
+        return overrides
+    dims = [int(w.dim()) if hasattr(w, 'dim') else int(w) for w in W]
+    if len(set(dims)) != 1:
+        return overrides
+    return dict(overrides, num_functions=len(dims))
+
+
 def _device_ptr(x):
     """(pointer, keepalive) for a torch CUDA tensor / object with data_ptr()."""
     if hasattr(x, 'data_ptr') and getattr(x, 'is_cuda', False):
@@ -120,7 +133,7 @@ class MetricAMG:
 
     def __init__(self, A, W=None, idofs=None, parameters=None, setup='auto', **overrides):
         self._L = _lib.lib()
-        self.params = make_params(parameters, **overrides)
+        self.params = make_params(parameters, **_with_functions(W, parameters, overrides))
         if idofs is not None:
             self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
             ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
@@ -482,7 +495,7 @@ class DistMetricAMG:
         indptr, indices, data, n, m = csr_arrays(A)
         self.shape = (n, n)
         self.W = _dims(W, n)
-        self.params = make_params(parameters, **overrides)
+        self.params = make_params(parameters, **_with_functions(W, parameters, overrides))
         self._A = (indptr, indices, data)
         csr = _lib.as_csr_struct(indptr, indices, data, m)
         if idofs is not None:

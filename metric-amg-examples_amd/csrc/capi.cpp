@@ -197,14 +197,15 @@ int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
   mamg_hier* h = new mamg_hier();
   std::string err;
-  Seeds S(idofs, n_idofs, v.n, params);
-  rc = mamg::host_setup(v, S.ptr, S.n, *params, &h->H, &err);
+  Seeds S(idofs, n_idofs, v.n, &P);
+  rc = mamg::host_setup(v, S.ptr, S.n, P, &h->H, &err);
   if (rc) { set_error(err); delete h; return rc; }
   *out = h;
   return MAMG_OK;
@@ -315,17 +316,18 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     int64_t rep_nodes, mamg_dhandle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
   mamg::Hierarchy H;
   std::string err;
-  Seeds S(idofs, n_idofs, v.n, params);
+  Seeds S(idofs, n_idofs, v.n, &P);
   // setup phases to stderr with print_level >= 2 (HAZmath's setup printing)
   auto t_0 = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
-    if (params->print_level < 2) return;
+    if (P.print_level < 2) return;
     const auto t = std::chrono::steady_clock::now();
     std::fprintf(stderr, "[mamg] rank %d/%d setup: %-24s %.3f s\n", rank, nranks, what,
                  std::chrono::duration<double>(t - t_0).count());
@@ -339,13 +341,13 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   mamg::GHier G;
   mamg::DevMat dA;
   bool on_device = false;   // rank-local operators built from G in HBM
-  if (params->num_functions == 2 && params->node_block_smoother &&
-      (params->AMG_type == MAMG_UA_AMG || params->sa_block_diag)) {
-    G.device = params->device;
-    mamg::dev_prereserve(params->device, v.nnz(), nranks);   // rank-local layout memory first
+  if (P.num_functions == 2 && P.node_block_smoother &&
+      (P.AMG_type == MAMG_UA_AMG || P.sa_block_diag)) {
+    G.device = P.device;
+    mamg::dev_prereserve(P.device, v.nnz(), nranks);   // rank-local layout memory first
     rc = mamg::upload_a0(v, &G, &dA, &err);
     lap("A0 upload");
-    if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err);
+    if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, P, &G, &err);
     lap("GPU setup");
     // default: ghost lists marked on the GPU, the rank's operators cut out of
     // G in HBM.  MAMG_DIST_TEST=full: the whole hierarchy downloaded and
@@ -358,7 +360,7 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     } else if (mode == 1) {
       rc = mamg::ghier_download(G, v, &H, &err);
     } else {
-      rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, params->post_fusion != 0, &H,
+      rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, P.post_fusion != 0, &H,
                                      &ghosts, &err, mode == 2);
       pre = !rc;
       on_device = !rc && mode != 2;
@@ -366,10 +368,10 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     lap(on_device ? "ghost lists" : "hierarchy download");
     if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
-  if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
+  if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, P, &H, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
-  rc = mamg::dist_upload(H, v, *params, rank, nranks, comm_id, rep_nodes, &d, &err, pre ? &ghosts : nullptr,
+  rc = mamg::dist_upload(H, v, P, rank, nranks, comm_id, rep_nodes, &d, &err, pre ? &ghosts : nullptr,
                          on_device ? &G : nullptr, on_device ? &dA : nullptr);
   lap("plan + rank-local upload");
   mamg::dev_prereserve_release();
@@ -453,17 +455,18 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
   mamg::Hierarchy H;
   std::string err;
-  Seeds S(idofs, n_idofs, v.n, params);
-  rc = mamg::host_setup(v, S.ptr, S.n, *params, &H, &err);
+  Seeds S(idofs, n_idofs, v.n, &P);
+  rc = mamg::host_setup(v, S.ptr, S.n, P, &H, &err);
   if (rc) { set_error(err); return rc; }
   mamg::DeviceHandle* d = nullptr;
-  rc = mamg::dev_upload(H, v, *params, &d, &err);
+  rc = mamg::dev_upload(H, v, P, &d, &err);
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
   return MAMG_OK;
@@ -474,23 +477,24 @@ int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                    const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
   std::string err;
   mamg::GHier G;
-  G.device = params->device;
+  G.device = P.device;
   mamg::DevMat dA;
-  Seeds S(idofs, n_idofs, v.n, params);
-  mamg::dev_prereserve(params->device, v.nnz(), 1);   // layout memory before the setup churn
-  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err))) {
+  Seeds S(idofs, n_idofs, v.n, &P);
+  mamg::dev_prereserve(P.device, v.nnz(), 1);   // layout memory before the setup churn
+  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, S.ptr, S.n, P, &G, &err))) {
     mamg::dev_prereserve_release();
     set_error(err);
     return rc;
   }
   mamg::DeviceHandle* d = nullptr;
-  rc = mamg::dev_from_ghier(&G, dA, *params, &d, &err);
+  rc = mamg::dev_from_ghier(&G, dA, P, &d, &err);
   mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
@@ -505,6 +509,7 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
     set_error("null argument");
     return MAMG_ERR_ARG;
   }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   if (dA->nrows <= 0 || dA->ncols <= 0 || dA->nnz < 0 || dA->nrows > INT32_MAX || dA->ncols > INT32_MAX) {
     set_error("bad CSR sizes");
@@ -519,13 +524,13 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
   M.val = const_cast<double*>(dA->values);
   std::string err;
   mamg::GHier G;
-  G.device = params->device;
-  Seeds S(idofs, n_idofs, M.n, params);
-  mamg::dev_prereserve(params->device, M.nnz, 1);   // layout memory before the setup churn
-  int rc = mamg::gpu_setup(M, S.ptr, S.n, *params, &G, &err);
+  G.device = P.device;
+  Seeds S(idofs, n_idofs, M.n, &P);
+  mamg::dev_prereserve(P.device, M.nnz, 1);   // layout memory before the setup churn
+  int rc = mamg::gpu_setup(M, S.ptr, S.n, P, &G, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DeviceHandle* d = nullptr;
-  rc = mamg::dev_from_ghier(&G, M, *params, &d, &err);
+  rc = mamg::dev_from_ghier(&G, M, P, &d, &err);
   mamg::dev_prereserve_release();
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
@@ -537,16 +542,17 @@ int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs
                         const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
   std::string err;
   mamg::GHier G;
-  G.device = params->device;
+  G.device = P.device;
   mamg::DevMat dA;
-  Seeds S(idofs, n_idofs, v.n, params);
-  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, S.ptr, S.n, *params, &G, &err))) {
+  Seeds S(idofs, n_idofs, v.n, &P);
+  if ((rc = mamg::upload_a0(v, &G, &dA, &err)) || (rc = mamg::gpu_setup(dA, S.ptr, S.n, P, &G, &err))) {
     set_error(err);
     return rc;
   }
@@ -568,6 +574,7 @@ int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params
                 mamg_handle** out) {
   GUARD_BEGIN
   if (!h || !out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v = h->H.A0;
   if (A) {
@@ -580,7 +587,7 @@ int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params
   }
   std::string err;
   mamg::DeviceHandle* d = nullptr;
-  int rc = mamg::dev_upload(h->H, v, *params, &d, &err);
+  int rc = mamg::dev_upload(h->H, v, P, &d, &err);
   if (rc) { set_error(err); return rc; }
   *out = new mamg_handle{d};
   return MAMG_OK;

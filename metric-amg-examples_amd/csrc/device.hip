@@ -110,12 +110,12 @@ __device__ __forceinline__ void vset(double* v, int64_t stride, int64_t I, int f
 // consecutive workgroups (neighbouring rows, which gather the same x entries)
 // would land in 8 different L2s.  Renumber so that every XCD walks one
 // contiguous range of rows (bijective for any grid size).
-__device__ __forceinline__ int64_t row_block(int remap) {
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ int64_t row_block_of(uint32_t b, uint32_t G, int remap) {
   if (!remap) return b;
-  const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = b & 7;
+  const uint32_t q = G >> 3, r = G & 7, x = b & 7;
   return (int64_t)(x * q + (x < r ? x : r) + (b >> 3));
 }
+__device__ __forceinline__ int64_t row_block(int remap) { return row_block_of(blockIdx.x, gridDim.x, remap); }
 
 // block k of a BSR2 value array: 4 doubles (0,0) (0,1) (1,0) (1,1) per block,
 // or in the symmetric-block format (SYM) two aligned streams: the diagonal
@@ -147,7 +147,7 @@ __device__ __forceinline__ double2 xget(const double* x, int64_t xs, int32_t c) 
   return reinterpret_cast<const double2*>(x)[c];
 }
 
-template <int VL, int EPI, bool XFM, bool SYM, int TAG>
+template <int VL, int EPI, bool XFM, bool SYM, int TAG, bool NT = false>
 __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
     const double* __restrict__ bval, const double* __restrict__ x, int64_t xs,
@@ -167,8 +167,8 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
       const int64_t ka = base + lane, kb = ka + VL;
       const bool ha = ka < p1, hb = kb < p1;
       const int64_t la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
-      const int32_t c0 = bcol[la], c1 = bcol[lb];
-      const dv4 v0 = blk<SYM>(bval, offd, la), v1 = blk<SYM>(bval, offd, lb);
+      const int32_t c0 = ldg<NT>(bcol + la), c1 = ldg<NT>(bcol + lb);
+      const dv4 v0 = blk<SYM, NT>(bval, offd, la), v1 = blk<SYM, NT>(bval, offd, lb);
       const double2 a = xget<XFM>(x, xs, c0), e = xget<XFM>(x, xs, c1);
       s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
       s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
@@ -343,6 +343,63 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   vset(out, os, node, 1, o1);
 }
 
+// Level-0 fused post operator z = x1 + W r1 + K e on the SELL-64 K with LPR
+// lanes per node row: a wavefront takes 64 / LPR rows of a 64-row slice, part
+// q < LPR - 1 of a row takes its blocks [q U, (q + 1) U), the last part the
+// rest in chunks of U, so a ~9-block row is one load -> gather round trip per
+// lane instead of two chained chunks of one lane.  For a fixed chunk slot the
+// lanes of one part read 64 / LPR consecutive slots.  The parts' sums meet by
+// a __shfl_xor butterfly (every lane of a row ends with the same bits), then
+// part f < 2 writes field f of the output; its epilogue operands (x1_f, W's
+// row f, r1) are loaded before the block loop.  LPR 2, U 5: K 1.46 -> 1.33 ms
+// at nrefs=6 on one upload (profiles/r03_kvariants*.txt).
+template <int LPR, int U, bool SPL, int TAG, int PROBE = 0>
+__global__ __launch_bounds__(256) void kpost_kernel(
+    int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
+    const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
+    const double* __restrict__ e, const double* __restrict__ x1, const double* __restrict__ r1,
+    const dv4* __restrict__ W, double* out, int64_t os) {
+  constexpr int RW = 64 / LPR;                          // rows per wavefront
+  const int lane = threadIdx.x & 63, q = lane / RW;
+  const int64_t node = (int64_t)blockIdx.x * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
+  const bool live = node < nr;
+  const int64_t nd = live ? node : nr - 1;            // dead lanes mirror the last row, write nothing
+  const int len = meta[nd] & 0xffff;
+  const int64_t k = soff[nd / SELL_C] + (nd & (SELL_C - 1));
+  const int f = q & 1;
+  const double yf = q < 2 ? x1[2 * nd + f] : 0.0;
+  const dv2 wf = q < 2 ? reinterpret_cast<const dv2*>(W + nd)[f] : dv2{0.0, 0.0};
+  const double2 rr = q < 2 ? reinterpret_cast<const double2*>(r1)[nd] : double2{0.0, 0.0};
+  double s0 = 0.0, s1 = 0.0;
+  const int j0 = q * U, j1 = q == LPR - 1 ? len : (len < j0 + U ? len : j0 + U);
+  for (int j = j0; j < j1; j += U) {
+    int32_t c[U];
+    dv4 v[U];
+    double2 a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
+      c[u] = bcol[kk];
+      v[u] = SPL ? blk_split(bval, nbs, kk) : blk<false>(bval, nullptr, kk);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)   // PROBE 1 (A/B only, wrong results): no gather, the column as the value
+      a[u] = PROBE ? double2{(double)c[u], 1.0} : reinterpret_cast<const double2*>(e)[c[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = j + u < j1;
+      s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+      s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+    }
+  }
+#pragma unroll
+  for (int off = RW; off < 64; off <<= 1) {   // addition commutes: all parts end bitwise equal
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+  }
+  if (live && q < 2) vset(out, os, node, f, yf + (wf.x * rr.x + wf.y * rr.y) + (f ? s1 : s0));
+}
+
 // ---------------------------------------------------------------------------
 // Half-symmetric ELL-64 for a symmetric A0 (A_JI = A_IJ^T bitwise and every
 // block symmetric, so A_JI = A_IJ): only the upper part J >= I is streamed
@@ -460,6 +517,120 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
   }
   vset(out, os, node, 0, o0);
   vset(out, os, node, 1, o1);
+}
+
+// hsell2_kernel with two lanes per node row: part 0 sums the lower blocks
+// (mirror pointers), part 1 the upper blocks then the ghost blocks, and the
+// row's sum is lower + (upper + ghost) on both lanes (__shfl_xor 32).  A
+// workgroup takes half of a 256-row block of the one-lane kernel: workgroup
+// b = 8 i + x (XCD x) takes half i & 1 of the one-lane kernel's workgroup
+// x + 8 (i >> 1), so every XCD walks the same rows in the same band order.
+template <int EPI, bool XFM, int U, bool GH, int TAG>
+__global__ __launch_bounds__(256) void hsell2x2_kernel(
+    int64_t row0, int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
+    const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
+    const int64_t* __restrict__ gsoff, const int32_t* __restrict__ gcol, const double* __restrict__ gval,
+    int64_t ngs, const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
+    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap,
+    const int32_t* __restrict__ sched, uint32_t G) {
+  const uint32_t bx = blockIdx.x, xcd = bx & 7, i = bx >> 3;
+  const uint32_t ob = xcd + 8 * (i >> 1);
+  if (ob >= G) return;
+  const int64_t blk0 = sched ? (int64_t)sched[ob] : row_block_of(ob, G, remap);
+  const int lane = threadIdx.x & 63, q = lane >> 5;
+  const int64_t node0 = row0 + blk0 * 256 + (i & 1) * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+  const bool live = node0 < nr;
+  const int64_t node = live ? node0 : nr - 1;
+  const double* offd = uval + 2 * nbs;
+  const int m = meta[node];
+  const uint32_t urow = 64u * (uint32_t)hwu;
+  double s0 = 0.0, s1 = 0.0;
+  if (q == 0) {
+    const int llen = (m >> 8) & 0xff;
+    const int64_t k = (node >> 6) * (int64_t)(64 * hwl) + (node & 63);
+    for (int j = 0; j < llen; j += U) {
+      uint32_t p[U];
+      dv4 v[U];
+      double2 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) p[u] = (uint32_t)lptr[k + (int64_t)SELL_C * (j + u < llen ? j + u : llen - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t c = (int32_t)((p[u] / urow) * 64u + (p[u] & 63u));
+        v[u] = blk<true>(uval, offd, p[u]);
+        a[u] = xget<XFM>(x, xs, c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j + u < llen;
+        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+      }
+    }
+  } else {
+    const int ulen = m & 0xff;
+    const int64_t k = (node >> 6) * (int64_t)urow + (node & 63);
+    for (int j = 0; j < ulen; j += U) {
+      int32_t c[U];
+      dv4 v[U];
+      double2 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t kk = k + (int64_t)SELL_C * (j + u < ulen ? j + u : ulen - 1);
+        c[u] = ucol[kk];
+        v[u] = blk<true>(uval, offd, kk);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j + u < ulen;
+        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+      }
+    }
+    if (GH) {
+      const int glen = m >> 16;
+      const int64_t kg = gsoff[node >> 6] + (node & 63);
+      const double* goff = gval + 2 * ngs;
+      for (int j = 0; j < glen; j += U) {
+        int32_t c[U];
+        dv4 v[U];
+        double2 a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t kk = kg + (int64_t)SELL_C * (j + u < glen ? j + u : glen - 1);
+          c[u] = gcol[kk];
+          v[u] = blk<true>(gval, goff, kk);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = j + u < glen;
+          s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
+          s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
+        }
+      }
+    }
+  }
+  s0 += __shfl_xor(s0, 32);
+  s1 += __shfl_xor(s1, 32);
+  if (!live) return;
+  const int f = q;
+  double o;
+  if (EPI == EPI_Y) {
+    o = f ? s1 : s0;
+  } else if (EPI == EPI_YADD) {
+    o = y[2 * node + f] + (f ? s1 : s0);
+  } else if (EPI == EPI_RESID) {
+    o = vget(b, bs, node, f) - (f ? s1 : s0);
+  } else {  // EPI_BJAC
+    const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
+    const dv2 w = reinterpret_cast<const dv2*>(W + node)[f];
+    o = y[2 * node + f] + (w.x * r0 + w.y * r1);
+  }
+  vset(out, os, node, f, o);
 }
 
 // fused prolongation + first post sweep on a SELL-64 [P | AP] (see
@@ -1216,10 +1387,22 @@ constexpr int64_t g_sell_max_len = 40;
 int g_half = 1;
 int g_half_bands = 1;
 int g_post_k = 1;
+int g_kvar = 0;
+int g_rvar = 0;
+int g_rrvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
+void read_kvar() {
+  const char* e = std::getenv("MAMG_K_VARIANT");
+  g_kvar = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_R_VARIANT");
+  g_rvar = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_RR_VARIANT");
+  g_rrvar = e ? std::atoi(e) : 0;
+}
 void read_knobs() {
+  read_kvar();
   const char* e = std::getenv("MAMG_POST_K");
-  g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K, layout timed; 2 / 3: K, split / block forced
+  g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
   e = std::getenv("MAMG_HALF");
@@ -1392,6 +1575,8 @@ struct DeviceHandle {
   std::vector<void*> allocs;
   char* arena = nullptr;           // pre-reserved HBM, bump-allocated (dev_prereserve)
   size_t arena_left = 0;
+  char* arena0 = nullptr;          // the reservation's range [arena0, arena1)
+  char* arena1 = nullptr;
   hipStream_t cap = nullptr;
   std::vector<Graph> graphs;
   double* hr = nullptr;            // host-apply staging (device)
@@ -2814,7 +2999,11 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
   if (g == 0) return;
 #define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o)
   switch (o.epi) {
-    case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_Y:
+      // the level-0 restriction with non-temporal matrix loads (A/B, MAMG_RR_VARIANT=1)
+      if (TAG == 0 && o.remap && g_rrvar == 1) bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG, true><<<g, 256, 0, s>>>(BSR_ARGS);
+      else bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS);
+      break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_KPOST:   // K is never symmetric and e is node-major
@@ -2845,10 +3034,36 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 #undef SELL_ARGS
 }
 
+template <int LPR, int U, bool SPL, int PROBE = 0>
+void launch_kpost(const Op& o, hipStream_t s) {
+  const DBsr& M = *o.Mb;
+  const int64_t rows = 256 / LPR;
+  const unsigned g = (unsigned)((M.nr + rows - 1) / rows);
+  if (g == 0) return;
+  kpost_kernel<LPR, U, SPL, 0, PROBE><<<g, 256, 0, s>>>(M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.y, o.b,
+                                                        o.W, o.out, o.os);
+}
+
+// the level-0 K kernel (MAMG_K_VARIANT for A/Bs, read at upload and by
+// mamg_time_apply): 0 two lanes per row, chunks of 5 (default); 1 one lane
+// per row, chunks of 6 (sell2_kernel, round 2); 2 four lanes per row, chunks of 3
+template <bool SPL>
+bool launch_kvariant(const Op& o, hipStream_t s) {
+  switch (g_kvar) {
+    case 1: return false;
+    case 2: launch_kpost<4, 3, SPL>(o, s); return true;
+    case 9: launch_kpost<2, 5, SPL, 1>(o, s); return true;   // probe: no e gathers (wrong results)
+    default: launch_kpost<2, 5, SPL>(o, s); return true;
+  }
+}
+
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   // level-0 K operator: chunks of 6 blocks (two chunks cover its ~9-block
   // rows); everything else 8
+  if constexpr (TAG == 0 && !XFM && !SYM) {
+    if (o.epi == EPI_KPOST && (o.Mb->split ? launch_kvariant<true>(o, s) : launch_kvariant<false>(o, s))) return;
+  }
   if (o.Mb->split && TAG == 0) launch_sell_u<XFM, SYM, g_post_u, true, TAG>(o, s);
   else if (o.Mb->split) launch_sell_u<XFM, SYM, g_sell_u, true, TAG>(o, s);
   else if (TAG == 0 && o.epi == EPI_KPOST) launch_sell_u<XFM, SYM, g_post_u, false, TAG>(o, s);
@@ -2911,6 +3126,17 @@ void launch_half_u(const Op& o, hipStream_t s) {
     o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, 1, \
     (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched \
     : (r0 == M.sr0 && r1 == M.sr1 && (int64_t)g == M.nsched_r) ? M.sched_r : nullptr
+  if (g_rvar == 1) {   // two lanes per row (A/B, MAMG_R_VARIANT)
+    const unsigned g2 = 16 * ((g + 7) / 8);
+    switch (o.epi) {
+      case EPI_Y: hsell2x2_kernel<EPI_Y, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
+      case EPI_YADD: hsell2x2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
+      case EPI_RESID: hsell2x2_kernel<EPI_RESID, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
+      case EPI_KPOST: break;
+      default: hsell2x2_kernel<EPI_BJAC, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
+    }
+    return;
+  }
   switch (o.epi) {
     case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
@@ -3084,7 +3310,10 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // The arena's copies stay unused.
 // move one array into a fresh, physically contiguous allocation (plain
 // hipMalloc where the driver has none; the old copy is kept if both fail)
-void rehome_array(std::vector<void*>* allocs, void** ptr, size_t b) {
+// hipMalloc (the old copy is kept if both fail).  An old copy of its own
+// allocation is freed; one inside the pre-reserved arena stays (the arena is
+// one allocation).
+void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
   void* r = nullptr;
   if (!*ptr || b == 0) return;
   if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
@@ -3094,99 +3323,70 @@ void rehome_array(std::vector<void*>* allocs, void** ptr, size_t b) {
     (void)hipFree(r);
     return;
   }
-  allocs->push_back(r);
+  void* old = *ptr;
+  h->allocs.push_back(r);
   *ptr = r;
+  const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
+  auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
+  if (!in_arena && it != h->allocs.end()) {
+    (void)hipFree(old);
+    h->allocs.erase(it);
+  }
 }
 
 // values and columns of one operator (half-symmetric: the upper part)
-void rehome_bsr(std::vector<void*>* allocs, DBsr& M) {
+void rehome_bsr(DeviceHandle* h, DBsr& M) {
   if (M.nr == 0) return;
   const int64_t slots = (M.sell || M.half) ? M.nbs : M.nb;
-  rehome_array(allocs, (void**)&M.val, (size_t)slots * ((M.sym || M.half) ? 3 : 4) * sizeof(double));
-  rehome_array(allocs, (void**)&M.col, (size_t)slots * sizeof(int32_t));
+  rehome_array(h, (void**)&M.val, (size_t)slots * ((M.sym || M.half) ? 3 : 4) * sizeof(double));
+  rehome_array(h, (void**)&M.col, (size_t)slots * sizeof(int32_t));
 }
 
 void rehome_operators(DeviceHandle* h) {
-  if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell) return;
+  const char* e = std::getenv("MAMG_REHOME");   // 0: keep the operators where the layout builder put them (tests)
+  if (e && std::atoi(e) == 0) return;
+  if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < g_sell_min_rows || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
-  rehome_bsr(&h->allocs, L.KPb);          // the largest stream first
-  if (L.Ab.half) rehome_bsr(&h->allocs, L.Ab);
+  rehome_bsr(h, L.KPb);          // the largest stream first
+  if (L.Ab.half) rehome_bsr(h, L.Ab);
   if (!L.Rb.sell && !L.Rb.sym)
-    rehome_array(&h->allocs, (void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
+    rehome_array(h, (void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
   // the coarser levels' operators too (coarse levels 0.41 -> 0.395 ms per apply)
   for (size_t l = 1; l < h->L.size(); ++l) {
     DLevel& D = h->L[l];
     if (D.coarsest) break;
     for (DBsr* M : {&D.Ab, &D.KPb, &D.Rb, &D.Pb})
-      if (!M->half) rehome_bsr(&h->allocs, *M);
+      if (!M->half) rehome_bsr(h, *M);
   }
 }
 
-// Block layout of the level-0 K values, chosen on the device at hand.  One
-// 32-byte block per SELL slot, or two 16-byte streams per slot (sell2_kernel
-// SPL: each wave load 1 KB contiguous).  Which is faster depends on the box,
-// for the same bytes: K 1.712 -> 1.572 ms split on one MI355X, 1.64 -> 1.745 ms
-// on another (alternating processes, profiles/r02_ab_k_split.txt).  Both are
-// timed in the same allocation (the values are rearranged in place) over
-// whole eager applies, and the faster is kept; the arithmetic is the same, so
-// results are bitwise equal either way.
-// MAMG_POST_K=2 / =3 force the split / block layout on every SELL-stored K
-// (tests: both layouts at small sizes).
-void choose_k_layout(DeviceHandle* h) {
-  if (!h->bsr || h->L.size() < 2 || g_post_k == 3) return;
-  if (g_post_k == 2) {                       // forced split, every level stored SELL
-    for (DLevel& D : h->L) {
-      if (D.coarsest || !D.KPb.sell || D.KPb.sym || D.KPb.split) continue;
-      void* t = nullptr;
-      if (hipMalloc(&t, (size_t)D.KPb.nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
-      split_blocks_kernel<<<nblocks(D.KPb.nbs), 256>>>(D.KPb.nbs, reinterpret_cast<const dv4*>(D.KPb.val), (dv2*)t);
-      (void)hipMemcpy(D.KPb.val, t, (size_t)D.KPb.nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
-      (void)hipFree(t);
-      D.KPb.split = true;
-    }
-    return;
-  }
-  if (h->L[0].KPb.nr < (1 << 20) || !h->L[0].KPb.sell || h->L[0].KPb.sym) return;
-  DLevel& L = h->L[0];
-  const int64_t nbs = L.KPb.nbs;
-  void* tmp = nullptr;
-  if (hipMalloc(&tmp, (size_t)nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
-  (void)hipMemset(h->hr, 0, L.n * sizeof(double));
-  std::vector<Op> ops;
-  apply_ops(h, h->hr, h->hz, &ops);
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
-  auto time_apply = [&]() {
-    for (int i = 0; i < 2; ++i) for (const Op& o : ops) launch(o, nullptr);
-    (void)hipEventRecord(e0, nullptr);
-    for (int i = 0; i < 6; ++i) for (const Op& o : ops) launch(o, nullptr);
-    (void)hipEventRecord(e1, nullptr);
-    (void)hipEventSynchronize(e1);
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    return ms / 6;
-  };
-  auto rearrange = [&](bool to_split) {
-    if (to_split)
-      split_blocks_kernel<<<nblocks(nbs), 256>>>(nbs, reinterpret_cast<const dv4*>(L.KPb.val), (dv2*)tmp);
-    else
-      unsplit_blocks_kernel<<<nblocks(nbs), 256>>>(nbs, reinterpret_cast<const dv2*>(L.KPb.val), (dv4*)tmp);
-    (void)hipMemcpy(L.KPb.val, tmp, (size_t)nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
-    L.KPb.split = to_split;
-  };
-  const float t_block = time_apply();
-  rearrange(true);
-  const float t_split = time_apply();
-  if (t_split >= t_block) rearrange(false);
-  if (h->p.print_level >= 2)
-    std::fprintf(stderr, "[mamg] K layout: one block per slot %.4f ms/apply, split %.4f ms/apply -> %s\n", t_block,
-                 t_split, L.KPb.split ? "split" : "block");
-  (void)hipDeviceSynchronize();
-  (void)hipFree(tmp);
-  (void)hipGetLastError();
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+// Block layout of a SELL-stored K's values: one 32-byte block per slot, or two
+// 16-byte streams per slot (SPL: each wave load reads contiguous pairs).  The
+// arithmetic is the same, so results are bitwise equal either way
+// (test_k_block_layouts_bitwise).  Rearranged in place through a temporary.
+void set_k_split(DBsr& K, bool to_split) {
+  if (!K.sell || K.sym || K.split == to_split || K.nbs == 0) return;
+  void* t = nullptr;
+  if (hipMalloc(&t, (size_t)K.nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
+  if (to_split)
+    split_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (dv2*)t);
+  else
+    unsplit_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv2*>(K.val), (dv4*)t);
+  (void)hipMemcpy(K.val, t, (size_t)K.nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
+  (void)hipFree(t);
+  K.split = to_split;
+}
+
+// Round 2 chose the layout per box by timing both at upload (split 1.57 vs
+// 1.71 ms on one box, the opposite on another).  With the two-lanes-per-row
+// K kernel (kpost_kernel) the one-block layout is kept everywhere
+// (DESIGN.md section 4); MAMG_POST_K=2 forces the split layout on every
+// SELL-stored K (tests), MAMG_K_LAYOUT=split|block switches level 0 at
+// mamg_time_apply (A/Bs on one upload).
+void apply_k_layout_knob(DeviceHandle* h) {
+  if (!h->bsr || h->L.size() < 2 || g_post_k != 2) return;
+  for (DLevel& D : h->L)
+    if (!D.coarsest) set_k_split(D.KPb, true);
 }
 
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
@@ -3203,8 +3403,11 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   h->L.resize(nl);
   h->bsr = bsr_eligible(H, A0, p);
   read_knobs();
-  if (gs_smoother(p) && !h->bsr) {
-    *err = "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned smoother blocks)";
+  if ((gs_smoother(p) || patch_schwarz(p)) && !h->bsr) {
+    *err = patch_schwarz(p) ? "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on "
+                              "every level)"
+                            : "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned "
+                              "smoother blocks)";
     return MAMG_ERR_UNSUPPORTED;
   }
   int rc;
@@ -3287,7 +3490,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
-  choose_k_layout(h.get());
+  apply_k_layout_knob(h.get());
   *out = h.release();
   return MAMG_OK;
 }
@@ -3334,6 +3537,10 @@ void adopt_prereserve(HT* h) {
   h->allocs.push_back(g_pre);
   h->arena = (char*)g_pre;
   h->arena_left = g_pre_bytes;
+  if constexpr (std::is_same<HT, DeviceHandle>::value) {
+    h->arena0 = (char*)g_pre;
+    h->arena1 = (char*)g_pre + g_pre_bytes;
+  }
   g_pre = nullptr;
   g_pre_bytes = 0;
   g_pre_dev = -1;
@@ -3408,7 +3615,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
-  choose_k_layout(h.get());
+  apply_k_layout_knob(h.get());
   h->setup_ms[GS_LAYOUT] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = h.release();
@@ -3580,6 +3787,12 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
   hipStream_t s = (hipStream_t)stream;
   int rc = order_begin(h, s, err);
   if (rc) return rc;
+  read_kvar();   // A/B of the K kernel variants on one upload (eager launches)
+  if (const char* kl = std::getenv("MAMG_K_LAYOUT"))
+    if (h->bsr && h->L.size() > 1) {
+      set_k_split(h->L[0].KPb, std::strcmp(kl, "split") == 0);
+      HIPCHK(hipDeviceSynchronize());
+    }
   std::vector<Op> ops;
   apply_ops(h, d_r, d_z, &ops);
   if (class_bytes) {

@@ -60,6 +60,7 @@ struct Hierarchy {
 // setup.cpp
 int host_setup(const CsrView& A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* out, std::string* err);
+mamg_params resolve_params(const mamg_params& in);
 int check_params(const mamg_params& p, std::string* err);
 int check_patch_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err);
 // SMOOTHER_POLY step weights w[0..poly_degree) (oracle mamg_oracle.poly_weights)

@@ -913,6 +913,23 @@ int poly_weights(const mamg_params& p, double* w) {
   return m;
 }
 
+// The reference's Schwarz_type names mean multiplicative Schwarz on the
+// overlapping blocks seed + Schwarz_maxlvl ring (src/amg_parameters.py:83-87,
+// comment src/utils.py:84).  SYMMETRIC on the 1-rings of a nodal system is
+// exactly SCHWARZ_PATCHES (one patch per seeded node: both fields of its closed
+// neighbourhood, exact local solves), so it runs as that; check_patch_seeds
+// then requires a seed on every node.  With Schwarz_maxlvl 0 the blocks are
+// the seeds' nodes, which do not overlap: the matching level smoother on the
+// seed blocks.  Anything else keeps its name and check_params rejects it.
+mamg_params resolve_params(const mamg_params& in) {
+  mamg_params p = in;
+  if (p.Schwarz_levels < 1) return p;
+  if (p.Schwarz_type == MAMG_SCHWARZ_SYMMETRIC && p.Schwarz_maxlvl == 1 && p.num_functions == 2 &&
+      p.node_block_smoother)
+    p.Schwarz_type = MAMG_SCHWARZ_PATCHES;
+  return p;
+}
+
 int check_params(const mamg_params& p, std::string* err) {
   if (p.abi_version != MAMG_ABI_VERSION) { *err = "mamg_params.abi_version mismatch"; return MAMG_ERR_ARG; }
   if (p.AMG_type != MAMG_SA_AMG && p.AMG_type != MAMG_UA_AMG) { *err = "AMG_type must be SA_AMG or UA_AMG"; return MAMG_ERR_UNSUPPORTED; }
@@ -941,26 +958,45 @@ int check_params(const mamg_params& p, std::string* err) {
   if (p.coarse_solver != MAMG_COARSE_DENSE) { *err = "coarse_solver must be 32 (direct)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels > 1) { *err = "Schwarz_levels > 1 not supported (seeds exist on level 0 only)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels == 1) {
-    // the level-0 seed blocks are smoothed by the level smoother: additive
-    // (block Jacobi) with the Jacobi smoothers, multiplicative in colour order
-    // with GS (forward) / SGS (symmetric)
+    // (after resolve_params) the level-0 blocks: the reference's overlapping
+    // multiplicative form as node patches, additive overlapping rings, or the
+    // level smoother on non-overlapping seed blocks
     const bool gsm = p.smoother == MAMG_SMOOTHER_GS || p.smoother == MAMG_SMOOTHER_SGS;
-    const int want = p.smoother == MAMG_SMOOTHER_SGS ? MAMG_SCHWARZ_SYMMETRIC
-                     : p.smoother == MAMG_SMOOTHER_GS ? MAMG_SCHWARZ_FORWARD : MAMG_SCHWARZ_BLOCK_JACOBI;
-    const bool additive_ok = !gsm && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE;
-    if (p.Schwarz_type == MAMG_SCHWARZ_PATCHES) {
+    const int t = p.Schwarz_type;
+    if (t == MAMG_SCHWARZ_PATCHES) {
       if (p.num_functions != 2 || !p.node_block_smoother || p.Schwarz_maxlvl != 1) {
         *err = "SCHWARZ_PATCHES (multiplicative node-patch Schwarz) needs num_functions 2, node_block_smoother 1 "
                "and Schwarz_maxlvl 1";
         return MAMG_ERR_UNSUPPORTED;
       }
-    } else if (p.Schwarz_type != want && !additive_ok) {
-      *err = std::string("Schwarz_type must match the smoother: SCHWARZ_BLOCK_JACOBI with the Jacobi smoothers, ") +
-             "SCHWARZ_SYMMETRIC with SMOOTHER_SGS, SCHWARZ_FORWARD with SMOOTHER_GS (SCHWARZ_ADDITIVE: overlapping "
-             "seed rings with the Jacobi-family smoothers)";
-      return MAMG_ERR_UNSUPPORTED;
+    } else if (t == MAMG_SCHWARZ_SYMMETRIC || t == MAMG_SCHWARZ_FORWARD || t == MAMG_SCHWARZ_BACKWARD) {
+      if (p.Schwarz_maxlvl >= 1) {
+        *err = std::string("Schwarz_type ") + (t == MAMG_SCHWARZ_SYMMETRIC ? "SYMMETRIC" : t == MAMG_SCHWARZ_FORWARD ? "FORWARD" : "BACKWARD") +
+               " with Schwarz_maxlvl " + std::to_string(p.Schwarz_maxlvl) +
+               " is multiplicative Schwarz on overlapping seed + ring blocks; implemented only as SYMMETRIC with "
+               "Schwarz_maxlvl 1 on nodal systems (num_functions 2, a seed on every node: SCHWARZ_PATCHES). "
+               "Alternatives: SCHWARZ_ADDITIVE (the same overlapping blocks, additive) or SCHWARZ_SEED_BLOCKS "
+               "(non-overlapping blocks, the level smoother)";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+      const int want = p.smoother == MAMG_SMOOTHER_SGS ? MAMG_SCHWARZ_SYMMETRIC
+                       : p.smoother == MAMG_SMOOTHER_GS ? MAMG_SCHWARZ_FORWARD : -1;
+      if (t != want) {
+        *err = "Schwarz_type SYMMETRIC / FORWARD on the seeds' nodes (Schwarz_maxlvl 0) must match the smoother "
+               "(SMOOTHER_SGS / SMOOTHER_GS); SCHWARZ_SEED_BLOCKS applies any level smoother to the seed blocks";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+    } else if (t == MAMG_SCHWARZ_ADDITIVE || t == MAMG_SCHWARZ_BLOCK_JACOBI) {
+      if (gsm) {
+        *err = "SCHWARZ_ADDITIVE / SCHWARZ_BLOCK_JACOBI are additive: use them with the Jacobi-family smoothers "
+               "(SCHWARZ_SEED_BLOCKS or SCHWARZ_SYMMETRIC / FORWARD with Schwarz_maxlvl 0 for GS / SGS)";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+    } else if (t != MAMG_SCHWARZ_SEED_BLOCKS) {
+      *err = "unknown Schwarz_type " + std::to_string(t);
+      return MAMG_ERR_ARG;
     }
-    if (p.Schwarz_maxlvl > 1 && p.Schwarz_type != MAMG_SCHWARZ_ADDITIVE) {
+    if (p.Schwarz_maxlvl > 1 && t != MAMG_SCHWARZ_ADDITIVE) {
       *err = "Schwarz_maxlvl > 1 needs SCHWARZ_ADDITIVE (overlapping seed + ring blocks); the non-overlapping "
              "seed blocks are the seeds' 1-rings";
       return MAMG_ERR_UNSUPPORTED;
@@ -989,6 +1025,7 @@ int check_params(const mamg_params& p, std::string* err) {
 // (the bidomain's idofs = every u2 dof, src/bidomain_3d.py:138)
 int check_patch_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err) {
   if (p.Schwarz_levels < 1 || p.Schwarz_type != MAMG_SCHWARZ_PATCHES) return MAMG_OK;
+  if (n < 2 || n % 2) { *err = "SCHWARZ_PATCHES needs a nodal system of even size (num_functions 2)"; return MAMG_ERR_ARG; }
   const int64_t nv = n / 2;
   std::vector<char> has(nv, 0);
   for (int64_t i = 0; i < n_idofs; ++i)

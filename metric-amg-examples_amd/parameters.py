@@ -7,24 +7,31 @@ values are build-defined (HAZmath's are not available here).
 * ``parameters_standard``, ``parameters_standard_schwarz``,
   ``parameters_metric``, ``parameters_metric_schwarz``: the reference's
   presets with their values verbatim.  ``MetricAMG`` runs what they select
-  (parameters_metric(_schwarz): UA + parallel HEM + W-cycle + multicolour SGS
-  + coarse scaling, on nodal systems) or raises MAMG_ERR_UNSUPPORTED naming
-  the component it lacks (VMB aggregation; SGS on scalar systems); there is
-  no silent substitution under these names.
+  (parameters_metric_schwarz: UA + parallel HEM + W-cycle + multicolour SGS
+  + coarse scaling, and on level 0 the reference's SCHWARZ_SYMMETRIC on the
+  seeds' overlapping 1-ring blocks, which on a nodal system with a seed on
+  every node is exactly ``SCHWARZ_PATCHES``) or raises MAMG_ERR_UNSUPPORTED
+  naming the component it lacks (VMB aggregation; SGS on scalar systems;
+  multiplicative Schwarz on overlapping blocks of sparse seed sets); there
+  is no silent substitution under these names.  ``MetricAMG(A, W, ...)``
+  takes ``num_functions`` from W (equal-sized blocks) when the dict does
+  not set it, as the reference's metricAMG receives the block space W.
 * ``parameters_metric_mi355x``: the GPU profile "mi355x_sa_v" (nodal SA,
   V-cycle, node-block Jacobi): the north star's profile, the drivers' and
   the bench's default.
 * ``parameters_metric_mi355x_poly``: the same with the Chebyshev smoother --
   the shortest time to solution measured.
 * ``parameters_metric_mi355x_sgs``: the reference's smoother family on the
-  GPU: multicolour node-block SGS on every level (level 0: multiplicative
-  Schwarz on the seed blocks), coarse-grid correction scaling ON.
+  GPU: multicolour node-block SGS on every level (level 0: the SGS order on
+  the non-overlapping seed blocks, ``SCHWARZ_SEED_BLOCKS``), coarse-grid
+  correction scaling ON.
 * ``parameters_metric_mi355x_patch``: the reference's level-0 smoother --
   symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
   (``SCHWARZ_PATCHES``), node-block Jacobi below.
-  ``SCHWARZ_SYMMETRIC`` itself names multiplicative Schwarz on the
-  non-overlapping seed blocks (node blocks); ``to_gpu_profile`` maps the
-  reference's SYMMETRIC 1-ring blocks onto ``SCHWARZ_PATCHES``.
+  ``SCHWARZ_SYMMETRIC`` keeps the reference's meaning (overlapping
+  seed + ``Schwarz_maxlvl``-ring blocks): with ``Schwarz_maxlvl`` 1 on a
+  nodal system it runs as ``SCHWARZ_PATCHES``; ``SCHWARZ_SEED_BLOCKS``
+  names the non-overlapping seed blocks under the level smoother.
 * ``parameters_metric_3d1d``: additive overlapping Schwarz on the 1-D seeds'
   rings.
 * ``to_gpu_profile(d)``: explicit opt-in mapping of a HAZmath dict onto
@@ -48,6 +55,7 @@ SCHWARZ_FORWARD, SCHWARZ_BACKWARD, SCHWARZ_SYMMETRIC, SCHWARZ_BLOCK_JACOBI = 1, 
 SCHWARZ_ADDITIVE = 5          # overlapping seed + Schwarz_maxlvl-ring blocks, additive (sparse seed sets)
 SCHWARZ_PATCHES = 6           # the reference's overlapping seed + 1-ring blocks, symmetric multiplicative
                               # (one patch per node, distance-3 multicolour order; level 0, nodal)
+SCHWARZ_SEED_BLOCKS = 7       # the level smoother on non-overlapping seed blocks (seed + joined non-seeds)
 OFF, ON = 0, 1
 SOLVER_UMFPACK = 32          # coarse_solver / Schwarz_blksolver: dense direct here
 
@@ -102,11 +110,11 @@ parameters_metric_3d1d = dict(
     Schwarz_mmsize=200, coarse_dof=300, max_levels=30)
 
 # the reference's smoothers on the GPU: multicolour
-# node-block SGS (level 0: symmetric multiplicative Schwarz on the seed blocks)
-# and coarse-grid correction scaling, on the nodal SA V-cycle
+# node-block SGS (level 0: the same SGS order on the non-overlapping seed
+# blocks) and coarse-grid correction scaling, on the nodal SA V-cycle
 parameters_metric_mi355x_sgs = dict(
     parameters_metric_mi355x, smoother=SMOOTHER_SGS, coarse_scaling=ON,
-    Schwarz_type=SCHWARZ_SYMMETRIC)
+    Schwarz_type=SCHWARZ_SEED_BLOCKS)
 
 # the reference's level-0 smoother on the GPU:
 # symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
@@ -151,26 +159,33 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
         notes.append('aggregation_type %r -> MIS (deterministic parallel MIS-2)'
                      % out.get('aggregation_type'))
         out['aggregation_type'] = MIS
-    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_maxlvl', 1) > 1:
-        notes.append('Schwarz_maxlvl %d -> 1 (non-overlapping partition of the seeds\' 1-rings)'
-                     % out['Schwarz_maxlvl'])
-        out['Schwarz_maxlvl'] = 1
     if out.get('Schwarz_levels', 0) > 1:
         notes.append('Schwarz_levels %d -> 1' % out['Schwarz_levels'])
         out['Schwarz_levels'] = 1
     smo = out.get('smoother', SMOOTHER_JACOBI_RHO)
-    want = {SMOOTHER_SGS: SCHWARZ_SYMMETRIC, SMOOTHER_GS: SCHWARZ_FORWARD}.get(smo, SCHWARZ_BLOCK_JACOBI)
-    if out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type') == SCHWARZ_SYMMETRIC \
-            and out.get('Schwarz_maxlvl', 1) == 1:
-        notes.append('Schwarz_type SCHWARZ_SYMMETRIC on the seeds\' 1-rings -> SCHWARZ_PATCHES (the same '
-                     'overlapping blocks, multiplicative in a distance-3 multicolour order; nodal systems '
-                     'with a seed on every node)')
-        out['Schwarz_type'] = SCHWARZ_PATCHES
-        out['num_functions'] = 2
-    elif out.get('Schwarz_levels', 0) >= 1 and out.get('Schwarz_type', want) != want:
-        notes.append('Schwarz_type %r -> %r (the level-0 seed blocks use the level smoother)'
-                     % (out.get('Schwarz_type'), want))
-        out['Schwarz_type'] = want
+    gsm = smo in (SMOOTHER_GS, SMOOTHER_SGS)
+    st, lvl = out.get('Schwarz_type'), out.get('Schwarz_maxlvl', 1)
+    if out.get('Schwarz_levels', 0) >= 1:
+        if st == SCHWARZ_SYMMETRIC and lvl == 1:
+            # the library runs this as given on a nodal system; stated here too
+            notes.append('Schwarz_type SCHWARZ_SYMMETRIC on the seeds\' 1-rings = SCHWARZ_PATCHES (the same '
+                         'overlapping blocks, multiplicative in a distance-3 multicolour order; nodal systems '
+                         'with a seed on every node)')
+            out['Schwarz_type'] = SCHWARZ_PATCHES
+            out['num_functions'] = 2
+        elif st in (SCHWARZ_SYMMETRIC, SCHWARZ_FORWARD, SCHWARZ_BACKWARD) and lvl >= 1:
+            notes.append('Schwarz_type %r on overlapping seed + %d-ring blocks -> SCHWARZ_SEED_BLOCKS (the level '
+                         'smoother on the non-overlapping seed blocks, seed + joined 1-ring)' % (st, lvl))
+            out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS
+            out['Schwarz_maxlvl'] = 1
+        elif st in (SCHWARZ_BLOCK_JACOBI, SCHWARZ_ADDITIVE) and gsm:
+            notes.append('Schwarz_type %r -> SCHWARZ_SEED_BLOCKS (GS/SGS on the seed blocks)' % st)
+            out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS
+        elif st is None:
+            out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS if gsm else SCHWARZ_BLOCK_JACOBI
+        if out.get('Schwarz_maxlvl', 1) > 1 and out['Schwarz_type'] != SCHWARZ_ADDITIVE:
+            notes.append('Schwarz_maxlvl %d -> 1' % out['Schwarz_maxlvl'])
+            out['Schwarz_maxlvl'] = 1
     if smo in (SMOOTHER_GS, SMOOTHER_SGS) and out.get('num_functions', 1) != 2:
         notes.append('num_functions -> 2 (the multicolour GS smoothers are node-block smoothers)')
         out['num_functions'] = 2

@@ -221,7 +221,8 @@ class Params:
     Schwarz_levels: int = 1       # 1: seed-block Jacobi on level 0 (needs idofs)
     Schwarz_mmsize: int = 100     # max dofs per seed block
     Schwarz_maxlvl: int = 1       # 1: seed + joined 1-ring neighbours; 0: the seed's node (node blocks)
-    Schwarz_type: int = 4         # 4: non-overlapping seed blocks (block Jacobi); 5: additive overlapping rings; 6: node patches
+    Schwarz_type: int = 4         # 4 / 7: non-overlapping seed blocks (the level smoother); 5: additive overlapping rings;
+                                  # 6: node patches (3 on the 1-rings of a nodal system resolves to 6)
     sa_omega: float = 4.0 / 3.0   # prolongator smoothing  w = sa_omega / rho
     rho_iters: int = 0            # 0: Gershgorin bound; >0: inf-norm power its
     max_coarse_dense: int = 8192
@@ -1157,8 +1158,22 @@ def coarse_scale(Ac, bc, e):
     return alpha * e
 
 
+SCHWARZ_SYMMETRIC = 3
+SCHWARZ_SEED_BLOCKS = 7        # the level smoother on non-overlapping seed blocks
+
+
+def resolve_params(p: Params) -> Params:
+    """The reference's SCHWARZ_SYMMETRIC on the seeds' 1-rings
+    (src/amg_parameters.py:83-87, src/utils.py:84) of a nodal system is the
+    node-patch Schwarz (SCHWARZ_PATCHES); mirrors setup.cpp resolve_params."""
+    if p.Schwarz_levels >= 1 and p.Schwarz_type == SCHWARZ_SYMMETRIC and p.Schwarz_maxlvl == 1 \
+            and p.num_functions == 2 and p.node_block_smoother:
+        return dataclasses.replace(p, Schwarz_type=SCHWARZ_PATCHES)
+    return p
+
+
 def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarchy:
-    p = params or Params()
+    p = resolve_params(params or Params())
     A = A.tocsr()
     A.sort_indices()
     levels = []

@@ -444,10 +444,9 @@ def test_device_conjgrad_requires_own_operator(lib_built):
 
 
 def test_k_block_layouts_bitwise(lib_built, monkeypatch):
-    """The K values stored one 32-byte block per SELL slot (MAMG_POST_K=3) or
-    as two 16-byte streams (=2, sell2_kernel SPL): the same sums, so the apply
-    and the device PCG are bitwise equal; the default (=1) times both on large
-    problems and keeps the faster."""
+    """The K values stored one 32-byte block per SELL slot (default) or as two
+    16-byte streams (MAMG_POST_K=2, kpost_kernel SPL): the same sums, so the
+    apply and the device PCG are bitwise equal."""
     import torch
     M = _mamg()
     monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
@@ -469,3 +468,42 @@ def test_k_block_layouts_bitwise(lib_built, monkeypatch):
     assert its[0][0] == its[1][0] and np.array_equal(its[0][1], its[1][1])
     h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
     assert rel(zs[1].cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
+
+
+@pytest.mark.parametrize('variant', ['0', '1', '2'])
+def test_k_kernel_variants(lib_built, monkeypatch, variant):
+    """The level-0 K kernel with 2 lanes per row (default), 1 lane (round 2's
+    sell2_kernel) or 4 lanes: the same operator up to the order of a row's
+    partial sums (1e-14), each = the oracle; the layouts block <-> split
+    switched back and forth on one handle give the apply's bits back, and the
+    operators re-homed after the setup give the bits of the un-moved ones."""
+    import torch
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    monkeypatch.setenv('MAMG_K_VARIANT', '1')
+    B1 = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    z1 = B1.matvec(r)
+    monkeypatch.setenv('MAMG_K_VARIANT', variant)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    assert B.level_format(0)['post_sell']
+    z = B.matvec(r)
+    zz = torch.empty_like(z)
+    for lay in ('split', 'block'):     # in-place re-layout through mamg_time_apply
+        monkeypatch.setenv('MAMG_K_LAYOUT', lay)
+        B.time_apply(r, zz, 1, 0)
+    monkeypatch.delenv('MAMG_K_LAYOUT')
+    B.time_apply(r, zz, 1, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(zz, z)
+    monkeypatch.setenv('MAMG_REHOME', '0')
+    B0 = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    assert torch.equal(B0.matvec(r), z)
+    torch.cuda.synchronize()
+    assert rel(z.cpu().numpy(), z1.cpu().numpy()) < 1e-14
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    assert rel(z.cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
+    for b in (B, B0, B1):
+        b.close()

@@ -25,8 +25,8 @@ def _mamg():
 def to_c(kw):
     c = dict(kw)
     if 'smoother' in c:
-        # the level-0 seed blocks take the level smoother (check_params)
-        c['Schwarz_type'] = {'SGS': 3, 'GS': 1}[c['smoother']]
+        # the level-0 seed blocks take the level smoother (SCHWARZ_SEED_BLOCKS)
+        c['Schwarz_type'] = 7
         c['smoother'] = SMO[c['smoother']]
     if 'cycle_type' in c:
         c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
@@ -108,7 +108,7 @@ def test_sgs_symmetric_and_deterministic(lib_built):
     M = _mamg()
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
-    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, smoother=SMO['SGS'], Schwarz_type=3)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, smoother=SMO['SGS'], Schwarz_type=7)
     r1 = torch.as_tensor(mo.seeded_rhs(s.N, 1)).cuda()
     r2 = torch.as_tensor(mo.seeded_rhs(s.N, 2)).cuda()
     z1, z2 = B.matvec(r1), B.matvec(r2)
