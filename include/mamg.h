@@ -180,6 +180,10 @@ int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, mamg_hier** out);
 void mamg_hier_free(mamg_hier* h);
 int mamg_hier_num_levels(const mamg_hier* h);
+/* The parameters the setup ran with, after the reference's Schwarz names are
+ * resolved (SCHWARZ_SYMMETRIC on the 1-rings of a nodal system ->
+ * SCHWARZ_PATCHES; see the Schwarz_type enum). */
+int mamg_hier_params(const mamg_hier* h, mamg_params* out);
 /* Sizes of level l: n, nnz(A), nnz(P), nnz(R), nnz(WB) (0 if point smoother),
  * ncoarse (n of level l+1, 0 on the coarsest). */
 int mamg_hier_level_sizes(const mamg_hier* h, int l, int64_t* sizes6);
@@ -309,8 +313,12 @@ int mamg_device_layout(const mamg_handle* h);
  * only, results are bitwise those of row order).
  * Returns flags >= 0, or < 0. */
 enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_POST_K = 8,
-       MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32, MAMG_FMT_BANDS = 64 };
+       MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32, MAMG_FMT_BANDS = 64,
+       MAMG_FMT_PATCHES = 128,  /* smoother: multiplicative node-patch Schwarz (SCHWARZ_PATCHES) */
+       MAMG_FMT_GS = 256 };     /* smoother: multicolour node-block GS / SGS sweeps */
 int mamg_level_format(const mamg_handle* h, int level);
+/* The parameters the handle runs (as mamg_hier_params). */
+int mamg_handle_params(const mamg_handle* h, mamg_params* out);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */
 int mamg_apply_bytes(const mamg_handle* h, double* total_bytes);

@@ -78,6 +78,7 @@ SIGNATURES = {
                                   C.POINTER(mamg_params), C.POINTER(VP)]),
     'mamg_hier_free': (None, [VP]),
     'mamg_hier_num_levels': (C.c_int, [VP]),
+    'mamg_hier_params': (C.c_int, [VP, C.POINTER(mamg_params)]),
     'mamg_hier_level_sizes': (C.c_int, [VP, C.c_int, P_I64]),
     'mamg_hier_level_export': (C.c_int, [VP, C.c_int] + [P_I64, P_I32, P_F64] * 4
                                + [P_F64, P_I64, P_F64]),
@@ -115,6 +116,7 @@ SIGNATURES = {
     'mamg_num_levels': (C.c_int, [VP]),
     'mamg_device_layout': (C.c_int, [VP]),
     'mamg_level_format': (C.c_int, [VP, C.c_int]),
+    'mamg_handle_params': (C.c_int, [VP, C.POINTER(mamg_params)]),
     'mamg_apply_bytes': (C.c_int, [VP, P_F64]),
     'mamg_apply': (C.c_int, [VP, P_F64, P_F64]),
     'mamg_apply_device': (C.c_int, [VP, VP, VP, VP]),

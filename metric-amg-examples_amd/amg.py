@@ -17,7 +17,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .parameters import make_params
+from .parameters import make_params, params_to_dict
 
 
 def csr_arrays(A):
@@ -231,7 +231,15 @@ class MetricAMG:
         _lib.check(min(f, 0))
         return {'sell': bool(f & 1), 'sym': bool(f & 2), 'post_fused': bool(f & 4),
                 'post_k': bool(f & 8), 'post_sell': bool(f & 16), 'half': bool(f & 32),
-                'bands': bool(f & 64)}
+                'bands': bool(f & 64), 'patches': bool(f & 128), 'gs': bool(f & 256)}
+
+    @property
+    def effective_params(self) -> dict:
+        """The parameters the handle runs, after the reference's Schwarz
+        names are resolved (mamg_handle_params)."""
+        p = _lib.mamg_params()
+        _lib.check(self._L.mamg_handle_params(self._h, C.byref(p)))
+        return params_to_dict(p)
 
     @property
     def apply_bytes(self) -> float:
@@ -321,6 +329,13 @@ class HostHierarchy:
         fn = self._L.mamg_gpu_host_setup if gpu else self._L.mamg_host_setup
         _lib.check(fn(C.byref(csr), ip, ni, C.byref(self.params), C.byref(h)))
         self._h = h
+
+    @property
+    def effective_params(self) -> dict:
+        """The parameters the setup ran with (mamg_hier_params)."""
+        p = _lib.mamg_params()
+        _lib.check(self._L.mamg_hier_params(self._h, C.byref(p)))
+        return params_to_dict(p)
 
     @property
     def num_levels(self):

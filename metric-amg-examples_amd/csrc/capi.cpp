@@ -216,6 +216,12 @@ void mamg_hier_free(mamg_hier* h) { delete h; }
 
 int mamg_hier_num_levels(const mamg_hier* h) { return h ? (int)h->H.levels.size() : MAMG_ERR_ARG; }
 
+int mamg_hier_params(const mamg_hier* h, mamg_params* out) {
+  if (!h || !out) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = h->H.params;
+  return MAMG_OK;
+}
+
 int mamg_hier_level_sizes(const mamg_hier* h, int l, int64_t* s) {
   if (!h || l < 0 || l >= (int)h->H.levels.size() || !s) { set_error("bad level"); return MAMG_ERR_ARG; }
   const auto& L = h->H.levels[l];
@@ -609,6 +615,12 @@ int mamg_level_format(const mamg_handle* h, int level) {
     return MAMG_ERR_ARG;
   }
   return mamg::dev_level_format(h->d, level);
+}
+
+int mamg_handle_params(const mamg_handle* h, mamg_params* out) {
+  if (!h || !out) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = mamg::dev_params(h->d);
+  return MAMG_OK;
 }
 
 int mamg_apply_bytes(const mamg_handle* h, double* total) {

@@ -343,33 +343,39 @@ __global__ __launch_bounds__(256) void sell2_kernel(
   vset(out, os, node, 1, o1);
 }
 
-// Level-0 fused post operator z = x1 + W r1 + K e on the SELL-64 K with LPR
-// lanes per node row: a wavefront takes 64 / LPR rows of a 64-row slice, part
-// q < LPR - 1 of a row takes its blocks [q U, (q + 1) U), the last part the
-// rest in chunks of U, so a ~9-block row is one load -> gather round trip per
-// lane instead of two chained chunks of one lane.  For a fixed chunk slot the
-// lanes of one part read 64 / LPR consecutive slots.  The parts' sums meet by
-// a __shfl_xor butterfly (every lane of a row ends with the same bits), then
-// part f < 2 writes field f of the output; its epilogue operands (x1_f, W's
-// row f, r1) are loaded before the block loop.  LPR 2, U 5: K 1.46 -> 1.33 ms
-// at nrefs=6 on one upload (profiles/r03_kvariants*.txt).
-template <int LPR, int U, bool SPL, int TAG, int PROBE = 0>
-__global__ __launch_bounds__(256) void kpost_kernel(
+// SELL-64 operator with LPR lanes per node row (multi-lane SELL).  A wavefront
+// takes 64 / LPR rows of a 64-row slice; part q < LPR - 1 of a row takes its
+// blocks [q U, (q + 1) U), the last part the rest in chunks of U, so a row of
+// up to LPR U blocks is one load -> gather round trip per lane instead of a
+// chain of chunks on one lane.  For a fixed chunk slot the lanes of one part
+// read 64 / LPR consecutive slots.  The parts' sums meet by a __shfl_xor
+// butterfly (addition commutes: every lane of a row ends with the same bits),
+// then part f < 2 writes field f; its epilogue operands are loaded before
+// the block loop.  Used for the level-0 fused post operator
+// z = x1 + W r1 + K e (EPI_KPOST, LPR 2, U 5: K 1.69 -> 1.54 ms on one
+// upload) and the SELL-stored coarse operators.
+template <int LPR, int U, int EPI, bool XFM, bool SYM, bool SPL, int TAG, int PROBE = 0>
+__global__ __launch_bounds__(256) void msell_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
-    const double* __restrict__ e, const double* __restrict__ x1, const double* __restrict__ r1,
-    const dv4* __restrict__ W, double* out, int64_t os) {
+    const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b, int64_t bs,
+    const dv4* __restrict__ W, double* out, int64_t os, int remap) {
   constexpr int RW = 64 / LPR;                          // rows per wavefront
   const int lane = threadIdx.x & 63, q = lane / RW;
-  const int64_t node = (int64_t)blockIdx.x * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
+  const int64_t node = row_block(remap) * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
   const bool live = node < nr;
   const int64_t nd = live ? node : nr - 1;            // dead lanes mirror the last row, write nothing
   const int len = meta[nd] & 0xffff;
   const int64_t k = soff[nd / SELL_C] + (nd & (SELL_C - 1));
+  const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int f = q & 1;
-  const double yf = q < 2 ? x1[2 * nd + f] : 0.0;
-  const dv2 wf = q < 2 ? reinterpret_cast<const dv2*>(W + nd)[f] : dv2{0.0, 0.0};
-  const double2 rr = q < 2 ? reinterpret_cast<const double2*>(r1)[nd] : double2{0.0, 0.0};
+  const bool wr = q < 2;
+  constexpr bool NB = EPI == EPI_RESID || EPI == EPI_BJAC || EPI == EPI_KPOST;
+  constexpr bool NY = EPI == EPI_YADD || EPI == EPI_BJAC || EPI == EPI_KPOST;
+  constexpr bool NW = EPI == EPI_BJAC || EPI == EPI_KPOST;
+  const double yf = NY && wr ? y[2 * nd + f] : 0.0;
+  const dv2 wf = NW && wr ? reinterpret_cast<const dv2*>(W + nd)[f] : dv2{0.0, 0.0};
+  const double2 bb = NB && wr ? double2{vget(b, bs, nd, 0), vget(b, bs, nd, 1)} : double2{0.0, 0.0};
   double s0 = 0.0, s1 = 0.0;
   const int j0 = q * U, j1 = q == LPR - 1 ? len : (len < j0 + U ? len : j0 + U);
   for (int j = j0; j < j1; j += U) {
@@ -380,11 +386,11 @@ __global__ __launch_bounds__(256) void kpost_kernel(
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
       c[u] = bcol[kk];
-      v[u] = SPL ? blk_split(bval, nbs, kk) : blk<false>(bval, nullptr, kk);
+      v[u] = SPL ? blk_split(bval, nbs, kk) : blk<SYM>(bval, offd, kk);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)   // PROBE 1 (A/B only, wrong results): no gather, the column as the value
-      a[u] = PROBE ? double2{(double)c[u], 1.0} : reinterpret_cast<const double2*>(e)[c[u]];
+      a[u] = PROBE ? double2{(double)c[u], 1.0} : xget<XFM>(x, xs, c[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool ok = j + u < j1;
@@ -393,11 +399,26 @@ __global__ __launch_bounds__(256) void kpost_kernel(
     }
   }
 #pragma unroll
-  for (int off = RW; off < 64; off <<= 1) {   // addition commutes: all parts end bitwise equal
+  for (int off = RW; off < 64; off <<= 1) {
     s0 += __shfl_xor(s0, off);
     s1 += __shfl_xor(s1, off);
   }
-  if (live && q < 2) vset(out, os, node, f, yf + (wf.x * rr.x + wf.y * rr.y) + (f ? s1 : s0));
+  if (!live || !wr) return;
+  const double sf = f ? s1 : s0;
+  double o;
+  if (EPI == EPI_Y) {
+    o = sf;
+  } else if (EPI == EPI_YADD) {
+    o = yf + sf;
+  } else if (EPI == EPI_RESID) {
+    o = (f ? bb.y : bb.x) - sf;
+  } else if (EPI == EPI_KPOST) {
+    o = yf + (wf.x * bb.x + wf.y * bb.y) + sf;
+  } else {  // EPI_BJAC
+    const double r0 = bb.x - s0, r1 = bb.y - s1;
+    o = yf + (wf.x * r0 + wf.y * r1);
+  }
+  vset(out, os, node, f, o);
 }
 
 // ---------------------------------------------------------------------------
@@ -1369,6 +1390,9 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_SELL_MIN_ROWS  node rows from which a level-0-class operator is stored
 //                       SELL-64 / half-symmetric (default 2^20; tests lower it
 //                       to exercise those formats on small problems)
+//   MAMG_MSELL_MIN_ROWS node rows from which a coarse level's A and K are stored
+//                       SELL-64 with several lanes per row (msell_kernel; off by
+//                       default: slower than the lane-group BSR kernels there)
 //   MAMG_HALF           0: SELL-64 instead of the half-symmetric ELL-64 A0 (1)
 //   MAMG_HALF_BANDS     band schedule of the half-symmetric kernel: sub-bands per
 //                       XCD (1; 0 = row order)
@@ -1391,6 +1415,7 @@ int g_kvar = 0;
 int g_rvar = 0;
 int g_rrvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
+int64_t g_msell_min_rows = (int64_t)1 << 40;   // off: coarse levels 0.41 -> 0.50 ms
 void read_kvar() {
   const char* e = std::getenv("MAMG_K_VARIANT");
   g_kvar = e ? std::atoi(e) : 0;
@@ -1405,6 +1430,8 @@ void read_knobs() {
   g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
+  e = std::getenv("MAMG_MSELL_MIN_ROWS");
+  g_msell_min_rows = e ? std::atoll(e) : ((int64_t)1 << 40);
   e = std::getenv("MAMG_HALF");
   g_half = e ? std::atoi(e) != 0 : 1;
   e = std::getenv("MAMG_HALF_BANDS");
@@ -1451,6 +1478,7 @@ struct DBsr {              // 2x2 blocks, node-major
   // col / val hold nbs (>= nb, padded) slots
   bool sell = false;
   bool split = false;       // SELL general blocks as two 16-byte streams (sell2_kernel SPL)
+  int lpr = 1;              // SELL lanes per row: 1 sell2_kernel, > 1 msell_kernel
   int64_t nbs = 0;
   int64_t* soff = nullptr;
   int32_t* meta = nullptr;
@@ -1565,6 +1593,24 @@ struct Graph {
   hipGraph_t graph = nullptr;
 };
 
+// one PCG iteration captured for a solution vector x and a history length
+// (dev_pcg): reused by later solves into the same x (drivers, gamma sweeps)
+struct PcgGraph {
+  double* x = nullptr;
+  int maxiter = 0;
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+  double* hist = nullptr;          // residuals[maxiter + 1], alphas[maxiter], betas[maxiter]
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  void release() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (hipEvent_t e : ev) if (e) (void)hipEventDestroy(e);
+    if (hist) (void)hipFree(hist);
+    *this = PcgGraph();
+  }
+};
+
 }  // namespace
 
 struct DeviceHandle {
@@ -1579,6 +1625,7 @@ struct DeviceHandle {
   char* arena1 = nullptr;
   hipStream_t cap = nullptr;
   std::vector<Graph> graphs;
+  std::vector<PcgGraph> pcgs;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
   double *cr = nullptr, *cz = nullptr, *cd = nullptr, *cq = nullptr;  // PCG
@@ -1597,6 +1644,7 @@ struct DeviceHandle {
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
       if (g.graph) (void)hipGraphDestroy(g.graph);
     }
+    for (auto& g : pcgs) g.release();
     for (void* a : allocs) (void)hipFree(a);
     if (hres) (void)hipHostFree(hres);
     if (cap) (void)hipStreamDestroy(cap);
@@ -2260,7 +2308,7 @@ int upload_half_or_bsr(HT* h, const HBsr& B, DBsr* D, std::string* err) {
 // packing where every block has (0,1) == (1,0) bitwise, else 4 doubles/block
 template <class HT>
 int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, std::string* err,
-                 bool allow_sell = true, bool allow_half = false) {
+                 bool allow_sell = true, bool allow_half = false, bool allow_msell = false) {
   int rc;
   const int64_t nr = B.nr, np = B.merged ? 2 * nr + 1 : nr + 1;
   D->nr = nr;
@@ -2279,7 +2327,14 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   }
   D->sym = sym;
   const int per = sym ? 3 : 4;
-  if (allow_sell && nr >= g_sell_min_rows && D->nb <= g_sell_max_len * nr && !B.merged) {
+  // multi-lane SELL (msell_kernel) for the coarse levels' A and K: lanes per
+  // row from the mean row length, chunks of 5 blocks per lane
+  const bool msell = allow_sell && allow_msell && !B.merged && nr >= g_msell_min_rows && nr < g_sell_min_rows;
+  if (msell) {
+    const double mean = nr ? (double)D->nb / (double)nr : 0.0;
+    D->lpr = mean <= 10.0 ? 2 : mean <= 20.0 ? 4 : mean <= 40.0 ? 8 : 16;
+  }
+  if (allow_sell && ((nr >= g_sell_min_rows && D->nb <= g_sell_max_len * nr) || msell) && !B.merged) {
     if (allow_half && g_half && sym && nr == B.nc) {
       if ((rc = try_half(h, T, B, D, err))) return rc;
       if (D->half) return MAMG_OK;
@@ -2588,8 +2643,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
   {
     TBsr B;
     if ((rc = dev_csr_to_bsr(&T, S.A, nv, nv, &B, err))) return rc;
-    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true,
-                           l == 0)))
+    if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true, l == 0, l > 0)))
       return rc;
     const bool patches = l == 0 && patch_schwarz(p);
     if (gs_smoother(p) && !patches)
@@ -2621,7 +2675,8 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     // K: SELL-64 with 4-block chunks (K rows hold ~9 blocks at level 0; A/B in
     // DESIGN.md section 4), lane-group BSR if MAMG_POST_SELL=0; the merged
     // window is never SELL on this path
-    if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0)))
+    if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0, false,
+                           l > 0 && g_post_k != 0)))
       return rc;
   } else {
     TBsr Pb;
@@ -3034,35 +3089,58 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 #undef SELL_ARGS
 }
 
-template <int LPR, int U, bool SPL, int PROBE = 0>
-void launch_kpost(const Op& o, hipStream_t s) {
+template <int LPR, int U, bool XFM, bool SYM, bool SPL, int TAG, int PROBE = 0>
+void launch_msell(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const int64_t rows = 256 / LPR;
   const unsigned g = (unsigned)((M.nr + rows - 1) / rows);
   if (g == 0) return;
-  kpost_kernel<LPR, U, SPL, 0, PROBE><<<g, 256, 0, s>>>(M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.y, o.b,
-                                                        o.W, o.out, o.os);
+#define MSELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
+    (TAG == 0 && g_kvar == 3) ? 1 : 0
+  switch (o.epi) {
+    case EPI_Y: msell_kernel<LPR, U, EPI_Y, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
+    case EPI_YADD: msell_kernel<LPR, U, EPI_YADD, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
+    case EPI_RESID: msell_kernel<LPR, U, EPI_RESID, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
+    case EPI_KPOST:
+      if constexpr (!XFM && !SYM) msell_kernel<LPR, U, EPI_KPOST, false, false, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS);
+      break;
+    default: msell_kernel<LPR, U, EPI_BJAC, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
+  }
+#undef MSELL_ARGS
 }
 
 // the level-0 K kernel (MAMG_K_VARIANT for A/Bs, read at upload and by
 // mamg_time_apply): 0 two lanes per row, chunks of 5 (default); 1 one lane
-// per row, chunks of 6 (sell2_kernel, round 2); 2 four lanes per row, chunks of 3
+// per row, chunks of 6 (sell2_kernel, round 2); 2 four lanes per row, chunks
+// of 3; 9 a probe without the e gathers (wrong results, timing only)
 template <bool SPL>
 bool launch_kvariant(const Op& o, hipStream_t s) {
   switch (g_kvar) {
     case 1: return false;
-    case 2: launch_kpost<4, 3, SPL>(o, s); return true;
-    case 9: launch_kpost<2, 5, SPL, 1>(o, s); return true;   // probe: no e gathers (wrong results)
-    default: launch_kpost<2, 5, SPL>(o, s); return true;
+    case 2: launch_msell<4, 3, false, false, SPL, 0>(o, s); return true;
+    case 3: launch_msell<2, 5, false, false, SPL, 0>(o, s); return true;   // XCD-contiguous rows
+    case 9: launch_msell<2, 5, false, false, SPL, 0, 1>(o, s); return true;
+    default: launch_msell<2, 5, false, false, SPL, 0>(o, s); return true;
   }
 }
 
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
-  // level-0 K operator: chunks of 6 blocks (two chunks cover its ~9-block
-  // rows); everything else 8
+  // level-0 K operator: two lanes per row (launch_kvariant); multi-lane SELL
+  // coarse operators: lanes per row from the mean row length; everything else
+  // one lane, chunks of 8
   if constexpr (TAG == 0 && !XFM && !SYM) {
     if (o.epi == EPI_KPOST && (o.Mb->split ? launch_kvariant<true>(o, s) : launch_kvariant<false>(o, s))) return;
+  }
+  if constexpr (!XFM) {
+    if (o.Mb->lpr > 1 && !o.Mb->split) {
+      switch (o.Mb->lpr) {
+        case 2: launch_msell<2, 5, false, SYM, false, TAG>(o, s); return;
+        case 4: launch_msell<4, 5, false, SYM, false, TAG>(o, s); return;
+        case 8: launch_msell<8, 5, false, SYM, false, TAG>(o, s); return;
+        default: launch_msell<16, 5, false, SYM, false, TAG>(o, s); return;
+      }
+    }
   }
   if (o.Mb->split && TAG == 0) launch_sell_u<XFM, SYM, g_post_u, true, TAG>(o, s);
   else if (o.Mb->split) launch_sell_u<XFM, SYM, g_sell_u, true, TAG>(o, s);
@@ -3379,7 +3457,7 @@ void set_k_split(DBsr& K, bool to_split) {
 
 // Round 2 chose the layout per box by timing both at upload (split 1.57 vs
 // 1.71 ms on one box, the opposite on another).  With the two-lanes-per-row
-// K kernel (kpost_kernel) the one-block layout is kept everywhere
+// K kernel (msell_kernel) the one-block layout is kept everywhere
 // (DESIGN.md section 4); MAMG_POST_K=2 forces the split layout on every
 // SELL-stored K (tests), MAMG_K_LAYOUT=split|block switches level 0 at
 // mamg_time_apply (A/Bs on one upload).
@@ -3641,8 +3719,11 @@ int dev_level_format(const DeviceHandle* h, int level) {
   const DLevel& L = h->L[level];
   return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) | (L.Ab.half ? MAMG_FMT_HALF : 0) |
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
-         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0);
+         (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0) |
+         (L.pcs.size() > 1 ? MAMG_FMT_PATCHES : 0) | (L.gcs.size() > 1 ? MAMG_FMT_GS : 0);
 }
+
+mamg_params dev_params(const DeviceHandle* h) { return h->p; }
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
@@ -3704,20 +3785,55 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
   }
   PcgState* st = reinterpret_cast<PcgState*>(h->dres);
   PcgState* hst = reinterpret_cast<PcgState*>(h->hres);
-  double* dhist = nullptr;   // residuals[maxiter + 1], alphas[maxiter], betas[maxiter]
-  HIPCHK(hipMalloc(&dhist, (3 * (size_t)maxiter + 1) * sizeof(double)));
-  double *dres = dhist, *dal = dhist + maxiter + 1, *dbe = dal + maxiter;
-  struct Cleanup {
-    double* p; hipGraphExec_t e; hipGraph_t g; hipEvent_t ev[2];
-    ~Cleanup() {
-      if (e) (void)hipGraphExecDestroy(e);
-      if (g) (void)hipGraphDestroy(g);
-      for (hipEvent_t x : ev) if (x) (void)hipEventDestroy(x);
-      if (p) (void)hipFree(p);
-    }
-  } cl{dhist, nullptr, nullptr, {nullptr, nullptr}};
   const unsigned g = nblocks(n);
   if ((rc = order_begin(h, s, err))) return rc;
+  // the iteration graph for (x, maxiter), captured once and kept on the
+  // handle (at most 4; the oldest evicted after the handle's work is done)
+  PcgGraph* pg = nullptr;
+  for (auto& q : h->pcgs)
+    if (q.x == d_x && q.maxiter == maxiter) pg = &q;
+  if (!pg) {
+    if (h->pcgs.size() >= 4) {
+      if (h->last) HIPCHK(hipEventSynchronize(h->last));
+      HIPCHK(hipStreamSynchronize(s));
+      h->pcgs.front().release();
+      h->pcgs.erase(h->pcgs.begin());
+    }
+    PcgGraph q;
+    q.x = d_x;
+    q.maxiter = maxiter;
+    if (hipMalloc(&q.hist, (3 * (size_t)maxiter + 1) * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      *err = "PCG history allocation failed";
+      return MAMG_ERR_HIP;
+    }
+    double *dres = q.hist, *dal = q.hist + maxiter + 1, *dbe = dal + maxiter;
+    std::vector<Op> ops;
+    apply_ops(h, h->cr, h->cz, &ops);
+    hipError_t e = hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+      launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), h->cap);           // q = A d
+      dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cd, h->cq, h->part);
+      pcg_alpha_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st);
+      pcg_xr_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cd, h->cq, d_x, h->cr);
+      for (const Op& o : ops) launch(o, h->cap);                          // z = B r
+      dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cr, h->cz, h->part);
+      pcg_beta_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st, dres, dal, dbe);
+      pcg_d_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cz, h->cd, d_x);
+      e = hipStreamEndCapture(h->cap, &q.graph);
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&q.exec, q.graph, nullptr, nullptr, 0);
+    for (hipEvent_t& x : q.ev)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      q.release();
+      *err = std::string("PCG graph: ") + hipGetErrorString(e);
+      return MAMG_ERR_HIP;
+    }
+    h->pcgs.push_back(q);
+    pg = &h->pcgs.back();
+  }
+  double *dres = pg->hist, *dal = pg->hist + maxiter + 1, *dbe = dal + maxiter;
   launch(a0_op(h, EPI_RESID, d_x, d_b, h->cr), s);                 // r = b - A x
   if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;         // z = B r
   HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -3733,28 +3849,14 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     return MAMG_ERR_BREAKDOWN;
   }
   if (hst[0].active) {
-    std::vector<Op> ops;
-    apply_ops(h, h->cr, h->cz, &ops);
-    HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
-    launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), h->cap);           // q = A d
-    dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cd, h->cq, h->part);
-    pcg_alpha_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st);
-    pcg_xr_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cd, h->cq, d_x, h->cr);
-    for (const Op& o : ops) launch(o, h->cap);                          // z = B r
-    dot_partial_kernel<<<DOT_BLOCKS, 256, 0, h->cap>>>(n, h->cr, h->cz, h->part);
-    pcg_beta_kernel<<<1, 256, 0, h->cap>>>(DOT_BLOCKS, h->part, st, dres, dal, dbe);
-    pcg_d_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cz, h->cd, d_x);
-    HIPCHK(hipStreamEndCapture(h->cap, &cl.g));
-    HIPCHK(hipGraphInstantiate(&cl.e, cl.g, nullptr, nullptr, 0));
-    for (hipEvent_t& x : cl.ev) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
     // iteration k's state lands in hst[k & 1]; iteration k + 1 is queued
     // before the host waits for iteration k
     for (int k = 0; k < maxiter; ++k) {
-      HIPCHK(hipGraphLaunch(cl.e, s));
+      HIPCHK(hipGraphLaunch(pg->exec, s));
       HIPCHK(hipMemcpyAsync(&hst[k & 1], st, sizeof(PcgState), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipEventRecord(cl.ev[k & 1], s));
+      HIPCHK(hipEventRecord(pg->ev[k & 1], s));
       if (k == 0) continue;
-      HIPCHK(hipEventSynchronize(cl.ev[(k - 1) & 1]));
+      HIPCHK(hipEventSynchronize(pg->ev[(k - 1) & 1]));
       if (!hst[(k - 1) & 1].active) break;
     }
   }
@@ -3788,6 +3890,53 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
   int rc = order_begin(h, s, err);
   if (rc) return rc;
   read_kvar();   // A/B of the K kernel variants on one upload (eager launches)
+  if (const char* mv = std::getenv("MAMG_KMOVE")) {
+    // placement diagnosis: move one of the level-0 K
+    // kernel's arrays into a fresh allocation (same bytes), so its time can be
+    // compared across placements within one process.  val / col: K's values /
+    // columns; x1 / r1 / w: the epilogue vectors; e: the coarse correction;
+    // a trailing '+' asks for a physically contiguous allocation
+    if (h->bsr && h->L.size() > 1 && *mv) {
+      DLevel& L = h->L[0];
+      const int64_t nv = L.n / 2;
+      const std::string w = mv;
+      void** ptr = nullptr;
+      size_t bytes = 0;
+      const bool contig = !w.empty() && w.back() == '+';   // "val+": physically contiguous allocation
+      const std::string wn = contig ? w.substr(0, w.size() - 1) : w;
+      if (wn == "val") { ptr = (void**)&L.KPb.val; bytes = (size_t)L.KPb.nbs * 4 * sizeof(double); }
+      else if (wn == "col") { ptr = (void**)&L.KPb.col; bytes = (size_t)L.KPb.nbs * sizeof(int32_t); }
+      else if (wn == "x1") { ptr = (void**)&L.t; bytes = (size_t)L.n * sizeof(double); }
+      else if (wn == "r1") { ptr = (void**)&L.r; bytes = (size_t)L.n * sizeof(double); }
+      else if (wn == "w") { ptr = (void**)&L.Wd; bytes = (size_t)nv * sizeof(dv4); }
+      else if (wn == "e") { ptr = (void**)&h->L[1].x; bytes = (size_t)h->L[1].n * sizeof(double); }
+      if (ptr) {
+        void* r = nullptr;
+        HIPCHK(hipDeviceSynchronize());
+        if (contig) HIPCHK(hipExtMallocWithFlags(&r, bytes, hipDeviceMallocContiguous));
+        else HIPCHK(hipMalloc(&r, bytes));
+        HIPCHK(hipMemcpy(r, *ptr, bytes, hipMemcpyDeviceToDevice));
+        void* old = *ptr;
+        *ptr = r;
+        h->allocs.push_back(r);
+        const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
+        auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
+        if (!in_arena && it != h->allocs.end()) {
+          (void)hipFree(old);
+          h->allocs.erase(it);
+        }
+        for (auto& g : h->graphs) {   // captured with the old pointer
+          (void)hipGraphExecDestroy(g.exec);
+          (void)hipGraphDestroy(g.graph);
+        }
+        h->graphs.clear();
+        for (auto& g : h->pcgs) g.release();
+        h->pcgs.clear();
+        if (std::getenv("MAMG_KMOVE_PRINT"))
+          std::fprintf(stderr, "[mamg] moved %s (%zu B) %p -> %p\n", mv, bytes, old, r);
+      }
+    }
+  }
   if (const char* kl = std::getenv("MAMG_K_LAYOUT"))
     if (h->bsr && h->L.size() > 1) {
       set_k_split(h->L[0].KPb, std::strcmp(kl, "split") == 0);

@@ -1138,6 +1138,11 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
     hem_number_kernel<<<nblk(m), 256>>>(m, act, mate, f, a);
     hem_compose_kernel<<<nblk(n), 256>>>(n, a, agg);
     HIPCHK(hipGetLastError());
+    if (nagg == 0) {   // no strong edge on this level (theta > 0): no aggregates, every agg[i] = -1
+      *agg_out = agg;
+      *nagg_out = 0;
+      return MAMG_OK;
+    }
     if (ps + 1 == PASSES) break;
     DevMat T, Tt, WT, C;   // W_next = T^T W T without its diagonal
     T.n = m; T.m = nagg;

@@ -455,6 +455,8 @@ def aggregate_hem(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
     agg = np.where(active, np.arange(n), -1)
     cur, act = W, active
     nagg = n
+    if not active.any():             # no strong edge (e.g. theta > 0 on a coarse level): no aggregates
+        return np.full(n, -1, dtype=np.int64), 0
     for ps in range(HEM_PASSES):
         m = cur.shape[0]
         mate = hem_match(cur, act, 16 * level + ps)

@@ -43,7 +43,9 @@ def test_params_struct_layout(lib_built):
     (dict(smoother=11), -4),                 # SGS is a node-block smoother: num_functions 2
     (dict(aggregation_type=1), -4),          # VMB rejected (HEM runs: parallel matching)
     (dict(coarse_scaling=2), -1),
-    (dict(Schwarz_type=3), -4),              # multiplicative seed blocks need the SGS smoother
+    (dict(Schwarz_type=3), -4),              # overlapping multiplicative Schwarz: nodal systems only
+    (dict(num_functions=2, Schwarz_type=3, Schwarz_maxlvl=0), -4),   # seed nodes: SYMMETRIC needs SGS
+    (dict(num_functions=2, smoother=11, Schwarz_type=9), -1),        # unknown Schwarz_type
     (dict(num_functions=2, smoother=11, Schwarz_type=4), -4),
     (dict(Schwarz_maxlvl=2), -4),            # overlapping seed + ring blocks need SCHWARZ_ADDITIVE
     (dict(Schwarz_maxlvl=0), -4),            # seed-node blocks need num_functions >= 2
@@ -79,7 +81,23 @@ def test_reference_presets_map_and_report(lib_built):
     s = M.problems.bidomain(2, 16, 1e4)
     H = M.HostHierarchy(s, idofs=s.idofs, parameters=P.parameters_metric_schwarz, num_functions=2)
     assert H.num_levels >= 2
+    # the reference's SCHWARZ_SYMMETRIC on the seeds' 1-rings runs as the
+    # overlapping node patches (not the non-overlapping seed blocks)
+    assert H.effective_params['Schwarz_type'] == P.SCHWARZ_PATCHES
     H.close()
+    # its old meaning has its own name; GS/SGS on the seed blocks
+    H = M.HostHierarchy(s, idofs=s.idofs, parameters=P.parameters_metric_mi355x_sgs)
+    assert H.effective_params['Schwarz_type'] == P.SCHWARZ_SEED_BLOCKS
+    H.close()
+    # sparse seeds (not one on every node): the reference's overlapping
+    # multiplicative form is rejected, naming the gap
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy(s, idofs=s.idofs[::2], parameters=P.parameters_metric_schwarz, num_functions=2)
+    assert ei.value.code == -4 and 'every node' in str(ei.value)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy(s, idofs=s.idofs, parameters=dict(P.parameters_metric_schwarz, Schwarz_maxlvl=2),
+                        num_functions=2)
+    assert ei.value.code == -4 and 'SCHWARZ_ADDITIVE' in str(ei.value)
     # explicit mapping keeps what is implemented and reports what it changes
     mapped, notes = P.to_gpu_profile(P.parameters_standard)
     assert mapped['aggregation_type'] == P.MIS and any('VMB' in n or '1' in n for n in notes)

@@ -75,7 +75,8 @@ def test_apply_matches_oracle(lib_built, dim, n, g, kw):
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
-    B = M.MetricAMG(A, s.W, idofs=s.idofs, **to_c(kw))
+    # num_functions explicit: MetricAMG would take 2 from the two equal blocks of W
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, **to_c(dict(dict(num_functions=1), **kw)))
     h = mo.setup(A, mo.Params(**oracle_kw(kw)), idofs=s.idofs)
     assert B.num_levels == len(h.levels)
     # gamma >= 1e8 makes A_l badly conditioned (entries span ~gamma); the
@@ -507,3 +508,49 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
     assert rel(z.cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
     for b in (B, B0, B1):
         b.close()
+
+
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e4, dict(smoother='POLY')),
+                                        (3, 16, 1e6, dict(presmooth_iter=2, postsmooth_iter=2))])
+def test_coarse_multilane_sell(lib_built, monkeypatch, dim, n, g, kw):
+    """Coarse levels' A and K stored SELL-64 with several lanes per row
+    (msell_kernel; MAMG_MSELL_MIN_ROWS lowered so every level takes it) equal
+    the lane-group BSR kernels up to summation order, and the oracle."""
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    zs = []
+    for rows in ('1', str(1 << 30)):
+        monkeypatch.setenv('MAMG_MSELL_MIN_ROWS', rows)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+        assert B.level_format(1)['sell'] == (rows == '1')
+        zs.append(B * r)
+        B.close()
+    assert rel(zs[0], zs[1]) < 1e-13
+    h = mo.setup(A, mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    assert rel(zs[0], h.apply(r)) < APPLY_TOL
+
+
+def test_pcg_graph_reused_across_solves(lib_built):
+    """mamg_pcg_device keeps the captured iteration graph per (x, maxiter):
+    repeated solves (driver loops, gamma sweeps) into the same x give the same
+    iterations and bits as the first, and a different maxiter gets its own."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    b = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    x = torch.zeros_like(b)
+    outs = []
+    for maxiter in (500, 500, 7, 500):
+        x.zero_()
+        cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=maxiter)
+        cg.solve_device(b, x)
+        torch.cuda.synchronize()
+        outs.append((list(cg.residuals), x.clone()))
+    assert outs[0][0] == outs[1][0] == outs[3][0] and len(outs[2][0]) == 8
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][1], outs[3][1])
+    ref = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs), mo.seeded_rhs(s.N), 1e-8, 500)
+    assert len(outs[0][0]) == len(ref.residuals)
