@@ -4039,6 +4039,8 @@ struct DDLevel {
   std::vector<dv4*> Wk;    // SMOOTHER_POLY step smoothers w_k W (empty: Jacobi)
   double* Ainv = nullptr;
   double *b = nullptr, *x = nullptr, *t = nullptr, *t2 = nullptr, *r = nullptr;
+  double *c = nullptr, *e = nullptr;     // W-cycle: second visit's right-hand side / correction
+  double *q = nullptr, *part2 = nullptr; // coarse scaling of this level's correction: A e, dot partials
   double* spx = nullptr;   // level 0: [owned | ghost] operand of the standalone SpMV
   int64_t ib0 = 0, ib1 = 0;  // longest run of A_loc rows without ghost columns
   int64_t* send_idx = nullptr;
@@ -4151,7 +4153,32 @@ void halo_residual(const DistHandle* h, int l, double* x, const Op& op, std::vec
   }
 }
 
-// multi-GPU cycle from x = 0 (V-cycle, nu1 = nu2 = 1): see dist.cpp / dist_ref.py
+// coarse-grid correction scaling of level lc's correction C.x against C.b on
+// N ranks: halo of C.x (distributed level), q = A_c x on the owned rows,
+// partial sums of <b, x>, <q, x> over the owned rows, one all-reduce of the
+// partials (distributed level), alpha = num / den on every rank, x <- alpha x
+// on the owned rows and the ghosts (so the post step needs no second halo)
+void dscale_ops(const DistHandle* h, int lc, std::vector<DOp>* ops) {
+  const DDLevel& C = h->L[lc];
+  const Op q = bsr_op(C.A, EPI_Y, C_MISC, 1, C.x, 0, nullptr, nullptr, 0, nullptr, C.q, 0);
+  if (C.replicated) ops->push_back(wrap(q)); else halo_residual(h, lc, C.x, q, ops);
+  Op d;
+  d.kind = OP_DOT2; d.cls = C_MISC; d.n = 2 * C.nloc; d.b = C.b; d.x = C.x; d.y = C.q; d.part = C.part2;
+  d.bytes = 24.0 * d.n;
+  ops->push_back(wrap(d));
+  if (!C.replicated) {
+    DOp a;
+    a.dk = D_ALLREDUCE; a.cls = C_COMM; a.buf = C.part2; a.count = 2 * SCALE_BLOCKS; a.bytes = 16.0 * SCALE_BLOCKS;
+    ops->push_back(a);
+  }
+  Op sc;
+  sc.kind = OP_CSCALE; sc.cls = C_MISC; sc.n = 2 * (C.nloc + C.ng); sc.part = C.part2; sc.out = C.x;
+  sc.bytes = 16.0 * sc.n;
+  ops->push_back(wrap(sc));
+}
+
+// multi-GPU cycle from x = 0 (V or W, nu1 / nu2 sweeps, optional coarse-grid
+// scaling): see dist.cpp / dist_ref.py
 void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
                 std::vector<DOp>* ops) {
   const DDLevel& D = h->L[l];
@@ -4166,6 +4193,7 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   }
   const DDLevel& C = h->L[l + 1];
   const int m = smoother_steps(h->p);   // steps per smoothing (POLY: Chebyshev degree)
+  const int npre = h->p.presmooth_iter * m, npost = h->p.postsmooth_iter * m;
   auto wk = [&](int s, bool pre) -> const dv4* { return D.Wk.empty() ? D.W : D.Wk[step_index(m, s, pre)]; };
   const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
   double* X = D.t;
@@ -4176,7 +4204,7 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
     o.out = X; o.bytes = 64.0 * D.nloc;
     ops->push_back(wrap(o));
   }
-  for (int s = 1; s < m; ++s) {   // further pre steps: halo of X, then x + w_s W (b - A x)
+  for (int s = 1; s < npre; ++s) {   // further pre steps: halo of X, then x + w_s W (b - A x)
     const Op bj = bsr_op(D.A, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, wk(s, true), X2, 0);
     if (D.replicated) ops->push_back(wrap(bj)); else halo_residual(h, l, X, bj, ops);
     std::swap(X, X2);
@@ -4205,10 +4233,17 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
     ops->push_back(d);
   }
   dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
-  if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  if (h->p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {   // second visit on the updated residual
+    const Op res = bsr_op(C.A, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0);
+    if (C.replicated) ops->push_back(wrap(res)); else halo_residual(h, l + 1, C.x, res, ops);
+    dcycle_ops(h, l + 1, C.c, 0, C.e, 0, ops);
+    ops->push_back(wrap(axpy_op(2 * C.nloc, C.e, C.x)));
+  }
+  if (h->p.coarse_scaling) dscale_ops(h, l + 1, ops);      // ghosts of C.x scaled too
+  else if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
   int s0 = 0;
   if (D.K.nr > 0 || D.PA.nr > 0) {   // fused first post step (K built with its smoother), operands local
-    const bool last = m == 1;
+    const bool last = npost == 1;
     if (D.K.nr > 0)   // X + W r + K e
       ops->push_back(wrap(bsr_op(D.K, EPI_KPOST, clsS, tagA, C.x, 0, X, D.r, 0, wk(0, false),
                                  last ? xout : X2, last ? os : 0)));
@@ -4222,8 +4257,8 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
     ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0,
                                nullptr, X, 0)));
   }
-  for (int s = s0; s < m; ++s) {   // halo of the iterate, then x + w W (b - A x)
-    const bool last = s == m - 1;
+  for (int s = s0; s < npost; ++s) {   // halo of the iterate, then x + w W (b - A x)
+    const bool last = s == npost - 1;
     const Op bj = bsr_op(D.A, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, wk(s, false), last ? xout : X2,
                          last ? os : 0);
     if (D.replicated) ops->push_back(wrap(bj)); else halo_residual(h, l, X, bj, ops);
@@ -4692,12 +4727,13 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
 int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
                 const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
                 const GhostLists* ghosts, const GHier* G, const DevMat* A0d) {
-  if (p.cycle_type != MAMG_V_CYCLE || p.maxit != 1 || p.presmooth_iter != 1 || p.postsmooth_iter != 1) {
-    *err = "multi-GPU apply supports V-cycle, maxit 1, presmooth/postsmooth 1 (round 1)";
+  if (p.maxit != 1) {
+    *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (gs_smoother(p) || p.coarse_scaling || patch_schwarz(p)) {
-    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers without coarse scaling or node patches";
+  if (gs_smoother(p) || patch_schwarz(p)) {
+    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers (multicolour GS and node patches "
+           "would need one halo per colour)";
     return MAMG_ERR_UNSUPPORTED;
   }
   read_knobs();
@@ -4812,6 +4848,14 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     if ((rc = ddalloc(h.get(), &D.t2, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
     if (l == 0 && !D.coarsest && (rc = ddalloc(h.get(), &D.spx, 2 * full, err))) return rc;
+    if (l > 0 && p.cycle_type == MAMG_W_CYCLE) {
+      if ((rc = ddalloc(h.get(), &D.c, 2 * full, err))) return rc;
+      if ((rc = ddalloc(h.get(), &D.e, 2 * full, err))) return rc;
+    }
+    if (l > 0 && p.coarse_scaling) {
+      if ((rc = ddalloc(h.get(), &D.q, 2 * full, err))) return rc;
+      if ((rc = ddalloc(h.get(), &D.part2, 2 * SCALE_BLOCKS, err))) return rc;
+    }
     const int64_t ns = P.send_idx.size();
     if (ns) {
       if ((rc = ddalloc(h.get(), &D.send_idx, ns, err))) return rc;
@@ -5031,6 +5075,7 @@ int dist_set_exchange(DistHandle* h, const mamg_exchange& ex, std::string* err) 
         return rc;
       red = std::max(red, 2 * D.nv);
     }
+    red = std::max<int64_t>(red, 2 * SCALE_BLOCKS);   // coarse scaling partials
     int rc = pin(&h->hred, red);
     if (rc) return rc;
   }

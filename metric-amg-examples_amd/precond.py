@@ -94,9 +94,11 @@ class _Product:
 def get_hazmath_metric_precond_mono(A, W, bcs=None, parameters=None, interface_dofs=None, **kw):
     """metricAMG(A, W, idofs=interface_dofs, parameters=parameters)  (src/utils.py:56-90).
     ``parameters`` None -> the GPU profile (parameters_metric_mi355x).  A dict
-    is used as given: a HAZmath preset with a component this build lacks
-    (e.g. HEM aggregation) raises MamgError; ``parameters.to_gpu_profile``
-    is the explicit opt-in mapping."""
+    is used as given (parameters_metric_schwarz runs as the reference's
+    algorithm: UA + HEM + W + SGS + scaling + node patches on level 0); a
+    component this build lacks (VMB aggregation, multiplicative Schwarz on
+    overlapping blocks of sparse seed sets) raises MamgError;
+    ``parameters.to_gpu_profile`` is the explicit opt-in mapping."""
     if parameters is None:
         parameters = P.parameters_metric_mi355x
     B = MetricAMG(A, W, idofs=interface_dofs, parameters=parameters, **kw)

@@ -8,10 +8,12 @@ Tests compare the gathered result with the single-rank oracle
 (mamg_oracle.Hierarchy.apply): the partition must not change the cycle beyond
 summation order.
 
-Per distributed level (V-cycle, nu1 = nu2 = 1; POLY: the step weights w_k):
+Per distributed level (POLY: the step weights w_k; nu1 / nu2 repeat them):
   X = W b [; halo(X) ; X += w_k W (b - A X)] ; halo(X) ; r = b - A X ;
   part = Rp r ; [next distributed: reverse-add ghost partials to owners |
                  next replicated: all-reduce] ; xc = cycle(l+1, bc) ;
+  [W-cycle: halo(xc) ; xc += cycle(l+1, bc - A_c xc)] ;
+  [scaling: halo(xc) ; all-reduce(<bc, xc>, <A_c xc, xc>) ; xc *= alpha] ;
   [next distributed: halo(xc)] ; X += P xc ; halo(X) ; z = X + W (b - A X)
 Replicated levels run the same cycle on global arrays without exchange.
 """
@@ -104,13 +106,19 @@ class GlooComm:
 class DistCycle:
     """poly: the POLY step weights (mamg_oracle.poly_weights): pre-smoothing
     takes x = w_1 W b then x += w_k W (b - A x) for k = 2..m (a halo before
-    each), post-smoothing the steps m..1; None = one Jacobi step each."""
+    each), post-smoothing the steps m..1; None = one Jacobi step each.
+    nu1 / nu2 repeat the pre / post steps (presmooth_iter, postsmooth_iter);
+    wcycle: a second coarse visit on the updated coarse residual
+    (src/amg_parameters.py:69); scaling: the coarse correction e scaled by
+    <b_c, e> / <A_c e, e> with the two sums all-reduced over the ranks
+    (src/amg_parameters.py:78; mamg_oracle.coarse_scale)."""
 
-    def __init__(self, plan_levels, Ainv_nodemajor, comm, poly=None):
+    def __init__(self, plan_levels, Ainv_nodemajor, comm, poly=None, wcycle=False, scaling=False, nu1=1, nu2=1):
         self.L = plan_levels
         self.Ainv = Ainv_nodemajor
         self.comm = comm
         self.ws = list(poly) if poly else [1.0]
+        self.wcycle, self.scaling, self.nu1, self.nu2 = wcycle, scaling, nu1, nu2
 
     # forward halo: fill ghost rows of x2 (nloc+ng, 2)
     def halo(self, lv, x2):
@@ -136,47 +144,52 @@ class DistCycle:
             np.add.at(out, si[so[q]:so[q + 1]], got[q])
         return out
 
+    def ghosted(self, lv, x):
+        """x (owned rows) -> [owned | ghost] with the ghosts filled (distributed
+        level) or x itself (replicated level)."""
+        if lv['replicated']:
+            return x
+        xg = np.zeros((lv['nloc'] + len(lv['ghosts']), 2))
+        xg[:lv['nloc']] = x
+        self.halo(lv, xg)
+        return xg
+
+    def smooth(self, lv, b2, X, ws):
+        """steps x += w W (b - A x) for w in ws (X owned rows)."""
+        for w in ws:
+            X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], self.ghosted(lv, X)))
+        return X
+
     def cycle(self, l, b2):
         lv = self.L[l]
         if lv['coarsest']:
             return (self.Ainv @ b2.ravel()).reshape(-1, 2)
         C = self.L[l + 1]
-        ws = self.ws
-        if lv['replicated']:
-            X = ws[0] * bd_mv(lv['W'], b2)
-            for w in ws[1:]:
-                X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
-            r = b2 - bsr_mv(lv['A'], X)
-            xc = self.cycle(l + 1, bsr_mv(lv['R'], r))
-            X = X + bsr_mv(lv['P'], xc)
-            for w in ws[::-1]:
-                X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], X))
-            return X
-        nloc, ng = lv['nloc'], len(lv['ghosts'])
-        Xg = np.zeros((nloc + ng, 2))
-        Xg[:nloc] = ws[0] * bd_mv(lv['W'], b2)
-        for w in ws[1:]:
-            self.halo(lv, Xg)
-            Xg[:nloc] = Xg[:nloc] + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
-        self.halo(lv, Xg)
-        r = b2 - bsr_mv(lv['A'], Xg)
+        pre = self.ws * self.nu1
+        post = self.ws[::-1] * self.nu2
+        X = pre[0] * bd_mv(lv['W'], b2)
+        X = self.smooth(lv, b2, X, pre[1:])
+        r = b2 - bsr_mv(lv['A'], self.ghosted(lv, X))
         part = bsr_mv(lv['R'], r)
-        if C['replicated']:
+        if lv['replicated']:
+            bc = part
+        elif C['replicated']:
             bc = self.comm.allreduce_sum(part)
         else:
             bc = self.reverse_add(C, part)
         xc = self.cycle(l + 1, bc)
-        if not C['replicated']:
-            xcg = np.zeros((C['nloc'] + len(C['ghosts']), 2))
-            xcg[:C['nloc']] = xc
-            self.halo(C, xcg)
-        else:
-            xcg = xc
-        Xg[:nloc] = Xg[:nloc] + bsr_mv(lv['P'], xcg)
-        for w in ws[::-1]:
-            self.halo(lv, Xg)
-            Xg[:nloc] = Xg[:nloc] + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], Xg))
-        return Xg[:nloc]
+        if self.wcycle and not C['coarsest']:
+            cc = bc - bsr_mv(C['A'], self.ghosted(C, xc))
+            xc = xc + self.cycle(l + 1, cc)
+        if self.scaling:
+            q = bsr_mv(C['A'], self.ghosted(C, xc))
+            sums = np.array([[np.sum(bc * xc), np.sum(q * xc)]])
+            if not C['replicated']:
+                sums = self.comm.allreduce_sum(sums)
+            num, den = float(sums[0, 0]), float(sums[0, 1])
+            xc = (num / den if den > 0 else 1.0) * xc
+        X = X + bsr_mv(lv['P'], self.ghosted(C, xc))
+        return self.smooth(lv, b2, X, post)
 
     def apply_local(self, r_local_fieldmajor):
         """r_local: [u1 owned ; u2 owned] (length 2*nloc) -> z_local, same layout."""

@@ -40,12 +40,33 @@ def _system(problem, kw):
     return M, s, kw
 
 
+def _c_kw(kw):
+    """oracle Params keys -> the C-ABI's enum values"""
+    c = dict(kw)
+    if c.get('smoother') == 'POLY':
+        c['smoother'] = 12
+    if 'cycle_type' in c:
+        c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
+    return c
+
+
+def _cycle_kw(kw):
+    """oracle Params keys -> dist_ref.DistCycle flags"""
+    return dict(wcycle=kw.get('cycle_type') == 'W', scaling=bool(kw.get('coarse_scaling', 0)),
+                nu1=kw.get('presmooth_iter', 1), nu2=kw.get('postsmooth_iter', 1))
+
+
 @pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('bidomain', dict(smoother='POLY')),
-                                        ('emi', {}), ('emi', dict(smoother='POLY'))])
+                                        ('emi', {}), ('emi', dict(smoother='POLY')),
+                                        ('bidomain', dict(cycle_type='W')),
+                                        ('bidomain', dict(coarse_scaling=1)),
+                                        ('bidomain', dict(cycle_type='W', coarse_scaling=1, presmooth_iter=2,
+                                                          postsmooth_iter=2)),
+                                        ('emi', dict(smoother='POLY', cycle_type='W', coarse_scaling=1))])
 @pytest.mark.parametrize('P,rep', [(1, 100), (2, 100), (2, 10 ** 6), (3, 100), (4, 100)])
 def test_dist_cycle_threads(lib_built, P, rep, problem, kw):
     M, s, kw = _system(problem, kw)
-    ckw = dict(kw, smoother=12) if kw.get('smoother') == 'POLY' else kw
+    ckw = _c_kw(kw)
     H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **ckw)
     prm = mo.Params(num_functions=2, **kw)
     h = mo.setup(s.scipy(), prm, idofs=s.idofs)
@@ -60,7 +81,7 @@ def test_dist_cycle_threads(lib_built, P, rep, problem, kw):
 
     def run(p):
         L0 = lvls[p][0]
-        dc = dr.DistCycle(lvls[p], Ainv, comm.view(p), poly)
+        dc = dr.DistCycle(lvls[p], Ainv, comm.view(p), poly, **_cycle_kw(kw))
         outs[p] = dc.apply_local(dr.local_slice(r, s.nv, L0['o0'], L0['o1']))
 
     th = [threading.Thread(target=run, args=(p,)) for p in range(P)]
@@ -123,7 +144,7 @@ def _gloo_worker(rank, world, port, q, problem='bidomain', kw=None):
         import dist_ref
         import mamg_oracle
         M, s, kw = _system(problem, kw or {})
-        ckw = dict(kw, smoother=12) if kw.get('smoother') == 'POLY' else kw
+        ckw = _c_kw(kw)
         H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **ckw)
         plan = M.DistPlan(H, rank, world, 100)
         lv = [plan.level(l) for l in range(plan.num_levels)]
@@ -131,14 +152,15 @@ def _gloo_worker(rank, world, port, q, problem='bidomain', kw=None):
         r = mamg_oracle.seeded_rhs(s.N)
         prm = mamg_oracle.Params(num_functions=2, **kw)
         poly = mamg_oracle.poly_weights(prm) if prm.smoother == 'POLY' else None
-        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm(), poly)
+        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm(), poly, **_cycle_kw(kw))
         z = dc.apply_local(dist_ref.local_slice(r, s.nv, lv[0]['o0'], lv[0]['o1']))
         q.put((rank, lv[0]['o0'], lv[0]['o1'], z))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother='POLY'))])
+@pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother='POLY')),
+                                        ('bidomain', dict(cycle_type='W', coarse_scaling=1))])
 def test_dist_cycle_gloo_world2(lib_built, problem, kw):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')

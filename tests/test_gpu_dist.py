@@ -79,6 +79,42 @@ def test_virtual_ranks_poly_and_emi(lib_built, problem, kw, P):
         hh.close()
 
 
+@pytest.mark.parametrize('kw,P,rep', [
+    (dict(cycle_type='W'), 2, 100), (dict(cycle_type='W'), 3, 1), (dict(coarse_scaling=1), 3, 100),
+    (dict(coarse_scaling=1), 8, 1), (dict(cycle_type='W', coarse_scaling=1, presmooth_iter=2, postsmooth_iter=2), 3, 1),
+    (dict(smoother='POLY', coarse_scaling=1, cycle_type='W'), 8, 100),
+    (dict(AMG_type='UA', aggregation_type='HEM', cycle_type='W', coarse_scaling=1), 4, 1)])
+def test_virtual_ranks_w_cycle_and_scaling(lib_built, kw, P, rep):
+    """The W-cycle (second coarse visit: halo + coarse residual, the whole
+    coarse cycle again, x += e), coarse-grid correction scaling (halo,
+    q = A_c e on the owned rows, dot partials all-reduced, alpha on every rank,
+    ghosts scaled with their owners) and more than one sweep per smoothing on
+    P virtual ranks equal the single-rank oracle apply (src/amg_parameters.py:
+    69, 74-75, 78); rep_nodes 1 keeps every level above the coarsest
+    distributed."""
+    import torch
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e6)
+    ckw = dict(kw)
+    conv = {'smoother': {'POLY': 12}, 'cycle_type': {'W': 2}, 'AMG_type': {'UA': 1}, 'aggregation_type': {'HEM': 5}}
+    for k, m in conv.items():
+        if k in ckw:
+            ckw[k] = m[ckw[k]]
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
+                          num_functions=2, **ckw) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    z = _gather(s, hs, zs)
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
+    for hh in hs:
+        hh.close()
+
+
 @pytest.mark.parametrize('case,P,rep', [('bidomain', 3, 100), ('bidomain', 8, 1), ('unfused', 2, 100),
                                          ('emi_poly', 4, 100), ('bidomain2d', 5, 10), ('sell', 3, 100),
                                          ('merged', 2, 100)])
