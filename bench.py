@@ -369,6 +369,7 @@ def main():
     # only when it was measured on this kernel source (device.hip sha256)
     # and this layout; the line carries its provenance either way.
     fmt0 = B.level_format(0) if world == 1 and layout == 'bsr2' else {}
+    kregion = B.kregion if world == 1 and layout == 'bsr2' else None
     post_mode = 'k' if (fmt0.get('post_k') or world > 1) else 'merged'   # rank-local K by default
     a0_mode = 'half' if fmt0.get('half') else 'sell'
     traffic, traffic_src = {}, None
@@ -440,6 +441,7 @@ def main():
         'roofline': roofline,
         'roofline_kernels': rooflines,
         'level0_format': fmt0,
+        'k_region': kregion,
         'cpu_baseline': cpu,
         'setup': dict(setup_info, generate_s=round(t_gen, 2)),
         'breakdown': breakdown,

@@ -23,6 +23,8 @@ def main():
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--moves', default='val:4,col:3,x1:3,r1:3,w:3,e:2')
     ap.add_argument('--variants', default='0', help='K kernel variants timed at every placement')
+    ap.add_argument('--shuffle', type=int, default=0,
+                    help='store K\'s SELL slices in a scrambled order (groups of this many slices) first')
     args = ap.parse_args()
     import torch
     import metric_amg_examples_amd as M
@@ -35,14 +37,20 @@ def main():
     st = torch.cuda.current_stream()
 
     def timed(tag):
-        for v in args.variants.split(','):
-            os.environ['MAMG_K_VARIANT'] = v
+        for v in args.variants.split(','):   # <K variant>[s|t]: K values split globally / per slot row
+            os.environ['MAMG_K_VARIANT'] = v.rstrip('st')
+            os.environ['MAMG_K_LAYOUT'] = 'split' if v.endswith('s') else 'split2' if v.endswith('t') else 'block'
             B.time_apply(r, z, 3, 0, st)
             ms, kms, _ = B.time_apply(r, z, args.reps, 0, st)
-            print(json.dumps({'moved': tag, 'variant': int(v), 'K_ms': round(kms[1], 4),
+            print(json.dumps({'moved': tag, 'variant': v, 'K_ms': round(kms[1], 4),
                               'resid_ms': round(kms[0], 4), 'ms_per_apply': round(ms, 4)}), flush=True)
         os.environ['MAMG_K_VARIANT'] = '0'
+        os.environ['MAMG_K_LAYOUT'] = 'block'
 
+    if args.shuffle:
+        os.environ['MAMG_K_SHUFFLE'] = str(args.shuffle)
+        B.time_apply(r, z, 1, 0, st)          # performs the re-layout
+        del os.environ['MAMG_K_SHUFFLE']
     timed('start')
     timed('start')
     for item in args.moves.split(','):

@@ -7,7 +7,8 @@ physical placement of the operators.
     python bench/kvariants.py [--nrefs 6] [--reps 20] [--rounds 3] k0 k1 k0r1 k0s
 
 A variant is a word of k<K variant>, r<residual variant>, q<restriction
-variant> and s (K values in the split layout; default one block per slot).
+variant> and s / t (K values split into two streams globally / inside each
+slot row; default one block per slot).
 
 Variants are timed round-robin (`rounds` times each) with mamg_time_apply
 mode 0 (HIP events around the level-0 residual and K launches of every
@@ -50,7 +51,7 @@ def main():
             os.environ['MAMG_K_VARIANT'] = tok.get('k', '0')
             os.environ['MAMG_R_VARIANT'] = tok.get('r', '0')
             os.environ['MAMG_RR_VARIANT'] = tok.get('q', '0')
-            os.environ['MAMG_K_LAYOUT'] = 'split' if v.endswith('s') else 'block'
+            os.environ['MAMG_K_LAYOUT'] = 'split' if v.endswith('s') else 'split2' if v.endswith('t') else 'block'
             B.time_apply(r, z, 3, 0, stream)                       # warm
             _, cms, _ = B.time_apply(r, z, 5, 1, stream)           # every launch timed: class ms
             ms, kms, _ = B.time_apply(r, z, args.reps, 0, stream)

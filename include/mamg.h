@@ -319,6 +319,10 @@ enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_PO
 int mamg_level_format(const mamg_handle* h, int level);
 /* The parameters the handle runs (as mamg_hier_params). */
 int mamg_handle_params(const mamg_handle* h, mamg_params* out);
+/* Placement of the level-0 K values: the K kernel's
+ * time per candidate memory region tried at upload, ms[0 .. *n) (at most cap),
+ * and the index kept (*kept = -1: no selection ran). */
+int mamg_kregion_info(const mamg_handle* h, double* ms, int cap, int* n, int* kept);
 /* Algorithmic HBM bytes of one apply (SURVEY 8d formula) and of its dominant
  * kernel class; see DESIGN.md section 4. */
 int mamg_apply_bytes(const mamg_handle* h, double* total_bytes);

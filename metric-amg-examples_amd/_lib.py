@@ -117,6 +117,7 @@ SIGNATURES = {
     'mamg_device_layout': (C.c_int, [VP]),
     'mamg_level_format': (C.c_int, [VP, C.c_int]),
     'mamg_handle_params': (C.c_int, [VP, C.POINTER(mamg_params)]),
+    'mamg_kregion_info': (C.c_int, [VP, P_F64, C.c_int, P_I32, P_I32]),
     'mamg_apply_bytes': (C.c_int, [VP, P_F64]),
     'mamg_apply': (C.c_int, [VP, P_F64, P_F64]),
     'mamg_apply_device': (C.c_int, [VP, VP, VP, VP]),

@@ -234,6 +234,15 @@ class MetricAMG:
                 'bands': bool(f & 64), 'patches': bool(f & 128), 'gs': bool(f & 256)}
 
     @property
+    def kregion(self) -> dict:
+        """Placement of the level-0 K values chosen at upload: K ms per
+        candidate memory region and the index kept (mamg_kregion_info)."""
+        ms = (C.c_double * 16)()
+        n, kept = C.c_int(), C.c_int()
+        _lib.check(self._L.mamg_kregion_info(self._h, ms, 16, C.byref(n), C.byref(kept)))
+        return {'candidates_ms': [round(ms[i], 4) for i in range(min(n.value, 16))], 'kept': kept.value}
+
+    @property
     def effective_params(self) -> dict:
         """The parameters the handle runs, after the reference's Schwarz
         names are resolved (mamg_handle_params)."""

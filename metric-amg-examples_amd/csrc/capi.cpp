@@ -623,6 +623,15 @@ int mamg_handle_params(const mamg_handle* h, mamg_params* out) {
   return MAMG_OK;
 }
 
+int mamg_kregion_info(const mamg_handle* h, double* ms, int cap, int* n, int* kept) {
+  if (!h || !n || !kept || (cap > 0 && !ms)) { set_error("null argument"); return MAMG_ERR_ARG; }
+  std::vector<double> v;
+  mamg::dev_kregion(h->d, &v, kept);
+  *n = (int)v.size();
+  for (int i = 0; i < cap && i < (int)v.size(); ++i) ms[i] = v[i];
+  return MAMG_OK;
+}
+
 int mamg_apply_bytes(const mamg_handle* h, double* total) {
   if (!h || !total) { set_error("null argument"); return MAMG_ERR_ARG; }
   *total = mamg::dev_apply_bytes(h->d);

@@ -25,6 +25,7 @@ int dev_num_levels(const DeviceHandle* h);
 int dev_layout(const DeviceHandle* h);
 int dev_level_format(const DeviceHandle* h, int level);
 mamg_params dev_params(const DeviceHandle* h);
+void dev_kregion(const DeviceHandle* h, std::vector<double>* ms, int* kept);
 double dev_apply_bytes(const DeviceHandle* h);
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
 int dev_apply_host(DeviceHandle* h, const double* r, double* z, std::string* err);

@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <numeric>
 #include <vector>
 
 #include "device.h"
@@ -59,6 +60,8 @@ enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4,
 
 typedef double dv4 __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
+
+constexpr int SCALE_BLOCKS = 256;   // partial-sum blocks of the coarse-scaling dots
 
 // ---------------------------------------------------------------------------
 // CSR kernels (general layout)
@@ -282,6 +285,21 @@ __device__ __forceinline__ dv4 blk_split(const double* __restrict__ v, int64_t n
   const dv2 b = reinterpret_cast<const dv2*>(v + 2 * nbs)[k];
   return dv4{a.x, a.y, b.x, b.y};
 }
+// split inside each 64-slot SELL slot row: the row's 64 (0,0)(0,1) pairs
+// (1 KB) then its 64 (1,0)(1,1) pairs, so a 16-byte-per-lane load of
+// consecutive slots reads one contiguous piece and the slot row stays 2 KB
+__device__ __forceinline__ dv4 blk_split_local(const double* __restrict__ v, int64_t k) {
+  const int64_t r = k & ~(int64_t)63, i = k & 63;
+  const dv2 a = reinterpret_cast<const dv2*>(v + 4 * r)[i];
+  const dv2 b = reinterpret_cast<const dv2*>(v + 4 * r + 128)[i];
+  return dv4{a.x, a.y, b.x, b.y};
+}
+template <int SPL>
+__device__ __forceinline__ dv4 blk_any(const double* __restrict__ v, int64_t nbs, int64_t k) {
+  if (SPL == 1) return blk_split(v, nbs, k);
+  if (SPL == 2) return blk_split_local(v, k);
+  return reinterpret_cast<const dv4*>(v)[k];
+}
 
 template <int EPI, bool XFM, bool SYM, int U, bool SPL, int TAG>
 __global__ __launch_bounds__(256) void sell2_kernel(
@@ -354,7 +372,7 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 // the block loop.  Used for the level-0 fused post operator
 // z = x1 + W r1 + K e (EPI_KPOST, LPR 2, U 5: K 1.69 -> 1.54 ms on one
 // upload) and the SELL-stored coarse operators.
-template <int LPR, int U, int EPI, bool XFM, bool SYM, bool SPL, int TAG, int PROBE = 0>
+template <int LPR, int U, int EPI, bool XFM, bool SYM, int SPL, int TAG, int PROBE = 0>
 __global__ __launch_bounds__(256) void msell_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
@@ -386,7 +404,7 @@ __global__ __launch_bounds__(256) void msell_kernel(
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
       c[u] = bcol[kk];
-      v[u] = SPL ? blk_split(bval, nbs, kk) : blk<SYM>(bval, offd, kk);
+      v[u] = SPL ? blk_any<SPL>(bval, nbs, kk) : blk<SYM>(bval, offd, kk);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)   // PROBE 1 (A/B only, wrong results): no gather, the column as the value
@@ -935,6 +953,188 @@ __global__ __launch_bounds__(256) void gs2_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Coarse tail: the whole cycle of the levels from tail_level down (the
+// recursion below one coarse level, V or W), run by ONE workgroup of 1024
+// threads that walks the same op list the launch path would launch, with a
+// workgroup barrier between ops instead of a kernel boundary.  Each op
+// computes every row exactly as its kernel does (same lane groups, chunks,
+// shuffle order; runtime lane count), so the results equal the launch path's
+// up to FMA contraction.  For the deep levels of the reference family's
+// W-cycle (HEM ratio ~4, levels visited 2^l times, one launch per colour)
+// this replaces tens of thousands of ~5 us launches per apply.
+// ---------------------------------------------------------------------------
+enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7 };
+struct TOp {
+  int kind = 0, epi = 0, vl = 1, sym = 0;
+  int64_t n = 0, r0 = 0, r1 = 0, nb = 0;
+  const int64_t* ptr = nullptr;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  const double *x = nullptr, *y = nullptr, *b = nullptr, *w = nullptr;
+  const dv4* W = nullptr;
+  double* out = nullptr;
+  const int32_t* perm = nullptr;
+  double* part = nullptr;
+};
+constexpr int TAIL_THREADS = 1024;
+
+// rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
+// vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place
+__device__ void tail_bsr(const TOp& o, bool gs) {
+  const int VL = o.vl;
+  const int lane = threadIdx.x & (VL - 1);
+  const int64_t rows = gs ? o.r1 - o.r0 : o.n;
+  const double* offd = o.sym ? o.val + 2 * o.nb : nullptr;
+  const double2* x2 = reinterpret_cast<const double2*>(o.x);
+  for (int64_t base = 0; base < rows * VL; base += TAIL_THREADS) {   // uniform trip count
+    const int64_t v = base + threadIdx.x;
+    const int64_t node = (gs ? o.r0 : 0) + v / VL;
+    const bool live = v / VL < rows;
+    double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+    if (live) {
+      const int64_t p0 = o.ptr[node], p1 = o.ptr[node + 1];
+      for (int64_t kb0 = p0; kb0 < p1; kb0 += 2 * VL) {
+        const int64_t ka = kb0 + lane, kb = ka + VL;
+        const bool ha = ka < p1, hb = kb < p1;
+        const int64_t la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
+        const int32_t c0 = o.col[la], c1 = o.col[lb];
+        const dv4 v0 = o.sym ? blk<true>(o.val, offd, la) : blk<false>(o.val, nullptr, la);
+        const dv4 v1 = o.sym ? blk<true>(o.val, offd, lb) : blk<false>(o.val, nullptr, lb);
+        const double2 a = x2[c0], e = x2[c1];
+        s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
+        s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
+        t0 += hb ? v1.x * e.x + v1.y * e.y : 0.0;
+        t1 += hb ? v1.z * e.x + v1.w * e.y : 0.0;
+      }
+    }
+    s0 += t0;
+    s1 += t1;
+    for (int off = VL / 2; off > 0; off >>= 1) {
+      s0 += __shfl_xor(s0, off, VL);
+      s1 += __shfl_xor(s1, off, VL);
+    }
+    if (!live || lane != 0) continue;
+    if (gs) {
+      if (o.perm[node] < 0) continue;
+      const int64_t I = o.perm[node];
+      const double r0 = o.b[2 * I] - s0, r1 = o.b[2 * I + 1] - s1;
+      const dv4 d = o.W[node];
+      const double2 xi = x2[I];
+      o.out[2 * I] = xi.x + (d.x * r0 + d.y * r1);
+      o.out[2 * I + 1] = xi.y + (d.z * r0 + d.w * r1);
+      continue;
+    }
+    double o0, o1;
+    if (o.epi == EPI_Y) {
+      o0 = s0; o1 = s1;
+    } else if (o.epi == EPI_YADD) {
+      o0 = o.y[2 * node] + s0; o1 = o.y[2 * node + 1] + s1;
+    } else if (o.epi == EPI_RESID) {
+      o0 = o.b[2 * node] - s0; o1 = o.b[2 * node + 1] - s1;
+    } else if (o.epi == EPI_KPOST) {
+      const double r0 = o.b[2 * node], r1 = o.b[2 * node + 1];
+      const dv4 w = o.W[node];
+      o0 = o.y[2 * node] + (w.x * r0 + w.y * r1) + s0;
+      o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1) + s1;
+    } else {  // EPI_BJAC
+      const double r0 = o.b[2 * node] - s0, r1 = o.b[2 * node + 1] - s1;
+      const dv4 w = o.W[node];
+      o0 = o.y[2 * node] + (w.x * r0 + w.y * r1);
+      o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1);
+    }
+    o.out[2 * node] = o0;
+    o.out[2 * node + 1] = o1;
+  }
+}
+
+__global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ prog, int nops) {
+  __shared__ double red[TAIL_THREADS / 64][2];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  for (int k = 0; k < nops; ++k) {
+    const TOp o = prog[k];
+    switch (o.kind) {
+      case T_BSR: tail_bsr(o, false); break;
+      case T_GS: tail_bsr(o, true); break;
+      case T_BD:
+        for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
+          const double b0 = o.b[2 * I], b1 = o.b[2 * I + 1];
+          const dv4 w = o.W[I];
+          o.out[2 * I] = w.x * b0 + w.y * b1;
+          o.out[2 * I + 1] = w.z * b0 + w.w * b1;
+        }
+        break;
+      case T_AXPY:
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.out[i] + o.x[i];
+        break;
+      case T_ZERO:
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = 0.0;
+        break;
+      case T_GEMV:   // gemv_kernel: one wave per row
+        for (int64_t row0 = 0; row0 < o.n; row0 += TAIL_THREADS / 64) {
+          const int64_t row = row0 + wave;
+          double sum = 0.0;
+          if (row < o.n) {
+            const double* a = o.w + row * o.n;
+            for (int64_t j = lane; j < o.n; j += 64) sum += a[j] * o.x[j];
+          }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+          if (row < o.n && lane == 0) o.out[row] = sum;
+        }
+        break;
+      case T_DOT2:   // dot2_partial_kernel's SCALE_BLOCKS blocks, four at a time
+        for (int vb0 = 0; vb0 < SCALE_BLOCKS; vb0 += TAIL_THREADS / 256) {
+          const int vb = vb0 + (t >> 8), tt = t & 255;
+          double a = 0.0, c = 0.0;
+          for (int64_t i = (int64_t)vb * 256 + tt; i < o.n; i += (int64_t)SCALE_BLOCKS * 256) {
+            a += o.b[i] * o.x[i];
+            c += o.y[i] * o.x[i];
+          }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            c += __shfl_xor(c, off, 64);
+          }
+          if (lane == 0) { red[wave][0] = a; red[wave][1] = c; }
+          __syncthreads();
+          if (tt == 0) {
+            const int w0 = (t >> 8) * 4;
+            o.part[2 * vb] = (red[w0][0] + red[w0 + 1][0]) + (red[w0 + 2][0] + red[w0 + 3][0]);
+            o.part[2 * vb + 1] = (red[w0][1] + red[w0 + 1][1]) + (red[w0 + 2][1] + red[w0 + 3][1]);
+          }
+          __syncthreads();
+        }
+        break;
+      case T_CSCALE: {   // cscale_kernel: alpha from the partials (one block's order), then scale
+        __shared__ double alpha;
+        if (t < 256) {
+          double a = 0.0, c = 0.0;
+          for (int i = t; i < SCALE_BLOCKS; i += 256) { a += o.part[2 * i]; c += o.part[2 * i + 1]; }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            c += __shfl_xor(c, off, 64);
+          }
+          if (lane == 0) { red[wave][0] = a; red[wave][1] = c; }
+        }
+        __syncthreads();
+        if (t == 0) {
+          const double num = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+          const double den = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+          alpha = den > 0.0 ? num / den : 1.0;
+        }
+        __syncthreads();
+        const double al = alpha;
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = al * o.out[i];
+        break;
+      }
+      default: break;
+    }
+    __syncthreads();   // the next op reads what this one wrote (workgroup-scope visibility)
+  }
+}
+
 __device__ __forceinline__ uint32_t hash32_dev(uint64_t i, int level) {   // = host.h hash32
   uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
   const uint32_t lv = (uint32_t)(((uint64_t)(int64_t)level * 0x85EBCA77ull) & 0xFFFFFFFFull);
@@ -1336,7 +1536,6 @@ __global__ __launch_bounds__(256) void perm_fill_kernel(int64_t nr, const int32_
 // e <- alpha e; alpha = 1 if the denominator is not positive.  Partial sums
 // per block, then every block of the scaling launch reduces the partials in
 // the same fixed order (so all agree on alpha).  Oracle: mamg_oracle.coarse_scale.
-constexpr int SCALE_BLOCKS = 256;
 __global__ __launch_bounds__(256) void dot2_partial_kernel(int64_t n, const double* __restrict__ bc,
                                                            const double* __restrict__ e,
                                                            const double* __restrict__ q,
@@ -1415,7 +1614,9 @@ int g_kvar = 0;
 int g_rvar = 0;
 int g_rrvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
-int64_t g_msell_min_rows = (int64_t)1 << 40;   // off: coarse levels 0.41 -> 0.50 ms
+int64_t g_msell_min_rows = (int64_t)1 << 40;
+int64_t g_tail_nodes = 4096;
+bool g_tail_set = false;   // MAMG_TAIL_NODES given: applies to every smoother (tests)   // off: coarse levels 0.41 -> 0.50 ms
 void read_kvar() {
   const char* e = std::getenv("MAMG_K_VARIANT");
   g_kvar = e ? std::atoi(e) : 0;
@@ -1430,6 +1631,9 @@ void read_knobs() {
   g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
+  e = std::getenv("MAMG_TAIL_NODES");
+  g_tail_nodes = e ? std::atoll(e) : 4096;
+  g_tail_set = e != nullptr;
   e = std::getenv("MAMG_MSELL_MIN_ROWS");
   g_msell_min_rows = e ? std::atoll(e) : ((int64_t)1 << 40);
   e = std::getenv("MAMG_HALF");
@@ -1477,7 +1681,8 @@ struct DBsr {              // 2x2 blocks, node-major
   // SELL-64 storage (sell == true): ptr unused; soff per slice, meta per row,
   // col / val hold nbs (>= nb, padded) slots
   bool sell = false;
-  bool split = false;       // SELL general blocks as two 16-byte streams (sell2_kernel SPL)
+  int split = 0;            // SELL general blocks as two 16-byte streams (1: two global streams,
+                            // 2: split inside each slot row; sell2_kernel / msell_kernel SPL)
   int lpr = 1;              // SELL lanes per row: 1 sell2_kernel, > 1 msell_kernel
   int64_t nbs = 0;
   int64_t* soff = nullptr;
@@ -1551,7 +1756,7 @@ struct DLevel {
 };
 
 enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7,
-              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11, OP_PATCH = 12 };
+              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11, OP_PATCH = 12, OP_TAIL = 13 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -1581,6 +1786,7 @@ struct Op {
   const int32_t* perm = nullptr;    // GS: node of each permuted row
   double* part = nullptr;           // DOT2 / CSCALE partial sums
   const struct DLevel* lev = nullptr;   // PATCH: the level's patch data
+  const TOp* prog = nullptr;        // TAIL: the device op list (n ops)
   double bytes = 0.0;
 };
 
@@ -1626,6 +1832,13 @@ struct DeviceHandle {
   hipStream_t cap = nullptr;
   std::vector<Graph> graphs;
   std::vector<PcgGraph> pcgs;
+  // coarse tail (tail_kernel): first level run by it (0 = off) and the
+  // device op lists built so far, one per (b, x) entry of that level
+  int tail_level = 0;
+  std::vector<double> kregion_ms;  // select_k_region: K ms per candidate region, the one kept
+  int kregion_best = -1;
+  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; };
+  mutable std::vector<TailProg> tails;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
   double *cr = nullptr, *cz = nullptr, *cd = nullptr, *cq = nullptr;  // PCG
@@ -1645,6 +1858,7 @@ struct DeviceHandle {
       if (g.graph) (void)hipGraphDestroy(g.graph);
     }
     for (auto& g : pcgs) g.release();
+    for (auto& t : tails) (void)hipFree(t.prog);
     for (void* a : allocs) (void)hipFree(a);
     if (hres) (void)hipHostFree(hres);
     if (cap) (void)hipStreamDestroy(cap);
@@ -2522,6 +2736,32 @@ __global__ __launch_bounds__(256) void split_blocks_kernel(int64_t nbs, const dv
   out[nbs + k] = dv2{v.z, v.w};
 }
 
+__global__ __launch_bounds__(256) void split_local_kernel(int64_t nbs, const dv4* __restrict__ in, double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nbs) return;
+  const dv4 v = in[k];
+  const int64_t r = k & ~(int64_t)63, i = k & 63;
+  reinterpret_cast<dv2*>(out + 4 * r)[i] = dv2{v.x, v.y};
+  reinterpret_cast<dv2*>(out + 4 * r + 128)[i] = dv2{v.z, v.w};
+}
+__global__ __launch_bounds__(256) void unsplit_local_kernel(int64_t nbs, const double* __restrict__ in, dv4* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nbs) return;
+  out[k] = blk_split_local(in, k);
+}
+// SELL slice s (64 w_s slots) moved from soff_old[s] to soff_new[s] (one workgroup per slice)
+__global__ __launch_bounds__(256) void slice_move_kernel(int64_t ns, const int64_t* __restrict__ so,
+                                                         const int64_t* __restrict__ sn, const dv4* __restrict__ vin,
+                                                         const int32_t* __restrict__ cin, dv4* __restrict__ vout,
+                                                         int32_t* __restrict__ cout) {
+  const int64_t sl = blockIdx.x;
+  if (sl >= ns) return;
+  const int64_t a = so[sl], len = so[sl + 1] - so[sl], d = sn[sl];
+  for (int64_t i = threadIdx.x; i < len; i += 256) {
+    vout[d + i] = vin[a + i];
+    cout[d + i] = cin[a + i];
+  }
+}
 __global__ __launch_bounds__(256) void unsplit_blocks_kernel(int64_t nbs, const dv2* __restrict__ in, dv4* __restrict__ out) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= nbs) return;
@@ -2891,8 +3131,72 @@ void scale_ops(const DeviceHandle* h, int lc, std::vector<Op>* ops) {
 
 // ---- BSR2 layout.  b / xout of level 0 are the caller's field-major vectors
 // (stride nv0); all other vectors are node-interleaved (stride 0).
+// one op of the launch path as a coarse-tail op (tail_kernel); false if
+// the tail cannot express it (level-0 formats and strides, patches, CSR)
+bool to_tail(const Op& o, TOp* t) {
+  *t = TOp();
+  switch (o.kind) {
+    case OP_BSR:
+    case OP_GS: {
+      const DBsr& M = *o.Mb;
+      if (M.sell || M.half || M.split || o.xs || o.bs || o.os || o.xfm || M.lanes < 1 || M.lanes > 64) return false;
+      t->kind = o.kind == OP_GS ? T_GS : T_BSR;
+      t->epi = o.epi; t->vl = M.lanes; t->sym = M.sym ? 1 : 0; t->n = M.nr; t->nb = M.nb;
+      t->ptr = M.ptr; t->col = M.col; t->val = M.val;
+      t->x = o.kind == OP_GS ? o.out : o.x; t->y = o.y; t->b = o.b; t->W = o.W; t->out = o.out;
+      t->r0 = o.r0; t->r1 = o.r1; t->perm = o.perm;
+      return true;
+    }
+    case OP_BD:
+      if (o.bs || o.os) return false;
+      t->kind = T_BD; t->n = o.n; t->W = o.W; t->b = o.b; t->out = o.out;
+      return true;
+    case OP_GEMV: t->kind = T_GEMV; t->n = o.n; t->w = o.w; t->x = o.x; t->out = o.out; return true;
+    case OP_AXPY: t->kind = T_AXPY; t->n = o.n; t->x = o.x; t->out = o.out; return true;
+    case OP_ZERO: t->kind = T_ZERO; t->n = o.n; t->out = o.out; return true;
+    case OP_DOT2: t->kind = T_DOT2; t->n = o.n; t->b = o.b; t->x = o.x; t->y = o.y; t->part = o.part; return true;
+    case OP_CSCALE: t->kind = T_CSCALE; t->n = o.n; t->part = o.part; t->out = o.out; return true;
+    default: return false;
+  }
+}
+
 void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
-                   int64_t os, std::vector<Op>* ops) {
+                   int64_t os, std::vector<Op>* ops, bool tail_ok = true);
+
+// the cycle of level l and everything below as one tail_kernel launch; the
+// device op list is built once per (b, x) and kept on the handle
+bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
+  const DeviceHandle::TailProg* tp = nullptr;
+  for (const auto& t : h->tails)
+    if (t.b == b && t.x == xout) tp = &t;
+  if (!tp) {
+    std::vector<Op> sub;
+    cycle_ops_bsr(h, l, b, 0, xout, 0, &sub, false);
+    std::vector<TOp> prog(sub.size());
+    double bytes = 0.0;
+    for (size_t k = 0; k < sub.size(); ++k) {
+      if (!to_tail(sub[k], &prog[k])) return false;
+      bytes += sub[k].bytes;
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, prog.size() * sizeof(TOp)) != hipSuccess) { (void)hipGetLastError(); return false; }
+    if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(d);
+      return false;
+    }
+    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes});
+    tp = &h->tails.back();
+  }
+  Op o;
+  o.kind = OP_TAIL; o.cls = C_COARSE; o.prog = tp->prog; o.n = tp->n; o.bytes = tp->bytes;
+  ops->push_back(o);
+  return true;
+}
+
+void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
+                   int64_t os, std::vector<Op>* ops, bool tail_ok) {
+  if (tail_ok && l > 0 && l == h->tail_level && bs == 0 && os == 0 && tail_ops(h, l, b, xout, ops)) return;
   const DLevel& L = h->L[l];
   const mamg_params& p = h->p;
   const bool l0 = l == 0;
@@ -2936,10 +3240,10 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   ops->push_back(bsr_op(L.Rb, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, 0, nullptr, nullptr, 0,
                         nullptr, C.b, 0));
   ops->back().remap = 1;
-  cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops);
+  cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops, tail_ok);
   if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
     ops->push_back(bsr_op(C.Ab, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0));
-    cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops);
+    cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops, tail_ok);
     ops->push_back(axpy_op(C.n, C.e, C.x));
   }
   if (p.coarse_scaling) scale_ops(h, l + 1, ops);
@@ -3089,7 +3393,7 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 #undef SELL_ARGS
 }
 
-template <int LPR, int U, bool XFM, bool SYM, bool SPL, int TAG, int PROBE = 0>
+template <int LPR, int U, bool XFM, bool SYM, int SPL, int TAG, int PROBE = 0>
 void launch_msell(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const int64_t rows = 256 / LPR;
@@ -3113,10 +3417,10 @@ void launch_msell(const Op& o, hipStream_t s) {
 // mamg_time_apply): 0 two lanes per row, chunks of 5 (default); 1 one lane
 // per row, chunks of 6 (sell2_kernel, round 2); 2 four lanes per row, chunks
 // of 3; 9 a probe without the e gathers (wrong results, timing only)
-template <bool SPL>
+template <int SPL>
 bool launch_kvariant(const Op& o, hipStream_t s) {
   switch (g_kvar) {
-    case 1: return false;
+    case 1: return SPL == 2 ? (launch_msell<1, 6, false, false, SPL, 0>(o, s), true) : false;
     case 2: launch_msell<4, 3, false, false, SPL, 0>(o, s); return true;
     case 3: launch_msell<2, 5, false, false, SPL, 0>(o, s); return true;   // XCD-contiguous rows
     case 9: launch_msell<2, 5, false, false, SPL, 0, 1>(o, s); return true;
@@ -3130,7 +3434,10 @@ void launch_sell_x(const Op& o, hipStream_t s) {
   // coarse operators: lanes per row from the mean row length; everything else
   // one lane, chunks of 8
   if constexpr (TAG == 0 && !XFM && !SYM) {
-    if (o.epi == EPI_KPOST && (o.Mb->split ? launch_kvariant<true>(o, s) : launch_kvariant<false>(o, s))) return;
+    if (o.epi == EPI_KPOST && (o.Mb->split == 2   ? launch_kvariant<2>(o, s)
+                               : o.Mb->split ? launch_kvariant<1>(o, s)
+                                             : launch_kvariant<0>(o, s)))
+      return;
   }
   if constexpr (!XFM) {
     if (o.Mb->lpr > 1 && !o.Mb->split) {
@@ -3316,6 +3623,9 @@ void launch(const Op& o, hipStream_t s) {
     case OP_DOT2:
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
       break;
+    case OP_TAIL:
+      if (o.n) tail_kernel<<<1, TAIL_THREADS, 0, s>>>(o.prog, (int)o.n);
+      break;
     case OP_CSCALE:
       if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
       break;
@@ -3420,12 +3730,91 @@ void rehome_bsr(DeviceHandle* h, DBsr& M) {
   rehome_array(h, (void**)&M.col, (size_t)slots * sizeof(int32_t));
 }
 
+// Level-0 K values placed by measurement.  The K
+// kernel's time follows the physical memory region its value stream (5.7 GB at
+// nrefs=6) lands in: 1.37 vs 1.55 ms for the same bytes, layout and kernel,
+// with identical fabric request counts and no TLB misses (bench/kplace.py,
+// profiles/r03_k_placement.txt); slice order, split layouts and XCD row order
+// do not remove it.  So the values are copied into up to MAMG_KREGION_TRIES
+// (4) distinct fresh allocations (physically contiguous where the driver has
+// them), K is timed in each (one warm + three launches), and the fastest
+// region is kept.  Same bytes: results are bitwise equal.
+void select_k_region(DeviceHandle* h) {
+  DLevel& L = h->L[0];
+  DBsr& K = L.KPb;
+  const size_t bytes = (size_t)K.nbs * 4 * sizeof(double);
+  const char* e = std::getenv("MAMG_KREGION_TRIES");
+  const int tries = e ? std::atoi(e) : 4;
+  if (tries <= 1 || K.sym || !L.r || !L.t || !L.Wd || !h->L[1].x) {
+    rehome_array(h, (void**)&K.val, bytes);
+    return;
+  }
+  std::vector<void*> bufs;
+  for (int t = 0; t < tries; ++t) {   // all allocated first: distinct regions
+    void* r = nullptr;
+    if (hipExtMallocWithFlags(&r, bytes, hipDeviceMallocContiguous) != hipSuccess) {
+      (void)hipGetLastError();
+      r = nullptr;
+      if (hipMalloc(&r, bytes) != hipSuccess) { (void)hipGetLastError(); break; }
+    }
+    bufs.push_back(r);
+  }
+  double* out = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (bufs.empty() || hipMalloc(&out, L.n * sizeof(double)) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    (void)hipGetLastError();
+    for (void* b : bufs) (void)hipFree(b);
+    if (out) (void)hipFree(out);
+    rehome_array(h, (void**)&K.val, bytes);
+    return;
+  }
+  void* old = K.val;
+  const Op op = bsr_op(K, EPI_KPOST, C_L0_SMOOTH, 0, h->L[1].x, 0, L.t, L.r, 0, L.Wd, out, L.n / 2);
+  std::vector<float> ms(bufs.size(), 1e30f);
+  size_t best = 0;
+  for (size_t i = 0; i < bufs.size(); ++i) {
+    (void)hipMemcpy(bufs[i], old, bytes, hipMemcpyDeviceToDevice);
+    K.val = (double*)bufs[i];
+    launch(op, nullptr);
+    (void)hipEventRecord(e0, nullptr);
+    for (int k = 0; k < 3; ++k) launch(op, nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms[i], e0, e1);
+    if (ms[i] < ms[best]) best = i;
+  }
+  K.val = (double*)bufs[best];
+  h->allocs.push_back(bufs[best]);
+  for (size_t i = 0; i < bufs.size(); ++i)
+    if (i != best) (void)hipFree(bufs[i]);
+  const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
+  auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
+  if (!in_arena && it != h->allocs.end()) {
+    (void)hipFree(old);
+    h->allocs.erase(it);
+  }
+  (void)hipFree(out);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipGetLastError();
+  if (h->p.print_level >= 2) {
+    std::fprintf(stderr, "[mamg] K value regions (ms per K launch):");
+    for (float m : ms) std::fprintf(stderr, " %.4f", m / 3);
+    std::fprintf(stderr, " -> %zu\n", best);
+  }
+  h->kregion_ms.assign(ms.begin(), ms.end());
+  for (auto& m : h->kregion_ms) m /= 3.0;
+  h->kregion_best = (int)best;
+}
+
 void rehome_operators(DeviceHandle* h) {
   const char* e = std::getenv("MAMG_REHOME");   // 0: keep the operators where the layout builder put them (tests)
   if (e && std::atoi(e) == 0) return;
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < g_sell_min_rows || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
-  rehome_bsr(h, L.KPb);          // the largest stream first
+  select_k_region(h);            // the largest stream first, placed by measurement
+  rehome_array(h, (void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
   if (L.Ab.half) rehome_bsr(h, L.Ab);
   if (!L.Rb.sell && !L.Rb.sym)
     rehome_array(h, (void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
@@ -3442,17 +3831,22 @@ void rehome_operators(DeviceHandle* h) {
 // 16-byte streams per slot (SPL: each wave load reads contiguous pairs).  The
 // arithmetic is the same, so results are bitwise equal either way
 // (test_k_block_layouts_bitwise).  Rearranged in place through a temporary.
-void set_k_split(DBsr& K, bool to_split) {
-  if (!K.sell || K.sym || K.split == to_split || K.nbs == 0) return;
+void set_k_split(DBsr& K, int mode) {
+  if (!K.sell || K.sym || K.split == mode || K.nbs == 0 || (K.nbs & 63)) return;
   void* t = nullptr;
   if (hipMalloc(&t, (size_t)K.nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
-  if (to_split)
-    split_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (dv2*)t);
-  else
-    unsplit_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv2*>(K.val), (dv4*)t);
-  (void)hipMemcpy(K.val, t, (size_t)K.nbs * sizeof(dv4), hipMemcpyDeviceToDevice);
+  const size_t bytes = (size_t)K.nbs * sizeof(dv4);
+  if (K.split) {   // back to one block per slot first
+    if (K.split == 2) unsplit_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, K.val, (dv4*)t);
+    else unsplit_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv2*>(K.val), (dv4*)t);
+    (void)hipMemcpy(K.val, t, bytes, hipMemcpyDeviceToDevice);
+    K.split = 0;
+  }
+  if (mode == 1) split_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (dv2*)t);
+  if (mode == 2) split_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (double*)t);
+  if (mode) (void)hipMemcpy(K.val, t, bytes, hipMemcpyDeviceToDevice);
   (void)hipFree(t);
-  K.split = to_split;
+  K.split = mode;
 }
 
 // Round 2 chose the layout per box by timing both at upload (split 1.57 vs
@@ -3461,10 +3855,25 @@ void set_k_split(DBsr& K, bool to_split) {
 // (DESIGN.md section 4); MAMG_POST_K=2 forces the split layout on every
 // SELL-stored K (tests), MAMG_K_LAYOUT=split|block switches level 0 at
 // mamg_time_apply (A/Bs on one upload).
+// the coarse tail (tail_kernel) takes over from the first level with at most
+// MAMG_TAIL_NODES node rows (0 = off); a coarsest level alone stays a launch
+// and not for the multicolour GS smoothers: a colour step is latency-bound on
+// one CU as much as across the chip, and the reference family's W-cycle ran
+// 80 -> 120 ms per apply with the tail at 4096 nodes (Jacobi V-cycle: 3.495 ->
+// 3.462 ms; bench/tail_ab.py)
+void set_tail_level(DeviceHandle* h) {
+  h->tail_level = 0;
+  if (!h->bsr || g_tail_nodes <= 0 || (gs_smoother(h->p) && !g_tail_set)) return;
+  for (int l = 1; l < (int)h->L.size(); ++l) {
+    if (h->L[l].coarsest) return;
+    if (h->L[l].n / 2 <= g_tail_nodes) { h->tail_level = l; return; }
+  }
+}
+
 void apply_k_layout_knob(DeviceHandle* h) {
   if (!h->bsr || h->L.size() < 2 || g_post_k != 2) return;
   for (DLevel& D : h->L)
-    if (!D.coarsest) set_k_split(D.KPb, true);
+    if (!D.coarsest) set_k_split(D.KPb, 1);
 }
 
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
@@ -3569,6 +3978,10 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
   apply_k_layout_knob(h.get());
+  set_tail_level(h.get());
+  // every layout kernel and device-to-device copy (asynchronous to the host)
+  // done before the handle is used on another stream
+  HIPCHK(hipDeviceSynchronize());
   *out = h.release();
   return MAMG_OK;
 }
@@ -3694,6 +4107,8 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   HIPCHK(hipDeviceSynchronize());
   rehome_operators(h.get());
   apply_k_layout_knob(h.get());
+  set_tail_level(h.get());
+  HIPCHK(hipDeviceSynchronize());   // as in dev_upload
   h->setup_ms[GS_LAYOUT] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = h.release();
@@ -3724,6 +4139,10 @@ int dev_level_format(const DeviceHandle* h, int level) {
 }
 
 mamg_params dev_params(const DeviceHandle* h) { return h->p; }
+void dev_kregion(const DeviceHandle* h, std::vector<double>* ms, int* kept) {
+  *ms = h->kregion_ms;
+  *kept = h->kregion_best;
+}
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
@@ -3932,14 +4351,54 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         h->graphs.clear();
         for (auto& g : h->pcgs) g.release();
         h->pcgs.clear();
+        for (auto& t : h->tails) (void)hipFree(t.prog);
+        h->tails.clear();
         if (std::getenv("MAMG_KMOVE_PRINT"))
           std::fprintf(stderr, "[mamg] moved %s (%zu B) %p -> %p\n", mv, bytes, old, r);
       }
     }
   }
+  if (const char* ks = std::getenv("MAMG_K_SHUFFLE"))   // A/B: SELL slices of K stored in a scrambled order
+    if (h->bsr && h->L.size() > 1 && h->L[0].KPb.sell && !h->L[0].KPb.split && std::atoi(ks) > 0) {
+      DBsr& K = h->L[0].KPb;
+      const int64_t ns = (K.nr + SELL_C - 1) / SELL_C;
+      std::vector<int64_t> so(ns + 1), sn(ns + 1, 0);
+      HIPCHK(hipMemcpy(so.data(), K.soff, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+      // storage order: groups of G consecutive slices; group g stored at place
+      // (g A) mod ngr with A odd, coprime to ngr and ~ngr / golden ratio, so
+      // consecutive groups land far apart; offsets by a scan in storage order
+      const int64_t G = std::max<int64_t>(1, std::atoll(ks));
+      const int64_t ngr = (ns + G - 1) / G;
+      int64_t A = (int64_t)((double)ngr * 0.6180339887) | 1;
+      while (std::gcd(A, ngr) != 1) A += 2;
+      std::vector<int64_t> order(ngr);
+      for (int64_t g = 0; g < ngr; ++g) order[(int64_t)(((__int128)g * A) % ngr)] = g;
+      int64_t off = 0;
+      for (int64_t pl = 0; pl < ngr; ++pl)
+        for (int64_t sl = order[pl] * G; sl < std::min(ns, order[pl] * G + G); ++sl) {
+          sn[sl] = off;
+          off += so[sl + 1] - so[sl];
+        }
+      int64_t* dsn = nullptr;
+      dv4* nv = nullptr;
+      int32_t* nc = nullptr;
+      HIPCHK(hipMalloc(&dsn, (ns + 1) * sizeof(int64_t)));
+      HIPCHK(hipMalloc(&nv, (size_t)K.nbs * sizeof(dv4)));
+      HIPCHK(hipMalloc(&nc, (size_t)K.nbs * sizeof(int32_t)));
+      sn[ns] = off;
+      HIPCHK(hipMemcpy(dsn, sn.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+      slice_move_kernel<<<(unsigned)ns, 256>>>(ns, K.soff, dsn, reinterpret_cast<const dv4*>(K.val), K.col, nv, nc);
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipMemcpy(K.val, nv, (size_t)K.nbs * sizeof(dv4), hipMemcpyDeviceToDevice));
+      HIPCHK(hipMemcpy(K.col, nc, (size_t)K.nbs * sizeof(int32_t), hipMemcpyDeviceToDevice));
+      HIPCHK(hipMemcpy(K.soff, dsn, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+      (void)hipFree(dsn); (void)hipFree(nv); (void)hipFree(nc);
+      for (auto& g : h->graphs) { (void)hipGraphExecDestroy(g.exec); (void)hipGraphDestroy(g.graph); }
+      h->graphs.clear();
+    }
   if (const char* kl = std::getenv("MAMG_K_LAYOUT"))
     if (h->bsr && h->L.size() > 1) {
-      set_k_split(h->L[0].KPb, std::strcmp(kl, "split") == 0);
+      set_k_split(h->L[0].KPb, std::strcmp(kl, "split") == 0 ? 1 : std::strcmp(kl, "split2") == 0 ? 2 : 0);
       HIPCHK(hipDeviceSynchronize());
     }
   std::vector<Op> ops;

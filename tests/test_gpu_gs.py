@@ -119,3 +119,29 @@ def test_sgs_symmetric_and_deterministic(lib_built):
     assert abs(a - c) <= 1e-12 * abs(a)
     assert torch.equal(z1, z1b)
 
+
+
+@pytest.mark.parametrize('dim,n,g,kw', [
+    (3, 16, 1e6, dict(smoother='SGS', coarse_scaling=1, cycle_type='W', AMG_type='UA', aggregation_type='HEM')),
+    (3, 32, 1e6, dict(smoother='SGS', coarse_scaling=1, cycle_type='W', AMG_type='UA', aggregation_type='HEM')),
+    (2, 64, 1e4, dict(smoother='SGS', coarse_scaling=1, cycle_type='W')),
+    (3, 16, 1e6, dict(smoother='SGS')),
+])
+def test_coarse_tail_equals_launches(lib_built, monkeypatch, dim, n, g, kw):
+    """The coarse tail (one 1024-thread workgroup runs the whole cycle below
+    tail_level, device.hip tail_kernel) equals the launch-by-launch cycle up
+    to FMA contraction (1e-13) and the oracle (1e-10): SGS colour sweeps,
+    coarse scaling, W-cycle second visits, the dense coarsest solve."""
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    zs = []
+    for nodes in ('100000000', '0'):
+        monkeypatch.setenv('MAMG_TAIL_NODES', nodes)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+        zs.append(B * r)
+        B.close()
+    assert rel(zs[0], zs[1]) < 1e-13
+    h = mo.setup(A, mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    assert rel(zs[0], h.apply(r)) < 1e-10
