@@ -395,7 +395,7 @@ def main():
         names = ('csr_kernel<*,RESID,0>', 'csr_kernel<*,BJAC/JACOBI,0>')
     elif post_mode == 'k':
         names = ('%s<RESID,...,0>' % rk,
-                 '%s<KPOST,...,0>' % ('sell2_kernel' if (fmt0.get('post_sell') or world > 1) else 'bsr2_kernel'))
+                 'msell_kernel<2,5,KPOST,...,0>' if (fmt0.get('post_sell') or world > 1) else 'bsr2_kernel<KPOST,...,0>')
     else:
         names = ('%s<RESID,...,0>' % rk,
                  'bsr2_post_kernel<8,...,0>' if fmt0.get('post_fused', True) else 'bsr2_kernel<*,BJAC,...,0>')

@@ -25,10 +25,12 @@ WRITE_SCALE = 1024
 
 
 def classify(name):
-    m = re.search(r'(hsell2_kernel|sell2_kernel|bsr2_kernel|bsr2_post_kernel)<([^>]*)>', name)
+    m = re.search(r'(hsell2_kernel|msell_kernel|sell2_kernel|bsr2_kernel|bsr2_post_kernel)<([^>]*)>', name)
     if not m:
         return None
     kind, targs = m.group(1), [t.strip() for t in m.group(2).split(',')]
+    if kind == 'msell_kernel':          # <LPR, U, EPI, XFM, SYM, SPL, TAG, PROBE>: the level-0 K operator
+        return 'L0_smooth_spmv' if targs[2] == '5' and targs[6] == '0' else None
     if kind == 'bsr2_post_kernel':
         return 'L0_smooth_spmv' if targs[-1] == '0' else None
     epi, xfm = (targs[0], targs[1]) if kind in ('sell2_kernel', 'hsell2_kernel') else (targs[1], targs[2])
