@@ -92,9 +92,11 @@ def _stream_ptr(stream):
 
 
 def gpu_setup_supported(p) -> bool:
-    """The GPU setup (mamg_setup_gpu) covers the nodal 2-field profile."""
-    return p.num_functions == 2 and p.node_block_smoother != 0 and \
-        (p.AMG_type == 1 or p.sa_block_diag != 0)
+    """The GPU setup (mamg_setup_gpu) covers num_functions 1 and 2: node-block,
+    general seed-block, overlapping-ring (SCHWARZ_ADDITIVE) and point smoothers,
+    nodal or point SA (csrc/gsetup.hip).  What it still refuses at run time
+    (MAMG_ERR_UNSUPPORTED) 'auto' hands to the host setup."""
+    return p.num_functions in (1, 2)
 
 
 def _device_csr(A):

@@ -363,7 +363,7 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     const std::string et = e ? e : "";
     const int mode = et == "full" ? 1 : et == "rows" ? 2 : 0;
     if (rc) {
-    } else if (mode == 1) {
+    } else if (mode == 1 || G.generic) {   // generic smoothers: the host plan of the whole hierarchy
       rc = mamg::ghier_download(G, v, &H, &err);
     } else {
       rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, P.post_fusion != 0, &H,

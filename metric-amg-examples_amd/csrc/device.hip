@@ -1912,6 +1912,24 @@ int upload_csr(DeviceHandle* h, const CsrView& M, DCsr* D, int lanes, std::strin
   return MAMG_OK;
 }
 
+// a device CSR (GPU setup output) copied into the handle's memory
+int adopt_csr(DeviceHandle* h, const DevMat& M, DCsr* D, int lanes, std::string* err) {
+  D->n = M.n;
+  D->m = M.m;
+  D->nnz = M.nnz;
+  D->lanes = lanes > 0 ? lanes : pick_lanes(M.n, D->nnz);
+  int rc;
+  if ((rc = dalloc(h, &D->ptr, M.n + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nnz, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nnz, 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->ptr, M.ptr, (M.n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  if (D->nnz) {
+    HIPCHK(hipMemcpy(D->col, M.col, D->nnz * sizeof(int32_t), hipMemcpyDeviceToDevice));
+    HIPCHK(hipMemcpy(D->val, M.val, D->nnz * sizeof(double), hipMemcpyDeviceToDevice));
+  }
+  return MAMG_OK;
+}
+
 // lanes per node row for 2x2 blocks: ~2 blocks per lane (VL = 8 for the
 // ~15-block level-0 rows: 1.87 ms vs 2.00 ms at VL = 4, bench/spmv_micro.hip)
 int pick_lanes_bsr(int64_t nr, int64_t nb) {
@@ -4047,7 +4065,14 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   HIPCHK(hipSetDevice(p.device));
   HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
   read_knobs();
-  h->bsr = true;
+  h->bsr = !G->generic;   // a general block or point smoother: the CSR layout (as dev_upload)
+  if ((gs_smoother(p) || patch_schwarz(p)) && !h->bsr) {
+    *err = patch_schwarz(p) ? "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on "
+                              "every level)"
+                            : "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned "
+                              "smoother blocks)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   const int nl = (int)G->levels.size();
   h->L.resize(nl);
   int rc;
@@ -4056,7 +4081,36 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
     DLevel& D = h->L[l];
     D.n = g.n;
     D.coarsest = g.coarsest;
-    if (l == 0 && D.coarsest) {          // single-level hierarchy: CSR A0 + dense inverse
+    if (!h->bsr) {                       // CSR layout from the device CSRs (dev_upload's CSR branch)
+      if ((rc = adopt_csr(h.get(), l == 0 ? A0 : g.A, &D.A, l == 0 ? p.spmv_lanes : 0, err))) return rc;
+      if (D.coarsest) {
+        if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
+        HIPCHK(hipMemcpy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double), hipMemcpyDeviceToDevice));
+      } else {
+        if ((rc = adopt_csr(h.get(), g.P, &D.P, 0, err))) return rc;
+        if ((rc = adopt_csr(h.get(), g.R, &D.R, 0, err))) return rc;
+        if (g.WB.n > 0) {
+          if ((rc = adopt_csr(h.get(), g.WB, &D.WB, 0, err))) return rc;
+        } else {
+          if ((rc = dalloc(h.get(), &D.winv, D.n, err))) return rc;
+          HIPCHK(hipMemcpy(D.winv, g.winv, D.n * sizeof(double), hipMemcpyDeviceToDevice));
+        }
+        if (p.smoother == MAMG_SMOOTHER_POLY) {   // step smoothers w_k W (values only)
+          std::vector<double*> wk;
+          const bool blk = g.WB.n > 0;
+          if ((rc = poly_scaled(h.get(), blk ? D.WB.val : D.winv, blk ? D.WB.nnz : D.n, &wk, err))) return rc;
+          for (double* q : wk) {
+            if (blk) {
+              DCsr c = D.WB;
+              c.val = q;
+              D.WBk.push_back(c);
+            } else {
+              D.winvk.push_back(q);
+            }
+          }
+        }
+      }
+    } else if (l == 0 && D.coarsest) {          // single-level hierarchy: CSR A0 + dense inverse
       if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double), hipMemcpyDeviceToDevice));
       D.A.n = A0.n; D.A.m = A0.m; D.A.nnz = A0.nnz;
@@ -4080,13 +4134,13 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
     // Galerkin product only, which is done)
     for (void* q : {(void*)g.P.ptr, (void*)g.P.col, (void*)g.P.val, (void*)g.R.ptr, (void*)g.R.col,
                     (void*)g.R.val, (void*)g.AP.ptr, (void*)g.AP.col, (void*)g.AP.val, (void*)g.W,
-                    (void*)g.Ainv})
+                    (void*)g.Ainv, (void*)g.WB.ptr, (void*)g.WB.col, (void*)g.WB.val, (void*)g.winv})
       if (q) G->release(q);
     if (l > 0)
       for (void* q : {(void*)g.A.ptr, (void*)g.A.col, (void*)g.A.val})
         if (q) G->release(q);
-    g.P = g.R = g.AP = DevMat();
-    g.W = g.Ainv = nullptr;
+    g.P = g.R = g.AP = g.WB = DevMat();
+    g.W = g.Ainv = g.winv = nullptr;
     if (l > 0) g.A = DevMat();
     double** vecs[] = {&D.b, &D.x, &D.t, &D.t2, &D.r, &D.c, &D.e};
     for (double** v : vecs)

@@ -31,9 +31,10 @@ int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std
   return MAMG_OK;
 }
 
-// stable LSD radix sort of (key, value) pairs on the low key_bits of the key
-int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, int64_t* vout,
-                        int64_t n, int key_bits, void* stream, std::string* err) {
+namespace {
+template <class K>
+int sort_pairs(const K* kin, K* kout, const int64_t* vin, int64_t* vout, int64_t n, int key_bits,
+               void* stream, std::string* err) {
   if (n <= 0) return MAMG_OK;
   hipStream_t s = (hipStream_t)stream;
   size_t bytes = 0;
@@ -47,6 +48,19 @@ int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, i
   if (e != hipSuccess) return hip_fail(e, "DeviceRadixSort::SortPairs", err);
   if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync(sort)", err);
   return MAMG_OK;
+}
+}  // namespace
+
+// the same for 64-bit keys (composite (row, column) keys of the GPU setup)
+int dsort_pairs_u64_i64(const uint64_t* kin, uint64_t* kout, const int64_t* vin, int64_t* vout,
+                        int64_t n, int key_bits, void* stream, std::string* err) {
+  return sort_pairs(kin, kout, vin, vout, n, key_bits, stream, err);
+}
+
+// stable LSD radix sort of (key, value) pairs on the low key_bits of the key
+int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, int64_t* vout,
+                        int64_t n, int key_bits, void* stream, std::string* err) {
+  return sort_pairs(kin, kout, vin, vout, n, key_bits, stream, err);
 }
 
 }  // namespace mamg

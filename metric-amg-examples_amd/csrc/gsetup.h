@@ -18,14 +18,19 @@ struct DevMat {
   double* val = nullptr;
 };
 
-// one level of the nodal (num_functions == 2) SA hierarchy on the device;
-// every field-major CSR follows the host setup's definition bit for bit
+// one level of the SA hierarchy on the device (num_functions 1 or 2); every
+// field-major CSR follows the host setup's definition bit for bit.  The
+// smoother is exactly one of: W (2x2 node blocks), WB (general block CSR:
+// seed blocks that are not node-aligned, or overlapping seed rings), winv
+// (point smoother, one weight per dof)
 struct GLevel {
-  int64_t n = 0;              // dofs (2 nv)
+  int64_t n = 0;              // dofs (nf nv)
   bool coarsest = false;
   DevMat A;                   // level 0: the caller's matrix (not owned)
   DevMat P, R, AP;            // prolongation, restriction = P^T, A P
   double* W = nullptr;        // 2x2 smoother block per node, node-major (4 nv)
+  DevMat WB;                  // general block smoother (host HostLevel::WB)
+  double* winv = nullptr;     // point smoother weights (host HostLevel::winv)
   uint8_t* joined = nullptr;  // level 0: 1 if node I's two dofs form one seed block
   double* Ainv = nullptr;     // coarsest: dense inverse, n x n row-major, dof order
   int64_t* agg = nullptr;     // aggregate of each node (-1 isolated)
@@ -36,6 +41,7 @@ struct GLevel {
 struct GHier {
   mamg_params params;
   int device = 0;
+  bool generic = false;       // some level's smoother is WB or winv: CSR apply layout
   std::vector<GLevel> levels;
   std::vector<void*> allocs;  // every device buffer above (owned)
   double phase_ms[8] = {};    // setup phase timings (see gsetup.hip)
@@ -69,6 +75,8 @@ enum { GS_AGGREGATE = 0, GS_SMOOTHER = 1, GS_PROLONG = 2, GS_GALERKIN = 3, GS_CO
 // device primitives (dprims.hip)
 int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std::string* err);
 int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, int64_t* vout,
+                        int64_t n, int key_bits, void* stream, std::string* err);
+int dsort_pairs_u64_i64(const uint64_t* kin, uint64_t* kout, const int64_t* vin, int64_t* vout,
                         int64_t n, int key_bits, void* stream, std::string* err);
 
 }  // namespace mamg

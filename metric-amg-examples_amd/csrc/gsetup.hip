@@ -507,24 +507,6 @@ __global__ __launch_bounds__(256) void best_seed_kernel(int64_t n, const int64_t
   best[j] = bs;
 }
 
-// seed blocks are node-aligned iff every joiner joins its own node's other
-// dof; joined[I]: dofs I and nv + I form one block (needs Schwarz_mmsize >= 2)
-__global__ __launch_bounds__(256) void seed_align_kernel(int64_t nv, const uint8_t* __restrict__ isseed,
-                                                         const int64_t* __restrict__ best, int mmsize,
-                                                         uint8_t* __restrict__ joined, int* bad) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (I >= nv) return;
-  bool j = false;
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int64_t d = f * nv + I, partner = (1 - f) * nv + I;
-    if (isseed[d] || best[d] < 0) continue;
-    if (best[d] != partner) { atomicAdd(bad, 1); continue; }
-    j = j || mmsize >= 2;
-  }
-  joined[I] = j;
-}
-
 // 2x2 node-block inverse by Gauss-Jordan without pivoting (setup.cpp
 // gauss_jordan on the block [[a00 a01] [a10 a11]]); a block split into two
 // singletons (joined == 0) has its coupling entries set to 0, which gives the
@@ -902,6 +884,533 @@ __global__ __launch_bounds__(256) void gj_extract_kernel(int64_t n, const double
   inv[t] = M[i * 2 * n + n + j];
 }
 
+// ---------------------------------------------------------------------------
+// point quantities (setup.cpp diag_of, abs_rowsum, rho_estimate, winv) and
+// the point SA prolongator (smooth_prolongator + smooth_merge)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void point_diag_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val, double* __restrict__ dg,
+                                                         double* __restrict__ dinv, double* __restrict__ rs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = dfind(ptr, col, i, i);
+  const double d = p >= 0 ? val[p] : 0.0;
+  dg[i] = d;
+  dinv[i] = 1.0 / d;
+  double s = 0.0;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) s += fabs(val[k]) * 1.0;
+  rs[i] = s;
+}
+
+// y_i = scale_i * sum_k a_ik x_k (sum in CSR order from 0.0; scale == nullptr: 1)
+__global__ __launch_bounds__(256) void row_spmv_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const double* __restrict__ scale,
+                                                       const double* __restrict__ x, double* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) s += val[k] * x[col[k]];
+  y[i] = scale ? scale[i] * s : s;
+}
+
+// power-iteration start vector (setup.cpp rho_estimate / overlap_smoother)
+__global__ __launch_bounds__(256) void hash_vec_kernel(int64_t n, double* __restrict__ v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = ((double)dhash32((uint64_t)i, 977) / 4294967296.0) * 2.0 - 1.0;
+}
+
+// bits[0] = max |v_i|, bits[1] = max |w_i| (non-negative doubles order as
+// their bit patterns, so the atomic max is exact in any order)
+__global__ __launch_bounds__(256) void maxabs2_kernel(int64_t n, const double* __restrict__ v,
+                                                      const double* __restrict__ w, unsigned long long* bits) {
+  double a = 0.0, b = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    a = fmax(a, fabs(v[i]));
+    b = fmax(b, fabs(w[i]));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a = fmax(a, __shfl_xor(a, o));
+    b = fmax(b, __shfl_xor(b, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(bits, (unsigned long long)__double_as_longlong(a));
+    atomicMax(bits + 1, (unsigned long long)__double_as_longlong(b));
+  }
+}
+
+// v = w / max|w| (the power iteration's normalisation)
+__global__ __launch_bounds__(256) void vnorm_kernel(int64_t n, const double* __restrict__ w,
+                                                    const unsigned long long* __restrict__ bits,
+                                                    double* __restrict__ v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = w[i] / __longlong_as_double((long long)bits[1]);
+}
+
+// max_i a_i b_i from -inf (Gershgorin bound; the products may be negative),
+// one workgroup: fmax is exact and order-free for non-NaN values, and skips
+// NaN as std::max(r, NaN) keeps r
+__global__ __launch_bounds__(1024) void maxprod_kernel(int64_t n, const double* __restrict__ a,
+                                                       const double* __restrict__ b, double* out) {
+  __shared__ double red[16];
+  double m = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) m = fmax(m, a[i] * b[i]);
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int t = 1; t < 16; ++t) m = fmax(m, red[t]);
+    *out = m;
+  }
+}
+
+// point smoother weights: relaxation / d, d = a_ii (JACOBI), sum |a_ij|
+// (L1DIAG) or a_ii rho (JACOBI_RHO, POLY)
+__global__ __launch_bounds__(256) void winv_kernel(int64_t n, int kind, double relax, double rho,
+                                                   const double* __restrict__ dg, const double* __restrict__ rs,
+                                                   double* __restrict__ winv) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double d = kind == 0 ? dg[i] : kind == 1 ? rs[i] : dg[i] * rho;
+  winv[i] = relax / d;
+}
+
+// point SA: P_i = T_i - (w dinv_i) (A T)_i, merged as setup.cpp smooth_merge
+// (T row i: column f nagg + agg(I) when aggregated)
+template <bool FILL>
+__global__ __launch_bounds__(256) void smooth_pt_kernel(int64_t n, int64_t nv, const int64_t* __restrict__ agg,
+                                                        int64_t nagg, double w, const double* __restrict__ dinv,
+                                                        const int64_t* __restrict__ aptr,
+                                                        const int32_t* __restrict__ acol,
+                                                        const double* __restrict__ aval, int64_t* pptr,
+                                                        int32_t* __restrict__ pcol, double* __restrict__ pval) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t I = i % nv, f = i / nv;
+  const bool ht = agg[I] >= 0;
+  const int32_t tc = ht ? (int32_t)(f * nagg + agg[I]) : -1;
+  bool tdone = !ht;
+  const double ci = w * dinv[i];
+  int64_t o = FILL ? pptr[i] : 0;
+  for (int64_t k = aptr[i]; k < aptr[i + 1]; ++k) {
+    const int32_t j = acol[k];
+    const double x = ci * aval[k];
+    if (!tdone && tc < j) {
+      if (FILL) { pcol[o] = tc; pval[o] = 1.0; }
+      ++o;
+      tdone = true;
+    }
+    double r;
+    if (x == 0.0) {
+      if (!tdone && tc == j) { r = 1.0; tdone = true; } else continue;
+    } else if (!tdone && tc == j) {
+      r = 1.0 - x; tdone = true;
+    } else {
+      r = 0.0 - x;
+    }
+    if (r != 0.0) {
+      if (FILL) { pcol[o] = j; pval[o] = r; }
+      ++o;
+    }
+  }
+  if (!tdone) {
+    if (FILL) { pcol[o] = tc; pval[o] = 1.0; }
+    ++o;
+  }
+  if (!FILL) pptr[i + 1] = o;
+}
+
+// ---------------------------------------------------------------------------
+// general seed blocks (setup.cpp block_smoother / block_inverse / block_rho)
+// ---------------------------------------------------------------------------
+// sort key of every dof: its strongest seed, or n (no seed neighbour)
+__global__ __launch_bounds__(256) void best_key_kernel(int64_t n, const int64_t* __restrict__ best,
+                                                       int32_t* __restrict__ key, int64_t* __restrict__ idx) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  key[j] = best[j] >= 0 ? (int32_t)best[j] : (int32_t)n;
+  idx[j] = j;
+}
+
+// joiners sorted by (seed, index): the first mmsize - 1 of each seed join it
+// (setup.cpp: ascending j, cnt[s] < mmsize - 1), the others stay alone
+__global__ __launch_bounds__(256) void owner_kernel(int64_t n, const int32_t* __restrict__ skey,
+                                                    const int64_t* __restrict__ sidx, int mmsize,
+                                                    int64_t* __restrict__ owner, uint8_t* __restrict__ isowner) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const int32_t s = skey[q];
+  const int64_t j = sidx[q];
+  int64_t o = j;
+  if (s < n) {
+    int64_t lo = 0, hi = q;          // first position of key s
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (skey[mid] < s) lo = mid + 1; else hi = mid;
+    }
+    if (q - lo < (int64_t)mmsize - 1) o = s;
+  }
+  owner[j] = o;
+  isowner[o] = 1;                    // benign race: every writer stores 1
+}
+
+__global__ __launch_bounds__(256) void u8_to_i64_kernel(int64_t n, const uint8_t* __restrict__ a,
+                                                        int64_t* __restrict__ b) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+// block id = rank of the owner among the owners (ascending index)
+__global__ __launch_bounds__(256) void bid_kernel(int64_t n, const int64_t* __restrict__ owner,
+                                                  const int64_t* __restrict__ oscan, int64_t* __restrict__ bid,
+                                                  int32_t* __restrict__ bkey, int64_t* __restrict__ idx,
+                                                  unsigned long long* __restrict__ bcnt) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int64_t b = oscan[owner[j]] - 1;
+  bid[j] = b;
+  bkey[j] = (int32_t)b;
+  idx[j] = j;
+  atomicAdd(bcnt + b + 1, 1ull);
+}
+
+// the blocks are node-aligned (convert.cpp node_blocks_of holds for the
+// block CSR) iff every block is one dof or the two dofs of one node
+__global__ __launch_bounds__(256) void align_kernel(int64_t nv, const int64_t* __restrict__ bid,
+                                                    const int64_t* __restrict__ bptr,
+                                                    uint8_t* __restrict__ joined, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  const int64_t b0 = bid[I], b1 = bid[nv + I];
+  const int64_t s0 = bptr[b0 + 1] - bptr[b0], s1 = bptr[b1 + 1] - bptr[b1];
+  const bool j = b0 == b1;
+  if (s0 > 2 || s1 > 2 || (s0 == 2 && !j) || (s1 == 2 && !j)) atomicAdd(bad, 1);
+  joined[I] = j;
+}
+
+// member position inside its block, and the block CSR's row lengths
+__global__ __launch_bounds__(256) void member_pos_kernel(int64_t n, const int64_t* __restrict__ mem,
+                                                         const int64_t* __restrict__ bid,
+                                                         const int64_t* __restrict__ bptr, int64_t* __restrict__ pos,
+                                                         int64_t* __restrict__ dptr) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const int64_t j = mem[q], b = bid[j];
+  pos[j] = q - bptr[b];
+  dptr[j + 1] = bptr[b + 1] - bptr[b];
+}
+
+// Gauss-Jordan without pivoting (setup.cpp gauss_jordan) of the s x 2s matrix
+// M (row-major, [A | I]) by one workgroup of one wave; F = s multipliers.
+// Every element sees the host's operations in the host's order (row k scaled,
+// then M_ij -= f_i M_kj with f read after the scaling), so the bits agree.
+__device__ bool wave_gauss_jordan(double* M, double* F, int64_t s) {
+  const int64_t w = 2 * s;
+  const int lane = threadIdx.x;
+  for (int64_t k = 0; k < s; ++k) {
+    const double p = M[k * w + k];
+    __syncthreads();
+    if (!(p > 0.0)) return false;
+    for (int64_t j = lane; j < w; j += 64) M[k * w + j] = M[k * w + j] / p;
+    __syncthreads();
+    for (int64_t i = lane; i < s; i += 64) F[i] = i == k ? 0.0 : M[i * w + k];
+    __syncthreads();
+    for (int64_t t = lane; t < s * w; t += 64) {
+      const int64_t i = t / w, j = t - i * w;
+      if (i != k) M[i * w + j] = M[i * w + j] - F[i] * M[k * w + j];
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+// one-dof blocks: inverse 1 / a_ii (Gauss-Jordan on a 1 x 1 block)
+__global__ __launch_bounds__(256) void blk_single_kernel(int64_t nb, const int64_t* __restrict__ bptr,
+                                                         const int64_t* __restrict__ mem,
+                                                         const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const double* __restrict__ val,
+                                                         const int64_t* __restrict__ dptr,
+                                                         int32_t* __restrict__ dcol, double* __restrict__ dval,
+                                                         int* bad) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb || bptr[b + 1] - bptr[b] != 1) return;
+  const int64_t i = mem[bptr[b]];
+  const int64_t q = dfind(ptr, col, i, i);
+  const double p = q >= 0 ? val[q] : 0.0;
+  if (!(p > 0.0)) atomicAdd(bad, 1);
+  dcol[dptr[i]] = (int32_t)i;
+  dval[dptr[i]] = 1.0 / p;
+}
+
+__global__ __launch_bounds__(256) void multi_flag_kernel(int64_t nb, const int64_t* __restrict__ bptr,
+                                                         int64_t* __restrict__ f) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b < nb) f[b] = bptr[b + 1] - bptr[b] >= 2;
+}
+
+// list of the blocks of >= 2 dofs and their Gauss-Jordan scratch (2 s^2 + s)
+__global__ __launch_bounds__(256) void multi_list_kernel(int64_t nb, const int64_t* __restrict__ bptr,
+                                                         const int64_t* __restrict__ fscan,
+                                                         int64_t* __restrict__ list, int64_t* __restrict__ gj) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb) return;
+  const int64_t s = bptr[b + 1] - bptr[b];
+  if (s < 2) return;
+  const int64_t q = fscan[b] - 1;
+  list[q] = b;
+  gj[q] = 2 * s * s + s;
+}
+
+// blocks of >= 2 dofs, one wave each: dense block from A's rows (entries
+// whose column lies in the block), Gauss-Jordan in scratch, rows of D_B^-1
+__global__ __launch_bounds__(64) void blk_multi_kernel(const int64_t* __restrict__ list, int64_t nlist,
+                                                       const int64_t* __restrict__ moff,
+                                                       const int64_t* __restrict__ bptr,
+                                                       const int64_t* __restrict__ mem,
+                                                       const int64_t* __restrict__ bid,
+                                                       const int64_t* __restrict__ pos,
+                                                       const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val, double* scratch,
+                                                       const int64_t* __restrict__ dptr, int32_t* __restrict__ dcol,
+                                                       double* __restrict__ dval, int* bad) {
+  const int64_t t0 = blockIdx.x;
+  if (t0 >= nlist) return;
+  const int64_t b = list[t0], s = bptr[b + 1] - bptr[b], w = 2 * s;
+  const int64_t* m = mem + bptr[b];
+  double* M = scratch + (t0 ? moff[t0 - 1] : 0);
+  double* F = M + s * w;
+  const int lane = threadIdx.x;
+  for (int64_t t = lane; t < s * w; t += 64) M[t] = 0.0;
+  __syncthreads();
+  for (int64_t a = lane; a < s; a += 64) {
+    const int64_t i = m[a];
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+      if (bid[col[k]] == b) M[a * w + pos[col[k]]] = val[k];
+    M[a * w + s + a] = 1.0;
+  }
+  __syncthreads();
+  if (!wave_gauss_jordan(M, F, s)) {
+    if (lane == 0) atomicAdd(bad, 1);
+    return;
+  }
+  for (int64_t t = lane; t < s * s; t += 64) {
+    const int64_t a = t / s, c = t - a * s, i = m[a];
+    dcol[dptr[i] + c] = (int32_t)m[c];
+    dval[dptr[i] + c] = M[a * w + s + c];
+  }
+}
+
+// max_i sum_j |C_ij| over a CSR with sorted columns and no exact zeros
+__global__ __launch_bounds__(256) void rowabs_max_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const double* __restrict__ val, unsigned long long* bits) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+  if (i < n)
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+      if (val[k] != 0.0) s += fabs(val[k]) * 1.0;
+  for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(bits, (unsigned long long)__double_as_longlong(s));
+}
+
+__global__ __launch_bounds__(256) void scale_vals_kernel(int64_t n, double sc, double* __restrict__ v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = sc * v[i];
+}
+
+// ---------------------------------------------------------------------------
+// additive Schwarz on the seeds' overlapping rings (setup.cpp overlap_smoother)
+// ---------------------------------------------------------------------------
+// breadth-first ring of one seed, one wave: the visit order of the host's
+// loop (neighbours in CSR order, at most mmsize dofs, depth <= maxlvl), the
+// membership test spread over the lanes; then the members sorted
+__global__ __launch_bounds__(64) void ring_bfs_kernel(int64_t ns, const int32_t* __restrict__ seeds,
+                                                      const int64_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ col, int maxlvl, int mm,
+                                                      int32_t* __restrict__ blk, int64_t* __restrict__ blen) {
+  extern __shared__ int32_t sh[];
+  int32_t* order = sh;
+  int32_t* depth = sh + mm;
+  const int64_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (k >= ns) return;
+  if (lane == 0) { order[0] = seeds[k]; depth[0] = 0; }
+  __syncthreads();
+  int size = 1, head = 0;
+  while (head < size && size < mm) {
+    const int32_t v = order[head];
+    const int dv = depth[head];
+    ++head;
+    if (dv == maxlvl) continue;
+    bool full = false;
+    for (int64_t q = ptr[v]; q < ptr[v + 1] && !full; ++q) {
+      const int32_t j = col[q];
+      bool hit = false;
+      for (int t = lane; t < size; t += 64) hit |= order[t] == j;
+      if (__any(hit)) continue;
+      if (lane == 0) { order[size] = j; depth[size] = dv + 1; }
+      ++size;
+      __syncthreads();
+      full = size >= mm;
+    }
+  }
+  __syncthreads();
+  for (int e = lane; e < size; e += 64) {
+    const int32_t key = order[e];
+    int rank = 0;
+    for (int t = 0; t < size; ++t) rank += order[t] < key;
+    blk[k * mm + rank] = key;
+  }
+  if (lane == 0) blen[k] = size;
+}
+
+__global__ __launch_bounds__(256) void sq_len_kernel(int64_t ns, const int64_t* __restrict__ blen,
+                                                     int64_t* __restrict__ sq, int64_t* __restrict__ gj) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= ns) return;
+  const int64_t m = blen[k];
+  sq[k] = m * m;
+  gj[k] = 2 * m * m + m;
+}
+
+// dense ring block from A (binary searches), its inverse into inv (row-major
+// at the block's contribution offset), and the covered flags
+__global__ __launch_bounds__(64) void ring_inv_kernel(int64_t ns, int mm, const int32_t* __restrict__ blk,
+                                                      const int64_t* __restrict__ blen,
+                                                      const int64_t* __restrict__ sqscan,
+                                                      const int64_t* __restrict__ gjscan,
+                                                      const int64_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ col,
+                                                      const double* __restrict__ val, double* scratch,
+                                                      double* __restrict__ inv, uint8_t* __restrict__ cov, int* bad) {
+  const int64_t k = blockIdx.x;
+  if (k >= ns) return;
+  const int64_t s = blen[k], w = 2 * s;
+  const int32_t* b = blk + k * mm;
+  double* M = scratch + (k ? gjscan[k - 1] : 0);
+  double* F = M + s * w;
+  double* out = inv + (k ? sqscan[k - 1] : 0);
+  const int lane = threadIdx.x;
+  for (int64_t t = lane; t < s * w; t += 64) {
+    const int64_t a = t / w, c = t - a * w;
+    double x = 0.0;
+    if (c < s) {
+      const int64_t q = dfind(ptr, col, b[a], b[c]);
+      if (q >= 0) x = val[q];
+    } else if (c - s == a) {
+      x = 1.0;
+    }
+    M[t] = x;
+  }
+  for (int64_t a = lane; a < s; a += 64) cov[b[a]] = 1;
+  __syncthreads();
+  if (!wave_gauss_jordan(M, F, s)) {
+    if (lane == 0) atomicAdd(bad, 1);
+    return;
+  }
+  for (int64_t t = lane; t < s * s; t += 64) {
+    const int64_t a = t / s, c = t - a * s;
+    out[t] = M[a * w + s + c];
+  }
+}
+
+// (row, column) keys of every block contribution, in block order, then one
+// diagonal key per uncovered dof (source -1 - i: 1 / a_ii)
+__global__ __launch_bounds__(64) void ring_keys_kernel(int64_t ns, int mm, int64_t n, const int32_t* __restrict__ blk,
+                                                       const int64_t* __restrict__ blen,
+                                                       const int64_t* __restrict__ sqscan, uint64_t* __restrict__ key,
+                                                       int64_t* __restrict__ src) {
+  const int64_t k = blockIdx.x;
+  if (k >= ns) return;
+  const int64_t s = blen[k], o = k ? sqscan[k - 1] : 0;
+  const int32_t* b = blk + k * mm;
+  for (int64_t t = threadIdx.x; t < s * s; t += 64) {
+    const int64_t a = t / s, c = t - a * s;
+    key[o + t] = (uint64_t)b[a] * (uint64_t)n + (uint64_t)b[c];
+    src[o + t] = o + t;
+  }
+}
+
+__global__ __launch_bounds__(256) void uncov_keys_kernel(int64_t n, const uint8_t* __restrict__ cov,
+                                                         const int64_t* __restrict__ uscan, int64_t base,
+                                                         uint64_t* __restrict__ key, int64_t* __restrict__ src) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || cov[i]) return;
+  const int64_t q = base + uscan[i] - 1;
+  key[q] = (uint64_t)i * (uint64_t)n + (uint64_t)i;
+  src[q] = -1 - i;
+}
+
+__global__ __launch_bounds__(256) void uncov_flag_kernel(int64_t n, const uint8_t* __restrict__ cov,
+                                                         int64_t* __restrict__ f) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) f[i] = cov[i] ? 0 : 1;
+}
+
+__global__ __launch_bounds__(256) void run_flag_kernel(int64_t e, const uint64_t* __restrict__ key,
+                                                       int64_t* __restrict__ f) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < e) f[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
+}
+
+// run starts, column indices and row counts of the merged pattern
+__global__ __launch_bounds__(256) void run_start_kernel(int64_t e, int64_t n, const uint64_t* __restrict__ key,
+                                                        const int64_t* __restrict__ fscan,
+                                                        int64_t* __restrict__ ustart, int32_t* __restrict__ wcol,
+                                                        unsigned long long* __restrict__ wcnt) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= e || !(t == 0 || key[t] != key[t - 1])) return;
+  const int64_t u = fscan[t] - 1;
+  ustart[u] = t;
+  wcol[u] = (int32_t)(key[t] % (uint64_t)n);
+  atomicAdd(wcnt + key[t] / (uint64_t)n + 1, 1ull);
+}
+
+// each merged entry sums its run in block order from 0.0 (setup.cpp: W_ij +=
+// inv in seed order), or is 1 / a_ii for an uncovered dof
+__global__ __launch_bounds__(256) void run_sum_kernel(int64_t nu, int64_t e, const int64_t* __restrict__ ustart,
+                                                      const int64_t* __restrict__ src, const double* __restrict__ inv,
+                                                      const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                      const double* __restrict__ val, double* __restrict__ wval) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= nu) return;
+  const int64_t t1 = u + 1 < nu ? ustart[u + 1] : e;
+  double s = 0.0;
+  for (int64_t t = ustart[u]; t < t1; ++t) {
+    const int64_t q = src[t];
+    if (q >= 0) {
+      s += inv[q];
+    } else {
+      const int64_t i = -1 - q, p = dfind(ptr, col, i, i);
+      s = 1.0 / (p >= 0 ? val[p] : 0.0);
+    }
+  }
+  wval[u] = s;
+}
+
+// 2x2 node blocks as the host's block CSR (ghier_download's rule: rows
+// {I, nv + I}, or the diagonal alone where seed blocks split the node)
+__global__ __launch_bounds__(256) void node_wb_kernel(int64_t nv, const dv4_t* __restrict__ W,
+                                                      const uint8_t* __restrict__ joined, int64_t* __restrict__ ptr,
+                                                      int32_t* __restrict__ col, double* __restrict__ val, int fill) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * nv) return;
+  const int64_t I = i % nv, f = i / nv;
+  const bool jn = joined ? joined[I] != 0 : true;
+  if (!fill) { ptr[i + 1] = jn ? 2 : 1; return; }
+  const dv4_t w = W[I];
+  const int64_t o = ptr[i];
+  if (jn) {
+    col[o] = (int32_t)I; val[o] = f ? w.z : w.x;
+    col[o + 1] = (int32_t)(nv + I); val[o + 1] = f ? w.w : w.y;
+  } else {
+    col[o] = (int32_t)i; val[o] = f ? w.w : w.x;
+  }
+}
+
 // input check (setup.cpp host_setup): monotone row pointers, columns in
 // range and strictly increasing within each row
 __global__ __launch_bounds__(256) void validate_kernel(int64_t n, int64_t m, const int64_t* __restrict__ ptr,
@@ -1192,21 +1701,26 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
   return MAMG_OK;
 }
 
-// aggregation of the node graph of A (setup.cpp node_graph + strength + aggregate_mis2)
-int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, int64_t** agg_out,
+// aggregation of the node graph of A (setup.cpp node_graph + strength +
+// aggregate_mis2 / aggregate_hem); scalar: of A itself (num_functions 1)
+int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bool scalar, int64_t** agg_out,
               int64_t* nagg_out, std::string* err) {
   Scratch S;
   DevMat Gr;
-  Gr.n = Gr.m = nv;
-  RCHK(S.alloc(&Gr.ptr, nv + 1, err));
-  HIPCHK(hipMemset(Gr.ptr, 0, sizeof(int64_t)));
-  node_graph_kernel<false><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
-  HIPCHK(hipGetLastError());
-  RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
-  RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
-  RCHK(S.alloc(&Gr.col, Gr.nnz, err));
-  RCHK(S.alloc(&Gr.val, Gr.nnz, err));
-  node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+  if (scalar) {
+    Gr = A;
+  } else {
+    Gr.n = Gr.m = nv;
+    RCHK(S.alloc(&Gr.ptr, nv + 1, err));
+    HIPCHK(hipMemset(Gr.ptr, 0, sizeof(int64_t)));
+    node_graph_kernel<false><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
+    HIPCHK(hipGetLastError());
+    RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
+    RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
+    RCHK(S.alloc(&Gr.col, Gr.nnz, err));
+    RCHK(S.alloc(&Gr.val, Gr.nnz, err));
+    node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+  }
   double* d = nullptr;
   uint8_t *flag = nullptr, *nonisol = nullptr;
   int* ctr = nullptr;
@@ -1292,6 +1806,306 @@ int coarsest_inverse(GHier* G, const DevMat& A, double** inv_out, std::string* e
   return MAMG_OK;
 }
 
+int bits_for(int64_t v) {   // key bits covering 0..v
+  int b = 1;
+  while (b < 63 && (int64_t(1) << b) <= v) ++b;
+  return b;
+}
+
+// point quantities of one level (setup.cpp host_setup: dg, dinv, rs, rho)
+struct PointLevel {
+  double *dg = nullptr, *dinv = nullptr, *rs = nullptr;
+  double rho = 0.0;
+};
+
+// rho_estimate: Gershgorin bound (iters 0) or inf-norm power iterations of
+// D^-1 A; the maxima are exact, each row sums in CSR order
+int rho_estimate_dev(const DevMat& A, const PointLevel& P, int iters, Scratch* S, double* rho, std::string* err) {
+  const int64_t n = A.n;
+  if (iters == 0) {
+    double* m = nullptr;
+    RCHK(S->alloc(&m, 1, err));
+    maxprod_kernel<<<1, 1024>>>(n, P.dinv, P.rs, m);
+    HIPCHK(hipGetLastError());
+    return to_host(rho, m, 1, err);
+  }
+  double *v = nullptr, *w = nullptr;
+  unsigned long long* bits = nullptr;
+  RCHK(S->alloc(&v, n, err));
+  RCHK(S->alloc(&w, n, err));
+  RCHK(S->alloc(&bits, 2, err));
+  hash_vec_kernel<<<nblk(n), 256>>>(n, v);
+  const unsigned gm = (unsigned)std::min<int64_t>(nblk(n), 1024);
+  for (int it = 0; it < iters; ++it) {
+    row_spmv_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, P.dinv, v, w);
+    HIPCHK(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned long long), nullptr));
+    maxabs2_kernel<<<gm, 256>>>(n, v, w, bits);
+    vnorm_kernel<<<nblk(n), 256>>>(n, w, bits, v);
+  }
+  HIPCHK(hipGetLastError());
+  unsigned long long hb[2] = {0, 0};
+  RCHK(to_host(hb, bits, 2, err));
+  double mv, mw;
+  std::memcpy(&mv, &hb[0], sizeof(double));
+  std::memcpy(&mw, &hb[1], sizeof(double));
+  *rho = mw / mv;
+  return MAMG_OK;
+}
+
+int point_level(const DevMat& A, const mamg_params& p, bool need_rho, Scratch* S, PointLevel* P,
+                std::string* err) {
+  const int64_t n = A.n;
+  RCHK(S->alloc(&P->dg, n, err));
+  RCHK(S->alloc(&P->dinv, n, err));
+  RCHK(S->alloc(&P->rs, n, err));
+  point_diag_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, P->dg, P->dinv, P->rs);
+  HIPCHK(hipGetLastError());
+  P->rho = 0.0;
+  if (need_rho) RCHK(rho_estimate_dev(A, *P, p.rho_iters, S, &P->rho, err));
+  return MAMG_OK;
+}
+
+// seed blocks (setup.cpp block_smoother): every non-seed dof joins its
+// strongest seed neighbour, at most Schwarz_mmsize - 1 joiners per seed (the
+// lowest indices); blocks numbered by their owner's index.  bid: block of
+// every dof, bptr: block offsets of the members mem (ascending in a block)
+struct SeedBlocks {
+  int64_t *bid = nullptr, *bptr = nullptr, *mem = nullptr;
+  int64_t nb = 0;
+};
+
+int seed_blocks_dev(const DevMat& A, const int32_t* idofs, int64_t n_idofs, int mmsize, Scratch* S,
+                    SeedBlocks* B, std::string* err) {
+  const int64_t n = A.n;
+  int32_t* di = nullptr;
+  uint8_t *isseed = nullptr, *isowner = nullptr;
+  int64_t *best = nullptr, *idx = nullptr, *sidx = nullptr, *owner = nullptr, *oscan = nullptr;
+  int32_t *key = nullptr, *skey = nullptr;
+  int* bad = nullptr;
+  RCHK(S->alloc(&di, n_idofs, err));
+  RCHK(S->alloc(&isseed, n, err));
+  RCHK(S->alloc(&isowner, n, err));
+  RCHK(S->alloc(&best, n, err));
+  RCHK(S->alloc(&idx, n, err));
+  RCHK(S->alloc(&sidx, n, err));
+  RCHK(S->alloc(&owner, n, err));
+  RCHK(S->alloc(&oscan, n, err));
+  RCHK(S->alloc(&key, n, err));
+  RCHK(S->alloc(&skey, n, err));
+  RCHK(S->alloc(&bad, 1, err));
+  HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(isseed, 0, n));
+  HIPCHK(hipMemset(isowner, 0, n));
+  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
+  best_seed_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
+  best_key_kernel<<<nblk(n), 256>>>(n, best, key, idx);
+  HIPCHK(hipGetLastError());
+  int hb = 0;
+  RCHK(read_int(bad, &hb, err));
+  if (hb) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+  RCHK(dsort_pairs_i32_i64(key, skey, idx, sidx, n, bits_for(n), nullptr, err));
+  owner_kernel<<<nblk(n), 256>>>(n, skey, sidx, mmsize, owner, isowner);
+  u8_to_i64_kernel<<<nblk(n), 256>>>(n, isowner, oscan);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(oscan, oscan, n, nullptr, err));
+  RCHK(to_host(&B->nb, oscan + n - 1, 1, err));
+  RCHK(S->alloc(&B->bid, n, err));
+  RCHK(S->alloc(&B->bptr, B->nb + 1, err));
+  RCHK(S->alloc(&B->mem, n, err));
+  HIPCHK(hipMemset(B->bptr, 0, (B->nb + 1) * sizeof(int64_t)));
+  bid_kernel<<<nblk(n), 256>>>(n, owner, oscan, B->bid, key, idx, (unsigned long long*)B->bptr);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(B->bptr, B->bptr, B->nb + 1, nullptr, err));
+  return dsort_pairs_i32_i64(key, skey, idx, B->mem, n, bits_for(B->nb), nullptr, err);
+}
+
+// D = D_B^-1 as a block CSR (setup.cpp block_inverse: row i holds its
+// block's inverse row, columns = the block's members ascending)
+int block_inverse_dev(GHier* G, const DevMat& A, const SeedBlocks& B, Scratch* S, DevMat* D, std::string* err) {
+  const int64_t n = A.n, nb = B.nb;
+  int64_t *pos = nullptr, *f = nullptr;
+  int* bad = nullptr;
+  RCHK(S->alloc(&pos, n, err));
+  RCHK(S->alloc(&f, nb, err));
+  RCHK(S->alloc(&bad, 1, err));
+  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  D->n = D->m = n;
+  RCHK(galloc(G, &D->ptr, n + 1, err));
+  HIPCHK(hipMemset(D->ptr, 0, sizeof(int64_t)));
+  member_pos_kernel<<<nblk(n), 256>>>(n, B.mem, B.bid, B.bptr, pos, D->ptr);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(D->ptr, D->ptr, n + 1, nullptr, err));
+  RCHK(to_host(&D->nnz, D->ptr + n, 1, err));
+  RCHK(galloc(G, &D->col, D->nnz, err));
+  RCHK(galloc(G, &D->val, D->nnz, err));
+  blk_single_kernel<<<nblk(nb), 256>>>(nb, B.bptr, B.mem, A.ptr, A.col, A.val, D->ptr, D->col, D->val, bad);
+  multi_flag_kernel<<<nblk(nb), 256>>>(nb, B.bptr, f);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(f, f, nb, nullptr, err));
+  int64_t nm = 0;
+  RCHK(to_host(&nm, f + nb - 1, 1, err));
+  if (nm) {
+    int64_t *list = nullptr, *gj = nullptr;
+    RCHK(S->alloc(&list, nm, err));
+    RCHK(S->alloc(&gj, nm, err));
+    multi_list_kernel<<<nblk(nb), 256>>>(nb, B.bptr, f, list, gj);
+    HIPCHK(hipGetLastError());
+    RCHK(dscan_incl_i64(gj, gj, nm, nullptr, err));
+    int64_t tot = 0;
+    RCHK(to_host(&tot, gj + nm - 1, 1, err));
+    double* scratch = nullptr;
+    RCHK(S->alloc(&scratch, tot, err));
+    blk_multi_kernel<<<(unsigned)nm, 64>>>(list, nm, gj, B.bptr, B.mem, B.bid, pos, A.ptr, A.col, A.val, scratch,
+                                           D->ptr, D->col, D->val, bad);
+    HIPCHK(hipGetLastError());
+  }
+  int hb = 0;
+  RCHK(read_int(bad, &hb, err));
+  if (hb) { *err = "smoother block not SPD (non-positive pivot)"; return MAMG_ERR_SETUP; }
+  return MAMG_OK;
+}
+
+// rho_B = max_i sum_j |(D A)_ij| (setup.cpp block_rho: SMMP row of D A, sorted
+// columns, zeros skipped) through the hash SpGEMM
+int block_rho_dev(const DevMat& D, const DevMat& A, double* rho, std::string* err) {
+  GHier tmp;
+  DevMat C;
+  RCHK(spgemm(&tmp, D, BCsr{A.ptr, A.col, A.val}, A.m, &C, err, A.n ? (double)A.nnz / (double)A.n : 1.0));
+  Scratch S;
+  unsigned long long* bits = nullptr;
+  RCHK(S.alloc(&bits, 1, err));
+  HIPCHK(hipMemset(bits, 0, sizeof(unsigned long long)));
+  rowabs_max_kernel<<<nblk(C.n), 256>>>(C.n, C.ptr, C.val, bits);
+  HIPCHK(hipGetLastError());
+  unsigned long long h = 0;
+  RCHK(to_host(&h, bits, 1, err));
+  std::memcpy(rho, &h, sizeof(double));
+  return MAMG_OK;
+}
+
+// additive Schwarz on the seeds' overlapping rings (setup.cpp
+// overlap_smoother): the blocks' inverses summed in seed order into the
+// merged pattern (sorted (row, column) keys, stable, so each entry's run is in
+// seed order), 1 / a_ii on uncovered dofs, then W = (relaxation / lambda) S
+// with lambda from max(rho_iters, 30) power iterations of S A
+int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_t ns, const mamg_params& p,
+                         DevMat* W, std::string* err) {
+  const int64_t n = A.n;
+  const int maxlvl = p.Schwarz_maxlvl, mm = p.Schwarz_mmsize;
+  if (ns > std::max<int64_t>(n / 8, 1) || (double)ns * mm * mm > 4e9) {
+    *err = "SCHWARZ_ADDITIVE (dense overlapping seed blocks) is for sparse seed sets: " + std::to_string(ns) +
+           " seeds of up to " + std::to_string(mm) + " dofs";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  if (mm < 1 || mm > 8192) {
+    *err = "GPU setup: SCHWARZ_ADDITIVE with Schwarz_mmsize " + std::to_string(mm) +
+           " (1..8192 on the GPU); use the host setup (mamg_setup)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  for (int64_t k = 0; k < ns; ++k)
+    if (seeds[k] < 0 || seeds[k] >= n) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+  Scratch S;
+  int32_t *ds = nullptr, *blk = nullptr;
+  int64_t *blen = nullptr, *sq = nullptr, *gj = nullptr;
+  uint8_t* cov = nullptr;
+  int* bad = nullptr;
+  RCHK(S.alloc(&ds, ns, err));
+  RCHK(S.alloc(&blk, ns * mm, err));
+  RCHK(S.alloc(&blen, ns, err));
+  RCHK(S.alloc(&sq, ns, err));
+  RCHK(S.alloc(&gj, ns, err));
+  RCHK(S.alloc(&cov, n, err));
+  RCHK(S.alloc(&bad, 1, err));
+  HIPCHK(hipMemcpy(ds, seeds, ns * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(cov, 0, n));
+  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  ring_bfs_kernel<<<(unsigned)ns, 64, 2 * (size_t)mm * sizeof(int32_t)>>>(ns, ds, A.ptr, A.col, maxlvl, mm, blk, blen);
+  sq_len_kernel<<<nblk(ns), 256>>>(ns, blen, sq, gj);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(sq, sq, ns, nullptr, err));
+  RCHK(dscan_incl_i64(gj, gj, ns, nullptr, err));
+  int64_t nc = 0, ngj = 0;
+  RCHK(to_host(&nc, sq + ns - 1, 1, err));
+  RCHK(to_host(&ngj, gj + ns - 1, 1, err));
+  double *inv = nullptr, *scratch = nullptr;
+  RCHK(S.alloc(&inv, nc, err));
+  RCHK(S.alloc(&scratch, ngj, err));
+  ring_inv_kernel<<<(unsigned)ns, 64>>>(ns, mm, blk, blen, sq, gj, A.ptr, A.col, A.val, scratch, inv, cov, bad);
+  HIPCHK(hipGetLastError());
+  int hb = 0;
+  RCHK(read_int(bad, &hb, err));
+  if (hb) { *err = "Schwarz block not SPD"; return MAMG_ERR_SETUP; }
+  S.release(scratch);
+  // contributions: block keys, then the uncovered diagonal
+  int64_t* uscan = nullptr;
+  RCHK(S.alloc(&uscan, n, err));
+  uncov_flag_kernel<<<nblk(n), 256>>>(n, cov, uscan);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(uscan, uscan, n, nullptr, err));
+  int64_t nu = 0;
+  RCHK(to_host(&nu, uscan + n - 1, 1, err));
+  const int64_t e = nc + nu;
+  uint64_t *key = nullptr, *skey = nullptr;
+  int64_t *src = nullptr, *ssrc = nullptr;
+  RCHK(S.alloc(&key, e, err));
+  RCHK(S.alloc(&skey, e, err));
+  RCHK(S.alloc(&src, e, err));
+  RCHK(S.alloc(&ssrc, e, err));
+  ring_keys_kernel<<<(unsigned)ns, 64>>>(ns, mm, n, blk, blen, sq, key, src);
+  uncov_keys_kernel<<<nblk(n), 256>>>(n, cov, uscan, nc, key, src);
+  HIPCHK(hipGetLastError());
+  RCHK(dsort_pairs_u64_i64(key, skey, src, ssrc, e, bits_for(n * n - 1), nullptr, err));
+  S.release(key);
+  S.release(src);
+  int64_t* fscan = nullptr;
+  RCHK(S.alloc(&fscan, e, err));
+  run_flag_kernel<<<nblk(e), 256>>>(e, skey, fscan);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(fscan, fscan, e, nullptr, err));
+  int64_t nw = 0;
+  RCHK(to_host(&nw, fscan + e - 1, 1, err));
+  int64_t* ustart = nullptr;
+  RCHK(S.alloc(&ustart, nw, err));
+  W->n = W->m = n;
+  W->nnz = nw;
+  RCHK(galloc(G, &W->ptr, n + 1, err));
+  RCHK(galloc(G, &W->col, nw, err));
+  RCHK(galloc(G, &W->val, nw, err));
+  HIPCHK(hipMemset(W->ptr, 0, (n + 1) * sizeof(int64_t)));
+  run_start_kernel<<<nblk(e), 256>>>(e, n, skey, fscan, ustart, W->col, (unsigned long long*)W->ptr);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(W->ptr, W->ptr, n + 1, nullptr, err));
+  run_sum_kernel<<<nblk(nw), 256>>>(nw, e, ustart, ssrc, inv, A.ptr, A.col, A.val, W->val);
+  HIPCHK(hipGetLastError());
+  // lambda_max(S A): inf-norm power iterations from the hash start vector
+  double *v = nullptr, *t = nullptr, *w = nullptr;
+  unsigned long long* bits = nullptr;
+  RCHK(S.alloc(&v, n, err));
+  RCHK(S.alloc(&t, n, err));
+  RCHK(S.alloc(&w, n, err));
+  RCHK(S.alloc(&bits, 2, err));
+  hash_vec_kernel<<<nblk(n), 256>>>(n, v);
+  const unsigned gm = (unsigned)std::min<int64_t>(nblk(n), 1024);
+  for (int it = 0; it < std::max(p.rho_iters, 30); ++it) {
+    row_spmv_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, nullptr, v, t);
+    row_spmv_kernel<<<nblk(n), 256>>>(n, W->ptr, W->col, W->val, nullptr, t, w);
+    HIPCHK(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned long long), nullptr));
+    maxabs2_kernel<<<gm, 256>>>(n, v, w, bits);
+    vnorm_kernel<<<nblk(n), 256>>>(n, w, bits, v);
+  }
+  HIPCHK(hipGetLastError());
+  unsigned long long hbits[2] = {0, 0};
+  RCHK(to_host(hbits, bits, 2, err));
+  double mv, mw;
+  std::memcpy(&mv, &hbits[0], sizeof(double));
+  std::memcpy(&mw, &hbits[1], sizeof(double));
+  const double lam = mw / mv;
+  scale_vals_kernel<<<nblk(nw), 256>>>(nw, p.relaxation / lam, W->val);
+  HIPCHK(hipGetLastError());
+  return MAMG_OK;
+}
+
 }  // namespace
 
 int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mamg_params& p, GHier* G,
@@ -1299,15 +2113,20 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
   int rc = check_params(p, err);
   if (rc) return rc;
   if ((rc = check_patch_seeds(p, idofs, n_idofs, A0.n, err))) return rc;
-  if (p.num_functions != 2 || !p.node_block_smoother || (p.AMG_type == MAMG_SA_AMG && !p.sa_block_diag)) {
-    *err = "GPU setup covers the nodal 2-field profile (num_functions 2, node_block_smoother 1, "
-           "sa_block_diag 1); use the host setup (mamg_setup) for other profiles";
+  const int nf = p.num_functions;
+  if (nf != 1 && nf != 2) {
+    *err = "GPU setup covers num_functions 1 and 2; use the host setup (mamg_setup) for other profiles";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (A0.n != A0.m || A0.n <= 0 || A0.n % 2) { *err = "A must be square with an even size"; return MAMG_ERR_ARG; }
+  const bool nodal = nf == 2;
+  if (A0.n != A0.m || A0.n <= 0 || A0.n % nf) {
+    *err = "A must be square with a size divisible by num_functions";
+    return MAMG_ERR_ARG;
+  }
   G->params = p;
   G->device = p.device;
   G->levels.clear();
+  G->generic = false;
   HIPCHK(hipSetDevice(p.device));
   Clock clk, tot;
   {
@@ -1324,21 +2143,24 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       return MAMG_ERR_ARG;
     }
   }
+  // the host setup's per-level decisions (setup.cpp host_setup)
+  const bool blockP = nodal && p.sa_block_diag;
+  const bool rho_smoother = p.smoother == MAMG_SMOOTHER_JACOBI_RHO || p.smoother == MAMG_SMOOTHER_POLY;
   DevMat cur = A0;
   for (int l = 0; l < p.max_levels; ++l) {
     G->levels.emplace_back();
     GLevel& L = G->levels.back();
     if (l > 0) L.A = cur;
-    const int64_t n = cur.n, nv = n / 2;
+    const int64_t n = cur.n, nv = n / nf;
     L.n = n;
     bool last = (n <= p.coarse_dof) || (l == p.max_levels - 1);
     int64_t* agg = nullptr;
     int64_t nagg = 0;
-    if (n % 2) { *err = "matrix size not divisible by num_functions"; return MAMG_ERR_ARG; }
+    if (n % nf) { *err = "matrix size not divisible by num_functions"; return MAMG_ERR_ARG; }
     clk.lap();
     if (!last) {
-      RCHK(aggregate(G, cur, nv, l, p.strong_coupled, &agg, &nagg, err));
-      if (nagg == 0 || 2 * nagg >= n) last = true;
+      RCHK(aggregate(G, cur, nv, l, p.strong_coupled, !nodal, &agg, &nagg, err));
+      if (nagg == 0 || nf * nagg >= n) last = true;
     }
     G->phase_ms[0] += clk.lap();
     if (last) {
@@ -1353,55 +2175,72 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     }
     L.agg = agg;
     L.nagg = nagg;
-    // smoother blocks (level 0: seed blocks from idofs when node-aligned)
     Scratch S;
-    dv4_t* Dsm = nullptr;
-    RCHK(S.alloc(&Dsm, nv, err));
+    // smoother: overlapping seed rings (ADDITIVE), seed blocks (node-aligned:
+    // 2x2 node blocks with split nodes; else a general block CSR), 2x2 node
+    // blocks, or point weights
     const bool seeds = seed_blocks_on(p, l, idofs, n_idofs);
-    if (seeds && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
-      *err = "GPU setup: SCHWARZ_ADDITIVE (overlapping seed rings) is built by the host setup (mamg_setup)";
-      return MAMG_ERR_UNSUPPORTED;
-    }
-    if (seeds) {
-      int32_t* di = nullptr;
-      uint8_t* isseed = nullptr;
-      int64_t* best = nullptr;
-      int* bad = nullptr;
-      RCHK(S.alloc(&di, n_idofs, err));
-      RCHK(S.alloc(&isseed, n, err));
-      RCHK(S.alloc(&best, n, err));
-      RCHK(S.alloc(&bad, 2, err));
-      RCHK(galloc(G, &L.joined, nv, err));
-      HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIPCHK(hipMemset(isseed, 0, n));
-      HIPCHK(hipMemset(bad, 0, 2 * sizeof(int)));
-      seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
-      best_seed_kernel<<<nblk(n), 256>>>(n, cur.ptr, cur.col, cur.val, isseed, best);
-      seed_align_kernel<<<nblk(nv), 256>>>(nv, isseed, best, p.Schwarz_mmsize, L.joined, bad + 1);
-      HIPCHK(hipGetLastError());
-      int hb[2] = {0, 0};
-      RCHK(to_host(hb, bad, 2, err));
-      if (hb[0]) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
-      if (hb[1]) {
-        *err = "GPU setup: the idofs seed blocks are not node-aligned (a dof joins another node's "
-               "seed); use the host setup (mamg_setup)";
-        return MAMG_ERR_UNSUPPORTED;
-      }
-      RCHK(node_inverse(cur, nv, L.joined, Dsm, "smoother", err));
-    } else {
-      RCHK(node_inverse(cur, nv, nullptr, Dsm, "smoother", err));
-    }
+    const bool pointSA = p.AMG_type == MAMG_SA_AMG && !blockP;
+    bool node = false;              // smoother as 2x2 node blocks in Dsm / L.W
+    bool full_nodes = false;        // ... and those are the full node blocks
+    dv4_t* Dsm = nullptr;
     double rho_sm = 0.0;
-    RCHK(block_rho(cur, nv, Dsm, &rho_sm, err));
-    RCHK(galloc(G, (dv4_t**)&L.W, nv, err));
-    scale_blocks_kernel<<<nblk(nv), 256>>>(nv, p.relaxation / rho_sm, Dsm, (dv4_t*)L.W);
-    HIPCHK(hipGetLastError());
+    PointLevel PL;
+    const bool point_smoother = !seeds && !(nodal && p.node_block_smoother);
+    if (pointSA || point_smoother) RCHK(point_level(cur, p, pointSA || (point_smoother && rho_smoother), &S, &PL, err));
+    if (seeds && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
+      RCHK(overlap_smoother_dev(G, cur, idofs, n_idofs, p, &L.WB, err));
+    } else if (seeds) {
+      SeedBlocks B;
+      RCHK(seed_blocks_dev(cur, idofs, n_idofs, p.Schwarz_mmsize, &S, &B, err));
+      bool aligned = false;
+      if (nodal) {
+        int* bad = nullptr;
+        RCHK(S.alloc(&bad, 1, err));
+        HIPCHK(hipMemset(bad, 0, sizeof(int)));
+        RCHK(galloc(G, &L.joined, nv, err));
+        align_kernel<<<nblk(nv), 256>>>(nv, B.bid, B.bptr, L.joined, bad);
+        HIPCHK(hipGetLastError());
+        int hb = 0;
+        RCHK(read_int(bad, &hb, err));
+        aligned = hb == 0;
+        if (!aligned) { G->release(L.joined); L.joined = nullptr; }
+      }
+      if (aligned) {
+        RCHK(S.alloc(&Dsm, nv, err));
+        RCHK(node_inverse(cur, nv, L.joined, Dsm, "smoother", err));
+        node = true;
+      } else {
+        RCHK(block_inverse_dev(G, cur, B, &S, &L.WB, err));
+        double rho = 0.0;
+        RCHK(block_rho_dev(L.WB, cur, &rho, err));
+        scale_vals_kernel<<<nblk(L.WB.nnz), 256>>>(L.WB.nnz, p.relaxation / rho, L.WB.val);
+        HIPCHK(hipGetLastError());
+      }
+    } else if (nodal && p.node_block_smoother) {
+      RCHK(S.alloc(&Dsm, nv, err));
+      RCHK(node_inverse(cur, nv, nullptr, Dsm, "smoother", err));
+      node = full_nodes = true;
+    } else {
+      RCHK(galloc(G, &L.winv, n, err));
+      const int kind = p.smoother == MAMG_SMOOTHER_JACOBI ? 0 : p.smoother == MAMG_SMOOTHER_L1DIAG ? 1 : 2;
+      winv_kernel<<<nblk(n), 256>>>(n, kind, p.relaxation, PL.rho, PL.dg, PL.rs, L.winv);
+      HIPCHK(hipGetLastError());
+    }
+    if (node) {
+      RCHK(block_rho(cur, nv, Dsm, &rho_sm, err));
+      RCHK(galloc(G, (dv4_t**)&L.W, nv, err));
+      scale_blocks_kernel<<<nblk(nv), 256>>>(nv, p.relaxation / rho_sm, Dsm, (dv4_t*)L.W);
+      HIPCHK(hipGetLastError());
+    } else {
+      G->generic = true;
+    }
     G->phase_ms[1] += clk.lap();
     // prolongator
-    if (p.AMG_type == MAMG_SA_AMG) {
+    if (p.AMG_type == MAMG_SA_AMG && blockP) {
       dv4_t* Dsa = Dsm;
       double rho_sa = rho_sm;
-      if (seeds) {                  // SA always smooths with the full node blocks
+      if (!full_nodes) {            // SA always smooths with the full node blocks
         RCHK(S.alloc(&Dsa, nv, err));
         RCHK(node_inverse(cur, nv, nullptr, Dsa, "SA node", err));
         RCHK(block_rho(cur, nv, Dsa, &rho_sa, err));
@@ -1426,9 +2265,30 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
                                               L.P.col, L.P.val);
       HIPCHK(hipGetLastError());
       HIPCHK(hipDeviceSynchronize());
+    } else if (pointSA) {           // point SA: c_i = (sa_omega / rho) / a_ii
+      const double w = p.sa_omega / PL.rho;
+      L.w_sa = w;
+      GHier tmp;
+      DevMat AT;
+      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, nf * nagg, &AT, err, 1.0));
+      L.P.n = n;
+      L.P.m = nf * nagg;
+      RCHK(galloc(G, &L.P.ptr, n + 1, err));
+      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      smooth_pt_kernel<false><<<nblk(n), 256>>>(n, nv, agg, nagg, w, PL.dinv, AT.ptr, AT.col, AT.val, L.P.ptr,
+                                                nullptr, nullptr);
+      HIPCHK(hipGetLastError());
+      RCHK(dscan_incl_i64(L.P.ptr, L.P.ptr, n + 1, nullptr, err));
+      RCHK(to_host(&L.P.nnz, L.P.ptr + n, 1, err));
+      RCHK(galloc(G, &L.P.col, L.P.nnz, err));
+      RCHK(galloc(G, &L.P.val, L.P.nnz, err));
+      smooth_pt_kernel<true><<<nblk(n), 256>>>(n, nv, agg, nagg, w, PL.dinv, AT.ptr, AT.col, AT.val, L.P.ptr,
+                                               L.P.col, L.P.val);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipDeviceSynchronize());
     } else {
       L.P.n = n;
-      L.P.m = 2 * nagg;
+      L.P.m = nf * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
       HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
       tent_kernel<<<nblk(n), 256>>>(n, nv, agg, nagg, L.P.ptr, nullptr, nullptr, 0);
@@ -1445,7 +2305,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err, (double)L.P.nnz / std::max<int64_t>(1, L.P.n)));
     DevMat next;
     RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err, (double)L.AP.nnz / std::max<int64_t>(1, L.AP.n)));
-    if (!p.post_fusion) {
+    if (!p.post_fusion || !nodal) {   // host: A P kept for the fused post-smoothing of nodal levels
       for (void* q : {(void*)L.AP.ptr, (void*)L.AP.col, (void*)L.AP.val}) G->release(q);
       L.AP = DevMat();
     }
@@ -1456,6 +2316,24 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
                    (long long)cur.nnz, (long long)nagg, (long long)L.P.nnz);
     cur = next;
   }
+  if (G->generic)   // CSR apply layout: node-block levels as block CSRs too
+    for (GLevel& L : G->levels) {
+      if (L.coarsest || !L.W) continue;
+      const int64_t nv = L.n / 2;
+      L.WB.n = L.WB.m = L.n;
+      RCHK(galloc(G, &L.WB.ptr, L.n + 1, err));
+      HIPCHK(hipMemset(L.WB.ptr, 0, sizeof(int64_t)));
+      node_wb_kernel<<<nblk(L.n), 256>>>(nv, (const dv4_t*)L.W, L.joined, L.WB.ptr, nullptr, nullptr, 0);
+      HIPCHK(hipGetLastError());
+      RCHK(dscan_incl_i64(L.WB.ptr, L.WB.ptr, L.n + 1, nullptr, err));
+      RCHK(to_host(&L.WB.nnz, L.WB.ptr + L.n, 1, err));
+      RCHK(galloc(G, &L.WB.col, L.WB.nnz, err));
+      RCHK(galloc(G, &L.WB.val, L.WB.nnz, err));
+      node_wb_kernel<<<nblk(L.n), 256>>>(nv, (const dv4_t*)L.W, L.joined, L.WB.ptr, L.WB.col, L.WB.val, 1);
+      HIPCHK(hipGetLastError());
+      G->release(L.W);
+      L.W = nullptr;
+    }
   HIPCHK(hipDeviceSynchronize());
   G->phase_ms[6] = tot.lap();
   return MAMG_OK;
@@ -1506,7 +2384,7 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
       RCHK(to_host(h.Ainv.data(), g.Ainv, g.n * g.n, err));
       break;
     }
-    const int64_t nv = g.n / 2;
+    const int64_t nv = g.n / G.params.num_functions;
     RCHK(dl(g.P, &h.P));
     RCHK(dl(g.R, &h.R));
     if (g.AP.n) RCHK(dl(g.AP, &h.AP));
@@ -1514,6 +2392,15 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
     RCHK(to_host(h.agg.data(), g.agg, nv, err));
     h.nagg = g.nagg;
     h.w_sa = g.w_sa;
+    if (g.WB.n) {                   // general block smoother
+      RCHK(dl(g.WB, &h.WB));
+      continue;
+    }
+    if (g.winv) {                   // point smoother
+      h.winv.resize(g.n);
+      RCHK(to_host(h.winv.data(), g.winv, g.n, err));
+      continue;
+    }
     // smoother as the host's block CSR: node blocks {I, nv + I} (2 entries per
     // row), or singletons where level-0 seed blocks split a node
     std::vector<double> W(4 * nv);
@@ -1578,6 +2465,7 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H, GhostLists* ghosts,
                         std::string* err, bool matrices) {
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
+  if (G.generic) { *err = "rank download of a hierarchy without node-block smoothers"; return MAMG_ERR_UNSUPPORTED; }
   H->params = G.params;
   H->A0 = A0;
   H->levels.clear();

@@ -35,8 +35,9 @@ def test_emi_block_form_pcg_matches_oracle(lib_built, dim, n, g):
     s = M.problems.emi(dim, n, g)
     BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
     # interface seeds recruit their own side's interior neighbours: blocks are
-    # not node-aligned, so 'auto' takes the host setup and says why
-    assert BB.monolithic.setup_path.startswith('host (') and 'node-aligned' in BB.monolithic.setup_path
+    # not node-aligned, so the GPU setup builds a general block smoother and
+    # the handle runs the CSR layout
+    assert BB.monolithic.setup_path == 'gpu'
     assert BB.monolithic.layout == 'csr'
     b = [M.problems.seeded_rhs(s.W[0], 1234), M.problems.seeded_rhs(s.W[1], 4321)]
     # block apply == monolithic apply
@@ -52,6 +53,32 @@ def test_emi_block_form_pcg_matches_oracle(lib_built, dim, n, g):
     assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
     assert len(solver.residuals) < 80                                  # gamma-robust
     assert isinstance(x, list) and len(x[0]) == s.W[0]
+
+
+@pytest.mark.parametrize('dim,n,g', [(3, 16, 1e6), (2, 64, 1e6), (3, 8, 1e10)])
+def test_emi_reference_rings_gpu_setup(lib_built, dim, n, g):
+    """The reference's EMI smoother blocks: the interface seeds' overlapping
+    2-rings (get_hazmath_metric_precond_mono's Schwarz_maxlvl 2,
+    /root/reference/src/utils.py:60-86), smoothed additively
+    (SCHWARZ_ADDITIVE), built by the GPU setup: PCG history of the oracle."""
+    M = _M()
+    P = M.parameters
+    s = M.problems.emi(dim, n, g)
+    A = s.tocsr()
+    kw = dict(num_functions=2, Schwarz_type=P.SCHWARZ_ADDITIVE, Schwarz_maxlvl=2)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, **kw)
+    assert B.setup_path == 'gpu' and B.layout == 'csr'
+    b = M.problems.seeded_rhs(s.N, 1234)
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-10, maxiter=500)
+    solver * b
+    h = mo.setup(A, mo.Params(num_functions=2, Schwarz_type=5, Schwarz_maxlvl=2), idofs=one_sided(s))
+    ref = mo.pcg(A, h, b, 1e-10, 500)
+    if g < 1e8:
+        assert len(solver.residuals) == len(ref.residuals)
+        assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+    else:
+        assert abs(len(solver.residuals) - len(ref.residuals)) <= 1
+    assert len(solver.residuals) < 80
 
 
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, {}), (3, 32, 1e6, dict(smoother=12)),

@@ -117,23 +117,82 @@ def test_gpu_setup_device_input_and_pcg(lib_built):
     assert len(solver.residuals) == len(ref.residuals)
 
 
+def _generic_case(name):
+    """(A, W, idofs, parameter overrides) of the hierarchies whose smoothers
+    are not 2x2 node blocks: general seed blocks, overlapping seed rings
+    (SCHWARZ_ADDITIVE), point smoothers, scalar (num_functions 1) AMG."""
+    M = _mamg()
+    P = M.parameters
+    if name.startswith('emi'):            # EMI interface seeds: not node-aligned
+        s = M.problems.emi(3, 16, 1e6)
+        kw = dict(num_functions=2)
+        if name == 'emi_rings2':          # the reference's EMI default: 2-rings (src/utils.py:78)
+            kw.update(Schwarz_type=P.SCHWARZ_ADDITIVE, Schwarz_maxlvl=2)
+        if name == 'emi_rings2_poly':
+            kw.update(Schwarz_type=P.SCHWARZ_ADDITIVE, Schwarz_maxlvl=2, smoother=P.SMOOTHER_POLY)
+        return s.tocsr(), s.W, s.idofs, kw
+    if name.startswith('3d1d'):           # BASELINE config 5: scalar, additive 2-rings
+        s = M.problems.emi_3d1d(16, 1e4, 1.0 if name.endswith('r1') else 0.0)
+        return s.scipy(), s.W, s.idofs, dict(parameters=P.parameters_metric_3d1d)
+    s = M.problems.bidomain(3, 16, 1e4)
+    A = s.scipy()
+    if name == 'every3rd':                # seeds that do not pair up by node
+        return A, s.W, np.arange(0, s.N, 3, dtype=np.int32), dict(num_functions=2)
+    if name == 'nodal_point_smoother':    # node aggregates, point Jacobi, nodal SA
+        return A, s.W, None, dict(num_functions=2, node_block_smoother=0)
+    if name == 'nodal_point_sa':          # node aggregates, point SA prolongator
+        return A, s.W, None, dict(num_functions=2, sa_block_diag=0)
+    scalar = dict(num_functions=1)        # plain AMG (src/utils.py:15-42)
+    extra = {'scalar': {}, 'scalar_rho_iters': dict(rho_iters=5), 'scalar_ua': dict(AMG_type=1),
+             'scalar_hem': dict(aggregation_type=5), 'scalar_l1': dict(smoother=P.SMOOTHER_L1DIAG),
+             'scalar_jacobi': dict(smoother=P.SMOOTHER_JACOBI, strong_coupled=0.08),
+             'scalar_poly': dict(smoother=P.SMOOTHER_POLY)}[name]
+    return A, None, None, dict(scalar, **extra)
+
+
+GENERIC = ['emi_blocks', 'emi_rings2', 'emi_rings2_poly', '3d1d_r0', '3d1d_r1', 'every3rd',
+           'nodal_point_smoother', 'nodal_point_sa', 'scalar', 'scalar_rho_iters', 'scalar_ua',
+           'scalar_hem', 'scalar_l1', 'scalar_jacobi', 'scalar_poly']
+
+
+@pytest.mark.parametrize('name', GENERIC)
+def test_gpu_setup_generic_smoothers_bitwise(lib_built, name):
+    """The GPU setup of hierarchies without 2x2 node-block smoothers (general
+    seed blocks, SCHWARZ_ADDITIVE rings, point smoothers, scalar AMG) equals
+    the host setup bit for bit, level by level, and its CSR-layout handle
+    applies bitwise like the host setup's."""
+    M = _mamg()
+    A, W, idofs, kw = _generic_case(name)
+    Hh = M.HostHierarchy(A, idofs=idofs, **kw)
+    Hg = M.HostHierarchy(A, idofs=idofs, gpu=True, **kw)
+    hierarchies_equal(Hh, Hg)
+    Hh.close()
+    Hg.close()
+    Bg = M.MetricAMG(A, W, idofs=idofs, setup='gpu', **kw)
+    Bh = M.MetricAMG(A, W, idofs=idofs, setup='host', **kw)
+    # node-block smoothers with a point SA prolongator keep the BSR2 layout
+    assert Bg.setup_path == 'gpu' and Bg.layout == Bh.layout == ('bsr2' if name == 'nodal_point_sa' else 'csr')
+    assert Bg.num_levels == Bh.num_levels
+    for seed in (1234, 7):
+        r = mo.seeded_rhs(A.shape[0], seed)
+        assert np.array_equal(Bg * r, Bh * r)
+    auto = M.MetricAMG(A, W, idofs=idofs, **kw)      # 'auto' takes the GPU setup now
+    assert auto.setup_path == 'gpu'
+
+
 def test_gpu_setup_rejects_unsupported_and_bad_input(lib_built):
     M = _mamg()
     s = M.problems.bidomain(2, 16, 1e3)
     A = s.scipy()
-    with pytest.raises(M._lib.MamgError) as ei:           # scalar profile
-        M.MetricAMG(A, setup='gpu')
-    assert ei.value.code == -4
-    # 'auto' picks the host setup for it (recorded)
-    B = M.MetricAMG(A)
-    assert B.setup_path == 'host'
-    # seeds that are not node-aligned (every 3rd dof): GPU refuses, auto records why
+    # multicolour GS needs node-block smoothers: refused with the host's message
     idofs = np.arange(0, s.N, 3, dtype=np.int32)
     with pytest.raises(M._lib.MamgError) as ei:
-        M.MetricAMG(A, s.W, idofs=idofs, num_functions=2, setup='gpu')
+        M.MetricAMG(A, s.W, idofs=idofs, num_functions=2, smoother=M.parameters.SMOOTHER_SGS,
+                    Schwarz_type=M.parameters.SCHWARZ_SEED_BLOCKS, setup='gpu')
+    assert ei.value.code == -4 and 'BSR2' in str(ei.value)
+    with pytest.raises(M._lib.MamgError) as ei:           # three fields
+        M.MetricAMG(A[:3 * (s.N // 3), :3 * (s.N // 3)].tocsr(), num_functions=3, setup='gpu')
     assert ei.value.code == -4
-    B = M.MetricAMG(A, s.W, idofs=idofs, num_functions=2)
-    assert B.setup_path.startswith('host (') and 'node-aligned' in B.setup_path
     # unsorted columns in a row
     ip, ix, dv = s.indptr.copy(), s.indices.copy(), s.data.copy()
     ix[ip[5]], ix[ip[5] + 1] = ix[ip[5] + 1], ix[ip[5]]
