@@ -1103,21 +1103,23 @@ __global__ __launch_bounds__(256) void member_pos_kernel(int64_t n, const int64_
 }
 
 // Gauss-Jordan without pivoting (setup.cpp gauss_jordan) of the s x 2s matrix
-// M (row-major, [A | I]) by one workgroup of one wave; F = s multipliers.
+// M (row-major, [A | I]) by one workgroup of NT threads; F = s multipliers.
 // Every element sees the host's operations in the host's order (row k scaled,
 // then M_ij -= f_i M_kj with f read after the scaling), so the bits agree.
-__device__ bool wave_gauss_jordan(double* M, double* F, int64_t s) {
+template <int NT>
+__device__ bool block_gauss_jordan(double* M, double* F, int64_t s) {
   const int64_t w = 2 * s;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
   for (int64_t k = 0; k < s; ++k) {
     const double p = M[k * w + k];
     __syncthreads();
     if (!(p > 0.0)) return false;
-    for (int64_t j = lane; j < w; j += 64) M[k * w + j] = M[k * w + j] / p;
+    for (int64_t j = tid; j < w; j += NT) M[k * w + j] = M[k * w + j] / p;
     __syncthreads();
-    for (int64_t i = lane; i < s; i += 64) F[i] = i == k ? 0.0 : M[i * w + k];
+    for (int64_t i = tid; i < s; i += NT) F[i] = i == k ? 0.0 : M[i * w + k];
     __syncthreads();
-    for (int64_t t = lane; t < s * w; t += 64) {
+    // every element, as the host does (x - f 0 can turn -0 into +0)
+    for (int64_t t = tid; t < s * w; t += NT) {
       const int64_t i = t / w, j = t - i * w;
       if (i != k) M[i * w + j] = M[i * w + j] - F[i] * M[k * w + j];
     }
@@ -1193,7 +1195,7 @@ __global__ __launch_bounds__(64) void blk_multi_kernel(const int64_t* __restrict
     M[a * w + s + a] = 1.0;
   }
   __syncthreads();
-  if (!wave_gauss_jordan(M, F, s)) {
+  if (!block_gauss_jordan<64>(M, F, s)) {
     if (lane == 0) atomicAdd(bad, 1);
     return;
   }
@@ -1276,9 +1278,10 @@ __global__ __launch_bounds__(256) void sq_len_kernel(int64_t ns, const int64_t* 
   gj[k] = 2 * m * m + m;
 }
 
-// dense ring block from A (binary searches), its inverse into inv (row-major
+// dense ring block from A (binary searches), one workgroup of 256 threads
+// (blocks of up to Schwarz_mmsize 200 dofs), its inverse into inv (row-major
 // at the block's contribution offset), and the covered flags
-__global__ __launch_bounds__(64) void ring_inv_kernel(int64_t ns, int mm, const int32_t* __restrict__ blk,
+__global__ __launch_bounds__(256) void ring_inv_kernel(int64_t ns, int mm, const int32_t* __restrict__ blk,
                                                       const int64_t* __restrict__ blen,
                                                       const int64_t* __restrict__ sqscan,
                                                       const int64_t* __restrict__ gjscan,
@@ -1293,8 +1296,8 @@ __global__ __launch_bounds__(64) void ring_inv_kernel(int64_t ns, int mm, const 
   double* M = scratch + (k ? gjscan[k - 1] : 0);
   double* F = M + s * w;
   double* out = inv + (k ? sqscan[k - 1] : 0);
-  const int lane = threadIdx.x;
-  for (int64_t t = lane; t < s * w; t += 64) {
+  const int tid = threadIdx.x;
+  for (int64_t t = tid; t < s * w; t += 256) {
     const int64_t a = t / w, c = t - a * w;
     double x = 0.0;
     if (c < s) {
@@ -1305,13 +1308,13 @@ __global__ __launch_bounds__(64) void ring_inv_kernel(int64_t ns, int mm, const 
     }
     M[t] = x;
   }
-  for (int64_t a = lane; a < s; a += 64) cov[b[a]] = 1;
+  for (int64_t a = tid; a < s; a += 256) cov[b[a]] = 1;
   __syncthreads();
-  if (!wave_gauss_jordan(M, F, s)) {
-    if (lane == 0) atomicAdd(bad, 1);
+  if (!block_gauss_jordan<256>(M, F, s)) {
+    if (tid == 0) atomicAdd(bad, 1);
     return;
   }
-  for (int64_t t = lane; t < s * s; t += 64) {
+  for (int64_t t = tid; t < s * s; t += 256) {
     const int64_t a = t / s, c = t - a * s;
     out[t] = M[a * w + s + c];
   }
@@ -2031,7 +2034,7 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
   double *inv = nullptr, *scratch = nullptr;
   RCHK(S.alloc(&inv, nc, err));
   RCHK(S.alloc(&scratch, ngj, err));
-  ring_inv_kernel<<<(unsigned)ns, 64>>>(ns, mm, blk, blen, sq, gj, A.ptr, A.col, A.val, scratch, inv, cov, bad);
+  ring_inv_kernel<<<(unsigned)ns, 256>>>(ns, mm, blk, blen, sq, gj, A.ptr, A.col, A.val, scratch, inv, cov, bad);
   HIPCHK(hipGetLastError());
   int hb = 0;
   RCHK(read_int(bad, &hb, err));
