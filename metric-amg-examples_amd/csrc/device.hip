@@ -2649,17 +2649,13 @@ int poly_scaled(DeviceHandle* h, const double* W, int64_t n, std::vector<double*
   return MAMG_OK;
 }
 
-// Multicolour GS layout of one level from A_l's device BSR2 B and the
-// level's (scaled) smoother blocks W (only their pattern is used: a node
-// whose W block is diagonal has two 1x1 smoother blocks).  Colouring:
-// jp_round_kernel rounds (one 8-byte readback each); permutation: stable
-// radix sort of the nodes by colour (ascending node id within a colour);
-// then the permuted BSR2 copy, its block inverses, and the colour ranges.
-template <class HT>
-int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLevel* D, std::string* err) {
+// Jones-Plassmann colouring of the node graph of B (every node of the level;
+// jp_round_kernel rounds, one 8-byte readback each): *ca (TmpPool-owned, nr
+// bytes) = colour per node, *ncol = colours used
+int gs_colour(TmpPool* T, const TBsr& B, int level, int8_t** ca_out, int* ncol_out, std::string* err) {
   int rc;
   const int64_t nr = B.nr;
-  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 64 colours, [2] bad block
+  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 64 colours
   unsigned long long* left = nullptr;
   unsigned long long* cnt = nullptr;
   int8_t *ca = nullptr, *cb = nullptr;
@@ -2688,20 +2684,51 @@ int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLeve
   }
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[1]) { *err = "multicolour GS: more than 64 colours on level " + std::to_string(level); return MAMG_ERR_UNSUPPORTED; }
-  int32_t *ci = nullptr, *cs = nullptr;
-  int64_t *iota = nullptr, *sorted = nullptr;
+  int32_t* ci = nullptr;
+  int64_t* iota = nullptr;
   if ((rc = T->alloc(&ci, nr, err))) return rc;
-  if ((rc = T->alloc(&cs, nr, err))) return rc;
   if ((rc = T->alloc(&iota, nr, err))) return rc;
-  if ((rc = T->alloc(&sorted, nr, err))) return rc;
   colour_count_kernel<<<nblocks(nr), 256>>>(nr, ca, ci, iota, cnt);
   HIPCHK(hipGetLastError());
-  if ((rc = dsort_pairs_i32_i64(ci, cs, iota, sorted, nr, 6, nullptr, err))) return rc;
   unsigned long long hc[64];
   HIPCHK(hipMemcpy(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost));
   int ncol = 0;
   for (int c = 0; c < 64; ++c)
     if (hc[c]) ncol = c + 1;
+  for (void* q : {(void*)cb, (void*)ci, (void*)iota}) T->release(q);
+  *ca_out = ca;
+  *ncol_out = ncol;
+  return MAMG_OK;
+}
+
+// GS layout of the rows of B with colours ca (ncol colours; a colour may have
+// no rows here, as on one rank of a multi-GPU level): permutation by a stable
+// radix sort of the rows by colour (ascending row within a colour), the
+// permuted BSR2 copy, its block inverses (node blocks from W's pattern) and
+// the colour ranges (each colour padded to whole 64-row slices)
+template <class HT>
+int gs_layout(HT* h, TmpPool* T, const TBsr& B, const double* W, const int8_t* ca, int ncol, int level,
+              DBsr* Gb, int32_t** gperm, dv4** Gd, std::vector<int64_t>* gcs_out, std::vector<int64_t>* gbk,
+              std::string* err) {
+  int rc;
+  const int64_t nr = B.nr;
+  int* flags = nullptr;
+  unsigned long long* cnt = nullptr;
+  int32_t *ci = nullptr, *cs = nullptr;
+  int64_t *iota = nullptr, *sorted = nullptr;
+  if ((rc = T->alloc(&flags, 4, err))) return rc;
+  if ((rc = T->alloc(&cnt, 64, err))) return rc;
+  if ((rc = T->alloc(&ci, nr, err))) return rc;
+  if ((rc = T->alloc(&cs, nr, err))) return rc;
+  if ((rc = T->alloc(&iota, nr, err))) return rc;
+  if ((rc = T->alloc(&sorted, nr, err))) return rc;
+  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(hipMemset(cnt, 0, 64 * sizeof(unsigned long long)));
+  if (nr) colour_count_kernel<<<nblocks(nr), 256>>>(nr, ca, ci, iota, cnt);
+  HIPCHK(hipGetLastError());
+  if ((rc = dsort_pairs_i32_i64(ci, cs, iota, sorted, nr, 6, nullptr, err))) return rc;
+  unsigned long long hc[64];
+  HIPCHK(hipMemcpy(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost));
   // colour c: sorted positions [gcs[c], gcs[c+1]); permuted rows from pcs[c],
   // each colour padded to whole 64-row slices
   std::vector<int64_t> gcs(65, 0), pcs(65, 0);
@@ -2715,35 +2742,50 @@ int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLeve
   if ((rc = T->alloc(&pcs_d, 65, err))) return rc;
   HIPCHK(hipMemcpy(gcs_d, gcs.data(), 65 * sizeof(int64_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pcs_d, pcs.data(), 65 * sizeof(int64_t), hipMemcpyHostToDevice));
-  D->gcs.assign(pcs.begin(), pcs.begin() + ncol + 1);
+  gcs_out->assign(pcs.begin(), pcs.begin() + ncol + 1);
   TBsr G;
   G.nr = nrp; G.nc = B.nc; G.nb = B.nb;
   if ((rc = T->alloc(&G.ptr, nrp + 1, err))) return rc;
   HIPCHK(hipMemset(G.ptr, 0, sizeof(int64_t)));
-  if ((rc = dalloc(h, &D->gperm, nrp, err))) return rc;
-  if ((rc = dalloc(h, &D->Gd, nrp, err))) return rc;
-  HIPCHK(hipMemset(D->gperm, 0xff, nrp * sizeof(int32_t)));
-  perm_place_kernel<<<nblocks(nr), 256>>>(nr, cs, sorted, gcs_d, pcs_d, D->gperm);
+  if ((rc = dalloc(h, gperm, std::max<int64_t>(nrp, 1), err))) return rc;
+  if ((rc = dalloc(h, Gd, std::max<int64_t>(nrp, 1), err))) return rc;
+  HIPCHK(hipMemset(*gperm, 0xff, std::max<int64_t>(nrp, 1) * sizeof(int32_t)));
+  if (nr) perm_place_kernel<<<nblocks(nr), 256>>>(nr, cs, sorted, gcs_d, pcs_d, *gperm);
   HIPCHK(hipGetLastError());
-  perm_len_kernel<<<nblocks(nrp), 256>>>(nrp, D->gperm, B.ptr, G.ptr);
+  if (nrp) perm_len_kernel<<<nblocks(nrp), 256>>>(nrp, *gperm, B.ptr, G.ptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(G.ptr, G.ptr, nrp + 1, nullptr, err))) return rc;
   if ((rc = T->alloc(&G.col, G.nb, err))) return rc;
   if ((rc = T->alloc(&G.val, G.nb, err))) return rc;
-  perm_fill_kernel<<<nblocks(nrp), 256>>>(nrp, D->gperm, B.ptr, B.col, B.val, reinterpret_cast<const dv4*>(W),
-                                          G.ptr, G.col, G.val, D->Gd, flags + 2);
+  if (nrp)
+    perm_fill_kernel<<<nblocks(nrp), 256>>>(nrp, *gperm, B.ptr, B.col, B.val, reinterpret_cast<const dv4*>(W),
+                                            G.ptr, G.col, G.val, *Gd, flags + 2);
   HIPCHK(hipGetLastError());
+  int hf[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "multicolour GS: a smoother block is missing or not SPD on level " + std::to_string(level); return MAMG_ERR_SETUP; }
-  D->gbk.assign(ncol + 1, 0);
-  for (int c = 0; c <= ncol; ++c) HIPCHK(hipMemcpy(&D->gbk[c], G.ptr + D->gcs[c], sizeof(int64_t), hipMemcpyDeviceToHost));
+  gbk->assign(ncol + 1, 0);
+  for (int c = 0; c <= ncol; ++c) HIPCHK(hipMemcpy(&(*gbk)[c], G.ptr + (*gcs_out)[c], sizeof(int64_t), hipMemcpyDeviceToHost));
   // lane groups, not SELL-64: one lane per row over a colour's rows measured
   // 19.7 vs 11.5 ms for the four level-0 sweeps at nrefs=6
-  if ((rc = finalize_bsr(h, T, G, &D->Gb, 0, true, err, false))) return rc;
-  for (void* q : {(void*)ca, (void*)cb, (void*)ci, (void*)cs, (void*)iota, (void*)sorted, (void*)G.ptr, (void*)G.col,
-                  (void*)G.val})
+  if ((rc = finalize_bsr(h, T, G, Gb, 0, true, err, false))) return rc;
+  for (void* q : {(void*)ci, (void*)cs, (void*)iota, (void*)sorted, (void*)G.ptr, (void*)G.col, (void*)G.val})
     T->release(q);
   return MAMG_OK;
+}
+
+// Multicolour GS layout of one level from A_l's device BSR2 B and the
+// level's (scaled) smoother blocks W (only their pattern is used: a node
+// whose W block is diagonal has two 1x1 smoother blocks)
+template <class HT>
+int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLevel* D, std::string* err) {
+  int8_t* ca = nullptr;
+  int ncol = 0;
+  int rc = gs_colour(T, B, level, &ca, &ncol, err);
+  if (rc) return rc;
+  rc = gs_layout(h, T, B, W, ca, ncol, level, &D->Gb, &D->gperm, &D->Gd, &D->gcs, &D->gbk, err);
+  T->release(ca);
+  return rc;
 }
 
 __global__ __launch_bounds__(256) void split_blocks_kernel(int64_t nbs, const dv4* __restrict__ in, dv2* __restrict__ out) {
@@ -3090,7 +3132,8 @@ void cycle_ops_csr(const DeviceHandle* h, int l, const double* b, double* xout, 
 // ---- BSR2 layout.  b / xout of level 0 are the caller's field-major vectors
 // (stride nv0); all other vectors are node-interleaved (stride 0).
 // one multicolour GS sweep (colours ascending if fwd, else descending) in place on x
-Op gs_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int cls) {
+template <class LV>
+Op gs_op(const LV& L, int c, double* x, const double* b, int64_t bs, int cls) {
   Op o;
   o.kind = OP_GS; o.cls = cls; o.Mb = &L.Gb; o.perm = L.gperm; o.W = L.Gd;
   o.x = x; o.out = x; o.b = b; o.bs = bs;
@@ -4532,6 +4575,13 @@ __global__ __launch_bounds__(256) void pack2_kernel(int64_t n, const int64_t* __
   }
 }
 
+// ghost slots idx[k] of x (after the nloc owned nodes) <- buf pairs
+__global__ __launch_bounds__(256) void unpack2_kernel(int64_t n, const int64_t* __restrict__ idx, int64_t nloc,
+                                                      const double* __restrict__ buf, double* x) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) reinterpret_cast<double2*>(x)[nloc + idx[k]] = reinterpret_cast<const double2*>(buf)[k];
+}
+
 __global__ __launch_bounds__(256) void addidx2_kernel(int64_t n, const int64_t* __restrict__ idx,
                                                       const double* __restrict__ buf, double* x) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -4559,14 +4609,26 @@ struct DDLevel {
   int64_t* send_idx = nullptr;
   double *sendbuf = nullptr, *recvbuf = nullptr;
   std::vector<int64_t> send_off, ghost_off;
+  // multicolour GS (SMOOTHER_GS / SGS): the owned rows permuted colour by
+  // colour (gs_layout; the level's global colouring, so every rank has the
+  // same colours), and each colour's halo: its send nodes and ghost slots per
+  // peer, offsets cs_off / cg_off[c (P + 1) + q]
+  DBsr Gb;
+  int32_t* gperm = nullptr;
+  dv4* Gd = nullptr;
+  std::vector<int64_t> gcs, gbk;
+  int64_t *csend_idx = nullptr, *cghost_idx = nullptr;
+  std::vector<int64_t> cs_off, cg_off;
 };
 
-enum DKind { D_OP = 0, D_HALO = 1, D_REVERSE = 2, D_ALLREDUCE = 3, D_OVERLAP = 4 };
+// D_CHALO: the forward halo of one colour's nodes (after that colour's GS step)
+enum DKind { D_OP = 0, D_HALO = 1, D_REVERSE = 2, D_ALLREDUCE = 3, D_OVERLAP = 4, D_CHALO = 5 };
 
 struct DOp {
   int dk = D_OP;
   Op op;
   int level = 0;
+  int colour = 0;            // D_CHALO
   double* buf = nullptr;
   int64_t count = 0;
   double bytes = 0.0;
@@ -4690,10 +4752,110 @@ void dscale_ops(const DistHandle* h, int lc, std::vector<DOp>* ops) {
   ops->push_back(wrap(sc));
 }
 
+void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
+                std::vector<DOp>* ops);
+
+// coarse-grid correction of level l from its residual D.r: partial
+// restriction, reverse-add (or all-reduce into a replicated level), the
+// coarse cycle (W: twice), scaling, and the halo of the correction C.x
+void dcoarse_ops(const DistHandle* h, int l, std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[l];
+  const DDLevel& C = h->L[l + 1];
+  const bool l0 = l == 0;
+  const int tagA = l0 ? 0 : 1;
+  ops->push_back(wrap(bsr_op(D.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, D.r, 0, nullptr, nullptr, 0,
+                             nullptr, C.b, 0)));
+  ops->back().op.remap = 1;
+  if (!D.replicated) {
+    DOp d;
+    d.cls = C_COMM;
+    if (C.replicated) {
+      d.dk = D_ALLREDUCE; d.buf = C.b; d.count = 2 * C.nv; d.bytes = 16.0 * C.nv * 2;
+    } else {
+      d.dk = D_REVERSE; d.level = l + 1; d.buf = C.b;
+      const int64_t ns = C.send_off.back();
+      d.bytes = 16.0 * C.ng + 16.0 * ns * 3 + 8.0 * ns;
+    }
+    ops->push_back(d);
+  }
+  dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
+  if (h->p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {   // second visit on the updated residual
+    const Op res = bsr_op(C.A, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0);
+    if (C.replicated) ops->push_back(wrap(res)); else halo_residual(h, l + 1, C.x, res, ops);
+    dcycle_ops(h, l + 1, C.c, 0, C.e, 0, ops);
+    ops->push_back(wrap(axpy_op(2 * C.nloc, C.e, C.x)));
+  }
+  if (h->p.coarse_scaling) dscale_ops(h, l + 1, ops);      // ghosts of C.x scaled too
+  else if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+}
+
+DOp chalo_op(int level, int c, double* x, const DDLevel& D, int P) {
+  DOp d;
+  d.dk = D_CHALO; d.level = level; d.colour = c; d.buf = x; d.cls = C_COMM;
+  const int64_t ns = D.cs_off[(size_t)(c + 1) * (P + 1) - 1] - D.cs_off[(size_t)c * (P + 1)];
+  const int64_t ng = D.cg_off[(size_t)(c + 1) * (P + 1) - 1] - D.cg_off[(size_t)c * (P + 1)];
+  d.bytes = 8.0 * ns + 32.0 * ns + 8.0 * ng + 32.0 * ng;   // indices, pack, unpack
+  return d;
+}
+
+// one multicolour GS sweep on the owned rows, each colour's step followed by
+// that colour's halo so the next colour reads current ghosts; every rank
+// emits the same exchanges, also for colours it has no rows of
+void dgs_sweep(const DistHandle* h, int l, bool fwd, double* x, const double* b, int64_t bs, int cls,
+               std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[l];
+  const int nc = (int)D.gcs.size() - 1;
+  for (int k = 0; k < nc; ++k) {
+    const int c = fwd ? k : nc - 1 - k;
+    ops->push_back(wrap(gs_op(D, c, x, b, bs, cls)));   // empty here: not launched (same schedule on every rank)
+    if (!D.replicated) ops->push_back(chalo_op(l, c, x, D, h->nranks));
+  }
+}
+
+// multi-GPU cycle with multicolour GS / SGS (cycle_ops_bsr's GS branch): from
+// x = 0, pre sweeps, residual (ghosts current), coarse correction, x += P e,
+// halo, post sweeps; X holds [owned | ghost]
+void dcycle_gs(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
+               std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[l];
+  const DDLevel& C = h->L[l + 1];
+  const bool l0 = l == 0;
+  const int tagA = l0 ? 0 : 1;
+  const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
+  const int clsW = l0 ? C_L0_WB : C_COARSE;
+  const bool sgs = h->p.smoother == MAMG_SMOOTHER_SGS;
+  double* X = os == 0 ? xout : D.t;
+  {
+    Op z;
+    z.kind = OP_ZERO; z.cls = clsW; z.n = 2 * (D.nloc + D.ng); z.out = X; z.bytes = 8.0 * z.n;
+    ops->push_back(wrap(z));
+  }
+  for (int s = 0; s < h->p.presmooth_iter; ++s) {
+    dgs_sweep(h, l, true, X, b, bs, clsS, ops);
+    if (sgs) dgs_sweep(h, l, false, X, b, bs, clsS, ops);
+  }
+  ops->push_back(wrap(bsr_op(D.A, EPI_RESID, l0 ? C_L0_RESID : C_COARSE, tagA, X, 0, nullptr, b, bs, nullptr,
+                             D.r, 0)));
+  dcoarse_ops(h, l, ops);
+  ops->push_back(wrap(bsr_op(D.P, EPI_YADD, l0 ? C_L0_P : C_COARSE, tagA, C.x, 0, X, nullptr, 0, nullptr, X, 0)));
+  if (!D.replicated) ops->push_back(halo_op(l, X, D, C_COMM));
+  for (int s = 0; s < h->p.postsmooth_iter; ++s) {
+    if (sgs) dgs_sweep(h, l, true, X, b, bs, clsS, ops);
+    dgs_sweep(h, l, false, X, b, bs, clsS, ops);
+  }
+  if (X != xout) {
+    Op o;
+    o.kind = OP_ILV; o.epi = 1; o.cls = clsW; o.n = D.nloc; o.b = X; o.out = xout; o.os = os;
+    o.bytes = 32.0 * D.nloc;
+    ops->push_back(wrap(o));
+  }
+}
+
 // multi-GPU cycle from x = 0 (V or W, nu1 / nu2 sweeps, optional coarse-grid
 // scaling): see dist.cpp / dist_ref.py
 void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
                 std::vector<DOp>* ops) {
+  if (!h->L[l].coarsest && h->L[l].gcs.size() > 1) { dcycle_gs(h, l, b, bs, xout, os, ops); return; }
   const DDLevel& D = h->L[l];
   const bool l0 = l == 0;
   const int tagA = l0 ? 0 : 1;
@@ -4730,30 +4892,7 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
       halo_residual(h, l, X, res, ops);
     }
   }
-  ops->push_back(wrap(bsr_op(D.R, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, D.r, 0, nullptr, nullptr, 0,
-                             nullptr, C.b, 0)));
-  ops->back().op.remap = 1;
-  if (!D.replicated) {
-    DOp d;
-    d.cls = C_COMM;
-    if (C.replicated) {
-      d.dk = D_ALLREDUCE; d.buf = C.b; d.count = 2 * C.nv; d.bytes = 16.0 * C.nv * 2;
-    } else {
-      d.dk = D_REVERSE; d.level = l + 1; d.buf = C.b;
-      const int64_t ns = C.send_off.back();
-      d.bytes = 16.0 * C.ng + 16.0 * ns * 3 + 8.0 * ns;
-    }
-    ops->push_back(d);
-  }
-  dcycle_ops(h, l + 1, C.b, 0, C.x, 0, ops);
-  if (h->p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {   // second visit on the updated residual
-    const Op res = bsr_op(C.A, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0);
-    if (C.replicated) ops->push_back(wrap(res)); else halo_residual(h, l + 1, C.x, res, ops);
-    dcycle_ops(h, l + 1, C.c, 0, C.e, 0, ops);
-    ops->push_back(wrap(axpy_op(2 * C.nloc, C.e, C.x)));
-  }
-  if (h->p.coarse_scaling) dscale_ops(h, l + 1, ops);      // ghosts of C.x scaled too
-  else if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  dcoarse_ops(h, l, ops);
   int s0 = 0;
   if (D.K.nr > 0 || D.PA.nr > 0) {   // fused first post step (K built with its smoother), operands local
     const bool last = npost == 1;
@@ -4809,6 +4948,29 @@ int run_dop_host(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
   double* hs = h->hsend[d.level];
   double* hg = h->hghost[d.level];
   double* hr = h->hrecv[d.level];
+  if (d.dk == D_CHALO) {
+    const size_t b0 = (size_t)d.colour * (P + 1);
+    const int64_t s0 = D.cs_off[b0], s1 = D.cs_off[b0 + P], g0 = D.cg_off[b0], g1 = D.cg_off[b0 + P];
+    for (int q = 0; q < P; ++q) {
+      if (q == h->rank) continue;
+      snd[q] = hs + 2 * D.cs_off[b0 + q]; sc[q] = 2 * (D.cs_off[b0 + q + 1] - D.cs_off[b0 + q]);
+      rcv[q] = hg + 2 * D.cg_off[b0 + q]; rc[q] = 2 * (D.cg_off[b0 + q + 1] - D.cg_off[b0 + q]);
+    }
+    if (s1 > s0) {
+      pack2_kernel<<<nblocks(s1 - s0), 256, 0, s>>>(s1 - s0, D.csend_idx + s0, d.buf, D.sendbuf + 2 * s0);
+      HIPCHK(hipMemcpyAsync(hs + 2 * s0, D.sendbuf + 2 * s0, 2 * (s1 - s0) * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (h->ex.sendrecv(h->ex.ctx, P, snd.data(), sc.data(), rcv.data(), rc.data())) {
+      *err = "exchange sendrecv callback failed";
+      return MAMG_ERR_HIP;
+    }
+    if (g1 > g0) {
+      HIPCHK(hipMemcpyAsync(D.recvbuf + 2 * g0, hg + 2 * g0, 2 * (g1 - g0) * sizeof(double), hipMemcpyHostToDevice, s));
+      unpack2_kernel<<<nblocks(g1 - g0), 256, 0, s>>>(g1 - g0, D.cghost_idx + g0, D.nloc, D.recvbuf + 2 * g0, d.buf);
+    }
+    return MAMG_OK;
+  }
   for (int q = 0; q < P; ++q) {
     if (q == h->rank) continue;
     const int64_t sq = D.send_off[q + 1] - D.send_off[q], gq = D.ghost_off[q + 1] - D.ghost_off[q];
@@ -4884,6 +5046,22 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     int rc = run_dop(h, hd, s, err);
     HIPCHK(hipStreamWaitEvent(s, h->ev_out, 0));
     return rc;
+  }
+  if (d.dk == D_CHALO) {      // one colour's nodes: pack, send / receive, unpack into the ghost slots
+    const int P = h->nranks;
+    const size_t b0 = (size_t)d.colour * (P + 1);
+    const int64_t s0 = D.cs_off[b0], s1 = D.cs_off[b0 + P], g0 = D.cg_off[b0], g1 = D.cg_off[b0 + P];
+    if (s1 > s0) pack2_kernel<<<nblocks(s1 - s0), 256, 0, s>>>(s1 - s0, D.csend_idx + s0, d.buf, D.sendbuf + 2 * s0);
+    NCCLCHK(ncclGroupStart());
+    for (int q = 0; q < P; ++q) {
+      if (q == h->rank) continue;
+      const int64_t sc = D.cs_off[b0 + q + 1] - D.cs_off[b0 + q], gc = D.cg_off[b0 + q + 1] - D.cg_off[b0 + q];
+      if (sc) NCCLCHK(ncclSend(D.sendbuf + 2 * D.cs_off[b0 + q], 2 * sc, ncclDouble, q, h->comm, s));
+      if (gc) NCCLCHK(ncclRecv(D.recvbuf + 2 * D.cg_off[b0 + q], 2 * gc, ncclDouble, q, h->comm, s));
+    }
+    NCCLCHK(ncclGroupEnd());
+    if (g1 > g0) unpack2_kernel<<<nblocks(g1 - g0), 256, 0, s>>>(g1 - g0, D.cghost_idx + g0, D.nloc, D.recvbuf + 2 * g0, d.buf);
+    return MAMG_OK;
   }
   if (d.dk == D_HALO) {
     if (ns) pack2_kernel<<<nblocks(ns), 256, 0, s>>>(ns, D.send_idx, d.buf, D.sendbuf);
@@ -5115,10 +5293,46 @@ int dev_window_cols(TmpPool* T, const TBsr& B, int64_t w0, int64_t w1, TBsr* O, 
   return MAMG_OK;
 }
 
+// each colour's halo of a distributed level: colour c's nodes in every send
+// list and ghost list, in list order (so the sender's subset and the
+// receiver's subset match), offsets per (colour, peer); gcol = the level's
+// global colouring on the device
+int colour_halo_lists(DistHandle* h, const DistLevel& P, const int8_t* gcol, int ncol, DDLevel* D,
+                      std::string* err) {
+  const int R = h->nranks;
+  std::vector<int8_t> hc(P.nv);
+  if (P.nv) HIPCHK(hipMemcpy(hc.data(), gcol, P.nv, hipMemcpyDeviceToHost));
+  std::vector<int64_t> cs, cg;
+  D->cs_off.assign((size_t)ncol * (R + 1), 0);
+  D->cg_off.assign((size_t)ncol * (R + 1), 0);
+  for (int c = 0; c < ncol; ++c) {
+    for (int q = 0; q < R; ++q) {
+      D->cs_off[(size_t)c * (R + 1) + q] = (int64_t)cs.size();
+      D->cg_off[(size_t)c * (R + 1) + q] = (int64_t)cg.size();
+      for (int64_t t = P.send_off[q]; t < P.send_off[q + 1]; ++t)
+        if (hc[P.o0 + P.send_idx[t]] == c) cs.push_back(P.send_idx[t]);
+      for (int64_t g = P.ghost_off[q]; g < P.ghost_off[q + 1]; ++g)
+        if (hc[P.ghosts[g]] == c) cg.push_back(g);
+    }
+    D->cs_off[(size_t)c * (R + 1) + R] = (int64_t)cs.size();
+    D->cg_off[(size_t)c * (R + 1) + R] = (int64_t)cg.size();
+  }
+  int rc;
+  if (!cs.empty()) {
+    if ((rc = ddalloc(h, &D->csend_idx, (int64_t)cs.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->csend_idx, cs.data(), cs.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (!cg.empty()) {
+    if ((rc = ddalloc(h, &D->cghost_idx, (int64_t)cg.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->cghost_idx, cg.data(), cg.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+
 // level l's A_loc (+ overlap window, band schedule), K / [P | AP] / P, R_loc
 // and W from the GPU hierarchy (the operator block of dist_upload)
 int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPlan& plan, int l, double kw,
-                 std::string* err) {
+                 const int8_t* gcol, int ncol, std::string* err) {
   int rc;
   const DistLevel& P = plan.levels[l];
   const GLevel& g = G.levels[l];
@@ -5127,7 +5341,15 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
   TmpPool T;
   int32_t* map = nullptr;
   if (!P.replicated && (rc = dev_col_map(&T, P, &map, err))) return rc;
-  // A_loc
+  // W (node blocks of the owned rows)
+  if ((rc = ddalloc(h, &D.W, nloc, err))) return rc;
+  if (nloc) {
+    HIPCHK(hipMemcpy(D.W, reinterpret_cast<const dv4*>(g.W) + P.o0, nloc * sizeof(dv4), hipMemcpyDeviceToDevice));
+    if (g.joined) unjoin_kernel<<<nblocks(nloc), 256>>>(nloc, g.joined + P.o0, D.W);
+    HIPCHK(hipGetLastError());
+  }
+  // A_loc (+ the multicolour GS layout of its rows, colours of the level's
+  // global colouring gcol)
   {
     TBsr raw, tA;
     const DevMat& Am = l == 0 ? A0d : g.A;
@@ -5169,13 +5391,9 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
     }
     if (!half && (rc = finalize_bsr(h, &T, tA, &D.A, 0, true, err))) return rc;
     if (l == 0 && (rc = build_band_sched_range(h, &D.A, D.ib0, D.ib1, err))) return rc;
-  }
-  // W (node blocks of the owned rows)
-  if ((rc = ddalloc(h, &D.W, nloc, err))) return rc;
-  if (nloc) {
-    HIPCHK(hipMemcpy(D.W, reinterpret_cast<const dv4*>(g.W) + P.o0, nloc * sizeof(dv4), hipMemcpyDeviceToDevice));
-    if (g.joined) unjoin_kernel<<<nblocks(nloc), 256>>>(nloc, g.joined + P.o0, D.W);
-    HIPCHK(hipGetLastError());
+    if (gcol && (rc = gs_layout(h, &T, tA, reinterpret_cast<const double*>(D.W), gcol + P.o0, ncol, l, &D.Gb,
+                                &D.gperm, &D.Gd, &D.gcs, &D.gbk, err)))
+      return rc;
   }
   // prolongation side (level l+1 numbering)
   const DistLevel& C = plan.levels[l + 1];
@@ -5244,9 +5462,14 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (gs_smoother(p) || patch_schwarz(p)) {
-    *err = "multi-GPU apply supports the block-Jacobi and POLY smoothers (multicolour GS and node patches "
-           "would need one halo per colour)";
+  if (patch_schwarz(p)) {
+    *err = "multi-GPU apply: node-patch Schwarz (SCHWARZ_PATCHES) is single-GPU";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  const bool gs = gs_smoother(p);
+  if (gs && !G) {
+    *err = "multi-GPU multicolour GS needs the rank operators built from the GPU hierarchy (mamg_setup_dist "
+           "with a GPU-setup profile)";
     return MAMG_ERR_UNSUPPORTED;
   }
   read_knobs();
@@ -5255,7 +5478,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   DistPlan plan;
   const auto tp0 = std::chrono::steady_clock::now();
   const double kw = p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0;
-  bool fuse = p.post_fusion != 0;
+  bool fuse = p.post_fusion != 0 && !gs;   // GS post-smooths after x += P e (as on one GPU)
   if (G)                   // operators from the GPU hierarchy: fusion needs its A P on every level
     for (size_t l = 0; l + 1 < G->levels.size() && fuse; ++l)
       if (!G->levels[l].coarsest && G->levels[l].AP.n != G->levels[l].n) fuse = false;
@@ -5308,7 +5531,19 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.Ainv, n * n, err))) return rc;
       HIPCHK(hipMemcpy(D.Ainv, Ap.data(), n * n * sizeof(double), hipMemcpyHostToDevice));
     } else if (G) {
-      if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, err))) return rc;
+      // multicolour GS: the level's global colouring (every rank computes the
+      // same one, as the single-GPU build_gs), then each colour's halo lists
+      TmpPool TC;
+      int8_t* gcol = nullptr;
+      int ncol = 0;
+      if (gs) {
+        TBsr B;
+        if ((rc = dev_csr_to_bsr(&TC, l == 0 ? *A0d : G->levels[l].A, D.nv, D.nv, &B, err))) return rc;
+        if ((rc = gs_colour(&TC, B, l, &gcol, &ncol, err))) return rc;
+        TC.release(B.ptr); TC.release(B.col); TC.release(B.val);
+        if (!D.replicated && (rc = colour_halo_lists(h.get(), P, gcol, ncol, &D, err))) return rc;
+      }
+      if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, gcol, ncol, err))) return rc;
     } else {
       if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
         int64_t best0 = 0, best1 = 0, run0 = 0;
@@ -5374,8 +5609,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.send_idx, ns, err))) return rc;
       HIPCHK(hipMemcpy(D.send_idx, P.send_idx.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice));
       if ((rc = ddalloc(h.get(), &D.sendbuf, 2 * ns, err))) return rc;
-      if ((rc = ddalloc(h.get(), &D.recvbuf, 2 * ns, err))) return rc;
     }
+    if (std::max(ns, D.ng) > 0 && (rc = ddalloc(h.get(), &D.recvbuf, 2 * std::max(ns, D.ng), err))) return rc;
   }
   h->nv0 = plan.levels[0].nv;
   h->o0 = plan.levels[0].o0;
@@ -5524,6 +5759,35 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
                                 Q.sendbuf + 2 * Q.send_off[p], 2 * gc * sizeof(double),
                                 hipMemcpyDeviceToDevice, s));
         }
+      }
+    } else if (dk == D_CHALO) {
+      const int c = ops[0][k].colour;
+      const size_t b0 = (size_t)c * (P + 1);
+      for (int p = 0; p < P; ++p) {
+        const DDLevel& D = hs[p]->L[ops[p][k].level];
+        const int64_t s0 = D.cs_off[b0], s1 = D.cs_off[b0 + P];
+        if (s1 > s0)
+          pack2_kernel<<<nblocks(s1 - s0), 256, 0, s>>>(s1 - s0, D.csend_idx + s0, ops[p][k].buf, D.sendbuf + 2 * s0);
+      }
+      for (int p = 0; p < P; ++p) {          // p receives colour c's ghosts from q
+        const DDLevel& D = hs[p]->L[ops[p][k].level];
+        for (int q = 0; q < P; ++q) {
+          if (q == p) continue;
+          const int64_t gc = D.cg_off[b0 + q + 1] - D.cg_off[b0 + q];
+          const DDLevel& Q = hs[q]->L[ops[q][k].level];
+          const int64_t sc = Q.cs_off[b0 + p + 1] - Q.cs_off[b0 + p];
+          if (sc != gc) { *err = "colour halo count mismatch"; return MAMG_ERR_SETUP; }
+          if (!gc) continue;
+          HIPCHK(hipMemcpyAsync(D.recvbuf + 2 * D.cg_off[b0 + q], Q.sendbuf + 2 * Q.cs_off[b0 + p],
+                                2 * gc * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+      }
+      for (int p = 0; p < P; ++p) {
+        const DDLevel& D = hs[p]->L[ops[p][k].level];
+        const int64_t g0 = D.cg_off[b0], g1 = D.cg_off[b0 + P];
+        if (g1 > g0)
+          unpack2_kernel<<<nblocks(g1 - g0), 256, 0, s>>>(g1 - g0, D.cghost_idx + g0, D.nloc, D.recvbuf + 2 * g0,
+                                                          ops[p][k].buf);
       }
     } else if (dk == D_REVERSE) {
       for (int q = 0; q < P; ++q) {          // owner q receives partials from p

@@ -15,6 +15,8 @@ Per distributed level (POLY: the step weights w_k; nu1 / nu2 repeat them):
   [W-cycle: halo(xc) ; xc += cycle(l+1, bc - A_c xc)] ;
   [scaling: halo(xc) ; all-reduce(<bc, xc>, <A_c xc, xc>) ; xc *= alpha] ;
   [next distributed: halo(xc)] ; X += P xc ; halo(X) ; z = X + W (b - A X)
+Multicolour GS / SGS (gs=...): X = 0 ; sweeps with a halo after every colour ;
+  r = b - A X ; (coarse correction as above) ; X += P xc ; halo(X) ; sweeps.
 Replicated levels run the same cycle on global arrays without exchange.
 """
 from __future__ import annotations
@@ -113,12 +115,17 @@ class DistCycle:
     <b_c, e> / <A_c e, e> with the two sums all-reduced over the ranks
     (src/amg_parameters.py:78; mamg_oracle.coarse_scale)."""
 
-    def __init__(self, plan_levels, Ainv_nodemajor, comm, poly=None, wcycle=False, scaling=False, nu1=1, nu2=1):
+    def __init__(self, plan_levels, Ainv_nodemajor, comm, poly=None, wcycle=False, scaling=False, nu1=1, nu2=1,
+                 gs=None, sgs=True):
         self.L = plan_levels
         self.Ainv = Ainv_nodemajor
         self.comm = comm
         self.ws = list(poly) if poly else [1.0]
         self.wcycle, self.scaling, self.nu1, self.nu2 = wcycle, scaling, nu1, nu2
+        # multicolour GS (mamg_oracle Level.gs_sweep): per level the global
+        # colour of every node and its (2, 2) block inverse; sgs: forward then
+        # backward sweeps
+        self.gs, self.sgs = gs, sgs
 
     # forward halo: fill ghost rows of x2 (nloc+ng, 2)
     def halo(self, lv, x2):
@@ -160,16 +167,65 @@ class DistCycle:
             X = X + w * bd_mv(lv['W'], b2 - bsr_mv(lv['A'], self.ghosted(lv, X)))
         return X
 
+    def gs_sweep(self, l, lv, X, b2, fwd):
+        """one multicolour GS sweep on the owned nodes of X ([owned | ghost]
+        on a distributed level), the ghosts refreshed after every colour (the
+        product refreshes only that colour's: the others did not change)."""
+        colour, Dn = self.gs[l]
+        o0, nloc = lv['o0'], lv['nloc']
+        cl, D = colour[o0:o0 + nloc], Dn[o0:o0 + nloc]
+        nc = int(colour.max()) + 1
+        for c in (range(nc) if fwd else range(nc - 1, -1, -1)):
+            I = np.flatnonzero(cl == c)
+            if len(I):
+                res = b2[I] - bsr_mv(lv['A'], X)[I]
+                X[I] = X[I] + np.stack([D[I, 0, 0] * res[:, 0] + D[I, 0, 1] * res[:, 1],
+                                        D[I, 1, 0] * res[:, 0] + D[I, 1, 1] * res[:, 1]], axis=1)
+            if not lv['replicated']:
+                self.halo(lv, X)
+        return X
+
     def cycle(self, l, b2):
         lv = self.L[l]
         if lv['coarsest']:
             return (self.Ainv @ b2.ravel()).reshape(-1, 2)
+        if self.gs is not None and self.gs[l] is not None:
+            return self.cycle_gs(l, b2)
         C = self.L[l + 1]
         pre = self.ws * self.nu1
         post = self.ws[::-1] * self.nu2
         X = pre[0] * bd_mv(lv['W'], b2)
         X = self.smooth(lv, b2, X, pre[1:])
         r = b2 - bsr_mv(lv['A'], self.ghosted(lv, X))
+        xc = self.coarse(l, r)
+        X = X + bsr_mv(lv['P'], self.ghosted(C, xc))
+        return self.smooth(lv, b2, X, post)
+
+    def cycle_gs(self, l, b2):
+        lv = self.L[l]
+        C = self.L[l + 1]
+        full = lv['nloc'] + (0 if lv['replicated'] else len(lv['ghosts']))
+        X = np.zeros((full, 2))
+        for _ in range(self.nu1):
+            X = self.gs_sweep(l, lv, X, b2, True)
+            if self.sgs:
+                X = self.gs_sweep(l, lv, X, b2, False)
+        r = b2 - bsr_mv(lv['A'], X)
+        xc = self.coarse(l, r)
+        X[:lv['nloc']] = X[:lv['nloc']] + bsr_mv(lv['P'], self.ghosted(C, xc))
+        if not lv['replicated']:
+            self.halo(lv, X)
+        for _ in range(self.nu2):
+            if self.sgs:
+                X = self.gs_sweep(l, lv, X, b2, True)
+            X = self.gs_sweep(l, lv, X, b2, False)
+        return X[:lv['nloc']]
+
+    def coarse(self, l, r):
+        """coarse-grid correction from the owned residual rows r: restriction,
+        reverse-add / all-reduce, coarse cycle (W: twice), scaling."""
+        lv = self.L[l]
+        C = self.L[l + 1]
         part = bsr_mv(lv['R'], r)
         if lv['replicated']:
             bc = part
@@ -188,8 +244,7 @@ class DistCycle:
                 sums = self.comm.allreduce_sum(sums)
             num, den = float(sums[0, 0]), float(sums[0, 1])
             xc = (num / den if den > 0 else 1.0) * xc
-        X = X + bsr_mv(lv['P'], self.ghosted(C, xc))
-        return self.smooth(lv, b2, X, post)
+        return xc
 
     def apply_local(self, r_local_fieldmajor):
         """r_local: [u1 owned ; u2 owned] (length 2*nloc) -> z_local, same layout."""

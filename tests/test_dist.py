@@ -43,17 +43,32 @@ def _system(problem, kw):
 def _c_kw(kw):
     """oracle Params keys -> the C-ABI's enum values"""
     c = dict(kw)
-    if c.get('smoother') == 'POLY':
-        c['smoother'] = 12
+    if 'smoother' in c:
+        c['smoother'] = {'POLY': 12, 'GS': 10, 'SGS': 11}[c['smoother']]
     if 'cycle_type' in c:
         c['cycle_type'] = {'V': 1, 'W': 2}[c['cycle_type']]
     return c
 
 
-def _cycle_kw(kw):
-    """oracle Params keys -> dist_ref.DistCycle flags"""
-    return dict(wcycle=kw.get('cycle_type') == 'W', scaling=bool(kw.get('coarse_scaling', 0)),
-                nu1=kw.get('presmooth_iter', 1), nu2=kw.get('postsmooth_iter', 1))
+def _cycle_kw(kw, h=None):
+    """oracle Params keys -> dist_ref.DistCycle flags; multicolour GS takes
+    each level's global colouring and block inverses from the oracle
+    hierarchy h"""
+    out = dict(wcycle=kw.get('cycle_type') == 'W', scaling=bool(kw.get('coarse_scaling', 0)),
+               nu1=kw.get('presmooth_iter', 1), nu2=kw.get('postsmooth_iter', 1))
+    if kw.get('smoother') in ('GS', 'SGS'):
+        out['gs'] = [(lev.colour, lev.Dn) if lev.colour is not None else None for lev in h.levels]
+        out['sgs'] = kw['smoother'] == 'SGS'
+    return out
+
+
+# the reference's smoother family on N ranks: multicolour SGS (level 0 on the
+# seed blocks) with coarse scaling; GS; and UA + HEM + W + SGS + scaling
+GS_CASES = [('bidomain', dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7)),
+            ('bidomain', dict(smoother='GS', Schwarz_type=7)),
+            ('bidomain', dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7, AMG_type='UA',
+                              aggregation_type='HEM', cycle_type='W')),
+            ('emi', dict(smoother='SGS', coarse_scaling=1, Schwarz_type=3))]
 
 
 @pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('bidomain', dict(smoother='POLY')),
@@ -62,11 +77,15 @@ def _cycle_kw(kw):
                                         ('bidomain', dict(coarse_scaling=1)),
                                         ('bidomain', dict(cycle_type='W', coarse_scaling=1, presmooth_iter=2,
                                                           postsmooth_iter=2)),
-                                        ('emi', dict(smoother='POLY', cycle_type='W', coarse_scaling=1))])
+                                        ('emi', dict(smoother='POLY', cycle_type='W', coarse_scaling=1))]
+                         + GS_CASES)
 @pytest.mark.parametrize('P,rep', [(1, 100), (2, 100), (2, 10 ** 6), (3, 100), (4, 100)])
 def test_dist_cycle_threads(lib_built, P, rep, problem, kw):
     M, s, kw = _system(problem, kw)
     ckw = _c_kw(kw)
+    for k in ('AMG_type', 'aggregation_type'):
+        if k in ckw:
+            ckw[k] = {'UA': 1, 'SA': 2, 'MIS': 2, 'HEM': 5}[ckw[k]]
     H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **ckw)
     prm = mo.Params(num_functions=2, **kw)
     h = mo.setup(s.scipy(), prm, idofs=s.idofs)
@@ -81,7 +100,7 @@ def test_dist_cycle_threads(lib_built, P, rep, problem, kw):
 
     def run(p):
         L0 = lvls[p][0]
-        dc = dr.DistCycle(lvls[p], Ainv, comm.view(p), poly, **_cycle_kw(kw))
+        dc = dr.DistCycle(lvls[p], Ainv, comm.view(p), poly, **_cycle_kw(kw, h))
         outs[p] = dc.apply_local(dr.local_slice(r, s.nv, L0['o0'], L0['o1']))
 
     th = [threading.Thread(target=run, args=(p,)) for p in range(P)]
@@ -145,6 +164,9 @@ def _gloo_worker(rank, world, port, q, problem='bidomain', kw=None):
         import mamg_oracle
         M, s, kw = _system(problem, kw or {})
         ckw = _c_kw(kw)
+        for k in ('AMG_type', 'aggregation_type'):
+            if k in ckw:
+                ckw[k] = {'UA': 1, 'SA': 2, 'MIS': 2, 'HEM': 5}[ckw[k]]
         H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **ckw)
         plan = M.DistPlan(H, rank, world, 100)
         lv = [plan.level(l) for l in range(plan.num_levels)]
@@ -152,7 +174,8 @@ def _gloo_worker(rank, world, port, q, problem='bidomain', kw=None):
         r = mamg_oracle.seeded_rhs(s.N)
         prm = mamg_oracle.Params(num_functions=2, **kw)
         poly = mamg_oracle.poly_weights(prm) if prm.smoother == 'POLY' else None
-        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm(), poly, **_cycle_kw(kw))
+        h = mamg_oracle.setup(s.scipy(), prm, idofs=s.idofs) if kw.get('smoother') in ('GS', 'SGS') else None
+        dc = dist_ref.DistCycle(lv, Ainv, dist_ref.GlooComm(), poly, **_cycle_kw(kw, h))
         z = dc.apply_local(dist_ref.local_slice(r, s.nv, lv[0]['o0'], lv[0]['o1']))
         q.put((rank, lv[0]['o0'], lv[0]['o1'], z))
     finally:
@@ -160,7 +183,7 @@ def _gloo_worker(rank, world, port, q, problem='bidomain', kw=None):
 
 
 @pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother='POLY')),
-                                        ('bidomain', dict(cycle_type='W', coarse_scaling=1))])
+                                        ('bidomain', dict(cycle_type='W', coarse_scaling=1)), GS_CASES[2]])
 def test_dist_cycle_gloo_world2(lib_built, problem, kw):
     import torch.multiprocessing as mp
     ctx = mp.get_context('spawn')

@@ -115,6 +115,49 @@ def test_virtual_ranks_w_cycle_and_scaling(lib_built, kw, P, rep):
         hh.close()
 
 
+@pytest.mark.parametrize('kw,P,rep', [
+    (dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7), 2, 100),
+    (dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7), 3, 1),
+    (dict(smoother='GS', Schwarz_type=7), 3, 100),
+    (dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7, presmooth_iter=2, postsmooth_iter=2), 4, 1),
+    (dict(smoother='SGS', coarse_scaling=1, Schwarz_type=7, AMG_type='UA', aggregation_type='HEM',
+          cycle_type='W'), 8, 1)])
+def test_virtual_ranks_multicolour_gs(lib_built, kw, P, rep):
+    """The reference's smoother family on P virtual ranks: multicolour node-
+    block GS / SGS (level 0 on the seed blocks) with a halo of each colour's
+    nodes after its step, so every colour reads current ghosts -- the same
+    sweep as on one GPU (src/amg_parameters.py:72-78).  Equal to the one-GPU
+    handle's apply up to summation order, and to the oracle; the last case is
+    the reference family (UA + HEM + W-cycle + SGS + coarse scaling) with
+    every level above the coarsest distributed."""
+    import torch
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e6)
+    ckw = dict(kw)
+    conv = {'smoother': {'SGS': 11, 'GS': 10}, 'cycle_type': {'W': 2}, 'AMG_type': {'UA': 1},
+            'aggregation_type': {'HEM': 5}}
+    for k, m in conv.items():
+        if k in ckw:
+            ckw[k] = m[ckw[k]]
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    B1 = M.MetricAMG(s.scipy(), s.W, idofs=s.idofs, num_functions=2, setup='gpu', **ckw)
+    z1 = B1 * r
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
+                          num_functions=2, **ckw) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    z = _gather(s, hs, zs)
+    assert np.linalg.norm(z - z1) / np.linalg.norm(z1) < 1e-12
+    assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
+    for hh in hs:
+        hh.close()
+    B1.close()
+
+
 @pytest.mark.parametrize('case,P,rep', [('bidomain', 3, 100), ('bidomain', 8, 1), ('unfused', 2, 100),
                                          ('emi_poly', 4, 100), ('bidomain2d', 5, 10), ('sell', 3, 100),
                                          ('merged', 2, 100)])
@@ -376,7 +419,8 @@ def _host_exchange_worker(rank, world, port, q, problem, kw):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother=12, Schwarz_maxlvl=0))])
+@pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother=12, Schwarz_maxlvl=0)),
+                                        ('bidomain', dict(smoother=11, coarse_scaling=1, Schwarz_type=7))])
 def test_two_processes_host_exchange(lib_built, problem, kw):
     """Two rank processes on the one GPU of the box, exchanging through the
     host-staged gloo transport (RCCL refuses two ranks on one GPU): each
@@ -397,7 +441,11 @@ def test_two_processes_host_exchange(lib_built, problem, kw):
         p.join(timeout=60)
         assert p.exitcode == 0
     s = M.problems.emi(3, 16, 1e6) if problem == 'emi' else M.problems.bidomain(3, 16, 1e6)
-    okw = {'smoother': 'POLY', 'Schwarz_maxlvl': 0} if kw else {}
+    okw = {}
+    if kw.get('smoother') == 12:
+        okw = {'smoother': 'POLY', 'Schwarz_maxlvl': 0}
+    elif kw.get('smoother') == 11:
+        okw = {'smoother': 'SGS', 'coarse_scaling': 1, 'Schwarz_type': 7}
     A = s.scipy()
     h = mo.setup(A, mo.Params(num_functions=2, **okw), idofs=s.idofs)
     r = mo.seeded_rhs(s.N)
