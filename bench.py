@@ -402,6 +402,9 @@ def main():
     descr = ('level-0 residual r = b - A0 x', 'level-0 prolongation + post-smoothing '
              + ('z = x1 + W r1 + K e, K = P - W (A P)' if post_mode == 'k'
                 else 'z = x1 + P e + W (r1 - (AP) e)'))
+    if args.smoother in ('sgs', 'gs'):     # the smoothing class is the colour sweeps
+        names = (names[0], 'gs2_kernel<VL,SYM>, one launch per colour')
+        descr = (descr[0], 'level-0 multicolour node-block %s sweeps (pre + post)' % args.smoother.upper())
     rooflines = []
     for c, key in ((0, 'L0_resid'), (1, 'L0_smooth_spmv')):
         if kms[c] <= 0:
