@@ -403,12 +403,12 @@ __global__ __launch_bounds__(256) void msell_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
-      c[u] = bcol[kk];
-      v[u] = SPL ? blk_any<SPL>(bval, nbs, kk) : blk<SYM>(bval, offd, kk);
+      c[u] = PROBE == 2 ? __builtin_nontemporal_load(bcol + kk) : bcol[kk];
+      v[u] = SPL ? blk_any<SPL>(bval, nbs, kk) : blk<SYM, (PROBE >= 2)>(bval, offd, kk);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)   // PROBE 1 (A/B only, wrong results): no gather, the column as the value
-      a[u] = PROBE ? double2{(double)c[u], 1.0} : xget<XFM>(x, xs, c[u]);
+      a[u] = PROBE == 1 ? double2{(double)c[u], 1.0} : xget<XFM>(x, xs, c[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool ok = j + u < j1;
@@ -3477,10 +3477,14 @@ void launch_msell(const Op& o, hipStream_t s) {
 // the level-0 K kernel (MAMG_K_VARIANT for A/Bs, read at upload and by
 // mamg_time_apply): 0 two lanes per row, chunks of 5 (default); 1 one lane
 // per row, chunks of 6 (sell2_kernel, round 2); 2 four lanes per row, chunks
-// of 3; 9 a probe without the e gathers (wrong results, timing only)
+// of 3; 4 / 5 the default with non-temporal loads of the columns and values /
+// the values only (the K stream kept from evicting the gathered e from L2);
+// 9 a probe without the e gathers (wrong results, timing only)
 template <int SPL>
 bool launch_kvariant(const Op& o, hipStream_t s) {
   switch (g_kvar) {
+    case 4: launch_msell<2, 5, false, false, SPL, 0, 2>(o, s); return true;
+    case 5: launch_msell<2, 5, false, false, SPL, 0, 3>(o, s); return true;
     case 1: return SPL == 2 ? (launch_msell<1, 6, false, false, SPL, 0>(o, s), true) : false;
     case 2: launch_msell<4, 3, false, false, SPL, 0>(o, s); return true;
     case 3: launch_msell<2, 5, false, false, SPL, 0>(o, s); return true;   // XCD-contiguous rows

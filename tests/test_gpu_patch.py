@@ -189,3 +189,20 @@ def test_reference_preset_metric_schwarz(lib_built, setup):
     ref = mo.pcg(A, h, r, 1e-8, 500)
     assert len(solver.residuals) == len(ref.residuals)
     assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+
+
+def test_patches_refused_on_the_csr_layout(lib_built):
+    """Node patches run only in the BSR2 layout: with seeds that leave the
+    level-0 seed blocks not node-aligned (u1 of the even nodes, u0 of the odd
+    ones, gamma = 1: a u0 dof's strongest seed neighbour is another node's),
+    the hierarchy takes the CSR layout, and both setups refuse instead of
+    running seed-block Jacobi under the patch name."""
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(2, 16, 1.0)
+    nv = s.nv
+    idofs = np.array([nv + I if I % 2 == 0 else I for I in range(nv)], np.int32)
+    for setup in ('host', 'gpu'):
+        with pytest.raises(M._lib.MamgError) as ei:
+            M.MetricAMG(s.scipy(), s.W, idofs=idofs, num_functions=2, setup=setup,
+                        Schwarz_type=M.parameters.SCHWARZ_PATCHES)
+        assert ei.value.code == -4 and 'BSR2' in str(ei.value), (setup, str(ei.value))
