@@ -487,24 +487,53 @@ __global__ __launch_bounds__(256) void seed_mark_kernel(int64_t m, const int32_t
   isseed[s] = 1;
 }
 
-// strongest seed neighbour of every non-seed dof (setup.cpp block_smoother)
+// strongest seed neighbour of every non-seed dof (setup.cpp block_smoother):
+// max |a_js| over seed columns s != j, ties to the smaller s.  Eight lanes per
+// row, each over a strided part of it, then a butterfly of the eight
+// candidates: the order (|a| desc, s asc) is total, so the result is the
+// sequential scan's in any order (NaN entries never win either way)
 __global__ __launch_bounds__(256) void best_seed_kernel(int64_t n, const int64_t* __restrict__ ptr,
                                                         const int32_t* __restrict__ col,
                                                         const double* __restrict__ val,
                                                         const uint8_t* __restrict__ isseed, int64_t* __restrict__ best) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
+  const int lane = threadIdx.x & 7;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+  double bv = -1.0;
   int64_t bs = -1;
-  if (!isseed[j]) {
-    double bv = -1.0;
-    for (int64_t k = ptr[j]; k < ptr[j + 1]; ++k) {
+  if (j < n && !isseed[j])
+    for (int64_t k = ptr[j] + lane; k < ptr[j + 1]; k += 8) {
       const int64_t s = col[k];
       if (s == j || !isseed[s]) continue;
       const double v = fabs(val[k]);
       if (v > bv || (v == bv && s < bs)) { bv = v; bs = s; }
     }
+#pragma unroll
+  for (int off = 4; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(bv, off, 8);
+    const int64_t os = __shfl_xor(bs, off, 8);
+    if (ov > bv || (ov == bv && os < bs && os >= 0)) { bv = ov; bs = os; }
   }
-  best[j] = bs;
+  if (j < n && lane == 0) best[j] = bs;
+}
+
+// fast test of the common case: every joiner's strongest seed is its own
+// node's other dof (then each seed has at most that one joiner, and the
+// blocks are node-aligned exactly as block_smoother builds them);
+// joined[I]: dofs I and nv + I form one block (needs Schwarz_mmsize >= 2)
+__global__ __launch_bounds__(256) void seed_align_kernel(int64_t nv, const uint8_t* __restrict__ isseed,
+                                                         const int64_t* __restrict__ best, int mmsize,
+                                                         uint8_t* __restrict__ joined, int* bad) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  bool j = false;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t d = f * nv + I, partner = (1 - f) * nv + I;
+    if (isseed[d] || best[d] < 0) continue;
+    if (best[d] != partner) { atomicAdd(bad, 1); continue; }
+    j = j || mmsize >= 2;
+  }
+  joined[I] = j;
 }
 
 // 2x2 node-block inverse by Gauss-Jordan without pivoting (setup.cpp
@@ -1415,18 +1444,22 @@ __global__ __launch_bounds__(256) void node_wb_kernel(int64_t nv, const dv4_t* _
 }
 
 // input check (setup.cpp host_setup): monotone row pointers, columns in
-// range and strictly increasing within each row
+// range and strictly increasing within each row; eight lanes per row (a
+// wave reads its rows' columns contiguously), one flag per failing wave
 __global__ __launch_bounds__(256) void validate_kernel(int64_t n, int64_t m, const int64_t* __restrict__ ptr,
                                                        const int32_t* __restrict__ col, int* bad) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int64_t a = ptr[i], b = ptr[i + 1];
-  int nb = b < a;
-  for (int64_t k = a; k < b && !nb; ++k) {
-    const int32_t c = col[k];
-    nb |= (c < 0 || c >= m || (k > a && c <= col[k - 1]));
+  const int lane = threadIdx.x & 7;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+  int nb = 0;
+  if (i < n) {
+    const int64_t a = ptr[i], b = ptr[i + 1];
+    nb = b < a;
+    for (int64_t k = a + lane; k < b && !nb; k += 8) {
+      const int32_t c = col[k];
+      nb |= (c < 0 || c >= m || (k > a && c <= col[k - 1]));
+    }
   }
-  if (nb) atomicAdd(bad, 1);
+  if (__any(nb) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1901,7 +1934,7 @@ int seed_blocks_dev(const DevMat& A, const int32_t* idofs, int64_t n_idofs, int 
   HIPCHK(hipMemset(isowner, 0, n));
   HIPCHK(hipMemset(bad, 0, sizeof(int)));
   seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
-  best_seed_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
+  best_seed_kernel<<<nblk(8 * n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
   best_key_kernel<<<nblk(n), 256>>>(n, best, key, idx);
   HIPCHK(hipGetLastError());
   int hb = 0;
@@ -1921,6 +1954,34 @@ int seed_blocks_dev(const DevMat& A, const int32_t* idofs, int64_t n_idofs, int 
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(B->bptr, B->bptr, B->nb + 1, nullptr, err));
   return dsort_pairs_i32_i64(key, skey, idx, B->mem, n, bits_for(B->nb), nullptr, err);
+}
+
+// the node-aligned fast path of the seed blocks: *aligned and joined[] set
+// when every joiner joins its own node's other dof (seed_align_kernel)
+int seed_align_fast(const DevMat& A, int64_t nv, const int32_t* idofs, int64_t n_idofs, int mmsize, Scratch* S,
+                    uint8_t* joined, bool* aligned, std::string* err) {
+  const int64_t n = A.n;
+  int32_t* di = nullptr;
+  uint8_t* isseed = nullptr;
+  int64_t* best = nullptr;
+  int* bad = nullptr;
+  RCHK(S->alloc(&di, n_idofs, err));
+  RCHK(S->alloc(&isseed, n, err));
+  RCHK(S->alloc(&best, n, err));
+  RCHK(S->alloc(&bad, 2, err));
+  HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(isseed, 0, n));
+  HIPCHK(hipMemset(bad, 0, 2 * sizeof(int)));
+  seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
+  best_seed_kernel<<<nblk(8 * n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
+  seed_align_kernel<<<nblk(nv), 256>>>(nv, isseed, best, mmsize, joined, bad + 1);
+  HIPCHK(hipGetLastError());
+  int hb[2] = {0, 0};
+  RCHK(to_host(hb, bad, 2, err));
+  if (hb[0]) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+  *aligned = hb[1] == 0;
+  for (void* q : {(void*)di, (void*)isseed, (void*)best, (void*)bad}) S->release(q);
+  return MAMG_OK;
 }
 
 // D = D_B^-1 as a block CSR (setup.cpp block_inverse: row i holds its
@@ -2137,7 +2198,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     int* bad = nullptr;
     RCHK(S.alloc(&bad, 1, err));
     HIPCHK(hipMemset(bad, 0, sizeof(int)));
-    validate_kernel<<<nblk(A0.n), 256>>>(A0.n, A0.m, A0.ptr, A0.col, bad);
+    validate_kernel<<<nblk(8 * A0.n), 256>>>(A0.n, A0.m, A0.ptr, A0.col, bad);
     HIPCHK(hipGetLastError());
     int hb = 0;
     RCHK(read_int(bad, &hb, err));
@@ -2194,10 +2255,15 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     if (seeds && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
       RCHK(overlap_smoother_dev(G, cur, idofs, n_idofs, p, &L.WB, err));
     } else if (seeds) {
-      SeedBlocks B;
-      RCHK(seed_blocks_dev(cur, idofs, n_idofs, p.Schwarz_mmsize, &S, &B, err));
       bool aligned = false;
-      if (nodal) {
+      SeedBlocks B;
+      if (nodal) {                  // the bidomain's case: every joiner joins its node partner
+        RCHK(galloc(G, &L.joined, nv, err));
+        RCHK(seed_align_fast(cur, nv, idofs, n_idofs, p.Schwarz_mmsize, &S, L.joined, &aligned, err));
+        if (!aligned) { G->release(L.joined); L.joined = nullptr; }
+      }
+      if (!aligned) RCHK(seed_blocks_dev(cur, idofs, n_idofs, p.Schwarz_mmsize, &S, &B, err));
+      if (nodal && !aligned) {      // general blocks that may still be node-aligned
         int* bad = nullptr;
         RCHK(S.alloc(&bad, 1, err));
         HIPCHK(hipMemset(bad, 0, sizeof(int)));
