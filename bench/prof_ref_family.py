@@ -4,6 +4,11 @@ scaling) on one GPU: level sizes, colours per level and the apply's launch
 count / time, for rocprofv3 --kernel-trace --stats.
 
     python bench/prof_ref_family.py [--nrefs 5] [--reps 5] [--coarse-dof 100]
+        [--tail-nodes N] [--op-profile]
+
+--op-profile: per (op kind, rows) event time of one eager apply and the
+coarse tail's per-op wall-clock stamps (MAMG_OP_PROFILE, MAMG_TAIL_PROFILE;
+device.hip dev_time_apply), on stderr.
 """
 import argparse
 import os
@@ -19,7 +24,11 @@ def main():
     ap.add_argument('--nrefs', type=int, default=5)
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--coarse-dof', type=int, default=100)
+    ap.add_argument('--tail-nodes', type=int, default=None)
+    ap.add_argument('--op-profile', action='store_true')
     args = ap.parse_args()
+    if args.tail_nodes is not None:
+        os.environ['MAMG_TAIL_NODES'] = str(args.tail_nodes)
     import torch
     import metric_amg_examples_amd as M
     n = M.problems.finest_n(3, args.nrefs)
@@ -38,6 +47,13 @@ def main():
         B.apply_device(r, z)
     torch.cuda.synchronize()
     print('ms/apply %.3f' % ((time.time() - t) / args.reps * 1e3), flush=True)
+    if args.op_profile:
+        os.environ['MAMG_OP_PROFILE'] = '1'
+        os.environ['MAMG_TAIL_PROFILE'] = '1'
+        st = torch.cuda.current_stream()
+        ms, _, _ = B.time_apply(r, z, 2, 1, st)
+        torch.cuda.synchronize()
+        print('eager instrumented ms/apply %.3f' % ms, flush=True)
 
 
 if __name__ == '__main__':

@@ -4,12 +4,15 @@
     python -m metric_amg_examples_amd.drivers emi_3d -nrefs 5 -gamma 1e6 -precond metric
     python -m metric_amg_examples_amd.drivers emi_3d1d -gamma 1e4 -radius 1.0 -dump 1 -outdir D/
     python -m metric_amg_examples_amd.drivers run_solver_3d1d -infile input_metric.dat -indir D/ -outdir O/
+    torchrun --nproc-per-node 8 -m metric_amg_examples_amd.drivers emi_3d1d_sweep -n 48
 
 Each mirrors a reference script's CLI and output:
   bidomain_2d / bidomain_3d   src/bidomain_2d.py:105-278, src/bidomain_3d.py:52-220
   emi_2d / emi_3d             src/emi_2d.py:133-263, src/emi_3d.py:60-196
   emi_3d1d                    src/emi_3d1d.py:99-167 (dump / solve)
   run_solver_3d1d             src/run_solver_3d1d.py:17-38 (HAZmath file-based solve)
+  emi_3d1d_sweep              run_emi_3d1d.sh:5-17 (radius x gamma loop), its
+                              independent solves sharded over the ranks
 Mesh loops: n = 2^i for i in [5, 5+nrefs) (bidomain 2-D), [3, 3+nrefs)
 (bidomain 3-D), [6, 6+nrefs) (EMI 2-D), [2, 2+nrefs) (EMI 3-D).  Every solve
 appends the reference's iters row ``ndofs niters cond timeKSP r h``
@@ -262,6 +265,117 @@ def run_solver_3d1d(argv):
                                       os.path.abspath(args.outdir) + '/')
 
 
+# ---- the 3D-1D sweep (BASELINE config 5) on N GPUs --------------------------
+# run_emi_3d1d.sh:5-17 loops radius x gamma and runs one independent
+# assemble -> setup -> PCG per pair.  Those solves are the sweep's units: on N
+# GPUs every rank takes units k with k % N == rank (one process per GPU, no
+# data-path collective; the 117 K-row system is far too small to row-partition
+# profitably), and rank 0 gathers the rows (one all_gather_object over gloo at
+# the end) and writes them in the script's loop order.
+SWEEP_RADII = (0.0, 0.2, 1.0, 5.0)                      # run_emi_3d1d.sh:5
+SWEEP_GAMMAS = (1e0, 1e2, 1e4, 1e6, 1e8, 1e10)          # run_emi_3d1d.sh:7
+HEADERS_SWEEP = ['radius', 'gamma', 'ndofs', 'niters', 'timeKSP', 'relres', 'levels', 'rank']
+
+
+def sweep_units(radii=SWEEP_RADII, gammas=SWEEP_GAMMAS):
+    """(radius, gamma) pairs in the script's loop order (radius outer)."""
+    return [(float(r), float(g)) for r in radii for g in gammas]
+
+
+def shard_units(units, rank: int, world: int):
+    """The units of one rank: (index, unit) for index % world == rank."""
+    if not 0 <= rank < world:
+        raise ValueError('rank %d outside world %d' % (rank, world))
+    return [(k, u) for k, u in enumerate(units) if k % world == rank]
+
+
+def solve_3d1d_unit(n: int, radius: float, gamma: float, params=None, device=None,
+                    tol: float = 1e-6, maxiter: int = 1000) -> dict:
+    """One unit of the sweep: assemble (problems.emi_3d1d), metric-AMG setup
+    seeded at the 1D dofs, PCG stopped on ||r|| / ||b|| (the .dat file's
+    stop type 1, src/input_metric.dat:54) -- src/emi_3d1d.py:99-167 with
+    run_solver_3d1d's solve.  timeKSP = setup + PCG."""
+    s = problems.emi_3d1d(n, gamma, radius)
+    A = s.scipy()
+    b = problems.seeded_rhs(s.N)
+    t0 = time.time()
+    kw = {} if device is None else dict(device=device)
+    B = MetricAMG(A, s.W, idofs=s.idofs, parameters=params or P.parameters_metric_3d1d, **kw)
+    cg = ConjGrad(A, precond=B, tolerance=tol, maxiter=maxiter, stop_type=1)
+    x = cg * b
+    dt = time.time() - t0
+    xs = x.cpu().numpy() if hasattr(x, 'cpu') else np.asarray(x)
+    rel = float(np.linalg.norm(b - A @ xs) / np.linalg.norm(b))
+    row = dict(radius=radius, gamma=gamma, ndofs=int(s.N), niters=len(cg.residuals) - 1,
+               timeKSP=round(dt, 4), relres=rel, levels=B.num_levels)
+    B.close()
+    return row
+
+
+def run_sweep(units, solve, rank: int = 0, world: int = 1, gather=None):
+    """Solve this rank's shard of `units` with solve(unit) -> dict, then
+    gather every rank's rows (gather(obj) -> list over ranks, e.g.
+    torch.distributed.all_gather_object).  Returns (rows in unit order,
+    this rank's wall seconds, the max over ranks)."""
+    t0 = time.time()
+    mine = []
+    for k, u in shard_units(units, rank, world):
+        row = dict(solve(u))
+        row['rank'] = rank
+        mine.append((k, row))
+    wall = time.time() - t0
+    parts = [(mine, wall)] if gather is None else gather((mine, wall))
+    rows = sorted((kr for part, _ in parts for kr in part), key=lambda kr: kr[0])
+    if [k for k, _ in rows] != list(range(len(units))):
+        raise RuntimeError('sweep gather lost or duplicated units: %s' % [k for k, _ in rows])
+    return [r for _, r in rows], wall, max(w for _, w in parts)
+
+
+def emi_3d1d_sweep(argv):
+    ap = argparse.ArgumentParser(prog='emi_3d1d_sweep')
+    ap.add_argument('-n', type=int, default=48, help='cells per direction of the tissue cube')
+    ap.add_argument('-radii', type=str, default=','.join(map(str, SWEEP_RADII)))
+    ap.add_argument('-gammas', type=str, default=','.join('%g' % g for g in SWEEP_GAMMAS))
+    ap.add_argument('-results', type=str, default='./results')
+    args, _ = ap.parse_known_args(argv)
+    import json
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    gather = None
+    device = None
+    import torch
+    if torch.cuda.is_available():
+        device = local % torch.cuda.device_count()
+        torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('gloo')   # one gather of the result rows at the end
+
+        def gather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+    units = sweep_units([float(v) for v in args.radii.split(',')], [float(v) for v in args.gammas.split(',')])
+    rows, _, wall = run_sweep(units, lambda u: solve_3d1d_unit(args.n, u[0], u[1], device=device),
+                              rank, world, gather)
+    if rank == 0:
+        rdir = os.path.join(args.results, 'emi_3d1d')
+        os.makedirs(rdir, exist_ok=True)
+        path = os.path.join(rdir, 'iters_sweep_n%d.txt' % args.n)
+        for k, r in enumerate(rows):
+            _append(path, [r[h] for h in HEADERS_SWEEP], k == 0, HEADERS_SWEEP)
+            print('emi_3d1d radius=%g gamma=%g ndofs=%d niters=%d timeKSP=%.3fs relres=%.2e (rank %d)'
+                  % (r['radius'], r['gamma'], r['ndofs'], r['niters'], r['timeKSP'], r['relres'], r['rank']),
+                  flush=True)
+        print(json.dumps({'sweep': 'emi_3d1d', 'n': args.n, 'units': len(units), 'ranks': world,
+                          'wall_s': round(wall, 3), 'solves_per_s': round(len(units) / wall, 3),
+                          'niters': [r['niters'] for r in rows]}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    return rows
+
+
 COMMANDS = {
     'bidomain_2d': lambda a: bidomain(a, 2),
     'bidomain_3d': lambda a: bidomain(a, 3),
@@ -269,6 +383,7 @@ COMMANDS = {
     'emi_3d': lambda a: emi(a, 3),
     'emi_3d1d': emi_3d1d,
     'run_solver_3d1d': run_solver_3d1d,
+    'emi_3d1d_sweep': emi_3d1d_sweep,
 }
 
 

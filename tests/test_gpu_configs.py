@@ -211,3 +211,70 @@ def test_emi_3d1d_gamma_sweep(lib_built, radius):
         H.close()
     assert max(its.values()) < 200
     assert max(its.values()) <= 3 * min(its.values()), its
+
+
+def _sweep_worker(rank, world, port, q):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, 'oracle')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import metric_amg_examples_amd.drivers as D
+
+        def gather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        torch.cuda.set_device(0)
+        units = D.sweep_units([0.0, 1.0], [1.0, 1e4, 1e8])
+        rows, _, _ = D.run_sweep(units, lambda u: D.solve_3d1d_unit(16, u[0], u[1], device=0), rank, world, gather)
+        q.put((rank, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_emi_3d1d_sweep_two_processes(lib_built):
+    """BASELINE config 5 on N ranks (drivers.emi_3d1d_sweep): the radius x
+    gamma solves of run_emi_3d1d.sh:5-17 sharded over two processes on the
+    GPU (units k % 2), rows gathered over gloo.  Every unit's PCG iteration
+    count equals the oracle's (the host setup's hierarchy run by the C cycle,
+    PCG stopped on ||r|| / ||b|| < 1e-6) and its true relative residual is
+    below the tolerance."""
+    import socket
+    import torch.multiprocessing as mp
+    M = _M()
+    import metric_amg_examples_amd.drivers as D
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = [ctx.Process(target=_sweep_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    units = D.sweep_units([0.0, 1.0], [1.0, 1e4, 1e8])
+    rows = res[0]
+    assert [(r['radius'], r['gamma']) for r in rows] == units
+    assert [r['rank'] for r in rows] == [k % 2 for k in range(len(units))]
+    P = M.parameters
+    for (radius, g), row in zip(units, rows):
+        s = M.problems.emi_3d1d(16, g, radius)
+        A = s.scipy()
+        b = M.problems.seeded_rhs(s.N)
+        H = M.HostHierarchy(A, idofs=s.idofs, parameters=P.parameters_metric_3d1d)
+        ch = c_hierarchy(H, A)
+        _, n_or = _relres_pcg(A, ch.apply, b, 1e-6, 1000)
+        H.close()
+        say('sweep radius', radius, 'gamma', g, 'rank', row['rank'], 'its', row['niters'], 'oracle', n_or)
+        assert row['niters'] == n_or
+        assert row['relres'] <= 1e-6
