@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--coarse-dof', type=int, default=100)
     ap.add_argument('--tail-nodes', type=int, default=None)
     ap.add_argument('--op-profile', action='store_true')
+    ap.add_argument('--timeline', action='store_true', help='with --op-profile: every tail op')
     args = ap.parse_args()
     if args.tail_nodes is not None:
         os.environ['MAMG_TAIL_NODES'] = str(args.tail_nodes)
@@ -49,7 +50,7 @@ def main():
     print('ms/apply %.3f' % ((time.time() - t) / args.reps * 1e3), flush=True)
     if args.op_profile:
         os.environ['MAMG_OP_PROFILE'] = '1'
-        os.environ['MAMG_TAIL_PROFILE'] = '1'
+        os.environ['MAMG_TAIL_PROFILE'] = '2' if args.timeline else '1'
         st = torch.cuda.current_stream()
         ms, _, _ = B.time_apply(r, z, 2, 1, st)
         torch.cuda.synchronize()

@@ -30,10 +30,10 @@ __global__ void step_kernel(int iters, double* __restrict__ g, const int* __rest
   for (int i = t; i < 4096; i += blockDim.x) sx[i] = 0.0;
   __syncthreads();
   double* fp = flatsel ? sx : g;   // generic pointer: LDS or global by a runtime flag
-  const uint64_t t0 = wall_clock64();
+  const uint64_t t0 = wall_clock64(), c0 = clock64();
   double acc = 0.0;
   for (int it = 0; it < iters; ++it) {
-    const int i = (t + it * 7) % n;
+    const int i = (int)(((long long)t * 131 + (long long)it * 1031) % n);
     if (MODE == 1) sx[i] += 1.0;
     if (MODE == 2) g[i] += 1.0;
     if (MODE == 3) { const int c = idx[i]; acc += val[i] * g[c]; if (t == 0) g[n + (it & 63)] = acc; }
@@ -42,8 +42,8 @@ __global__ void step_kernel(int iters, double* __restrict__ g, const int* __rest
     if (MODE == 6) g[i] = (double)it;
     __syncthreads();
   }
-  const uint64_t t1 = wall_clock64();
-  if (t == 0) out[0] = t1 - t0;
+  const uint64_t t1 = wall_clock64(), c1 = clock64();
+  if (t == 0) { out[0] = t1 - t0; out[1] = c1 - c0; }
   if (acc == 12345.0) g[0] = acc;
 }
 
@@ -53,22 +53,24 @@ double run(int threads, int iters, double* g, int* idx, double* val, uint64_t* o
   CK(hipDeviceSynchronize());
   step_kernel<MODE><<<1, threads>>>(iters, g, idx, val, out, n, flatsel);
   CK(hipDeviceSynchronize());
-  uint64_t ticks = 0;
-  CK(hipMemcpy(&ticks, out, 8, hipMemcpyDeviceToHost));
-  return ticks * 10.0 / iters;   // 100 MHz -> ns per iteration
+  uint64_t ticks[2] = {0, 0};
+  CK(hipMemcpy(ticks, out, 16, hipMemcpyDeviceToHost));
+  if (MODE == 3) printf("[shader clock during mode 3: %.0f MHz] ", 100.0 * ticks[1] / ticks[0]);
+  return ticks[0] * 10.0 / iters;   // 100 MHz -> ns per iteration
 }
 
-int main() {
-  const int n = 2048, iters = 20000;
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? std::atoi(argv[1]) : 2048, iters = 20000;
   double *g, *val;
   int* idx;
   uint64_t* out;
   CK(hipMalloc(&g, (n + 64) * sizeof(double)));
   CK(hipMalloc(&val, n * sizeof(double)));
   CK(hipMalloc(&idx, n * sizeof(int)));
-  CK(hipMalloc(&out, 8));
+  CK(hipMalloc(&out, 16));
   std::vector<int> hi(n);
-  for (int i = 0; i < n; ++i) hi[i] = (i * 97 + 13) % n;
+  for (int i = 0; i < n; ++i) hi[i] = (int)(((long long)i * 97 + 13) % n);
+  printf("working set: %d doubles + %d ints (%.1f KB)\n", n, n, n * 12.0 / 1024);
   CK(hipMemcpy(idx, hi.data(), n * sizeof(int), hipMemcpyHostToDevice));
   CK(hipMemset(g, 0, (n + 64) * sizeof(double)));
   CK(hipMemset(val, 0, n * sizeof(double)));

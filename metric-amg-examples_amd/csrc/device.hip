@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <numeric>
 #include <vector>
 
@@ -964,7 +965,16 @@ __global__ __launch_bounds__(256) void gs2_kernel(
 // W-cycle (HEM ratio ~4, levels visited 2^l times, one launch per colour)
 // this replaces tens of thousands of ~5 us launches per apply.
 // ---------------------------------------------------------------------------
-enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7 };
+enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7,
+             T_COPY = 8 };
+// LDS residency (tail_lds_plan): the program itself and every work vector of
+// the tail levels live in the workgroup's LDS for the whole launch; a vector
+// field of a TOp then holds (byte offset in the dynamic LDS) | 1 instead of a
+// global pointer (doubles are 8-aligned, so bit 0 tags it), resolved per op.
+// T_COPY ops at the ends move the vectors read before written in, and the
+// written ones out.  The colour steps' dependent chain becomes LDS op
+// descriptor (scalar loads) -> global (L2) row pointers, columns, values ->
+// LDS x gathers.
 struct TOp {
   int kind = 0, epi = 0, vl = 1, sym = 0;
   int64_t n = 0, r0 = 0, r1 = 0, nb = 0;
@@ -979,25 +989,92 @@ struct TOp {
 };
 constexpr int TAIL_THREADS = 1024;
 
+template <class T>
+__device__ __forceinline__ T* tail_res(T* p, char* lds) {
+  const uintptr_t u = (uintptr_t)p;
+  return (u & 1) ? reinterpret_cast<T*>(lds + (u & ~(uintptr_t)1)) : p;
+}
+__device__ __forceinline__ TOp tail_resolve(const TOp& a, char* lds) {
+  TOp o = a;
+  o.x = tail_res(a.x, lds);
+  o.y = tail_res(a.y, lds);
+  o.b = tail_res(a.b, lds);
+  o.out = tail_res(a.out, lds);
+  o.part = tail_res(a.part, lds);
+  return o;
+}
+
 // rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
 // vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place
 __device__ void tail_bsr(const TOp& o, bool gs) {
-  const int VL = o.vl;
+  // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
+  // a 64-bit division per row chunk cost more than the chunk's loads
+  const int VL = o.vl, lvl = 31 - __builtin_clz(VL);
   const int lane = threadIdx.x & (VL - 1);
-  const int64_t rows = gs ? o.r1 - o.r0 : o.n;
+  const int rows = (int)(gs ? o.r1 - o.r0 : o.n);
+  const int row0 = gs ? (int)o.r0 : 0;
   const double* offd = o.sym ? o.val + 2 * o.nb : nullptr;
   const double2* x2 = reinterpret_cast<const double2*>(o.x);
-  for (int64_t base = 0; base < rows * VL; base += TAIL_THREADS) {   // uniform trip count
-    const int64_t v = base + threadIdx.x;
-    const int64_t node = (gs ? o.r0 : 0) + v / VL;
-    const bool live = v / VL < rows;
+  for (int base = 0; base < (rows << lvl); base += TAIL_THREADS) {   // uniform trip count
+    const int v = base + (int)threadIdx.x;
+    const int node = row0 + (v >> lvl);
+    const bool live = (v >> lvl) < rows;
     double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
-    if (live) {
-      const int64_t p0 = o.ptr[node], p1 = o.ptr[node + 1];
-      for (int64_t kb0 = p0; kb0 < p1; kb0 += 2 * VL) {
-        const int64_t ka = kb0 + lane, kb = ka + VL;
+    // GS: the row's own operands loaded before the block loop (its latency
+    // overlaps the gathers; x(I) is not written by this colour step's other rows)
+    // every lane issues its row's pointer, permutation and block-inverse
+    // loads together, branch-free (a dead lane reads row row0 and drops it),
+    // so they form one round trip instead of a chain behind a branch
+    const int nodec = live ? node : row0;
+    const int p0 = (int)o.ptr[nodec], p1 = live ? (int)o.ptr[nodec + 1] : p0;
+    int gI = -1;
+    dv4 gd = {0.0, 0.0, 0.0, 0.0};
+    if (gs) {
+      gI = live ? o.perm[nodec] : -1;
+      gd = o.W[nodec];
+    }
+    const int gIc = gI >= 0 ? gI : 0;
+    double gb0 = 0.0, gb1 = 0.0;
+    double2 gx = {0.0, 0.0};
+    if (gs) {
+      gb0 = o.b[2 * gIc];
+      gb1 = o.b[2 * gIc + 1];
+      gx = x2[gIc];
+    }
+    if (p1 > p0) {
+      // the first two chunks: all column and value loads issued before any
+      // gather, so a row of up to 4 VL blocks is one load -> gather round trip
+      {
+        int kk[4], ll[4];
+        bool hh[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          kk[q] = p0 + lane + q * VL;
+          hh[q] = kk[q] < p1;
+          ll[q] = hh[q] ? kk[q] : p1 - 1;
+        }
+        int32_t cc[4];
+        dv4 vv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          cc[q] = o.col[ll[q]];
+          vv[q] = o.sym ? blk<true>(o.val, offd, ll[q]) : blk<false>(o.val, nullptr, ll[q]);
+        }
+        double2 xa[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xa[q] = x2[cc[q]];
+#pragma unroll
+        for (int q = 0; q < 4; q += 2) {
+          s0 += hh[q] ? vv[q].x * xa[q].x + vv[q].y * xa[q].y : 0.0;
+          s1 += hh[q] ? vv[q].z * xa[q].x + vv[q].w * xa[q].y : 0.0;
+          t0 += hh[q + 1] ? vv[q + 1].x * xa[q + 1].x + vv[q + 1].y * xa[q + 1].y : 0.0;
+          t1 += hh[q + 1] ? vv[q + 1].z * xa[q + 1].x + vv[q + 1].w * xa[q + 1].y : 0.0;
+        }
+      }
+      for (int kb0 = p0 + 4 * VL; kb0 < p1; kb0 += 2 * VL) {
+        const int ka = kb0 + lane, kb = ka + VL;
         const bool ha = ka < p1, hb = kb < p1;
-        const int64_t la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
+        const int la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
         const int32_t c0 = o.col[la], c1 = o.col[lb];
         const dv4 v0 = o.sym ? blk<true>(o.val, offd, la) : blk<false>(o.val, nullptr, la);
         const dv4 v1 = o.sym ? blk<true>(o.val, offd, lb) : blk<false>(o.val, nullptr, lb);
@@ -1016,13 +1093,10 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     }
     if (!live || lane != 0) continue;
     if (gs) {
-      if (o.perm[node] < 0) continue;
-      const int64_t I = o.perm[node];
-      const double r0 = o.b[2 * I] - s0, r1 = o.b[2 * I + 1] - s1;
-      const dv4 d = o.W[node];
-      const double2 xi = x2[I];
-      o.out[2 * I] = xi.x + (d.x * r0 + d.y * r1);
-      o.out[2 * I + 1] = xi.y + (d.z * r0 + d.w * r1);
+      if (gI < 0) continue;
+      const double r0 = gb0 - s0, r1 = gb1 - s1;
+      o.out[2 * gI] = gx.x + (gd.x * r0 + gd.y * r1);
+      o.out[2 * gI + 1] = gx.y + (gd.z * r0 + gd.w * r1);
       continue;
     }
     double o0, o1;
@@ -1048,12 +1122,24 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
   }
 }
 
-__global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ prog, int nops) {
+// STAMP: thread 0 records the 100 MHz wall clock at the start and after every
+// op's barrier (stamps[0..nops]; MAMG_TAIL_PROFILE diagnosis, dev_time_apply)
+// dynamic LDS: the tail levels' work vectors (tail_lds_plan)
+extern __shared__ double tail_lds[];
+
+template <bool STAMP>
+__global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ gprog, int nops,
+                                                           uint64_t* __restrict__ stamps) {
   __shared__ double red[TAIL_THREADS / 64][2];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  char* lds = reinterpret_cast<char*>(tail_lds);
+  if (STAMP && t == 0) stamps[0] = wall_clock64();
   for (int k = 0; k < nops; ++k) {
-    const TOp o = prog[k];
+    const TOp o = tail_resolve(gprog[k], lds);   // uniform: scalar loads
     switch (o.kind) {
+      case T_COPY:
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
+        break;
       case T_BSR: tail_bsr(o, false); break;
       case T_GS: tail_bsr(o, true); break;
       case T_BD:
@@ -1070,7 +1156,18 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       case T_ZERO:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = 0.0;
         break;
-      case T_GEMV:   // gemv_kernel: one wave per row
+      case T_GEMV:   // gemv_kernel: one wave per row; small: one thread per row
+        if (o.n <= TAIL_THREADS) {   // no shuffle tree on the dependent chain
+          if (t < o.n) {
+            const double* a = o.w + (int64_t)t * o.n;
+            double s0 = 0.0, s1 = 0.0;
+            int j = 0;
+            for (; j + 1 < (int)o.n; j += 2) { s0 += a[j] * o.x[j]; s1 += a[j + 1] * o.x[j + 1]; }
+            if (j < (int)o.n) s0 += a[j] * o.x[j];
+            o.out[t] = s0 + s1;
+          }
+          break;
+        }
         for (int64_t row0 = 0; row0 < o.n; row0 += TAIL_THREADS / 64) {
           const int64_t row = row0 + wave;
           double sum = 0.0;
@@ -1083,8 +1180,15 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           if (row < o.n && lane == 0) o.out[row] = sum;
         }
         break;
-      case T_DOT2:   // dot2_partial_kernel's SCALE_BLOCKS blocks, four at a time
-        for (int vb0 = 0; vb0 < SCALE_BLOCKS; vb0 += TAIL_THREADS / 256) {
+      case T_DOT2: {   // dot2_partial_kernel's SCALE_BLOCKS blocks, four at a time
+        // blocks past the data hold (0 + 0) + (0 + 0) = +0.0 in the launch
+        // path: written directly, so only the blocks with rows loop and sync
+        const int nbl = (int)std::min<int64_t>(SCALE_BLOCKS, (o.n + 255) / 256);
+        for (int i = nbl + t; i < SCALE_BLOCKS; i += TAIL_THREADS) {
+          o.part[2 * i] = 0.0;
+          o.part[2 * i + 1] = 0.0;
+        }
+        for (int vb0 = 0; vb0 < nbl; vb0 += TAIL_THREADS / 256) {
           const int vb = vb0 + (t >> 8), tt = t & 255;
           double a = 0.0, c = 0.0;
           for (int64_t i = (int64_t)vb * 256 + tt; i < o.n; i += (int64_t)SCALE_BLOCKS * 256) {
@@ -1098,7 +1202,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           }
           if (lane == 0) { red[wave][0] = a; red[wave][1] = c; }
           __syncthreads();
-          if (tt == 0) {
+          if (tt == 0 && vb < nbl) {
             const int w0 = (t >> 8) * 4;
             o.part[2 * vb] = (red[w0][0] + red[w0 + 1][0]) + (red[w0 + 2][0] + red[w0 + 3][0]);
             o.part[2 * vb + 1] = (red[w0][1] + red[w0 + 1][1]) + (red[w0 + 2][1] + red[w0 + 3][1]);
@@ -1106,6 +1210,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           __syncthreads();
         }
         break;
+      }
       case T_CSCALE: {   // cscale_kernel: alpha from the partials (one block's order), then scale
         __shared__ double alpha;
         if (t < 256) {
@@ -1132,6 +1237,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       default: break;
     }
     __syncthreads();   // the next op reads what this one wrote (workgroup-scope visibility)
+    if (STAMP && t == 0) stamps[k + 1] = wall_clock64();
   }
 }
 
@@ -1617,6 +1723,7 @@ int64_t g_sell_min_rows = 1 << 20;
 int64_t g_msell_min_rows = (int64_t)1 << 40;
 int64_t g_tail_nodes = 4096;
 bool g_tail_set = false;   // MAMG_TAIL_NODES given: applies to every smoother (tests)   // off: coarse levels 0.41 -> 0.50 ms
+int g_tail_vl = 4;           // lanes per row cap inside the coarse tail (MAMG_TAIL_VL; 1/2/4/8/64 measured)
 void read_kvar() {
   const char* e = std::getenv("MAMG_K_VARIANT");
   g_kvar = e ? std::atoi(e) : 0;
@@ -1634,6 +1741,8 @@ void read_knobs() {
   e = std::getenv("MAMG_TAIL_NODES");
   g_tail_nodes = e ? std::atoll(e) : 4096;
   g_tail_set = e != nullptr;
+  e = std::getenv("MAMG_TAIL_VL");
+  g_tail_vl = e ? std::max(1, std::min(64, std::atoi(e))) : 4;
   e = std::getenv("MAMG_MSELL_MIN_ROWS");
   g_msell_min_rows = e ? std::atoll(e) : ((int64_t)1 << 40);
   e = std::getenv("MAMG_HALF");
@@ -1837,7 +1946,7 @@ struct DeviceHandle {
   int tail_level = 0;
   std::vector<double> kregion_ms;  // select_k_region: K ms per candidate region, the one kept
   int kregion_best = -1;
-  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; };
+  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; };
   mutable std::vector<TailProg> tails;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
@@ -3202,7 +3311,7 @@ bool to_tail(const Op& o, TOp* t) {
       const DBsr& M = *o.Mb;
       if (M.sell || M.half || M.split || o.xs || o.bs || o.os || o.xfm || M.lanes < 1 || M.lanes > 64) return false;
       t->kind = o.kind == OP_GS ? T_GS : T_BSR;
-      t->epi = o.epi; t->vl = M.lanes; t->sym = M.sym ? 1 : 0; t->n = M.nr; t->nb = M.nb;
+      t->epi = o.epi; t->vl = std::min(M.lanes, g_tail_vl); t->sym = M.sym ? 1 : 0; t->n = M.nr; t->nb = M.nb;
       t->ptr = M.ptr; t->col = M.col; t->val = M.val;
       t->x = o.kind == OP_GS ? o.out : o.x; t->y = o.y; t->b = o.b; t->W = o.W; t->out = o.out;
       t->r0 = o.r0; t->r1 = o.r1; t->perm = o.perm;
@@ -3224,6 +3333,100 @@ bool to_tail(const Op& o, TOp* t) {
 void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
                    int64_t os, std::vector<Op>* ops, bool tail_ok = true);
 
+static_assert(sizeof(TOp) % 8 == 0, "TOp is copied into LDS as 8-byte words");
+constexpr int64_t TAIL_LDS_MAX = 160 * 1024 - 1024;   // gfx950: 160 KB per workgroup, minus the static arrays
+
+// LDS residency of a coarse-tail program (see T_COPY): every work vector of
+// levels >= l the program touches gets an LDS slot; the fields are rewritten
+// to tagged LDS offsets, vectors read before written are copied in first and
+// written ones copied out last.  Returns the dynamic LDS bytes, or 0 (program
+// unchanged: global vectors) when the plan exceeds the LDS.
+int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
+  if (const char* e = std::getenv("MAMG_TAIL_LDS"))
+    if (std::atoi(e) == 0) return 0;
+  struct Vec {
+    double* base;
+    int64_t n;
+    bool used = false, in = false, out = false, seen = false, lds = false;
+    int64_t off = 0, uses = 0;
+  };
+  std::vector<Vec> vecs;
+  for (size_t ll = l; ll < h->L.size(); ++ll) {
+    const DLevel& L = h->L[ll];
+    for (double* v : {L.b, L.x, L.t, L.t2, L.r, L.c, L.e, L.q})
+      if (v) vecs.push_back({v, L.n});
+    if (L.part2) vecs.push_back({L.part2, 2 * SCALE_BLOCKS});
+  }
+  auto find = [&](const double* p) -> Vec* {
+    for (auto& v : vecs)
+      if (p >= v.base && p < v.base + v.n) return &v;
+    return nullptr;
+  };
+  auto touch = [&](const double* p, bool write) {
+    Vec* v = find(p);
+    if (!v) return;
+    v->used = true;
+    ++v->uses;
+    if (!v->seen && !write) v->in = true;
+    v->seen = true;
+    if (write) v->out = true;
+  };
+  for (const TOp& o : *prog) {   // reads of an op before its writes
+    const bool rmw = o.kind == T_GS || o.kind == T_AXPY || o.kind == T_CSCALE;
+    for (const double* r : {o.x, o.y, o.b}) if (r) touch(r, false);
+    if (o.part) touch(o.part, o.kind != T_CSCALE ? true : false);
+    if (o.out) { if (rmw) touch(o.out, false); touch(o.out, true); }
+  }
+  // the most-used bytes first (the deepest levels: small and visited most
+  // often) until the LDS is full; the rest stay global
+  std::vector<Vec*> order;
+  for (auto& v : vecs)
+    if (v.used) order.push_back(&v);
+  std::stable_sort(order.begin(), order.end(),
+                   [](const Vec* a, const Vec* b) { return a->uses * b->n > b->uses * a->n; });
+  int64_t off = 0;
+  for (Vec* v : order) {
+    const int64_t sz = (v->n * 8 + 15) / 16 * 16;
+    if (off + sz > TAIL_LDS_MAX) continue;
+    v->lds = true;
+    v->off = off;
+    off += sz;
+  }
+  if (off == 0) return 0;
+  auto tag = [&](const double* p) -> double* {
+    Vec* v = find(p);
+    if (!v || !v->lds) return const_cast<double*>(p);
+    return reinterpret_cast<double*>((uintptr_t)(v->off + 8 * (p - v->base)) | 1);
+  };
+  for (TOp& o : *prog) {
+    o.x = tag(o.x); o.y = tag(o.y); o.b = tag(o.b); o.out = tag(o.out); o.part = tag(o.part);
+  }
+  std::vector<TOp> full;
+  for (const auto& v : vecs)
+    if (v.lds && v.in) {
+      TOp c;
+      c.kind = T_COPY; c.n = v.n; c.x = v.base; c.out = reinterpret_cast<double*>((uintptr_t)v.off | 1);
+      full.push_back(c);
+    }
+  full.insert(full.end(), prog->begin(), prog->end());
+  for (const auto& v : vecs)
+    if (v.lds && v.out) {
+      TOp c;
+      c.kind = T_COPY; c.n = v.n; c.x = reinterpret_cast<double*>((uintptr_t)v.off | 1); c.out = v.base;
+      full.push_back(c);
+    }
+  prog->swap(full);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)tail_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TAIL_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)tail_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)TAIL_LDS_MAX);
+    attr = true;
+  }
+  return off;
+}
+
 // the cycle of level l and everything below as one tail_kernel launch; the
 // device op list is built once per (b, x) and kept on the handle
 bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
@@ -3239,6 +3442,7 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       if (!to_tail(sub[k], &prog[k])) return false;
       bytes += sub[k].bytes;
     }
+    const int64_t lds = tail_lds_plan(h, l, &prog);
     void* d = nullptr;
     if (hipMalloc(&d, prog.size() * sizeof(TOp)) != hipSuccess) { (void)hipGetLastError(); return false; }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
@@ -3246,11 +3450,12 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       (void)hipFree(d);
       return false;
     }
-    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes});
+    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds});
     tp = &h->tails.back();
   }
   Op o;
   o.kind = OP_TAIL; o.cls = C_COARSE; o.prog = tp->prog; o.n = tp->n; o.bytes = tp->bytes;
+  o.r0 = tp->lds;   // dynamic LDS bytes (0: the program reads global vectors)
   ops->push_back(o);
   return true;
 }
@@ -3689,7 +3894,7 @@ void launch(const Op& o, hipStream_t s) {
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
       break;
     case OP_TAIL:
-      if (o.n) tail_kernel<<<1, TAIL_THREADS, 0, s>>>(o.prog, (int)o.n);
+      if (o.n) tail_kernel<false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
       break;
     case OP_CSCALE:
       if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
@@ -3921,17 +4126,19 @@ void set_k_split(DBsr& K, int mode) {
 // SELL-stored K (tests), MAMG_K_LAYOUT=split|block switches level 0 at
 // mamg_time_apply (A/Bs on one upload).
 // the coarse tail (tail_kernel) takes over from the first level with at most
-// MAMG_TAIL_NODES node rows (0 = off); a coarsest level alone stays a launch
-// and not for the multicolour GS smoothers: a colour step is latency-bound on
-// one CU as much as across the chip, and the reference family's W-cycle ran
-// 80 -> 120 ms per apply with the tail at 4096 nodes (Jacobi V-cycle: 3.495 ->
-// 3.462 ms; bench/tail_ab.py)
+// MAMG_TAIL_NODES node rows (0 = off; default 4096, and 1024 for the
+// multicolour GS smoothers, whose colour steps cost ~2 us each inside the
+// tail as well); a coarsest level alone stays a launch.  Measured at nrefs=6
+// (bench/tail_ab.py): the reference family's W-cycle
+// 186.8 -> 166-168 ms per apply at 1024 nodes (168-188 at 4096), the Jacobi
+// V-cycle 3.69 -> 3.52-3.57 ms at 4096.
 void set_tail_level(DeviceHandle* h) {
   h->tail_level = 0;
-  if (!h->bsr || g_tail_nodes <= 0 || (gs_smoother(h->p) && !g_tail_set)) return;
+  const int64_t nodes = g_tail_set ? g_tail_nodes : (gs_smoother(h->p) ? 1024 : g_tail_nodes);
+  if (!h->bsr || nodes <= 0) return;
   for (int l = 1; l < (int)h->L.size(); ++l) {
     if (h->L[l].coarsest) return;
-    if (h->L[l].n / 2 <= g_tail_nodes) { h->tail_level = l; return; }
+    if (h->L[l].n / 2 <= nodes) { h->tail_level = l; return; }
   }
 }
 
@@ -4543,6 +4750,57 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         kernel_ms[ops[inst[ii]].cls] += t / reps;
         q += 2;
       }
+  }
+  if (mode == 1 && std::getenv("MAMG_OP_PROFILE")) {
+    // diagnosis: event time per (op kind, rows) summed over one apply
+    std::map<std::pair<int, int64_t>, std::pair<int, double>> acc;
+    q = 2;
+    for (int rp = 0; rp < reps; ++rp)
+      for (size_t ii = 0; ii < inst.size(); ++ii) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, ev[q], ev[q + 1]));
+        const Op& o = ops[inst[ii]];
+        auto& a = acc[{o.kind, o.Mb ? o.Mb->nr : (o.M ? o.M->n : o.n)}];
+        a.first += 1;
+        a.second += t;
+        q += 2;
+      }
+    for (const auto& kv : acc)
+      std::fprintf(stderr, "[mamg op] kind %d rows %lld launches/apply %.1f ms/apply %.4f us/launch %.2f\n",
+                   kv.first.first, (long long)kv.first.second, kv.second.first / (double)reps,
+                   kv.second.second / reps, 1e3 * kv.second.second / kv.second.first);
+  }
+  if (std::getenv("MAMG_TAIL_PROFILE")) {
+    // diagnosis: wall-clock stamps after every op of each coarse-tail program
+    for (const auto& tp : h->tails) {
+      std::vector<TOp> prog(tp.n);
+      std::vector<uint64_t> st(tp.n + 1);
+      uint64_t* dst = nullptr;
+      HIPCHK(hipMalloc(&dst, (tp.n + 1) * sizeof(uint64_t)));
+      HIPCHK(hipMemcpy(prog.data(), tp.prog, tp.n * sizeof(TOp), hipMemcpyDeviceToHost));
+      for (int rep = 0; rep < 2; ++rep)
+        tail_kernel<true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(st.data(), dst, (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      (void)hipFree(dst);
+      std::map<std::pair<int, int64_t>, std::pair<int, double>> acc;
+      for (int k = 0; k < tp.n; ++k) {
+        auto& a = acc[{prog[k].kind, prog[k].n}];
+        a.first += 1;
+        a.second += (double)(st[k + 1] - st[k]) * 0.01;   // 100 MHz ticks -> us
+      }
+      std::fprintf(stderr, "[mamg tail] program of %d ops: %.1f us\n", tp.n, (double)(st[tp.n] - st[0]) * 0.01);
+      if (std::atoi(std::getenv("MAMG_TAIL_PROFILE")) > 1)
+        for (int k = 0; k < tp.n; ++k)
+          std::fprintf(stderr, "[mamg tail op] %d kind %d n %lld rows [%lld, %lld) vl %d lds %d us %.2f\n", k,
+                       prog[k].kind, (long long)prog[k].n, (long long)prog[k].r0, (long long)prog[k].r1,
+                       prog[k].vl, (int)(((uintptr_t)prog[k].x | (uintptr_t)prog[k].out) & 1),
+                       (double)(st[k + 1] - st[k]) * 0.01);
+      for (const auto& kv : acc)
+        std::fprintf(stderr, "[mamg tail] kind %d rows %lld ops %d us %.1f us/op %.3f\n", kv.first.first,
+                     (long long)kv.first.second, kv.second.first, kv.second.second,
+                     kv.second.second / kv.second.first);
+    }
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   return MAMG_OK;
