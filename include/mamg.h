@@ -61,8 +61,10 @@ enum {                                                          /* smoother   */
 };
 enum {                                                   /* aggregation_type  */
   MAMG_VMB = 1, MAMG_MIS = 2, MAMG_MWM = 3, MAMG_HEC = 4, MAMG_HEM = 5
-};  /* accepted: MIS (deterministic parallel MIS-2) and HEM (parallel heavy-edge
-       matching); VMB/MWM/HEC -> MAMG_ERR_UNSUPPORTED */
+};  /* accepted: MIS (deterministic parallel MIS-2), HEM (parallel heavy-edge
+       matching) and VMB (sequential Vanek-Mandel-
+       Brezina, host setup only: mamg_setup_gpu returns MAMG_ERR_UNSUPPORTED);
+       MWM/HEC -> MAMG_ERR_UNSUPPORTED */
 enum {                                                   /* Schwarz_type      */
   /* The reference's names (src/amg_parameters.py:83-87, src/utils.py:84):
    * multiplicative Schwarz on the OVERLAPPING blocks seed + Schwarz_maxlvl
@@ -105,7 +107,7 @@ typedef struct mamg_params {
   int32_t coarse_dof;        /* 100                                          */
   int32_t coarse_solver;     /* 32 -> dense direct                           */
   int32_t coarse_scaling;    /* MAMG_OFF | MAMG_ON: e <- <b_c,e>/<A_c e,e> e  */
-  int32_t aggregation_type;  /* MAMG_MIS (parallel MIS-2) | MAMG_HEM          */
+  int32_t aggregation_type;  /* MAMG_MIS (parallel MIS-2) | MAMG_HEM | MAMG_VMB */
   double strong_coupled;     /* SoC threshold theta, 0.0                     */
   int32_t max_aggregation;   /* accepted, unused by MIS-2 (documented)       */
   int32_t amli_degree;       /* accepted, unused (no AMLI cycle)             */

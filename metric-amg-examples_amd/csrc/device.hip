@@ -2043,6 +2043,12 @@ int adopt_csr(DeviceHandle* h, const DevMat& M, DCsr* D, int lanes, std::string*
 // ~15-block level-0 rows: 1.87 ms vs 2.00 ms at VL = 4, bench/spmv_micro.hip)
 int pick_lanes_bsr(int64_t nr, int64_t nb) {
   const double avg = nr ? (double)nb / (double)nr : 1.0;
+  if (const char* e = std::getenv("MAMG_BSR_LANES_X")) {   // A/B: lanes = x * avg, power of two
+    const double want = std::atof(e) * avg;
+    int l = 2;
+    while (l < 64 && 2 * l <= want) l *= 2;
+    return l;
+  }
   int l = 2;
   while (l < 64 && 2.0 * (2 * l) <= 2.0 * avg) l *= 2;
   return l;

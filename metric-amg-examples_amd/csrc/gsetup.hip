@@ -2182,6 +2182,10 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     *err = "GPU setup covers num_functions 1 and 2; use the host setup (mamg_setup) for other profiles";
     return MAMG_ERR_UNSUPPORTED;
   }
+  if (p.aggregation_type == MAMG_VMB) {   // sequential by definition (setup.cpp aggregate_vmb)
+    *err = "aggregation_type VMB (sequential Vanek-Mandel-Brezina) runs on the host setup (mamg_setup)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   const bool nodal = nf == 2;
   if (A0.n != A0.m || A0.n <= 0 || A0.n % nf) {
     *err = "A must be square with a size divisible by num_functions";

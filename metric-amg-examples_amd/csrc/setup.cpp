@@ -289,6 +289,57 @@ int aggregate_mis2(const CsrView& A, const Strength& S, int level,
 }
 
 // ---------------------------------------------------------------------------
+// Vanek-Mandel-Brezina aggregation (oracle aggregate_vmb): sequential, index
+// order.  Phase 1: a non-isolated node whose strong neighbourhood is all
+// free starts an aggregate {i} + N(i).  Phase 2: every other non-isolated
+// node joins the phase-1 aggregate of its strongest weighted neighbour
+// (ties: smallest aggregate id).  The reference's parameters_standard and
+// 3D-1D .dat select it (src/amg_parameters.py:16,36, src/input_metric.dat:89).
+// ---------------------------------------------------------------------------
+int aggregate_vmb(const CsrView& A, const Strength& S, int level,
+                  std::vector<int64_t>* agg_out, int64_t* nagg_out, std::string* err) {
+  (void)level;
+  const int64_t n = A.n;
+  std::vector<int64_t>& agg = *agg_out;
+  agg.assign(n, -1);
+  std::vector<uint8_t> nonisol(n, 0);
+  int64_t nagg = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    bool any = false, taken = false;
+    for_strong(A, S, i, [&](int64_t j) {
+      any = true;
+      taken = taken || agg[j] >= 0;
+    });
+    nonisol[i] = any;
+    if (!any || agg[i] >= 0 || taken) continue;
+    agg[i] = nagg;
+    for_strong(A, S, i, [&](int64_t j) { agg[j] = nagg; });
+    ++nagg;
+  }
+  std::vector<int64_t> agg1(agg);
+  int bad = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : bad)
+  for (int64_t i = 0; i < n; ++i) {
+    if (!nonisol[i] || agg1[i] >= 0) continue;
+    double bw = -1.0;
+    int64_t ba = -1;
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
+      if (!S.flag[k]) continue;
+      const double w = std::fabs(A.val[k]) * 1.0;
+      if (w == 0.0) continue;
+      const int64_t a = agg1[A.col[k]];
+      if (a < 0) continue;
+      if (w > bw || (w == bw && a < ba)) { bw = w; ba = a; }
+    }
+    if (ba < 0) bad++;
+    agg[i] = ba;
+  }
+  if (bad) { *err = "VMB aggregation left a non-isolated node unassigned"; return MAMG_ERR_SETUP; }
+  *nagg_out = nagg;
+  return MAMG_OK;
+}
+
+// ---------------------------------------------------------------------------
 // parallel heavy-edge matching aggregation (oracle aggregate_hem / hem_match)
 // ---------------------------------------------------------------------------
 constexpr int HEM_PASSES = 2, HEM_MAX_ROUNDS = 64;
@@ -949,9 +1000,10 @@ int check_params(const mamg_params& p, std::string* err) {
     *err = "multicolour GS/SGS smoothers are node-block smoothers: num_functions 2 and node_block_smoother 1";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (p.aggregation_type != MAMG_MIS && p.aggregation_type != MAMG_HEM) {
-    *err = "aggregation_type must be MIS (deterministic parallel MIS-2) or HEM (parallel heavy-edge matching): "
-           "VMB/HEC/MWM are not implemented (parameters.to_gpu_profile maps a HAZmath dict explicitly)";
+  if (p.aggregation_type != MAMG_MIS && p.aggregation_type != MAMG_HEM && p.aggregation_type != MAMG_VMB) {
+    *err = "aggregation_type must be MIS (deterministic parallel MIS-2), HEM (parallel heavy-edge matching) or "
+           "VMB (sequential Vanek-Mandel-Brezina, host setup): HEC/MWM are not implemented "
+           "(parameters.to_gpu_profile maps a HAZmath dict explicitly)";
     return MAMG_ERR_UNSUPPORTED;
   }
   if (p.coarse_scaling != MAMG_OFF && p.coarse_scaling != MAMG_ON) { *err = "coarse_scaling must be OFF or ON"; return MAMG_ERR_ARG; }
@@ -1077,14 +1129,16 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
         Strength S;
         strength(G.view(), p.strong_coupled, &S);
         rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(G.view(), S, l, &agg, &nagg, err)
-                                            : aggregate_mis2(G.view(), S, l, &agg, &nagg, err);
+             : p.aggregation_type == MAMG_VMB ? aggregate_vmb(G.view(), S, l, &agg, &nagg, err)
+                                              : aggregate_mis2(G.view(), S, l, &agg, &nagg, err);
         if (rc) return rc;
         if (nagg == 0 || nf * nagg >= n) last = true;
       } else {
         Strength S;
         strength(cur, p.strong_coupled, &S);
         rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(cur, S, l, &agg, &nagg, err)
-                                            : aggregate_mis2(cur, S, l, &agg, &nagg, err);
+             : p.aggregation_type == MAMG_VMB ? aggregate_vmb(cur, S, l, &agg, &nagg, err)
+                                              : aggregate_mis2(cur, S, l, &agg, &nagg, err);
         if (rc) return rc;
         if (nagg == 0 || nagg >= n) last = true;
       }

@@ -7,11 +7,13 @@ values are build-defined (HAZmath's are not available here).
 * ``parameters_standard``, ``parameters_standard_schwarz``,
   ``parameters_metric``, ``parameters_metric_schwarz``: the reference's
   presets with their values verbatim.  ``MetricAMG`` runs what they select
-  (parameters_metric_schwarz: UA + parallel HEM + W-cycle + multicolour SGS
+  (parameters_standard: UA + sequential Vanek-Mandel-Brezina aggregation
+  (VMB, on the host setup) + W-cycle + multicolour SGS + coarse scaling;
+  parameters_metric_schwarz: UA + parallel HEM + W-cycle + multicolour SGS
   + coarse scaling, and on level 0 the reference's SCHWARZ_SYMMETRIC on the
   seeds' overlapping 1-ring blocks, which on a nodal system with a seed on
   every node is exactly ``SCHWARZ_PATCHES``) or raises MAMG_ERR_UNSUPPORTED
-  naming the component it lacks (VMB aggregation; SGS on scalar systems;
+  naming the component it lacks (SGS on scalar systems;
   multiplicative Schwarz on overlapping blocks of sparse seed sets); there
   is no silent substitution under these names.  ``MetricAMG(A, W, ...)``
   takes ``num_functions`` from W (equal-sized blocks) when the dict does
@@ -155,7 +157,7 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
     opt-in).  Returns (mapped dict, list of human-readable substitutions)."""
     out = dict(params)
     notes = []
-    if out.get('aggregation_type', MIS) not in (MIS, HEM):
+    if out.get('aggregation_type', MIS) not in (MIS, HEM, VMB):
         notes.append('aggregation_type %r -> MIS (deterministic parallel MIS-2)'
                      % out.get('aggregation_type'))
         out['aggregation_type'] = MIS

@@ -96,8 +96,8 @@ def get_hazmath_metric_precond_mono(A, W, bcs=None, parameters=None, interface_d
     ``parameters`` None -> the GPU profile (parameters_metric_mi355x).  A dict
     is used as given (parameters_metric_schwarz runs as the reference's
     algorithm: UA + HEM + W + SGS + scaling + node patches on level 0); a
-    component this build lacks (VMB aggregation, multiplicative Schwarz on
-    overlapping blocks of sparse seed sets) raises MamgError;
+    component this build lacks (multiplicative Schwarz on overlapping blocks
+    of sparse seed sets, MWM/HEC aggregation) raises MamgError;
     ``parameters.to_gpu_profile`` is the explicit opt-in mapping."""
     if parameters is None:
         parameters = P.parameters_metric_mi355x

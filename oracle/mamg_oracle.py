@@ -209,7 +209,7 @@ class Params:
     """Algorithm profile; keys mirror src/amg_parameters.py:67-89 names."""
     AMG_type: str = 'SA'          # 'SA' | 'UA'
     cycle_type: str = 'V'         # 'V' | 'W'
-    aggregation_type: str = 'MIS'  # 'MIS' (MIS-2) | 'HEM' (parallel heavy-edge matching, 2 passes)
+    aggregation_type: str = 'MIS'  # 'MIS' (MIS-2) | 'HEM' (parallel heavy-edge matching, 2 passes) | 'VMB'
     max_levels: int = 20
     maxit: int = 1
     smoother: str = 'JACOBI_RHO'  # 'L1DIAG' | 'JACOBI' | 'JACOBI_RHO' | 'POLY' | 'GS' | 'SGS'
@@ -440,6 +440,54 @@ def hem_match(W: sp.csr_matrix, active: np.ndarray, level: int):
             break
         mate[mutual] = choice[mutual]
     return mate
+
+
+def aggregate_vmb(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
+    """Vanek-Mandel-Brezina aggregation (aggregation_type VMB, the
+    reference's parameters_standard, src/amg_parameters.py:16,36, and the
+    3D-1D .dat file, src/input_metric.dat:89), sequential, in index order.
+    HAZmath's own VMB source is absent, so this is the
+    published algorithm (Vanek, Mandel, Brezina 1996, section 3):
+      phase 1: node i, non-isolated, with itself and every strong neighbour
+               still free -> a new aggregate {i} + N(i);
+      phase 2: every remaining non-isolated node joins the phase-1 aggregate
+               of its strong neighbour with the largest weight (|a_ij|, or
+               s_IJ for nodal aggregation; ties: smallest aggregate id).
+    Every non-isolated node left free by phase 1 has a phase-1-aggregated
+    strong neighbour (else phase 1 would have started an aggregate at it).
+    Isolated nodes: agg = -1.  `level` is unused (no random priorities)."""
+    n = S.shape[0]
+    ip, ix = S.indptr, S.indices
+    agg = np.full(n, -1, dtype=np.int64)
+    nagg = 0
+    for i in range(n):
+        if ip[i + 1] == ip[i] or agg[i] >= 0:
+            continue
+        nb = ix[ip[i]:ip[i + 1]]
+        if (agg[nb] >= 0).any():
+            continue
+        agg[i] = nagg
+        agg[nb] = nagg
+        nagg += 1
+    agg1 = agg.copy()
+    need = (np.diff(ip) > 0) & (agg1 < 0)
+    if need.any():
+        W = Wabs.multiply(S).tocsr()
+        W.sort_indices()
+        for i in np.flatnonzero(need):
+            cols = W.indices[W.indptr[i]:W.indptr[i + 1]]
+            ws = W.data[W.indptr[i]:W.indptr[i + 1]]
+            best_w, best_a = -1.0, -1
+            for j, w in zip(cols, ws):
+                a = agg1[j]
+                if w == 0.0 or a < 0:
+                    continue
+                if w > best_w or (w == best_w and a < best_a):
+                    best_w, best_a = w, a
+            if best_a < 0:
+                raise RuntimeError('aggregation left a non-isolated node unassigned')
+            agg[i] = best_a
+    return agg, nagg
 
 
 def aggregate_hem(Wabs: sp.csr_matrix, S: sp.csr_matrix, level: int):
@@ -1174,6 +1222,10 @@ def resolve_params(p: Params) -> Params:
     return p
 
 
+
+AGGREGATORS = {'MIS': aggregate_mis2, 'HEM': aggregate_hem, 'VMB': aggregate_vmb}
+
+
 def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarchy:
     p = resolve_params(params or Params())
     A = A.tocsr()
@@ -1189,11 +1241,11 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         if not last:
             if nf > 1:
                 S, Wn = node_strength(cur, nf, p.strong_coupled)
-                agg, nagg = (aggregate_hem if p.aggregation_type == 'HEM' else aggregate_mis2)(Wn, S, l)
+                agg, nagg = AGGREGATORS[p.aggregation_type](Wn, S, l)
                 last = nagg == 0 or nf * nagg >= n
             else:
                 S = strength(cur, p.strong_coupled)
-                agg, nagg = (aggregate_hem if p.aggregation_type == 'HEM' else aggregate_mis2)(abs(cur), S, l)
+                agg, nagg = AGGREGATORS[p.aggregation_type](abs(cur), S, l)
                 last = nagg == 0 or nagg >= n
         if last:
             if n > p.max_coarse_dense:

@@ -41,7 +41,7 @@ def test_params_struct_layout(lib_built):
 
 @pytest.mark.parametrize('bad,code', [
     (dict(smoother=11), -4),                 # SGS is a node-block smoother: num_functions 2
-    (dict(aggregation_type=1), -4),          # VMB rejected (HEM runs: parallel matching)
+    (dict(aggregation_type=3), -4),          # MWM rejected (MIS, HEM and VMB run)
     (dict(coarse_scaling=2), -1),
     (dict(Schwarz_type=3), -4),              # overlapping multiplicative Schwarz: nodal systems only
     (dict(num_functions=2, Schwarz_type=3, Schwarz_maxlvl=0), -4),   # seed nodes: SYMMETRIC needs SGS
@@ -100,7 +100,9 @@ def test_reference_presets_map_and_report(lib_built):
     assert ei.value.code == -4 and 'SCHWARZ_ADDITIVE' in str(ei.value)
     # explicit mapping keeps what is implemented and reports what it changes
     mapped, notes = P.to_gpu_profile(P.parameters_standard)
-    assert mapped['aggregation_type'] == P.MIS and any('VMB' in n or '1' in n for n in notes)
+    assert mapped['aggregation_type'] == P.VMB and not any('aggregation' in n for n in notes)
+    mapped_mwm, notes = P.to_gpu_profile(dict(P.parameters_standard, aggregation_type=P.MWM))
+    assert mapped_mwm['aggregation_type'] == P.MIS and any('aggregation_type' in n for n in notes)
     mapped, notes = P.to_gpu_profile(P.parameters_metric_schwarz)
     assert mapped['smoother'] == P.SMOOTHER_SGS and mapped['aggregation_type'] == P.HEM
     assert mapped['Schwarz_type'] == P.SCHWARZ_PATCHES and mapped['coarse_scaling'] == P.ON

@@ -148,7 +148,8 @@ def test_file_based_3d1d_solve(lib_built, tmp_path, radius, g):
     x = M.fileio.read_solution(str(odir / 'solution.txt'))
     assert np.linalg.norm(b - A @ x) <= 1e-6 * np.linalg.norm(b) * (1 + 1e-9)
     # the file's Schwarz (maxlvl 2, mmsize 200) -> additive overlapping rings
-    prm = mo.Params(coarse_dof=300, max_levels=30, Schwarz_mmsize=200, Schwarz_type=5, Schwarz_maxlvl=2)
+    prm = mo.Params(coarse_dof=300, max_levels=30, Schwarz_mmsize=200, Schwarz_type=5, Schwarz_maxlvl=2,
+                    aggregation_type='VMB')      # AMG_aggregation_type 1, as the file says
     h = mo.setup(A, prm, idofs=s.idofs)
     xo, it = _oracle_pcg_relres(A, h, b, 1e-6, 1000)
     assert niters == it

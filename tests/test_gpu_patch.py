@@ -148,13 +148,13 @@ def _oracle_params(d, **kw):
     return mo.Params(
         AMG_type={P.UA_AMG: 'UA', P.SA_AMG: 'SA'}[d['AMG_type']],
         cycle_type={P.V_CYCLE: 'V', P.W_CYCLE: 'W'}[d['cycle_type']],
-        aggregation_type={P.MIS: 'MIS', P.HEM: 'HEM'}[d['aggregation_type']],
+        aggregation_type={P.MIS: 'MIS', P.HEM: 'HEM', P.VMB: 'VMB'}[d['aggregation_type']],
         smoother={P.SMOOTHER_SGS: 'SGS', P.SMOOTHER_GS: 'GS', P.SMOOTHER_JACOBI_RHO: 'JACOBI_RHO'}[d['smoother']],
         max_levels=d['max_levels'], maxit=d['maxit'], relaxation=d['relaxation'],
         presmooth_iter=d['presmooth_iter'], postsmooth_iter=d['postsmooth_iter'], coarse_dof=d['coarse_dof'],
         strong_coupled=d['strong_coupled'], coarse_scaling=d['coarse_scaling'],
-        Schwarz_levels=d['Schwarz_levels'], Schwarz_mmsize=d['Schwarz_mmsize'],
-        Schwarz_maxlvl=d['Schwarz_maxlvl'], Schwarz_type=d['Schwarz_type'], **kw)
+        Schwarz_levels=d['Schwarz_levels'], Schwarz_mmsize=d.get('Schwarz_mmsize', 100),
+        Schwarz_maxlvl=d.get('Schwarz_maxlvl', 1), Schwarz_type=d.get('Schwarz_type', 4), **kw)
 
 
 @pytest.mark.parametrize('setup', ['host', 'gpu'])
@@ -189,6 +189,36 @@ def test_reference_preset_metric_schwarz(lib_built, setup):
     ref = mo.pcg(A, h, r, 1e-8, 500)
     assert len(solver.residuals) == len(ref.residuals)
     assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+
+
+def test_reference_preset_standard_vmb(lib_built):
+    """metricAMG(A, W, parameters=parameters_standard): the reference's
+    standard preset verbatim (src/amg_parameters.py:16-36: UA, sequential
+    Vanek-Mandel-Brezina aggregation, W-cycle, SGS, coarse scaling, no
+    Schwarz).  VMB is sequential, so 'auto' takes the host setup (recorded in
+    setup_path) and the GPU runs the cycle; one apply equals the oracle's
+    restatement to 1e-10, and the PCG iteration count and residuals match."""
+    M = _mamg()
+    P = M.parameters
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    B = M.metricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_standard)
+    assert B.setup_path == 'host', B.setup_path
+    assert B.effective_params['aggregation_type'] == P.VMB
+    assert B.level_format(1)['gs']
+    h = mo.setup(A, _oracle_params(P.parameters_standard, num_functions=2), idofs=s.idofs)
+    assert B.num_levels == len(h.levels)
+    r = mo.seeded_rhs(s.N)
+    zo = h.apply(r)
+    assert rel(B * r, zo) < 1e-10
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+    solver * r
+    ref = mo.pcg(A, h, r, 1e-8, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+    with pytest.raises(M._lib.MamgError) as ei:     # explicit GPU setup: refused, naming the reason
+        M.metricAMG(A, s.W, idofs=s.idofs, parameters=P.parameters_standard, setup='gpu')
+    assert ei.value.code == -4 and 'VMB' in str(ei.value)
 
 
 def test_patches_refused_on_the_csr_layout(lib_built):

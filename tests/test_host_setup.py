@@ -23,6 +23,11 @@ CASES = [
     (3, 16, 1e6, dict(num_functions=2, aggregation_type='HEM', AMG_type='UA')),
     (3, 8, 1e4, dict(num_functions=2, aggregation_type='HEM')),
     (2, 32, 1e3, dict(aggregation_type='HEM', AMG_type='UA')),
+    # sequential Vanek-Mandel-Brezina aggregation (aggregation_type VMB, the
+    # reference's parameters_standard): nodal and scalar, UA and SA, theta > 0
+    (3, 16, 1e6, dict(num_functions=2, aggregation_type='VMB', AMG_type='UA', strong_coupled=0.1)),
+    (2, 32, 1e4, dict(num_functions=2, aggregation_type='VMB')),
+    (2, 32, 1e3, dict(aggregation_type='VMB', AMG_type='UA', strong_coupled=0.1)),
 ]
 
 
@@ -35,7 +40,7 @@ def to_c(kw):
     if 'smoother' in c:
         c['smoother'] = {'JACOBI': 1, 'L1DIAG': 2, 'JACOBI_RHO': 3}[c['smoother']]
     if 'aggregation_type' in c:
-        c['aggregation_type'] = {'MIS': 2, 'HEM': 5}[c['aggregation_type']]
+        c['aggregation_type'] = {'VMB': 1, 'MIS': 2, 'HEM': 5}[c['aggregation_type']]
     return c
 
 

@@ -110,7 +110,7 @@ def test_dat_reader_and_mapping():
     prm, solver, notes = M.fileio.dat_to_parameters(d)
     P = M.parameters
     assert prm['AMG_type'] == P.SA_AMG and prm['cycle_type'] == P.V_CYCLE
-    assert prm['smoother'] == P.SMOOTHER_JACOBI_RHO and prm['aggregation_type'] == P.MIS
+    assert prm['smoother'] == P.SMOOTHER_JACOBI_RHO and prm['aggregation_type'] == P.VMB   # as the file says
     # HAZmath's multiplicative Schwarz on the 1-D seeds' 2-rings -> the
     # additive overlapping Schwarz on the same blocks
     assert prm['Schwarz_type'] == P.SCHWARZ_ADDITIVE and prm['Schwarz_mmsize'] == 200
