@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -3399,6 +3400,18 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
     off += sz;
   }
   if (off == 0) return 0;
+  static std::atomic<uint64_t> attr_devices{0};   // the attribute is set once per device
+  const int dev = h->device & 63;
+  if (!(attr_devices >> dev & 1)) {
+    if (hipFuncSetAttribute((const void*)tail_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)TAIL_LDS_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void*)tail_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)TAIL_LDS_MAX) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;                        // no large dynamic LDS: keep the global-vector program
+    }
+    attr_devices.fetch_or(1ull << dev);
+  }
   auto tag = [&](const double* p) -> double* {
     Vec* v = find(p);
     if (!v || !v->lds) return const_cast<double*>(p);
@@ -3422,14 +3435,6 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
       full.push_back(c);
     }
   prog->swap(full);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)tail_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)TAIL_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)tail_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)TAIL_LDS_MAX);
-    attr = true;
-  }
   return off;
 }
 
