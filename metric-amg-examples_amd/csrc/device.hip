@@ -2041,15 +2041,11 @@ int adopt_csr(DeviceHandle* h, const DevMat& M, DCsr* D, int lanes, std::string*
 }
 
 // lanes per node row for 2x2 blocks: ~2 blocks per lane (VL = 8 for the
-// ~15-block level-0 rows: 1.87 ms vs 2.00 ms at VL = 4, bench/spmv_micro.hip)
+// ~15-block level-0 rows: 1.87 ms vs 2.00 ms at VL = 4, bench/spmv_micro.hip;
+// round 3 at nrefs=6: 1/4, 1/2 and 2x these lanes on the coarse levels were
+// 0.419-0.527 ms vs 0.421 ms, profiles/r03_ab_coarse_lanes.txt)
 int pick_lanes_bsr(int64_t nr, int64_t nb) {
   const double avg = nr ? (double)nb / (double)nr : 1.0;
-  if (const char* e = std::getenv("MAMG_BSR_LANES_X")) {   // A/B: lanes = x * avg, power of two
-    const double want = std::atof(e) * avg;
-    int l = 2;
-    while (l < 64 && 2 * l <= want) l *= 2;
-    return l;
-  }
   int l = 2;
   while (l < 64 && 2.0 * (2 * l) <= 2.0 * avg) l *= 2;
   return l;
