@@ -1722,7 +1722,7 @@ int g_rvar = 0;
 int g_rrvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
 int64_t g_msell_min_rows = (int64_t)1 << 40;
-int64_t g_tail_nodes = 4096;
+int64_t g_tail_nodes = 0;
 bool g_tail_set = false;   // MAMG_TAIL_NODES given: applies to every smoother (tests)   // off: coarse levels 0.41 -> 0.50 ms
 int g_tail_vl = 4;           // lanes per row cap inside the coarse tail (MAMG_TAIL_VL; 1/2/4/8/64 measured)
 void read_kvar() {
@@ -1740,7 +1740,7 @@ void read_knobs() {
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
   e = std::getenv("MAMG_TAIL_NODES");
-  g_tail_nodes = e ? std::atoll(e) : 4096;
+  g_tail_nodes = e ? std::atoll(e) : 0;
   g_tail_set = e != nullptr;
   e = std::getenv("MAMG_TAIL_VL");
   g_tail_vl = e ? std::max(1, std::min(64, std::atoi(e))) : 4;
@@ -4133,15 +4133,17 @@ void set_k_split(DBsr& K, int mode) {
 // SELL-stored K (tests), MAMG_K_LAYOUT=split|block switches level 0 at
 // mamg_time_apply (A/Bs on one upload).
 // the coarse tail (tail_kernel) takes over from the first level with at most
-// MAMG_TAIL_NODES node rows (0 = off; default 4096, and 1024 for the
-// multicolour GS smoothers, whose colour steps cost ~2 us each inside the
-// tail as well); a coarsest level alone stays a launch.  Measured at nrefs=6
-// (bench/tail_ab.py): the reference family's W-cycle
-// 186.8 -> 166-168 ms per apply at 1024 nodes (168-188 at 4096), the Jacobi
-// V-cycle 3.69 -> 3.52-3.57 ms at 4096.
+// MAMG_TAIL_NODES node rows (0 = off).  Default: off for the Jacobi-family
+// smoothers and 1024 for the multicolour GS smoothers; a coarsest level alone
+// stays a launch.  Measured at nrefs=6 in the bench's timed loop (DESIGN.md
+// section 4.2, profiles/r03_ab_tail.txt): the Jacobi V-cycle 276.1-276.3 vs
+// 277.5-277.7 applies/s without it (2-D nrefs=6: 4601 vs 4971), because one
+// tail op costs ~2 us, more than the kernel boundary it replaces; the
+// reference family's W-cycle, whose colour steps are the launches, 196.7 ->
+// 182.5 ms per apply with it (PCG graph replay).
 void set_tail_level(DeviceHandle* h) {
   h->tail_level = 0;
-  const int64_t nodes = g_tail_set ? g_tail_nodes : (gs_smoother(h->p) ? 1024 : g_tail_nodes);
+  const int64_t nodes = g_tail_set ? g_tail_nodes : (gs_smoother(h->p) ? 1024 : 0);
   if (!h->bsr || nodes <= 0) return;
   for (int l = 1; l < (int)h->L.size(); ++l) {
     if (h->L[l].coarsest) return;

@@ -1,9 +1,9 @@
 # A/B of environment knobs on the default bench workload (one process per
 # configuration, short runs); summary lines in gpurun_out/$TAG/summary.txt
-#   bash scripts/ab_env.sh TAG "CFG1" "CFG2" ...   (CFG = space-separated VAR=value, or X=0 for the default)
+#   [BENCH_ARGS="--dim 2"] bash scripts/ab_env.sh TAG "CFG1" "CFG2" ...   (CFG = space-separated VAR=value, or X=0 for the default)
 TAG=$1; shift
 mkdir -p gpurun_out/$TAG
-L="--steps 30 --warmup 3 --cpu-sample 0 --pcg 0 --compare-profiles 0"
+L="--steps 30 --warmup 3 --cpu-sample 0 --pcg 0 --compare-profiles 0 ${BENCH_ARGS:-}"
 for cfg in "$@"; do
   env $cfg timeout -k 10 200 python -u bench.py $L > gpurun_out/$TAG/run.log 2>&1 || exit 1
   python3 -c "
