@@ -63,7 +63,7 @@ enum {                                                   /* aggregation_type  */
   MAMG_VMB = 1, MAMG_MIS = 2, MAMG_MWM = 3, MAMG_HEC = 4, MAMG_HEM = 5
 };  /* accepted: MIS (deterministic parallel MIS-2), HEM (parallel heavy-edge
        matching) and VMB (sequential Vanek-Mandel-
-       Brezina, host setup only: mamg_setup_gpu returns MAMG_ERR_UNSUPPORTED);
+       Brezina; mamg_setup_gpu runs that one step on the host);
        MWM/HEC -> MAMG_ERR_UNSUPPORTED */
 enum {                                                   /* Schwarz_type      */
   /* The reference's names (src/amg_parameters.py:83-87, src/utils.py:84):

@@ -96,7 +96,7 @@ def gpu_setup_supported(p) -> bool:
     general seed-block, overlapping-ring (SCHWARZ_ADDITIVE) and point smoothers,
     nodal or point SA (csrc/gsetup.hip).  What it still refuses at run time
     (MAMG_ERR_UNSUPPORTED) 'auto' hands to the host setup."""
-    return p.num_functions in (1, 2) and p.aggregation_type != 1   # VMB: host setup (sequential)
+    return p.num_functions in (1, 2)
 
 
 def _device_csr(A):

@@ -1777,6 +1777,37 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     return MAMG_ERR_UNSUPPORTED;
   }
   if (G->params.aggregation_type == MAMG_HEM) return aggregate_hem_dev(G, Gr, flag, level, agg_out, nagg_out, err);
+  if (G->params.aggregation_type == MAMG_VMB) {
+    // sequential by definition: the strong graph built here goes to the
+    // host, setup.cpp's aggregate_vmb (bitwise the host setup's, which
+    // builds the same graph and flags) numbers the aggregates, and they come
+    // back; every other setup step stays on the device
+    std::vector<int64_t> hptr(nv + 1);
+    std::vector<int32_t> hcol(Gr.nnz);
+    std::vector<double> hval(Gr.nnz);
+    std::vector<uint8_t> hflag(Gr.nnz);
+    RCHK(to_host(hptr.data(), Gr.ptr, nv + 1, err));
+    if (Gr.nnz) {
+      RCHK(to_host(hcol.data(), Gr.col, Gr.nnz, err));
+      RCHK(to_host(hval.data(), Gr.val, Gr.nnz, err));
+      RCHK(to_host(hflag.data(), flag, Gr.nnz, err));
+    }
+    CsrView V;
+    V.n = V.m = nv;
+    V.ptr = hptr.data();
+    V.col = hcol.data();
+    V.val = hval.data();
+    std::vector<int64_t> hagg;
+    int64_t nagg = 0;
+    int rc = aggregate_vmb_flags(V, hflag.data(), &hagg, &nagg, err);
+    if (rc) return rc;
+    int64_t* agg = nullptr;
+    RCHK(galloc(G, &agg, nv, err));
+    HIPCHK(hipMemcpy(agg, hagg.data(), nv * sizeof(int64_t), hipMemcpyHostToDevice));
+    *agg_out = agg;
+    *nagg_out = nagg;
+    return MAMG_OK;
+  }
   uint64_t *state = nullptr, *low = nullptr, *key = nullptr, *m1 = nullptr;
   unsigned long long* und = nullptr;
   RCHK(S.alloc(&state, nv, err));
@@ -2180,10 +2211,6 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
   const int nf = p.num_functions;
   if (nf != 1 && nf != 2) {
     *err = "GPU setup covers num_functions 1 and 2; use the host setup (mamg_setup) for other profiles";
-    return MAMG_ERR_UNSUPPORTED;
-  }
-  if (p.aggregation_type == MAMG_VMB) {   // sequential by definition (setup.cpp aggregate_vmb)
-    *err = "aggregation_type VMB (sequential Vanek-Mandel-Brezina) runs on the host setup (mamg_setup)";
     return MAMG_ERR_UNSUPPORTED;
   }
   const bool nodal = nf == 2;

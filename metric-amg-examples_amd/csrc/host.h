@@ -58,6 +58,13 @@ struct Hierarchy {
 };
 
 // setup.cpp
+// Vanek-Mandel-Brezina aggregation on a strength graph given as the CSR G
+// (node graph or scalar matrix; weights |val|) and one strong flag per entry
+// (symmetric pattern: no extras).  Used by the GPU setup, which builds G and
+// the flags on the device and runs this sequential step on the host.
+int aggregate_vmb_flags(const CsrView& G, const uint8_t* flag, std::vector<int64_t>* agg, int64_t* nagg,
+                        std::string* err);
+
 int host_setup(const CsrView& A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* out, std::string* err);
 mamg_params resolve_params(const mamg_params& in);

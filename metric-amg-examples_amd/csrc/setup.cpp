@@ -950,6 +950,15 @@ int smooth_prolongator_block(const CsrView& A, const Csr& T, int nf, const mamg_
 
 }  // namespace
 
+// exported for the GPU setup (host.h): VMB on a device-built strength graph
+int aggregate_vmb_flags(const CsrView& G, const uint8_t* flag, std::vector<int64_t>* agg, int64_t* nagg,
+                        std::string* err) {
+  Strength S;
+  S.flag.assign(flag, flag + G.nnz());
+  S.xptr.assign(G.n + 1, 0);
+  return aggregate_vmb(G, S, 0, agg, nagg, err);
+}
+
 // Chebyshev polynomial of degree m in W A on [hi / poly_ratio, hi], hi =
 // relaxation (a bound of lambda_max(W A): W = (relaxation / rho_B) D^-1 with
 // rho_B a Gershgorin bound), as m Richardson steps with w_k = 1 / tau_k, tau_k

@@ -8,7 +8,7 @@ values are build-defined (HAZmath's are not available here).
   ``parameters_metric``, ``parameters_metric_schwarz``: the reference's
   presets with their values verbatim.  ``MetricAMG`` runs what they select
   (parameters_standard: UA + sequential Vanek-Mandel-Brezina aggregation
-  (VMB, on the host setup) + W-cycle + multicolour SGS + coarse scaling;
+  (VMB) + W-cycle + multicolour SGS + coarse scaling;
   parameters_metric_schwarz: UA + parallel HEM + W-cycle + multicolour SGS
   + coarse scaling, and on level 0 the reference's SCHWARZ_SYMMETRIC on the
   seeds' overlapping 1-ring blocks, which on a nodal system with a seed on

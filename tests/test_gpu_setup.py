@@ -37,6 +37,10 @@ CASES = [
     (3, 16, 1e6, dict(aggregation_type=5, AMG_type=1)),
     (2, 64, 1e2, dict(aggregation_type=5)),
     (3, 16, 1e10, dict(aggregation_type=5, AMG_type=1)),
+    # sequential Vanek-Mandel-Brezina (aggregation_type VMB): the GPU setup
+    # runs this one step on the host, on the strong graph it built
+    (3, 16, 1e6, dict(aggregation_type=1, AMG_type=1, strong_coupled=0.1)),
+    (2, 64, 1e4, dict(aggregation_type=1)),
 ]
 
 
@@ -87,7 +91,7 @@ def test_gpu_setup_apply_bitwise_equals_host_setup(lib_built, dim, n, g, kw):
     if 'AMG_type' in oracle_kw:
         oracle_kw['AMG_type'] = {1: 'UA', 2: 'SA'}[oracle_kw['AMG_type']]
     if 'aggregation_type' in oracle_kw:
-        oracle_kw['aggregation_type'] = {2: 'MIS', 5: 'HEM'}[oracle_kw['aggregation_type']]
+        oracle_kw['aggregation_type'] = {1: 'VMB', 2: 'MIS', 5: 'HEM'}[oracle_kw['aggregation_type']]
     h = mo.setup(A, mo.Params(num_functions=2, **oracle_kw), idofs=s.idofs)
     r = mo.seeded_rhs(s.N)
     zo = h.apply(r)
