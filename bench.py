@@ -282,6 +282,10 @@ def main():
                           '(src/amg_parameters.py:67-89)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
                                Schwarz_type=7)),
+                         ('parameters_standard: UA + sequential Vanek-Mandel-Brezina (VMB) + W-cycle + '
+                          'multicolour SGS + coarse scaling (src/amg_parameters.py:16-36)',
+                          dict(AMG_type=1, aggregation_type=1, cycle_type=2, smoother=11, coarse_scaling=1,
+                               strong_coupled=0.1, Schwarz_type=7)),
                          ('reference family, coarse_dof 2048 (dense solve instead of the launch-bound W bottom)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
                                Schwarz_type=7, coarse_dof=2048)),

@@ -197,12 +197,15 @@ __global__ __launch_bounds__(256) void strength_kernel(int64_t n, const int64_t*
                                                        double theta, uint8_t* flag, int* nextra) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  double m = 0.0;   // the row's largest coupling: theta is relative to it
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+    if (col[k] != i) m = fmax(m, fabs(val[k]));
   for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
     const int64_t j = col[k];
     if (j == i) continue;
     const double av = fabs(val[k]);
     const double s = sqrt(d[i] * d[j]);
-    if ((av >= theta * s) && (av > 1e-12 * s)) {
+    if ((av >= theta * m) && (av > 1e-12 * s)) {
       flag[k] = 1;
       const int64_t q = dfind(ptr, col, j, i);
       if (q >= 0) flag[q] = 1;

@@ -162,14 +162,18 @@ void strength(const CsrView& A, double theta, Strength* S) {
   for (int64_t i = 0; i < n; ++i) d[i] = std::fabs(diag_of(A, i));
   std::vector<uint8_t> f0(nnz, 0);
 #pragma omp parallel for schedule(dynamic, 4096)
-  for (int64_t i = 0; i < n; ++i)
+  for (int64_t i = 0; i < n; ++i) {
+    double m = 0.0;   // the row's largest coupling (oracle strength / node_strength)
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+      if (A.col[k] != i) m = std::max(m, std::fabs(A.val[k]));
     for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
       const int64_t j = A.col[k];
       if (j == i) continue;
       const double av = std::fabs(A.val[k]);
       const double s = std::sqrt(d[i] * d[j]);
-      f0[k] = (av >= theta * s) && (av > 1e-12 * s);
+      f0[k] = (av >= theta * m) && (av > 1e-12 * s);
     }
+  }
   S->flag.assign(nnz, 0);
   std::vector<std::vector<std::pair<int32_t, int32_t>>> extra(omp_get_max_threads());
 #pragma omp parallel

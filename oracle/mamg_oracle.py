@@ -240,9 +240,23 @@ def _rowsum_seq(A: sp.csr_matrix, x: np.ndarray) -> np.ndarray:
     return A @ x
 
 
+def _offdiag_row_max(n: int, r: np.ndarray, c: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """max over j != i of v_ij per row i (0 for rows without one)."""
+    m = np.zeros(n)
+    off = r != c
+    np.maximum.at(m, r[off], v[off])
+    return m
+
+
 def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
-    """Symmetric SoC: j strong for i iff |a_ij| >= theta*sqrt(|a_ii||a_jj|)
+    """Symmetric SoC: j strong for i iff |a_ij| >= theta*max_{k != i}|a_ik|
     and |a_ij| > 1e-12*sqrt(|a_ii||a_jj|) (j != i); then S <- S | S^T.
+    The threshold is relative to the row's largest coupling, so every row
+    with a (numerically nonzero) coupling keeps a strong neighbour: measured
+    against sqrt(|a_ii||a_jj|) instead, the mass-dominated coarse levels of
+    the bidomain at gamma = 1e6 lost every connection at theta = 0.1 (the
+    reference presets' strong_coupled, src/amg_parameters.py:57,79) and the
+    hierarchy collapsed (3-D n = 128: 324-336 PCG iterations).
     Returns boolean-valued CSR (values 1.0), sorted, no diagonal."""
     n = A.shape[0]
     d = np.abs(A.diagonal())
@@ -250,7 +264,8 @@ def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
     c = A.indices
     av = np.abs(A.data)
     s = np.sqrt(d[r] * d[c])
-    strong = (r != c) & (av >= theta * s) & (av > 1e-12 * s)
+    m = _offdiag_row_max(n, r, c, av)
+    strong = (r != c) & (av >= theta * m[r]) & (av > 1e-12 * s)
     S = sp.csr_matrix((np.ones(int(strong.sum())), (r[strong], c[strong])),
                       shape=(n, n))
     S = ((S + S.T) != 0).astype(np.float64).tocsr()
@@ -308,8 +323,8 @@ def node_strength(A: sp.csr_matrix, nf: int, theta: float):
 
     s_IJ = sqrt(sum over the nf x nf block (I,J) of a^2), accumulated
     sequentially in CSR order (rows f*nv+I for f = 0..nf-1, columns sorted).
-    J strong for I iff s_IJ >= theta*sqrt(s_II s_JJ) and
-    s_IJ > 1e-12*sqrt(s_II s_JJ) (J != I); then S <- S | S^T.
+    J strong for I iff s_IJ >= theta*max_{K != I} s_IK and
+    s_IJ > 1e-12*sqrt(s_II s_JJ) (J != I); then S <- S | S^T (see strength).
     Returns (S, Wn): strong pattern (values 1.0) and the s_IJ matrix."""
     n = A.shape[0]
     nv = n // nf
@@ -326,7 +341,8 @@ def node_strength(A: sp.csr_matrix, nf: int, theta: float):
     dmask = ui == uj
     d[ui[dmask]] = s[dmask]
     sd = np.sqrt(d[ui] * d[uj])
-    strong = (ui != uj) & (s >= theta * sd) & (s > 1e-12 * sd)
+    m = _offdiag_row_max(nv, ui, uj, s)
+    strong = (ui != uj) & (s >= theta * m[ui]) & (s > 1e-12 * sd)
     S = sp.csr_matrix((np.ones(int(strong.sum())), (ui[strong], uj[strong])), shape=(nv, nv))
     S = ((S + S.T) != 0).astype(np.float64).tocsr()
     S.sort_indices()
