@@ -278,24 +278,28 @@ def main():
                          ('mi355x_sa_v (node-block Jacobi)', dict(smoother=3)),
                          ('mi355x_sgs (multicolour node-block SGS, coarse scaling ON)',
                           dict(smoother=11, coarse_scaling=1, Schwarz_type=7)),
-                         ('reference family: UA + parallel HEM + W-cycle + multicolour SGS + coarse scaling '
-                          '(src/amg_parameters.py:67-89)',
+                         ('reference family: UA + parallel HEM + W-cycle + multicolour SGS + coarse scaling, '
+                          'strong_coupled 0.1 (src/amg_parameters.py:67-89)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=7)),
+                               strong_coupled=0.1, Schwarz_type=7)),
                          ('parameters_standard: UA + sequential Vanek-Mandel-Brezina (VMB) + W-cycle + '
                           'multicolour SGS + coarse scaling (src/amg_parameters.py:16-36)',
                           dict(AMG_type=1, aggregation_type=1, cycle_type=2, smoother=11, coarse_scaling=1,
                                strong_coupled=0.1, Schwarz_type=7)),
                          ('reference family, coarse_dof 2048 (dense solve instead of the launch-bound W bottom)',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=7, coarse_dof=2048)),
+                               strong_coupled=0.1, Schwarz_type=7, coarse_dof=2048)),
                          ('mi355x_patch: the reference\'s level-0 smoother (symmetric multiplicative Schwarz on '
                           'the overlapping 1-ring node patches, SCHWARZ_PATCHES), node-block Jacobi below',
                           dict(smoother=3, Schwarz_type=6)),
                          ('reference family with its level-0 node-patch Schwarz: UA + parallel HEM + W-cycle + '
                           'SGS + coarse scaling + SCHWARZ_PATCHES, coarse_dof 2048',
                           dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                               Schwarz_type=6, coarse_dof=2048)),):
+                               strong_coupled=0.1, Schwarz_type=6, coarse_dof=2048)),
+                         ('parameters_metric_schwarz verbatim (the reference preset: UA + HEM + W + SGS + scaling + '
+                          'SCHWARZ_SYMMETRIC 1-rings = SCHWARZ_PATCHES, strong_coupled 0.1, coarse_dof 100)',
+                          dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
+                               strong_coupled=0.1, Schwarz_type=6, relaxation=1.2)),):
             if (kw['smoother'] == prof['smoother'] and kw.get('coarse_scaling', 0) == prof['coarse_scaling']
                     and kw.get('aggregation_type', 2) == 2 and kw.get('Schwarz_type', 4) == prof['Schwarz_type']):
                 continue
