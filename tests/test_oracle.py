@@ -268,3 +268,31 @@ def test_poly_halves_jacobi_iterations():
     nj = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2), idofs=s['idofs']), b).niters
     npoly = mo.pcg(A, mo.setup(A, mo.Params(num_functions=2, smoother='POLY'), idofs=s['idofs']), b).niters
     assert npoly <= 0.6 * nj, (npoly, nj)
+
+
+def test_strength_keeps_a_strong_neighbour_per_coupled_row():
+    """Strength is relative to the row's largest coupling: at theta = 0.1 (the
+    reference presets' strong_coupled) every node with a nonzero coupling
+    keeps at least its strongest neighbour, also on a mass-dominated matrix
+    (gamma = 1e10, where the couplings are far below sqrt(s_II s_JJ)); the
+    largest coupling itself is always strong, and theta = 0 keeps every one."""
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 8, 1e10)
+    A = s.scipy()
+    S, Wn = mo.node_strength(A, 2, 0.1)
+    off = Wn.copy()
+    off.setdiag(0)
+    off.eliminate_zeros()
+    coupled = np.diff(off.indptr) > 0
+    assert (np.diff(S.indptr)[coupled] > 0).all()
+    for i in np.flatnonzero(coupled)[:200]:
+        row = off.indices[off.indptr[i]:off.indptr[i + 1]]
+        j = row[np.argmax(off.data[off.indptr[i]:off.indptr[i + 1]])]
+        assert S[i, j] == 1.0
+    S0, _ = mo.node_strength(A, 2, 0.0)
+    assert S0.nnz == off.nnz
+    Ss = mo.strength(A, 0.1)
+    offs = A.copy()
+    offs.setdiag(0)
+    offs.eliminate_zeros()
+    assert (np.diff(Ss.indptr)[np.diff(offs.indptr) > 0] > 0).all()
