@@ -1977,6 +1977,18 @@ struct DeviceHandle {
 
 namespace {
 
+// MAMG_POISON=1 (tests): every double array a handle or the layout builder
+// allocates starts as NaN bytes instead of whatever the memory held, so a
+// read of a value nothing wrote shows in the result (index arrays are left
+// alone: a poisoned index would fault instead of showing)
+template <class T>
+void poison_doubles(T* p, size_t bytes) {
+  if constexpr (std::is_same<T, double>::value) {
+    const char* e = std::getenv("MAMG_POISON");
+    if (e && std::atoi(e) != 0) (void)hipMemset(p, 0xff, bytes);
+  }
+}
+
 // device allocation owned by a handle (single-GPU or multi-GPU: both keep `allocs`)
 template <class HT, class T>
 int dalloc(HT* h, T** p, int64_t count, std::string* err) {
@@ -1987,12 +1999,14 @@ int dalloc(HT* h, T** p, int64_t count, std::string* err) {
     *p = (T*)h->arena;
     h->arena += bytes;
     h->arena_left -= bytes;
+    poison_doubles(*p, bytes);
     return MAMG_OK;
   }
   void* q = nullptr;
   HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
   *p = (T*)q;
+  poison_doubles(*p, (size_t)count * sizeof(T));
   return MAMG_OK;
 }
 
@@ -2389,20 +2403,34 @@ struct TBsr {
   dv4* val = nullptr;
 };
 
-struct TmpPool {            // scoped temporaries of the layout builder
+// scoped temporaries of the layout builder.  A temporary is freed only after
+// the device has drained: the kernels reading it are queued asynchronously
+// to the host, and memory freed under a running kernel can be handed to the
+// next allocation and overwritten before that kernel has read it
+struct TmpPool {
   std::vector<void*> v;
-  ~TmpPool() { for (void* p : v) (void)hipFree(p); }
+  ~TmpPool() {
+    bool any = false;
+    for (void* p : v) any |= p != nullptr;
+    if (any) (void)hipDeviceSynchronize();
+    for (void* p : v) (void)hipFree(p);
+  }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
     void* q = nullptr;
     HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
     v.push_back(q);
     *p = (T*)q;
+    poison_doubles(*p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
     return MAMG_OK;
   }
   void release(void* p) {
     for (auto& q : v)
-      if (q == p) { (void)hipFree(q); q = nullptr; }
+      if (q == p) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(q);
+        q = nullptr;
+      }
   }
 };
 

@@ -51,14 +51,18 @@ typedef double dv4_t __attribute__((ext_vector_type(4)));
 
 namespace mamg {
 
+// buffers are freed only after the device has drained (kernels reading them
+// are queued asynchronously; freed memory can be handed to the next
+// allocation and overwritten under a kernel still reading it)
 GHier::~GHier() {
+  (void)hipDeviceSynchronize();
   for (void* p : allocs)
     if (p) (void)hipFree(p);
 }
 
 void GHier::release(void* p) {
   for (auto& q : allocs)
-    if (q == p) { (void)hipFree(q); q = nullptr; }
+    if (q == p) { (void)hipDeviceSynchronize(); (void)hipFree(q); q = nullptr; }
 }
 
 namespace {
@@ -110,7 +114,10 @@ __device__ __forceinline__ int64_t dfind(const int64_t* __restrict__ ptr, const 
 // ---------------------------------------------------------------------------
 struct Scratch {            // temporaries of one setup call
   std::vector<void*> v;
-  ~Scratch() { for (void* p : v) if (p) (void)hipFree(p); }
+  ~Scratch() {
+    (void)hipDeviceSynchronize();   // as GHier::release
+    for (void* p : v) if (p) (void)hipFree(p);
+  }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
     void* q = nullptr;
@@ -121,7 +128,7 @@ struct Scratch {            // temporaries of one setup call
   }
   void release(void* p) {
     for (auto& q : v)
-      if (q == p) { (void)hipFree(q); q = nullptr; }
+      if (q == p) { (void)hipDeviceSynchronize(); (void)hipFree(q); q = nullptr; }
   }
 };
 
