@@ -1989,6 +1989,15 @@ void poison_doubles(T* p, size_t bytes) {
   }
 }
 
+// free a device buffer once the device has drained: copies and kernels that
+// read it are asynchronous to the host, and freed memory can be handed to
+// the next allocation and overwritten under them (see TmpPool)
+inline void drained_free(void* p) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();
+  (void)hipFree(p);
+}
+
 // device allocation owned by a handle (single-GPU or multi-GPU: both keep `allocs`)
 template <class HT, class T>
 int dalloc(HT* h, T** p, int64_t count, std::string* err) {
@@ -4022,7 +4031,7 @@ void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
   const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
   auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
   if (!in_arena && it != h->allocs.end()) {
-    (void)hipFree(old);
+    drained_free(old);
     h->allocs.erase(it);
   }
 }
@@ -4092,14 +4101,14 @@ void select_k_region(DeviceHandle* h) {
   K.val = (double*)bufs[best];
   h->allocs.push_back(bufs[best]);
   for (size_t i = 0; i < bufs.size(); ++i)
-    if (i != best) (void)hipFree(bufs[i]);
+    if (i != best) drained_free(bufs[i]);
   const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
   auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
   if (!in_arena && it != h->allocs.end()) {
-    (void)hipFree(old);
+    drained_free(old);
     h->allocs.erase(it);
   }
-  (void)hipFree(out);
+  drained_free(out);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipGetLastError();
@@ -4150,7 +4159,7 @@ void set_k_split(DBsr& K, int mode) {
   if (mode == 1) split_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (dv2*)t);
   if (mode == 2) split_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (double*)t);
   if (mode) (void)hipMemcpy(K.val, t, bytes, hipMemcpyDeviceToDevice);
-  (void)hipFree(t);
+  drained_free(t);
   K.split = mode;
 }
 
@@ -4686,7 +4695,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
         auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
         if (!in_arena && it != h->allocs.end()) {
-          (void)hipFree(old);
+          drained_free(old);
           h->allocs.erase(it);
         }
         for (auto& g : h->graphs) {   // captured with the old pointer
@@ -4737,7 +4746,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
       HIPCHK(hipMemcpy(K.val, nv, (size_t)K.nbs * sizeof(dv4), hipMemcpyDeviceToDevice));
       HIPCHK(hipMemcpy(K.col, nc, (size_t)K.nbs * sizeof(int32_t), hipMemcpyDeviceToDevice));
       HIPCHK(hipMemcpy(K.soff, dsn, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
-      (void)hipFree(dsn); (void)hipFree(nv); (void)hipFree(nc);
+      drained_free(dsn); drained_free(nv); drained_free(nc);
       for (auto& g : h->graphs) { (void)hipGraphExecDestroy(g.exec); (void)hipGraphDestroy(g.graph); }
       h->graphs.clear();
     }

@@ -2566,7 +2566,11 @@ __global__ void ghost_mark_kernel(const int64_t* __restrict__ ptr, const int32_t
 
 struct DevScratch {             // plain hipMalloc buffer, freed on scope exit
   void* p = nullptr;
-  ~DevScratch() { if (p) (void)hipFree(p); }
+  ~DevScratch() {
+    if (!p) return;
+    (void)hipDeviceSynchronize();   // as GHier::release
+    (void)hipFree(p);
+  }
 };
 
 }  // namespace
