@@ -1,0 +1,117 @@
+// free_race.hip -- does hipFree wait for queued work that still reads the
+// freed buffer, and can the next allocation be written under that work?
+// (VERDICT r03 "next round" #1: the round-3 intermittent wrong operators were
+// cured by draining the device before every free; this names the mechanism.)
+//
+// Each case: T = hipMalloc(64 MB) filled with 1.0; a one-wave kernel on stream
+// S1 spins ~SPIN ms and then sums T; the host frees T at once (timing the
+// hipFree call), allocates U of the same size (same address?), writes 2.0 into
+// U by one of several paths on stream S2, drains, and reads the kernel's sum:
+// old (= n) means the kernel still saw T's data, new (= 2n) means U's write
+// landed under the running reader.
+// Build: hipcc -O3 --offload-arch=gfx950 free_race.hip -o free_race
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+__global__ void fill_kernel(double* p, int64_t n, double v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// one wave: spin `ticks` of the constant wall clock, then sum p[0..n)
+__global__ void spin_sum_kernel(const double* p, int64_t n, uint64_t ticks, double* out) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 64) s += p[i];
+  for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+enum Writer { W_H2D, W_KERNEL, W_D2D, W_MEMSET, W_H2D_ASYNC };
+static const char* wname[] = {"hipMemcpy H2D", "fill kernel", "hipMemcpy D2D", "hipMemset(0)", "hipMemcpyAsync H2D"};
+
+int main(int argc, char** argv) {
+  const double spin_ms = argc > 1 ? std::atof(argv[1]) : 200.0;
+  int rate_khz = 0;
+  CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+  const uint64_t ticks = (uint64_t)(spin_ms * rate_khz);
+  const int64_t n = 8 << 20;                       // 64 MB of doubles
+  const size_t bytes = n * sizeof(double);
+  std::vector<double> two(n, 2.0);
+  double *out, *src;
+  CK(hipMalloc(&out, sizeof(double)));
+  CK(hipMalloc(&src, bytes));
+  fill_kernel<<<(unsigned)(n / 256), 256>>>(src, n, 2.0);
+  CK(hipDeviceSynchronize());
+  hipStream_t nb1, nb2;
+  CK(hipStreamCreateWithFlags(&nb1, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&nb2, hipStreamNonBlocking));
+  std::printf("wall clock %d kHz, spin %.0f ms, buffer %zu MB\n", rate_khz, spin_ms, bytes >> 20);
+  struct Case { const char* name; hipStream_t s1, s2; Writer w; bool async_free; };
+  const Case cases[] = {
+      {"reader null, writer null", nullptr, nullptr, W_KERNEL, false},
+      {"reader null, writer null", nullptr, nullptr, W_H2D, false},
+      {"reader null, writer null", nullptr, nullptr, W_D2D, false},
+      {"reader null, writer null", nullptr, nullptr, W_MEMSET, false},
+      {"reader nonblocking, writer null", nb1, nullptr, W_KERNEL, false},
+      {"reader nonblocking, writer null", nb1, nullptr, W_H2D, false},
+      {"reader nonblocking, writer null", nb1, nullptr, W_D2D, false},
+      {"reader nonblocking, writer other nonblocking", nb1, nb2, W_KERNEL, false},
+      {"reader nonblocking, writer other nonblocking", nb1, nb2, W_H2D_ASYNC, false},
+      {"reader null, hipFreeAsync(null) then hipMallocAsync(null)", nullptr, nullptr, W_KERNEL, true},
+      {"reader nonblocking, hipFreeAsync(nb1) then hipMallocAsync(nb2)", nb1, nb2, W_KERNEL, true},
+  };
+  for (const Case& c : cases) {
+    double* T = nullptr;
+    if (c.async_free) CK(hipMallocAsync((void**)&T, bytes, c.s1));
+    else CK(hipMalloc(&T, bytes));
+    fill_kernel<<<(unsigned)(n / 256), 256, 0, c.s1>>>(T, n, 1.0);
+    CK(hipDeviceSynchronize());
+    spin_sum_kernel<<<1, 64, 0, c.s1>>>(T, n, ticks, out);
+    const double t0 = now_ms();
+    if (c.async_free) CK(hipFreeAsync(T, c.s1));
+    else CK(hipFree(T));
+    const double t1 = now_ms();
+    double* U = nullptr;
+    if (c.async_free) CK(hipMallocAsync((void**)&U, bytes, c.s2));
+    else CK(hipMalloc(&U, bytes));
+    switch (c.w) {
+      case W_KERNEL: fill_kernel<<<(unsigned)(n / 256), 256, 0, c.s2>>>(U, n, 2.0); break;
+      case W_H2D: CK(hipMemcpy(U, two.data(), bytes, hipMemcpyHostToDevice)); break;
+      case W_H2D_ASYNC: CK(hipMemcpyAsync(U, two.data(), bytes, hipMemcpyHostToDevice, c.s2)); break;
+      case W_D2D: CK(hipMemcpy(U, src, bytes, hipMemcpyDeviceToDevice)); break;
+      case W_MEMSET: CK(hipMemset(U, 0, bytes)); break;
+    }
+    const double t2 = now_ms();
+    CK(hipDeviceSynchronize());
+    const double t3 = now_ms();
+    double s = 0.0;
+    CK(hipMemcpy(&s, out, sizeof(double), hipMemcpyDeviceToHost));
+    const char* seen = s == (double)n ? "old data (safe)" : s == 2.0 * n ? "NEW data (race)"
+                       : s == 0.0 ? "NEW data (race, memset)" : "mixed (race)";
+    std::printf("%-62s %-18s free %7.2f ms | same address %d | write returned after %7.2f ms | drain %7.2f ms | reader saw %s\n",
+                c.name, wname[c.w], t1 - t0, (void*)U == (void*)T, t2 - t0, t3 - t2, seen);
+    if (c.async_free) CK(hipFreeAsync(U, c.s2));
+    else CK(hipFree(U));
+    CK(hipDeviceSynchronize());
+  }
+  return 0;
+}

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MAMG_ABI_VERSION 3
+#define MAMG_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------- */
 enum {
@@ -68,11 +68,15 @@ enum {                                                   /* aggregation_type  */
 enum {                                                   /* Schwarz_type      */
   /* The reference's names (src/amg_parameters.py:83-87, src/utils.py:84):
    * multiplicative Schwarz on the OVERLAPPING blocks seed + Schwarz_maxlvl
-   * ring.  SYMMETRIC with Schwarz_maxlvl 1 on a nodal system (num_functions
-   * 2) runs as MAMG_SCHWARZ_PATCHES (the same blocks and local solves);
-   * with Schwarz_maxlvl 0 the blocks are the seeds' nodes (no overlap) and
-   * the type must match the smoother (SYMMETRIC: SGS, FORWARD: GS).  Every
-   * other overlapping combination returns MAMG_ERR_UNSUPPORTED. */
+   * ring.  SYMMETRIC with Schwarz_maxlvl >= 1 on a nodal system
+   * (num_functions 2) runs as MAMG_SCHWARZ_PATCHES when the rings are 1-rings
+   * and every node holds a seed (the bidomain), else as MAMG_SCHWARZ_RINGS
+   * (sparse seed sets, e.g. EMI's interface); without seeds the level
+   * smoother runs everywhere (Schwarz_levels resolved to 0).  With
+   * Schwarz_maxlvl 0 the blocks are the seeds' nodes (no overlap) and the
+   * type must match the smoother (SYMMETRIC: SGS, FORWARD: GS).  FORWARD /
+   * BACKWARD on overlapping blocks and scalar systems return
+   * MAMG_ERR_UNSUPPORTED. */
   MAMG_SCHWARZ_FORWARD = 1, MAMG_SCHWARZ_BACKWARD = 2, MAMG_SCHWARZ_SYMMETRIC = 3,
   MAMG_SCHWARZ_BLOCK_JACOBI = 4, /* additive non-overlapping seed blocks (GPU) */
   MAMG_SCHWARZ_ADDITIVE = 5,     /* additive overlapping seed + maxlvl-ring blocks
@@ -87,9 +91,27 @@ enum {                                                   /* Schwarz_type      */
      the non-seed dofs that join it, <= Schwarz_mmsize): additive with the
      Jacobi family, multicolour forward with GS, symmetric with SGS (for the
      bidomain: node-block SGS on level 0) */
-  MAMG_SCHWARZ_SEED_BLOCKS = 7
+  MAMG_SCHWARZ_SEED_BLOCKS = 7,
+  /* symmetric multiplicative Schwarz on one block per seed = the seed and its
+     breadth-first Schwarz_maxlvl ring (<= Schwarz_mmsize dofs), exact local
+     solves, blocks in a greedy conflict-colour order, plus node-block GS on
+     the dofs in no block (src/utils.py:84: "the interface_dofs has the
+     Schwarz and the rest the GS smoother"): the reference's SCHWARZ_SYMMETRIC
+     for any seed set that is not one seed per node with 1-rings (EMI's
+     interface seeds, the default dict of src/utils.py:60-82); level 0, BSR2
+     layout (num_functions 2), single GPU */
+  MAMG_SCHWARZ_RINGS = 8
 };
 enum { MAMG_OFF = 0, MAMG_ON = 1 };
+enum {                                                   /* strength_measure  */
+  /* J strong for I iff |a_IJ| >= strong_coupled * (the row's largest
+   * off-diagonal |a_IK|): the default, because the classical measure below
+   * collapses the bidomain hierarchy at strong_coupled 0.1 */
+  MAMG_STRENGTH_ROWMAX = 1,
+  /* classical: |a_IJ| >= strong_coupled * sqrt(|a_II a_JJ|) (Vanek, Mandel,
+   * Brezina 1996; the measure HAZmath's aggregations are described with) */
+  MAMG_STRENGTH_DIAG = 0
+};
 enum { MAMG_COARSE_DENSE = 32 };  /* coarse_solver: 32 (UMFPACK in HAZmath)  */
 
 /* Parameter dictionary keys of /root/reference/src/amg_parameters.py:67-89
@@ -136,6 +158,9 @@ typedef struct mamg_params {
   /* MAMG_SMOOTHER_POLY: Chebyshev degree (1..8, 2) and interval ratio (16) */
   int32_t poly_degree;
   double poly_ratio;
+  /* strength of connection: MAMG_STRENGTH_ROWMAX (default) | MAMG_STRENGTH_DIAG
+   * (ABI 4) */
+  int32_t strength_measure;
 } mamg_params;
 
 /* Host CSR view (caller-owned). */
@@ -224,9 +249,13 @@ typedef struct mamg_dhandle mamg_dhandle;
 /* size of the RCCL unique id (128); rank 0 creates it, every rank passes it */
 int mamg_comm_id_bytes(void);
 int mamg_comm_unique_id(void* id);
-/* Every rank passes the same global A / idofs / params (the host setup is
- * replicated and deterministic) and uploads only its node range of each
- * level; levels with <= rep_nodes nodes are replicated.  V-cycle only. */
+/* Every rank passes the same global A / idofs / params (the setup -- on the
+ * rank's GPU where the profile allows it, else on the host -- is replicated
+ * and deterministic) and keeps only its node range of each level; levels
+ * with <= rep_nodes nodes are replicated.  V and W cycles, coarse-grid
+ * scaling, nu1 / nu2 >= 1; Jacobi-family, POLY and multicolour GS / SGS
+ * smoothers on BSR2 (nodal) hierarchies.  SCHWARZ_PATCHES / SCHWARZ_RINGS,
+ * CSR-layout hierarchies and maxit > 1 return MAMG_ERR_UNSUPPORTED. */
 int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, int rank, int nranks, const void* comm_id,
                     int64_t rep_nodes, mamg_dhandle** out);
@@ -272,13 +301,16 @@ int mamg_dist_set_exchange(mamg_dhandle* h, const mamg_exchange* ex);
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out);
 /* GPU setup: the same hierarchy as mamg_setup, bit
- * for bit, built by gfx950 kernels -- strength, MIS-2 aggregation, node-block
- * smoothers, SA prolongator, Galerkin products, coarsest inverse -- and the
- * apply layouts built in HBM (no host round trip).  Covers the nodal 2-field
- * profile (num_functions 2, node_block_smoother 1, sa_block_diag 1; level-0
- * seed blocks must be node-aligned, as the bidomain's idofs are); anything
- * else returns MAMG_ERR_UNSUPPORTED (use mamg_setup).  Replaces the setup
- * half of metricAMG.__init__ (src/utils.py:86).  A: host CSR, copied once. */
+ * for bit, built by gfx950 kernels -- strength, MIS-2 / HEM aggregation (VMB:
+ * its one sequential step on the host), smoothers, SA prolongator, Galerkin
+ * products, coarsest inverse -- and the apply layouts built in HBM (no host
+ * round trip).  Covers num_functions 1 and 2 with every smoother the host
+ * setup builds: node blocks, general (not node-aligned) seed blocks,
+ * SCHWARZ_ADDITIVE rings, SCHWARZ_PATCHES / SCHWARZ_RINGS level-0 Schwarz,
+ * point smoothers; nodal or point SA.  Other profiles (num_functions > 2, a
+ * hash SpGEMM row of more than 2048 distinct columns) return
+ * MAMG_ERR_UNSUPPORTED (use mamg_setup).  Replaces the setup half of
+ * metricAMG.__init__ (src/utils.py:86).  A: host CSR, copied once. */
 int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                    const mamg_params* params, mamg_handle** out);
 /* Same with A's rowptr/colind/values in device memory (read during setup
@@ -293,6 +325,11 @@ int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs
  * prolongator, Galerkin, coarsest, apply-layout build, setup total, A upload
  * (zeros for handles from mamg_setup / mamg_upload). */
 int mamg_setup_timings(const mamg_handle* h, double* ms8);
+/* The apply-layout phase of any handle split, ms[4]: layout build (device
+ * formats of every level), level-0 K value region trials (bounded by time and
+ * free HBM), operator re-homing, finish (tail plan,
+ * final synchronisation). */
+int mamg_layout_timings(const mamg_handle* h, double* ms4);
 
 /* Upload an existing host hierarchy (level 0 matrix taken from A). */
 int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
@@ -317,7 +354,8 @@ int mamg_device_layout(const mamg_handle* h);
 enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_POST_K = 8,
        MAMG_FMT_POST_SELL = 16, MAMG_FMT_HALF = 32, MAMG_FMT_BANDS = 64,
        MAMG_FMT_PATCHES = 128,  /* smoother: multiplicative node-patch Schwarz (SCHWARZ_PATCHES) */
-       MAMG_FMT_GS = 256 };     /* smoother: multicolour node-block GS / SGS sweeps */
+       MAMG_FMT_GS = 256,       /* smoother: multicolour node-block GS / SGS sweeps */
+       MAMG_FMT_RINGS = 512 };  /* smoother: multiplicative seed-ring Schwarz + GS on the rest (SCHWARZ_RINGS) */
 int mamg_level_format(const mamg_handle* h, int level);
 /* The parameters the handle runs (as mamg_hier_params). */
 int mamg_handle_params(const mamg_handle* h, mamg_params* out);

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('MAMG_LIB', os.path.join(_HERE, 'libmamg.so'))
 
-MAMG_ABI_VERSION = 3
+MAMG_ABI_VERSION = 4
 OK, ERR_ARG, ERR_HIP, ERR_SETUP, ERR_UNSUPPORTED, ERR_NOMEM, ERR_BREAKDOWN = 0, -1, -2, -3, -4, -5, -6
 
 
@@ -41,6 +41,7 @@ class mamg_params(C.Structure):
         ('num_functions', C.c_int32), ('node_block_smoother', C.c_int32),
         ('sa_block_diag', C.c_int32), ('post_fusion', C.c_int32),
         ('poly_degree', C.c_int32), ('poly_ratio', C.c_double),
+        ('strength_measure', C.c_int32),
     ]
 
 
@@ -110,6 +111,7 @@ SIGNATURES = {
     'mamg_gpu_host_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                                       C.POINTER(VP)]),
     'mamg_setup_timings': (C.c_int, [VP, P_F64]),
+    'mamg_layout_timings': (C.c_int, [VP, P_F64]),
     'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),
     'mamg_destroy': (None, [VP]),
     'mamg_nrows': (C.c_int64, [VP]),

@@ -190,7 +190,12 @@ class MetricAMG:
         _lib.check(self._L.mamg_setup_timings(self._h, ms))
         names = ('aggregate', 'smoother', 'prolongator', 'galerkin', 'coarsest', 'layout',
                  'setup_total', 'upload_A0')
-        return {k: round(ms[i], 3) for i, k in enumerate(names)}
+        out = {k: round(ms[i], 3) for i, k in enumerate(names)}
+        lm = (C.c_double * 4)()
+        _lib.check(self._L.mamg_layout_timings(self._h, lm))
+        for i, k in enumerate(('layout_build', 'layout_kregion', 'layout_rehome', 'layout_finish')):
+            out[k] = round(lm[i], 3)
+        return out
 
     @classmethod
     def from_host(cls, H: 'HostHierarchy', W=None):
@@ -233,7 +238,8 @@ class MetricAMG:
         _lib.check(min(f, 0))
         return {'sell': bool(f & 1), 'sym': bool(f & 2), 'post_fused': bool(f & 4),
                 'post_k': bool(f & 8), 'post_sell': bool(f & 16), 'half': bool(f & 32),
-                'bands': bool(f & 64), 'patches': bool(f & 128), 'gs': bool(f & 256)}
+                'bands': bool(f & 64), 'patches': bool(f & 128), 'gs': bool(f & 256),
+                'rings': bool(f & 512)}
 
     @property
     def kregion(self) -> dict:

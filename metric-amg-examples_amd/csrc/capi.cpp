@@ -94,7 +94,10 @@ struct Seeds {
   const int32_t* ptr = nullptr;
   int64_t n = 0;
   Seeds(const int32_t* idofs, int64_t n_idofs, int64_t N, const mamg_params* p) : ptr(idofs), n(n_idofs) {
-    if (!idofs || n_idofs <= 0 || !p || p->num_functions != 2 || N % 2) return;
+    // the seed-ring Schwarz keeps every seed: overlapping blocks, as the reference's
+    if (!idofs || n_idofs <= 0 || !p || p->num_functions != 2 || N % 2 ||
+        (p->Schwarz_type == MAMG_SCHWARZ_RINGS && p->Schwarz_levels >= 1))
+      return;
     const int64_t nv = N / 2;
     std::vector<uint8_t> seed(N, 0);
     for (int64_t t = 0; t < n_idofs; ++t)
@@ -154,6 +157,7 @@ void mamg_params_default(mamg_params* p) {
   p->post_fusion = 1;
   p->poly_degree = 2;
   p->poly_ratio = 16.0;
+  p->strength_measure = MAMG_STRENGTH_ROWMAX;
 }
 
 int mamg_gen_bidomain_size(int dim, int64_t n, int64_t* nrows, int64_t* nnz) {
@@ -197,11 +201,11 @@ int mamg_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg_hier* h = new mamg_hier();
   std::string err;
   Seeds S(idofs, n_idofs, v.n, &P);
@@ -322,11 +326,11 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     int64_t rep_nodes, mamg_dhandle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
   Seeds S(idofs, n_idofs, v.n, &P);
@@ -461,11 +465,11 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
   Seeds S(idofs, n_idofs, v.n, &P);
@@ -483,11 +487,11 @@ int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                    const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   std::string err;
   mamg::GHier G;
   G.device = P.device;
@@ -515,7 +519,7 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
     set_error("null argument");
     return MAMG_ERR_ARG;
   }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, dA->nrows);   // the reference's Schwarz names
   *out = nullptr;
   if (dA->nrows <= 0 || dA->ncols <= 0 || dA->nnz < 0 || dA->nrows > INT32_MAX || dA->ncols > INT32_MAX) {
     set_error("bad CSR sizes");
@@ -548,11 +552,11 @@ int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs
                         const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
   *out = nullptr;
   mamg::CsrView v;
   int rc = to_view(A, &v);
   if (rc) return rc;
+  const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   std::string err;
   mamg::GHier G;
   G.device = P.device;
@@ -576,11 +580,17 @@ int mamg_setup_timings(const mamg_handle* h, double* ms8) {
   return MAMG_OK;
 }
 
+int mamg_layout_timings(const mamg_handle* h, double* ms4) {
+  if (!h || !ms4) { set_error("null argument"); return MAMG_ERR_ARG; }
+  mamg::dev_layout_ms(h->d, ms4);
+  return MAMG_OK;
+}
+
 int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
                 mamg_handle** out) {
   GUARD_BEGIN
   if (!h || !out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  const mamg_params P = mamg::resolve_params(*params);   // the reference's Schwarz names
+  const mamg_params P = mamg::resolve_like(*params, h->H.params);   // as the setup resolved it
   *out = nullptr;
   mamg::CsrView v = h->H.A0;
   if (A) {

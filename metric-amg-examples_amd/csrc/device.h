@@ -19,6 +19,8 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
                    std::string* err);
 // setup phase timings of a handle built by the GPU setup (ms; zeros otherwise)
 void dev_setup_ms(const DeviceHandle* h, double* ms8);
+// apply-layout phases (ms): build, K value region trials, operator re-homing, finish
+void dev_layout_ms(const DeviceHandle* h, double* ms4);
 void dev_destroy(DeviceHandle* h);
 int64_t dev_nrows(const DeviceHandle* h);
 int dev_num_levels(const DeviceHandle* h);

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "device.h"
+#include "dmem.h"
 #include "rowstage.h"
 
 namespace mamg {
@@ -1595,6 +1596,94 @@ __global__ __launch_bounds__(256) void patch_kernel(int64_t c0, int64_t c1, cons
   }
 }
 
+// ---------------------------------------------------------------------------
+// Multiplicative seed-ring Schwarz (Schwarz_type RINGS, level 0): the
+// reference's SCHWARZ_SYMMETRIC on one block per seed = the seed and its
+// breadth-first Schwarz_maxlvl ring (src/utils.py:60-86), exact local solves.
+// Blocks of one colour share no member and read no x another one writes, so
+// a colour is one launch, one 128-thread workgroup per block:
+//   r|_k = b|_k - (A x)|_k  (one thread per member: the member's field row of
+//   A_0's node BSR2 row), then x|_k += Minv_k r|_k  (thread a: sum over c of
+//   Minv(a, c) r_c from the transposed inverse, coalesced over the threads).
+// x node-interleaved; b with field stride bs.  Oracle: mamg_oracle.Rings.sweep.
+constexpr int RING_THREADS = 128;
+__global__ __launch_bounds__(RING_THREADS) void ring_kernel(int64_t k0, const int64_t* __restrict__ mo,
+                                                         const int32_t* __restrict__ mem,
+                                                         const int64_t* __restrict__ io,
+                                                         const double* __restrict__ minvT,
+                                                         const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const dv4* __restrict__ val, double* x,
+                                                         const double* __restrict__ b, int64_t bs) {
+  __shared__ double res[RING_MAX_DOFS];
+  const int64_t k = k0 + blockIdx.x;
+  const int64_t m0 = mo[k];
+  const int d = (int)(mo[k + 1] - m0);
+  const double* T = minvT + io[k];
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  for (int a = threadIdx.x; a < d; a += RING_THREADS) {
+    const int32_t g = mem[m0 + a];
+    const int32_t I = g >> 1;
+    const int f = g & 1;
+    double s = 0.0;
+    const int64_t p1 = ptr[I + 1];
+    for (int64_t q = ptr[I]; q < p1; ++q) {
+      const dv4 v = val[q];
+      const double2 xj = x2[col[q]];
+      s += f ? v.z * xj.x + v.w * xj.y : v.x * xj.x + v.y * xj.y;
+    }
+    res[a] = vget(b, bs, I, f) - s;
+  }
+  __syncthreads();
+  for (int a = threadIdx.x; a < d; a += RING_THREADS) {
+    double dl = 0.0;
+    for (int c = 0; c < d; ++c) dl += T[(int64_t)c * d + a] * res[c];
+    x[mem[m0 + a]] += dl;
+  }
+}
+
+// block j of the colour order <- block ord[j] of ring_blocks_dev's output:
+// its inverse transposed into rinv at rio[j]
+__global__ __launch_bounds__(256) void ring_perm_inv_kernel(int64_t nb, const int32_t* __restrict__ ord,
+                                                            const int64_t* __restrict__ blen,
+                                                            const int64_t* __restrict__ sq,
+                                                            const double* __restrict__ inv,
+                                                            const int64_t* __restrict__ rio, double* __restrict__ rinv) {
+  const int64_t j = blockIdx.x;
+  if (j >= nb) return;
+  const int64_t o = ord[j], d = blen[o];
+  const double* src = inv + (o ? sq[o - 1] : 0);
+  double* dst = rinv + rio[j];
+  for (int64_t t = threadIdx.x; t < d * d; t += 256) {
+    const int64_t a = t / d, c = t - a * d;
+    dst[c * d + a] = src[t];
+  }
+}
+
+// the rest's GS (RINGS): node blocks with one covered dof become split
+// (diagonal) smoother blocks, so gs_layout inverts them as two 1x1 blocks;
+// cov[I]: bit f = dof f of node I lies in a seed block
+__global__ __launch_bounds__(256) void rest_w_kernel(int64_t nv, const dv4* __restrict__ W,
+                                                     const uint8_t* __restrict__ cov, dv4* __restrict__ Wp) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  const dv4 w = W[I];
+  const uint8_t c = cov[I];
+  Wp[I] = (c == 1 || c == 2) ? dv4{w.x, 0.0, 0.0, w.w} : w;
+}
+
+// ... and the covered dofs take no update: their rows / columns of D zeroed
+__global__ __launch_bounds__(256) void rest_mask_kernel(int64_t nr, const int32_t* __restrict__ perm,
+                                                        const uint8_t* __restrict__ cov, dv4* __restrict__ D) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nr || perm[i] < 0) return;
+  const uint8_t c = cov[perm[i]];
+  const dv4 d = D[i];
+  if (c == 3) D[i] = dv4{0.0, 0.0, 0.0, 0.0};
+  else if (c == 1) D[i] = dv4{0.0, 0.0, 0.0, d.w};
+  else if (c == 2) D[i] = dv4{d.x, 0.0, 0.0, 0.0};
+}
+
 // 2x2 Gauss-Jordan without pivoting in mamg_oracle.batched_inverse's
 // operation order (no contraction), on node I's diagonal block; the
 // off-diagonals are dropped when I's two dofs are separate smoother blocks
@@ -1859,6 +1948,19 @@ struct DLevel {
   double* pu = nullptr;
   int64_t pus = 0;
   std::vector<int64_t> pcs;
+  // level-0 seed-ring Schwarz (Schwarz_type RINGS): the blocks colour by
+  // colour (colour c = blocks [rcs[c], rcs[c + 1])), block k's members as
+  // node-interleaved dof indices 2 I + f at rmem[rmo[k] .. rmo[k + 1]), its
+  // Gauss-Jordan inverse transposed (column-major d x d) at rinv + rio[k];
+  // A_0's rows in Sptr / Scol / Sval; the rest's GS in Gb / gperm / Gd / gcs
+  // (covered dofs masked out of Gd)
+  int64_t* rmo = nullptr;
+  int32_t* rmem = nullptr;
+  int64_t* rio = nullptr;
+  double* rinv = nullptr;
+  std::vector<int64_t> rcs;
+  int64_t rnm = 0;          // members of all blocks
+  double rinv_n = 0.0;      // inverse entries of all blocks
   // coarse-grid correction scaling of the correction computed ON this level:
   // q = A_l e, partial sums of <b, e>, <q, e>
   double* q = nullptr;
@@ -1866,7 +1968,7 @@ struct DLevel {
 };
 
 enum OpKind { OP_CSR = 0, OP_SCALE = 1, OP_GEMV = 2, OP_AXPY = 3, OP_BSR = 4, OP_BD = 5, OP_POST = 6, OP_ILV = 7,
-              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11, OP_PATCH = 12, OP_TAIL = 13 };
+              OP_GS = 8, OP_ZERO = 9, OP_DOT2 = 10, OP_CSCALE = 11, OP_PATCH = 12, OP_TAIL = 13, OP_RING = 14 };
 // kernel classes (kernel_ms / class_bytes slots)
 enum Cls {
   C_L0_RESID = 0,   // dominant: r = b - A0 x (once per apply)
@@ -1957,6 +2059,7 @@ struct DeviceHandle {
   double* hres = nullptr;          // pinned host scalar
   double apply_bytes = 0.0;
   double setup_ms[8] = {};         // GPU setup phase timings (dev_from_ghier)
+  double layout_ms[4] = {};        // apply-layout phases: build, K region trials, re-homing, finish (LT_*)
   // every piece of work on the handle's scratch buffers (apply, host apply,
   // spmv, PCG, timing) waits for this event on its stream and re-records it
   // afterwards: work on one handle is serialized across streams
@@ -1977,6 +2080,8 @@ struct DeviceHandle {
 
 namespace {
 
+enum { LT_BUILD = 0, LT_KREGION = 1, LT_REHOME = 2, LT_FINISH = 3 };
+
 // MAMG_POISON=1 (tests): every double array a handle or the layout builder
 // allocates starts as NaN bytes instead of whatever the memory held, so a
 // read of a value nothing wrote shows in the result (index arrays are left
@@ -1992,11 +2097,7 @@ void poison_doubles(T* p, size_t bytes) {
 // free a device buffer once the device has drained: copies and kernels that
 // read it are asynchronous to the host, and freed memory can be handed to
 // the next allocation and overwritten under them (see TmpPool)
-inline void drained_free(void* p) {
-  if (!p) return;
-  (void)hipDeviceSynchronize();
-  (void)hipFree(p);
-}
+inline void drained_free(void* p) { free_after_drain(p, "drained_free"); }
 
 // device allocation owned by a handle (single-GPU or multi-GPU: both keep `allocs`)
 template <class HT, class T>
@@ -2419,10 +2520,7 @@ struct TBsr {
 struct TmpPool {
   std::vector<void*> v;
   ~TmpPool() {
-    bool any = false;
-    for (void* p : v) any |= p != nullptr;
-    if (any) (void)hipDeviceSynchronize();
-    for (void* p : v) (void)hipFree(p);
+    for (void* p : v) free_after_drain(p, "TmpPool::~TmpPool");
   }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
@@ -2436,8 +2534,7 @@ struct TmpPool {
   void release(void* p) {
     for (auto& q : v)
       if (q == p) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(q);
+        free_after_drain(q, "TmpPool::release");
         q = nullptr;
       }
   }
@@ -2760,6 +2857,7 @@ struct LevelSrc {
   DevMat A, P, AP, R;
   const double* W = nullptr;      // 4 nv node blocks (device)
   const double* Ainv = nullptr;   // coarsest: n x n dof order (device)
+  const std::vector<int32_t>* seeds = nullptr;   // level 0, SCHWARZ_RINGS
 };
 
 inline bool gs_smoother(const mamg_params& p) {
@@ -3075,6 +3173,105 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   return MAMG_OK;
 }
 
+inline bool rings_schwarz(const mamg_params& p) {
+  return p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_RINGS;
+}
+
+// Seed-ring Schwarz data of level 0 (Schwarz_type RINGS) from A_0's device
+// CSR S.A and node BSR2 B: the blocks and their inverses on the device
+// (ring_blocks_dev: the additive form's breadth-first rings and Gauss-Jordan
+// kernels), the greedy conflict colouring on the host (setup.cpp
+// ring_colouring, in seed order: the sequential step, as VMB's), the blocks
+// re-ordered colour by colour with their inverses transposed, A_0's plain
+// BSR2 copy for the block rows, and the rest's multicolour node-block GS with
+// the covered dofs masked out (mamg_oracle.rest_gs_inverse).
+int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, DLevel* D, std::string* err) {
+  const mamg_params& p = h->p;
+  if (!S.seeds || S.seeds->empty()) { *err = "seed rings: no seeds"; return MAMG_ERR_ARG; }
+  const int64_t n = S.A.n, nv = n / 2, ns = (int64_t)S.seeds->size();
+  RingBlocks RB;
+  int rc = ring_blocks_dev(S.A, S.seeds->data(), ns, p.Schwarz_maxlvl, p.Schwarz_mmsize, &RB, err);
+  if (rc) return rc;
+  struct Guard { RingBlocks* r; ~Guard() { ring_blocks_free(r); } } guard{&RB};
+  const int mm = RB.mm;
+  std::vector<int32_t> blk((size_t)ns * mm);
+  std::vector<int64_t> blen(ns), sq(ns);
+  HIPCHK(hipMemcpy(blk.data(), RB.blk, blk.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(blen.data(), RB.blen, ns * sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<int64_t> bptr(ns + 1, 0);
+  for (int64_t k = 0; k < ns; ++k) bptr[k + 1] = bptr[k] + blen[k];
+  std::vector<int32_t> mem(bptr[ns]);
+  for (int64_t k = 0; k < ns; ++k) std::copy(blk.begin() + k * mm, blk.begin() + k * mm + blen[k], mem.begin() + bptr[k]);
+  // A_0's pattern for the conflict graph
+  std::vector<int64_t> aptr(n + 1);
+  std::vector<int32_t> acol(S.A.nnz);
+  HIPCHK(hipMemcpy(aptr.data(), S.A.ptr, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(acol.data(), S.A.col, S.A.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+  CsrView Av;
+  Av.n = Av.m = n; Av.ptr = aptr.data(); Av.col = acol.data();
+  std::vector<int32_t> colour;
+  ring_colouring(Av, bptr, mem, &colour);
+  std::vector<int32_t>().swap(acol);
+  int ncol = 0;
+  for (int32_t c : colour) ncol = std::max(ncol, c + 1);
+  std::vector<int32_t> ord(ns);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return colour[a] < colour[b]; });
+  D->rcs.assign(ncol + 1, 0);
+  for (int32_t c : colour) D->rcs[c + 1]++;
+  for (int c = 0; c < ncol; ++c) D->rcs[c + 1] += D->rcs[c];
+  std::vector<int64_t> mo(ns + 1, 0), io(ns + 1, 0);
+  std::vector<int32_t> rm;
+  rm.reserve(mem.size());
+  std::vector<uint8_t> cov(nv, 0);
+  for (int64_t j = 0; j < ns; ++j) {
+    const int64_t o = ord[j], d = blen[o];
+    mo[j + 1] = mo[j] + d;
+    io[j + 1] = io[j] + d * d;
+    for (int64_t t = bptr[o]; t < bptr[o + 1]; ++t) {
+      const int64_t g = mem[t], I = g % nv, f = g / nv;
+      rm.push_back((int32_t)(2 * I + f));
+      cov[I] |= (uint8_t)(1u << f);
+    }
+  }
+  D->rnm = mo[ns];
+  D->rinv_n = (double)io[ns];
+  if ((rc = dalloc(h, &D->rmo, ns + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->rio, ns + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->rmem, std::max<int64_t>(D->rnm, 1), err))) return rc;
+  if ((rc = dalloc(h, &D->rinv, std::max<int64_t>(io[ns], 1), err))) return rc;
+  HIPCHK(hipMemcpy(D->rmo, mo.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(D->rio, io.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(D->rmem, rm.data(), rm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  int32_t* dord = nullptr;
+  if ((rc = T->alloc(&dord, ns, err))) return rc;
+  HIPCHK(hipMemcpy(dord, ord.data(), ns * sizeof(int32_t), hipMemcpyHostToDevice));
+  ring_perm_inv_kernel<<<(unsigned)ns, 256>>>(ns, dord, RB.blen, RB.sq, RB.inv, D->rio, D->rinv);
+  HIPCHK(hipGetLastError());
+  // A_0's block rows: plain BSR2 in node order
+  D->Snb = B.nb;
+  if ((rc = dalloc(h, &D->Sptr, B.nr + 1, err))) return rc;
+  if ((rc = dalloc(h, &D->Scol, B.nb, err))) return rc;
+  if ((rc = dalloc(h, &D->Sval, B.nb, err))) return rc;
+  HIPCHK(hipMemcpy(D->Sptr, B.ptr, (B.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->Scol, B.col, B.nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D->Sval, B.val, B.nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+  // the rest's GS: multicolour node-block GS, covered dofs masked
+  uint8_t* dcov = nullptr;
+  dv4* Wp = nullptr;
+  if ((rc = T->alloc(&dcov, nv, err))) return rc;
+  if ((rc = T->alloc(&Wp, nv, err))) return rc;
+  HIPCHK(hipMemcpy(dcov, cov.data(), nv, hipMemcpyHostToDevice));
+  rest_w_kernel<<<nblocks(nv), 256>>>(nv, reinterpret_cast<const dv4*>(S.W), dcov, Wp);
+  HIPCHK(hipGetLastError());
+  if ((rc = build_gs(h, T, B, reinterpret_cast<const double*>(Wp), 0, D, err))) return rc;
+  const int64_t nrp = D->gcs.empty() ? 0 : D->gcs.back();
+  if (nrp) rest_mask_kernel<<<nblocks(nrp), 256>>>(nrp, D->gperm, dcov, D->Gd);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());   // ring_blocks_dev's buffers are freed by the guard
+  return MAMG_OK;
+}
+
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
   DLevel& D = h->L[l];
   const mamg_params& p = h->p;
@@ -3095,10 +3292,13 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = finalize_bsr(h, &T, B, &D.Ab, lanesA, true, err, true, l == 0, l > 0)))
       return rc;
     const bool patches = l == 0 && patch_schwarz(p);
-    if (gs_smoother(p) && !patches)
+    const bool rings = l == 0 && rings_schwarz(p) && S.seeds && !S.seeds->empty();
+    if (gs_smoother(p) && !patches && !rings)
       if ((rc = build_gs(h, &T, B, S.W, l, &D, err))) return rc;
     if (patches)
       if ((rc = build_patches(h, &T, B, &D, err))) return rc;
+    if (rings)
+      if ((rc = build_rings(h, &T, B, S, &D, err))) return rc;
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
   if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
@@ -3108,7 +3308,8 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = poly_scaled(h, S.W, 4 * nv, &wk, err))) return rc;
     for (double* q : wk) D.Wk.push_back(reinterpret_cast<dv4*>(q));
   }
-  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p) && !(l == 0 && patch_schwarz(p))) {
+  if (p.post_fusion && p.postsmooth_iter >= 1 && S.AP.n == D.n && !gs_smoother(p) &&
+      !(l == 0 && (patch_schwarz(p) || rings_schwarz(p)))) {
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
@@ -3306,6 +3507,29 @@ Op patch_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int 
   const double mavg = nv > 0 ? (double)L.Snb / nv : 0.0;   // nodes per patch = blocks per row
   o.bytes = np * (8.0 * (double)L.pus + mavg * (36.0 * mavg + 8.0) + mavg * (16.0 + 32.0) + 12.0);
   return o;
+}
+
+// one colour of a seed-ring sweep: per block its transposed inverse, its
+// members' rows of A_0 (blocks + pointers), b and x read/write for its
+// members, the gathered x
+Op ring_op(const DLevel& L, int c, double* x, const double* b, int64_t bs, int cls) {
+  Op o;
+  o.kind = OP_RING; o.cls = cls; o.lev = &L;
+  o.out = x; o.b = b; o.bs = bs;
+  o.r0 = L.rcs[c]; o.r1 = L.rcs[c + 1]; o.n = o.r1 - o.r0;
+  const double nb = (double)(L.rcs.back()), frac = nb > 0 ? (double)o.n / nb : 0.0;
+  const double nv = (double)(L.n / 2), bpr = nv > 0 ? (double)L.Snb / nv : 0.0;   // blocks per node row
+  const double m = frac * (double)L.rnm;                                          // members of this colour
+  o.bytes = frac * 8.0 * L.rinv_n + m * (bpr * 36.0 + 16.0 + 4.0 + 8.0 + 16.0 + bpr * 16.0) + 16.0 * o.n;
+  return o;
+}
+
+void ring_sweep_ops(const DLevel& L, bool fwd, double* x, const double* b, int64_t bs, int cls, std::vector<Op>* ops) {
+  const int nc = (int)L.rcs.size() - 1;
+  for (int k = 0; k < nc; ++k) {
+    const int c = fwd ? k : nc - 1 - k;
+    if (L.rcs[c + 1] > L.rcs[c]) ops->push_back(ring_op(L, c, x, b, bs, cls));
+  }
 }
 
 void patch_sweep_ops(const DLevel& L, bool fwd, double* x, const double* b, int64_t bs, int cls, std::vector<Op>* ops) {
@@ -3517,11 +3741,18 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   const int clsS = l0 ? C_L0_SMOOTH : C_COARSE;
   const int clsW = l0 ? C_L0_WB : C_COARSE;
   const bool pat = L.pcs.size() > 1;                      // node-patch Schwarz on this level
-  const bool gs = L.gcs.size() > 1 || pat;                // multicolour GS on this level
-  const bool sgs = p.smoother == MAMG_SMOOTHER_SGS || pat;
+  const bool rng = L.rcs.size() > 1;                      // seed-ring Schwarz + the rest's GS
+  const bool gs = L.gcs.size() > 1 || pat || rng;         // multicolour GS on this level
+  const bool sgs = p.smoother == MAMG_SMOOTHER_SGS || pat || rng;
   auto sweep = [&](bool fwd, double* x) {
-    if (pat) patch_sweep_ops(L, fwd, x, b, bs, clsS, ops);
-    else gs_sweep_ops(L, fwd, x, b, bs, clsS, ops);
+    if (pat) {
+      patch_sweep_ops(L, fwd, x, b, bs, clsS, ops);
+    } else if (rng) {   // one symmetric step = rings fwd, rest fwd | rest bwd, rings bwd (mamg_oracle.rings_step)
+      if (fwd) { ring_sweep_ops(L, true, x, b, bs, clsS, ops); gs_sweep_ops(L, true, x, b, bs, clsS, ops); }
+      else { gs_sweep_ops(L, false, x, b, bs, clsS, ops); ring_sweep_ops(L, false, x, b, bs, clsS, ops); }
+    } else {
+      gs_sweep_ops(L, fwd, x, b, bs, clsS, ops);
+    }
   };
   const int steps = smoother_steps(p);
   const int npre = p.presmooth_iter * steps, npost = p.postsmooth_iter * steps;
@@ -3931,6 +4162,11 @@ void launch(const Op& o, hipStream_t s) {
         patch_kernel<<<(unsigned)((o.n + 3) / 4), 256, 0, s>>>(o.r0, o.r1, o.lev->pperm, o.lev->Sptr, o.lev->Scol,
                                                                 o.lev->Sval, o.lev->pu, o.lev->pus, o.out, o.b, o.bs);
       break;
+    case OP_RING:
+      if (o.n > 0)
+        ring_kernel<<<(unsigned)o.n, RING_THREADS, 0, s>>>(o.r0, o.lev->rmo, o.lev->rmem, o.lev->rio, o.lev->rinv,
+                                                          o.lev->Sptr, o.lev->Scol, o.lev->Sval, o.out, o.b, o.bs);
+      break;
     case OP_ZERO:
       if (o.n) (void)hipMemsetAsync(o.out, 0, o.n * sizeof(double), s);
       break;
@@ -4015,11 +4251,28 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // hipMalloc (the old copy is kept if both fail).  An old copy of its own
 // allocation is freed; one inside the pre-reserved arena stays (the arena is
 // one allocation).
-void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
+// a fresh allocation for a re-homed stream: physically contiguous where the
+// driver has it, plain hipMalloc otherwise.  A contiguous allocation that
+// takes longer than 50 ms (the driver compacting memory: on one round-3 box
+// the layout phase took 2.1 s against 0.23 s elsewhere) turns contiguous
+// allocations off for the rest of the process.
+bool g_contig_ok = true;
+void* placement_alloc(size_t b) {
   void* r = nullptr;
+  if (g_contig_ok) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 50.0)
+      g_contig_ok = false;
+  }
+  if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+  return r;
+}
+
+void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
   if (!*ptr || b == 0) return;
-  if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
-  if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); return; }
+  void* r = placement_alloc(b);
+  if (!r) return;
   if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipFree(r);
@@ -4053,50 +4306,66 @@ void rehome_bsr(DeviceHandle* h, DBsr& M) {
 // (4) distinct fresh allocations (physically contiguous where the driver has
 // them), K is timed in each (one warm + three launches), and the fastest
 // region is kept.  Same bytes: results are bitwise equal.
+// Bounded (round 4): candidates are tried one at a time while the search has
+// spent less than MAMG_KREGION_BUDGET_MS (200) and a quarter of the HBM stays
+// free after the next copy (a co-resident caller keeps its memory); the
+// losers are freed at the end (kept until then so that every candidate is a
+// distinct region).
 void select_k_region(DeviceHandle* h) {
   DLevel& L = h->L[0];
   DBsr& K = L.KPb;
   const size_t bytes = (size_t)K.nbs * 4 * sizeof(double);
   const char* e = std::getenv("MAMG_KREGION_TRIES");
   const int tries = e ? std::atoi(e) : 4;
+  const char* eb = std::getenv("MAMG_KREGION_BUDGET_MS");
+  const double budget = eb ? std::atof(eb) : 200.0;
   if (tries <= 1 || K.sym || !L.r || !L.t || !L.Wd || !h->L[1].x) {
     rehome_array(h, (void**)&K.val, bytes);
     return;
   }
-  std::vector<void*> bufs;
-  for (int t = 0; t < tries; ++t) {   // all allocated first: distinct regions
-    void* r = nullptr;
-    if (hipExtMallocWithFlags(&r, bytes, hipDeviceMallocContiguous) != hipSuccess) {
-      (void)hipGetLastError();
-      r = nullptr;
-      if (hipMalloc(&r, bytes) != hipSuccess) { (void)hipGetLastError(); break; }
-    }
-    bufs.push_back(r);
-  }
   double* out = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (bufs.empty() || hipMalloc(&out, L.n * sizeof(double)) != hipSuccess ||
-      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+  if (hipMalloc(&out, L.n * sizeof(double)) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess) {
     (void)hipGetLastError();
-    for (void* b : bufs) (void)hipFree(b);
     if (out) (void)hipFree(out);
     rehome_array(h, (void**)&K.val, bytes);
     return;
   }
+  const auto t0 = std::chrono::steady_clock::now();
   void* old = K.val;
   const Op op = bsr_op(K, EPI_KPOST, C_L0_SMOOTH, 0, h->L[1].x, 0, L.t, L.r, 0, L.Wd, out, L.n / 2);
-  std::vector<float> ms(bufs.size(), 1e30f);
+  std::vector<void*> bufs;
+  std::vector<float> ms;
   size_t best = 0;
-  for (size_t i = 0; i < bufs.size(); ++i) {
-    (void)hipMemcpy(bufs[i], old, bytes, hipMemcpyDeviceToDevice);
-    K.val = (double*)bufs[i];
+  for (int t = 0; t < tries; ++t) {
+    const double spent = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (t > 0 && spent > budget) break;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); break; }
+    if (fr < bytes + tot / 4) break;
+    void* r = placement_alloc(bytes);
+    if (!r) break;
+    bufs.push_back(r);
+    (void)hipMemcpy(r, old, bytes, hipMemcpyDeviceToDevice);
+    K.val = (double*)r;
     launch(op, nullptr);
     (void)hipEventRecord(e0, nullptr);
     for (int k = 0; k < 3; ++k) launch(op, nullptr);
     (void)hipEventRecord(e1, nullptr);
     (void)hipEventSynchronize(e1);
-    (void)hipEventElapsedTime(&ms[i], e0, e1);
-    if (ms[i] < ms[best]) best = i;
+    float m = 1e30f;
+    (void)hipEventElapsedTime(&m, e0, e1);
+    ms.push_back(m);
+    if (ms.back() < ms[best]) best = bufs.size() - 1;
+  }
+  if (bufs.empty()) {
+    K.val = (double*)old;
+    (void)hipFree(out);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    return;
   }
   K.val = (double*)bufs[best];
   h->allocs.push_back(bufs[best]);
@@ -4127,7 +4396,14 @@ void rehome_operators(DeviceHandle* h) {
   if (e && std::atoi(e) == 0) return;
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < g_sell_min_rows || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
+  auto lap = [t = std::chrono::steady_clock::now()]() mutable {
+    const auto n = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
+    return ms;
+  };
   select_k_region(h);            // the largest stream first, placed by measurement
+  h->layout_ms[LT_KREGION] = lap();
   rehome_array(h, (void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
   if (L.Ab.half) rehome_bsr(h, L.Ab);
   if (!L.Rb.sell && !L.Rb.sym)
@@ -4139,6 +4415,7 @@ void rehome_operators(DeviceHandle* h) {
     for (DBsr* M : {&D.Ab, &D.KPb, &D.Rb, &D.Pb})
       if (!M->half) rehome_bsr(h, *M);
   }
+  h->layout_ms[LT_REHOME] = lap();
 }
 
 // Block layout of a SELL-stored K's values: one 32-byte block per slot, or two
@@ -4194,8 +4471,17 @@ void apply_k_layout_knob(DeviceHandle* h) {
     if (!D.coarsest) set_k_split(D.KPb, 1);
 }
 
+std::string layout_error(const mamg_params& p) {
+  if (patch_schwarz(p))
+    return "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on every level)";
+  if (rings_schwarz(p))
+    return "SCHWARZ_RINGS needs the BSR2 layout (num_functions 2, node-block smoothers on every level)";
+  return "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned smoother blocks)";
+}
+
 int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, DeviceHandle** out,
                std::string* err) {
+  const auto t0 = std::chrono::steady_clock::now();
   std::unique_ptr<DeviceHandle> h(new DeviceHandle());
   h->p = p;
   h->device = p.device;
@@ -4208,11 +4494,8 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   h->L.resize(nl);
   h->bsr = bsr_eligible(H, A0, p);
   read_knobs();
-  if ((gs_smoother(p) || patch_schwarz(p)) && !h->bsr) {
-    *err = patch_schwarz(p) ? "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on "
-                              "every level)"
-                            : "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned "
-                              "smoother blocks)";
+  if ((gs_smoother(p) || patch_schwarz(p) || rings_schwarz(p)) && !h->bsr) {
+    *err = layout_error(p);
     return MAMG_ERR_UNSUPPORTED;
   }
   int rc;
@@ -4246,6 +4529,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
         if ((rc = T.alloc(&dW, 4 * nv, err))) return rc;
         HIPCHK(hipMemcpy(dW, blk.data(), 4 * nv * sizeof(double), hipMemcpyHostToDevice));
         S.W = dW;
+        S.seeds = &H.seeds;
         if ((rc = build_bsr_level(h.get(), l, S, nvc, lanesA, err))) return rc;
       }
     } else if (D.coarsest) {     // CSR layout, or a single-level hierarchy
@@ -4294,12 +4578,17 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   apply_ops(h.get(), h->hr, h->hz, &ops);
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   HIPCHK(hipDeviceSynchronize());
+  const auto t1 = std::chrono::steady_clock::now();
+  h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
   rehome_operators(h.get());
+  const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
   // every layout kernel and device-to-device copy (asynchronous to the host)
   // done before the handle is used on another stream
   HIPCHK(hipDeviceSynchronize());
+  h->layout_ms[LT_FINISH] =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
   *out = h.release();
   return MAMG_OK;
 }
@@ -4366,11 +4655,8 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
   read_knobs();
   h->bsr = !G->generic;   // a general block or point smoother: the CSR layout (as dev_upload)
-  if ((gs_smoother(p) || patch_schwarz(p)) && !h->bsr) {
-    *err = patch_schwarz(p) ? "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on "
-                              "every level)"
-                            : "multicolour GS/SGS smoothers need the BSR2 layout (num_functions 2, node-aligned "
-                              "smoother blocks)";
+  if ((gs_smoother(p) || patch_schwarz(p) || rings_schwarz(p)) && !h->bsr) {
+    *err = layout_error(p);
     return MAMG_ERR_UNSUPPORTED;
   }
   const int nl = (int)G->levels.size();
@@ -4427,6 +4713,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
       LevelSrc S;
       S.A = l == 0 ? A0 : g.A;
       S.P = g.P; S.R = g.R; S.AP = g.AP; S.W = g.W; S.Ainv = g.Ainv;
+      S.seeds = &G->seeds;
       const int64_t nvc = D.coarsest ? 0 : G->levels[l + 1].n / 2;
       if ((rc = build_bsr_level(h.get(), l, S, nvc, l == 0 ? p.spmv_lanes : 0, err))) return rc;
     }
@@ -4459,18 +4746,25 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
   HIPCHK(hipDeviceSynchronize());
+  const auto t1 = std::chrono::steady_clock::now();
+  h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
   rehome_operators(h.get());
+  const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
   HIPCHK(hipDeviceSynchronize());   // as in dev_upload
-  h->setup_ms[GS_LAYOUT] =
-      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const auto t3 = std::chrono::steady_clock::now();
+  h->layout_ms[LT_FINISH] = std::chrono::duration<double, std::milli>(t3 - t2).count();
+  h->setup_ms[GS_LAYOUT] = std::chrono::duration<double, std::milli>(t3 - t0).count();
   *out = h.release();
   return MAMG_OK;
 }
 
 void dev_setup_ms(const DeviceHandle* h, double* ms8) {
   for (int k = 0; k < 8; ++k) ms8[k] = h->setup_ms[k];
+}
+void dev_layout_ms(const DeviceHandle* h, double* ms4) {
+  for (int k = 0; k < 4; ++k) ms4[k] = h->layout_ms[k];
 }
 
 void dev_destroy(DeviceHandle* h) {
@@ -4489,7 +4783,8 @@ int dev_level_format(const DeviceHandle* h, int level) {
   return (L.Ab.sell ? MAMG_FMT_SELL : 0) | (L.Ab.sym ? MAMG_FMT_SYM : 0) | (L.Ab.half ? MAMG_FMT_HALF : 0) |
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
          (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0) |
-         (L.pcs.size() > 1 ? MAMG_FMT_PATCHES : 0) | (L.gcs.size() > 1 ? MAMG_FMT_GS : 0);
+         (L.pcs.size() > 1 ? MAMG_FMT_PATCHES : 0) | (L.gcs.size() > 1 ? MAMG_FMT_GS : 0) |
+         (L.rcs.size() > 1 ? MAMG_FMT_RINGS : 0);
 }
 
 mamg_params dev_params(const DeviceHandle* h) { return h->p; }
@@ -5770,8 +6065,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (patch_schwarz(p)) {
-    *err = "multi-GPU apply: node-patch Schwarz (SCHWARZ_PATCHES) is single-GPU";
+  if (patch_schwarz(p) || rings_schwarz(p)) {
+    *err = "multi-GPU apply: node-patch / seed-ring Schwarz (SCHWARZ_PATCHES / SCHWARZ_RINGS) is single-GPU";
     return MAMG_ERR_UNSUPPORTED;
   }
   const bool gs = gs_smoother(p);

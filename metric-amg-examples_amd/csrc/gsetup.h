@@ -43,6 +43,7 @@ struct GHier {
   int device = 0;
   bool generic = false;       // some level's smoother is WB or winv: CSR apply layout
   std::vector<GLevel> levels;
+  std::vector<int32_t> seeds; // SCHWARZ_RINGS: the level-0 seeds (blocks built with the apply layout)
   std::vector<void*> allocs;  // every device buffer above (owned)
   double phase_ms[8] = {};    // setup phase timings (see gsetup.hip)
   ~GHier();
@@ -65,6 +66,22 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H,
                         std::vector<std::vector<std::vector<int64_t>>>* ghosts, std::string* err,
                         bool matrices = true);
+// SCHWARZ_RINGS level-0 blocks (one per seed, setup.cpp overlap_smoother's
+// breadth-first rings: members sorted, <= mm dofs) and their Gauss-Jordan
+// inverses, from the device CSR A.  Device buffers (hipMalloc, the caller
+// frees them): blk[ns * mm] members of block k at k * mm, blen[ns],
+// sq[ns] inclusive scan of blen^2, inv[sq[ns - 1]] the row-major inverse of
+// block k at sq[k - 1]; nothing in *R is allocated on error.
+struct RingBlocks {
+  int32_t* blk = nullptr;
+  int64_t *blen = nullptr, *sq = nullptr;
+  double* inv = nullptr;
+  int64_t ns = 0, ninv = 0;
+  int mm = 0;
+};
+int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlvl, int mm, RingBlocks* R,
+                    std::string* err);
+void ring_blocks_free(RingBlocks* R);
 // host CSR -> HBM, buffers owned by G (G->device selects the GPU)
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err);
 

@@ -44,6 +44,7 @@
 #include <cstring>
 
 #include "dist.h"
+#include "dmem.h"
 #include "gsetup.h"
 #include "rowstage.h"
 
@@ -55,14 +56,13 @@ namespace mamg {
 // are queued asynchronously; freed memory can be handed to the next
 // allocation and overwritten under a kernel still reading it)
 GHier::~GHier() {
-  (void)hipDeviceSynchronize();
   for (void* p : allocs)
-    if (p) (void)hipFree(p);
+    if (p) free_after_drain(p, "GHier::~GHier");
 }
 
 void GHier::release(void* p) {
   for (auto& q : allocs)
-    if (q == p) { (void)hipDeviceSynchronize(); (void)hipFree(q); q = nullptr; }
+    if (q == p) { free_after_drain(q, "GHier::release"); q = nullptr; }
 }
 
 namespace {
@@ -115,8 +115,7 @@ __device__ __forceinline__ int64_t dfind(const int64_t* __restrict__ ptr, const 
 struct Scratch {            // temporaries of one setup call
   std::vector<void*> v;
   ~Scratch() {
-    (void)hipDeviceSynchronize();   // as GHier::release
-    for (void* p : v) if (p) (void)hipFree(p);
+    for (void* p : v) if (p) free_after_drain(p, "Scratch::~Scratch");
   }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
@@ -128,7 +127,7 @@ struct Scratch {            // temporaries of one setup call
   }
   void release(void* p) {
     for (auto& q : v)
-      if (q == p) { (void)hipDeviceSynchronize(); (void)hipFree(q); q = nullptr; }
+      if (q == p) { free_after_drain(q, "Scratch::release"); q = nullptr; }
   }
 };
 
@@ -201,7 +200,7 @@ __global__ __launch_bounds__(256) void absdiag_kernel(int64_t n, const int64_t* 
 __global__ __launch_bounds__(256) void strength_kernel(int64_t n, const int64_t* __restrict__ ptr,
                                                        const int32_t* __restrict__ col,
                                                        const double* __restrict__ val, const double* __restrict__ d,
-                                                       double theta, uint8_t* flag, int* nextra) {
+                                                       double theta, int rowmax, uint8_t* flag, int* nextra) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   double m = 0.0;   // the row's largest coupling: theta is relative to it
@@ -212,7 +211,7 @@ __global__ __launch_bounds__(256) void strength_kernel(int64_t n, const int64_t*
     if (j == i) continue;
     const double av = fabs(val[k]);
     const double s = sqrt(d[i] * d[j]);
-    if ((av >= theta * m) && (av > 1e-12 * s)) {
+    if ((av >= theta * (rowmax ? m : s)) && (av > 1e-12 * s)) {
       flag[k] = 1;
       const int64_t q = dfind(ptr, col, j, i);
       if (q >= 0) flag[q] = 1;
@@ -1777,7 +1776,8 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   HIPCHK(hipMemset(flag, 0, std::max<int64_t>(Gr.nnz, 1)));
   HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
   absdiag_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d);
-  strength_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d, theta, flag, ctr);
+  strength_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d, theta,
+                                     G->params.strength_measure == MAMG_STRENGTH_ROWMAX, flag, ctr);
   HIPCHK(hipGetLastError());
   int nextra = 0;
   RCHK(read_int(ctr, &nextra, err));
@@ -2213,6 +2213,71 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
 
 }  // namespace
 
+void ring_blocks_free(RingBlocks* R) {
+  for (void* q : {(void*)R->blk, (void*)R->blen, (void*)R->sq, (void*)R->inv}) free_after_drain(q, "ring_blocks_free");
+  *R = RingBlocks();
+}
+
+// the SCHWARZ_RINGS blocks: ring_bfs_kernel / ring_inv_kernel of the
+// additive form (the same blocks and Gauss-Jordan inverses), kept per block
+int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlvl, int mm, RingBlocks* R,
+                    std::string* err) {
+  *R = RingBlocks();
+  const int64_t n = A.n;
+  if (ns <= 0) { *err = "seed rings: no seeds"; return MAMG_ERR_ARG; }
+  if (mm < 1 || mm > 8192) { *err = "seed rings: Schwarz_mmsize must be in [1, 8192]"; return MAMG_ERR_UNSUPPORTED; }
+  for (int64_t k = 0; k < ns; ++k)
+    if (seeds[k] < 0 || seeds[k] >= n) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+  Scratch S;
+  RingBlocks B;
+  B.ns = ns;
+  B.mm = mm;
+  int32_t* ds = nullptr;
+  int64_t* gj = nullptr;
+  uint8_t* cov = nullptr;
+  int* bad = nullptr;
+  auto fail = [&](int rc) { ring_blocks_free(&B); return rc; };
+  if (hipMalloc(&B.blk, (size_t)ns * mm * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&B.blen, (size_t)ns * sizeof(int64_t)) != hipSuccess ||
+      hipMalloc(&B.sq, (size_t)ns * sizeof(int64_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    *err = "seed rings: device allocation failed";
+    return fail(MAMG_ERR_HIP);
+  }
+  int rc;
+  if ((rc = S.alloc(&ds, ns, err)) || (rc = S.alloc(&gj, ns, err)) || (rc = S.alloc(&cov, n, err)) ||
+      (rc = S.alloc(&bad, 1, err)))
+    return fail(rc);
+  if (hipMemcpy(ds, seeds, ns * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(bad, 0, sizeof(int)) != hipSuccess) {
+    *err = "seed rings: copy failed";
+    return fail(MAMG_ERR_HIP);
+  }
+  ring_bfs_kernel<<<(unsigned)ns, 64, 2 * (size_t)mm * sizeof(int32_t)>>>(ns, ds, A.ptr, A.col, maxlvl, mm, B.blk,
+                                                                         B.blen);
+  sq_len_kernel<<<nblk(ns), 256>>>(ns, B.blen, B.sq, gj);
+  if (hipGetLastError() != hipSuccess) { *err = "seed rings: launch failed"; return fail(MAMG_ERR_HIP); }
+  if ((rc = dscan_incl_i64(B.sq, B.sq, ns, nullptr, err)) || (rc = dscan_incl_i64(gj, gj, ns, nullptr, err)))
+    return fail(rc);
+  int64_t ngj = 0;
+  if ((rc = to_host(&B.ninv, B.sq + ns - 1, 1, err)) || (rc = to_host(&ngj, gj + ns - 1, 1, err))) return fail(rc);
+  double* scratch = nullptr;
+  if (hipMalloc(&B.inv, (size_t)std::max<int64_t>(B.ninv, 1) * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    *err = "seed rings: device allocation failed";
+    return fail(MAMG_ERR_HIP);
+  }
+  if ((rc = S.alloc(&scratch, ngj, err))) return fail(rc);
+  ring_inv_kernel<<<(unsigned)ns, 256>>>(ns, mm, B.blk, B.blen, B.sq, gj, A.ptr, A.col, A.val, scratch, B.inv, cov,
+                                         bad);
+  if (hipGetLastError() != hipSuccess) { *err = "seed rings: launch failed"; return fail(MAMG_ERR_HIP); }
+  int hb = 0;
+  if ((rc = read_int(bad, &hb, err))) return fail(rc);
+  if (hb) { *err = "seed rings: a Schwarz block is not SPD (non-positive pivot)"; return fail(MAMG_ERR_SETUP); }
+  *R = B;
+  return MAMG_OK;
+}
+
 int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mamg_params& p, GHier* G,
               std::string* err) {
   int rc = check_params(p, err);
@@ -2231,6 +2296,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
   G->params = p;
   G->device = p.device;
   G->levels.clear();
+  G->seeds.clear();
   G->generic = false;
   HIPCHK(hipSetDevice(p.device));
   Clock clk, tot;
@@ -2284,7 +2350,14 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     // smoother: overlapping seed rings (ADDITIVE), seed blocks (node-aligned:
     // 2x2 node blocks with split nodes; else a general block CSR), 2x2 node
     // blocks, or point weights
-    const bool seeds = seed_blocks_on(p, l, idofs, n_idofs);
+    // seed rings (SCHWARZ_RINGS): the level-0 Schwarz data are built with the
+    // apply layout (device.hip build_rings); the node-block smoother stands in
+    const bool rings = seed_blocks_on(p, l, idofs, n_idofs) && p.Schwarz_type == MAMG_SCHWARZ_RINGS;
+    const bool seeds = seed_blocks_on(p, l, idofs, n_idofs) && !rings;
+    if (rings) {
+      RCHK(check_ring_seeds(p, idofs, n_idofs, n, err));
+      G->seeds.assign(idofs, idofs + n_idofs);
+    }
     const bool pointSA = p.AMG_type == MAMG_SA_AMG && !blockP;
     bool node = false;              // smoother as 2x2 node blocks in Dsm / L.W
     bool full_nodes = false;        // ... and those are the full node blocks
@@ -2471,6 +2544,7 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
   H->params = G.params;
   H->A0 = A0;
   H->levels.clear();
+  H->seeds = G.seeds;
   auto dl = [&](const DevMat& M, Csr* C) -> int {
     C->n = M.n;
     C->m = M.m;

@@ -54,6 +54,7 @@ struct Hierarchy {
   mamg_params params;
   CsrView A0;               // level-0 matrix (caller-owned during setup)
   std::vector<HostLevel> levels;
+  std::vector<int32_t> seeds;   // SCHWARZ_RINGS: the level-0 seeds (the blocks are built with the apply layout)
   CsrView A(int l) const { return l == 0 ? A0 : levels[l].A.view(); }
 };
 
@@ -67,9 +68,19 @@ int aggregate_vmb_flags(const CsrView& G, const uint8_t* flag, std::vector<int64
 
 int host_setup(const CsrView& A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* out, std::string* err);
-mamg_params resolve_params(const mamg_params& in);
+mamg_params resolve_params(const mamg_params& in, const int32_t* idofs, int64_t n_idofs, int64_t n);
+mamg_params resolve_like(const mamg_params& in, const mamg_params& built);
 int check_params(const mamg_params& p, std::string* err);
 int check_patch_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err);
+int check_ring_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err);
+// SCHWARZ_RINGS: most dofs per seed block (one 128-thread workgroup per block
+// holds its residual in LDS; device.hip ring_kernel)
+constexpr int RING_MAX_DOFS = 256;
+// greedy first-fit colouring of seed blocks (members sorted, any order) in
+// block order on the conflict graph: a member of one in the closed
+// neighbourhood (A's pattern) of a member of the other (mamg_oracle.ring_colouring)
+void ring_colouring(const CsrView& A, const std::vector<int64_t>& bptr, const std::vector<int32_t>& mem,
+                    std::vector<int32_t>* colour);
 // SMOOTHER_POLY step weights w[0..poly_degree) (oracle mamg_oracle.poly_weights)
 constexpr int MAMG_POLY_MAX = 8;
 int poly_weights(const mamg_params& p, double* w);

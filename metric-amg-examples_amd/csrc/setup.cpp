@@ -155,7 +155,9 @@ struct Strength {
   std::vector<int32_t> xcol;
 };
 
-void strength(const CsrView& A, double theta, Strength* S) {
+// rowmax: theta relative to the row's largest off-diagonal coupling (the
+// default), else to sqrt(|a_ii a_jj|) (classical, MAMG_STRENGTH_DIAG)
+void strength(const CsrView& A, double theta, bool rowmax, Strength* S) {
   const int64_t n = A.n, nnz = A.nnz();
   std::vector<double> d(n);
 #pragma omp parallel for schedule(static)
@@ -171,7 +173,7 @@ void strength(const CsrView& A, double theta, Strength* S) {
       if (j == i) continue;
       const double av = std::fabs(A.val[k]);
       const double s = std::sqrt(d[i] * d[j]);
-      f0[k] = (av >= theta * m) && (av > 1e-12 * s);
+      f0[k] = (av >= theta * (rowmax ? m : s)) && (av > 1e-12 * s);
     }
   }
   S->flag.assign(nnz, 0);
@@ -954,6 +956,47 @@ int smooth_prolongator_block(const CsrView& A, const Csr& T, int nf, const mamg_
 
 }  // namespace
 
+// greedy first-fit colour per seed block in block order (host.h): block k
+// takes the smallest colour no earlier conflicting block holds; blocks
+// conflict iff a member of one lies in the closed neighbourhood of a member of
+// the other (so a colour's blocks write no x another of them reads)
+void ring_colouring(const CsrView& A, const std::vector<int64_t>& bptr, const std::vector<int32_t>& mem,
+                    std::vector<int32_t>* colour) {
+  const int64_t nb = (int64_t)bptr.size() - 1, n = A.n;
+  // blocks holding each dof (CSR, ascending block ids)
+  std::vector<int64_t> dptr(n + 1, 0);
+  for (int64_t k = 0; k < nb; ++k)
+    for (int64_t t = bptr[k]; t < bptr[k + 1]; ++t) dptr[mem[t] + 1]++;
+  for (int64_t i = 0; i < n; ++i) dptr[i + 1] += dptr[i];
+  std::vector<int32_t> dblk(dptr[n]);
+  {
+    std::vector<int64_t> fill(dptr.begin(), dptr.end() - 1);
+    for (int64_t k = 0; k < nb; ++k)
+      for (int64_t t = bptr[k]; t < bptr[k + 1]; ++t) dblk[fill[mem[t]]++] = (int32_t)k;
+  }
+  colour->assign(nb, -1);
+  std::vector<int64_t> mark;   // mark[c] == k: colour c taken by a conflicting block of k
+  for (int64_t k = 0; k < nb; ++k) {
+    auto touch = [&](int64_t j) {
+      for (int64_t q = dptr[j]; q < dptr[j + 1]; ++q) {
+        const int32_t l = dblk[q];
+        if (l >= k) break;                 // ascending: only earlier (coloured) blocks
+        const int32_t c = (*colour)[l];
+        if ((int64_t)mark.size() <= c) mark.resize(c + 1, -1);
+        mark[c] = k;
+      }
+    };
+    for (int64_t t = bptr[k]; t < bptr[k + 1]; ++t) {
+      const int64_t i = mem[t];
+      touch(i);
+      for (int64_t q = A.ptr[i]; q < A.ptr[i + 1]; ++q) touch(A.col[q]);
+    }
+    int32_t c = 0;
+    while (c < (int32_t)mark.size() && mark[c] == k) ++c;
+    (*colour)[k] = c;
+  }
+}
+
 // exported for the GPU setup (host.h): VMB on a device-built strength graph
 int aggregate_vmb_flags(const CsrView& G, const uint8_t* flag, std::vector<int64_t>* agg, int64_t* nagg,
                         std::string* err) {
@@ -979,18 +1022,49 @@ int poly_weights(const mamg_params& p, double* w) {
 
 // The reference's Schwarz_type names mean multiplicative Schwarz on the
 // overlapping blocks seed + Schwarz_maxlvl ring (src/amg_parameters.py:83-87,
-// comment src/utils.py:84).  SYMMETRIC on the 1-rings of a nodal system is
-// exactly SCHWARZ_PATCHES (one patch per seeded node: both fields of its closed
-// neighbourhood, exact local solves), so it runs as that; check_patch_seeds
-// then requires a seed on every node.  With Schwarz_maxlvl 0 the blocks are
-// the seeds' nodes, which do not overlap: the matching level smoother on the
-// seed blocks.  Anything else keeps its name and check_params rejects it.
-mamg_params resolve_params(const mamg_params& in) {
+// src/utils.py:60-86).  SYMMETRIC with rings (Schwarz_maxlvl >= 1) on a nodal
+// system runs as
+//  * SCHWARZ_PATCHES when the rings are 1-rings and every node holds a seed
+//    (the bidomain: one patch per node, both fields of its closed
+//    neighbourhood -- the same blocks, a dedicated kernel);
+//  * SCHWARZ_RINGS otherwise (sparse seed sets: EMI's interface dofs with the
+//    default dict's 2-rings): one block per seed, greedy conflict colours, and
+//    node-block GS on the dofs in no block ("the rest the GS smoother");
+//  * without seeds no Schwarz level: the level smoother everywhere.
+// With Schwarz_maxlvl 0 the blocks are the seeds' nodes, which do not
+// overlap: the matching level smoother on the seed blocks.  Anything else
+// keeps its name and check_params rejects it.  Mirrored by
+// mamg_oracle.resolve_params.
+mamg_params resolve_params(const mamg_params& in, const int32_t* idofs, int64_t n_idofs, int64_t n) {
   mamg_params p = in;
   if (p.Schwarz_levels < 1) return p;
-  if (p.Schwarz_type == MAMG_SCHWARZ_SYMMETRIC && p.Schwarz_maxlvl == 1 && p.num_functions == 2 &&
-      p.node_block_smoother)
-    p.Schwarz_type = MAMG_SCHWARZ_PATCHES;
+  if (p.Schwarz_type == MAMG_SCHWARZ_SYMMETRIC && p.Schwarz_maxlvl >= 1 && p.num_functions == 2 &&
+      p.node_block_smoother) {
+    if (!idofs || n_idofs <= 0) {
+      p.Schwarz_levels = 0;
+      return p;
+    }
+    bool every = p.Schwarz_maxlvl == 1 && n >= 2 && n % 2 == 0;
+    if (every) {
+      const int64_t nv = n / 2;
+      std::vector<char> has(nv, 0);
+      for (int64_t t = 0; t < n_idofs; ++t)
+        if (idofs[t] >= 0 && idofs[t] < n) has[idofs[t] % nv] = 1;
+      for (int64_t I = 0; I < nv && every; ++I) every = has[I] != 0;
+    }
+    p.Schwarz_type = every ? MAMG_SCHWARZ_PATCHES : MAMG_SCHWARZ_RINGS;
+  }
+  return p;
+}
+
+// a caller's dict applied to a hierarchy built earlier (mamg_upload): the
+// Schwarz name resolves as it did at setup
+mamg_params resolve_like(const mamg_params& in, const mamg_params& built) {
+  mamg_params p = in;
+  if (p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_SYMMETRIC && p.Schwarz_maxlvl >= 1) {
+    p.Schwarz_type = built.Schwarz_type;
+    p.Schwarz_levels = built.Schwarz_levels;
+  }
   return p;
 }
 
@@ -1020,6 +1094,10 @@ int check_params(const mamg_params& p, std::string* err) {
     return MAMG_ERR_UNSUPPORTED;
   }
   if (p.coarse_scaling != MAMG_OFF && p.coarse_scaling != MAMG_ON) { *err = "coarse_scaling must be OFF or ON"; return MAMG_ERR_ARG; }
+  if (p.strength_measure != MAMG_STRENGTH_ROWMAX && p.strength_measure != MAMG_STRENGTH_DIAG) {
+    *err = "strength_measure must be STRENGTH_ROWMAX (1) or STRENGTH_DIAG (0)";
+    return MAMG_ERR_ARG;
+  }
   if (p.coarse_solver != MAMG_COARSE_DENSE) { *err = "coarse_solver must be 32 (direct)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels > 1) { *err = "Schwarz_levels > 1 not supported (seeds exist on level 0 only)"; return MAMG_ERR_UNSUPPORTED; }
   if (p.Schwarz_levels == 1) {
@@ -1034,12 +1112,23 @@ int check_params(const mamg_params& p, std::string* err) {
                "and Schwarz_maxlvl 1";
         return MAMG_ERR_UNSUPPORTED;
       }
+    } else if (t == MAMG_SCHWARZ_RINGS) {
+      if (p.num_functions != 2 || !p.node_block_smoother || p.Schwarz_maxlvl < 1) {
+        *err = "SCHWARZ_RINGS (multiplicative seed-ring Schwarz) needs num_functions 2, node_block_smoother 1 "
+               "and Schwarz_maxlvl >= 1";
+        return MAMG_ERR_UNSUPPORTED;
+      }
+      if (p.Schwarz_mmsize > RING_MAX_DOFS) {
+        *err = "SCHWARZ_RINGS: Schwarz_mmsize " + std::to_string(p.Schwarz_mmsize) + " > " +
+               std::to_string(RING_MAX_DOFS) + " dofs per block";
+        return MAMG_ERR_UNSUPPORTED;
+      }
     } else if (t == MAMG_SCHWARZ_SYMMETRIC || t == MAMG_SCHWARZ_FORWARD || t == MAMG_SCHWARZ_BACKWARD) {
       if (p.Schwarz_maxlvl >= 1) {
         *err = std::string("Schwarz_type ") + (t == MAMG_SCHWARZ_SYMMETRIC ? "SYMMETRIC" : t == MAMG_SCHWARZ_FORWARD ? "FORWARD" : "BACKWARD") +
                " with Schwarz_maxlvl " + std::to_string(p.Schwarz_maxlvl) +
-               " is multiplicative Schwarz on overlapping seed + ring blocks; implemented only as SYMMETRIC with "
-               "Schwarz_maxlvl 1 on nodal systems (num_functions 2, a seed on every node: SCHWARZ_PATCHES). "
+               " is multiplicative Schwarz on overlapping seed + ring blocks; implemented as SYMMETRIC on nodal "
+               "systems (num_functions 2, node_block_smoother 1: SCHWARZ_PATCHES / SCHWARZ_RINGS). "
                "Alternatives: SCHWARZ_ADDITIVE (the same overlapping blocks, additive) or SCHWARZ_SEED_BLOCKS "
                "(non-overlapping blocks, the level smoother)";
         return MAMG_ERR_UNSUPPORTED;
@@ -1061,9 +1150,9 @@ int check_params(const mamg_params& p, std::string* err) {
       *err = "unknown Schwarz_type " + std::to_string(t);
       return MAMG_ERR_ARG;
     }
-    if (p.Schwarz_maxlvl > 1 && t != MAMG_SCHWARZ_ADDITIVE) {
-      *err = "Schwarz_maxlvl > 1 needs SCHWARZ_ADDITIVE (overlapping seed + ring blocks); the non-overlapping "
-             "seed blocks are the seeds' 1-rings";
+    if (p.Schwarz_maxlvl > 1 && t != MAMG_SCHWARZ_ADDITIVE && t != MAMG_SCHWARZ_RINGS) {
+      *err = "Schwarz_maxlvl > 1 needs overlapping seed + ring blocks (SCHWARZ_SYMMETRIC on a nodal system, "
+             "SCHWARZ_RINGS, or SCHWARZ_ADDITIVE); the non-overlapping seed blocks are the seeds' 1-rings";
       return MAMG_ERR_UNSUPPORTED;
     }
   }
@@ -1103,6 +1192,18 @@ int check_patch_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idof
   return MAMG_OK;
 }
 
+// SCHWARZ_RINGS: seeds in range, and the dense blocks bounded
+int check_ring_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs, int64_t n, std::string* err) {
+  for (int64_t t = 0; t < n_idofs; ++t)
+    if (idofs[t] < 0 || idofs[t] >= n) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
+  if ((double)n_idofs * p.Schwarz_mmsize * p.Schwarz_mmsize > 4e9) {
+    *err = "SCHWARZ_RINGS (dense overlapping seed blocks) is for sparse seed sets: " + std::to_string(n_idofs) +
+           " seeds of up to " + std::to_string(p.Schwarz_mmsize) + " dofs";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  return MAMG_OK;
+}
+
 int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
                const mamg_params& p, Hierarchy* H, std::string* err) {
   int rc = check_params(p, err);
@@ -1122,6 +1223,7 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
   H->params = p;
   H->A0 = A0;
   H->levels.clear();
+  H->seeds.clear();
   CsrView cur = A0;
   Csr next;
   for (int l = 0; l < p.max_levels; ++l) {
@@ -1140,7 +1242,7 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
         Csr G;
         node_graph(cur, nf, &G);
         Strength S;
-        strength(G.view(), p.strong_coupled, &S);
+        strength(G.view(), p.strong_coupled, p.strength_measure == MAMG_STRENGTH_ROWMAX, &S);
         rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(G.view(), S, l, &agg, &nagg, err)
              : p.aggregation_type == MAMG_VMB ? aggregate_vmb(G.view(), S, l, &agg, &nagg, err)
                                               : aggregate_mis2(G.view(), S, l, &agg, &nagg, err);
@@ -1148,7 +1250,7 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
         if (nagg == 0 || nf * nagg >= n) last = true;
       } else {
         Strength S;
-        strength(cur, p.strong_coupled, &S);
+        strength(cur, p.strong_coupled, p.strength_measure == MAMG_STRENGTH_ROWMAX, &S);
         rc = p.aggregation_type == MAMG_HEM ? aggregate_hem(cur, S, l, &agg, &nagg, err)
              : p.aggregation_type == MAMG_VMB ? aggregate_vmb(cur, S, l, &agg, &nagg, err)
                                               : aggregate_mis2(cur, S, l, &agg, &nagg, err);
@@ -1177,7 +1279,18 @@ int host_setup(const CsrView& A0, const int32_t* idofs, int64_t n_idofs,
     const bool need_rho = (p.AMG_type == MAMG_SA_AMG && !blockP) || p.smoother == MAMG_SMOOTHER_JACOBI_RHO ||
                           p.smoother == MAMG_SMOOTHER_POLY;
     const double rho = need_rho ? rho_estimate(cur, dinv, rs, p.rho_iters) : 0.0;
-    if (seed_blocks_on(p, l, idofs, n_idofs) && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
+    const bool rings = seed_blocks_on(p, l, idofs, n_idofs) && p.Schwarz_type == MAMG_SCHWARZ_RINGS;
+    if (rings) {
+      // seed rings: the level-0 Schwarz data are built with the apply layout
+      // (device.hip build_rings); the node-block smoother stands in for W
+      if ((rc = check_ring_seeds(p, idofs, n_idofs, n, err))) return rc;
+      H->seeds.assign(idofs, idofs + n_idofs);
+      std::vector<int64_t> bid;
+      int64_t nb;
+      node_blocks(n, nf, &bid, &nb);
+      rc = block_smoother_from(cur, bid, nb, p, &lev.WB, err);
+      if (rc) return rc;
+    } else if (seed_blocks_on(p, l, idofs, n_idofs) && p.Schwarz_type == MAMG_SCHWARZ_ADDITIVE) {
       rc = overlap_smoother(cur, idofs, n_idofs, p, &lev.WB, err);
       if (rc) return rc;
     } else if (seed_blocks_on(p, l, idofs, n_idofs)) {

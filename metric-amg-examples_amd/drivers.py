@@ -24,6 +24,10 @@ and append the error row
 ``ndofs h |eu1|_1 r|eu1|_1 |eu2|_1 r|eu2|_1`` (H1 errors and rates,
 src/bidomain_2d.py:150,239-270) to results/<problem>/error_<...>.txt;
 ``-rhs random`` uses the bench's seeded uniform(-1,1) vector instead.
+``-profile reference`` (default) takes the AMG parameters the reference's
+driver takes (metric_mono: parameters_metric_schwarz; metric / amg: the
+factories' default dicts); ``-profile mi355x`` the GPU profile
+(parameters_metric_mi355x) for every -precond choice.
 Differences (stated, not hidden): the matrices come from the in-library
 generators (problems.py; FEniCS is absent); the EMI drivers' manufactured
 solutions are restated in mms.py (src/emi_2d.py:8-128); the 3D-1D neuron mesh
@@ -60,6 +64,20 @@ def _append(path, row, first, headers=HEADERS_KSP):
         out.write('%s\n' % ' '.join(map(str, row)))
 
 
+def _profile_params(profile, precond):
+    """The parameter dict of a -precond choice: 'reference' = the dict the
+    reference's driver passes (src/bidomain_3d.py:138-147: metric_mono ->
+    parameters_metric_schwarz; 'metric' and 'amg' call the factories without
+    parameters, i.e. their defaults, src/utils.py:20-38,60-82), 'mi355x' =
+    the GPU profile (parameters_metric_mi355x, nodal SA V-cycle, node-block
+    Jacobi) for every choice."""
+    if profile == 'mi355x':
+        return P.parameters_metric_mi355x
+    if precond in ('metric_mono', 'metric_hazmath'):
+        return P.parameters_metric_schwarz
+    return None
+
+
 def _solve(A, W, b, precond, idofs, tol, maxiter, monolithic_params=None):
     """setup + CG, timed together (the reference's timeKSP)."""
     then = time.time()
@@ -74,7 +92,7 @@ def _solve(A, W, b, precond, idofs, tol, maxiter, monolithic_params=None):
                                         num_functions=nf)
         Aop = BB.Aop
     elif precond == 'amg':
-        BB = get_hazmath_amg_precond(Asp, W)
+        BB = get_hazmath_amg_precond(Asp, W, parameters=monolithic_params)
         Aop = BB._Aop
     elif precond == 'diag':
         BB = get_block_diag_precond(Asp, W)
@@ -102,7 +120,10 @@ def bidomain(argv, dim):
     ap.add_argument('-save', type=int, default=0)
     ap.add_argument('-results', type=str, default='./results')
     ap.add_argument('-rhs', type=str, default='mms', choices=('mms', 'random'))
+    ap.add_argument('-profile', type=str, default='reference', choices=('reference', 'mi355x'),
+                    help="AMG parameters: the reference driver's dicts, or the GPU profile")
     args, _ = ap.parse_known_args(argv)
+    prm = _profile_params(args.profile, args.precond)
     rdir = os.path.join(args.results, 'bidomain_%dd' % dim)
     os.makedirs(rdir, exist_ok=True)
     tags = dict(kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma, pdegree=args.pdegree)
@@ -118,10 +139,10 @@ def bidomain(argv, dim):
         else:
             b = problems.seeded_rhs(s.N)
         if args.precond == 'metric_hazmath':     # the whole solve in the library (src/bidomain_2d.py:181-186)
-            niters, xb, dt = solve_haznics(s, b, s.W, interface_dofs=s.idofs)
+            niters, xb, dt = solve_haznics(s, b, s.W, interface_dofs=s.idofs, parameters=prm)
             x, cond, r = np.concatenate(xb), -1, 0
         else:
-            x, niters, cond, dt, r, _ = _solve(s, s.W, b, args.precond, s.idofs, 1e-8, 500)
+            x, niters, cond, dt, r, _ = _solve(s, s.W, b, args.precond, s.idofs, 1e-8, 500, prm)
         h = np.sqrt(dim) / n            # dolfin hmin: the simplices' longest edge
         row = (s.N, niters, cond, dt, r, h)
         rows.append(row)
@@ -152,7 +173,10 @@ def emi(argv, dim):
     ap.add_argument('-save', type=int, default=0)
     ap.add_argument('-results', type=str, default='./results')
     ap.add_argument('-rhs', type=str, default='mms', choices=('mms', 'random'))
+    ap.add_argument('-profile', type=str, default='reference', choices=('reference', 'mi355x'),
+                    help="AMG parameters: the reference's default dict (src/utils.py:60-82), or the GPU profile")
     args, _ = ap.parse_known_args(argv)
+    prm = _profile_params(args.profile, args.precond)
     rdir = os.path.join(args.results, 'emi_%dd' % dim)
     os.makedirs(rdir, exist_ok=True)
     tags = dict(kappa1=args.kappa1, kappa2=args.kappa2, gamma=args.gamma, pdegree=args.pdegree)
@@ -171,7 +195,8 @@ def emi(argv, dim):
         if args.precond == 'diag':
             BB = get_block_diag_precond(s.blocks, s.W)
         else:
-            BB = get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+            BB = get_hazmath_metric_precond(s.blocks, s.W, parameters=prm, interface_dofs=s.idofs,
+                                            num_functions=2)
         solver = ConjGrad(s, precond=BB, tolerance=1e-10, maxiter=500)   # src/emi_3d.py:143
         x = solver * b
         dt = time.time() - then

@@ -12,10 +12,10 @@ values are build-defined (HAZmath's are not available here).
   parameters_metric_schwarz: UA + parallel HEM + W-cycle + multicolour SGS
   + coarse scaling, and on level 0 the reference's SCHWARZ_SYMMETRIC on the
   seeds' overlapping 1-ring blocks, which on a nodal system with a seed on
-  every node is exactly ``SCHWARZ_PATCHES``) or raises MAMG_ERR_UNSUPPORTED
-  naming the component it lacks (SGS on scalar systems;
-  multiplicative Schwarz on overlapping blocks of sparse seed sets); there
-  is no silent substitution under these names.  ``MetricAMG(A, W, ...)``
+  every node is exactly ``SCHWARZ_PATCHES``, and ``SCHWARZ_RINGS`` for sparse
+  seed sets) or raises MAMG_ERR_UNSUPPORTED naming the component it lacks
+  (SGS and multiplicative Schwarz on scalar systems); there is no silent
+  substitution under these names.  ``MetricAMG(A, W, ...)``
   takes ``num_functions`` from W (equal-sized blocks) when the dict does
   not set it, as the reference's metricAMG receives the block space W.
 * ``parameters_metric_mi355x``: the GPU profile "mi355x_sa_v" (nodal SA,
@@ -36,6 +36,12 @@ values are build-defined (HAZmath's are not available here).
   names the non-overlapping seed blocks under the level smoother.
 * ``parameters_metric_3d1d``: additive overlapping Schwarz on the 1-D seeds'
   rings.
+* ``parameters_metric_default`` / ``parameters_amg_default``: the dicts the
+  reference's factories use when called without parameters
+  (src/utils.py:60-82 / :20-38); ``precond`` falls back to them, so
+  ``get_hazmath_metric_precond(A, W, bcs, interface_dofs=...)`` (the EMI
+  drivers) runs the reference's SCHWARZ_SYMMETRIC on the interface seeds'
+  2-rings as ``SCHWARZ_RINGS``.
 * ``to_gpu_profile(d)``: explicit opt-in mapping of a HAZmath dict onto
   implemented components; returns the mapped dict and every substitution.
   ``*_gpu_mapped`` are the reference presets passed through it.
@@ -58,7 +64,11 @@ SCHWARZ_ADDITIVE = 5          # overlapping seed + Schwarz_maxlvl-ring blocks, a
 SCHWARZ_PATCHES = 6           # the reference's overlapping seed + 1-ring blocks, symmetric multiplicative
                               # (one patch per node, distance-3 multicolour order; level 0, nodal)
 SCHWARZ_SEED_BLOCKS = 7       # the level smoother on non-overlapping seed blocks (seed + joined non-seeds)
+SCHWARZ_RINGS = 8             # the reference's overlapping seed + Schwarz_maxlvl-ring blocks, symmetric
+                              # multiplicative (one block per seed, greedy conflict colours) + node-block GS
+                              # on the dofs in no block (level 0, nodal; sparse seed sets such as EMI's)
 OFF, ON = 0, 1
+STRENGTH_DIAG, STRENGTH_ROWMAX = 0, 1   # strength_measure: classical theta sqrt(|a_ii a_jj|) | row maximum (default)
 SOLVER_UMFPACK = 32          # coarse_solver / Schwarz_blksolver: dense direct here
 
 KEYS = ('prectype', 'AMG_type', 'cycle_type', 'max_levels', 'maxit', 'smoother',
@@ -69,7 +79,7 @@ KEYS = ('prectype', 'AMG_type', 'cycle_type', 'max_levels', 'maxit', 'smoother',
         # build-defined extensions
         'sa_omega', 'rho_iters', 'max_coarse_dense', 'device', 'spmv_lanes',
         'num_functions', 'node_block_smoother', 'sa_block_diag', 'post_fusion',
-        'poly_degree', 'poly_ratio')
+        'poly_degree', 'poly_ratio', 'strength_measure')
 
 # ---- the GPU profile "mi355x_sa_v"  -------------------
 parameters_metric_mi355x = {
@@ -145,6 +155,27 @@ parameters_metric = {
 parameters_metric_schwarz = dict(
     parameters_metric, Schwarz_levels=1, Schwarz_mmsize=100, Schwarz_maxlvl=1,
     Schwarz_type=SCHWARZ_SYMMETRIC, Schwarz_blksolver=32)
+# the defaults the reference's factories fall back to when called without
+# parameters: get_hazmath_metric_precond(_mono) (src/utils.py:60-82; the EMI
+# drivers' call, src/emi_3d.py:139, src/emi_2d.py:207) and
+# get_hazmath_amg_precond (src/utils.py:20-38).  On a nodal system with
+# sparse seeds the first runs SCHWARZ_SYMMETRIC on the seeds' 2-rings as
+# SCHWARZ_RINGS; with a seed on every node its 2-rings are too (the 1-ring
+# node patches need Schwarz_maxlvl 1)
+parameters_metric_default = {
+    "AMG_type": UA_AMG, "cycle_type": W_CYCLE, "max_levels": 20, "maxit": 1,
+    "smoother": SMOOTHER_SGS, "relaxation": 1.2, "presmooth_iter": 1, "postsmooth_iter": 1,
+    "coarse_dof": 100, "coarse_solver": 32, "coarse_scaling": ON, "aggregation_type": HEM,
+    "strong_coupled": 0.1, "max_aggregation": 100, "amli_degree": 3, "Schwarz_levels": 1,
+    "Schwarz_mmsize": 100, "Schwarz_maxlvl": 2, "Schwarz_type": SCHWARZ_SYMMETRIC,
+    "Schwarz_blksolver": 32, "print_level": 10,
+}
+parameters_amg_default = {
+    "prectype": 2, "AMG_type": UA_AMG, "cycle_type": W_CYCLE, "max_levels": 20, "maxit": 1,
+    "smoother": SMOOTHER_SGS, "relaxation": 1.2, "presmooth_iter": 1, "postsmooth_iter": 1,
+    "coarse_dof": 100, "coarse_solver": 32, "coarse_scaling": ON, "aggregation_type": VMB,
+    "strong_coupled": 0.1, "max_aggregation": 100, "Schwarz_levels": 0, "print_level": 10,
+}
 # round-1 names of the same verbatim dicts
 hazmath_parameters_standard = parameters_standard
 hazmath_parameters_standard_schwarz = parameters_standard_schwarz
@@ -172,10 +203,16 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
             # the library runs this as given on a nodal system; stated here too
             notes.append('Schwarz_type SCHWARZ_SYMMETRIC on the seeds\' 1-rings = SCHWARZ_PATCHES (the same '
                          'overlapping blocks, multiplicative in a distance-3 multicolour order; nodal systems '
-                         'with a seed on every node)')
+                         'with a seed on every node) or, for sparse seed sets, SCHWARZ_RINGS')
             out['Schwarz_type'] = SCHWARZ_PATCHES
             out['num_functions'] = 2
-        elif st in (SCHWARZ_SYMMETRIC, SCHWARZ_FORWARD, SCHWARZ_BACKWARD) and lvl >= 1:
+        elif st == SCHWARZ_SYMMETRIC and lvl >= 2:
+            notes.append('Schwarz_type SCHWARZ_SYMMETRIC on the seeds\' %d-rings = SCHWARZ_RINGS (the same '
+                         'overlapping blocks, multiplicative in a greedy conflict-colour order, node-block GS on '
+                         'the rest; nodal systems)' % lvl)
+            out['Schwarz_type'] = SCHWARZ_RINGS
+            out['num_functions'] = 2
+        elif st in (SCHWARZ_FORWARD, SCHWARZ_BACKWARD) and lvl >= 1:
             notes.append('Schwarz_type %r on overlapping seed + %d-ring blocks -> SCHWARZ_SEED_BLOCKS (the level '
                          'smoother on the non-overlapping seed blocks, seed + joined 1-ring)' % (st, lvl))
             out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS
@@ -185,7 +222,7 @@ def to_gpu_profile(params: dict) -> tuple[dict, list[str]]:
             out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS
         elif st is None:
             out['Schwarz_type'] = SCHWARZ_SEED_BLOCKS if gsm else SCHWARZ_BLOCK_JACOBI
-        if out.get('Schwarz_maxlvl', 1) > 1 and out['Schwarz_type'] != SCHWARZ_ADDITIVE:
+        if out.get('Schwarz_maxlvl', 1) > 1 and out['Schwarz_type'] not in (SCHWARZ_ADDITIVE, SCHWARZ_RINGS):
             notes.append('Schwarz_maxlvl %d -> 1' % out['Schwarz_maxlvl'])
             out['Schwarz_maxlvl'] = 1
     if smo in (SMOOTHER_GS, SMOOTHER_SGS) and out.get('num_functions', 1) != 2:

@@ -93,14 +93,15 @@ class _Product:
 
 def get_hazmath_metric_precond_mono(A, W, bcs=None, parameters=None, interface_dofs=None, **kw):
     """metricAMG(A, W, idofs=interface_dofs, parameters=parameters)  (src/utils.py:56-90).
-    ``parameters`` None -> the GPU profile (parameters_metric_mi355x).  A dict
-    is used as given (parameters_metric_schwarz runs as the reference's
-    algorithm: UA + HEM + W + SGS + scaling + node patches on level 0); a
-    component this build lacks (multiplicative Schwarz on overlapping blocks
-    of sparse seed sets, MWM/HEC aggregation) raises MamgError;
+    ``parameters`` None -> the reference's default dict (src/utils.py:60-82,
+    ``parameters.parameters_metric_default``: UA + HEM + W + SGS + scaling +
+    SCHWARZ_SYMMETRIC on the seeds' 2-rings, which runs as SCHWARZ_RINGS).  A
+    dict is used as given (parameters_metric_schwarz: node patches on level 0;
+    ``parameters_metric_mi355x``: the GPU profile, an explicit opt-in); a
+    component this build lacks (MWM/HEC aggregation, AMLI) raises MamgError;
     ``parameters.to_gpu_profile`` is the explicit opt-in mapping."""
     if parameters is None:
-        parameters = P.parameters_metric_mi355x
+        parameters = P.parameters_metric_default
     B = MetricAMG(A, W, idofs=interface_dofs, parameters=parameters, **kw)
     B.substitutions = []
     return B
@@ -119,8 +120,10 @@ def get_hazmath_metric_precond(A, W, bcs=None, parameters=None, interface_dofs=N
 
 def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs=None, **kw):
     """Plain (non-metric) AMG on the monolithic matrix (src/utils.py:15-42):
-    no interface seeds, point smoothers."""
-    params = dict(P.parameters_metric_mi355x) if parameters is None else dict(parameters)
+    no interface seeds.  ``parameters`` None -> the reference's default dict
+    (src/utils.py:20-38, ``parameters.parameters_amg_default``: UA + VMB + W +
+    SGS + scaling); ``num_functions`` from W as for metricAMG."""
+    params = dict(P.parameters_amg_default) if parameters is None else dict(parameters)
     params['Schwarz_levels'] = 0
     return MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
 

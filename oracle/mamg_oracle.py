@@ -232,6 +232,7 @@ class Params:
     coarse_scaling: int = 0       # 1: e <- alpha e, alpha = <b_c, e> / <A_c e, e>
     poly_degree: int = 2          # POLY: Chebyshev degree (steps per smoothing)
     poly_ratio: float = 16.0      # POLY: interval [hi / poly_ratio, hi] of W A
+    strength_measure: int = 1     # 1: theta relative to the row's largest coupling; 0: classical sqrt(a_ii a_jj)
 
 
 
@@ -248,7 +249,7 @@ def _offdiag_row_max(n: int, r: np.ndarray, c: np.ndarray, v: np.ndarray) -> np.
     return m
 
 
-def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
+def strength(A: sp.csr_matrix, theta: float, measure: int = 1) -> sp.csr_matrix:
     """Symmetric SoC: j strong for i iff |a_ij| >= theta*max_{k != i}|a_ik|
     and |a_ij| > 1e-12*sqrt(|a_ii||a_jj|) (j != i); then S <- S | S^T.
     The threshold is relative to the row's largest coupling, so every row
@@ -257,6 +258,8 @@ def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
     the bidomain at gamma = 1e6 lost every connection at theta = 0.1 (the
     reference presets' strong_coupled, src/amg_parameters.py:57,79) and the
     hierarchy collapsed (3-D n = 128: 324-336 PCG iterations).
+    measure 0 (STRENGTH_DIAG) is that classical rule, |a_ij| >=
+    theta*sqrt(|a_ii||a_jj|) (Vanek, Mandel, Brezina 1996), kept selectable.
     Returns boolean-valued CSR (values 1.0), sorted, no diagonal."""
     n = A.shape[0]
     d = np.abs(A.diagonal())
@@ -265,7 +268,8 @@ def strength(A: sp.csr_matrix, theta: float) -> sp.csr_matrix:
     av = np.abs(A.data)
     s = np.sqrt(d[r] * d[c])
     m = _offdiag_row_max(n, r, c, av)
-    strong = (r != c) & (av >= theta * m[r]) & (av > 1e-12 * s)
+    ref = m[r] if measure == 1 else s
+    strong = (r != c) & (av >= theta * ref) & (av > 1e-12 * s)
     S = sp.csr_matrix((np.ones(int(strong.sum())), (r[strong], c[strong])),
                       shape=(n, n))
     S = ((S + S.T) != 0).astype(np.float64).tocsr()
@@ -318,7 +322,7 @@ def mis2(S: sp.csr_matrix, level: int) -> np.ndarray:
     return state.astype(np.uint8)
 
 
-def node_strength(A: sp.csr_matrix, nf: int, theta: float):
+def node_strength(A: sp.csr_matrix, nf: int, theta: float, measure: int = 1):
     """Nodal strength for nf fields laid out field-major (dof = f*nv + I).
 
     s_IJ = sqrt(sum over the nf x nf block (I,J) of a^2), accumulated
@@ -342,7 +346,8 @@ def node_strength(A: sp.csr_matrix, nf: int, theta: float):
     d[ui[dmask]] = s[dmask]
     sd = np.sqrt(d[ui] * d[uj])
     m = _offdiag_row_max(nv, ui, uj, s)
-    strong = (ui != uj) & (s >= theta * m[ui]) & (s > 1e-12 * sd)
+    ref = m[ui] if measure == 1 else sd
+    strong = (ui != uj) & (s >= theta * ref) & (s > 1e-12 * sd)
     S = sp.csr_matrix((np.ones(int(strong.sum())), (ui[strong], uj[strong])), shape=(nv, nv))
     S = ((S + S.T) != 0).astype(np.float64).tocsr()
     S.sort_indices()
@@ -1093,6 +1098,114 @@ class Patches:
         return x
 
 
+# --------------------------------------------------------------------------
+# Multiplicative Schwarz on the seeds' overlapping rings (Schwarz_type RINGS):
+# the reference's level-0 smoother for sparse seed sets.  The EMI drivers call
+# get_hazmath_metric_precond without parameters (src/emi_3d.py:133-139), i.e.
+# the default dict of src/utils.py:60-82: SCHWARZ_SYMMETRIC on seed +
+# Schwarz_maxlvl = 2 ring blocks of at most Schwarz_mmsize = 100 dofs, seeded
+# by the interface dofs of both sides; "the interface_dofs has the Schwarz and
+# the rest the GS smoother" (src/utils.py:84).  Restated in a parallel order:
+# * one block per seed, in the given seed order (seed_ring_blocks), exact
+#   local solves (Gauss-Jordan, batched_inverse);
+# * blocks k and l conflict iff a member of one lies in the closed
+#   neighbourhood (A's pattern) of a member of the other; greedy first-fit
+#   colouring in seed order, so no block of a colour writes an x another block
+#   of that colour reads, and one colour is one parallel update;
+# * the rest: node-block Gauss-Seidel restricted to the dofs in no block, in
+#   the multicolour node order of the level-0 GS (jp_colouring): a node with
+#   both dofs uncovered takes its 2x2 block inverse, a node with one its
+#   1 / a_ii, a covered dof no update;
+# * one symmetric step = ring sweep forward (colours ascending), rest GS
+#   forward, rest GS backward, ring sweep backward -- palindromic, so the
+#   same step serves pre- and post-smoothing and the cycle stays symmetric.
+# --------------------------------------------------------------------------
+SCHWARZ_RINGS = 8
+
+
+def ring_colouring(A: sp.csr_matrix, blocks) -> np.ndarray:
+    """Greedy first-fit colour of every ring block in block (= seed) order on
+    the conflict graph (member of one block in the closed neighbourhood of a
+    member of the other).  Returns int32 colour per block."""
+    n = A.shape[0]
+    nb = len(blocks)
+    if nb == 0:
+        return np.zeros(0, np.int32)
+    rows = np.concatenate([np.full(len(b), k, np.int64) for k, b in enumerate(blocks)])
+    cols = np.concatenate(blocks)
+    Mem = sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(nb, n))
+    G = A.tocsr().copy()
+    G.data = np.ones_like(G.data)
+    G = (G + sp.identity(n, format='csr')).tocsr()
+    G.data[:] = 1.0
+    C = (Mem @ (Mem @ G).T).tocsr()
+    colour = np.full(nb, -1, np.int64)
+    for k in range(nb):
+        nb_k = C.indices[C.indptr[k]:C.indptr[k + 1]]
+        used = set(colour[nb_k[nb_k < k]].tolist())
+        c = 0
+        while c in used:
+            c += 1
+        colour[k] = c
+    return colour.astype(np.int32)
+
+
+class Rings:
+    """Level-0 seed-ring blocks (Schwarz_type RINGS): members sorted per block
+    (seed_ring_blocks), Gauss-Jordan inverses, greedy conflict colouring."""
+
+    def __init__(self, A: sp.csr_matrix, seeds, maxlvl: int, mmsize: int):
+        A = A.tocsr()
+        n = A.shape[0]
+        seeds = np.asarray(seeds, np.int64)
+        if seeds.size == 0:
+            raise ValueError('seed-ring Schwarz needs seeds')
+        if float(seeds.size) * mmsize * mmsize > 4e9:
+            raise ValueError('seed-ring Schwarz (dense overlapping blocks) is for sparse seed sets')
+        self.blocks = seed_ring_blocks(A, seeds, maxlvl, mmsize)
+        self.Minv = [batched_inverse(A[b][:, b].toarray()[None, :, :])[0] for b in self.blocks]
+        self.colour = ring_colouring(A, self.blocks)
+        self.ncolours = int(self.colour.max()) + 1
+        self.cblocks = [np.flatnonzero(self.colour == c) for c in range(self.ncolours)]
+        self.cov = np.zeros(n, dtype=bool)
+        for b in self.blocks:
+            self.cov[b] = True
+
+    def sweep(self, A: sp.csr_matrix, x: np.ndarray, b: np.ndarray, forward=True):
+        """x <- x + Minv_k (b - A x)|_k for the blocks of each colour in turn
+        (ascending if forward, else descending); blocks of one colour are
+        independent, so their residuals are taken before any of them updates."""
+        order = range(self.ncolours) if forward else range(self.ncolours - 1, -1, -1)
+        for c in order:
+            ks = self.cblocks[c]
+            rows = np.concatenate([self.blocks[k] for k in ks])
+            res = b[rows] - A[rows] @ x
+            off = 0
+            for k in ks:
+                m = len(self.blocks[k])
+                x[self.blocks[k]] += self.Minv[k] @ res[off:off + m]
+                off += m
+        return x
+
+
+def rest_gs_inverse(A: sp.csr_matrix, cov: np.ndarray) -> np.ndarray:
+    """(nv, 2, 2) node-block inverses of the rest Gauss-Seidel: both dofs of
+    node I uncovered -> the 2x2 Gauss-Jordan inverse of A's diagonal block
+    (node_block_inverse); one uncovered dof f -> 1 / a_ff at (f, f); covered
+    dofs -> 0 (no update)."""
+    n = A.shape[0]
+    nv = n // 2
+    Dn = node_block_inverse(A, np.arange(n) % nv, nv)
+    d = A.diagonal()
+    c0, c1 = cov[:nv], cov[nv:]
+    half0 = ~c0 & c1                      # only field 0 uncovered
+    half1 = c0 & ~c1
+    Dn[c0 | c1] = 0.0
+    Dn[half0, 0, 0] = 1.0 / d[:nv][half0]
+    Dn[half1, 1, 1] = 1.0 / d[nv:][half1]
+    return Dn
+
+
 @dataclasses.dataclass
 class Level:
     A: sp.csr_matrix
@@ -1111,6 +1224,7 @@ class Level:
     crows: list = None               # node ids of each colour (ascending)
     polyW: list = None               # POLY: w_k W per Chebyshev step (poly_weights)
     patches: 'Patches' = None        # level 0, Schwarz_type PATCHES
+    rings: 'Rings' = None            # level 0, Schwarz_type RINGS (Dn / colour: the rest GS)
 
     def step_smoother(self, k):
         return None if self.polyW is None else self.polyW[k]
@@ -1152,7 +1266,11 @@ class Hierarchy:
             return lev.Ainv @ b
         A = lev.A
         gs = lev.colour is not None
-        if lev.patches is not None:                  # symmetric multiplicative patch Schwarz
+        if lev.rings is not None:                    # seed-ring Schwarz + the rest's GS (symmetric step)
+            x = np.zeros_like(b)
+            for _ in range(p.presmooth_iter):
+                x = self.rings_step(lev, x, b)
+        elif lev.patches is not None:                # symmetric multiplicative patch Schwarz
             x = np.zeros_like(b)
             for _ in range(p.presmooth_iter):
                 x = lev.patches.sweep(A, x, b, True)
@@ -1184,7 +1302,9 @@ class Hierarchy:
         if lev.polyW is not None:
             post = lev.polyW[::-1]                   # POLY: steps m..1
         for _ in range(p.postsmooth_iter):
-            if lev.patches is not None:
+            if lev.rings is not None:
+                x = self.rings_step(lev, x, b)
+            elif lev.patches is not None:
                 x = lev.patches.sweep(A, x, b, True)
                 x = lev.patches.sweep(A, x, b, False)
             elif gs:                                 # SGS: forward + backward; GS: backward
@@ -1195,6 +1315,15 @@ class Hierarchy:
                 for S in post:
                     x = x + lev.smooth_apply(b - A @ x, S)
         return x
+
+    @staticmethod
+    def rings_step(lev, x, b):
+        """One symmetric level-0 step of Schwarz_type RINGS: ring sweep
+        forward, rest GS forward and backward, ring sweep backward."""
+        x = lev.rings.sweep(lev.A, x, b, True)
+        x = lev.gs_sweep(x, b, True)
+        x = lev.gs_sweep(x, b, False)
+        return lev.rings.sweep(lev.A, x, b, False)
 
     def apply(self, r: np.ndarray) -> np.ndarray:
         """z = B r: ``maxit`` cycles (src/amg_parameters.py:71), x0 = 0."""
@@ -1228,13 +1357,22 @@ SCHWARZ_SYMMETRIC = 3
 SCHWARZ_SEED_BLOCKS = 7        # the level smoother on non-overlapping seed blocks
 
 
-def resolve_params(p: Params) -> Params:
-    """The reference's SCHWARZ_SYMMETRIC on the seeds' 1-rings
-    (src/amg_parameters.py:83-87, src/utils.py:84) of a nodal system is the
-    node-patch Schwarz (SCHWARZ_PATCHES); mirrors setup.cpp resolve_params."""
-    if p.Schwarz_levels >= 1 and p.Schwarz_type == SCHWARZ_SYMMETRIC and p.Schwarz_maxlvl == 1 \
+def resolve_params(p: Params, idofs=None, n: int = 0) -> Params:
+    """The reference's SCHWARZ_SYMMETRIC on the seeds' overlapping
+    seed + Schwarz_maxlvl ring blocks (src/amg_parameters.py:83-87,
+    src/utils.py:60-86) of a nodal system; mirrors setup.cpp resolve_params:
+    * no seeds: no Schwarz level (the level smoother everywhere);
+    * 1-rings with a seed on every node: the node patches (SCHWARZ_PATCHES,
+      the same blocks, a dedicated kernel);
+    * otherwise: the seed rings (SCHWARZ_RINGS)."""
+    if p.Schwarz_levels >= 1 and p.Schwarz_type == SCHWARZ_SYMMETRIC and p.Schwarz_maxlvl >= 1 \
             and p.num_functions == 2 and p.node_block_smoother:
-        return dataclasses.replace(p, Schwarz_type=SCHWARZ_PATCHES)
+        if idofs is None or len(idofs) == 0:
+            return dataclasses.replace(p, Schwarz_levels=0)
+        nv = n // 2
+        every = p.Schwarz_maxlvl == 1 and n > 0 and \
+            np.unique(np.asarray(idofs, np.int64) % nv).size == nv
+        return dataclasses.replace(p, Schwarz_type=SCHWARZ_PATCHES if every else SCHWARZ_RINGS)
     return p
 
 
@@ -1243,7 +1381,7 @@ AGGREGATORS = {'MIS': aggregate_mis2, 'HEM': aggregate_hem, 'VMB': aggregate_vmb
 
 
 def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarchy:
-    p = resolve_params(params or Params())
+    p = resolve_params(params or Params(), idofs, A.shape[0])
     A = A.tocsr()
     A.sort_indices()
     levels = []
@@ -1256,11 +1394,11 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         nf = p.num_functions
         if not last:
             if nf > 1:
-                S, Wn = node_strength(cur, nf, p.strong_coupled)
+                S, Wn = node_strength(cur, nf, p.strong_coupled, p.strength_measure)
                 agg, nagg = AGGREGATORS[p.aggregation_type](Wn, S, l)
                 last = nagg == 0 or nf * nagg >= n
             else:
-                S = strength(cur, p.strong_coupled)
+                S = strength(cur, p.strong_coupled, p.strength_measure)
                 agg, nagg = AGGREGATORS[p.aggregation_type](abs(cur), S, l)
                 last = nagg == 0 or nagg >= n
         if last:
@@ -1272,7 +1410,12 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
         if gs and (nf != 2 or not p.node_block_smoother):
             raise ValueError('multicolour GS needs num_functions = 2 and node-block smoothers')
         pj = dataclasses.replace(p, smoother='JACOBI_RHO') if gs else p
-        if l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1 \
+        rings = l == 0 and p.Schwarz_levels >= 1 and p.Schwarz_type == SCHWARZ_RINGS and idofs is not None
+        if rings and (nf != 2 or not p.node_block_smoother):
+            raise ValueError('seed-ring Schwarz needs num_functions = 2 and node-block smoothers')
+        if rings:                                    # node blocks (the level-0 W is not applied)
+            lev.WB, lev.bid, nbk = block_smoother(cur, None, pj, node_blocks(n, nf))
+        elif l < p.Schwarz_levels and idofs is not None and l == 0 and p.Schwarz_maxlvl >= 1 \
                 and p.Schwarz_type == SCHWARZ_ADDITIVE:
             lev.WB, _ = overlap_smoother(cur, idofs, pj)
             nbk = 0
@@ -1286,6 +1429,12 @@ def setup(A: sp.csr_matrix, params: Params | None = None, idofs=None) -> Hierarc
             lev.polyW = [scaled_smoother(lev, w) for w in poly_weights(p)]
         if gs:
             lev.Dn = node_block_inverse(cur, lev.bid, nbk)
+            lev.colour = jp_colouring(node_pattern(cur, 2), l)
+            lev.ncolours = int(lev.colour.max()) + 1 if len(lev.colour) else 0
+            lev.crows = [np.flatnonzero(lev.colour == c) for c in range(lev.ncolours)]
+        if rings:
+            lev.rings = Rings(cur, idofs, p.Schwarz_maxlvl, p.Schwarz_mmsize)
+            lev.Dn = rest_gs_inverse(cur, lev.rings.cov)
             lev.colour = jp_colouring(node_pattern(cur, 2), l)
             lev.ncolours = int(lev.colour.max()) + 1 if len(lev.colour) else 0
             lev.crows = [np.flatnonzero(lev.colour == c) for c in range(lev.ncolours)]

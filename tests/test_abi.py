@@ -30,7 +30,7 @@ def test_exports_every_declared_symbol(lib_built):
 def test_params_struct_layout(lib_built):
     import metric_amg_examples_amd as M
     p = M.parameters.make_params()
-    assert p.abi_version == 3 and p.post_fusion == 1 and p.AMG_type == 2 and p.cycle_type == 1
+    assert p.abi_version == 4 and p.strength_measure == 1 and p.post_fusion == 1 and p.AMG_type == 2 and p.cycle_type == 1
     assert p.poly_degree == 2 and p.poly_ratio == 16.0     # last fields: struct tail matches mamg.h
     assert abs(p.relaxation - 4.0 / 3.0) < 1e-15 and p.coarse_dof == 100
     assert p.num_functions == 1 and p.node_block_smoother == 1
@@ -89,14 +89,27 @@ def test_reference_presets_map_and_report(lib_built):
     H = M.HostHierarchy(s, idofs=s.idofs, parameters=P.parameters_metric_mi355x_sgs)
     assert H.effective_params['Schwarz_type'] == P.SCHWARZ_SEED_BLOCKS
     H.close()
-    # sparse seeds (not one on every node): the reference's overlapping
-    # multiplicative form is rejected, naming the gap
-    with pytest.raises(M._lib.MamgError) as ei:
-        M.HostHierarchy(s, idofs=s.idofs[::2], parameters=P.parameters_metric_schwarz, num_functions=2)
-    assert ei.value.code == -4 and 'every node' in str(ei.value)
-    with pytest.raises(M._lib.MamgError) as ei:
-        M.HostHierarchy(s, idofs=s.idofs, parameters=dict(P.parameters_metric_schwarz, Schwarz_maxlvl=2),
+    # sparse seeds (not one on every node), or rings of 2: the reference's
+    # overlapping multiplicative form runs as the seed rings (SCHWARZ_RINGS)
+    H = M.HostHierarchy(s, idofs=s.idofs[::2], parameters=P.parameters_metric_schwarz, num_functions=2)
+    assert H.effective_params['Schwarz_type'] == P.SCHWARZ_RINGS
+    H.close()
+    H = M.HostHierarchy(s, idofs=s.idofs, parameters=dict(P.parameters_metric_schwarz, Schwarz_maxlvl=2),
                         num_functions=2)
+    assert H.effective_params['Schwarz_type'] == P.SCHWARZ_RINGS
+    H.close()
+    # ... the reference's default dict too (src/utils.py:60-82); without seeds
+    # no Schwarz level (the level smoother everywhere, src/utils.py:88)
+    H = M.HostHierarchy(s, idofs=s.idofs[::3], parameters=P.parameters_metric_default, num_functions=2)
+    assert H.effective_params['Schwarz_type'] == P.SCHWARZ_RINGS
+    H.close()
+    H = M.HostHierarchy(s, parameters=P.parameters_metric_default, num_functions=2)
+    assert H.effective_params['Schwarz_levels'] == 0
+    H.close()
+    # forward-only multiplicative Schwarz on overlapping blocks is not built
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.HostHierarchy(s, idofs=s.idofs, parameters=dict(P.parameters_metric_schwarz, Schwarz_maxlvl=2,
+                                                           Schwarz_type=P.SCHWARZ_FORWARD), num_functions=2)
     assert ei.value.code == -4 and 'SCHWARZ_ADDITIVE' in str(ei.value)
     # explicit mapping keeps what is implemented and reports what it changes
     mapped, notes = P.to_gpu_profile(P.parameters_standard)

@@ -33,7 +33,10 @@ def one_sided(s):
 def test_emi_block_form_pcg_matches_oracle(lib_built, dim, n, g):
     M = _M()
     s = M.problems.emi(dim, n, g)
-    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+    # the GPU profile (explicit; parameters=None is the reference's default
+    # dict, tests/test_gpu_rings.py)
+    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, parameters=M.parameters.parameters_metric_mi355x,
+                                              interface_dofs=s.idofs, num_functions=2)
     # interface seeds recruit their own side's interior neighbours: blocks are
     # not node-aligned, so the GPU setup builds a general block smoother and
     # the handle runs the CSR layout
@@ -184,7 +187,9 @@ def test_drivers_write_reference_iters_schema(lib_built, tmp_path):
                            '-results', str(tmp_path)], 2)
     assert hz[0][1] == rows[0][1] and hz[0][2] == -1
     rows = drivers.emi(['-nrefs', '1', '-gamma', '1e4', '-results', str(tmp_path)], 3)
-    assert rows[0][1] < 80
+    assert rows[0][1] < 30          # the reference's default dict: seed-ring Schwarz
+    rows_g = drivers.emi(['-nrefs', '1', '-gamma', '1e4', '-profile', 'mi355x', '-results', str(tmp_path)], 3)
+    assert rows_g[0][1] < 80
     rows = drivers.bidomain(['-nrefs', '1', '-gamma', '1e2', '-precond', 'metric',
                              '-results', str(tmp_path)], 3)
     assert rows[0][1] < 80

@@ -80,13 +80,45 @@ def test_bidomain_baseline_config_apply_and_pcg(lib_built, dim, nrefs):
     B.close()
 
 
+def test_emi_3d_nrefs5_reference_default_rings(lib_built):
+    """BASELINE config 4's system (emi_3d nrefs=5, N = 278,850) with the EMI
+    drivers' own preconditioner call (no parameters: the reference's default
+    dict, seed-ring Schwarz on the 8,450 interface seeds' 2-rings): the GPU
+    and the host setup give bitwise-equal applies, the cycle without coarse
+    scaling is symmetric, and PCG (tolerance 1e-10, src/emi_3d.py:143)
+    converges in few iterations."""
+    import torch
+    M = _M()
+    P = M.parameters
+    s = M.problems.emi(3, 64, 1e6)
+    A = s.scipy()
+    Bg = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs, setup='gpu')
+    Bh = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs, setup='host')
+    assert Bg.setup_path == 'gpu' and Bg.level_format(0)['rings']
+    r = M.problems.seeded_rhs(s.N)
+    assert np.array_equal(Bg * r, Bh * r)
+    Bh.close()
+    Bs = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs,
+                                                   parameters=dict(P.parameters_metric_default, coarse_scaling=0))
+    r1, r2 = torch.as_tensor(r).cuda(), torch.as_tensor(M.problems.seeded_rhs(s.N, 5)).cuda()
+    a, c = float(torch.dot(r2, Bs.matvec(r1))), float(torch.dot(r1, Bs.matvec(r2)))
+    assert abs(a - c) <= 1e-9 * abs(a)
+    Bs.close()
+    solver = M.ConjGrad(A, precond=Bg, tolerance=1e-10, maxiter=500)
+    solver * r
+    say('EMI 3-D nrefs=5, reference default dict (seed rings): PCG iterations %d' % (len(solver.residuals) - 1))
+    assert len(solver.residuals) - 1 <= 40
+    Bg.close()
+
+
 def test_emi_3d_nrefs5_block_form(lib_built):
     import torch
     M = _M()
     n = 2 ** (2 + 5 - 1)                                   # src/emi_3d.py:119, nrefs=5
     s = M.problems.emi(3, n, 1e6)
     assert s.N == 278850
-    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, parameters=M.parameters.parameters_metric_mi355x,
+                                              interface_dofs=s.idofs, num_functions=2)
     Bm = BB.monolithic
     A = s.scipy()
     b = [M.problems.seeded_rhs(s.W[0], 1234), M.problems.seeded_rhs(s.W[1], 4321)]

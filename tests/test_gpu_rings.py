@@ -1,0 +1,153 @@
+"""GPU parity of the multiplicative seed-ring Schwarz smoother (Schwarz_type
+SCHWARZ_RINGS): the reference's level-0 SCHWARZ_SYMMETRIC on the interface
+seeds' overlapping Schwarz_maxlvl-ring blocks plus GS on the rest
+(/root/reference/src/utils.py:60-86), which is what the EMI drivers run when
+they call get_hazmath_metric_precond without parameters
+(/root/reference/src/emi_3d.py:133-139, src/emi_2d.py:207), against the CPU
+oracle (mamg_oracle.Rings, rest_gs_inverse, Hierarchy.rings_step).
+
+Tolerances as tests/test_gpu_patch.py: one apply to 1e-10 relative (blocks,
+colours and inverses are exact; only summation order differs), PCG iteration
+count equal to the oracle's, residuals within 1e-6 relative.
+"""
+import numpy as np
+import pytest
+
+import mamg_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+REF_DEFAULT = dict(AMG_type='UA', cycle_type='W', smoother='SGS', relaxation=1.2, coarse_scaling=1,
+                   aggregation_type='HEM', strong_coupled=0.1, Schwarz_levels=1, Schwarz_mmsize=100,
+                   Schwarz_maxlvl=2, Schwarz_type=3, num_functions=2)     # src/utils.py:60-82
+
+
+def _M():
+    import metric_amg_examples_amd as M
+    return M
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def _check_apply(B, h, N):
+    import torch
+    for seed in (1234, 7):
+        r = mo.seeded_rhs(N, seed)
+        zo = h.apply(r)
+        assert rel(B * r, zo) < 1e-10
+        zt = B.matvec(torch.as_tensor(r).cuda())
+        torch.cuda.synchronize()
+        assert rel(zt.cpu().numpy(), zo) < 1e-10
+
+
+@pytest.mark.parametrize('setup', ['host', 'gpu'])
+@pytest.mark.parametrize('dim,n,g', [(3, 8, 1e6), (3, 16, 1e6), (3, 32, 1e6), (2, 64, 1e6), (3, 16, 1.0)])
+def test_reference_default_dict_emi(lib_built, dim, n, g, setup):
+    """get_hazmath_metric_precond_mono(A, W, bcs, interface_dofs) with no
+    parameters = the reference's default dict: UA + HEM + W + SGS + scaling +
+    SCHWARZ_SYMMETRIC on the seeds' 2-rings, run as SCHWARZ_RINGS on the BSR2
+    layout; apply = the oracle's to 1e-10, the PCG count and residuals
+    (tolerance 1e-10, src/emi_3d.py:143) = the oracle's."""
+    M = _M()
+    P = M.parameters
+    s = M.problems.emi(dim, n, g)
+    A = s.scipy()
+    B = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs, setup=setup)
+    assert B.setup_path == setup, B.setup_path
+    assert B.effective_params['Schwarz_type'] == P.SCHWARZ_RINGS
+    assert B.layout == 'bsr2' and B.level_format(0)['rings'] and B.level_format(1)['gs']
+    h = mo.setup(A, mo.Params(**REF_DEFAULT), idofs=s.idofs)
+    assert h.levels[0].rings is not None and B.num_levels == len(h.levels)
+    _check_apply(B, h, s.N)
+    b = mo.seeded_rhs(s.N)
+    solver = M.ConjGrad(A, precond=B, tolerance=1e-10, maxiter=500)
+    solver * b
+    ref = mo.pcg(A, h, b, 1e-10, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+    assert len(solver.residuals) - 1 <= 30
+
+
+@pytest.mark.parametrize('kw', [dict(cycle_type='V', coarse_scaling=0, smoother='JACOBI_RHO', AMG_type='SA',
+                                     aggregation_type='MIS', relaxation=4.0 / 3.0, strong_coupled=0.0),
+                                dict(Schwarz_maxlvl=1, presmooth_iter=2, postsmooth_iter=2),
+                                dict(Schwarz_mmsize=40, smoother='POLY', cycle_type='V', coarse_scaling=0)])
+def test_rings_profiles(lib_built, kw):
+    """Seed rings under other level smoothers and cycle shapes (Jacobi SA
+    V-cycle below level 0, 1-rings of sparse seeds, nu = 2, POLY, capped
+    blocks): GPU apply = oracle, GPU setup = host setup (bitwise applies)."""
+    M = _M()
+    s = M.problems.emi(3, 16, 1e4)
+    A = s.scipy()
+    prm = dict(REF_DEFAULT, **kw)
+    C = {'smoother': {'SGS': 11, 'GS': 10, 'POLY': 12, 'JACOBI_RHO': 3}, 'cycle_type': {'V': 1, 'W': 2},
+         'AMG_type': {'SA': 2, 'UA': 1}, 'aggregation_type': {'MIS': 2, 'HEM': 5}}
+    ck = {k: (C[k][v] if k in C else v) for k, v in prm.items()}
+    Bh = M.MetricAMG(A, s.W, idofs=s.idofs, setup='host', **ck)
+    Bg = M.MetricAMG(A, s.W, idofs=s.idofs, setup='gpu', **ck)
+    assert Bg.setup_path == 'gpu' and Bg.level_format(0)['rings']
+    h = mo.setup(A, mo.Params(**prm), idofs=s.idofs)
+    _check_apply(Bg, h, s.N)
+    r = mo.seeded_rhs(s.N, 11)
+    assert np.array_equal(Bh * r, Bg * r)
+
+
+def test_rings_symmetric_and_deterministic(lib_built):
+    """Palindromic level-0 step: without coarse scaling the cycle is a
+    symmetric operator; graph replays give identical bits (no races inside a
+    colour: blocks of one colour share no dof and read no x another writes)."""
+    import torch
+    M = _M()
+    s = M.problems.emi(3, 16, 1e6)
+    A = s.scipy()
+    B = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs,
+                                                  parameters=dict(M.parameters.parameters_metric_default,
+                                                                  coarse_scaling=0))
+    r1 = torch.as_tensor(mo.seeded_rhs(s.N, 1)).cuda()
+    r2 = torch.as_tensor(mo.seeded_rhs(s.N, 2)).cuda()
+    z1, z2 = B.matvec(r1), B.matvec(r2)
+    z1b = B.matvec(r1)
+    torch.cuda.synchronize()
+    a, c = float(torch.dot(r2, z1)), float(torch.dot(r1, z2))
+    assert abs(a - c) <= 1e-10 * abs(a)
+    assert torch.equal(z1, z1b)
+
+
+def test_emi_block_form_reference_call(lib_built):
+    """The EMI drivers' call verbatim: R.T * Minv * R from
+    get_hazmath_metric_precond(AA, W, bcs, interface_dofs=...) without
+    parameters (src/emi_3d.py:139), block vectors in and out, PCG as the
+    reference (tolerance 1e-10, src/emi_3d.py:143) with the oracle's count;
+    and the driver's iters table."""
+    M = _M()
+    s = M.problems.emi(3, 16, 1e6)
+    BB = M.precond.get_hazmath_metric_precond(s.blocks, s.W, interface_dofs=s.idofs, num_functions=2)
+    assert BB.monolithic.level_format(0)['rings']
+    b = [M.problems.seeded_rhs(s.W[0], 1234), M.problems.seeded_rhs(s.W[1], 4321)]
+    z = BB * b
+    assert np.array_equal(np.concatenate(z), BB.monolithic * np.concatenate(b))
+    solver = M.ConjGrad(s, precond=BB, tolerance=1e-10, maxiter=500)
+    solver * b
+    A = s.scipy()
+    h = mo.setup(A, mo.Params(**REF_DEFAULT), idofs=s.idofs)
+    ref = mo.pcg(A, h, np.concatenate(b), 1e-10, 500)
+    assert len(solver.residuals) == len(ref.residuals)
+    assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
+
+
+def test_rings_refused_where_not_built(lib_built):
+    """Seed rings are single-GPU and nodal: the multi-GPU setup refuses them
+    with a message; scalar systems refuse the multiplicative overlapping form."""
+    M = _M()
+    s = M.problems.emi(3, 8, 1e4)
+    A = s.scipy()
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.DistMetricAMG(A, s.W, idofs=s.idofs, parameters=M.parameters.parameters_metric_default,
+                        rank=0, nranks=1)
+    assert ei.value.code == -4 and 'SCHWARZ_RINGS' in str(ei.value)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M.MetricAMG(A, None, idofs=s.idofs, parameters=dict(M.parameters.parameters_metric_default,
+                                                             smoother=M.parameters.SMOOTHER_JACOBI_RHO))
+    assert ei.value.code == -4

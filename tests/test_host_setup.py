@@ -28,6 +28,12 @@ CASES = [
     (3, 16, 1e6, dict(num_functions=2, aggregation_type='VMB', AMG_type='UA', strong_coupled=0.1)),
     (2, 32, 1e4, dict(num_functions=2, aggregation_type='VMB')),
     (2, 32, 1e3, dict(aggregation_type='VMB', AMG_type='UA', strong_coupled=0.1)),
+    # the classical strength measure theta sqrt(|a_ii a_jj|) (strength_measure 0):
+    # nodal HEM, scalar VMB, nodal MIS
+    (3, 16, 1e2, dict(num_functions=2, aggregation_type='HEM', AMG_type='UA', strong_coupled=0.1,
+                      strength_measure=0)),
+    (2, 32, 1e3, dict(aggregation_type='VMB', AMG_type='UA', strong_coupled=0.1, strength_measure=0)),
+    (3, 8, 1e4, dict(num_functions=2, strong_coupled=0.05, strength_measure=0)),
 ]
 
 

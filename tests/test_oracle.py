@@ -296,3 +296,23 @@ def test_strength_keeps_a_strong_neighbour_per_coupled_row():
     offs.setdiag(0)
     offs.eliminate_zeros()
     assert (np.diff(Ss.indptr)[np.diff(offs.indptr) > 0] > 0).all()
+
+
+def test_classical_strength_measure_kat():
+    """strength_measure 0 pins the classical definition (Vanek, Mandel,
+    Brezina 1996): j strong for i iff |a_ij| >= theta sqrt(|a_ii| |a_jj|),
+    symmetrised, on a hand-checkable 4 x 4 matrix; measure 1 (the default)
+    thresholds against the row's largest coupling instead."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix(np.array([[4.0, -1.0, -0.1, 0.0],
+                                [-1.0, 9.0, 0.0, -0.5],
+                                [-0.1, 0.0, 1.0, -0.02],
+                                [0.0, -0.5, -0.02, 25.0]]))
+    # classical, theta = 0.1: |a_01| = 1 >= 0.1 sqrt(36) = 0.6 strong; |a_02| = 0.1 >= 0.1 sqrt(4) = 0.2? no;
+    # |a_13| = 0.5 >= 0.1 sqrt(225) = 1.5? no; |a_23| = 0.02 >= 0.1 sqrt(25) = 0.5? no
+    S = mo.strength(A, 0.1, 0).toarray()
+    assert S.tolist() == [[0, 1, 0, 0], [1, 0, 0, 0], [0, 0, 0, 0], [0, 0, 0, 0]]
+    # row maximum, theta = 0.1: row 0 max 1 -> 0.1 >= 0.1 strong (0-2); row 1 max 1 -> 0.5 strong (1-3);
+    # row 2 max 0.1 -> 0.02 < 0.01? no, 0.02 >= 0.01 strong (2-3); row 3 max 0.5 -> 0.02 < 0.05
+    S1 = mo.strength(A, 0.1, 1).toarray()
+    assert S1.tolist() == [[0, 1, 1, 0], [1, 0, 0, 1], [1, 0, 0, 1], [0, 1, 1, 0]]
