@@ -61,6 +61,30 @@ def device_src_sha():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def rss_gb():
+    """peak resident set size of this process (GB)."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
+
+
+def cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max / cfs quota), or None."""
+    try:
+        q, p = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            return int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        p = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            return q / p
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_model():
     try:
         for line in open('/proc/cpuinfo'):
@@ -84,7 +108,8 @@ def main():
                          'with node-aligned blocks, Schwarz_maxlvl 0)')
     ap.add_argument('--rep-nodes', type=int, default=32768,
                     help='multi-GPU: replicate levels with <= this many nodes')
-    ap.add_argument('--cpu-sample', type=int, default=3, help='CPU baseline applies (0: skip)')
+    ap.add_argument('--cpu-sample', type=int, default=10,
+                    help='CPU baseline: timed applies after 2 warm-ups, median reported (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
     ap.add_argument('--pcg', type=int, default=-1,
                     help='run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL); '
@@ -105,6 +130,9 @@ def main():
     ap.add_argument('--exchange', choices=('rccl', 'gloo'), default='rccl',
                     help='N > 1 transport: RCCL (default), or the host-staged gloo exchange '
                          '(mamg_dist_set_exchange; runs several ranks on one GPU, for rehearsals)')
+    ap.add_argument('--host-matrix', action='store_true',
+                    help='N > 1: generate the global A_0 on the host of every rank (before round 4) instead of '
+                         'in each rank\'s HBM')
     ap.add_argument('--compare-host-setup', action='store_true',
                     help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
@@ -135,14 +163,22 @@ def main():
 
     n = M.problems.finest_n(args.dim, args.nrefs, args.problem)
     t0 = time.time()
+    A0dev = None
     if args.problem == 'emi':      # src/emi_3d.py:119-144 (split cube, trace coupling, interface seeds)
         sysm = M.problems.emi(args.dim, n, args.gamma)
         prof['Schwarz_maxlvl'] = 0
+    elif world > 1 and not args.host_matrix:
+        # N > 1: every rank generates A_0 in its own HBM (mamg_gen_bidomain_device,
+        # bitwise the host generator's); no rank holds the global matrix on the
+        # host (13-14 GB of RSS per rank before round 4)
+        A0dev = M.problems.bidomain_device(args.dim, n, args.gamma, device=dev)
+        sysm = M.problems.bidomain_meta(args.dim, n, int(A0dev[1].numel()))
     else:
         sysm = M.problems.bidomain(args.dim, n, args.gamma)
     Aop = sysm.tocsr() if args.problem == 'emi' else sysm   # the operator PCG and the setup share
     t_gen = time.time() - t0
-    log('rank %d: generated %dD n=%d N=%d nnz=%d in %.1fs' % (rank, args.dim, n, sysm.N, sysm.nnz, t_gen))
+    log('rank %d: generated %dD n=%d N=%d nnz=%d in %.1fs%s' % (rank, args.dim, n, sysm.N, sysm.nnz, t_gen,
+                                                               ' (in HBM)' if A0dev is not None else ''))
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
@@ -197,13 +233,16 @@ def main():
         uid = [M.DistMetricAMG.unique_id() if (rank == 0 and not gloo) else None]
         torch.distributed.broadcast_object_list(uid, src=0)
         t0 = time.time()
-        B = M.DistMetricAMG(sysm, sysm.W, idofs=sysm.idofs, rank=rank, nranks=world,
-                            comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local,
+        B = M.DistMetricAMG(A0dev if A0dev is not None else sysm, sysm.W, idofs=sysm.idofs, rank=rank,
+                            nranks=world, comm_id=uid[0], rep_nodes=args.rep_nodes, num_functions=2, device=local,
                             exchange='gloo' if gloo else None, **prof)
         t_setup = time.time() - t0
+        A0dev = None                       # the rank keeps only its operators
+        torch.cuda.empty_cache()
         setup_info = {'path': 'deterministic setup replicated on every rank (GPU setup; host setup if the '
                               'profile is unsupported) + rank-local upload',
-                      'wall_s': round(t_setup, 3)}
+                      'A0': 'host' if hasattr(sysm, 'indptr') else 'generated in HBM per rank',
+                      'wall_s': round(t_setup, 3), 'host_rss_gb_max_rank': round(allmax(rss_gb()), 2)}
         levels = None
         layout = 'bsr2-dist'
         r = torch.as_tensor(B.local_slice(r_full)).to(dev)
@@ -345,18 +384,28 @@ def main():
             poly = mo.poly_weights(mo.Params(smoother='POLY', poly_degree=args.poly_degree,
                                              relaxation=B.params.relaxation, poly_ratio=B.params.poly_ratio))
         ch = cref.CHierarchy(lv, wcycle=args.cycle == 'W', poly=poly)
-        ch.apply(r_full)                                     # warm (page-in)
-        t0 = time.time()
+        # every CPU this process may use: the affinity set, capped by the
+        # cgroup quota when one is set (all the host's cores)
+        aff = len(os.sched_getaffinity(0))
+        quota = cpu_quota()
+        nthr = max(1, min(aff, int(quota))) if quota else aff
+        ch.set_threads(nthr)
+        for _ in range(2):
+            ch.apply(r_full)                                 # warm-ups (page-in, thread pool)
+        times = []
         for _ in range(args.cpu_sample):
+            t0 = time.time()
             zc = ch.apply(r_full)
-        tc = (time.time() - t0) / args.cpu_sample
+            times.append(time.time() - t0)
+        tc = float(np.median(times))
         zg = z.cpu().numpy()
         err = float(np.linalg.norm(zc - zg) / np.linalg.norm(zc))
         cpu = {'value': round(1.0 / tc, 4), 'unit': 'V-cycle applies/s', 'cores': ch.threads(),
-               'kind': 'port', 'nproc': os.cpu_count(),
-               'affinity': len(os.sched_getaffinity(0)), 'cpu_model': cpu_model(),
-               'sample': '%d applies of the full nrefs=%d hierarchy (oracle/vcycle_ref.c, OpenMP), '
-                         'GPU-vs-CPU rel diff %.1e' % (args.cpu_sample, args.nrefs, err)}
+               'kind': 'port', 'nproc': os.cpu_count(), 'affinity': aff, 'cgroup_cpu_quota': quota,
+               'cpu_model': cpu_model(), 'apply_s': [round(t, 4) for t in times],
+               'sample': 'median of %d applies after 2 warm-ups of the full nrefs=%d hierarchy '
+                         '(oracle/vcycle_ref.c, OpenMP, %d threads), GPU-vs-CPU rel diff %.1e'
+                         % (args.cpu_sample, args.nrefs, ch.threads(), err)}
         if args.cpu_pcg and pcg is not None:
             # N1: PCG iteration count of the CPU path (same hierarchy bits,
             # C cycle + C SpMV) against the GPU's (src/bidomain_3d.py:149-157)

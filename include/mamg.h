@@ -188,6 +188,13 @@ int mamg_gen_bidomain(int dim, int64_t n, double gamma, double kappa1,
                       double kappa2, int64_t* rowptr, int32_t* colind,
                       double* values);
 
+/* The same matrix built in device memory by gfx950 kernels (bitwise the host
+ * generator's), into caller buffers d_rowptr[nrows+1], d_colind / d_values[nnz]
+ * (sizes from mamg_gen_bidomain_size); synchronous.  Multi-GPU ranks generate
+ * A_0 in HBM instead of holding it on the host. */
+int mamg_gen_bidomain_device(int dim, int64_t n, double gamma, double kappa1, double kappa2, int64_t nnz,
+                             int64_t* d_rowptr, int32_t* d_colind, double* d_values);
+
 /* Manufactured solution of the bidomain drivers (src/bidomain_2d.py:7-99,
  * src/bidomain_3d.py:7-49): b[nrows] = the right-hand side of the system
  * mamg_gen_bidomain builds (loads, full-flux terms on tags 3/4, Dirichlet
@@ -259,6 +266,14 @@ int mamg_comm_unique_id(void* id);
 int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, int rank, int nranks, const void* comm_id,
                     int64_t rep_nodes, mamg_dhandle** out);
+/* Same with A_0's rowptr / colind / values in device memory (read during
+ * setup only), e.g. from mamg_gen_bidomain_device: no rank holds the global
+ * matrix on the host.  Covers the GPU setup's node-block profiles (the rank's
+ * operators are cut out of the hierarchy in HBM); profiles that plan on the
+ * host return MAMG_ERR_UNSUPPORTED. */
+int mamg_setup_dist_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_idofs,
+                           const mamg_params* params, int rank, int nranks, const void* comm_id,
+                           int64_t rep_nodes, mamg_dhandle** out);
 /* local node range [o0, o1) of level 0; local vectors are field-major
  * [u1(o0:o1); u2(o0:o1)] of length 2*(o1-o0) */
 int mamg_dist_range(const mamg_dhandle* h, int64_t* o0, int64_t* o1, int64_t* nv);

@@ -72,6 +72,8 @@ SIGNATURES = {
     'mamg_gen_bidomain_size': (C.c_int, [C.c_int, C.c_int64, P_I64, P_I64]),
     'mamg_gen_bidomain': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double,
                                     P_I64, P_I32, P_F64]),
+    'mamg_gen_bidomain_device': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int64,
+                                           VP, VP, VP]),
     'mamg_gen_bidomain_mms': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, P_F64]),
     'mamg_bidomain_mms_error': (C.c_int, [C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double,
                                           P_F64, P_F64]),
@@ -93,6 +95,8 @@ SIGNATURES = {
     'mamg_comm_unique_id': (C.c_int, [C.c_char_p]),
     'mamg_setup_dist': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                                   C.c_int, C.c_int, C.c_char_p, C.c_int64, C.POINTER(VP)]),
+    'mamg_setup_dist_device': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
+                                         C.c_int, C.c_int, C.c_char_p, C.c_int64, C.POINTER(VP)]),
     'mamg_dist_range': (C.c_int, [VP, P_I64, P_I64, P_I64]),
     'mamg_dist_apply_bytes': (C.c_int, [VP, P_F64]),
     'mamg_dist_apply_device': (C.c_int, [VP, VP, VP, VP]),

@@ -515,8 +515,10 @@ class GlooExchange:
 class DistMetricAMG:
     """Multi-GPU preconditioner: one process per GPU (``mamg_setup_dist``).
 
-    Every rank passes the same global A (the deterministic host setup is
-    replicated) and applies B to its local slice r_local = [u1(o0:o1);
+    Every rank passes the same global A (the deterministic setup is
+    replicated) -- a host CSR, or a tuple of CUDA tensors already in HBM
+    (``problems.bidomain_device``: no rank then holds the global matrix on the
+    host, ``mamg_setup_dist_device``) -- and applies B to its local slice r_local = [u1(o0:o1);
     u2(o0:o1)] (field-major, length 2*(o1-o0)).  comm_id: bytes from
     ``DistMetricAMG.unique_id()`` on rank 0, broadcast to all ranks; None
     builds a virtual (single-GPU, no RCCL) rank for tests."""
@@ -524,20 +526,26 @@ class DistMetricAMG:
     def __init__(self, A, W=None, idofs=None, parameters=None, rank=0, nranks=1, comm_id=None,
                  rep_nodes=32768, exchange=None, **overrides):
         self._L = _lib.lib()
-        indptr, indices, data, n, m = csr_arrays(A)
+        dev = _device_csr(A)
+        if dev is not None:                      # A_0 already in HBM (mamg_setup_dist_device)
+            csr, n, m = dev
+            self._A = None
+        else:
+            indptr, indices, data, n, m = csr_arrays(A)
+            self._A = (indptr, indices, data)
+            csr = _lib.as_csr_struct(indptr, indices, data, m)
         self.shape = (n, n)
         self.W = _dims(W, n)
         self.params = make_params(parameters, **_with_functions(W, parameters, overrides))
-        self._A = (indptr, indices, data)
-        csr = _lib.as_csr_struct(indptr, indices, data, m)
         if idofs is not None:
             self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
             ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
         else:
             self.idofs, ip, ni = None, None, 0
         h = C.c_void_p()
-        _lib.check(self._L.mamg_setup_dist(C.byref(csr), ip, ni, C.byref(self.params), rank, nranks,
-                                           comm_id, int(rep_nodes), C.byref(h)))
+        setup = self._L.mamg_setup_dist_device if dev is not None else self._L.mamg_setup_dist
+        _lib.check(setup(C.byref(csr), ip, ni, C.byref(self.params), rank, nranks,
+                         comm_id, int(rep_nodes), C.byref(h)))
         self._h = h
         self.rank, self.nranks = rank, nranks
         self._exchange = None

@@ -321,15 +321,15 @@ int mamg_comm_unique_id(void* id) {
   GUARD_END
 }
 
-int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
-                    const mamg_params* params, int rank, int nranks, const void* comm_id,
-                    int64_t rep_nodes, mamg_dhandle** out) {
-  GUARD_BEGIN
-  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
-  *out = nullptr;
-  mamg::CsrView v;
-  int rc = to_view(A, &v);
-  if (rc) return rc;
+namespace {
+// v: the host A_0, or (devA != nullptr) only its sizes -- A_0 then lives in
+// HBM (mamg_setup_dist_device) and every path that would read it on the host
+// is refused
+int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, int rank, int nranks, const void* comm_id, int64_t rep_nodes,
+                    mamg_dhandle** out) {
+  int rc;
+  const int64_t nnz0 = devA ? devA->nnz : v.nnz();
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
@@ -354,8 +354,9 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   if (P.num_functions == 2 && P.node_block_smoother &&
       (P.AMG_type == MAMG_UA_AMG || P.sa_block_diag)) {
     G.device = P.device;
-    mamg::dev_prereserve(P.device, v.nnz(), nranks);   // rank-local layout memory first
-    rc = mamg::upload_a0(v, &G, &dA, &err);
+    mamg::dev_prereserve(P.device, nnz0, nranks);   // rank-local layout memory first
+    if (devA) { dA = *devA; rc = MAMG_OK; }
+    else rc = mamg::upload_a0(v, &G, &dA, &err);
     lap("A0 upload");
     if (!rc) rc = mamg::gpu_setup(dA, S.ptr, S.n, P, &G, &err);
     lap("GPU setup");
@@ -367,6 +368,14 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     const std::string et = e ? e : "";
     const int mode = et == "full" ? 1 : et == "rows" ? 2 : 0;
     if (rc) {
+    } else if (devA && (mode != 0 || G.generic)) {
+      err = "multi-GPU setup from a device A_0: this profile plans on the host from the host matrix "
+            "(CSR-layout smoothers, MAMG_DIST_TEST); pass the host CSR (mamg_setup_dist)";
+      rc = MAMG_ERR_UNSUPPORTED;
+      devA = nullptr;   // not a fallback: reported below
+      mamg::dev_prereserve_release();
+      set_error(err);
+      return rc;
     } else if (mode == 1 || G.generic) {   // generic smoothers: the host plan of the whole hierarchy
       rc = mamg::ghier_download(G, v, &H, &err);
     } else {
@@ -378,6 +387,12 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
     lap(on_device ? "ghost lists" : "hierarchy download");
     if (rc && rc != MAMG_ERR_UNSUPPORTED) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   }
+  if (rc == MAMG_ERR_UNSUPPORTED && devA) {
+    mamg::dev_prereserve_release();
+    set_error("multi-GPU setup from a device A_0 needs the GPU setup's profiles (num_functions 2, node-block "
+              "smoothers, UA or block-diagonal SA): " + err);
+    return MAMG_ERR_UNSUPPORTED;
+  }
   if (rc == MAMG_ERR_UNSUPPORTED) rc = mamg::host_setup(v, S.ptr, S.n, P, &H, &err);
   if (rc) { mamg::dev_prereserve_release(); set_error(err); return rc; }
   mamg::DistHandle* d = nullptr;
@@ -388,6 +403,57 @@ int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   if (rc) { set_error(err); return rc; }
   *out = new mamg_dhandle{d};
   return MAMG_OK;
+}
+}  // namespace
+
+int mamg_setup_dist(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
+                    const mamg_params* params, int rank, int nranks, const void* comm_id,
+                    int64_t rep_nodes, mamg_dhandle** out) {
+  GUARD_BEGIN
+  if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
+  *out = nullptr;
+  mamg::CsrView v;
+  int rc = to_view(A, &v);
+  if (rc) return rc;
+  return setup_dist_impl(v, nullptr, idofs, n_idofs, params, rank, nranks, comm_id, rep_nodes, out);
+  GUARD_END
+}
+
+int mamg_setup_dist_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_idofs,
+                           const mamg_params* params, int rank, int nranks, const void* comm_id,
+                           int64_t rep_nodes, mamg_dhandle** out) {
+  GUARD_BEGIN
+  if (!out || !params || !dA || !dA->rowptr || (dA->nnz > 0 && (!dA->colind || !dA->values))) {
+    set_error("null argument");
+    return MAMG_ERR_ARG;
+  }
+  *out = nullptr;
+  if (dA->nrows <= 0 || dA->ncols <= 0 || dA->nnz < 0 || dA->nrows > INT32_MAX || dA->ncols > INT32_MAX) {
+    set_error("bad CSR sizes");
+    return MAMG_ERR_ARG;
+  }
+  mamg::DevMat M;
+  M.n = dA->nrows;
+  M.m = dA->ncols;
+  M.nnz = dA->nnz;
+  M.ptr = const_cast<int64_t*>(dA->rowptr);
+  M.col = const_cast<int32_t*>(dA->colind);
+  M.val = const_cast<double*>(dA->values);
+  mamg::CsrView v;          // sizes only: nothing on the host reads A_0
+  v.n = M.n;
+  v.m = M.m;
+  return setup_dist_impl(v, &M, idofs, n_idofs, params, rank, nranks, comm_id, rep_nodes, out);
+  GUARD_END
+}
+
+int mamg_gen_bidomain_device(int dim, int64_t n, double gamma, double kappa1, double kappa2, int64_t nnz,
+                             int64_t* d_rowptr, int32_t* d_colind, double* d_values) {
+  GUARD_BEGIN
+  if (!d_rowptr || !d_colind || !d_values) { set_error("null output buffer"); return MAMG_ERR_ARG; }
+  std::string err;
+  int rc = mamg::gen_bidomain_dev(dim, n, gamma, kappa1, kappa2, nnz, d_rowptr, d_colind, d_values, &err);
+  if (rc) set_error(err);
+  return rc;
   GUARD_END
 }
 

@@ -82,6 +82,11 @@ struct RingBlocks {
 int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlvl, int mm, RingBlocks* R,
                     std::string* err);
 void ring_blocks_free(RingBlocks* R);
+// the bidomain generator (gen.cpp) on the current device into caller
+// buffers (ptr[2 nv + 1], colind / values[nnz] with nnz from
+// gen_bidomain_size); bitwise the host generator's matrix
+int gen_bidomain_dev(int dim, int64_t n, double gamma, double k1, double k2, int64_t nnz, int64_t* ptr,
+                     int32_t* colind, double* values, std::string* err);
 // host CSR -> HBM, buffers owned by G (G->device selects the GPU)
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err);
 

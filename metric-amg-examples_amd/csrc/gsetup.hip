@@ -2522,6 +2522,173 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
   return MAMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The bidomain generator (gen.cpp) on the device: one thread per vertex
+// computes the vertex's integer P1 stencil on the Kuhn-split lattice and
+// writes its two rows; same operations as the host generator (this file is
+// compiled without FMA contraction), so the matrix is bitwise the host's.
+// Multi-GPU ranks build A_0 in HBM this way instead of holding the global
+// matrix in host memory (13 GB per rank at nrefs=6).
+// ---------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ bool gen_bc(int dim, int64_t n, int64_t v) {
+  const int64_t nn = n + 1;
+  const int64_t a = dim == 2 ? v % nn : v / (nn * nn);
+  return a == 0 || a == n;
+}
+
+__device__ __forceinline__ int gen_kpath(int dim, int a, int b) {
+  if (a == b) return (a == 0 || a == dim) ? 1 : 2;
+  return (a - b == 1 || b - a == 1) ? -1 : 0;
+}
+
+// the vertex's stencil in column order: cnt entries of (column, cK, cM)
+__device__ int gen_stencil(int dim, int64_t n, int64_t v, int64_t* col, int* cK, int* cM) {
+  const int64_t nn = n + 1;
+  const int64_t c[3] = {v % nn, (v / nn) % nn, dim == 3 ? v / (nn * nn) : 0};
+  const int64_t stride[3] = {1, nn, nn * nn};
+  int accK[27], accM[27];
+  bool used[27];
+  for (int s = 0; s < 27; ++s) { accK[s] = 0; accM[s] = 0; used[s] = false; }
+  const int perms3[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+  const int perms2[2][3] = {{0, 1, 0}, {1, 0, 0}};
+  const int ncorner = dim == 3 ? 8 : 4, npath = dim == 3 ? 6 : 2;
+  for (int q = 0; q < ncorner; ++q) {
+    const int d[3] = {q & 1, (q >> 1) & 1, (q >> 2) & 1};
+    bool ok = true;
+    for (int k = 0; k < dim; ++k) {
+      const int64_t lo = c[k] - d[k];
+      if (lo < 0 || lo >= n) ok = false;
+    }
+    if (!ok) continue;
+    for (int pth = 0; pth < npath; ++pth) {
+      const int* perm = dim == 3 ? perms3[pth] : perms2[pth];
+      int pv[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+      for (int t = 1; t <= dim; ++t) {
+        for (int k = 0; k < 3; ++k) pv[t][k] = pv[t - 1][k];
+        pv[t][perm[t - 1]] += 1;
+      }
+      int t_me = -1;
+      for (int t = 0; t <= dim; ++t)
+        if (pv[t][0] == d[0] && pv[t][1] == d[1] && pv[t][2] == d[2]) t_me = t;
+      if (t_me < 0) continue;
+      for (int s = 0; s <= dim; ++s) {
+        const int slot = (pv[s][0] - d[0] + 1) + 3 * (pv[s][1] - d[1] + 1) + 9 * (pv[s][2] - d[2] + 1);
+        used[slot] = true;
+        accK[slot] += gen_kpath(dim, t_me, s);
+        accM[slot] += (t_me == s) ? 2 : 1;
+      }
+    }
+  }
+  int cnt = 0;
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int slot = (dx + 1) + 3 * (dy + 1) + 9 * (dz + 1);
+        if (!used[slot]) continue;
+        col[cnt] = v + dx * stride[0] + dy * stride[1] + dz * stride[2];
+        cK[cnt] = accK[slot];
+        cM[cnt] = accM[slot];
+        ++cnt;
+      }
+  return cnt;
+}
+
+// row length of vertex v's rows (2 k, or 1 on a Dirichlet vertex)
+__global__ __launch_bounds__(256) void gen_len_kernel(int dim, int64_t n, int64_t nv, int64_t* __restrict__ len) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= nv) return;
+  if (gen_bc(dim, n, v)) { len[v] = 1; return; }
+  int64_t col[27];
+  int cK[27], cM[27];
+  const int cnt = gen_stencil(dim, n, v, col, cK, cM);
+  int k = 0;
+  for (int j = 0; j < cnt; ++j) k += !gen_bc(dim, n, col[j]);
+  len[v] = 2 * k;
+}
+
+// rowptr of the u1 rows [0, nv] and the u2 rows [nv, 2 nv] from the
+// inclusive scan of the lengths
+__global__ __launch_bounds__(256) void gen_ptr_kernel(int64_t nv, const int64_t* __restrict__ scan,
+                                                      int64_t* __restrict__ ptr) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v > nv) return;
+  const int64_t s = v ? scan[v - 1] : 0;
+  ptr[v] = s;
+  ptr[nv + v] = scan[nv - 1] + s;
+}
+
+__global__ __launch_bounds__(256) void gen_fill_kernel(int dim, int64_t n, int64_t nv, double kf1, double kf2,
+                                                       double mf, const int64_t* __restrict__ ptr,
+                                                       int32_t* __restrict__ colind, double* __restrict__ values) {
+#pragma clang fp contract(off)
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= nv) return;
+  const int64_t p1 = ptr[v], p2 = ptr[nv + v];
+  if (gen_bc(dim, n, v)) {
+    colind[p1] = (int32_t)v; values[p1] = 1.0;
+    colind[p2] = (int32_t)(v + nv); values[p2] = 1.0;
+    return;
+  }
+  int64_t col[27];
+  int cK[27], cM[27];
+  const int cnt = gen_stencil(dim, n, v, col, cK, cM);
+  int k = 0;
+  for (int j = 0; j < cnt; ++j)
+    if (!gen_bc(dim, n, col[j])) { col[k] = col[j]; cK[k] = cK[j]; cM[k] = cM[j]; ++k; }
+  for (int j = 0; j < k; ++j) {
+    const double fK = (double)cK[j], fM = (double)cM[j];
+    const double a11 = kf1 * fK + mf * fM, a22 = kf2 * fK + mf * fM, a12 = -(mf * fM);
+    colind[p1 + j] = (int32_t)col[j];
+    values[p1 + j] = a11;
+    colind[p1 + k + j] = (int32_t)(col[j] + nv);
+    values[p1 + k + j] = a12;
+    colind[p2 + j] = (int32_t)col[j];
+    values[p2 + j] = a12;
+    colind[p2 + k + j] = (int32_t)(col[j] + nv);
+    values[p2 + k + j] = a22;
+  }
+}
+
+}  // namespace
+
+int gen_bidomain_dev(int dim, int64_t n, double gamma, double k1, double k2, int64_t nnz, int64_t* ptr,
+                     int32_t* colind, double* values, std::string* err) {
+  if ((dim != 2 && dim != 3) || n < 1) { *err = "gen_bidomain_device: dim must be 2 or 3 and n >= 1"; return MAMG_ERR_ARG; }
+  const int64_t nn = n + 1, nv = dim == 3 ? nn * nn * nn : nn * nn;
+  if (2 * nv >= (int64_t)INT32_MAX) { *err = "gen_bidomain_device: too many rows for int32 columns"; return MAMG_ERR_ARG; }
+  // the host generator's factors (gen.cpp gen_bidomain), computed on the host
+  const double h = 1.0 / (double)n;
+  double kf1, kf2, mf;
+  if (dim == 3) {
+    kf1 = k1 * h / 6.0;
+    kf2 = k2 * h / 6.0;
+    mf = gamma * h * h * h / 120.0;
+  } else {
+    kf1 = k1 / 2.0;
+    kf2 = k2 / 2.0;
+    mf = gamma * h * h / 24.0;
+  }
+  Scratch S;
+  int64_t* len = nullptr;
+  RCHK(S.alloc(&len, nv, err));
+  gen_len_kernel<<<nblk(nv), 256>>>(dim, n, nv, len);
+  HIPCHK(hipGetLastError());
+  RCHK(dscan_incl_i64(len, len, nv, nullptr, err));
+  int64_t half = 0;
+  RCHK(to_host(&half, len + nv - 1, 1, err));
+  if (2 * half != nnz) {
+    *err = "gen_bidomain_device: nnz " + std::to_string(nnz) + " != the generator's " + std::to_string(2 * half);
+    return MAMG_ERR_ARG;
+  }
+  gen_ptr_kernel<<<nblk(nv + 1), 256>>>(nv, len, ptr);
+  gen_fill_kernel<<<nblk(nv), 256>>>(dim, n, nv, kf1, kf2, mf, ptr, colind, values);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return MAMG_OK;
+}
+
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   HIPCHK(hipSetDevice(G->device));
   Clock clk;

@@ -70,6 +70,52 @@ def bidomain(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float 
     return System(indptr, indices, data, int(N.value), int(N.value) // 2, dim, n, float(gamma))
 
 
+@dataclasses.dataclass
+class SystemMeta:
+    """Sizes and seeds of a bidomain system whose matrix lives elsewhere (in
+    HBM, bidomain_device): what a multi-GPU rank needs on the host."""
+    N: int
+    nv: int
+    dim: int
+    n: int
+    nnz: int
+
+    @property
+    def idofs(self) -> np.ndarray:
+        return np.arange(self.nv, 2 * self.nv, dtype=np.int32)
+
+    @property
+    def W(self):
+        return [self.nv, self.nv]
+
+
+def bidomain_meta(dim: int, n: int, nnz: int) -> SystemMeta:
+    nv = (n + 1) ** dim
+    return SystemMeta(2 * nv, nv, dim, n, int(nnz))
+
+
+def bidomain_device(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0, device=None):
+    """The same matrix as ``bidomain`` built in HBM by the gfx950 generator
+    (mamg_gen_bidomain_device, bitwise the host generator's): a tuple of CUDA
+    tensors (indptr int64, indices int32, data float64) for MetricAMG /
+    DistMetricAMG, so a rank of a multi-GPU job never holds the global matrix
+    on the host."""
+    import ctypes as C
+    import torch
+    L = _lib.lib()
+    N, nnz = C.c_int64(), C.c_int64()
+    _lib.check(L.mamg_gen_bidomain_size(dim, n, C.byref(N), C.byref(nnz)))
+    dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
+    ip = torch.empty(N.value + 1, dtype=torch.int64, device=dev)
+    ix = torch.empty(nnz.value, dtype=torch.int32, device=dev)
+    dv = torch.empty(nnz.value, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.device(dev):
+        _lib.check(L.mamg_gen_bidomain_device(dim, n, gamma, kappa1, kappa2, nnz.value, C.c_void_p(ip.data_ptr()),
+                                              C.c_void_p(ix.data_ptr()), C.c_void_p(dv.data_ptr())))
+    return ip, ix, dv
+
+
 def bidomain_mms_rhs(dim: int, n: int, gamma: float, kappa1: float = 2.0, kappa2: float = 3.0) -> np.ndarray:
     """Right-hand side of bidomain(dim, n, ...) for the reference's manufactured
     solution (src/bidomain_2d.py:7-99, src/bidomain_3d.py:7-49; csrc/mms.cpp)."""

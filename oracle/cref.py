@@ -39,6 +39,8 @@ def _lib():
     L.oracle_set_poly.restype = C.c_int
     L.oracle_set_poly.argtypes = [C.c_int, C.c_void_p]
     L.oracle_num_threads.restype = C.c_int
+    L.oracle_set_threads.restype = None
+    L.oracle_set_threads.argtypes = [C.c_int]
     L.oracle_pcg.restype = C.c_int
     L.oracle_pcg.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                              C.c_void_p, C.c_double, C.c_int, C.c_void_p, C.c_void_p]
@@ -113,6 +115,9 @@ class CHierarchy:
 
     def threads(self):
         return self.L.oracle_num_threads()
+
+    def set_threads(self, n):
+        self.L.oracle_set_threads(int(n))
 
 
 def _tup(M):

@@ -144,6 +144,15 @@ int oracle_apply(olevel* L, int nlev, int wcyc, int nu1, int nu2, int maxit, con
   return 0;
 }
 
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+  extern void omp_set_num_threads(int);
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
 int oracle_num_threads(void) {
   int n = 1;
 #pragma omp parallel

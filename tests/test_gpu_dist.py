@@ -460,3 +460,49 @@ def test_two_processes_host_exchange(lib_built, problem, kw):
         assert np.allclose(resid, ref.residuals, rtol=1e-6, atol=0)
     assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
     assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-6
+
+
+@pytest.mark.parametrize('dim,n', [(2, 64), (3, 16), (3, 33)])
+def test_device_generator_bitwise(lib_built, dim, n):
+    """mamg_gen_bidomain_device (gfx950 kernels, no FMA contraction) builds
+    the host generator's matrix bit for bit."""
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(dim, n, 1e6)
+    ip, ix, dv = M.problems.bidomain_device(dim, n, 1e6)
+    assert np.array_equal(ip.cpu().numpy(), s.indptr)
+    assert np.array_equal(ix.cpu().numpy(), s.indices)
+    assert np.array_equal(dv.cpu().numpy(), s.data)
+
+
+@pytest.mark.parametrize('P,kw', [(2, {}), (4, dict(smoother='SGS', coarse_scaling=1, cycle_type='W'))])
+def test_dist_setup_from_device_matrix(lib_built, P, kw):
+    """mamg_setup_dist_device: every rank sets up from A_0 generated in its
+    HBM (no host matrix); the virtual-rank applies are bitwise those of the
+    ranks set up from the host matrix, and equal the oracle."""
+    import torch
+    import metric_amg_examples_amd as M
+    ck = dict(kw)
+    if 'smoother' in ck:
+        ck['smoother'] = {'SGS': 11}[ck['smoother']]
+        ck['Schwarz_type'] = M.parameters.SCHWARZ_SEED_BLOCKS
+    if 'cycle_type' in ck:
+        ck['cycle_type'] = {'W': 2}[ck['cycle_type']]
+    s = M.problems.bidomain(3, 16, 1e6)
+    A0 = M.problems.bidomain_device(3, 16, 1e6)
+    meta = M.problems.bidomain_meta(3, 16, int(A0[1].numel()))
+    r = mo.seeded_rhs(s.N)
+    outs = []
+    for A in (s, A0):
+        hs = [M.DistMetricAMG(A, meta.W, idofs=meta.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                              num_functions=2, **ck) for p in range(P)]
+        rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+        zs = [torch.zeros_like(x) for x in rs]
+        M.DistMetricAMG.virtual_apply(hs, rs, zs)
+        torch.cuda.synchronize()
+        outs.append(_gather(s, hs, zs))
+        for hh in hs:
+            hh.close()
+    assert np.array_equal(outs[0], outs[1])
+    okw = dict(kw, Schwarz_type=7) if kw else {}
+    h = mo.setup(s.scipy(), mo.Params(num_functions=2, **okw), idofs=s.idofs)
+    assert np.linalg.norm(outs[0] - h.apply(r)) / np.linalg.norm(outs[0]) < 1e-10
