@@ -561,120 +561,6 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
   vset(out, os, node, 1, o1);
 }
 
-// hsell2_kernel with two lanes per node row: part 0 sums the lower blocks
-// (mirror pointers), part 1 the upper blocks then the ghost blocks, and the
-// row's sum is lower + (upper + ghost) on both lanes (__shfl_xor 32).  A
-// workgroup takes half of a 256-row block of the one-lane kernel: workgroup
-// b = 8 i + x (XCD x) takes half i & 1 of the one-lane kernel's workgroup
-// x + 8 (i >> 1), so every XCD walks the same rows in the same band order.
-template <int EPI, bool XFM, int U, bool GH, int TAG>
-__global__ __launch_bounds__(256) void hsell2x2_kernel(
-    int64_t row0, int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
-    const double* __restrict__ uval, int64_t nbs, int hwu, const int32_t* __restrict__ lptr, int hwl,
-    const int64_t* __restrict__ gsoff, const int32_t* __restrict__ gcol, const double* __restrict__ gval,
-    int64_t ngs, const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
-    int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap,
-    const int32_t* __restrict__ sched, uint32_t G) {
-  const uint32_t bx = blockIdx.x, xcd = bx & 7, i = bx >> 3;
-  const uint32_t ob = xcd + 8 * (i >> 1);
-  if (ob >= G) return;
-  const int64_t blk0 = sched ? (int64_t)sched[ob] : row_block_of(ob, G, remap);
-  const int lane = threadIdx.x & 63, q = lane >> 5;
-  const int64_t node0 = row0 + blk0 * 256 + (i & 1) * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
-  const bool live = node0 < nr;
-  const int64_t node = live ? node0 : nr - 1;
-  const double* offd = uval + 2 * nbs;
-  const int m = meta[node];
-  const uint32_t urow = 64u * (uint32_t)hwu;
-  double s0 = 0.0, s1 = 0.0;
-  if (q == 0) {
-    const int llen = (m >> 8) & 0xff;
-    const int64_t k = (node >> 6) * (int64_t)(64 * hwl) + (node & 63);
-    for (int j = 0; j < llen; j += U) {
-      uint32_t p[U];
-      dv4 v[U];
-      double2 a[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) p[u] = (uint32_t)lptr[k + (int64_t)SELL_C * (j + u < llen ? j + u : llen - 1)];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t c = (int32_t)((p[u] / urow) * 64u + (p[u] & 63u));
-        v[u] = blk<true>(uval, offd, p[u]);
-        a[u] = xget<XFM>(x, xs, c);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool ok = j + u < llen;
-        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
-        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
-      }
-    }
-  } else {
-    const int ulen = m & 0xff;
-    const int64_t k = (node >> 6) * (int64_t)urow + (node & 63);
-    for (int j = 0; j < ulen; j += U) {
-      int32_t c[U];
-      dv4 v[U];
-      double2 a[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t kk = k + (int64_t)SELL_C * (j + u < ulen ? j + u : ulen - 1);
-        c[u] = ucol[kk];
-        v[u] = blk<true>(uval, offd, kk);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool ok = j + u < ulen;
-        s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
-        s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
-      }
-    }
-    if (GH) {
-      const int glen = m >> 16;
-      const int64_t kg = gsoff[node >> 6] + (node & 63);
-      const double* goff = gval + 2 * ngs;
-      for (int j = 0; j < glen; j += U) {
-        int32_t c[U];
-        dv4 v[U];
-        double2 a[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t kk = kg + (int64_t)SELL_C * (j + u < glen ? j + u : glen - 1);
-          c[u] = gcol[kk];
-          v[u] = blk<true>(gval, goff, kk);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) a[u] = xget<XFM>(x, xs, c[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const bool ok = j + u < glen;
-          s0 += ok ? v[u].x * a[u].x + v[u].y * a[u].y : 0.0;
-          s1 += ok ? v[u].z * a[u].x + v[u].w * a[u].y : 0.0;
-        }
-      }
-    }
-  }
-  s0 += __shfl_xor(s0, 32);
-  s1 += __shfl_xor(s1, 32);
-  if (!live) return;
-  const int f = q;
-  double o;
-  if (EPI == EPI_Y) {
-    o = f ? s1 : s0;
-  } else if (EPI == EPI_YADD) {
-    o = y[2 * node + f] + (f ? s1 : s0);
-  } else if (EPI == EPI_RESID) {
-    o = vget(b, bs, node, f) - (f ? s1 : s0);
-  } else {  // EPI_BJAC
-    const double r0 = vget(b, bs, node, 0) - s0, r1 = vget(b, bs, node, 1) - s1;
-    const dv2 w = reinterpret_cast<const dv2*>(W + node)[f];
-    o = y[2 * node + f] + (w.x * r0 + w.y * r1);
-  }
-  vset(out, os, node, f, o);
-}
-
 // fused prolongation + first post sweep on a SELL-64 [P | AP] (see
 // bsr2_post_kernel).  Rows are sorted by length inside windows of
 // SELL_SIGMA rows (slot i holds row perm[i]) so a wavefront's lanes have
@@ -1807,24 +1693,15 @@ int g_half = 1;
 int g_half_bands = 1;
 int g_post_k = 1;
 int g_kvar = 0;
-int g_rvar = 0;
-int g_rrvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
 int64_t g_msell_min_rows = (int64_t)1 << 40;
 int64_t g_tail_nodes = 0;
 bool g_tail_set = false;   // MAMG_TAIL_NODES given: applies to every smoother (tests)   // off: coarse levels 0.41 -> 0.50 ms
 int g_tail_vl = 4;           // lanes per row cap inside the coarse tail (MAMG_TAIL_VL; 1/2/4/8/64 measured)
-void read_kvar() {
-  const char* e = std::getenv("MAMG_K_VARIANT");
-  g_kvar = e ? std::atoi(e) : 0;
-  e = std::getenv("MAMG_R_VARIANT");
-  g_rvar = e ? std::atoi(e) : 0;
-  e = std::getenv("MAMG_RR_VARIANT");
-  g_rrvar = e ? std::atoi(e) : 0;
-}
 void read_knobs() {
-  read_kvar();
-  const char* e = std::getenv("MAMG_POST_K");
+  const char* e = std::getenv("MAMG_K_VARIANT");   // the level-0 K kernel (tests; read at upload)
+  g_kvar = e ? std::atoi(e) : 0;
+  e = std::getenv("MAMG_POST_K");
   g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
@@ -2094,10 +1971,12 @@ void poison_doubles(T* p, size_t bytes) {
   }
 }
 
-// free a device buffer once the device has drained: copies and kernels that
-// read it are asynchronous to the host, and freed memory can be handed to
-// the next allocation and overwritten under them (see TmpPool)
-inline void drained_free(void* p) { free_after_drain(p, "drained_free"); }
+// free a handle-owned (hipMalloc) array replaced during the upload, behind
+// its last reader on the null stream (dmem.h ordered_free)
+inline void drained_free(void* p) { ordered_free(p); }
+
+// wait for the layout builder's queued work (all of it on the null stream)
+inline hipError_t null_sync() { return hipStreamSynchronize(nullptr); }
 
 // device allocation owned by a handle (single-GPU or multi-GPU: both keep `allocs`)
 template <class HT, class T>
@@ -2513,19 +2392,18 @@ struct TBsr {
   dv4* val = nullptr;
 };
 
-// scoped temporaries of the layout builder.  A temporary is freed only after
-// the device has drained: the kernels reading it are queued asynchronously
-// to the host, and memory freed under a running kernel can be handed to the
-// next allocation and overwritten before that kernel has read it
+// scoped temporaries of the layout builder, null-stream ordered (dmem.h):
+// the layout kernels that read them are queued on the null stream, and
+// hipFreeAsync there returns a block to the pool only behind them
 struct TmpPool {
   std::vector<void*> v;
   ~TmpPool() {
-    for (void* p : v) free_after_drain(p, "TmpPool::~TmpPool");
+    for (void* p : v) tmp_free(p);
   }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
     void* q = nullptr;
-    HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+    HIPCHK(tmp_malloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
     v.push_back(q);
     *p = (T*)q;
     poison_doubles(*p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
@@ -2534,7 +2412,7 @@ struct TmpPool {
   void release(void* p) {
     for (auto& q : v)
       if (q == p) {
-        free_after_drain(q, "TmpPool::release");
+        tmp_free(q);
         q = nullptr;
       }
   }
@@ -2775,7 +2653,6 @@ int upload_half_or_bsr(HT* h, const HBsr& B, DBsr* D, std::string* err) {
     D->lanes = pick_lanes_bsr(B.nr, D->nb);
     D->sym = true;
     if ((rc = try_half(h, &T, tb, D, err))) return rc;
-    HIPCHK(hipDeviceSynchronize());
     if (D->half) return MAMG_OK;
   }
   return upload_bsr(h, B, D, 0, err, true);
@@ -3057,18 +2934,6 @@ __global__ __launch_bounds__(256) void unsplit_local_kernel(int64_t nbs, const d
   out[k] = blk_split_local(in, k);
 }
 // SELL slice s (64 w_s slots) moved from soff_old[s] to soff_new[s] (one workgroup per slice)
-__global__ __launch_bounds__(256) void slice_move_kernel(int64_t ns, const int64_t* __restrict__ so,
-                                                         const int64_t* __restrict__ sn, const dv4* __restrict__ vin,
-                                                         const int32_t* __restrict__ cin, dv4* __restrict__ vout,
-                                                         int32_t* __restrict__ cout) {
-  const int64_t sl = blockIdx.x;
-  if (sl >= ns) return;
-  const int64_t a = so[sl], len = so[sl + 1] - so[sl], d = sn[sl];
-  for (int64_t i = threadIdx.x; i < len; i += 256) {
-    vout[d + i] = vin[a + i];
-    cout[d + i] = cin[a + i];
-  }
-}
 __global__ __launch_bounds__(256) void unsplit_blocks_kernel(int64_t nbs, const dv2* __restrict__ in, dv4* __restrict__ out) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= nbs) return;
@@ -3268,8 +3133,7 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   const int64_t nrp = D->gcs.empty() ? 0 : D->gcs.back();
   if (nrp) rest_mask_kernel<<<nblocks(nrp), 256>>>(nrp, D->gperm, dcov, D->Gd);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipDeviceSynchronize());   // ring_blocks_dev's buffers are freed by the guard
-  return MAMG_OK;
+  return MAMG_OK;   // ring_blocks_dev's buffers: freed by the guard, null-stream ordered
 }
 
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
@@ -3338,7 +3202,6 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
     if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
   }
-  HIPCHK(hipDeviceSynchronize());
   return MAMG_OK;
 }
 
@@ -3899,11 +3762,7 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
   if (g == 0) return;
 #define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o)
   switch (o.epi) {
-    case EPI_Y:
-      // the level-0 restriction with non-temporal matrix loads (A/B, MAMG_RR_VARIANT=1)
-      if (TAG == 0 && o.remap && g_rrvar == 1) bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG, true><<<g, 256, 0, s>>>(BSR_ARGS);
-      else bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS);
-      break;
+    case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_KPOST:   // K is never symmetric and e is node-major
@@ -4056,17 +3915,6 @@ void launch_half_u(const Op& o, hipStream_t s) {
     o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, 1, \
     (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched \
     : (r0 == M.sr0 && r1 == M.sr1 && (int64_t)g == M.nsched_r) ? M.sched_r : nullptr
-  if (g_rvar == 1) {   // two lanes per row (A/B, MAMG_R_VARIANT)
-    const unsigned g2 = 16 * ((g + 7) / 8);
-    switch (o.epi) {
-      case EPI_Y: hsell2x2_kernel<EPI_Y, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
-      case EPI_YADD: hsell2x2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
-      case EPI_RESID: hsell2x2_kernel<EPI_RESID, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
-      case EPI_KPOST: break;
-      default: hsell2x2_kernel<EPI_BJAC, XFM, U, GH, TAG><<<g2, 256, 0, s>>>(HALF_ARGS, g); break;
-    }
-    return;
-  }
   switch (o.epi) {
     case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
@@ -4577,16 +4425,17 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   std::vector<Op> ops;
   apply_ops(h.get(), h->hr, h->hz, &ops);
   for (const Op& o : ops) h->apply_bytes += o.bytes;
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(null_sync());
   const auto t1 = std::chrono::steady_clock::now();
   h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
   rehome_operators(h.get());
   const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
-  // every layout kernel and device-to-device copy (asynchronous to the host)
-  // done before the handle is used on another stream
-  HIPCHK(hipDeviceSynchronize());
+  // every layout kernel and device-to-device copy (null stream) ordered
+  // before the handle's first use on any stream (order_begin waits on it)
+  if ((rc = order_end(h.get(), nullptr, err))) return rc;
+  HIPCHK(hipEventSynchronize(h->last));
   h->layout_ms[LT_FINISH] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
   *out = h.release();
@@ -4745,14 +4594,15 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   apply_ops(h.get(), h->hr, h->hz, &ops);
   for (const Op& o : ops) h->apply_bytes += o.bytes;
   for (int k = 0; k < 8; ++k) h->setup_ms[k] = G->phase_ms[k];
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(null_sync());
   const auto t1 = std::chrono::steady_clock::now();
   h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
   rehome_operators(h.get());
   const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
-  HIPCHK(hipDeviceSynchronize());   // as in dev_upload
+  if ((rc = order_end(h.get(), nullptr, err))) return rc;   // as in dev_upload
+  HIPCHK(hipEventSynchronize(h->last));
   const auto t3 = std::chrono::steady_clock::now();
   h->layout_ms[LT_FINISH] = std::chrono::duration<double, std::milli>(t3 - t2).count();
   h->setup_ms[GS_LAYOUT] = std::chrono::duration<double, std::milli>(t3 - t0).count();
@@ -4770,7 +4620,10 @@ void dev_layout_ms(const DeviceHandle* h, double* ms4) {
 void dev_destroy(DeviceHandle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  (void)hipDeviceSynchronize();
+  // every use of the handle (applies, PCG, timing, host applies) recorded
+  // h->last on its stream: wait for that, not for the device
+  if (h->last) (void)hipEventSynchronize(h->last);
+  if (h->cap) (void)hipStreamSynchronize(h->cap);
   delete h;
 }
 
@@ -4957,99 +4810,6 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
   hipStream_t s = (hipStream_t)stream;
   int rc = order_begin(h, s, err);
   if (rc) return rc;
-  read_kvar();   // A/B of the K kernel variants on one upload (eager launches)
-  if (const char* mv = std::getenv("MAMG_KMOVE")) {
-    // placement diagnosis: move one of the level-0 K
-    // kernel's arrays into a fresh allocation (same bytes), so its time can be
-    // compared across placements within one process.  val / col: K's values /
-    // columns; x1 / r1 / w: the epilogue vectors; e: the coarse correction;
-    // a trailing '+' asks for a physically contiguous allocation
-    if (h->bsr && h->L.size() > 1 && *mv) {
-      DLevel& L = h->L[0];
-      const int64_t nv = L.n / 2;
-      const std::string w = mv;
-      void** ptr = nullptr;
-      size_t bytes = 0;
-      const bool contig = !w.empty() && w.back() == '+';   // "val+": physically contiguous allocation
-      const std::string wn = contig ? w.substr(0, w.size() - 1) : w;
-      if (wn == "val") { ptr = (void**)&L.KPb.val; bytes = (size_t)L.KPb.nbs * 4 * sizeof(double); }
-      else if (wn == "col") { ptr = (void**)&L.KPb.col; bytes = (size_t)L.KPb.nbs * sizeof(int32_t); }
-      else if (wn == "x1") { ptr = (void**)&L.t; bytes = (size_t)L.n * sizeof(double); }
-      else if (wn == "r1") { ptr = (void**)&L.r; bytes = (size_t)L.n * sizeof(double); }
-      else if (wn == "w") { ptr = (void**)&L.Wd; bytes = (size_t)nv * sizeof(dv4); }
-      else if (wn == "e") { ptr = (void**)&h->L[1].x; bytes = (size_t)h->L[1].n * sizeof(double); }
-      if (ptr) {
-        void* r = nullptr;
-        HIPCHK(hipDeviceSynchronize());
-        if (contig) HIPCHK(hipExtMallocWithFlags(&r, bytes, hipDeviceMallocContiguous));
-        else HIPCHK(hipMalloc(&r, bytes));
-        HIPCHK(hipMemcpy(r, *ptr, bytes, hipMemcpyDeviceToDevice));
-        void* old = *ptr;
-        *ptr = r;
-        h->allocs.push_back(r);
-        const bool in_arena = (char*)old >= h->arena0 && (char*)old < h->arena1;
-        auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
-        if (!in_arena && it != h->allocs.end()) {
-          drained_free(old);
-          h->allocs.erase(it);
-        }
-        for (auto& g : h->graphs) {   // captured with the old pointer
-          (void)hipGraphExecDestroy(g.exec);
-          (void)hipGraphDestroy(g.graph);
-        }
-        h->graphs.clear();
-        for (auto& g : h->pcgs) g.release();
-        h->pcgs.clear();
-        for (auto& t : h->tails) (void)hipFree(t.prog);
-        h->tails.clear();
-        if (std::getenv("MAMG_KMOVE_PRINT"))
-          std::fprintf(stderr, "[mamg] moved %s (%zu B) %p -> %p\n", mv, bytes, old, r);
-      }
-    }
-  }
-  if (const char* ks = std::getenv("MAMG_K_SHUFFLE"))   // A/B: SELL slices of K stored in a scrambled order
-    if (h->bsr && h->L.size() > 1 && h->L[0].KPb.sell && !h->L[0].KPb.split && std::atoi(ks) > 0) {
-      DBsr& K = h->L[0].KPb;
-      const int64_t ns = (K.nr + SELL_C - 1) / SELL_C;
-      std::vector<int64_t> so(ns + 1), sn(ns + 1, 0);
-      HIPCHK(hipMemcpy(so.data(), K.soff, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-      // storage order: groups of G consecutive slices; group g stored at place
-      // (g A) mod ngr with A odd, coprime to ngr and ~ngr / golden ratio, so
-      // consecutive groups land far apart; offsets by a scan in storage order
-      const int64_t G = std::max<int64_t>(1, std::atoll(ks));
-      const int64_t ngr = (ns + G - 1) / G;
-      int64_t A = (int64_t)((double)ngr * 0.6180339887) | 1;
-      while (std::gcd(A, ngr) != 1) A += 2;
-      std::vector<int64_t> order(ngr);
-      for (int64_t g = 0; g < ngr; ++g) order[(int64_t)(((__int128)g * A) % ngr)] = g;
-      int64_t off = 0;
-      for (int64_t pl = 0; pl < ngr; ++pl)
-        for (int64_t sl = order[pl] * G; sl < std::min(ns, order[pl] * G + G); ++sl) {
-          sn[sl] = off;
-          off += so[sl + 1] - so[sl];
-        }
-      int64_t* dsn = nullptr;
-      dv4* nv = nullptr;
-      int32_t* nc = nullptr;
-      HIPCHK(hipMalloc(&dsn, (ns + 1) * sizeof(int64_t)));
-      HIPCHK(hipMalloc(&nv, (size_t)K.nbs * sizeof(dv4)));
-      HIPCHK(hipMalloc(&nc, (size_t)K.nbs * sizeof(int32_t)));
-      sn[ns] = off;
-      HIPCHK(hipMemcpy(dsn, sn.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-      slice_move_kernel<<<(unsigned)ns, 256>>>(ns, K.soff, dsn, reinterpret_cast<const dv4*>(K.val), K.col, nv, nc);
-      HIPCHK(hipDeviceSynchronize());
-      HIPCHK(hipMemcpy(K.val, nv, (size_t)K.nbs * sizeof(dv4), hipMemcpyDeviceToDevice));
-      HIPCHK(hipMemcpy(K.col, nc, (size_t)K.nbs * sizeof(int32_t), hipMemcpyDeviceToDevice));
-      HIPCHK(hipMemcpy(K.soff, dsn, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
-      drained_free(dsn); drained_free(nv); drained_free(nc);
-      for (auto& g : h->graphs) { (void)hipGraphExecDestroy(g.exec); (void)hipGraphDestroy(g.graph); }
-      h->graphs.clear();
-    }
-  if (const char* kl = std::getenv("MAMG_K_LAYOUT"))
-    if (h->bsr && h->L.size() > 1) {
-      set_k_split(h->L[0].KPb, std::strcmp(kl, "split") == 0 ? 1 : std::strcmp(kl, "split2") == 0 ? 2 : 0);
-      HIPCHK(hipDeviceSynchronize());
-    }
   std::vector<Op> ops;
   apply_ops(h, d_r, d_z, &ops);
   if (class_bytes) {
@@ -5254,6 +5014,7 @@ struct DistHandle {
   bool dry = false;                    // MAMG_DIST_TEST=dry: virtual rank skips its exchanges (timing only)
   hipStream_t side = nullptr;          // stream of the interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipEvent_t last = nullptr;           // recorded after every apply / spmv / timing (dist_destroy waits)
   // host-staged exchange backend (mamg_dist_set_exchange): pinned staging
   // per level (sends, ghost payloads, receives of the reverse-add) and one
   // all-reduce buffer
@@ -5266,6 +5027,7 @@ struct DistHandle {
     for (void* q : pinned) (void)hipHostFree(q);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
+    if (last) (void)hipEventDestroy(last);
     if (side) (void)hipStreamDestroy(side);
     for (void* a : allocs) (void)hipFree(a);
     if (comm) (void)ncclCommDestroy(comm);
@@ -5988,7 +5750,6 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
         D.A.lanes = pick_lanes_bsr(tA.nr, tA.nb);
         D.A.sym = true;
         if ((rc = try_half(h, &T, tA, &D.A, err))) return rc;
-        HIPCHK(hipDeviceSynchronize());
         half = D.A.half;
       }
     }
@@ -6052,7 +5813,6 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
     if ((rc = dev_window_cols(&T, raw, P.o0, P.o1, &tR, err))) return rc;
     if ((rc = finalize_bsr(h, &T, tR, &D.R, 0, false, err))) return rc;
   }
-  HIPCHK(hipDeviceSynchronize());
   return MAMG_OK;
 }
 
@@ -6224,7 +5984,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   std::vector<DOp> ops;
   dapply_ops(h.get(), nullptr, nullptr, &ops);
   for (const DOp& d : ops) h->apply_bytes += d.bytes;
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(null_sync());
   *out = h.release();
   return MAMG_OK;
 }
@@ -6232,7 +5992,8 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
 void dist_destroy(DistHandle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  (void)hipDeviceSynchronize();
+  if (h->last) (void)hipEventSynchronize(h->last);   // the last apply / spmv / timing on any stream
+  if (h->side) (void)hipStreamSynchronize(h->side);
   delete h;
 }
 
@@ -6241,6 +6002,12 @@ void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv) {
 }
 
 double dist_apply_bytes(const DistHandle* h) { return h->apply_bytes; }
+
+int dist_mark(DistHandle* h, hipStream_t s, std::string* err) {
+  if (!h->last) HIPCHK(hipEventCreateWithFlags(&h->last, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(h->last, s));
+  return MAMG_OK;
+}
 
 int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
@@ -6251,7 +6018,7 @@ int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std:
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
-  return MAMG_OK;
+  return dist_mark(h, (hipStream_t)stream, err);
 }
 
 int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::string* err) {
@@ -6264,7 +6031,7 @@ int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
-  return MAMG_OK;
+  return dist_mark(h, (hipStream_t)stream, err);
 }
 
 int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
@@ -6426,6 +6193,10 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
     }
   }
   HIPCHK(hipGetLastError());
+  for (DistHandle* h : hs) {
+    const int rc = dist_mark(h, s, err);
+    if (rc) return rc;
+  }
   return MAMG_OK;
 }
 

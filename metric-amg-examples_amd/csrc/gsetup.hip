@@ -52,17 +52,16 @@ typedef double dv4_t __attribute__((ext_vector_type(4)));
 
 namespace mamg {
 
-// buffers are freed only after the device has drained (kernels reading them
-// are queued asynchronously; freed memory can be handed to the next
-// allocation and overwritten under a kernel still reading it)
+// buffers are null-stream ordered (dmem.h): freed behind the kernels queued
+// before the free, never under them
 GHier::~GHier() {
   for (void* p : allocs)
-    if (p) free_after_drain(p, "GHier::~GHier");
+    if (p) tmp_free(p);
 }
 
 void GHier::release(void* p) {
   for (auto& q : allocs)
-    if (q == p) { free_after_drain(q, "GHier::release"); q = nullptr; }
+    if (q == p) { tmp_free(q); q = nullptr; }
 }
 
 namespace {
@@ -115,26 +114,26 @@ __device__ __forceinline__ int64_t dfind(const int64_t* __restrict__ ptr, const 
 struct Scratch {            // temporaries of one setup call
   std::vector<void*> v;
   ~Scratch() {
-    for (void* p : v) if (p) free_after_drain(p, "Scratch::~Scratch");
+    for (void* p : v) if (p) tmp_free(p);
   }
   template <class T>
   int alloc(T** p, int64_t count, std::string* err) {
     void* q = nullptr;
-    HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+    HIPCHK(tmp_malloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
     v.push_back(q);
     *p = (T*)q;
     return MAMG_OK;
   }
   void release(void* p) {
     for (auto& q : v)
-      if (q == p) { free_after_drain(q, "Scratch::release"); q = nullptr; }
+      if (q == p) { tmp_free(q); q = nullptr; }
   }
 };
 
 template <class T>
 int galloc(GHier* G, T** p, int64_t count, std::string* err) {
   void* q = nullptr;
-  HIPCHK(hipMalloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+  HIPCHK(tmp_malloc(&q, (size_t)std::max<int64_t>(count, 1) * sizeof(T)));
   G->allocs.push_back(q);
   *p = (T*)q;
   return MAMG_OK;
@@ -2214,7 +2213,7 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
 }  // namespace
 
 void ring_blocks_free(RingBlocks* R) {
-  for (void* q : {(void*)R->blk, (void*)R->blen, (void*)R->sq, (void*)R->inv}) free_after_drain(q, "ring_blocks_free");
+  for (void* q : {(void*)R->blk, (void*)R->blen, (void*)R->sq, (void*)R->inv}) tmp_free(q);
   *R = RingBlocks();
 }
 
@@ -2237,9 +2236,9 @@ int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlv
   uint8_t* cov = nullptr;
   int* bad = nullptr;
   auto fail = [&](int rc) { ring_blocks_free(&B); return rc; };
-  if (hipMalloc(&B.blk, (size_t)ns * mm * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&B.blen, (size_t)ns * sizeof(int64_t)) != hipSuccess ||
-      hipMalloc(&B.sq, (size_t)ns * sizeof(int64_t)) != hipSuccess) {
+  if (tmp_malloc((void**)&B.blk, (size_t)ns * mm * sizeof(int32_t)) != hipSuccess ||
+      tmp_malloc((void**)&B.blen, (size_t)ns * sizeof(int64_t)) != hipSuccess ||
+      tmp_malloc((void**)&B.sq, (size_t)ns * sizeof(int64_t)) != hipSuccess) {
     (void)hipGetLastError();
     *err = "seed rings: device allocation failed";
     return fail(MAMG_ERR_HIP);
@@ -2262,7 +2261,7 @@ int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlv
   int64_t ngj = 0;
   if ((rc = to_host(&B.ninv, B.sq + ns - 1, 1, err)) || (rc = to_host(&ngj, gj + ns - 1, 1, err))) return fail(rc);
   double* scratch = nullptr;
-  if (hipMalloc(&B.inv, (size_t)std::max<int64_t>(B.ninv, 1) * sizeof(double)) != hipSuccess) {
+  if (tmp_malloc((void**)&B.inv, (size_t)std::max<int64_t>(B.ninv, 1) * sizeof(double)) != hipSuccess) {
     (void)hipGetLastError();
     *err = "seed rings: device allocation failed";
     return fail(MAMG_ERR_HIP);
@@ -2447,7 +2446,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       smooth_p_kernel<true><<<nblk(n), 256>>>(nv, AT.ptr, AT.col, AT.val, Dsa, agg, nagg, w, L.P.ptr,
                                               L.P.col, L.P.val);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipStreamSynchronize(nullptr));
     } else if (pointSA) {           // point SA: c_i = (sa_omega / rho) / a_ii
       const double w = p.sa_omega / PL.rho;
       L.w_sa = w;
@@ -2468,7 +2467,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       smooth_pt_kernel<true><<<nblk(n), 256>>>(n, nv, agg, nagg, w, PL.dinv, AT.ptr, AT.col, AT.val, L.P.ptr,
                                                L.P.col, L.P.val);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipStreamSynchronize(nullptr));
     } else {
       L.P.n = n;
       L.P.m = nf * nagg;
@@ -2492,7 +2491,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       for (void* q : {(void*)L.AP.ptr, (void*)L.AP.col, (void*)L.AP.val}) G->release(q);
       L.AP = DevMat();
     }
-    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipStreamSynchronize(nullptr));
     G->phase_ms[3] += clk.lap();
     if (p.print_level > 0)
       std::fprintf(stderr, "[mamg gpu] level %d: n=%lld nnz=%lld nagg=%lld nnzP=%lld\n", l, (long long)n,
@@ -2517,7 +2516,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       G->release(L.W);
       L.W = nullptr;
     }
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipStreamSynchronize(nullptr));
   G->phase_ms[6] = tot.lap();
   return MAMG_OK;
 }
@@ -2685,7 +2684,7 @@ int gen_bidomain_dev(int dim, int64_t n, double gamma, double k1, double k2, int
   gen_ptr_kernel<<<nblk(nv + 1), 256>>>(nv, len, ptr);
   gen_fill_kernel<<<nblk(nv), 256>>>(dim, n, nv, kf1, kf2, mf, ptr, colind, values);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipStreamSynchronize(nullptr));
   return MAMG_OK;
 }
 
@@ -2805,13 +2804,9 @@ __global__ void ghost_mark_kernel(const int64_t* __restrict__ ptr, const int32_t
   }
 }
 
-struct DevScratch {             // plain hipMalloc buffer, freed on scope exit
+struct DevScratch {             // a null-stream ordered temporary (dmem.h), freed on scope exit
   void* p = nullptr;
-  ~DevScratch() {
-    if (!p) return;
-    (void)hipDeviceSynchronize();   // as GHier::release
-    (void)hipFree(p);
-  }
+  ~DevScratch() { tmp_free(p); }
 };
 
 }  // namespace
@@ -2878,8 +2873,8 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
     if (!rep[l]) mark_bytes = std::max<int64_t>(mark_bytes, (int64_t)nranks * nv[l]);
   if (mark_bytes) {
     DevScratch rng, mk;
-    HIPCHK(hipMalloc(&rng.p, (size_t)nl * (nranks + 1) * sizeof(int64_t)));
-    HIPCHK(hipMalloc(&mk.p, (size_t)mark_bytes));
+    HIPCHK(tmp_malloc(&rng.p, (size_t)nl * (nranks + 1) * sizeof(int64_t)));
+    HIPCHK(tmp_malloc(&mk.p, (size_t)mark_bytes));
     int64_t* drng = (int64_t*)rng.p;
     uint8_t* mark = (uint8_t*)mk.p;
     for (int l = 0; l < nl; ++l)

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU call A: the free diagnosis (scripts/gpu_freediag.sh steps) and
-# the first seed-ring Schwarz GPU tests.
+# Round-4 GPU call A: the free diagnosis and the first tests of the round's
+# new paths (seed rings, device generator, multi-GPU setup from HBM).
 #   gpurun --timeout 1200 -- bash scripts/gpu_r04a.sh TAG
 TAG=${1:-r04a}
 OUT=$(pwd)/gpurun_out/$TAG
@@ -16,7 +16,10 @@ run() {   # run <name> <timeout> <cmd...>; stop on anything but pass/fail
 }
 run free_race 90 ./bench/free_race 200
 PYT="python -u -m pytest -v --timeout 200 --timeout-method thread"
-MAMG_POISON=1 MAMG_DRAIN=0 MAMG_FREELOG=1 run nodrain1 300 $PYT tests/test_gpu.py
-MAMG_POISON=1 MAMG_DRAIN=0 run nodrain2 300 $PYT tests/test_gpu.py
-run rings 600 $PYT tests/test_gpu_rings.py
+# hipMalloc / hipFree with no ordering of the library's own (round-2 code)
+MAMG_POISON=1 MAMG_FREE_MODE=plain run poison_plain 300 $PYT tests/test_gpu.py
+# null-stream ordered temporaries (round 4 default)
+MAMG_POISON=1 run poison_default 300 $PYT tests/test_gpu.py
+run rings 900 $PYT tests/test_gpu_rings.py
+run devgen 300 $PYT tests/test_gpu_dist.py -k "device"
 echo "== done"

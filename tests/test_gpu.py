@@ -479,9 +479,9 @@ def test_k_block_layouts_bitwise(lib_built, monkeypatch):
 def test_k_kernel_variants(lib_built, monkeypatch, variant):
     """The level-0 K kernel with 2 lanes per row (default), 1 lane (round 2's
     sell2_kernel) or 4 lanes: the same operator up to the order of a row's
-    partial sums (1e-14), each = the oracle; the layouts block <-> split
-    switched back and forth on one handle give the apply's bits back, and the
-    operators re-homed after the setup give the bits of the un-moved ones."""
+    partial sums (1e-14), each = the oracle; the eager (time_apply) launches
+    give the graph apply's bits, and the operators re-homed after the setup
+    give the bits of the un-moved ones."""
     import torch
     M = _mamg()
     monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
@@ -491,15 +491,12 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
     monkeypatch.setenv('MAMG_K_VARIANT', '1')
     B1 = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
     z1 = B1.matvec(r)
+    torch.cuda.synchronize()
     monkeypatch.setenv('MAMG_K_VARIANT', variant)
     B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
     assert B.level_format(0)['post_sell']
     z = B.matvec(r)
     zz = torch.empty_like(z)
-    for lay in ('split', 'block'):     # in-place re-layout through mamg_time_apply
-        monkeypatch.setenv('MAMG_K_LAYOUT', lay)
-        B.time_apply(r, zz, 1, 0)
-    monkeypatch.delenv('MAMG_K_LAYOUT')
     B.time_apply(r, zz, 1, 0)
     torch.cuda.synchronize()
     assert torch.equal(zz, z)
