@@ -13,6 +13,7 @@ libmamg.so or a HIP device the constructor raises.
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 
 import numpy as np
 
@@ -62,14 +63,26 @@ def _dims(W, n):
 def _with_functions(W, parameters, overrides):
     """The reference's metricAMG receives the block space W (src/utils.py:86):
     a W of k >= 2 equal-sized blocks (the bidomain's and EMI's P1 x P1) gives
-    num_functions = k unless the dict or an override sets it."""
+    num_functions = k unless the dict or an override sets it.
+
+    Returns (overrides, notes).  Whether HAZmath's metricAMG itself derives
+    num_functions from W is not pinned by the reference source, so the
+    inference is reported: as a note (MetricAMG.notes) and, when the caller
+    passed a dict without num_functions (a reference preset such as
+    parameters_standard, which would otherwise aggregate point-wise), as a
+    UserWarning.  A caller-supplied num_functions (dict or keyword) always
+    wins (INTEGRATION.md)."""
     if 'num_functions' in overrides or (parameters and 'num_functions' in parameters) \
             or W is None or not isinstance(W, (list, tuple)) or len(W) < 2:
-        return overrides
+        return overrides, []
     dims = [int(w.dim()) if hasattr(w, 'dim') else int(w) for w in W]
     if len(set(dims)) != 1:
-        return overrides
-    return dict(overrides, num_functions=len(dims))
+        return overrides, []
+    note = ('num_functions -> %d (inferred from W: %d equal blocks of %d dofs; '
+            'pass num_functions=1 for point-wise aggregation)' % (len(dims), len(dims), dims[0]))
+    if parameters:
+        warnings.warn(note, UserWarning, stacklevel=3)
+    return dict(overrides, num_functions=len(dims)), [note]
 
 
 def _device_ptr(x):
@@ -135,7 +148,8 @@ class MetricAMG:
 
     def __init__(self, A, W=None, idofs=None, parameters=None, setup='auto', **overrides):
         self._L = _lib.lib()
-        self.params = make_params(parameters, **_with_functions(W, parameters, overrides))
+        ov, self.notes = _with_functions(W, parameters, overrides)
+        self.params = make_params(parameters, **ov)
         if idofs is not None:
             self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
             ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)
@@ -536,7 +550,8 @@ class DistMetricAMG:
             csr = _lib.as_csr_struct(indptr, indices, data, m)
         self.shape = (n, n)
         self.W = _dims(W, n)
-        self.params = make_params(parameters, **_with_functions(W, parameters, overrides))
+        ov, self.notes = _with_functions(W, parameters, overrides)
+        self.params = make_params(parameters, **ov)
         if idofs is not None:
             self.idofs = np.ascontiguousarray(idofs, dtype=np.int32)
             ip, ni = _lib.ptr(self.idofs, C.c_int32), len(self.idofs)

@@ -333,6 +333,12 @@ int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int3
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
+  // parameters first: an invalid or single-GPU-only profile is refused
+  // before the rank touches its GPU
+  if ((rc = mamg::check_params(P, &err)) || (rc = mamg::dist_check(P, &err))) {
+    set_error(err);
+    return rc;
+  }
   Seeds S(idofs, n_idofs, v.n, &P);
   // setup phases to stderr with print_level >= 2 (HAZmath's setup printing)
   auto t_0 = std::chrono::steady_clock::now();
@@ -538,6 +544,12 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
+  // parameters first: an invalid or single-GPU-only profile is refused
+  // before the rank touches its GPU
+  if ((rc = mamg::check_params(P, &err)) || (rc = mamg::dist_check(P, &err))) {
+    set_error(err);
+    return rc;
+  }
   Seeds S(idofs, n_idofs, v.n, &P);
   rc = mamg::host_setup(v, S.ptr, S.n, P, &H, &err);
   if (rc) { set_error(err); return rc; }

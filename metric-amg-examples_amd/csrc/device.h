@@ -45,6 +45,9 @@ int dist_get_unique_id(void* id, std::string* err);
 // ghosts: precomputed ghost lists (ghier_download_rank), else nullptr; G / A0d:
 // build the rank-local operators on the device from this GPU hierarchy (H then
 // holds only level sizes and the coarsest inverse)
+// the multi-GPU path's parameter limits (maxit 1, no SCHWARZ_PATCHES /
+// SCHWARZ_RINGS), checked before a rank touches its GPU
+int dist_check(const mamg_params& p, std::string* err);
 int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
                 const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
                 const std::vector<std::vector<std::vector<int64_t>>>* ghosts = nullptr,

@@ -5818,9 +5818,7 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
 
 }  // namespace
 
-int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
-                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
-                const GhostLists* ghosts, const GHier* G, const DevMat* A0d) {
+int dist_check(const mamg_params& p, std::string* err) {
   if (p.maxit != 1) {
     *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
@@ -5829,6 +5827,13 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     *err = "multi-GPU apply: node-patch / seed-ring Schwarz (SCHWARZ_PATCHES / SCHWARZ_RINGS) is single-GPU";
     return MAMG_ERR_UNSUPPORTED;
   }
+  return MAMG_OK;
+}
+
+int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int rank, int nranks,
+                const void* comm_id, int64_t rep_nodes, DistHandle** out, std::string* err,
+                const GhostLists* ghosts, const GHier* G, const DevMat* A0d) {
+  if (int rc = dist_check(p, err)) return rc;
   const bool gs = gs_smoother(p);
   if (gs && !G) {
     *err = "multi-GPU multicolour GS needs the rank operators built from the GPU hierarchy (mamg_setup_dist "

@@ -166,3 +166,60 @@ def test_no_cpu_fallback_without_gpu(lib_built):
     with pytest.raises(M._lib.MamgError) as ei:
         M.MetricAMG(laplace1d(30))
     assert ei.value.code == -2                # HIP error, never a CPU fallback
+
+
+def _dist_rc(M, s, prm):
+    L = M._lib.lib()
+    csr = M._lib.as_csr_struct(s.indptr, s.indices, s.data, s.N)
+    cid, out = (C.c_char * 128)(), C.c_void_p()
+    rc = L.mamg_setup_dist(C.byref(csr), None, 0, C.byref(prm), 0, 2, cid, 0, C.byref(out))
+    return rc, L.mamg_last_error().decode()
+
+
+def test_setup_dist_parameter_checks_before_gpu(lib_built):
+    """mamg_setup_dist (include/mamg.h, multi-GPU section) takes V and W cycles:
+    a W-cycle profile passes every parameter check and reaches the device
+    (no device here: MAMG_ERR_HIP), while an invalid cycle, maxit > 1 and the
+    single-GPU Schwarz forms are refused before the rank touches its GPU."""
+    import torch
+    import metric_amg_examples_amd as M
+    if torch.cuda.is_available():
+        pytest.skip('GPU present: tests/test_gpu_dist.py runs the W cycle on two ranks')
+    P = M.parameters
+    s = M.problems.bidomain(2, 16, 1e4)
+    for cyc in (P.V_CYCLE, P.W_CYCLE):
+        rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_mi355x, cycle_type=cyc))
+        assert rc == -2 and 'hip' in msg.lower(), (cyc, rc, msg)
+    rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_mi355x, cycle_type=3))
+    assert rc == -4, msg
+    rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_mi355x, maxit=2))
+    assert rc == -4 and 'maxit' in msg
+    rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_schwarz_gpu_mapped))
+    assert rc == -4 and 'single-GPU' in msg
+
+
+def test_num_functions_inference_is_reported_and_overridable(lib_built):
+    """MetricAMG / DistMetricAMG infer num_functions from a W of equal blocks
+    (amg.py _with_functions); the inference is a note, a UserWarning when a
+    reference dict without num_functions is passed, and a caller's
+    num_functions (keyword or dict) always wins."""
+    import warnings
+    import metric_amg_examples_amd as M
+    from metric_amg_examples_amd.amg import _with_functions
+    P = M.parameters
+    W = [100, 100]
+    ov, notes = _with_functions(W, None, {})
+    assert ov == {'num_functions': 2} and len(notes) == 1 and 'num_functions=1' in notes[0]
+    with pytest.warns(UserWarning, match='inferred from W'):
+        ov, notes = _with_functions(W, P.parameters_standard, {})
+    assert ov['num_functions'] == 2
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        ov, notes = _with_functions(W, P.parameters_standard, {'num_functions': 1})
+        assert ov == {'num_functions': 1} and notes == []
+        ov, notes = _with_functions(W, dict(P.parameters_standard, num_functions=1), {})
+        assert ov == {} and notes == []
+        assert _with_functions([100, 50], P.parameters_standard, {}) == ({}, [])
+        assert _with_functions(None, P.parameters_standard, {}) == ({}, [])
+    assert P.make_params(P.parameters_standard, **_with_functions(W, P.parameters_standard,
+                                                                   {'num_functions': 1})[0]).num_functions == 1
