@@ -242,7 +242,9 @@ def main():
         setup_info = {'path': 'deterministic setup replicated on every rank (GPU setup; host setup if the '
                               'profile is unsupported) + rank-local upload',
                       'A0': 'host' if hasattr(sysm, 'indptr') else 'generated in HBM per rank',
-                      'wall_s': round(t_setup, 3), 'host_rss_gb_max_rank': round(allmax(rss_gb()), 2)}
+                      'wall_s': round(t_setup, 3), 'host_rss_gb_max_rank': round(allmax(rss_gb()), 2),
+                      # eager distributed apply: what rank 0 issues per apply
+                      'apply_launches_rank0': B.apply_launches}
         levels = None
         layout = 'bsr2-dist'
         r = torch.as_tensor(B.local_slice(r_full)).to(dev)

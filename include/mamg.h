@@ -278,6 +278,10 @@ int mamg_setup_dist_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_i
  * [u1(o0:o1); u2(o0:o1)] of length 2*(o1-o0) */
 int mamg_dist_range(const mamg_dhandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
 int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes);
+/* what one mamg_dist_apply_device issues on this rank (counted from its op
+ * list, nothing launched): counts[0] kernels, [1] RCCL send / receive groups,
+ * [2] point-to-point messages, [3] all-reduces, [4] side-stream forks */
+int mamg_dist_apply_launches(const mamg_dhandle* h, int64_t counts[5]);
 int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r_local, double* d_z_local,
                            void* stream);
 /* y = A x on the rank's rows (the PCG operator; x, y local field-major

@@ -630,6 +630,14 @@ class DistMetricAMG:
         _lib.check(self._L.mamg_dist_apply_bytes(self._h, C.byref(b)))
         return b.value
 
+    @property
+    def apply_launches(self):
+        """{'kernels', 'p2p_groups', 'p2p_messages', 'allreduces', 'stream_forks'}
+        one apply issues on this rank (mamg_dist_apply_launches)."""
+        c = (C.c_int64 * 5)()
+        _lib.check(self._L.mamg_dist_apply_launches(self._h, c))
+        return dict(zip(('kernels', 'p2p_groups', 'p2p_messages', 'allreduces', 'stream_forks'), list(c)))
+
     def apply_device(self, r, z, stream=None):
         _lib.check(self._L.mamg_dist_apply_device(self._h, _device_ptr(r), _device_ptr(z),
                                                   _stream_ptr(stream)))

@@ -475,6 +475,12 @@ int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes) {
   return MAMG_OK;
 }
 
+int mamg_dist_apply_launches(const mamg_dhandle* h, int64_t counts[5]) {
+  if (!h || !counts) { set_error("null argument"); return MAMG_ERR_ARG; }
+  mamg::dist_apply_launches(h->d, counts);
+  return MAMG_OK;
+}
+
 int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r, double* d_z, void* stream) {
   DEV_CALL(mamg::dist_apply(h->d, d_r, d_z, stream, &err))
 }

@@ -55,6 +55,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
 void dist_destroy(DistHandle* h);
 void dist_range(const DistHandle* h, int64_t* o0, int64_t* o1, int64_t* nv);
 double dist_apply_bytes(const DistHandle* h);
+void dist_apply_launches(const DistHandle* h, int64_t c[5]);
 int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
 int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::string* err);
 int dist_virtual_spmv(const std::vector<DistHandle*>& hs, const std::vector<const double*>& x,

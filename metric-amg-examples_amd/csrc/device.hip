@@ -6014,6 +6014,50 @@ int dist_mark(DistHandle* h, hipStream_t s, std::string* err) {
   return MAMG_OK;
 }
 
+// What one distributed apply issues on a rank with P > 1 peers over RCCL
+// (the same walk as run_dop, nothing launched): c[0] kernels, c[1] RCCL
+// send / receive groups, c[2] point-to-point messages, c[3] all-reduces,
+// c[4] stream forks (interior rows on the side stream).  With P == 1 only
+// the kernels remain.
+void dist_apply_launches(const DistHandle* h, int64_t c[5]) {
+  for (int k = 0; k < 5; ++k) c[k] = 0;
+  std::vector<DOp> ops;
+  dapply_ops(h, nullptr, nullptr, &ops);
+  const int P = h->nranks;
+  for (const DOp& d : ops) {
+    if (d.dk == D_OP || (P == 1 && d.dk == D_OVERLAP)) { ++c[0]; continue; }
+    if (P == 1) continue;
+    if (d.dk == D_ALLREDUCE) { ++c[3]; continue; }
+    const DDLevel& D = h->L[d.level];
+    const int64_t ns = D.send_off.back();
+    if (d.dk == D_OVERLAP) { ++c[0]; ++c[4]; }
+    if (d.dk == D_OVERLAP || d.dk == D_HALO) {
+      if (ns) ++c[0];
+      ++c[1];
+      for (int q = 0; q < P; ++q) {
+        if (q == h->rank) continue;
+        c[2] += (D.send_off[q + 1] > D.send_off[q]) + (D.ghost_off[q + 1] > D.ghost_off[q]);
+      }
+    } else if (d.dk == D_CHALO) {
+      const size_t b0 = (size_t)d.colour * (P + 1);
+      c[0] += (D.cs_off[b0 + P] > D.cs_off[b0]) + (D.cg_off[b0 + P] > D.cg_off[b0]);
+      ++c[1];
+      for (int q = 0; q < P; ++q) {
+        if (q == h->rank) continue;
+        c[2] += (D.cs_off[b0 + q + 1] > D.cs_off[b0 + q]) + (D.cg_off[b0 + q + 1] > D.cg_off[b0 + q]);
+      }
+    } else {   // D_REVERSE
+      ++c[1];
+      for (int q = 0; q < P; ++q) {
+        if (q == h->rank) continue;
+        const bool sc = D.send_off[q + 1] > D.send_off[q], gc = D.ghost_off[q + 1] > D.ghost_off[q];
+        c[2] += sc + gc;
+        c[0] += sc;
+      }
+    }
+  }
+}
+
 int dist_apply(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
   std::vector<DOp> ops;

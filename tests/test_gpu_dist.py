@@ -413,7 +413,7 @@ def _host_exchange_worker(rank, world, port, q, problem, kw):
         cg = M.DistConjGrad.for_handles(h, tolerance=1e-8, maxiter=500)
         x = cg.solve([r.clone()])[0]
         torch.cuda.synchronize()
-        q.put((rank, h.o0, h.o1, z.cpu().numpy(), x.cpu().numpy(), list(cg.residuals)))
+        q.put((rank, h.o0, h.o1, z.cpu().numpy(), x.cpu().numpy(), list(cg.residuals), h.apply_launches))
         h.close()
     finally:
         dist.destroy_process_group()
@@ -452,7 +452,10 @@ def test_two_processes_host_exchange(lib_built, problem, kw):
     zo = h.apply(r)
     ref = mo.pcg(A, h, r, 1e-8, 500)
     z, x = np.zeros(s.N), np.zeros(s.N)
-    for rank, o0, o1, zl, xl, resid in res:
+    for rank, o0, o1, zl, xl, resid, launches in res:
+        # what one apply issues per rank: printed for DESIGN
+        print('rank', rank, problem, kw, launches)
+        assert launches['kernels'] > 10 and launches['p2p_groups'] > 0 and launches['p2p_messages'] > 0
         nloc = o1 - o0
         z[o0:o1], z[s.nv + o0:s.nv + o1] = zl[:nloc], zl[nloc:]
         x[o0:o1], x[s.nv + o0:s.nv + o1] = xl[:nloc], xl[nloc:]
