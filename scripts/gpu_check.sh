@@ -44,6 +44,7 @@ if want pmc; then
       -- python3 $ROOT/bench.py $LIGHT; cd $ROOT
   F=$(find $OUT/pmc_fetch -name '*counter_collection.csv' | head -1)
   W=$(find $OUT/pmc_write -name '*counter_collection.csv' | head -1)
-  python3 scripts/traffic.py "$F" "$W" --N 33949186 --out $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic.json
+  BJ=""; [ -s $OUT/bench.json ] && BJ="--bench-json $OUT/bench.json"
+  python3 scripts/traffic.py "$F" "$W" --N 33949186 $BJ --out $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic.json
 fi
 echo "== done"
