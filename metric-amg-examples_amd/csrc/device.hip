@@ -158,9 +158,9 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
     const double* __restrict__ bval, const double* __restrict__ x, int64_t xs,
     const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os, int remap) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap, const int32_t* __restrict__ sched) {
   const int lane = threadIdx.x & (VL - 1);
-  const int64_t node = (row_block(remap) * 256 + threadIdx.x) / VL;
+  const int64_t node = ((sched ? (int64_t)sched[blockIdx.x] : row_block(remap)) * 256 + threadIdx.x) / VL;
   const double* offd = SYM ? bval + 2 * bptr[nr] : nullptr;
   double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
   if (node < nr) {
@@ -1677,6 +1677,8 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //   MAMG_HALF           0: SELL-64 instead of the half-symmetric ELL-64 A0 (1)
 //   MAMG_HALF_BANDS     band schedule of the half-symmetric kernel: sub-bands per
 //                       XCD (1; 0 = row order)
+//   MAMG_R_BANDS        plane-band schedule of the level-0 restriction: sub-bands
+//                       per XCD (1; 0 = XCD-contiguous rows)
 //   MAMG_POST_K         0: fused post sweep over [P | AP] instead of K = P - W A P (1)
 //   multi-GPU (mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch during
 //   the forward halo (1); MAMG_DIST_TEST=dry: a virtual rank skips its exchanges
@@ -1691,6 +1693,7 @@ constexpr int g_post_u = 6;
 constexpr int64_t g_sell_max_len = 40;
 int g_half = 1;
 int g_half_bands = 1;
+int g_r_bands = 1;
 int g_post_k = 1;
 int g_kvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
@@ -1716,6 +1719,8 @@ void read_knobs() {
   g_half = e ? std::atoi(e) != 0 : 1;
   e = std::getenv("MAMG_HALF_BANDS");
   g_half_bands = e ? std::atoi(e) : 1;
+  e = std::getenv("MAMG_R_BANDS");
+  g_r_bands = e ? std::atoi(e) : 1;
 }
 
 // every block symmetric (bitwise): then 3 doubles per block carry it exactly
@@ -1786,6 +1791,11 @@ struct DBsr {              // 2x2 blocks, node-major
   // band schedule of one sub-range launch [sr0, sr1) (multi-GPU interior rows)
   int32_t* sched_r = nullptr;
   int64_t nsched_r = 0, sr0 = 0, sr1 = 0;
+  // plane-band schedule of a lane-group BSR launch with rsched_vl lanes per
+  // row (the level-0 restriction): workgroup b processes row block rsched[b]
+  int32_t* rsched = nullptr;
+  int64_t nrsched = 0;
+  int rsched_vl = 0;
 };
 
 struct DLevel {
@@ -2558,6 +2568,83 @@ int build_band_sched_range(HT* h, DBsr* D, int64_t r0, int64_t r1, std::string* 
   return upload_sched(h, sched, &D->sched_r, &D->nsched_r, err);
 }
 
+// first column of the first non-empty row of each group of rpw rows (-1: none)
+__global__ void wg_first_col_kernel(int64_t G, int rpw, int64_t nr, const int64_t* __restrict__ ptr,
+                                    const int32_t* __restrict__ col, int32_t* __restrict__ out) {
+  const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (b >= G) return;
+  int32_t c = -1;
+  for (int64_t i = b * rpw; i < nr && i < (b + 1) * rpw; ++i)
+    if (ptr[i] < ptr[i + 1]) { c = col[ptr[i]]; break; }
+  out[b] = c;
+}
+
+// Plane-band schedule of the level-0 restriction R_0 (coarse rows, fine
+// columns).  A coarse row gathers r_1 over its smoothed aggregate, ~5 fine
+// planes deep; coarse rows come in aggregate order, i.e. coarse plane after
+// coarse plane, so a fine plane is gathered again by the next coarse plane's
+// rows -- one coarse plane of R_0 (~30 MB at n = 256) later, long gone from
+// an XCD's 4 MB L2 when each XCD walks whole planes.  Here a workgroup's key
+// is the in-plane position (first column mod the fine plane stride Sf) of its
+// first row: the plane is cut into 8 nsub bands, XCD x (workgroups b = x mod
+// 8) takes the bands x nsub .. x nsub + nsub - 1 and walks each through all
+// planes, so the re-gather is one band-plane of R_0 later and still in L2.
+// Only which workgroup computes which rows changes: results are bitwise.
+std::vector<int32_t> rest_band_sched(const std::vector<int32_t>& c0, int64_t Sf, int nsub) {
+  std::vector<int32_t> sched;
+  const int64_t G = (int64_t)c0.size(), nb = 8 * (int64_t)nsub;
+  if (nsub <= 0 || Sf <= 0 || G < 64 * nb) return sched;
+  std::vector<std::vector<int32_t>> L(8);
+  std::vector<std::vector<int32_t>> band(nb);
+  int64_t last = 0;
+  for (int64_t b = 0; b < G; ++b) {
+    const int64_t c = c0[b] >= 0 ? c0[b] : last;
+    last = c;
+    band[std::min<int64_t>(nb - 1, (c % Sf) * nb / Sf)].push_back((int32_t)b);
+  }
+  for (int64_t k = 0; k < nb; ++k) L[k / nsub].insert(L[k / nsub].end(), band[k].begin(), band[k].end());
+  std::vector<int32_t> spill;   // balance to the round-robin dispatch, as band_sched
+  for (int x = 0; x < 8; ++x) {
+    const size_t want = (size_t)(G / 8 + (x < G % 8 ? 1 : 0));
+    while (L[x].size() > want) { spill.push_back(L[x].back()); L[x].pop_back(); }
+  }
+  for (int x = 0; x < 8; ++x) {
+    const size_t want = (size_t)(G / 8 + (x < G % 8 ? 1 : 0));
+    while (L[x].size() < want && !spill.empty()) { L[x].push_back(spill.back()); spill.pop_back(); }
+  }
+  sched.resize(G);
+  std::vector<char> seen(G, 0);
+  for (int64_t b = 0; b < G; ++b) {
+    if ((size_t)(b / 8) >= L[b % 8].size()) return std::vector<int32_t>();
+    sched[b] = L[b % 8][b / 8];
+    if (sched[b] < 0 || sched[b] >= G || seen[sched[b]]++) return std::vector<int32_t>();
+  }
+  return sched;
+}
+
+// the schedule for D (a lane-group BSR, not SELL / merged) given the fine
+// plane stride Sf of its columns
+template <class HT>
+int build_rest_sched(HT* h, TmpPool* T, DBsr* D, int64_t Sf, std::string* err) {
+  if (g_r_bands <= 0 || Sf <= 0 || D->sell || D->half || !D->ptr || D->lanes <= 0) return MAMG_OK;
+  const int rpw = 256 / D->lanes;
+  const int64_t G = (D->nr * (int64_t)D->lanes + 255) / 256;
+  if (G < 64 * 8 * (int64_t)g_r_bands || G >= ((int64_t)1 << 31)) return MAMG_OK;
+  int rc;
+  int32_t* c0 = nullptr;
+  if ((rc = T->alloc(&c0, G, err))) return rc;
+  wg_first_col_kernel<<<nblocks(G), 256>>>(G, rpw, D->nr, D->ptr, D->col, c0);
+  HIPCHK(hipGetLastError());
+  std::vector<int32_t> hc(G);
+  HIPCHK(hipMemcpy(hc.data(), c0, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  T->release(c0);
+  const std::vector<int32_t> sched = rest_band_sched(hc, Sf, g_r_bands);
+  if (sched.empty()) return MAMG_OK;
+  if ((rc = upload_sched(h, sched, &D->rsched, &D->nrsched, err))) return rc;
+  D->rsched_vl = D->lanes;
+  return MAMG_OK;
+}
+
 // half-symmetric ELL-64 for a symmetric-block A whose owned part (columns
 // < nr) is symmetric bitwise; columns >= nr (ghosts of a rank-local A) go to
 // the ghost part (hsell2_kernel).  Returns MAMG_OK with D->half set, or
@@ -3201,6 +3288,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     TBsr Rb;
     if ((rc = dev_csr_to_bsr(&T, S.R, nvc, nv, &Rb, err))) return rc;
     if ((rc = finalize_bsr(h, &T, Rb, &D.Rb, 0, false, err))) return rc;
+    if (l == 0 && (rc = build_rest_sched(h, &T, &D.Rb, D.Ab.band_stride, err))) return rc;
   }
   return MAMG_OK;
 }
@@ -3760,7 +3848,8 @@ void launch_bsr_x(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const unsigned g = nblocks(M.nr * (int64_t)VL);
   if (g == 0) return;
-#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o)
+#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o), \
+    (M.rsched && M.rsched_vl == VL && (int64_t)g == M.nrsched) ? M.rsched : nullptr
   switch (o.epi) {
     case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
@@ -4637,7 +4726,7 @@ int dev_level_format(const DeviceHandle* h, int level) {
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
          (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0) |
          (L.pcs.size() > 1 ? MAMG_FMT_PATCHES : 0) | (L.gcs.size() > 1 ? MAMG_FMT_GS : 0) |
-         (L.rcs.size() > 1 ? MAMG_FMT_RINGS : 0);
+         (L.rcs.size() > 1 ? MAMG_FMT_RINGS : 0) | (L.Rb.nrsched > 0 ? MAMG_FMT_R_BANDS : 0);
 }
 
 mamg_params dev_params(const DeviceHandle* h) { return h->p; }

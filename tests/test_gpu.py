@@ -254,6 +254,30 @@ def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw):
 
 
 @pytest.mark.parametrize('bands', ['1', '2'])
+def test_restriction_band_schedule_bitwise(lib_built, monkeypatch, bands):
+    """The plane-band schedule of the level-0 restriction (coarse rows walked
+    band by band through the planes on each XCD) only reorders workgroups:
+    at 3-D n=128 the apply and the device PCG are bitwise those of the
+    XCD-contiguous order (MAMG_R_BANDS=0)."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 128, 1e6)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    outs, its = [], []
+    for b in (bands, '0'):
+        monkeypatch.setenv('MAMG_R_BANDS', b)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        assert B.level_format(0)['r_bands'] == (b != '0')
+        outs.append(B * r)
+        solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        solver * r
+        its.append(solver.residuals)
+        B.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert its[0] == its[1]
+
+
+@pytest.mark.parametrize('bands', ['1', '2'])
 def test_half_band_schedule_bitwise(lib_built, monkeypatch, bands):
     """The band schedule of the half-symmetric kernel (rows walked plane band
     by plane band on each XCD) only reorders workgroups: at 3-D n=128 (where
