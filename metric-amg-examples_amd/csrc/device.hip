@@ -892,8 +892,46 @@ __device__ __forceinline__ TOp tail_resolve(const TOp& a, char* lds) {
   return o;
 }
 
+// v + (v of the lane M away) inside groups of 4 lanes, by DPP quad
+// permutations (one VALU op per 32-bit half) instead of an LDS-routed
+// ds_bpermute; the same value and sum as __shfl_xor(v, M, 4)
+template <int M>
+__device__ __forceinline__ double quad_xor(double v) {
+  constexpr int ctrl = M == 1 ? 0xB1 : 0x4E;   // quad_perm [1,0,3,2] / [2,3,0,1]
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), ctrl, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// a load from an operand that is always in global memory (the tail's
+// matrices): the TOp fields are generic pointers (a vector field may hold an
+// LDS address), so without the cast every load would be a flat load
+template <class T>
+__device__ __forceinline__ T gload(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+template <bool SYM>
+__device__ __forceinline__ dv4 tail_blk(const double* v, const double* off, int k) {
+  if (SYM) {
+    const dv2 d = gload(reinterpret_cast<const dv2*>(v) + k);
+    const double b = gload(off + k);
+    return dv4{d.x, b, b, d.y};
+  }
+  return gload(reinterpret_cast<const dv4*>(v) + k);
+}
+
+// x(c) as a pair; XL: x is in the workgroup's LDS (ds_read, not a flat load)
+template <bool XL>
+__device__ __forceinline__ double2 tail_x(const double2* x2, int c) {
+  if (XL) return *((const __attribute__((address_space(3))) double2*)x2 + c);
+  return x2[c];
+}
+
 // rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
-// vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place
+// vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place.
+// XL: the gathered vector x lives in LDS
+template <bool XL>
 __device__ void tail_bsr(const TOp& o, bool gs) {
   // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
   // a 64-bit division per row chunk cost more than the chunk's loads
@@ -914,12 +952,12 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     // loads together, branch-free (a dead lane reads row row0 and drops it),
     // so they form one round trip instead of a chain behind a branch
     const int nodec = live ? node : row0;
-    const int p0 = (int)o.ptr[nodec], p1 = live ? (int)o.ptr[nodec + 1] : p0;
+    const int p0 = (int)gload(o.ptr + nodec), p1 = live ? (int)gload(o.ptr + nodec + 1) : p0;
     int gI = -1;
     dv4 gd = {0.0, 0.0, 0.0, 0.0};
     if (gs) {
-      gI = live ? o.perm[nodec] : -1;
-      gd = o.W[nodec];
+      gI = live ? gload(o.perm + nodec) : -1;
+      gd = gload(o.W + nodec);
     }
     const int gIc = gI >= 0 ? gI : 0;
     double gb0 = 0.0, gb1 = 0.0;
@@ -927,7 +965,7 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     if (gs) {
       gb0 = o.b[2 * gIc];
       gb1 = o.b[2 * gIc + 1];
-      gx = x2[gIc];
+      gx = tail_x<XL>(x2, gIc);
     }
     if (p1 > p0) {
       // the first two chunks: all column and value loads issued before any
@@ -945,12 +983,12 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         dv4 vv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          cc[q] = o.col[ll[q]];
-          vv[q] = o.sym ? blk<true>(o.val, offd, ll[q]) : blk<false>(o.val, nullptr, ll[q]);
+          cc[q] = gload(o.col + ll[q]);
+          vv[q] = o.sym ? tail_blk<true>(o.val, offd, ll[q]) : tail_blk<false>(o.val, nullptr, ll[q]);
         }
         double2 xa[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xa[q] = x2[cc[q]];
+        for (int q = 0; q < 4; ++q) xa[q] = tail_x<XL>(x2, cc[q]);
 #pragma unroll
         for (int q = 0; q < 4; q += 2) {
           s0 += hh[q] ? vv[q].x * xa[q].x + vv[q].y * xa[q].y : 0.0;
@@ -963,10 +1001,10 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         const int ka = kb0 + lane, kb = ka + VL;
         const bool ha = ka < p1, hb = kb < p1;
         const int la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
-        const int32_t c0 = o.col[la], c1 = o.col[lb];
-        const dv4 v0 = o.sym ? blk<true>(o.val, offd, la) : blk<false>(o.val, nullptr, la);
-        const dv4 v1 = o.sym ? blk<true>(o.val, offd, lb) : blk<false>(o.val, nullptr, lb);
-        const double2 a = x2[c0], e = x2[c1];
+        const int32_t c0 = gload(o.col + la), c1 = gload(o.col + lb);
+        const dv4 v0 = o.sym ? tail_blk<true>(o.val, offd, la) : tail_blk<false>(o.val, nullptr, la);
+        const dv4 v1 = o.sym ? tail_blk<true>(o.val, offd, lb) : tail_blk<false>(o.val, nullptr, lb);
+        const double2 a = tail_x<XL>(x2, c0), e = tail_x<XL>(x2, c1);
         s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
         s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
         t0 += hb ? v1.x * e.x + v1.y * e.y : 0.0;
@@ -975,9 +1013,20 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     }
     s0 += t0;
     s1 += t1;
-    for (int off = VL / 2; off > 0; off >>= 1) {
-      s0 += __shfl_xor(s0, off, VL);
-      s1 += __shfl_xor(s1, off, VL);
+    if (VL <= 4) {   // the tail's lane counts (MAMG_TAIL_VL <= 4): xor 2, then xor 1, as below
+      if (VL == 4) {
+        s0 += quad_xor<2>(s0);
+        s1 += quad_xor<2>(s1);
+      }
+      if (VL >= 2) {
+        s0 += quad_xor<1>(s0);
+        s1 += quad_xor<1>(s1);
+      }
+    } else {
+      for (int off = VL / 2; off > 0; off >>= 1) {
+        s0 += __shfl_xor(s0, off, VL);
+        s1 += __shfl_xor(s1, off, VL);
+      }
     }
     if (!live || lane != 0) continue;
     if (gs) {
@@ -996,12 +1045,12 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
       o0 = o.b[2 * node] - s0; o1 = o.b[2 * node + 1] - s1;
     } else if (o.epi == EPI_KPOST) {
       const double r0 = o.b[2 * node], r1 = o.b[2 * node + 1];
-      const dv4 w = o.W[node];
+      const dv4 w = gload(o.W + node);
       o0 = o.y[2 * node] + (w.x * r0 + w.y * r1) + s0;
       o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1) + s1;
     } else {  // EPI_BJAC
       const double r0 = o.b[2 * node] - s0, r1 = o.b[2 * node + 1] - s1;
-      const dv4 w = o.W[node];
+      const dv4 w = gload(o.W + node);
       o0 = o.y[2 * node] + (w.x * r0 + w.y * r1);
       o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1);
     }
@@ -1015,25 +1064,39 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
 // dynamic LDS: the tail levels' work vectors (tail_lds_plan)
 extern __shared__ double tail_lds[];
 
-template <bool STAMP>
+// XL: every SpMV / GS op of the program gathers from an LDS-resident x
+// (tail_lds_plan placed all of them), so the gathers are ds_reads
+template <bool STAMP, bool XL>
 __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ gprog, int nops,
                                                            uint64_t* __restrict__ stamps) {
   __shared__ double red[TAIL_THREADS / 64][2];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   char* lds = reinterpret_cast<char*>(tail_lds);
   if (STAMP && t == 0) stamps[0] = wall_clock64();
+  // op descriptors, double-buffered in LDS: the next op's is fetched by a
+  // few lanes (vector loads, completed at this op's closing barrier) while
+  // this op runs, so an op starts on an LDS read instead of a cold
+  // scalar-cache round trip to the program in global memory
+  constexpr int TW = (int)(sizeof(TOp) / 8);
+  __shared__ uint64_t pbuf[2][TW];
+  const uint64_t* gw = reinterpret_cast<const uint64_t*>(gprog);
+  if (t < TW) pbuf[0][t] = gw[t];
+  __syncthreads();
   for (int k = 0; k < nops; ++k) {
-    const TOp o = tail_resolve(gprog[k], lds);   // uniform: scalar loads
+    TOp od;
+    __builtin_memcpy(&od, pbuf[k & 1], sizeof(TOp));
+    const TOp o = tail_resolve(od, lds);   // uniform
+    if (k + 1 < nops && t < TW) pbuf[(k + 1) & 1][t] = gw[(size_t)(k + 1) * TW + t];
     switch (o.kind) {
       case T_COPY:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
         break;
-      case T_BSR: tail_bsr(o, false); break;
-      case T_GS: tail_bsr(o, true); break;
+      case T_BSR: tail_bsr<XL>(o, false); break;
+      case T_GS: tail_bsr<XL>(o, true); break;
       case T_BD:
         for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
           const double b0 = o.b[2 * I], b1 = o.b[2 * I + 1];
-          const dv4 w = o.W[I];
+          const dv4 w = gload(o.W + I);
           o.out[2 * I] = w.x * b0 + w.y * b1;
           o.out[2 * I + 1] = w.z * b0 + w.w * b1;
         }
@@ -1050,8 +1113,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
             const double* a = o.w + (int64_t)t * o.n;
             double s0 = 0.0, s1 = 0.0;
             int j = 0;
-            for (; j + 1 < (int)o.n; j += 2) { s0 += a[j] * o.x[j]; s1 += a[j + 1] * o.x[j + 1]; }
-            if (j < (int)o.n) s0 += a[j] * o.x[j];
+            for (; j + 1 < (int)o.n; j += 2) { s0 += gload(a + j) * o.x[j]; s1 += gload(a + j + 1) * o.x[j + 1]; }
+            if (j < (int)o.n) s0 += gload(a + j) * o.x[j];
             o.out[t] = s0 + s1;
           }
           break;
@@ -1061,7 +1124,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           double sum = 0.0;
           if (row < o.n) {
             const double* a = o.w + row * o.n;
-            for (int64_t j = lane; j < o.n; j += 64) sum += a[j] * o.x[j];
+            for (int64_t j = lane; j < o.n; j += 64) sum += gload(a + j) * o.x[j];
           }
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
@@ -1936,7 +1999,7 @@ struct DeviceHandle {
   int tail_level = 0;
   std::vector<double> kregion_ms;  // select_k_region: K ms per candidate region, the one kept
   int kregion_best = -1;
-  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; };
+  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; bool xl; };
   mutable std::vector<TailProg> tails;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
@@ -3611,9 +3674,13 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   static std::atomic<uint64_t> attr_devices{0};   // the attribute is set once per device
   const int dev = h->device & 63;
   if (!(attr_devices >> dev & 1)) {
-    if (hipFuncSetAttribute((const void*)tail_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)tail_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)TAIL_LDS_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void*)tail_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)tail_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)TAIL_LDS_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void*)tail_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)TAIL_LDS_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void*)tail_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)TAIL_LDS_MAX) != hipSuccess) {
       (void)hipGetLastError();
       return 0;                        // no large dynamic LDS: keep the global-vector program
@@ -3662,6 +3729,9 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       bytes += sub[k].bytes;
     }
     const int64_t lds = tail_lds_plan(h, l, &prog);
+    bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
+    for (const TOp& t : prog)
+      if ((t.kind == T_BSR || t.kind == T_GS) && !((uintptr_t)t.x & 1)) xl = false;
     void* d = nullptr;
     if (hipMalloc(&d, prog.size() * sizeof(TOp)) != hipSuccess) { (void)hipGetLastError(); return false; }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
@@ -3669,12 +3739,13 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       (void)hipFree(d);
       return false;
     }
-    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds});
+    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl});
     tp = &h->tails.back();
   }
   Op o;
   o.kind = OP_TAIL; o.cls = C_COARSE; o.prog = tp->prog; o.n = tp->n; o.bytes = tp->bytes;
   o.r0 = tp->lds;   // dynamic LDS bytes (0: the program reads global vectors)
+  o.r1 = tp->xl ? 1 : 0;
   ops->push_back(o);
   return true;
 }
@@ -4111,7 +4182,8 @@ void launch(const Op& o, hipStream_t s) {
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
       break;
     case OP_TAIL:
-      if (o.n) tail_kernel<false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
+      if (o.n && o.r1 == 1) tail_kernel<false, true><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
+      else if (o.n) tail_kernel<false, false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
       break;
     case OP_CSCALE:
       if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
@@ -4969,7 +5041,8 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
       HIPCHK(hipMalloc(&dst, (tp.n + 1) * sizeof(uint64_t)));
       HIPCHK(hipMemcpy(prog.data(), tp.prog, tp.n * sizeof(TOp), hipMemcpyDeviceToHost));
       for (int rep = 0; rep < 2; ++rep)
-        tail_kernel<true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
+        if (tp.xl) tail_kernel<true, true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
+        else tail_kernel<true, false><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
       HIPCHK(hipStreamSynchronize(s));
       HIPCHK(hipMemcpy(st.data(), dst, (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
       (void)hipFree(dst);
