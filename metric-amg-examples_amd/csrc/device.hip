@@ -924,7 +924,10 @@ __device__ __forceinline__ dv4 tail_blk(const double* v, const double* off, int 
 // x(c) as a pair; XL: x is in the workgroup's LDS (ds_read, not a flat load)
 template <bool XL>
 __device__ __forceinline__ double2 tail_x(const double2* x2, int c) {
-  if (XL) return *((const __attribute__((address_space(3))) double2*)x2 + c);
+  if (XL) {
+    const dv2 v = *((const __attribute__((address_space(3))) dv2*)x2 + c);
+    return double2{v.x, v.y};
+  }
   return x2[c];
 }
 
