@@ -854,7 +854,13 @@ __global__ __launch_bounds__(256) void gs2_kernel(
 // this replaces tens of thousands of ~5 us launches per apply.
 // ---------------------------------------------------------------------------
 enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7,
-             T_COPY = 8 };
+             T_COPY = 8, T_TOUCH = 9 };
+// T_TOUCH (the program's first op): one load per lane of every 16 KB chunk
+// of the tail levels' matrices (x: table of (chunk address, valid bytes),
+// n chunks <= TOUCH_MAX), so the ops that follow find them in this XCD's L2
+// instead of one HBM / MALL round trip per op; the loaded values are summed
+// into a never-taken store
+constexpr int TOUCH_MAX = 32;
 // LDS residency (tail_lds_plan): the program itself and every work vector of
 // the tail levels live in the workgroup's LDS for the whole launch; a vector
 // field of a TOp then holds (byte offset in the dynamic LDS) | 1 instead of a
@@ -1094,6 +1100,23 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       case T_COPY:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
         break;
+      case T_TOUCH: {
+        const int64_t* tab = reinterpret_cast<const int64_t*>(o.x);
+        double v[TOUCH_MAX];
+#pragma unroll
+        for (int j = 0; j < TOUCH_MAX; ++j) {
+          v[j] = 0.0;
+          if (j < (int)o.n) {
+            const char* base = reinterpret_cast<const char*>(gload(tab + 2 * j));
+            if ((int64_t)t * 16 + 16 <= gload(tab + 2 * j + 1)) v[j] = gload(reinterpret_cast<const dv2*>(base) + t).x;
+          }
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < TOUCH_MAX; ++j) acc += v[j];
+        if (acc == 1.0e308) red[0][0] = acc;   // keeps the loads; red is scratch between ops
+        break;
+      }
       case T_BSR: tail_bsr<XL>(o, false); break;
       case T_GS: tail_bsr<XL>(o, true); break;
       case T_BD:
@@ -3735,8 +3758,54 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
       if ((t.kind == T_BSR || t.kind == T_GS) && !((uintptr_t)t.x & 1)) xl = false;
+    // L2 warm-up table (T_TOUCH): the distinct matrix arrays the ops read,
+    // deepest levels first (visited most), cut into 16 KB chunks
+    std::vector<std::pair<const void*, int64_t>> arrs;
+    auto arr = [&](const void* p, int64_t bytes) {
+      if (!p || bytes < 16) return;
+      for (const auto& a : arrs)
+        if (a.first == p) return;
+      arrs.push_back({p, bytes});
+    };
+    for (auto it = sub.rbegin(); it != sub.rend(); ++it) {
+      const Op& o = *it;
+      if ((o.kind == OP_BSR || o.kind == OP_GS) && o.Mb) {
+        const DBsr& M = *o.Mb;
+        arr(M.ptr, 8 * (M.nr + 1));
+        arr(M.col, 4 * M.nb);
+        arr(M.val, (M.sym ? 24 : 32) * M.nb);
+        if (o.W) arr(o.W, 32 * M.nr);
+        if (o.perm) arr(o.perm, 4 * M.nr);
+      } else if (o.kind == OP_BD) {
+        arr(o.W, 32 * o.n);
+      } else if (o.kind == OP_GEMV) {
+        arr(o.w, 8 * o.n * o.n);
+      }
+    }
+    std::vector<int64_t> tab;
+    for (const auto& a : arrs)
+      for (int64_t off = 0; off + 16 <= a.second && (int64_t)tab.size() < 2 * TOUCH_MAX; off += 16384) {
+        tab.push_back((int64_t)((const char*)a.first + off));
+        tab.push_back(std::min<int64_t>(16384, a.second - off));
+      }
+    if (!tab.empty() && !std::getenv("MAMG_TAIL_NOTOUCH")) {
+      TOp t;
+      t.kind = T_TOUCH;
+      t.n = (int64_t)tab.size() / 2;
+      prog.insert(prog.begin(), t);
+    } else {
+      tab.clear();
+    }
+    const size_t pbytes = prog.size() * sizeof(TOp);
     void* d = nullptr;
-    if (hipMalloc(&d, prog.size() * sizeof(TOp)) != hipSuccess) { (void)hipGetLastError(); return false; }
+    if (hipMalloc(&d, pbytes + tab.size() * sizeof(int64_t)) != hipSuccess) { (void)hipGetLastError(); return false; }
+    if (!tab.empty()) prog[0].x = reinterpret_cast<const double*>((char*)d + pbytes);
+    if (!tab.empty() &&
+        hipMemcpy((char*)d + pbytes, tab.data(), tab.size() * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(d);
+      return false;
+    }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipGetLastError();
       (void)hipFree(d);
