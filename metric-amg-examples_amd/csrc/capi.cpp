@@ -550,12 +550,6 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
   mamg::Hierarchy H;
   std::string err;
-  // parameters first: an invalid or single-GPU-only profile is refused
-  // before the rank touches its GPU
-  if ((rc = mamg::check_params(P, &err)) || (rc = mamg::dist_check(P, &err))) {
-    set_error(err);
-    return rc;
-  }
   Seeds S(idofs, n_idofs, v.n, &P);
   rc = mamg::host_setup(v, S.ptr, S.n, P, &H, &err);
   if (rc) { set_error(err); return rc; }

@@ -4270,6 +4270,7 @@ int order_begin(DeviceHandle* h, hipStream_t s, std::string* err) {
   return MAMG_OK;
 }
 int order_end(DeviceHandle* h, hipStream_t s, std::string* err) {
+  if (!h->last) HIPCHK(hipEventCreateWithFlags(&h->last, hipEventDisableTiming));   // the upload's own mark
   HIPCHK(hipEventRecord(h->last, s));
   return MAMG_OK;
 }
