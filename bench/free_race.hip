@@ -9,9 +9,13 @@
 // U by one of several paths on stream S2, drains, and reads the kernel's sum:
 // old (= n) means the kernel still saw T's data, new (= 2n) means U's write
 // landed under the running reader.
+// Run: free_race [spin_ms] [buffer_bytes] (default 200 ms, 64 MB); small
+// buffers may come from the runtime's sub-allocator, whose frees can behave
+// differently from a whole-allocation unmap.
 // Build: hipcc -O3 --offload-arch=gfx950 free_race.hip -o free_race
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -53,18 +57,18 @@ int main(int argc, char** argv) {
   int rate_khz = 0;
   CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
   const uint64_t ticks = (uint64_t)(spin_ms * rate_khz);
-  const int64_t n = 8 << 20;                       // 64 MB of doubles
+  const int64_t n = argc > 2 ? std::max<int64_t>(64, std::atoll(argv[2]) / 8) : (8 << 20);   // doubles
   const size_t bytes = n * sizeof(double);
   std::vector<double> two(n, 2.0);
   double *out, *src;
   CK(hipMalloc(&out, sizeof(double)));
   CK(hipMalloc(&src, bytes));
-  fill_kernel<<<(unsigned)(n / 256), 256>>>(src, n, 2.0);
+  fill_kernel<<<(unsigned)((n + 255) / 256), 256>>>(src, n, 2.0);
   CK(hipDeviceSynchronize());
   hipStream_t nb1, nb2;
   CK(hipStreamCreateWithFlags(&nb1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&nb2, hipStreamNonBlocking));
-  std::printf("wall clock %d kHz, spin %.0f ms, buffer %zu MB\n", rate_khz, spin_ms, bytes >> 20);
+  std::printf("wall clock %d kHz, spin %.0f ms, buffer %zu bytes\n", rate_khz, spin_ms, bytes);
   struct Case { const char* name; hipStream_t s1, s2; Writer w; bool async_free; };
   const Case cases[] = {
       {"reader null, writer null", nullptr, nullptr, W_KERNEL, false},
@@ -83,7 +87,7 @@ int main(int argc, char** argv) {
     double* T = nullptr;
     if (c.async_free) CK(hipMallocAsync((void**)&T, bytes, c.s1));
     else CK(hipMalloc(&T, bytes));
-    fill_kernel<<<(unsigned)(n / 256), 256, 0, c.s1>>>(T, n, 1.0);
+    fill_kernel<<<(unsigned)((n + 255) / 256), 256, 0, c.s1>>>(T, n, 1.0);
     CK(hipDeviceSynchronize());
     spin_sum_kernel<<<1, 64, 0, c.s1>>>(T, n, ticks, out);
     const double t0 = now_ms();
@@ -94,7 +98,7 @@ int main(int argc, char** argv) {
     if (c.async_free) CK(hipMallocAsync((void**)&U, bytes, c.s2));
     else CK(hipMalloc(&U, bytes));
     switch (c.w) {
-      case W_KERNEL: fill_kernel<<<(unsigned)(n / 256), 256, 0, c.s2>>>(U, n, 2.0); break;
+      case W_KERNEL: fill_kernel<<<(unsigned)((n + 255) / 256), 256, 0, c.s2>>>(U, n, 2.0); break;
       case W_H2D: CK(hipMemcpy(U, two.data(), bytes, hipMemcpyHostToDevice)); break;
       case W_H2D_ASYNC: CK(hipMemcpyAsync(U, two.data(), bytes, hipMemcpyHostToDevice, c.s2)); break;
       case W_D2D: CK(hipMemcpy(U, src, bytes, hipMemcpyDeviceToDevice)); break;
