@@ -844,7 +844,7 @@ __global__ __launch_bounds__(256) void gs2_kernel(
 
 // ---------------------------------------------------------------------------
 // Coarse tail: the whole cycle of the levels from tail_level down (the
-// recursion below one coarse level, V or W), run by ONE workgroup of 1024
+// recursion below one coarse level, V or W), run by ONE workgroup of 512
 // threads that walks the same op list the launch path would launch, with a
 // workgroup barrier between ops instead of a kernel boundary.  Each op
 // computes every row exactly as its kernel does (same lane groups, chunks,
@@ -880,8 +880,39 @@ struct TOp {
   double* out = nullptr;
   const int32_t* perm = nullptr;
   double* part = nullptr;
+  // LDS staging (tail_stage_plan): stg >= 0 = byte offset of the staging
+  // buffer the op's matrix slice (row pointers, permutation, smoother blocks,
+  // columns and values of blocks [k0, k1)) is copied into while the previous
+  // op runs; -1 = read from global memory
+  int stg = -1, pad_ = 0;
+  int64_t k0 = 0, k1 = 0;
 };
-constexpr int TAIL_THREADS = 1024;
+// 512 threads: 256 VGPRs per lane (1024 would cap them at 128 and spill the
+// interpreter's loop state to scratch); the tail's ops hold a few hundred
+// rows x <= 4 lanes, so one or two passes either way
+constexpr int TAIL_THREADS = 512;
+
+// byte offsets of a staged op's arrays in its staging buffer (host and device)
+struct StageLayout {
+  int64_t ptr, perm, W, col, val, offd, total;
+};
+__host__ __device__ inline StageLayout stage_layout(bool gs, int64_t rows, int64_t nbk, bool hasW, bool sym) {
+  StageLayout L;
+  int64_t o = 0;
+  L.ptr = o;
+  o += (8 * (rows + 1) + 15) / 16 * 16;
+  L.perm = o;
+  if (gs) o += (4 * rows + 15) / 16 * 16;
+  L.W = o;
+  if (hasW) o += 32 * rows;
+  L.col = o;
+  o += (4 * nbk + 15) / 16 * 16;
+  L.val = o;
+  L.offd = o + 16 * nbk;   // sym: the (0,1) stream after the diagonal pairs
+  o += sym ? (24 * nbk + 15) / 16 * 16 : 32 * nbk;
+  L.total = o;
+  return L;
+}
 
 template <class T>
 __device__ __forceinline__ T* tail_res(T* p, char* lds) {
@@ -937,18 +968,106 @@ __device__ __forceinline__ double2 tail_x(const double2* x2, int c) {
   return x2[c];
 }
 
+#define AS1 __attribute__((address_space(1)))
+#define AS3 __attribute__((address_space(3)))
+
+// the matrix side of a tail SpMV / GS op: global arrays (ML false) or the
+// op's LDS staging buffer (ML true: indices shifted by the first staged row
+// r0 and block k0)
+template <bool ML>
+struct TailMat;
+template <>
+struct TailMat<false> {
+  const TOp& o;
+  const double* offd;
+  __device__ TailMat(const TOp& op, char*) : o(op), offd(op.sym ? op.val + 2 * op.nb : nullptr) {}
+  __device__ int P(int i) const { return (int)gload(o.ptr + i); }
+  __device__ int32_t perm(int i) const { return gload(o.perm + i); }
+  __device__ dv4 W(int i) const { return gload(o.W + i); }
+  __device__ int32_t C(int k) const { return gload(o.col + k); }
+  __device__ dv4 V(int k) const { return o.sym ? tail_blk<true>(o.val, offd, k) : tail_blk<false>(o.val, nullptr, k); }
+};
+template <>
+struct TailMat<true> {
+  const AS3 int64_t* ptr;
+  const AS3 int32_t* pm;
+  const AS3 dv4* w;
+  const AS3 int32_t* col;
+  const AS3 char* val;
+  int r0, k0, nbk;
+  bool sym;
+  __device__ TailMat(const TOp& o, char* lds) {
+    const bool gs = o.kind == T_GS;
+    r0 = gs ? (int)o.r0 : 0;
+    k0 = (int)o.k0;
+    nbk = (int)(o.k1 - o.k0);
+    sym = o.sym != 0;
+    const StageLayout L = stage_layout(gs, gs ? o.r1 - o.r0 : o.n, nbk, o.W != nullptr, sym);
+    const AS3 char* b = (const AS3 char*)(lds + o.stg);
+    ptr = (const AS3 int64_t*)(b + L.ptr);
+    pm = (const AS3 int32_t*)(b + L.perm);
+    w = (const AS3 dv4*)(b + L.W);
+    col = (const AS3 int32_t*)(b + L.col);
+    val = b + L.val;
+  }
+  __device__ int P(int i) const { return (int)ptr[i - r0]; }
+  __device__ int32_t perm(int i) const { return pm[i - r0]; }
+  __device__ dv4 W(int i) const { return w[i - r0]; }
+  __device__ int32_t C(int k) const { return col[k - k0]; }
+  __device__ dv4 V(int k) const {
+    if (sym) {
+      const dv2 d = ((const AS3 dv2*)val)[k - k0];
+      const double b = ((const AS3 double*)(val + 16 * (int64_t)nbk))[k - k0];
+      return dv4{d.x, b, b, d.y};
+    }
+    return ((const AS3 dv4*)val)[k - k0];
+  }
+};
+
+// copy `bytes` (a multiple of 4) from global src into the LDS at byte offset
+// dst with direct global -> LDS loads (no VGPRs, completed by vmcnt at the
+// issuing op's closing barrier): wave w copies 256-byte chunks w, w + 16, ..
+__device__ __forceinline__ void stage_range(const void* src, char* lds, int64_t dst, int64_t bytes) {
+  const int words = (int)(bytes >> 2);
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  for (int c = wave; c * 64 < words; c += TAIL_THREADS / 64) {
+    const int idx = c * 64 + lane;
+    if (idx < words)
+      __builtin_amdgcn_global_load_lds((AS1 void*)((const char*)src + 4 * (int64_t)idx),
+                                       (AS3 void*)(lds + dst + 256 * (int64_t)c), 4, 0, 0);
+  }
+}
+
+// the staged slice of op n (raw descriptor: global matrix pointers)
+__device__ void stage_op(const TOp& n, char* lds) {
+  const bool gs = n.kind == T_GS;
+  const int64_t r0 = gs ? n.r0 : 0, rows = gs ? n.r1 - n.r0 : n.n, nbk = n.k1 - n.k0;
+  const StageLayout L = stage_layout(gs, rows, nbk, n.W != nullptr, n.sym != 0);
+  const int64_t b = n.stg;
+  stage_range(n.ptr + r0, lds, b + L.ptr, 8 * (rows + 1));
+  if (gs) stage_range(n.perm + r0, lds, b + L.perm, 4 * rows);
+  if (n.W) stage_range(n.W + r0, lds, b + L.W, 32 * rows);
+  stage_range(n.col + n.k0, lds, b + L.col, 4 * nbk);
+  if (n.sym) {
+    stage_range(n.val + 2 * n.k0, lds, b + L.val, 16 * nbk);
+    stage_range(n.val + 2 * n.nb + n.k0, lds, b + L.offd, 8 * nbk);
+  } else {
+    stage_range(n.val + 4 * n.k0, lds, b + L.val, 32 * nbk);
+  }
+}
+
 // rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
 // vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place.
-// XL: the gathered vector x lives in LDS
-template <bool XL>
-__device__ void tail_bsr(const TOp& o, bool gs) {
+// XL: the gathered vector x lives in LDS; ML: the matrix slice too (staged)
+template <bool XL, bool ML>
+__device__ void tail_bsr(const TOp& o, bool gs, char* lds) {
+  const TailMat<ML> M(o, lds);
   // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
   // a 64-bit division per row chunk cost more than the chunk's loads
   const int VL = o.vl, lvl = 31 - __builtin_clz(VL);
   const int lane = threadIdx.x & (VL - 1);
   const int rows = (int)(gs ? o.r1 - o.r0 : o.n);
   const int row0 = gs ? (int)o.r0 : 0;
-  const double* offd = o.sym ? o.val + 2 * o.nb : nullptr;
   const double2* x2 = reinterpret_cast<const double2*>(o.x);
   for (int base = 0; base < (rows << lvl); base += TAIL_THREADS) {   // uniform trip count
     const int v = base + (int)threadIdx.x;
@@ -961,12 +1080,12 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     // loads together, branch-free (a dead lane reads row row0 and drops it),
     // so they form one round trip instead of a chain behind a branch
     const int nodec = live ? node : row0;
-    const int p0 = (int)gload(o.ptr + nodec), p1 = live ? (int)gload(o.ptr + nodec + 1) : p0;
+    const int p0 = M.P(nodec), p1 = live ? M.P(nodec + 1) : p0;
     int gI = -1;
     dv4 gd = {0.0, 0.0, 0.0, 0.0};
     if (gs) {
-      gI = live ? gload(o.perm + nodec) : -1;
-      gd = gload(o.W + nodec);
+      gI = live ? M.perm(nodec) : -1;
+      gd = M.W(nodec);
     }
     const int gIc = gI >= 0 ? gI : 0;
     double gb0 = 0.0, gb1 = 0.0;
@@ -992,8 +1111,8 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         dv4 vv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          cc[q] = gload(o.col + ll[q]);
-          vv[q] = o.sym ? tail_blk<true>(o.val, offd, ll[q]) : tail_blk<false>(o.val, nullptr, ll[q]);
+          cc[q] = M.C(ll[q]);
+          vv[q] = M.V(ll[q]);
         }
         double2 xa[4];
 #pragma unroll
@@ -1010,9 +1129,9 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         const int ka = kb0 + lane, kb = ka + VL;
         const bool ha = ka < p1, hb = kb < p1;
         const int la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
-        const int32_t c0 = gload(o.col + la), c1 = gload(o.col + lb);
-        const dv4 v0 = o.sym ? tail_blk<true>(o.val, offd, la) : tail_blk<false>(o.val, nullptr, la);
-        const dv4 v1 = o.sym ? tail_blk<true>(o.val, offd, lb) : tail_blk<false>(o.val, nullptr, lb);
+        const int32_t c0 = M.C(la), c1 = M.C(lb);
+        const dv4 v0 = M.V(la);
+        const dv4 v1 = M.V(lb);
         const double2 a = tail_x<XL>(x2, c0), e = tail_x<XL>(x2, c1);
         s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
         s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
@@ -1054,12 +1173,12 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
       o0 = o.b[2 * node] - s0; o1 = o.b[2 * node + 1] - s1;
     } else if (o.epi == EPI_KPOST) {
       const double r0 = o.b[2 * node], r1 = o.b[2 * node + 1];
-      const dv4 w = gload(o.W + node);
+      const dv4 w = M.W(node);
       o0 = o.y[2 * node] + (w.x * r0 + w.y * r1) + s0;
       o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1) + s1;
     } else {  // EPI_BJAC
       const double r0 = o.b[2 * node] - s0, r1 = o.b[2 * node + 1] - s1;
-      const dv4 w = gload(o.W + node);
+      const dv4 w = M.W(node);
       o0 = o.y[2 * node] + (w.x * r0 + w.y * r1);
       o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1);
     }
@@ -1086,39 +1205,71 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
   // few lanes (vector loads, completed at this op's closing barrier) while
   // this op runs, so an op starts on an LDS read instead of a cold
   // scalar-cache round trip to the program in global memory
+  // Three slots: op k's descriptor, op k + 1's (fetched during op k - 1,
+  // read now to start copying its matrix slice into LDS when it is staged),
+  // and op k + 2's, fetched during op k.
   constexpr int TW = (int)(sizeof(TOp) / 8);
-  __shared__ uint64_t pbuf[2][TW];
+  __shared__ uint64_t pbuf[3][TW];
   const uint64_t* gw = reinterpret_cast<const uint64_t*>(gprog);
-  if (t < TW) pbuf[0][t] = gw[t];
+  if (t < TW) {
+    pbuf[0][t] = gw[t];
+    if (nops > 1) pbuf[1][t] = gw[TW + t];
+  }
   __syncthreads();
+  int s0i = 0, s1i = 1, s2i = 2;   // slots of ops k, k + 1, k + 2
   for (int k = 0; k < nops; ++k) {
     TOp od;
-    __builtin_memcpy(&od, pbuf[k & 1], sizeof(TOp));
+    __builtin_memcpy(&od, pbuf[s0i], sizeof(TOp));
     const TOp o = tail_resolve(od, lds);   // uniform
-    if (k + 1 < nops && t < TW) pbuf[(k + 1) & 1][t] = gw[(size_t)(k + 1) * TW + t];
+    if (k + 2 < nops && t < TW) pbuf[s2i][t] = gw[(size_t)(k + 2) * TW + t];
+    if (XL && k + 1 < nops) {
+      const TOp* nx = reinterpret_cast<const TOp*>(pbuf[s1i]);
+      if (nx->stg >= 0) {
+        TOp n;
+        __builtin_memcpy(&n, nx, sizeof(TOp));
+        stage_op(n, lds);
+      }
+    }
+    {
+      const int r = s0i;
+      s0i = s1i;
+      s1i = s2i;
+      s2i = r;
+    }
     switch (o.kind) {
       case T_COPY:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
         break;
       case T_TOUCH: {
         const int64_t* tab = reinterpret_cast<const int64_t*>(o.x);
-        double v[TOUCH_MAX];
-#pragma unroll
-        for (int j = 0; j < TOUCH_MAX; ++j) {
-          v[j] = 0.0;
-          if (j < (int)o.n) {
-            const char* base = reinterpret_cast<const char*>(gload(tab + 2 * j));
-            if ((int64_t)t * 16 + 16 <= gload(tab + 2 * j + 1)) v[j] = gload(reinterpret_cast<const dv2*>(base) + t).x;
-          }
-        }
         double acc = 0.0;
+        for (int j0 = 0; j0 < (int)o.n; j0 += 8) {   // 8 loads in flight per lane (few VGPRs)
+          double v[8];
 #pragma unroll
-        for (int j = 0; j < TOUCH_MAX; ++j) acc += v[j];
+          for (int j = 0; j < 8; ++j) {
+            v[j] = 0.0;
+            if (j0 + j < (int)o.n) {
+              const char* base = reinterpret_cast<const char*>(gload(tab + 2 * (j0 + j)));
+              const int64_t valid = gload(tab + 2 * (j0 + j) + 1);
+              for (int64_t i = t; 16 * i + 16 <= valid; i += TAIL_THREADS)
+                v[j] += gload(reinterpret_cast<const dv2*>(base) + i).x;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += v[j];
+        }
         if (acc == 1.0e308) red[0][0] = acc;   // keeps the loads; red is scratch between ops
         break;
       }
-      case T_BSR: tail_bsr<XL>(o, false); break;
-      case T_GS: tail_bsr<XL>(o, true); break;
+      case T_BSR:
+      case T_GS:
+        if constexpr (XL) {
+          if (o.stg >= 0) tail_bsr<true, true>(o, o.kind == T_GS, lds);
+          else tail_bsr<true, false>(o, o.kind == T_GS, lds);
+        } else {
+          tail_bsr<false, false>(o, o.kind == T_GS, lds);
+        }
+        break;
       case T_BD:
         for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
           const double b0 = o.b[2 * I], b1 = o.b[2 * I + 1];
@@ -3739,6 +3890,44 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   return off;
 }
 
+// LDS staging plan of a tail program (TOp::stg; needs the LDS-resident
+// vectors of tail_lds_plan, whose `lds` bytes come first): two staging
+// buffers of up to 32 KB after them; the SpMV / GS ops whose slice (rows,
+// their blocks) fits a buffer are staged, alternately into the two, so the
+// copy for op i (issued while op i - 1 runs) never lands in the buffer op
+// i - 1 reads.  Returns the program's dynamic LDS bytes.
+int64_t tail_stage_plan(std::vector<TOp>* prog, int64_t lds) {
+  if (lds <= 0 || std::getenv("MAMG_TAIL_NOSTAGE")) return lds;
+  const int64_t base = (lds + 255) / 256 * 256;
+  const int64_t SB = std::min<int64_t>(32768, (TAIL_LDS_MAX - base) / 2) / 256 * 256;
+  if (SB < 4096) return lds;
+  std::map<const int64_t*, std::vector<int64_t>> ptrs;   // row pointers, downloaded once per matrix
+  int cnt = 0;
+  for (size_t i = 1; i < prog->size(); ++i) {
+    TOp& o = (*prog)[i];
+    if (o.kind != T_GS && o.kind != T_BSR) continue;
+    const bool gs = o.kind == T_GS;
+    auto it = ptrs.find(o.ptr);
+    if (it == ptrs.end()) {
+      std::vector<int64_t> hp(o.n + 1);
+      if (hipMemcpy(hp.data(), o.ptr, (o.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipGetLastError();
+        return lds;
+      }
+      it = ptrs.emplace(o.ptr, std::move(hp)).first;
+    }
+    const int64_t r0 = gs ? o.r0 : 0, r1 = gs ? o.r1 : o.n;
+    const int64_t k0 = it->second[r0], k1 = it->second[r1];
+    const StageLayout L = stage_layout(gs, r1 - r0, k1 - k0, o.W != nullptr, o.sym != 0);
+    if (L.total > SB) continue;
+    o.stg = (int)(base + (cnt & 1) * SB);
+    o.k0 = k0;
+    o.k1 = k1;
+    ++cnt;
+  }
+  return cnt ? base + 2 * SB : lds;
+}
+
 // the cycle of level l and everything below as one tail_kernel launch; the
 // device op list is built once per (b, x) and kept on the handle
 bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
@@ -3754,10 +3943,11 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       if (!to_tail(sub[k], &prog[k])) return false;
       bytes += sub[k].bytes;
     }
-    const int64_t lds = tail_lds_plan(h, l, &prog);
+    int64_t lds = tail_lds_plan(h, l, &prog);
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
       if ((t.kind == T_BSR || t.kind == T_GS) && !((uintptr_t)t.x & 1)) xl = false;
+    if (xl) lds = tail_stage_plan(&prog, lds);
     // L2 warm-up table (T_TOUCH): the distinct matrix arrays the ops read,
     // deepest levels first (visited most), cut into 16 KB chunks
     std::vector<std::pair<const void*, int64_t>> arrs;
