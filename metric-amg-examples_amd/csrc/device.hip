@@ -4743,6 +4743,8 @@ void apply_k_layout_knob(DeviceHandle* h) {
     if (!D.coarsest) set_k_split(D.KPb, 1);
 }
 
+void debug_sums(DeviceHandle* h, const char* stage);
+
 std::string layout_error(const mamg_params& p) {
   if (patch_schwarz(p))
     return "SCHWARZ_PATCHES needs the BSR2 layout (num_functions 2, node-block smoothers on every level)";
@@ -4860,6 +4862,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   // before the handle's first use on any stream (order_begin waits on it)
   if ((rc = order_end(h.get(), nullptr, err))) return rc;
   HIPCHK(hipEventSynchronize(h->last));
+  debug_sums(h.get(), "upload");
   h->layout_ms[LT_FINISH] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
   *out = h.release();
@@ -5027,6 +5030,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   set_tail_level(h.get());
   if ((rc = order_end(h.get(), nullptr, err))) return rc;   // as in dev_upload
   HIPCHK(hipEventSynchronize(h->last));
+  debug_sums(h.get(), "upload");
   const auto t3 = std::chrono::steady_clock::now();
   h->layout_ms[LT_FINISH] = std::chrono::duration<double, std::milli>(t3 - t2).count();
   h->setup_ms[GS_LAYOUT] = std::chrono::duration<double, std::milli>(t3 - t0).count();
@@ -5070,8 +5074,55 @@ void dev_kregion(const DeviceHandle* h, std::vector<double>* ms, int* kept) {
   *kept = h->kregion_best;
 }
 
+// MAMG_DEBUG_SUMS=1 (diagnosis): a 64-bit FNV-1a hash of every operator
+// array of the handle, per level, printed to stderr at the end of the upload
+// and before each apply, so two handles of one problem (which must hold the
+// same bytes wherever they live) name the array that differs
+void debug_sums(DeviceHandle* h, const char* stage) {
+  static const bool on = [] {
+    const char* e = std::getenv("MAMG_DEBUG_SUMS");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!on) return;
+  (void)hipDeviceSynchronize();
+  auto hash = [](const void* p, size_t b) -> unsigned long long {
+    if (!p || !b) return 0ull;
+    std::vector<unsigned char> v(b);
+    if (hipMemcpy(v.data(), p, b, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return 1ull; }
+    unsigned long long x = 1469598103934665603ull;
+    for (unsigned char c : v) x = (x ^ c) * 1099511628211ull;
+    return x;
+  };
+  std::string line;
+  char buf[160];
+  for (size_t l = 0; l < h->L.size(); ++l) {
+    const DLevel& L = h->L[l];
+    const std::pair<const char*, const DBsr*> ms[] = {{"A", &L.Ab}, {"K", &L.KPb}, {"PA", &L.PAb}, {"P", &L.Pb},
+                                                      {"R", &L.Rb}, {"G", &L.Gb}};
+    for (const auto& m : ms) {
+      const DBsr& M = *m.second;
+      if (!M.nr) continue;
+      const int per = (M.sym || M.half) ? 3 : 4;
+      const int64_t slots = (M.sell || M.half) ? M.nbs : M.nb;
+      std::snprintf(buf, sizeof buf, " L%zu.%s val %016llx col %016llx", l, m.first,
+                    hash(M.val, (size_t)slots * per * 8), hash(M.col, (size_t)slots * 4));
+      line += buf;
+    }
+    if (L.Wd) {
+      std::snprintf(buf, sizeof buf, " L%zu.W %016llx", l, hash(L.Wd, (size_t)(L.n / 2) * 32));
+      line += buf;
+    }
+    if (L.Ainv) {
+      std::snprintf(buf, sizeof buf, " L%zu.Ainv %016llx", l, hash(L.Ainv, (size_t)L.n * L.n * 8));
+      line += buf;
+    }
+  }
+  std::fprintf(stderr, "[mamg sums] %s%s\n", stage, line.c_str());
+}
+
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
+  debug_sums(h, "apply");
   HIPCHK(hipSetDevice(h->device));
   hipGraphExec_t exec;
   int rc = get_graph(h, d_r, d_z, &exec, err);
