@@ -854,13 +854,7 @@ __global__ __launch_bounds__(256) void gs2_kernel(
 // this replaces tens of thousands of ~5 us launches per apply.
 // ---------------------------------------------------------------------------
 enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7,
-             T_COPY = 8, T_TOUCH = 9 };
-// T_TOUCH (the program's first op): one load per lane of every 16 KB chunk
-// of the tail levels' matrices (x: table of (chunk address, valid bytes),
-// n chunks <= TOUCH_MAX), so the ops that follow find them in this XCD's L2
-// instead of one HBM / MALL round trip per op; the loaded values are summed
-// into a never-taken store
-constexpr int TOUCH_MAX = 32;
+             T_COPY = 8 };
 // LDS residency (tail_lds_plan): the program itself and every work vector of
 // the tail levels live in the workgroup's LDS for the whole launch; a vector
 // field of a TOp then holds (byte offset in the dynamic LDS) | 1 instead of a
@@ -880,39 +874,12 @@ struct TOp {
   double* out = nullptr;
   const int32_t* perm = nullptr;
   double* part = nullptr;
-  // LDS staging (tail_stage_plan): stg >= 0 = byte offset of the staging
-  // buffer the op's matrix slice (row pointers, permutation, smoother blocks,
-  // columns and values of blocks [k0, k1)) is copied into while the previous
-  // op runs; -1 = read from global memory
-  int stg = -1, pad_ = 0;
-  int64_t k0 = 0, k1 = 0;
 };
 // 512 threads: 256 VGPRs per lane (1024 would cap them at 128 and spill the
 // interpreter's loop state to scratch); the tail's ops hold a few hundred
 // rows x <= 4 lanes, so one or two passes either way
 constexpr int TAIL_THREADS = 512;
 
-// byte offsets of a staged op's arrays in its staging buffer (host and device)
-struct StageLayout {
-  int64_t ptr, perm, W, col, val, offd, total;
-};
-__host__ __device__ inline StageLayout stage_layout(bool gs, int64_t rows, int64_t nbk, bool hasW, bool sym) {
-  StageLayout L;
-  int64_t o = 0;
-  L.ptr = o;
-  o += (8 * (rows + 1) + 15) / 16 * 16;
-  L.perm = o;
-  if (gs) o += (4 * rows + 15) / 16 * 16;
-  L.W = o;
-  if (hasW) o += 32 * rows;
-  L.col = o;
-  o += (4 * nbk + 15) / 16 * 16;
-  L.val = o;
-  L.offd = o + 16 * nbk;   // sym: the (0,1) stream after the diagonal pairs
-  o += sym ? (24 * nbk + 15) / 16 * 16 : 32 * nbk;
-  L.total = o;
-  return L;
-}
 
 template <class T>
 __device__ __forceinline__ T* tail_res(T* p, char* lds) {
@@ -971,97 +938,23 @@ __device__ __forceinline__ double2 tail_x(const double2* x2, int c) {
 #define AS1 __attribute__((address_space(1)))
 #define AS3 __attribute__((address_space(3)))
 
-// the matrix side of a tail SpMV / GS op: global arrays (ML false) or the
-// op's LDS staging buffer (ML true: indices shifted by the first staged row
-// r0 and block k0)
-template <bool ML>
-struct TailMat;
-template <>
-struct TailMat<false> {
+// the matrix side of a tail SpMV / GS op (global arrays, typed loads)
+struct TailMat {
   const TOp& o;
   const double* offd;
-  __device__ TailMat(const TOp& op, char*) : o(op), offd(op.sym ? op.val + 2 * op.nb : nullptr) {}
+  __device__ explicit TailMat(const TOp& op) : o(op), offd(op.sym ? op.val + 2 * op.nb : nullptr) {}
   __device__ int P(int i) const { return (int)gload(o.ptr + i); }
   __device__ int32_t perm(int i) const { return gload(o.perm + i); }
   __device__ dv4 W(int i) const { return gload(o.W + i); }
   __device__ int32_t C(int k) const { return gload(o.col + k); }
   __device__ dv4 V(int k) const { return o.sym ? tail_blk<true>(o.val, offd, k) : tail_blk<false>(o.val, nullptr, k); }
 };
-template <>
-struct TailMat<true> {
-  const AS3 int64_t* ptr;
-  const AS3 int32_t* pm;
-  const AS3 dv4* w;
-  const AS3 int32_t* col;
-  const AS3 char* val;
-  int r0, k0, nbk;
-  bool sym;
-  __device__ TailMat(const TOp& o, char* lds) {
-    const bool gs = o.kind == T_GS;
-    r0 = gs ? (int)o.r0 : 0;
-    k0 = (int)o.k0;
-    nbk = (int)(o.k1 - o.k0);
-    sym = o.sym != 0;
-    const StageLayout L = stage_layout(gs, gs ? o.r1 - o.r0 : o.n, nbk, o.W != nullptr, sym);
-    const AS3 char* b = (const AS3 char*)(lds + o.stg);
-    ptr = (const AS3 int64_t*)(b + L.ptr);
-    pm = (const AS3 int32_t*)(b + L.perm);
-    w = (const AS3 dv4*)(b + L.W);
-    col = (const AS3 int32_t*)(b + L.col);
-    val = b + L.val;
-  }
-  __device__ int P(int i) const { return (int)ptr[i - r0]; }
-  __device__ int32_t perm(int i) const { return pm[i - r0]; }
-  __device__ dv4 W(int i) const { return w[i - r0]; }
-  __device__ int32_t C(int k) const { return col[k - k0]; }
-  __device__ dv4 V(int k) const {
-    if (sym) {
-      const dv2 d = ((const AS3 dv2*)val)[k - k0];
-      const double b = ((const AS3 double*)(val + 16 * (int64_t)nbk))[k - k0];
-      return dv4{d.x, b, b, d.y};
-    }
-    return ((const AS3 dv4*)val)[k - k0];
-  }
-};
-
-// copy `bytes` (a multiple of 4) from global src into the LDS at byte offset
-// dst with direct global -> LDS loads (no VGPRs, completed by vmcnt at the
-// issuing op's closing barrier): wave w copies 256-byte chunks w, w + 16, ..
-__device__ __forceinline__ void stage_range(const void* src, char* lds, int64_t dst, int64_t bytes) {
-  const int words = (int)(bytes >> 2);
-  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-  for (int c = wave; c * 64 < words; c += TAIL_THREADS / 64) {
-    const int idx = c * 64 + lane;
-    if (idx < words)
-      __builtin_amdgcn_global_load_lds((AS1 void*)((const char*)src + 4 * (int64_t)idx),
-                                       (AS3 void*)(lds + dst + 256 * (int64_t)c), 4, 0, 0);
-  }
-}
-
-// the staged slice of op n (raw descriptor: global matrix pointers)
-__device__ void stage_op(const TOp& n, char* lds) {
-  const bool gs = n.kind == T_GS;
-  const int64_t r0 = gs ? n.r0 : 0, rows = gs ? n.r1 - n.r0 : n.n, nbk = n.k1 - n.k0;
-  const StageLayout L = stage_layout(gs, rows, nbk, n.W != nullptr, n.sym != 0);
-  const int64_t b = n.stg;
-  stage_range(n.ptr + r0, lds, b + L.ptr, 8 * (rows + 1));
-  if (gs) stage_range(n.perm + r0, lds, b + L.perm, 4 * rows);
-  if (n.W) stage_range(n.W + r0, lds, b + L.W, 32 * rows);
-  stage_range(n.col + n.k0, lds, b + L.col, 4 * nbk);
-  if (n.sym) {
-    stage_range(n.val + 2 * n.k0, lds, b + L.val, 16 * nbk);
-    stage_range(n.val + 2 * n.nb + n.k0, lds, b + L.offd, 8 * nbk);
-  } else {
-    stage_range(n.val + 4 * n.k0, lds, b + L.val, 32 * nbk);
-  }
-}
-
 // rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
 // vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place.
-// XL: the gathered vector x lives in LDS; ML: the matrix slice too (staged)
-template <bool XL, bool ML>
-__device__ void tail_bsr(const TOp& o, bool gs, char* lds) {
-  const TailMat<ML> M(o, lds);
+// XL: the gathered vector x lives in LDS
+template <bool XL>
+__device__ void tail_bsr(const TOp& o, bool gs) {
+  const TailMat M(o);
   // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
   // a 64-bit division per row chunk cost more than the chunk's loads
   const int VL = o.vl, lvl = 31 - __builtin_clz(VL);
@@ -1195,81 +1088,48 @@ extern __shared__ double tail_lds[];
 // XL: every SpMV / GS op of the program gathers from an LDS-resident x
 // (tail_lds_plan placed all of them), so the gathers are ds_reads
 template <bool STAMP, bool XL>
-__global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ gprog, int nops,
+__global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ gprog, int nops, int prog_lds,
                                                            uint64_t* __restrict__ stamps) {
   __shared__ double red[TAIL_THREADS / 64][2];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   char* lds = reinterpret_cast<char*>(tail_lds);
   if (STAMP && t == 0) stamps[0] = wall_clock64();
-  // op descriptors, double-buffered in LDS: the next op's is fetched by a
-  // few lanes (vector loads, completed at this op's closing barrier) while
-  // this op runs, so an op starts on an LDS read instead of a cold
-  // scalar-cache round trip to the program in global memory
-  // Three slots: op k's descriptor, op k + 1's (fetched during op k - 1,
-  // read now to start copying its matrix slice into LDS when it is staged),
-  // and op k + 2's, fetched during op k.
+  // the op descriptors: copied whole into the dynamic LDS at prog_lds (>= 0)
+  // once, so an op starts on LDS reads, with no global round trip on the
+  // way from one op to the next; else read from global memory per op
   constexpr int TW = (int)(sizeof(TOp) / 8);
-  __shared__ uint64_t pbuf[3][TW];
   const uint64_t* gw = reinterpret_cast<const uint64_t*>(gprog);
-  if (t < TW) {
-    pbuf[0][t] = gw[t];
-    if (nops > 1) pbuf[1][t] = gw[TW + t];
+  const AS3 uint64_t* lw = (const AS3 uint64_t*)(lds + (prog_lds > 0 ? prog_lds : 0));
+  if (prog_lds >= 0) {
+    AS3 uint64_t* dst = (AS3 uint64_t*)(lds + prog_lds);
+    const int nw = nops * TW;
+    for (int i0 = t; i0 < nw; i0 += 8 * TAIL_THREADS) {   // 8 loads in flight per lane
+      uint64_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = i0 + q * TAIL_THREADS < nw ? gload(gw + i0 + q * TAIL_THREADS) : 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (i0 + q * TAIL_THREADS < nw) dst[i0 + q * TAIL_THREADS] = v[q];
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  int s0i = 0, s1i = 1, s2i = 2;   // slots of ops k, k + 1, k + 2
   for (int k = 0; k < nops; ++k) {
     TOp od;
-    __builtin_memcpy(&od, pbuf[s0i], sizeof(TOp));
+    if (prog_lds >= 0) {
+      uint64_t w[TW];
+#pragma unroll
+      for (int q = 0; q < TW; ++q) w[q] = lw[k * TW + q];
+      __builtin_memcpy(&od, w, sizeof(TOp));
+    } else {
+      od = gprog[k];
+    }
     const TOp o = tail_resolve(od, lds);   // uniform
-    if (k + 2 < nops && t < TW) pbuf[s2i][t] = gw[(size_t)(k + 2) * TW + t];
-    if (XL && k + 1 < nops) {
-      const TOp* nx = reinterpret_cast<const TOp*>(pbuf[s1i]);
-      if (nx->stg >= 0) {
-        TOp n;
-        __builtin_memcpy(&n, nx, sizeof(TOp));
-        stage_op(n, lds);
-      }
-    }
-    {
-      const int r = s0i;
-      s0i = s1i;
-      s1i = s2i;
-      s2i = r;
-    }
     switch (o.kind) {
       case T_COPY:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
         break;
-      case T_TOUCH: {
-        const int64_t* tab = reinterpret_cast<const int64_t*>(o.x);
-        double acc = 0.0;
-        for (int j0 = 0; j0 < (int)o.n; j0 += 8) {   // 8 loads in flight per lane (few VGPRs)
-          double v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = 0.0;
-            if (j0 + j < (int)o.n) {
-              const char* base = reinterpret_cast<const char*>(gload(tab + 2 * (j0 + j)));
-              const int64_t valid = gload(tab + 2 * (j0 + j) + 1);
-              for (int64_t i = t; 16 * i + 16 <= valid; i += TAIL_THREADS)
-                v[j] += gload(reinterpret_cast<const dv2*>(base) + i).x;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc += v[j];
-        }
-        if (acc == 1.0e308) red[0][0] = acc;   // keeps the loads; red is scratch between ops
-        break;
-      }
-      case T_BSR:
-      case T_GS:
-        if constexpr (XL) {
-          if (o.stg >= 0) tail_bsr<true, true>(o, o.kind == T_GS, lds);
-          else tail_bsr<true, false>(o, o.kind == T_GS, lds);
-        } else {
-          tail_bsr<false, false>(o, o.kind == T_GS, lds);
-        }
-        break;
+      case T_BSR: tail_bsr<XL>(o, false); break;
+      case T_GS: tail_bsr<XL>(o, true); break;
       case T_BD:
         for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
           const double b0 = o.b[2 * I], b1 = o.b[2 * I + 1];
@@ -2126,6 +1986,7 @@ struct Op {
   double* part = nullptr;           // DOT2 / CSCALE partial sums
   const struct DLevel* lev = nullptr;   // PATCH: the level's patch data
   const TOp* prog = nullptr;        // TAIL: the device op list (n ops)
+  int tail_pl = -1;                 // TAIL: the program's LDS byte offset (-1: read from global memory)
   double bytes = 0.0;
 };
 
@@ -2176,7 +2037,7 @@ struct DeviceHandle {
   int tail_level = 0;
   std::vector<double> kregion_ms;  // select_k_region: K ms per candidate region, the one kept
   int kregion_best = -1;
-  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; bool xl; };
+  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; bool xl; int prog_lds; };
   mutable std::vector<TailProg> tails;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
@@ -3890,44 +3751,6 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   return off;
 }
 
-// LDS staging plan of a tail program (TOp::stg; needs the LDS-resident
-// vectors of tail_lds_plan, whose `lds` bytes come first): two staging
-// buffers of up to 32 KB after them; the SpMV / GS ops whose slice (rows,
-// their blocks) fits a buffer are staged, alternately into the two, so the
-// copy for op i (issued while op i - 1 runs) never lands in the buffer op
-// i - 1 reads.  Returns the program's dynamic LDS bytes.
-int64_t tail_stage_plan(std::vector<TOp>* prog, int64_t lds) {
-  if (lds <= 0 || std::getenv("MAMG_TAIL_NOSTAGE")) return lds;
-  const int64_t base = (lds + 255) / 256 * 256;
-  const int64_t SB = std::min<int64_t>(32768, (TAIL_LDS_MAX - base) / 2) / 256 * 256;
-  if (SB < 4096) return lds;
-  std::map<const int64_t*, std::vector<int64_t>> ptrs;   // row pointers, downloaded once per matrix
-  int cnt = 0;
-  for (size_t i = 1; i < prog->size(); ++i) {
-    TOp& o = (*prog)[i];
-    if (o.kind != T_GS && o.kind != T_BSR) continue;
-    const bool gs = o.kind == T_GS;
-    auto it = ptrs.find(o.ptr);
-    if (it == ptrs.end()) {
-      std::vector<int64_t> hp(o.n + 1);
-      if (hipMemcpy(hp.data(), o.ptr, (o.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess) {
-        (void)hipGetLastError();
-        return lds;
-      }
-      it = ptrs.emplace(o.ptr, std::move(hp)).first;
-    }
-    const int64_t r0 = gs ? o.r0 : 0, r1 = gs ? o.r1 : o.n;
-    const int64_t k0 = it->second[r0], k1 = it->second[r1];
-    const StageLayout L = stage_layout(gs, r1 - r0, k1 - k0, o.W != nullptr, o.sym != 0);
-    if (L.total > SB) continue;
-    o.stg = (int)(base + (cnt & 1) * SB);
-    o.k0 = k0;
-    o.k1 = k1;
-    ++cnt;
-  }
-  return cnt ? base + 2 * SB : lds;
-}
-
 // the cycle of level l and everything below as one tail_kernel launch; the
 // device op list is built once per (b, x) and kept on the handle
 bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
@@ -3947,67 +3770,32 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
       if ((t.kind == T_BSR || t.kind == T_GS) && !((uintptr_t)t.x & 1)) xl = false;
-    if (xl) lds = tail_stage_plan(&prog, lds);
-    // L2 warm-up table (T_TOUCH): the distinct matrix arrays the ops read,
-    // deepest levels first (visited most), cut into 16 KB chunks
-    std::vector<std::pair<const void*, int64_t>> arrs;
-    auto arr = [&](const void* p, int64_t bytes) {
-      if (!p || bytes < 16) return;
-      for (const auto& a : arrs)
-        if (a.first == p) return;
-      arrs.push_back({p, bytes});
-    };
-    for (auto it = sub.rbegin(); it != sub.rend(); ++it) {
-      const Op& o = *it;
-      if ((o.kind == OP_BSR || o.kind == OP_GS) && o.Mb) {
-        const DBsr& M = *o.Mb;
-        arr(M.ptr, 8 * (M.nr + 1));
-        arr(M.col, 4 * M.nb);
-        arr(M.val, (M.sym ? 24 : 32) * M.nb);
-        if (o.W) arr(o.W, 32 * M.nr);
-        if (o.perm) arr(o.perm, 4 * M.nr);
-      } else if (o.kind == OP_BD) {
-        arr(o.W, 32 * o.n);
-      } else if (o.kind == OP_GEMV) {
-        arr(o.w, 8 * o.n * o.n);
+    // the program itself into the LDS after the vectors when it fits
+    // (TAIL_LDS_MAX); the dynamic LDS then covers both
+    int prog_lds = -1;
+    const int64_t pbytes = (int64_t)(prog.size() * sizeof(TOp));
+    if (lds > 0) {
+      const int64_t off = (lds + 15) / 16 * 16;
+      if (off + pbytes <= TAIL_LDS_MAX) {
+        prog_lds = (int)off;
+        lds = off + pbytes;
       }
     }
-    std::vector<int64_t> tab;
-    for (const auto& a : arrs)
-      for (int64_t off = 0; off + 16 <= a.second && (int64_t)tab.size() < 2 * TOUCH_MAX; off += 16384) {
-        tab.push_back((int64_t)((const char*)a.first + off));
-        tab.push_back(std::min<int64_t>(16384, a.second - off));
-      }
-    if (!tab.empty() && !std::getenv("MAMG_TAIL_NOTOUCH")) {
-      TOp t;
-      t.kind = T_TOUCH;
-      t.n = (int64_t)tab.size() / 2;
-      prog.insert(prog.begin(), t);
-    } else {
-      tab.clear();
-    }
-    const size_t pbytes = prog.size() * sizeof(TOp);
     void* d = nullptr;
-    if (hipMalloc(&d, pbytes + tab.size() * sizeof(int64_t)) != hipSuccess) { (void)hipGetLastError(); return false; }
-    if (!tab.empty()) prog[0].x = reinterpret_cast<const double*>((char*)d + pbytes);
-    if (!tab.empty() &&
-        hipMemcpy((char*)d + pbytes, tab.data(), tab.size() * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipFree(d);
-      return false;
-    }
+    if (hipMalloc(&d, (size_t)pbytes) != hipSuccess) { (void)hipGetLastError(); return false; }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipGetLastError();
       (void)hipFree(d);
       return false;
     }
-    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl});
+    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl, prog_lds});
     tp = &h->tails.back();
   }
   Op o;
   o.kind = OP_TAIL; o.cls = C_COARSE; o.prog = tp->prog; o.n = tp->n; o.bytes = tp->bytes;
   o.r0 = tp->lds;   // dynamic LDS bytes (0: the program reads global vectors)
   o.r1 = tp->xl ? 1 : 0;
+  o.tail_pl = tp->prog_lds;
   ops->push_back(o);
   return true;
 }
@@ -4444,8 +4232,10 @@ void launch(const Op& o, hipStream_t s) {
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
       break;
     case OP_TAIL:
-      if (o.n && o.r1 == 1) tail_kernel<false, true><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
-      else if (o.n) tail_kernel<false, false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, nullptr);
+      if (o.n && o.r1 == 1)
+        tail_kernel<false, true><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, o.tail_pl, nullptr);
+      else if (o.n)
+        tail_kernel<false, false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, o.tail_pl, nullptr);
       break;
     case OP_CSCALE:
       if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
@@ -5355,8 +5145,8 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
       HIPCHK(hipMalloc(&dst, (tp.n + 1) * sizeof(uint64_t)));
       HIPCHK(hipMemcpy(prog.data(), tp.prog, tp.n * sizeof(TOp), hipMemcpyDeviceToHost));
       for (int rep = 0; rep < 2; ++rep)
-        if (tp.xl) tail_kernel<true, true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
-        else tail_kernel<true, false><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, dst);
+        if (tp.xl) tail_kernel<true, true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
+        else tail_kernel<true, false><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
       HIPCHK(hipStreamSynchronize(s));
       HIPCHK(hipMemcpy(st.data(), dst, (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
       (void)hipFree(dst);
