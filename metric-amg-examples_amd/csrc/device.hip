@@ -4533,7 +4533,7 @@ void apply_k_layout_knob(DeviceHandle* h) {
     if (!D.coarsest) set_k_split(D.KPb, 1);
 }
 
-void debug_sums(DeviceHandle* h, const char* stage);
+void debug_sums(DeviceHandle* h, const char* stage, bool konly);
 
 std::string layout_error(const mamg_params& p) {
   if (patch_schwarz(p))
@@ -4644,7 +4644,9 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   HIPCHK(null_sync());
   const auto t1 = std::chrono::steady_clock::now();
   h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  debug_sums(h.get(), "pre-rehome", true);
   rehome_operators(h.get());
+  debug_sums(h.get(), "post-rehome", true);
   const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
@@ -4652,7 +4654,7 @@ int dev_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, Devi
   // before the handle's first use on any stream (order_begin waits on it)
   if ((rc = order_end(h.get(), nullptr, err))) return rc;
   HIPCHK(hipEventSynchronize(h->last));
-  debug_sums(h.get(), "upload");
+  debug_sums(h.get(), "upload", false);
   h->layout_ms[LT_FINISH] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
   *out = h.release();
@@ -4783,6 +4785,11 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
       const int64_t nvc = D.coarsest ? 0 : G->levels[l + 1].n / 2;
       if ((rc = build_bsr_level(h.get(), l, S, nvc, l == 0 ? p.spmv_lanes : 0, err))) return rc;
     }
+    {
+      char st[32];
+      std::snprintf(st, sizeof st, "built-L%d", l);
+      debug_sums(h.get(), st, true);
+    }
     // the level's GPU-setup buffers are no longer needed (A_l stays for l+1's
     // Galerkin product only, which is done)
     for (void* q : {(void*)g.P.ptr, (void*)g.P.col, (void*)g.P.val, (void*)g.R.ptr, (void*)g.R.col,
@@ -4814,13 +4821,15 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
   HIPCHK(null_sync());
   const auto t1 = std::chrono::steady_clock::now();
   h->layout_ms[LT_BUILD] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  debug_sums(h.get(), "pre-rehome", true);
   rehome_operators(h.get());
+  debug_sums(h.get(), "post-rehome", true);
   const auto t2 = std::chrono::steady_clock::now();
   apply_k_layout_knob(h.get());
   set_tail_level(h.get());
   if ((rc = order_end(h.get(), nullptr, err))) return rc;   // as in dev_upload
   HIPCHK(hipEventSynchronize(h->last));
-  debug_sums(h.get(), "upload");
+  debug_sums(h.get(), "upload", false);
   const auto t3 = std::chrono::steady_clock::now();
   h->layout_ms[LT_FINISH] = std::chrono::duration<double, std::milli>(t3 - t2).count();
   h->setup_ms[GS_LAYOUT] = std::chrono::duration<double, std::milli>(t3 - t0).count();
@@ -4868,13 +4877,14 @@ void dev_kregion(const DeviceHandle* h, std::vector<double>* ms, int* kept) {
 // array of the handle, per level, printed to stderr at the end of the upload
 // and before each apply, so two handles of one problem (which must hold the
 // same bytes wherever they live) name the array that differs
-void debug_sums(DeviceHandle* h, const char* stage) {
+void debug_sums(DeviceHandle* h, const char* stage, bool konly) {
   static const bool on = [] {
     const char* e = std::getenv("MAMG_DEBUG_SUMS");
     return e && std::atoi(e) != 0;
   }();
   if (!on) return;
-  (void)hipDeviceSynchronize();
+  // no device-wide sync: the copies below are ordered on the null stream,
+  // as every layout-builder step is
   auto hash = [](const void* p, size_t b) -> unsigned long long {
     if (!p || !b) return 0ull;
     std::vector<unsigned char> v(b);
@@ -4885,6 +4895,15 @@ void debug_sums(DeviceHandle* h, const char* stage) {
   };
   std::string line;
   char buf[160];
+  if (konly) {   // level 0's K values and where they live (build-time trace)
+    const DBsr& K = h->L[0].KPb;
+    const int64_t slots = (K.sell || K.half) ? K.nbs : K.nb;
+    const int per = (K.sym || K.half) ? 3 : 4;
+    const bool ar = (char*)K.val >= h->arena0 && (char*)K.val < h->arena1;
+    std::fprintf(stderr, "[mamg sums] %s L0.K val %016llx at %p (%s, %lld B)\n", stage,
+                 hash(K.val, (size_t)slots * per * 8), (void*)K.val, ar ? "arena" : "own", (long long)(slots * per * 8));
+    return;
+  }
   for (size_t l = 0; l < h->L.size(); ++l) {
     const DLevel& L = h->L[l];
     const std::pair<const char*, const DBsr*> ms[] = {{"A", &L.Ab}, {"K", &L.KPb}, {"PA", &L.PAb}, {"P", &L.Pb},
@@ -4912,7 +4931,7 @@ void debug_sums(DeviceHandle* h, const char* stage) {
 
 int dev_apply(DeviceHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
   if (d_r == d_z) { *err = "r and z must not alias"; return MAMG_ERR_ARG; }
-  debug_sums(h, "apply");
+  debug_sums(h, "apply", false);
   HIPCHK(hipSetDevice(h->device));
   hipGraphExec_t exec;
   int rc = get_graph(h, d_r, d_z, &exec, err);
