@@ -3324,8 +3324,31 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   return MAMG_OK;   // ring_blocks_dev's buffers: freed by the guard, null-stream ordered
 }
 
+// MAMG_DEBUG_SUMS: hash of a device array (null-stream ordered copy)
+void debug_hash(const char* tag, int l, const void* p, size_t b) {
+  static const bool on = [] {
+    const char* e = std::getenv("MAMG_DEBUG_SUMS");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!on || !p || !b) return;
+  std::vector<unsigned char> v(b);
+  if (hipMemcpy(v.data(), p, b, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return; }
+  unsigned long long x = 1469598103934665603ull;
+  for (unsigned char c : v) x = (x ^ c) * 1099511628211ull;
+  std::fprintf(stderr, "[mamg sums] src L%d.%s %016llx (%zu B)\n", l, tag, x, b);
+}
+
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
   DLevel& D = h->L[l];
+  if (l == 0) {
+    debug_hash("A.val", l, S.A.val, (size_t)S.A.nnz * 8);
+    debug_hash("P.col", l, S.P.col, (size_t)S.P.nnz * 4);
+    debug_hash("P.val", l, S.P.val, (size_t)S.P.nnz * 8);
+    debug_hash("AP.ptr", l, S.AP.ptr, (size_t)(S.AP.n + 1) * 8);
+    debug_hash("AP.col", l, S.AP.col, (size_t)S.AP.nnz * 4);
+    debug_hash("AP.val", l, S.AP.val, (size_t)S.AP.nnz * 8);
+    debug_hash("W", l, S.W, (size_t)(D.n / 2) * 32);
+  }
   const mamg_params& p = h->p;
   const int64_t nv = D.n / 2;
   int rc;
@@ -3369,6 +3392,13 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
                       // W = the first post-smoothing step's smoother
       const double* Wpost = reinterpret_cast<const double*>(step_wd(D, 0, false));
       if ((rc = dev_kmerge(&T, Pb, Qb, Wpost, &M, err))) return rc;
+      if (l == 0) {
+        debug_hash("Pb.val", l, Pb.val, (size_t)Pb.nb * 32);
+        debug_hash("Qb.val", l, Qb.val, (size_t)Qb.nb * 32);
+        debug_hash("Wpost", l, Wpost, (size_t)(D.n / 2) * 32);
+        debug_hash("Kraw.col", l, M.col, (size_t)M.nb * 4);
+        debug_hash("Kraw.val", l, M.val, (size_t)M.nb * 32);
+      }
     } else {          // P and AP blocks side by side in one row window
       if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
     }
