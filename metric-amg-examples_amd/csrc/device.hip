@@ -3325,12 +3325,15 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
 }
 
 // MAMG_DEBUG_SUMS: hash of a device array (null-stream ordered copy)
-void debug_hash(const char* tag, int l, const void* p, size_t b) {
+bool debug_on() {
   static const bool on = [] {
     const char* e = std::getenv("MAMG_DEBUG_SUMS");
     return e && std::atoi(e) != 0;
   }();
-  if (!on || !p || !b) return;
+  return on;
+}
+void debug_hash(const char* tag, int l, const void* p, size_t b) {
+  if (!debug_on() || !p || !b) return;
   std::vector<unsigned char> v(b);
   if (hipMemcpy(v.data(), p, b, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return; }
   unsigned long long x = 1469598103934665603ull;
@@ -3388,6 +3391,20 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
+    if (l == 0 && debug_on()) {   // the same conversion again: is it deterministic?
+      for (int rep = 0; rep < 3; ++rep) {
+        TBsr Q2;
+        if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Q2, err))) return rc;
+        debug_hash("Qb.ptr", l, Qb.ptr, (size_t)(Qb.nr + 1) * 8);
+        debug_hash("Q2.ptr", l, Q2.ptr, (size_t)(Q2.nr + 1) * 8);
+        debug_hash("Qb.col", l, Qb.col, (size_t)Qb.nb * 4);
+        debug_hash("Q2.col", l, Q2.col, (size_t)Q2.nb * 4);
+        debug_hash("Qb.val", l, Qb.val, (size_t)Qb.nb * 32);
+        debug_hash("Q2.val", l, Q2.val, (size_t)Q2.nb * 32);
+        debug_hash("AP.val again", l, S.AP.val, (size_t)S.AP.nnz * 8);
+        T.release(Q2.ptr); T.release(Q2.col); T.release(Q2.val);
+      }
+    }
     if (g_post_k) {   // one operator K = P - W (A P) on AP's pattern,
                       // W = the first post-smoothing step's smoother
       const double* Wpost = reinterpret_cast<const double*>(step_wd(D, 0, false));
