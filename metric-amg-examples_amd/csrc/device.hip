@@ -3402,6 +3402,25 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
         debug_hash("Qb.val", l, Qb.val, (size_t)Qb.nb * 32);
         debug_hash("Q2.val", l, Q2.val, (size_t)Q2.nb * 32);
         debug_hash("AP.val again", l, S.AP.val, (size_t)S.AP.nnz * 8);
+        {   // where the two conversions differ
+          std::vector<dv4> va(Qb.nb), vb(Qb.nb);
+          std::vector<int64_t> pa(Qb.nr + 1);
+          (void)hipMemcpy(va.data(), Qb.val, Qb.nb * sizeof(dv4), hipMemcpyDeviceToHost);
+          (void)hipMemcpy(vb.data(), Q2.val, Qb.nb * sizeof(dv4), hipMemcpyDeviceToHost);
+          (void)hipMemcpy(pa.data(), Qb.ptr, (Qb.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost);
+          int shown = 0;
+          int64_t ndiff = 0;
+          for (int64_t k = 0; k < Qb.nb; ++k) {
+            if (std::memcmp(&va[k], &vb[k], sizeof(dv4)) == 0) continue;
+            ++ndiff;
+            if (shown++ >= 6) continue;
+            const int64_t row = std::upper_bound(pa.begin(), pa.end(), k) - pa.begin() - 1;
+            std::fprintf(stderr, "[mamg sums] diff block %lld row %lld (wg %lld): %.17g %.17g %.17g %.17g vs %.17g %.17g %.17g %.17g\n",
+                         (long long)k, (long long)row, (long long)(row / RS_NODES), va[k].x, va[k].y, va[k].z, va[k].w,
+                         vb[k].x, vb[k].y, vb[k].z, vb[k].w);
+          }
+          if (ndiff) std::fprintf(stderr, "[mamg sums] %lld of %lld blocks differ\n", (long long)ndiff, (long long)Qb.nb);
+        }
         T.release(Q2.ptr); T.release(Q2.col); T.release(Q2.val);
       }
     }
