@@ -26,13 +26,28 @@ struct RowStage {
   double v[2][RS_CAP];
 };
 
-// Row view of one field: entry k of the field's rows is C[k - off], V[k - off]
+// Row view of one field: entry k of the field's rows is LC[k - off],
+// LV[k - off] in the staged LDS copy (lds), else C[k], V[k] in global memory.
+// The two address spaces are explicit: the reads are ds_read / global_load,
+// never FLAT loads (round 4: with one generic pointer for both, the FLAT
+// loads of staged values intermittently returned zeros for a lane's whole
+// row -- csr2bsr_kernel's 2x2 blocks of A P came out zero, and with them
+// the level-0 K = P - W A P)
+#define RS_AS1 __attribute__((address_space(1)))
+#define RS_AS3 __attribute__((address_space(3)))
 struct RowView {
   const int32_t* C;
   const double* V;
+  const RS_AS3 int32_t* LC;
+  const RS_AS3 double* LV;
   int64_t off;
-  __device__ __forceinline__ int32_t col(int64_t k) const { return C[k - off]; }
-  __device__ __forceinline__ double val(int64_t k) const { return V[k - off]; }
+  bool lds;
+  __device__ __forceinline__ int32_t col(int64_t k) const {
+    return lds ? LC[k - off] : *(const RS_AS1 int32_t*)(C + k);
+  }
+  __device__ __forceinline__ double val(int64_t k) const {
+    return lds ? LV[k - off] : *(const RS_AS1 double*)(V + k);
+  }
 };
 
 // Stage the rows of nodes [I0, I0 + RS_NODES) (clipped to nr) of both fields;
@@ -60,10 +75,11 @@ __device__ __forceinline__ void stage_rows(RowStage& S, const int64_t* __restric
       }
     __syncthreads();
 #pragma unroll
-    for (int f = 0; f < 2; ++f) view[f] = RowView{S.c[f], S.v[f], b[f]};
+    for (int f = 0; f < 2; ++f)
+      view[f] = RowView{col, val, (const RS_AS3 int32_t*)S.c[f], (const RS_AS3 double*)S.v[f], b[f], true};
   } else {
 #pragma unroll
-    for (int f = 0; f < 2; ++f) view[f] = RowView{col, val, 0};
+    for (int f = 0; f < 2; ++f) view[f] = RowView{col, val, nullptr, nullptr, 0, false};
   }
 }
 
