@@ -881,21 +881,6 @@ struct TOp {
 constexpr int TAIL_THREADS = 512;
 
 
-template <class T>
-__device__ __forceinline__ T* tail_res(T* p, char* lds) {
-  const uintptr_t u = (uintptr_t)p;
-  return (u & 1) ? reinterpret_cast<T*>(lds + (u & ~(uintptr_t)1)) : p;
-}
-__device__ __forceinline__ TOp tail_resolve(const TOp& a, char* lds) {
-  TOp o = a;
-  o.x = tail_res(a.x, lds);
-  o.y = tail_res(a.y, lds);
-  o.b = tail_res(a.b, lds);
-  o.out = tail_res(a.out, lds);
-  o.part = tail_res(a.part, lds);
-  return o;
-}
-
 // v + (v of the lane M away) inside groups of 4 lanes, by DPP quad
 // permutations (one VALU op per 32-bit half) instead of an LDS-routed
 // ds_bpermute; the same value and sum as __shfl_xor(v, M, 4)
@@ -925,18 +910,46 @@ __device__ __forceinline__ dv4 tail_blk(const double* v, const double* off, int 
   return gload(reinterpret_cast<const dv4*>(v) + k);
 }
 
-// x(c) as a pair; XL: x is in the workgroup's LDS (ds_read, not a flat load)
-template <bool XL>
-__device__ __forceinline__ double2 tail_x(const double2* x2, int c) {
-  if (XL) {
-    const dv2 v = *((const __attribute__((address_space(3))) dv2*)x2 + c);
-    return double2{v.x, v.y};
-  }
-  return x2[c];
-}
-
 #define AS1 __attribute__((address_space(1)))
 #define AS3 __attribute__((address_space(3)))
+
+// A vector operand of a tail op: in the workgroup's LDS (a tagged offset,
+// tail_lds_plan) or in global memory, known per op (uniform).  Every access
+// is a typed ds_ / global_ instruction, never a FLAT access through a generic
+// pointer (FLAT loads of LDS data returned zeros intermittently in the row
+// merges; rowstage.h).
+struct TVec {
+  double* g = nullptr;
+  AS3 double* l = nullptr;
+  bool lds = false;
+  __device__ __forceinline__ double ld(int64_t i) const { return lds ? l[i] : *(const AS1 double*)(g + i); }
+  __device__ __forceinline__ void st(int64_t i, double v) const {
+    if (lds) l[i] = v;
+    else *(AS1 double*)(g + i) = v;
+  }
+};
+__device__ __forceinline__ TVec tvec(const double* p, char* lds) {
+  const uintptr_t u = (uintptr_t)p;
+  TVec v;
+  v.lds = (u & 1) != 0;
+  if (v.lds) v.l = (AS3 double*)(lds + (u & ~(uintptr_t)1));
+  else v.g = const_cast<double*>(p);
+  return v;
+}
+struct TOpnd {   // the vector operands of one op
+  TVec x, y, b, out, part;
+};
+
+// x(c) as a pair; XL: x is in LDS for every op of the program (no branch)
+template <bool XL>
+__device__ __forceinline__ double2 tail_x(const TVec& x, int c) {
+  if (XL || x.lds) {
+    const dv2 v = ((const AS3 dv2*)x.l)[c];
+    return double2{v.x, v.y};
+  }
+  const dv2 v = ((const AS1 dv2*)x.g)[c];
+  return double2{v.x, v.y};
+}
 
 // the matrix side of a tail SpMV / GS op (global arrays, typed loads)
 struct TailMat {
@@ -953,7 +966,7 @@ struct TailMat {
 // vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place.
 // XL: the gathered vector x lives in LDS
 template <bool XL>
-__device__ void tail_bsr(const TOp& o, bool gs) {
+__device__ void tail_bsr(const TOp& o, const TOpnd& V, bool gs) {
   const TailMat M(o);
   // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
   // a 64-bit division per row chunk cost more than the chunk's loads
@@ -961,7 +974,7 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
   const int lane = threadIdx.x & (VL - 1);
   const int rows = (int)(gs ? o.r1 - o.r0 : o.n);
   const int row0 = gs ? (int)o.r0 : 0;
-  const double2* x2 = reinterpret_cast<const double2*>(o.x);
+  const TVec& X = V.x;
   for (int base = 0; base < (rows << lvl); base += TAIL_THREADS) {   // uniform trip count
     const int v = base + (int)threadIdx.x;
     const int node = row0 + (v >> lvl);
@@ -984,9 +997,9 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     double gb0 = 0.0, gb1 = 0.0;
     double2 gx = {0.0, 0.0};
     if (gs) {
-      gb0 = o.b[2 * gIc];
-      gb1 = o.b[2 * gIc + 1];
-      gx = tail_x<XL>(x2, gIc);
+      gb0 = V.b.ld(2 * gIc);
+      gb1 = V.b.ld(2 * gIc + 1);
+      gx = tail_x<XL>(X, gIc);
     }
     if (p1 > p0) {
       // the first two chunks: all column and value loads issued before any
@@ -1009,7 +1022,7 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         }
         double2 xa[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xa[q] = tail_x<XL>(x2, cc[q]);
+        for (int q = 0; q < 4; ++q) xa[q] = tail_x<XL>(X, cc[q]);
 #pragma unroll
         for (int q = 0; q < 4; q += 2) {
           s0 += hh[q] ? vv[q].x * xa[q].x + vv[q].y * xa[q].y : 0.0;
@@ -1025,7 +1038,7 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
         const int32_t c0 = M.C(la), c1 = M.C(lb);
         const dv4 v0 = M.V(la);
         const dv4 v1 = M.V(lb);
-        const double2 a = tail_x<XL>(x2, c0), e = tail_x<XL>(x2, c1);
+        const double2 a = tail_x<XL>(X, c0), e = tail_x<XL>(X, c1);
         s0 += ha ? v0.x * a.x + v0.y * a.y : 0.0;
         s1 += ha ? v0.z * a.x + v0.w * a.y : 0.0;
         t0 += hb ? v1.x * e.x + v1.y * e.y : 0.0;
@@ -1053,30 +1066,30 @@ __device__ void tail_bsr(const TOp& o, bool gs) {
     if (gs) {
       if (gI < 0) continue;
       const double r0 = gb0 - s0, r1 = gb1 - s1;
-      o.out[2 * gI] = gx.x + (gd.x * r0 + gd.y * r1);
-      o.out[2 * gI + 1] = gx.y + (gd.z * r0 + gd.w * r1);
+      V.out.st(2 * gI, gx.x + (gd.x * r0 + gd.y * r1));
+      V.out.st(2 * gI + 1, gx.y + (gd.z * r0 + gd.w * r1));
       continue;
     }
     double o0, o1;
     if (o.epi == EPI_Y) {
       o0 = s0; o1 = s1;
     } else if (o.epi == EPI_YADD) {
-      o0 = o.y[2 * node] + s0; o1 = o.y[2 * node + 1] + s1;
+      o0 = V.y.ld(2 * node) + s0; o1 = V.y.ld(2 * node + 1) + s1;
     } else if (o.epi == EPI_RESID) {
-      o0 = o.b[2 * node] - s0; o1 = o.b[2 * node + 1] - s1;
+      o0 = V.b.ld(2 * node) - s0; o1 = V.b.ld(2 * node + 1) - s1;
     } else if (o.epi == EPI_KPOST) {
-      const double r0 = o.b[2 * node], r1 = o.b[2 * node + 1];
+      const double r0 = V.b.ld(2 * node), r1 = V.b.ld(2 * node + 1);
       const dv4 w = M.W(node);
-      o0 = o.y[2 * node] + (w.x * r0 + w.y * r1) + s0;
-      o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1) + s1;
+      o0 = V.y.ld(2 * node) + (w.x * r0 + w.y * r1) + s0;
+      o1 = V.y.ld(2 * node + 1) + (w.z * r0 + w.w * r1) + s1;
     } else {  // EPI_BJAC
-      const double r0 = o.b[2 * node] - s0, r1 = o.b[2 * node + 1] - s1;
+      const double r0 = V.b.ld(2 * node) - s0, r1 = V.b.ld(2 * node + 1) - s1;
       const dv4 w = M.W(node);
-      o0 = o.y[2 * node] + (w.x * r0 + w.y * r1);
-      o1 = o.y[2 * node + 1] + (w.z * r0 + w.w * r1);
+      o0 = V.y.ld(2 * node) + (w.x * r0 + w.y * r1);
+      o1 = V.y.ld(2 * node + 1) + (w.z * r0 + w.w * r1);
     }
-    o.out[2 * node] = o0;
-    o.out[2 * node + 1] = o1;
+    V.out.st(2 * node, o0);
+    V.out.st(2 * node + 1, o1);
   }
 }
 
@@ -1123,26 +1136,32 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
     } else {
       od = gprog[k];
     }
-    const TOp o = tail_resolve(od, lds);   // uniform
+    const TOp& o = od;   // uniform; matrices global, vectors through V
+    TOpnd V;
+    V.x = tvec(od.x, lds);
+    V.y = tvec(od.y, lds);
+    V.b = tvec(od.b, lds);
+    V.out = tvec(od.out, lds);
+    V.part = tvec(od.part, lds);
     switch (o.kind) {
       case T_COPY:
-        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.x[i];
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) V.out.st(i, V.x.ld(i));
         break;
-      case T_BSR: tail_bsr<XL>(o, false); break;
-      case T_GS: tail_bsr<XL>(o, true); break;
+      case T_BSR: tail_bsr<XL>(o, V, false); break;
+      case T_GS: tail_bsr<XL>(o, V, true); break;
       case T_BD:
         for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
-          const double b0 = o.b[2 * I], b1 = o.b[2 * I + 1];
+          const double b0 = V.b.ld(2 * I), b1 = V.b.ld(2 * I + 1);
           const dv4 w = gload(o.W + I);
-          o.out[2 * I] = w.x * b0 + w.y * b1;
-          o.out[2 * I + 1] = w.z * b0 + w.w * b1;
+          V.out.st(2 * I, w.x * b0 + w.y * b1);
+          V.out.st(2 * I + 1, w.z * b0 + w.w * b1);
         }
         break;
       case T_AXPY:
-        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = o.out[i] + o.x[i];
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) V.out.st(i, V.out.ld(i) + V.x.ld(i));
         break;
       case T_ZERO:
-        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = 0.0;
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) V.out.st(i, 0.0);
         break;
       case T_GEMV:   // gemv_kernel: one wave per row; small: one thread per row
         if (o.n <= TAIL_THREADS) {   // no shuffle tree on the dependent chain
@@ -1150,9 +1169,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
             const double* a = o.w + (int64_t)t * o.n;
             double s0 = 0.0, s1 = 0.0;
             int j = 0;
-            for (; j + 1 < (int)o.n; j += 2) { s0 += gload(a + j) * o.x[j]; s1 += gload(a + j + 1) * o.x[j + 1]; }
-            if (j < (int)o.n) s0 += gload(a + j) * o.x[j];
-            o.out[t] = s0 + s1;
+            for (; j + 1 < (int)o.n; j += 2) { s0 += gload(a + j) * V.x.ld(j); s1 += gload(a + j + 1) * V.x.ld(j + 1); }
+            if (j < (int)o.n) s0 += gload(a + j) * V.x.ld(j);
+            V.out.st(t, s0 + s1);
           }
           break;
         }
@@ -1161,11 +1180,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           double sum = 0.0;
           if (row < o.n) {
             const double* a = o.w + row * o.n;
-            for (int64_t j = lane; j < o.n; j += 64) sum += gload(a + j) * o.x[j];
+            for (int64_t j = lane; j < o.n; j += 64) sum += gload(a + j) * V.x.ld(j);
           }
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-          if (row < o.n && lane == 0) o.out[row] = sum;
+          if (row < o.n && lane == 0) V.out.st(row, sum);
         }
         break;
       case T_DOT2: {   // dot2_partial_kernel's SCALE_BLOCKS blocks, four at a time
@@ -1173,15 +1192,15 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
         // path: written directly, so only the blocks with rows loop and sync
         const int nbl = (int)std::min<int64_t>(SCALE_BLOCKS, (o.n + 255) / 256);
         for (int i = nbl + t; i < SCALE_BLOCKS; i += TAIL_THREADS) {
-          o.part[2 * i] = 0.0;
-          o.part[2 * i + 1] = 0.0;
+          V.part.st(2 * i, 0.0);
+          V.part.st(2 * i + 1, 0.0);
         }
         for (int vb0 = 0; vb0 < nbl; vb0 += TAIL_THREADS / 256) {
           const int vb = vb0 + (t >> 8), tt = t & 255;
           double a = 0.0, c = 0.0;
           for (int64_t i = (int64_t)vb * 256 + tt; i < o.n; i += (int64_t)SCALE_BLOCKS * 256) {
-            a += o.b[i] * o.x[i];
-            c += o.y[i] * o.x[i];
+            a += V.b.ld(i) * V.x.ld(i);
+            c += V.y.ld(i) * V.x.ld(i);
           }
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) {
@@ -1192,8 +1211,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
           __syncthreads();
           if (tt == 0 && vb < nbl) {
             const int w0 = (t >> 8) * 4;
-            o.part[2 * vb] = (red[w0][0] + red[w0 + 1][0]) + (red[w0 + 2][0] + red[w0 + 3][0]);
-            o.part[2 * vb + 1] = (red[w0][1] + red[w0 + 1][1]) + (red[w0 + 2][1] + red[w0 + 3][1]);
+            V.part.st(2 * vb, (red[w0][0] + red[w0 + 1][0]) + (red[w0 + 2][0] + red[w0 + 3][0]));
+            V.part.st(2 * vb + 1, (red[w0][1] + red[w0 + 1][1]) + (red[w0 + 2][1] + red[w0 + 3][1]));
           }
           __syncthreads();
         }
@@ -1203,7 +1222,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
         __shared__ double alpha;
         if (t < 256) {
           double a = 0.0, c = 0.0;
-          for (int i = t; i < SCALE_BLOCKS; i += 256) { a += o.part[2 * i]; c += o.part[2 * i + 1]; }
+          for (int i = t; i < SCALE_BLOCKS; i += 256) { a += V.part.ld(2 * i); c += V.part.ld(2 * i + 1); }
 #pragma unroll
           for (int off = 32; off > 0; off >>= 1) {
             a += __shfl_xor(a, off, 64);
@@ -1219,7 +1238,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
         }
         __syncthreads();
         const double al = alpha;
-        for (int64_t i = t; i < o.n; i += TAIL_THREADS) o.out[i] = al * o.out[i];
+        for (int64_t i = t; i < o.n; i += TAIL_THREADS) V.out.st(i, al * V.out.ld(i));
         break;
       }
       default: break;
