@@ -2267,21 +2267,20 @@ __global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, con
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nr, I0, vw);
   if (I >= nr) return;
-  int64_t k[4], e[4];
-  stage_segs(ptr, vw, nr, nc, I, k, e);
+  Seg4 g;
+  stage_segs(ptr, vw, nr, nc, I, g.k, g.e);
+  g.init(vw, nc);
   int64_t o = FILL ? bptr[I] : 0;
   for (;;) {
-    int64_t J = INT64_MAX;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q]) J = min(J, (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nc);
+    const int64_t J = g.next();
     if (J == INT64_MAX) break;
     dv4 v = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q] && (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nc == J) {
-        if (FILL) v[q] = vw[q >> 1].val(k[q]);
-        ++k[q];
+      if (g.c[q] == J) {
+        if (FILL) v[q] = vw[q >> 1].val(g.k[q]);
+        ++g.k[q];
+        g.head(vw, nc, q);
       }
     if (FILL) { bcol[o] = (int32_t)J; bval[o] = v; }
     ++o;

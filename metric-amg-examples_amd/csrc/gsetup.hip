@@ -159,24 +159,23 @@ __global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nv, I0, vw);
   if (I >= nv) return;
-  int64_t k[4], e[4];
-  stage_segs(ptr, vw, nv, nv, I, k, e);
+  Seg4 g;
+  stage_segs(ptr, vw, nv, nv, I, g.k, g.e);
+  g.init(vw, nv);
   int64_t o = FILL ? gptr[I] : 0;
   for (;;) {
-    int64_t J = INT64_MAX;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (k[q] < e[q]) J = min(J, (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nv);
+    const int64_t J = g.next();
     if (J == INT64_MAX) break;
     double acc = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)          // order (f0,g0) (f0,g1) (f1,g0) (f1,g1)
-      if (k[q] < e[q] && (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nv == J) {
+      if (g.c[q] == J) {
         if (FILL) {
-          const double a = vw[q >> 1].val(k[q]);
+          const double a = vw[q >> 1].val(g.k[q]);
           acc += a * a;
         }
-        ++k[q];
+        ++g.k[q];
+        g.head(vw, nv, q);
       }
     if (FILL) { gcol[o] = (int32_t)J; gval[o] = sqrt(acc); }
     ++o;

@@ -99,4 +99,23 @@ __device__ __forceinline__ void stage_segs(const int64_t* __restrict__ ptr, cons
   }
 }
 
+// Merge cursor over node I's four sorted segments (stage_segs): c[q] is the
+// node column at segment q's head (INT64_MAX when exhausted).  Each column
+// is read once, when its segment advances: the next node column is
+// min(c), and the segments holding it are those with c[q] == J.
+struct Seg4 {
+  int64_t k[4], e[4], c[4];
+  __device__ __forceinline__ void head(const RowView* vw, int64_t nc, int q) {
+    c[q] = k[q] < e[q] ? (int64_t)vw[q >> 1].col(k[q]) - (q & 1) * nc : INT64_MAX;
+  }
+  __device__ __forceinline__ void init(const RowView* vw, int64_t nc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) head(vw, nc, q);
+  }
+  __device__ __forceinline__ int64_t next() const {
+    const int64_t a = c[0] < c[1] ? c[0] : c[1], b = c[2] < c[3] ? c[2] : c[3];
+    return a < b ? a : b;
+  }
+};
+
 }  // namespace mamg
