@@ -4,6 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 #include "gsetup.h"
 
 namespace mamg {
@@ -12,6 +16,45 @@ namespace {
 int hip_fail(hipError_t e, const char* what, std::string* err) {
   *err = std::string(what) + ": " + hipGetErrorString(e);
   return MAMG_ERR_HIP;
+}
+
+// Temporary storage of the scans and sorts: hipMalloc'd blocks kept for
+// these primitives only, per device, never returned to the allocator that
+// serves the setup's data arrays.  A block is reused
+// in null-stream order: every user issues on the null stream and returns
+// the block behind its last kernel.
+struct ScratchBlock {
+  int dev;
+  void* p;
+  size_t bytes;
+  bool busy;
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchBlock> g_scratch;
+
+void* scratch_get(size_t bytes, hipError_t* e) {
+  int dev = 0;
+  if ((*e = hipGetDevice(&dev)) != hipSuccess) return nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    for (auto& b : g_scratch)
+      if (!b.busy && b.dev == dev && b.bytes >= bytes) {
+        b.busy = true;
+        return b.p;
+      }
+  }
+  const size_t n = std::max<size_t>(bytes, (size_t)1 << 20);
+  void* p = nullptr;
+  if ((*e = hipMalloc(&p, n)) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(g_scratch_mu);
+  g_scratch.push_back({dev, p, n, true});
+  return p;
+}
+
+void scratch_put(void* p) {
+  std::lock_guard<std::mutex> g(g_scratch_mu);
+  for (auto& b : g_scratch)
+    if (b.p == p) b.busy = false;
 }
 }  // namespace
 
@@ -22,12 +65,11 @@ int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std
   size_t bytes = 0;
   hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out, (size_t)n, s);
   if (e != hipSuccess) return hip_fail(e, "DeviceScan::InclusiveSum(size)", err);
-  void* tmp = nullptr;
-  if ((e = hipMallocAsync(&tmp, bytes + 16, s)) != hipSuccess) return hip_fail(e, "hipMallocAsync(scan)", err);
+  void* tmp = scratch_get(bytes + 16, &e);
+  if (!tmp) return hip_fail(e, "hipMalloc(scan scratch)", err);
   e = hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out, (size_t)n, s);
-  hipError_t e2 = hipFreeAsync(tmp, s);
+  scratch_put(tmp);
   if (e != hipSuccess) return hip_fail(e, "DeviceScan::InclusiveSum", err);
-  if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync(scan)", err);
   return MAMG_OK;
 }
 
@@ -41,12 +83,11 @@ int sort_pairs(const K* kin, K* kout, const int64_t* vin, int64_t* vout, int64_t
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0,
                                                     key_bits, s);
   if (e != hipSuccess) return hip_fail(e, "DeviceRadixSort::SortPairs(size)", err);
-  void* tmp = nullptr;
-  if ((e = hipMallocAsync(&tmp, bytes + 16, s)) != hipSuccess) return hip_fail(e, "hipMallocAsync(sort)", err);
+  void* tmp = scratch_get(bytes + 16, &e);
+  if (!tmp) return hip_fail(e, "hipMalloc(sort scratch)", err);
   e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, key_bits, s);
-  hipError_t e2 = hipFreeAsync(tmp, s);
+  scratch_put(tmp);
   if (e != hipSuccess) return hip_fail(e, "DeviceRadixSort::SortPairs", err);
-  if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync(sort)", err);
   return MAMG_OK;
 }
 }  // namespace
