@@ -2547,6 +2547,15 @@ struct TmpPool {
   }
 };
 
+// MAMG_DEBUG_SUMS=1: the layout builder's diagnosis traces (see debug_sums)
+bool debug_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MAMG_DEBUG_SUMS");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B, std::string* err) {
   int rc;
   B->nr = nr; B->nc = nc; B->merged = false;
@@ -2558,6 +2567,7 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
+  if (debug_on()) HIPCHK(hipMemset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
   if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
@@ -3343,13 +3353,6 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
 }
 
 // MAMG_DEBUG_SUMS: hash of a device array (null-stream ordered copy)
-bool debug_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("MAMG_DEBUG_SUMS");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
 void debug_hash(const char* tag, int l, const void* p, size_t b) {
   if (!debug_on() || !p || !b) return;
   std::vector<unsigned char> v(b);
