@@ -2568,7 +2568,13 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
   if (debug_on()) HIPCHK(hipMemset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
-  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  // MAMG_C2B_LDS_PAD (diagnosis): extra dynamic LDS per workgroup, which
+  // lowers how many of these 48 KB workgroups share a CU's 160 KB
+  static const size_t pad = [] {
+    const char* e = std::getenv("MAMG_C2B_LDS_PAD");
+    return e ? (size_t)std::atoll(e) : (size_t)0;
+  }();
+  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES, pad>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
 }

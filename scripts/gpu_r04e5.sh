@@ -15,7 +15,7 @@ run() {   # run <name> <timeout> <cmd...>; stop on anything but pass/fail
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP ($rc)"; exit $rc; fi
 }
 PYT="python -u -m pytest -q -s --timeout 200 --timeout-method thread"
-for i in 1 2; do
+for i in 1 2 3; do
   MAMG_DEBUG_SUMS=1 MAMG_FREE_MODE=drain run drain_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
   MAMG_DEBUG_SUMS=1 run default_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
   MAMG_DEBUG_SUMS=1 MAMG_FREE_MODE=plain run plain_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
