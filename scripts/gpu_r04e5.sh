@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-4 GPU call E5: the repeated level-0 AP conversion (MAMG_DEBUG_SUMS)
-# under the three free modes, twice each: which lifetimes give zeros.
+# Round-4 GPU call E5-E9: the repeated level-0 AP conversion (MAMG_DEBUG_SUMS,
+# values NaN-filled before the fill kernel) with three, two or one of the
+# 48 KB csr2bsr workgroups per CU (MAMG_C2B_LDS_PAD).
 #   gpurun --timeout 900 -- bash scripts/gpu_r04e5.sh TAG
 TAG=${1:-r04e5}
 OUT=$(pwd)/gpurun_out/$TAG
@@ -10,14 +11,13 @@ run() {   # run <name> <timeout> <cmd...>; stop on anything but pass/fail
   echo "== $name" | tee -a $OUT/steps.log
   timeout -k 10 "$t" "$@" > "$OUT/$name.txt" 2>&1
   local rc=$?
-  echo "== $name rc=$rc" | tee -a $OUT/steps.log
-  grep -c "blocks differ" "$OUT/$name.txt" | sed 's/^/   conversions differing: /'
+  echo "== $name rc=$rc $(grep -c 'blocks differ' $OUT/$name.txt) differing" | tee -a $OUT/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP ($rc)"; exit $rc; fi
 }
 PYT="python -u -m pytest -q -s --timeout 200 --timeout-method thread"
 for i in 1 2 3; do
-  MAMG_DEBUG_SUMS=1 MAMG_FREE_MODE=drain run drain_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
-  MAMG_DEBUG_SUMS=1 run default_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
-  MAMG_DEBUG_SUMS=1 MAMG_FREE_MODE=plain run plain_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
+  MAMG_DEBUG_SUMS=1 run nopad_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
+  MAMG_DEBUG_SUMS=1 MAMG_C2B_LDS_PAD=34000 run pad1wg_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
+  MAMG_DEBUG_SUMS=1 MAMG_C2B_LDS_PAD=8000 run pad2wg_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
 done
 echo "== done"
