@@ -1,17 +1,18 @@
 #!/bin/bash
 # The GPU recipe: run on an MI355X box from the repo root,
 #   gpurun --timeout 1200 -- bash scripts/gpu_check.sh TAG [STEPS]
-# STEPS (default all): any of smoke tests bench trace pmc, comma-separated.
+# STEPS (default all): any of smoke tests bench trace pmc dist, comma-separated.
 #   smoke  __graft_entry__.smoke()
 #   tests  pytest -m gpu
 #   bench  python bench.py (N = 1 defaults) -> gpurun_out/TAG/bench.json
 #   trace  rocprofv3 --kernel-trace --stats of a bench run -> TAG/trace/*_kernel_stats.csv
 #   pmc    rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE (separate passes) ->
 #          scripts/traffic.py -> profiles/traffic.json (tagged with device.hip's sha256)
+#   dist   bench/dist_rehearsal.py: 8 virtual ranks of nrefs=6, A0 generated in HBM
 # Stops at the first crash / timeout / abort; logs in gpurun_out/TAG/.  Copy
 # the summaries to be kept into profiles/ afterwards.
 TAG=${1:-check}
-STEPS=${2:-smoke,tests,bench,trace,pmc}
+STEPS=${2:-smoke,tests,bench,trace,pmc,dist}
 OUT=$(pwd)/gpurun_out/$TAG
 ROOT=$(pwd)
 mkdir -p $OUT
@@ -47,4 +48,5 @@ if want pmc; then
   BJ=""; [ -s $OUT/bench.json ] && BJ="--bench-json $OUT/bench.json"
   python3 scripts/traffic.py "$F" "$W" --N 33949186 $BJ --out $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic.json
 fi
+want dist && step dist 600 python -u bench/dist_rehearsal.py --nrefs 6 --ranks 8 --source device
 echo "== done"
