@@ -3361,6 +3361,8 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
 // MAMG_DEBUG_SUMS: hash of a device array (null-stream ordered copy)
 void debug_hash(const char* tag, int l, const void* p, size_t b) {
   if (!debug_on() || !p || !b) return;
+  static const bool dsync = std::getenv("MAMG_DEBUG_SYNC") != nullptr;   // drain before reading back
+  if (dsync) (void)hipDeviceSynchronize();
   std::vector<unsigned char> v(b);
   if (hipMemcpy(v.data(), p, b, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return; }
   unsigned long long x = 1469598103934665603ull;
@@ -3430,6 +3432,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
         debug_hash("Q2.val", l, Q2.val, (size_t)Q2.nb * 32);
         debug_hash("AP.val again", l, S.AP.val, (size_t)S.AP.nnz * 8);
         {   // where the two conversions differ
+          if (std::getenv("MAMG_DEBUG_SYNC")) (void)hipDeviceSynchronize();
           std::vector<dv4> va(Qb.nb), vb(Qb.nb);
           std::vector<int64_t> pa(Qb.nr + 1);
           (void)hipMemcpy(va.data(), Qb.val, Qb.nb * sizeof(dv4), hipMemcpyDeviceToHost);
