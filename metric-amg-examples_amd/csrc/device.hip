@@ -2257,8 +2257,13 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
 // node I's four sorted column segments (rowstage.h stage_segs): q = 2 f + g
 // holds the entries of row f nr + I whose column lies in field g (node
 // column = col - g nc)
+#ifdef MAMG_C2B_OPTNONE   // diagnosis build: the row-merge conversion unoptimised
+#define C2B_ATTR __attribute__((optnone))
+#else
+#define C2B_ATTR
+#endif
 template <bool FILL>
-__global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
+__global__ C2B_ATTR __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
                                                      const int32_t* __restrict__ col,
                                                      const double* __restrict__ val, int64_t* bptr,
                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
