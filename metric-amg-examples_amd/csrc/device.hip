@@ -2097,7 +2097,7 @@ template <class T>
 void poison_doubles(T* p, size_t bytes) {
   if constexpr (std::is_same<T, double>::value) {
     const char* e = std::getenv("MAMG_POISON");
-    if (e && std::atoi(e) != 0) (void)hipMemset(p, 0xff, bytes);
+    if (e && std::atoi(e) != 0) (void)dev_memset(p, 0xff, bytes);
   }
 }
 
@@ -2165,10 +2165,10 @@ int adopt_csr(DeviceHandle* h, const DevMat& M, DCsr* D, int lanes, std::string*
   if ((rc = dalloc(h, &D->ptr, M.n + 1, err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nnz, 1), err))) return rc;
   if ((rc = dalloc(h, &D->val, std::max<int64_t>(D->nnz, 1), err))) return rc;
-  HIPCHK(hipMemcpy(D->ptr, M.ptr, (M.n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  HIPCHK(dev_copy(D->ptr, M.ptr, (M.n + 1) * sizeof(int64_t)));
   if (D->nnz) {
-    HIPCHK(hipMemcpy(D->col, M.col, D->nnz * sizeof(int32_t), hipMemcpyDeviceToDevice));
-    HIPCHK(hipMemcpy(D->val, M.val, D->nnz * sizeof(double), hipMemcpyDeviceToDevice));
+    HIPCHK(dev_copy(D->col, M.col, D->nnz * sizeof(int32_t)));
+    HIPCHK(dev_copy(D->val, M.val, D->nnz * sizeof(double)));
   }
   return MAMG_OK;
 }
@@ -2565,14 +2565,14 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   int rc;
   B->nr = nr; B->nc = nc; B->merged = false;
   if ((rc = T->alloc(&B->ptr, nr + 1, err))) return rc;
-  HIPCHK(hipMemset(B->ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(B->ptr, 0, sizeof(int64_t)));
   if (nr) csr2bsr_kernel<false><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(B->ptr, B->ptr, nr + 1, nullptr, err))) return rc;
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
-  if (debug_on()) HIPCHK(hipMemset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
+  if (debug_on()) HIPCHK(dev_memset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
   // MAMG_C2B_LDS_PAD (diagnosis): extra dynamic LDS per workgroup, which
   // lowers how many of these 48 KB workgroups share a CU's 160 KB
   static const size_t pad = [] {
@@ -2605,7 +2605,7 @@ int dev_kmerge(TmpPool* T, const TBsr& P, const TBsr& Q, const double* W, TBsr* 
   const int64_t nr = P.nr;
   K->nr = nr; K->nc = P.nc; K->merged = false;
   if ((rc = T->alloc(&K->ptr, nr + 1, err))) return rc;
-  HIPCHK(hipMemset(K->ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(K->ptr, 0, sizeof(int64_t)));
   const dv4* Wv = reinterpret_cast<const dv4*>(W);
   if (nr) kmerge_kernel<false><<<nblocks(nr), 256>>>(nr, P.ptr, P.col, P.val, Q.ptr, Q.col, Q.val, Wv, K->ptr,
                                                       nullptr, nullptr);
@@ -2803,8 +2803,8 @@ int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
   if ((rc = T->alloc(&meta, nr, err))) return rc;
   if ((rc = T->alloc(&nlod, 1, err))) return rc;
   if ((rc = T->alloc(&gsoff, ns + 1, err))) return rc;
-  HIPCHK(hipMemset(wm, 0, 4 * sizeof(int)));
-  HIPCHK(hipMemset(nlod, 0, sizeof(unsigned long long)));
+  HIPCHK(dev_memset(wm, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(nlod, 0, sizeof(unsigned long long)));
   half_meta_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, meta, wm, nlod);
   HIPCHK(hipGetLastError());
   int hw[4] = {0, 0, 0, 0};
@@ -2835,14 +2835,14 @@ int try_half(HT* h, TmpPool* T, const TBsr& B, DBsr* D, std::string* err) {
     if ((rc = dalloc(h, &D->gsoff, ns + 1, err))) return rc;
     if ((rc = dalloc(h, &D->gcol, ngs, err))) return rc;
     if ((rc = dalloc(h, &D->gval, 3 * ngs, err))) return rc;
-    HIPCHK(hipMemcpy(D->gsoff, gsoff, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
-    HIPCHK(hipMemset(D->gcol, 0, ngs * sizeof(int32_t)));
-    HIPCHK(hipMemset(D->gval, 0, 3 * ngs * sizeof(double)));
+    HIPCHK(dev_copy(D->gsoff, gsoff, (ns + 1) * sizeof(int64_t)));
+    HIPCHK(dev_memset(D->gcol, 0, ngs * sizeof(int32_t)));
+    HIPCHK(dev_memset(D->gval, 0, 3 * ngs * sizeof(double)));
   }
-  HIPCHK(hipMemcpy(D->meta, meta, nr * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemset(D->col, 0, std::max<int64_t>(su, 1) * sizeof(int32_t)));
-  HIPCHK(hipMemset(D->val, 0, std::max<int64_t>(3 * su, 1) * sizeof(double)));
-  HIPCHK(hipMemset(D->lptr, 0, std::max<int64_t>(sl, 1) * sizeof(int32_t)));
+  HIPCHK(dev_copy(D->meta, meta, nr * sizeof(int32_t)));
+  HIPCHK(dev_memset(D->col, 0, std::max<int64_t>(su, 1) * sizeof(int32_t)));
+  HIPCHK(dev_memset(D->val, 0, std::max<int64_t>(3 * su, 1) * sizeof(double)));
+  HIPCHK(dev_memset(D->lptr, 0, std::max<int64_t>(sl, 1) * sizeof(int32_t)));
   half_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, B.val, meta, hw[0], hw[1], su, D->col, D->val, D->lptr,
                                          D->gsoff, ngs, D->gcol, D->gval, wm + 3, 0);
   HIPCHK(hipGetLastError());
@@ -2901,7 +2901,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   if (sym_ok && !B.merged && B.nb > 0) {
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
-    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    HIPCHK(dev_memset(bad, 0, sizeof(int)));
     sym_check_kernel<<<nblocks(B.nb), 256>>>(B.nb, B.val, bad);
     int hb = 1;
     HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
@@ -2924,7 +2924,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
     const int64_t ns = (nr + SELL_C - 1) / SELL_C;
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
-    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    HIPCHK(dev_memset(bad, 0, sizeof(int)));
     D->sell = true;
     if ((rc = dalloc(h, &D->soff, ns + 1, err))) return rc;
     if ((rc = dalloc(h, &D->meta, std::max<int64_t>(nr, 1), err))) return rc;
@@ -2937,8 +2937,8 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
     HIPCHK(hipMemcpy(&D->nbs, D->soff + ns, sizeof(int64_t), hipMemcpyDeviceToHost));
     if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nbs, 1), err))) return rc;
     if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nbs, 1), err))) return rc;
-    HIPCHK(hipMemset(D->col, 0, std::max<int64_t>(D->nbs, 1) * sizeof(int32_t)));
-    HIPCHK(hipMemset(D->val, 0, std::max<int64_t>(per * D->nbs, 1) * sizeof(double)));
+    HIPCHK(dev_memset(D->col, 0, std::max<int64_t>(D->nbs, 1) * sizeof(int32_t)));
+    HIPCHK(dev_memset(D->val, 0, std::max<int64_t>(per * D->nbs, 1) * sizeof(double)));
     sell_fill_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, 0, B.col, B.val, D->soff, D->nbs, sym ? 1 : 0, D->col, D->val);
     HIPCHK(hipGetLastError());
     return MAMG_OK;
@@ -2946,11 +2946,11 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   if ((rc = dalloc(h, &D->ptr, np, err))) return rc;
   if ((rc = dalloc(h, &D->col, std::max<int64_t>(D->nb, 1), err))) return rc;
   if ((rc = dalloc(h, &D->val, std::max<int64_t>(per * D->nb, 1), err))) return rc;
-  HIPCHK(hipMemcpy(D->ptr, B.ptr, np * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  HIPCHK(dev_copy(D->ptr, B.ptr, np * sizeof(int64_t)));
   if (D->nb) {
-    HIPCHK(hipMemcpy(D->col, B.col, D->nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
+    HIPCHK(dev_copy(D->col, B.col, D->nb * sizeof(int32_t)));
     if (sym) pack_sym_kernel<<<nblocks(D->nb), 256>>>(D->nb, B.val, D->val);
-    else HIPCHK(hipMemcpy(D->val, B.val, D->nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+    else HIPCHK(dev_copy(D->val, B.val, D->nb * sizeof(dv4)));
     HIPCHK(hipGetLastError());
   }
   return MAMG_OK;
@@ -3015,17 +3015,17 @@ int gs_colour(TmpPool* T, const TBsr& B, int level, int8_t** ca_out, int* ncol_o
   if ((rc = T->alloc(&cnt, 64, err))) return rc;
   if ((rc = T->alloc(&ca, nr, err))) return rc;
   if ((rc = T->alloc(&cb, nr, err))) return rc;
-  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
-  HIPCHK(hipMemset(cnt, 0, 64 * sizeof(unsigned long long)));
+  HIPCHK(dev_memset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(cnt, 0, 64 * sizeof(unsigned long long)));
   pattern_sym_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, flags);
   HIPCHK(hipGetLastError());
   int hf[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[0]) { *err = "multicolour GS: node pattern of level " + std::to_string(level) + " not symmetric"; return MAMG_ERR_UNSUPPORTED; }
-  HIPCHK(hipMemset(ca, 0xff, nr));
+  HIPCHK(dev_memset(ca, 0xff, nr));
   for (int round = 0;; ++round) {
     unsigned long long nl = 0;
-    HIPCHK(hipMemset(left, 0, sizeof(unsigned long long)));
+    HIPCHK(dev_memset(left, 0, sizeof(unsigned long long)));
     jp_round_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, level, ca, cb, left, flags + 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&nl, left, sizeof(nl), hipMemcpyDeviceToHost));
@@ -3073,8 +3073,8 @@ int gs_layout(HT* h, TmpPool* T, const TBsr& B, const double* W, const int8_t* c
   if ((rc = T->alloc(&cs, nr, err))) return rc;
   if ((rc = T->alloc(&iota, nr, err))) return rc;
   if ((rc = T->alloc(&sorted, nr, err))) return rc;
-  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
-  HIPCHK(hipMemset(cnt, 0, 64 * sizeof(unsigned long long)));
+  HIPCHK(dev_memset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(cnt, 0, 64 * sizeof(unsigned long long)));
   if (nr) colour_count_kernel<<<nblocks(nr), 256>>>(nr, ca, ci, iota, cnt);
   HIPCHK(hipGetLastError());
   if ((rc = dsort_pairs_i32_i64(ci, cs, iota, sorted, nr, 6, nullptr, err))) return rc;
@@ -3097,10 +3097,10 @@ int gs_layout(HT* h, TmpPool* T, const TBsr& B, const double* W, const int8_t* c
   TBsr G;
   G.nr = nrp; G.nc = B.nc; G.nb = B.nb;
   if ((rc = T->alloc(&G.ptr, nrp + 1, err))) return rc;
-  HIPCHK(hipMemset(G.ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(G.ptr, 0, sizeof(int64_t)));
   if ((rc = dalloc(h, gperm, std::max<int64_t>(nrp, 1), err))) return rc;
   if ((rc = dalloc(h, Gd, std::max<int64_t>(nrp, 1), err))) return rc;
-  HIPCHK(hipMemset(*gperm, 0xff, std::max<int64_t>(nrp, 1) * sizeof(int32_t)));
+  HIPCHK(dev_memset(*gperm, 0xff, std::max<int64_t>(nrp, 1) * sizeof(int32_t)));
   if (nr) perm_place_kernel<<<nblocks(nr), 256>>>(nr, cs, sorted, gcs_d, pcs_d, *gperm);
   HIPCHK(hipGetLastError());
   if (nrp) perm_len_kernel<<<nblocks(nrp), 256>>>(nrp, *gperm, B.ptr, G.ptr);
@@ -3186,8 +3186,8 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   if ((rc = T->alloc(&flags, 4, err))) return rc;
   if ((rc = T->alloc(&left, 1, err))) return rc;
   if ((rc = T->alloc(&cnt, 64 * PATCH_WORDS, err))) return rc;
-  HIPCHK(hipMemset(flags, 0, 4 * sizeof(int)));
-  HIPCHK(hipMemset(cnt, 0, 64 * PATCH_WORDS * sizeof(unsigned long long)));
+  HIPCHK(dev_memset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(cnt, 0, 64 * PATCH_WORDS * sizeof(unsigned long long)));
   pattern_sym_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, flags);
   patch_rowlen_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, flags + 3);
   HIPCHK(hipGetLastError());
@@ -3206,10 +3206,10 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   if ((rc = T->alloc(&k2, nr, err))) return rc;
   if ((rc = T->alloc(&m1, PATCH_WORDS * nr, err))) return rc;
   if ((rc = T->alloc(&m2, PATCH_WORDS * nr, err))) return rc;
-  HIPCHK(hipMemset(c, 0xff, nr * sizeof(int16_t)));
+  HIPCHK(dev_memset(c, 0xff, nr * sizeof(int16_t)));
   for (int round = 0;; ++round) {
     unsigned long long nl = 0;
-    HIPCHK(hipMemset(left, 0, sizeof(unsigned long long)));
+    HIPCHK(dev_memset(left, 0, sizeof(unsigned long long)));
     pkey_init_kernel<<<nblocks(nr), 256>>>(nr, c, k1);
     pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k1, k2);
     pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k2, k1);
@@ -3252,9 +3252,9 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   if ((rc = dalloc(h, &D->Sptr, nr + 1, err))) return rc;
   if ((rc = dalloc(h, &D->Scol, B.nb, err))) return rc;
   if ((rc = dalloc(h, &D->Sval, B.nb, err))) return rc;
-  HIPCHK(hipMemcpy(D->Sptr, B.ptr, (nr + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->Scol, B.col, B.nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->Sval, B.val, B.nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+  HIPCHK(dev_copy(D->Sptr, B.ptr, (nr + 1) * sizeof(int64_t)));
+  HIPCHK(dev_copy(D->Scol, B.col, B.nb * sizeof(int32_t)));
+  HIPCHK(dev_copy(D->Sval, B.val, B.nb * sizeof(dv4)));
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
@@ -3345,9 +3345,9 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   if ((rc = dalloc(h, &D->Sptr, B.nr + 1, err))) return rc;
   if ((rc = dalloc(h, &D->Scol, B.nb, err))) return rc;
   if ((rc = dalloc(h, &D->Sval, B.nb, err))) return rc;
-  HIPCHK(hipMemcpy(D->Sptr, B.ptr, (B.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->Scol, B.col, B.nb * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D->Sval, B.val, B.nb * sizeof(dv4), hipMemcpyDeviceToDevice));
+  HIPCHK(dev_copy(D->Sptr, B.ptr, (B.nr + 1) * sizeof(int64_t)));
+  HIPCHK(dev_copy(D->Scol, B.col, B.nb * sizeof(int32_t)));
+  HIPCHK(dev_copy(D->Sval, B.val, B.nb * sizeof(dv4)));
   // the rest's GS: multicolour node-block GS, covered dofs masked
   uint8_t* dcov = nullptr;
   dv4* Wp = nullptr;
@@ -3414,7 +3414,7 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     T.release(B.ptr); T.release(B.col); T.release(B.val);
   }
   if ((rc = dalloc(h, &D.Wd, nv, err))) return rc;
-  HIPCHK(hipMemcpy(D.Wd, S.W, 4 * nv * sizeof(double), hipMemcpyDeviceToDevice));
+  HIPCHK(dev_copy(D.Wd, S.W, 4 * nv * sizeof(double)));
   if (p.smoother == MAMG_SMOOTHER_POLY) {
     std::vector<double*> wk;
     if ((rc = poly_scaled(h, S.W, 4 * nv, &wk, err))) return rc;
@@ -4327,7 +4327,7 @@ void launch(const Op& o, hipStream_t s) {
                                                           o.lev->Sptr, o.lev->Scol, o.lev->Sval, o.out, o.b, o.bs);
       break;
     case OP_ZERO:
-      if (o.n) (void)hipMemsetAsync(o.out, 0, o.n * sizeof(double), s);
+      if (o.n) (void)dev_memset(o.out, 0, o.n * sizeof(double), s);
       break;
     case OP_DOT2:
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
@@ -4436,7 +4436,7 @@ void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
   if (!*ptr || b == 0) return;
   void* r = placement_alloc(b);
   if (!r) return;
-  if (hipMemcpy(r, *ptr, b, hipMemcpyDeviceToDevice) != hipSuccess) {
+  if (dev_copy(r, *ptr, b) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipFree(r);
     return;
@@ -4510,7 +4510,7 @@ void select_k_region(DeviceHandle* h) {
     void* r = placement_alloc(bytes);
     if (!r) break;
     bufs.push_back(r);
-    (void)hipMemcpy(r, old, bytes, hipMemcpyDeviceToDevice);
+    (void)dev_copy(r, old, bytes);
     K.val = (double*)r;
     launch(op, nullptr);
     (void)hipEventRecord(e0, nullptr);
@@ -4593,12 +4593,12 @@ void set_k_split(DBsr& K, int mode) {
   if (K.split) {   // back to one block per slot first
     if (K.split == 2) unsplit_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, K.val, (dv4*)t);
     else unsplit_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv2*>(K.val), (dv4*)t);
-    (void)hipMemcpy(K.val, t, bytes, hipMemcpyDeviceToDevice);
+    (void)dev_copy(K.val, t, bytes);
     K.split = 0;
   }
   if (mode == 1) split_blocks_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (dv2*)t);
   if (mode == 2) split_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, reinterpret_cast<const dv4*>(K.val), (double*)t);
-  if (mode) (void)hipMemcpy(K.val, t, bytes, hipMemcpyDeviceToDevice);
+  if (mode) (void)dev_copy(K.val, t, bytes);
   drained_free(t);
   K.split = mode;
 }
@@ -4840,7 +4840,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
       if ((rc = adopt_csr(h.get(), l == 0 ? A0 : g.A, &D.A, l == 0 ? p.spmv_lanes : 0, err))) return rc;
       if (D.coarsest) {
         if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
-        HIPCHK(hipMemcpy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double), hipMemcpyDeviceToDevice));
+        HIPCHK(dev_copy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double)));
       } else {
         if ((rc = adopt_csr(h.get(), g.P, &D.P, 0, err))) return rc;
         if ((rc = adopt_csr(h.get(), g.R, &D.R, 0, err))) return rc;
@@ -4848,7 +4848,7 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
           if ((rc = adopt_csr(h.get(), g.WB, &D.WB, 0, err))) return rc;
         } else {
           if ((rc = dalloc(h.get(), &D.winv, D.n, err))) return rc;
-          HIPCHK(hipMemcpy(D.winv, g.winv, D.n * sizeof(double), hipMemcpyDeviceToDevice));
+          HIPCHK(dev_copy(D.winv, g.winv, D.n * sizeof(double)));
         }
         if (p.smoother == MAMG_SMOOTHER_POLY) {   // step smoothers w_k W (values only)
           std::vector<double*> wk;
@@ -4867,16 +4867,16 @@ int dev_from_ghier(GHier* G, const DevMat& A0, const mamg_params& p, DeviceHandl
       }
     } else if (l == 0 && D.coarsest) {          // single-level hierarchy: CSR A0 + dense inverse
       if ((rc = dalloc(h.get(), &D.Ainv, D.n * D.n, err))) return rc;
-      HIPCHK(hipMemcpy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double), hipMemcpyDeviceToDevice));
+      HIPCHK(dev_copy(D.Ainv, g.Ainv, D.n * D.n * sizeof(double)));
       D.A.n = A0.n; D.A.m = A0.m; D.A.nnz = A0.nnz;
       D.A.lanes = p.spmv_lanes > 0 ? p.spmv_lanes : pick_lanes(A0.n, A0.nnz);
       if ((rc = dalloc(h.get(), &D.A.ptr, A0.n + 1, err))) return rc;
       if ((rc = dalloc(h.get(), &D.A.col, std::max<int64_t>(A0.nnz, 1), err))) return rc;
       if ((rc = dalloc(h.get(), &D.A.val, std::max<int64_t>(A0.nnz, 1), err))) return rc;
-      HIPCHK(hipMemcpy(D.A.ptr, A0.ptr, (A0.n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+      HIPCHK(dev_copy(D.A.ptr, A0.ptr, (A0.n + 1) * sizeof(int64_t)));
       if (A0.nnz) {
-        HIPCHK(hipMemcpy(D.A.col, A0.col, A0.nnz * sizeof(int32_t), hipMemcpyDeviceToDevice));
-        HIPCHK(hipMemcpy(D.A.val, A0.val, A0.nnz * sizeof(double), hipMemcpyDeviceToDevice));
+        HIPCHK(dev_copy(D.A.col, A0.col, A0.nnz * sizeof(int32_t)));
+        HIPCHK(dev_copy(D.A.val, A0.val, A0.nnz * sizeof(double)));
       }
     } else {
       LevelSrc S;
@@ -5142,7 +5142,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
   double *dres = pg->hist, *dal = pg->hist + maxiter + 1, *dbe = dal + maxiter;
   launch(a0_op(h, EPI_RESID, d_x, d_b, h->cr), s);                 // r = b - A x
   if ((rc = dev_apply(h, h->cr, h->cz, s, err))) return rc;         // z = B r
-  HIPCHK(hipMemcpyAsync(h->cd, h->cz, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  HIPCHK(dev_copy(h->cd, h->cz, n * sizeof(double), s));
   dot_partial_kernel<<<DOT_BLOCKS, 256, 0, s>>>(n, h->cr, h->cz, h->part);
   pcg_init_kernel<<<1, 256, 0, s>>>(DOT_BLOCKS, h->part, st, tol, relativeconv, maxiter, dres);
   HIPCHK(hipGetLastError());
@@ -5428,7 +5428,7 @@ int ddalloc(DistHandle* h, T** p, int64_t count, std::string* err) {
   if (count <= 0) return MAMG_OK;
   void* q = nullptr;
   HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
-  HIPCHK(hipMemset(q, 0, (size_t)count * sizeof(T)));
+  HIPCHK(dev_memset(q, 0, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
   *p = (T*)q;
   return MAMG_OK;
@@ -5986,7 +5986,7 @@ int dev_rows_to_bsr(TmpPool* T, const DevMat& M, int64_t nvr, int64_t nvc, int64
   S.n = 2 * m;
   S.m = M.m;
   if ((rc = T->alloc(&S.ptr, 2 * m + 1, err))) return rc;
-  HIPCHK(hipMemset(S.ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(S.ptr, 0, sizeof(int64_t)));
   if (m) rowlen_gather_kernel<<<nblocks(2 * m), 256>>>(m, nvr, rows, r0, M.ptr, S.ptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(S.ptr, S.ptr, 2 * m + 1, nullptr, err))) return rc;
@@ -6002,7 +6002,7 @@ int dev_rows_to_bsr(TmpPool* T, const DevMat& M, int64_t nvr, int64_t nvc, int64
 int dev_col_map(TmpPool* T, const DistLevel& L, int32_t** map, std::string* err) {
   int rc;
   if ((rc = T->alloc(map, L.nv, err))) return rc;
-  HIPCHK(hipMemset(*map, 0xff, L.nv * sizeof(int32_t)));
+  HIPCHK(dev_memset(*map, 0xff, L.nv * sizeof(int32_t)));
   if (L.nloc) map_fill_kernel<<<nblocks(L.nloc), 256>>>(L.nloc, L.o0, 0, nullptr, *map);
   const int64_t ng = (int64_t)L.ghosts.size();
   if (ng) {
@@ -6032,7 +6032,7 @@ int dev_window_cols(TmpPool* T, const TBsr& B, int64_t w0, int64_t w1, TBsr* O, 
   int rc;
   O->nr = B.nr; O->nc = w1 - w0; O->merged = false;
   if ((rc = T->alloc(&O->ptr, B.nr + 1, err))) return rc;
-  HIPCHK(hipMemset(O->ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(O->ptr, 0, sizeof(int64_t)));
   if (B.nr) window_len_kernel<<<nblocks(B.nr), 256>>>(B.nr, B.ptr, B.col, w0, w1, O->ptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(O->ptr, O->ptr, B.nr + 1, nullptr, err))) return rc;
@@ -6095,7 +6095,7 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
   // W (node blocks of the owned rows)
   if ((rc = ddalloc(h, &D.W, nloc, err))) return rc;
   if (nloc) {
-    HIPCHK(hipMemcpy(D.W, reinterpret_cast<const dv4*>(g.W) + P.o0, nloc * sizeof(dv4), hipMemcpyDeviceToDevice));
+    HIPCHK(dev_copy(D.W, reinterpret_cast<const dv4*>(g.W) + P.o0, nloc * sizeof(dv4)));
     if (g.joined) unjoin_kernel<<<nblocks(nloc), 256>>>(nloc, g.joined + P.o0, D.W);
     HIPCHK(hipGetLastError());
   }
@@ -6127,7 +6127,7 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
     if (l == 0 && g_half && tA.nr >= g_sell_min_rows && tA.nb > 0) {   // upload_half_or_bsr
       int* bad = nullptr;
       if ((rc = T.alloc(&bad, 1, err))) return rc;
-      HIPCHK(hipMemset(bad, 0, sizeof(int)));
+      HIPCHK(dev_memset(bad, 0, sizeof(int)));
       sym_check_kernel<<<nblocks(tA.nb), 256>>>(tA.nb, tA.val, bad);
       int hb = 1;
       HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
@@ -6560,9 +6560,7 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
           const DDLevel& Q = hs[q]->L[ops[q][k].level];
           const int64_t sc = Q.send_off[p + 1] - Q.send_off[p];
           if (sc != gc) { *err = "halo count mismatch"; return MAMG_ERR_SETUP; }
-          HIPCHK(hipMemcpyAsync(ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]),
-                                Q.sendbuf + 2 * Q.send_off[p], 2 * gc * sizeof(double),
-                                hipMemcpyDeviceToDevice, s));
+          HIPCHK(dev_copy(ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]), Q.sendbuf + 2 * Q.send_off[p], 2 * gc * sizeof(double), s));
         }
       }
     } else if (dk == D_CHALO) {
@@ -6583,8 +6581,7 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
           const int64_t sc = Q.cs_off[b0 + p + 1] - Q.cs_off[b0 + p];
           if (sc != gc) { *err = "colour halo count mismatch"; return MAMG_ERR_SETUP; }
           if (!gc) continue;
-          HIPCHK(hipMemcpyAsync(D.recvbuf + 2 * D.cg_off[b0 + q], Q.sendbuf + 2 * Q.cs_off[b0 + p],
-                                2 * gc * sizeof(double), hipMemcpyDeviceToDevice, s));
+          HIPCHK(dev_copy(D.recvbuf + 2 * D.cg_off[b0 + q], Q.sendbuf + 2 * Q.cs_off[b0 + p], 2 * gc * sizeof(double), s));
         }
       }
       for (int p = 0; p < P; ++p) {
@@ -6604,9 +6601,7 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
           const DDLevel& D = hs[p]->L[ops[p][k].level];
           const int64_t gc = D.ghost_off[q + 1] - D.ghost_off[q];
           if (sc != gc) { *err = "reverse count mismatch"; return MAMG_ERR_SETUP; }
-          HIPCHK(hipMemcpyAsync(Q.recvbuf + 2 * Q.send_off[p],
-                                ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]),
-                                2 * sc * sizeof(double), hipMemcpyDeviceToDevice, s));
+          HIPCHK(dev_copy(Q.recvbuf + 2 * Q.send_off[p], ops[p][k].buf + 2 * (D.nloc + D.ghost_off[q]), 2 * sc * sizeof(double), s));
         }
       }
       for (int q = 0; q < P; ++q) {
@@ -6623,8 +6618,7 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
       for (int p = 1; p < P; ++p)
         vsum_kernel<<<nblocks(n), 256, 0, s>>>(n, ops[p][k].buf, ops[0][k].buf);
       for (int p = 1; p < P; ++p)
-        HIPCHK(hipMemcpyAsync(ops[p][k].buf, ops[0][k].buf, n * sizeof(double),
-                              hipMemcpyDeviceToDevice, s));
+        HIPCHK(dev_copy(ops[p][k].buf, ops[0][k].buf, n * sizeof(double), s));
     }
   }
   HIPCHK(hipGetLastError());

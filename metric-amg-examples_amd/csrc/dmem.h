@@ -21,10 +21,75 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 
 namespace mamg {
+
+// Device fills and device-to-device copies by the library's own kernels
+// instead of hipMemset / hipMemcpy(DeviceToDevice).  Round 4 traced the
+// intermittent wrong operators to whole 128-byte
+// lines of a kernel's output that still held the bytes an earlier runtime
+// fill had left in the same recycled memory (zeros, or the NaN pattern of a
+// diagnosis fill) after the kernel had written them: the runtime's fill /
+// copy kernels' writes surfaced over later data.  Every fill and device
+// copy of the setup, the layout builder and the apply goes through these
+// (same stream semantics: ordered on stream s, asynchronous to the host).
+namespace detail {
+template <class T>
+__global__ __launch_bounds__(256) void fill_words_kernel(T* __restrict__ p, T v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+template <class T>
+__global__ __launch_bounds__(256) void copy_words_kernel(T* __restrict__ d, const T* __restrict__ s, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d[i] = s[i];
+}
+inline unsigned words_grid(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+}
+}  // namespace detail
+
+inline hipError_t dev_memset(void* p, int v, size_t bytes, hipStream_t s = nullptr) {
+  if (!bytes) return hipSuccess;
+  const uint32_t b = (uint8_t)v, w = b * 0x01010101u;
+  const uintptr_t a = (uintptr_t)p;
+  if (a % 16 == 0 && bytes % 16 == 0) {
+    const int64_t n = (int64_t)(bytes / 16);
+    detail::fill_words_kernel<uint4><<<detail::words_grid(n), 256, 0, s>>>((uint4*)p, make_uint4(w, w, w, w), n);
+  } else if (a % 8 == 0 && bytes % 8 == 0) {
+    const int64_t n = (int64_t)(bytes / 8);
+    detail::fill_words_kernel<uint64_t><<<detail::words_grid(n), 256, 0, s>>>((uint64_t*)p,
+                                                                               ((uint64_t)w << 32) | w, n);
+  } else if (a % 4 == 0 && bytes % 4 == 0) {
+    const int64_t n = (int64_t)(bytes / 4);
+    detail::fill_words_kernel<uint32_t><<<detail::words_grid(n), 256, 0, s>>>((uint32_t*)p, w, n);
+  } else {
+    const int64_t n = (int64_t)bytes;
+    detail::fill_words_kernel<uint8_t><<<detail::words_grid(n), 256, 0, s>>>((uint8_t*)p, (uint8_t)b, n);
+  }
+  return hipGetLastError();
+}
+
+inline hipError_t dev_copy(void* d, const void* src, size_t bytes, hipStream_t s = nullptr) {
+  if (!bytes) return hipSuccess;
+  const uintptr_t a = (uintptr_t)d | (uintptr_t)src;
+  if (a % 16 == 0 && bytes % 16 == 0) {
+    const int64_t n = (int64_t)(bytes / 16);
+    detail::copy_words_kernel<uint4><<<detail::words_grid(n), 256, 0, s>>>((uint4*)d, (const uint4*)src, n);
+  } else if (a % 8 == 0 && bytes % 8 == 0) {
+    const int64_t n = (int64_t)(bytes / 8);
+    detail::copy_words_kernel<uint64_t><<<detail::words_grid(n), 256, 0, s>>>((uint64_t*)d, (const uint64_t*)src, n);
+  } else if (a % 4 == 0 && bytes % 4 == 0) {
+    const int64_t n = (int64_t)(bytes / 4);
+    detail::copy_words_kernel<uint32_t><<<detail::words_grid(n), 256, 0, s>>>((uint32_t*)d, (const uint32_t*)src, n);
+  } else {
+    const int64_t n = (int64_t)bytes;
+    detail::copy_words_kernel<uint8_t><<<detail::words_grid(n), 256, 0, s>>>((uint8_t*)d, (const uint8_t*)src, n);
+  }
+  return hipGetLastError();
+}
 
 // 0: stream-ordered (default), 1: drain + hipFree, 2: plain hipFree; read
 // once per process (a block must be freed the way it was allocated)

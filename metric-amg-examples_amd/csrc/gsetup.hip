@@ -1504,11 +1504,11 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
   RCHK(S.alloc(&l1, n, err));
   RCHK(S.alloc(&l2, n, err));
   RCHK(S.alloc(&ctr, 4, err));
-  HIPCHK(hipMemset(ctr, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(ctr, 0, 4 * sizeof(int)));
   C->n = n;
   C->m = ncols;
   RCHK(galloc(G, &C->ptr, n + 1, err));
-  HIPCHK(hipMemset(C->ptr, 0, (n + 1) * sizeof(int64_t)));
+  HIPCHK(dev_memset(C->ptr, 0, (n + 1) * sizeof(int64_t)));
   const unsigned g0 = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 3) / 4), 65536);
   int n1 = 0, n2 = 0;
   for (int pass = 0; pass < 2; ++pass) {
@@ -1577,7 +1577,7 @@ int transpose(GHier* G, const DevMat& P, DevMat* R, std::string* err) {
   RCHK(galloc(G, &R->ptr, P.m + 1, err));
   RCHK(galloc(G, &R->col, nnz, err));
   RCHK(galloc(G, &R->val, nnz, err));
-  HIPCHK(hipMemset(R->ptr, 0, (P.m + 1) * sizeof(int64_t)));
+  HIPCHK(dev_memset(R->ptr, 0, (P.m + 1) * sizeof(int64_t)));
   int64_t *idx = nullptr, *perm = nullptr;
   int32_t *keys = nullptr, *rowof = nullptr;
   RCHK(S.alloc(&idx, nnz, err));
@@ -1601,7 +1601,7 @@ int block_rho(const DevMat& A, int64_t nv, const dv4_t* D, double* rho, std::str
   Scratch S;
   unsigned long long* rb = nullptr;
   RCHK(S.alloc(&rb, 1, err));
-  HIPCHK(hipMemset(rb, 0, sizeof(unsigned long long)));
+  HIPCHK(dev_memset(rb, 0, sizeof(unsigned long long)));
   block_rho_kernel<<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, D, rb);
   HIPCHK(hipGetLastError());
   unsigned long long h = 0;
@@ -1615,7 +1615,7 @@ int node_inverse(const DevMat& A, int64_t nv, const uint8_t* joined, dv4_t* D, c
   Scratch S;
   int* bad = nullptr;
   RCHK(S.alloc(&bad, 1, err));
-  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
   node_inverse_kernel<<<nblk(nv), 256>>>(nv, A.ptr, A.col, A.val, joined, D, bad);
   HIPCHK(hipGetLastError());
   int hb = 0;
@@ -1629,7 +1629,7 @@ int wgraph(const DevMat& M, const uint8_t* flag, int absval, Scratch* S, DevMat*
   const int64_t n = M.n;
   W->n = W->m = n;
   RCHK(S->alloc(&W->ptr, n + 1, err));
-  HIPCHK(hipMemset(W->ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(W->ptr, 0, sizeof(int64_t)));
   wgraph_kernel<false><<<nblk(n), 256>>>(n, M.ptr, M.col, M.val, flag, absval, W->ptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(W->ptr, W->ptr, n + 1, nullptr, err));
@@ -1656,7 +1656,7 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
   {   // active = any strong neighbour
     int64_t* cnt = nullptr;
     RCHK(S.alloc(&cnt, n + 1, err));
-    HIPCHK(hipMemset(cnt, 0, sizeof(int64_t)));
+    HIPCHK(dev_memset(cnt, 0, sizeof(int64_t)));
     wgraph_kernel<false><<<nblk(n), 256>>>(n, Gr.ptr, Gr.col, Gr.val, flag, 2, cnt, nullptr, nullptr);
     nonzero_flag_kernel<<<nblk(n), 256>>>(n, cnt, act);
     HIPCHK(hipGetLastError());
@@ -1674,9 +1674,9 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
     RCHK(S.alloc(&choice, m, err));
     RCHK(S.alloc(&f, m, err));
     RCHK(S.alloc(&a, m, err));
-    HIPCHK(hipMemset(mate, 0xff, m * sizeof(int64_t)));
+    HIPCHK(dev_memset(mate, 0xff, m * sizeof(int64_t)));
     for (int round = 0; round < MAX_ROUNDS; ++round) {
-      HIPCHK(hipMemset(got, 0, sizeof(unsigned long long)));
+      HIPCHK(dev_memset(got, 0, sizeof(unsigned long long)));
       hem_pick_kernel<<<nblk(m), 256>>>(m, W.ptr, W.col, W.val, act, mate, 16 * level + ps, choice);
       hem_mutual_kernel<<<nblk(m), 256>>>(m, choice, mate, got);
       HIPCHK(hipGetLastError());
@@ -1699,7 +1699,7 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
     DevMat T, Tt, WT, C;   // W_next = T^T W T without its diagonal
     T.n = m; T.m = nagg;
     RCHK(S.alloc(&T.ptr, m + 1, err));
-    HIPCHK(hipMemset(T.ptr, 0, sizeof(int64_t)));
+    HIPCHK(dev_memset(T.ptr, 0, sizeof(int64_t)));
     hem_t_kernel<<<nblk(m), 256>>>(m, act, a, T.ptr, nullptr, nullptr, 0);
     RCHK(dscan_incl_i64(T.ptr, T.ptr, m + 1, nullptr, err));
     RCHK(to_host(&T.nnz, T.ptr + m, 1, err));
@@ -1727,8 +1727,8 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
     RCHK(S.alloc(&size, nagg, err));
     RCHK(S.alloc(&agg2, n, err));
     RCHK(S.alloc(&used, nagg, err));
-    HIPCHK(hipMemset(size, 0, std::max<int64_t>(nagg, 1) * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(used, 0, std::max<int64_t>(nagg, 1) * sizeof(int64_t)));
+    HIPCHK(dev_memset(size, 0, std::max<int64_t>(nagg, 1) * sizeof(unsigned long long)));
+    HIPCHK(dev_memset(used, 0, std::max<int64_t>(nagg, 1) * sizeof(int64_t)));
     agg_size_kernel<<<nblk(n), 256>>>(n, agg, size);
     hem_absorb_kernel<<<nblk(n), 256>>>(n, W1.ptr, W1.col, W1.val, agg, size, agg2, used);
     HIPCHK(hipGetLastError());
@@ -1755,7 +1755,7 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   } else {
     Gr.n = Gr.m = nv;
     RCHK(S.alloc(&Gr.ptr, nv + 1, err));
-    HIPCHK(hipMemset(Gr.ptr, 0, sizeof(int64_t)));
+    HIPCHK(dev_memset(Gr.ptr, 0, sizeof(int64_t)));
     node_graph_kernel<false><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
@@ -1771,8 +1771,8 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   RCHK(S.alloc(&flag, Gr.nnz, err));
   RCHK(S.alloc(&nonisol, nv, err));
   RCHK(S.alloc(&ctr, 2, err));
-  HIPCHK(hipMemset(flag, 0, std::max<int64_t>(Gr.nnz, 1)));
-  HIPCHK(hipMemset(ctr, 0, 2 * sizeof(int)));
+  HIPCHK(dev_memset(flag, 0, std::max<int64_t>(Gr.nnz, 1)));
+  HIPCHK(dev_memset(ctr, 0, 2 * sizeof(int)));
   absdiag_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d);
   strength_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, Gr.val, d, theta,
                                      G->params.strength_measure == MAMG_STRENGTH_ROWMAX, flag, ctr);
@@ -1826,7 +1826,7 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   mis_init_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, flag, level, state, low, nonisol);
   for (int rounds = 0;; ++rounds) {
     if (rounds > 10000) { *err = "mis2 did not converge"; return MAMG_ERR_SETUP; }
-    HIPCHK(hipMemset(und, 0, sizeof(unsigned long long)));
+    HIPCHK(dev_memset(und, 0, sizeof(unsigned long long)));
     mis_key_kernel<<<nblk(nv), 256>>>(nv, state, low, key, und);
     HIPCHK(hipGetLastError());
     unsigned long long hu = 0;
@@ -1865,7 +1865,7 @@ int coarsest_inverse(GHier* G, const DevMat& A, double** inv_out, std::string* e
   RCHK(S.alloc(&f, n + 1, err));
   RCHK(S.alloc(&bad, 1, err));
   RCHK(galloc(G, &inv, n * n, err));
-  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
   dense_init_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, M);
   for (int64_t k = 0; k < n; ++k) {
     gj_col_kernel<<<nblk(n), 256>>>(n, k, M, f);
@@ -1913,7 +1913,7 @@ int rho_estimate_dev(const DevMat& A, const PointLevel& P, int iters, Scratch* S
   const unsigned gm = (unsigned)std::min<int64_t>(nblk(n), 1024);
   for (int it = 0; it < iters; ++it) {
     row_spmv_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, P.dinv, v, w);
-    HIPCHK(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned long long), nullptr));
+    HIPCHK(dev_memset(bits, 0, 2 * sizeof(unsigned long long), nullptr));
     maxabs2_kernel<<<gm, 256>>>(n, v, w, bits);
     vnorm_kernel<<<nblk(n), 256>>>(n, w, bits, v);
   }
@@ -1969,9 +1969,9 @@ int seed_blocks_dev(const DevMat& A, const int32_t* idofs, int64_t n_idofs, int 
   RCHK(S->alloc(&skey, n, err));
   RCHK(S->alloc(&bad, 1, err));
   HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(isseed, 0, n));
-  HIPCHK(hipMemset(isowner, 0, n));
-  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  HIPCHK(dev_memset(isseed, 0, n));
+  HIPCHK(dev_memset(isowner, 0, n));
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
   seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
   best_seed_kernel<<<nblk(8 * n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
   best_key_kernel<<<nblk(n), 256>>>(n, best, key, idx);
@@ -1988,7 +1988,7 @@ int seed_blocks_dev(const DevMat& A, const int32_t* idofs, int64_t n_idofs, int 
   RCHK(S->alloc(&B->bid, n, err));
   RCHK(S->alloc(&B->bptr, B->nb + 1, err));
   RCHK(S->alloc(&B->mem, n, err));
-  HIPCHK(hipMemset(B->bptr, 0, (B->nb + 1) * sizeof(int64_t)));
+  HIPCHK(dev_memset(B->bptr, 0, (B->nb + 1) * sizeof(int64_t)));
   bid_kernel<<<nblk(n), 256>>>(n, owner, oscan, B->bid, key, idx, (unsigned long long*)B->bptr);
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(B->bptr, B->bptr, B->nb + 1, nullptr, err));
@@ -2009,8 +2009,8 @@ int seed_align_fast(const DevMat& A, int64_t nv, const int32_t* idofs, int64_t n
   RCHK(S->alloc(&best, n, err));
   RCHK(S->alloc(&bad, 2, err));
   HIPCHK(hipMemcpy(di, idofs, n_idofs * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(isseed, 0, n));
-  HIPCHK(hipMemset(bad, 0, 2 * sizeof(int)));
+  HIPCHK(dev_memset(isseed, 0, n));
+  HIPCHK(dev_memset(bad, 0, 2 * sizeof(int)));
   seed_mark_kernel<<<nblk(n_idofs), 256>>>(n_idofs, di, n, isseed, bad);
   best_seed_kernel<<<nblk(8 * n), 256>>>(n, A.ptr, A.col, A.val, isseed, best);
   seed_align_kernel<<<nblk(nv), 256>>>(nv, isseed, best, mmsize, joined, bad + 1);
@@ -2032,10 +2032,10 @@ int block_inverse_dev(GHier* G, const DevMat& A, const SeedBlocks& B, Scratch* S
   RCHK(S->alloc(&pos, n, err));
   RCHK(S->alloc(&f, nb, err));
   RCHK(S->alloc(&bad, 1, err));
-  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
   D->n = D->m = n;
   RCHK(galloc(G, &D->ptr, n + 1, err));
-  HIPCHK(hipMemset(D->ptr, 0, sizeof(int64_t)));
+  HIPCHK(dev_memset(D->ptr, 0, sizeof(int64_t)));
   member_pos_kernel<<<nblk(n), 256>>>(n, B.mem, B.bid, B.bptr, pos, D->ptr);
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(D->ptr, D->ptr, n + 1, nullptr, err));
@@ -2078,7 +2078,7 @@ int block_rho_dev(const DevMat& D, const DevMat& A, double* rho, std::string* er
   Scratch S;
   unsigned long long* bits = nullptr;
   RCHK(S.alloc(&bits, 1, err));
-  HIPCHK(hipMemset(bits, 0, sizeof(unsigned long long)));
+  HIPCHK(dev_memset(bits, 0, sizeof(unsigned long long)));
   rowabs_max_kernel<<<nblk(C.n), 256>>>(C.n, C.ptr, C.val, bits);
   HIPCHK(hipGetLastError());
   unsigned long long h = 0;
@@ -2121,8 +2121,8 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
   RCHK(S.alloc(&cov, n, err));
   RCHK(S.alloc(&bad, 1, err));
   HIPCHK(hipMemcpy(ds, seeds, ns * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(cov, 0, n));
-  HIPCHK(hipMemset(bad, 0, sizeof(int)));
+  HIPCHK(dev_memset(cov, 0, n));
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
   ring_bfs_kernel<<<(unsigned)ns, 64, 2 * (size_t)mm * sizeof(int32_t)>>>(ns, ds, A.ptr, A.col, maxlvl, mm, blk, blen);
   sq_len_kernel<<<nblk(ns), 256>>>(ns, blen, sq, gj);
   HIPCHK(hipGetLastError());
@@ -2175,7 +2175,7 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
   RCHK(galloc(G, &W->ptr, n + 1, err));
   RCHK(galloc(G, &W->col, nw, err));
   RCHK(galloc(G, &W->val, nw, err));
-  HIPCHK(hipMemset(W->ptr, 0, (n + 1) * sizeof(int64_t)));
+  HIPCHK(dev_memset(W->ptr, 0, (n + 1) * sizeof(int64_t)));
   run_start_kernel<<<nblk(e), 256>>>(e, n, skey, fscan, ustart, W->col, (unsigned long long*)W->ptr);
   HIPCHK(hipGetLastError());
   RCHK(dscan_incl_i64(W->ptr, W->ptr, n + 1, nullptr, err));
@@ -2193,7 +2193,7 @@ int overlap_smoother_dev(GHier* G, const DevMat& A, const int32_t* seeds, int64_
   for (int it = 0; it < std::max(p.rho_iters, 30); ++it) {
     row_spmv_kernel<<<nblk(n), 256>>>(n, A.ptr, A.col, A.val, nullptr, v, t);
     row_spmv_kernel<<<nblk(n), 256>>>(n, W->ptr, W->col, W->val, nullptr, t, w);
-    HIPCHK(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned long long), nullptr));
+    HIPCHK(dev_memset(bits, 0, 2 * sizeof(unsigned long long), nullptr));
     maxabs2_kernel<<<gm, 256>>>(n, v, w, bits);
     vnorm_kernel<<<nblk(n), 256>>>(n, w, bits, v);
   }
@@ -2247,7 +2247,7 @@ int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlv
       (rc = S.alloc(&bad, 1, err)))
     return fail(rc);
   if (hipMemcpy(ds, seeds, ns * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(bad, 0, sizeof(int)) != hipSuccess) {
+      dev_memset(bad, 0, sizeof(int)) != hipSuccess) {
     *err = "seed rings: copy failed";
     return fail(MAMG_ERR_HIP);
   }
@@ -2302,7 +2302,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     Scratch S;
     int* bad = nullptr;
     RCHK(S.alloc(&bad, 1, err));
-    HIPCHK(hipMemset(bad, 0, sizeof(int)));
+    HIPCHK(dev_memset(bad, 0, sizeof(int)));
     validate_kernel<<<nblk(8 * A0.n), 256>>>(A0.n, A0.m, A0.ptr, A0.col, bad);
     HIPCHK(hipGetLastError());
     int hb = 0;
@@ -2378,7 +2378,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       if (nodal && !aligned) {      // general blocks that may still be node-aligned
         int* bad = nullptr;
         RCHK(S.alloc(&bad, 1, err));
-        HIPCHK(hipMemset(bad, 0, sizeof(int)));
+        HIPCHK(dev_memset(bad, 0, sizeof(int)));
         RCHK(galloc(G, &L.joined, nv, err));
         align_kernel<<<nblk(nv), 256>>>(nv, B.bid, B.bptr, L.joined, bad);
         HIPCHK(hipGetLastError());
@@ -2434,7 +2434,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       L.P.n = n;
       L.P.m = 2 * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
-      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      HIPCHK(dev_memset(L.P.ptr, 0, sizeof(int64_t)));
       smooth_p_kernel<false><<<nblk(n), 256>>>(nv, AT.ptr, AT.col, AT.val, Dsa, agg, nagg, w, L.P.ptr,
                                                nullptr, nullptr);
       HIPCHK(hipGetLastError());
@@ -2455,7 +2455,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       L.P.n = n;
       L.P.m = nf * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
-      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      HIPCHK(dev_memset(L.P.ptr, 0, sizeof(int64_t)));
       smooth_pt_kernel<false><<<nblk(n), 256>>>(n, nv, agg, nagg, w, PL.dinv, AT.ptr, AT.col, AT.val, L.P.ptr,
                                                 nullptr, nullptr);
       HIPCHK(hipGetLastError());
@@ -2471,7 +2471,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       L.P.n = n;
       L.P.m = nf * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
-      HIPCHK(hipMemset(L.P.ptr, 0, sizeof(int64_t)));
+      HIPCHK(dev_memset(L.P.ptr, 0, sizeof(int64_t)));
       tent_kernel<<<nblk(n), 256>>>(n, nv, agg, nagg, L.P.ptr, nullptr, nullptr, 0);
       RCHK(dscan_incl_i64(L.P.ptr, L.P.ptr, n + 1, nullptr, err));
       RCHK(to_host(&L.P.nnz, L.P.ptr + n, 1, err));
@@ -2503,7 +2503,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       const int64_t nv = L.n / 2;
       L.WB.n = L.WB.m = L.n;
       RCHK(galloc(G, &L.WB.ptr, L.n + 1, err));
-      HIPCHK(hipMemset(L.WB.ptr, 0, sizeof(int64_t)));
+      HIPCHK(dev_memset(L.WB.ptr, 0, sizeof(int64_t)));
       node_wb_kernel<<<nblk(L.n), 256>>>(nv, (const dv4_t*)L.W, L.joined, L.WB.ptr, nullptr, nullptr, 0);
       HIPCHK(hipGetLastError());
       RCHK(dscan_incl_i64(L.WB.ptr, L.WB.ptr, L.n + 1, nullptr, err));
@@ -2882,7 +2882,7 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
     std::vector<uint8_t> hm;
     for (int l = 0; l < nl; ++l) {
       if (rep[l]) continue;
-      HIPCHK(hipMemset(mark, 0, (size_t)nranks * nv[l]));
+      HIPCHK(dev_memset(mark, 0, (size_t)nranks * nv[l]));
       auto marks = [&](const DevMat& M, int rl) {
         if (M.n == 0) return;
         ghost_mark_kernel<<<nblk(M.n), 256>>>(M.ptr, M.col, M.n, nv[rl], nv[l], drng + (size_t)rl * (nranks + 1),

@@ -18,6 +18,6 @@ PYT="python -u -m pytest -q -s --timeout 200 --timeout-method thread"
 for i in 1 2 3; do
   MAMG_DEBUG_SUMS=1 run nopad_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
   MAMG_DEBUG_SUMS=1 MAMG_DEBUG_SYNC=1 run dsync_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
-  MAMG_DEBUG_SUMS=1 MAMG_LIB=$(pwd)/ab/libmamg_c2b_optnone.so run optnone_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
+  MAMG_DEBUG_SUMS=1 MAMG_POISON=1 run poison_$i 200 $PYT tests/test_gpu.py -k k_kernel_variants
 done
 echo "== done"
