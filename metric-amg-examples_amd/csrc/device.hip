@@ -2573,6 +2573,11 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
   if (debug_on()) HIPCHK(dev_memset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
+  static const int dflush = [] {   // diagnosis: 1 = flush the L2s after the fill, 2 = after the conversion
+    const char* e = std::getenv("MAMG_DEBUG_FLUSH");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (dflush == 1) HIPCHK(l2_flush());
   // MAMG_C2B_LDS_PAD (diagnosis): extra dynamic LDS per workgroup, which
   // lowers how many of these 48 KB workgroups share a CU's 160 KB
   static const size_t pad = [] {
@@ -2581,6 +2586,7 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   }();
   if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES, pad>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
+  if (dflush == 2) HIPCHK(l2_flush());
   return MAMG_OK;
 }
 
