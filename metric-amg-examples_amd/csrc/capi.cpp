@@ -60,6 +60,12 @@ using mamg::set_error;
   GUARD_END
 
 namespace {
+// releases the setup temporaries' cached blocks (dmem.h) when a setup
+// returns, after its own temporaries went back to the cache
+struct TmpTrim {
+  ~TmpTrim() { mamg::dev_tmp_trim(); }
+};
+
 int to_view(const mamg_csr* A, mamg::CsrView* v) {
   if (!A || !A->rowptr || (A->nnz > 0 && (!A->colind || !A->values))) {
     set_error("null CSR pointer");
@@ -328,6 +334,7 @@ namespace {
 int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, int rank, int nranks, const void* comm_id, int64_t rep_nodes,
                     mamg_dhandle** out) {
+  TmpTrim trim;
   int rc;
   const int64_t nnz0 = devA ? devA->nnz : v.nnz();
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
@@ -542,6 +549,7 @@ void mamg_dist_destroy(mamg_dhandle* h) {
 int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
+  TmpTrim trim;
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
   *out = nullptr;
   mamg::CsrView v;
@@ -564,6 +572,7 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
 int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                    const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
+  TmpTrim trim;
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
   *out = nullptr;
   mamg::CsrView v;
@@ -593,6 +602,7 @@ int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
 int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_idofs,
                           const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN
+  TmpTrim trim;
   if (!out || !params || !dA || !dA->rowptr || (dA->nnz > 0 && (!dA->colind || !dA->values))) {
     set_error("null argument");
     return MAMG_ERR_ARG;
@@ -629,6 +639,7 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
 int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                         const mamg_params* params, mamg_hier** out) {
   GUARD_BEGIN
+  TmpTrim trim;
   if (!out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
   *out = nullptr;
   mamg::CsrView v;
@@ -667,6 +678,7 @@ int mamg_layout_timings(const mamg_handle* h, double* ms4) {
 int mamg_upload(const mamg_hier* h, const mamg_csr* A, const mamg_params* params,
                 mamg_handle** out) {
   GUARD_BEGIN
+  TmpTrim trim;
   if (!h || !out || !params) { set_error("null argument"); return MAMG_ERR_ARG; }
   const mamg_params P = mamg::resolve_like(*params, h->H.params);   // as the setup resolved it
   *out = nullptr;

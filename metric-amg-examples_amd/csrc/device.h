@@ -22,6 +22,8 @@ void dev_setup_ms(const DeviceHandle* h, double* ms8);
 // apply-layout phases (ms): build, K value region trials, operator re-homing, finish
 void dev_layout_ms(const DeviceHandle* h, double* ms4);
 void dev_destroy(DeviceHandle* h);
+// release the cached blocks of the setup temporaries (dmem.h tmp_trim_all)
+void dev_tmp_trim();
 int64_t dev_nrows(const DeviceHandle* h);
 int dev_num_levels(const DeviceHandle* h);
 int dev_layout(const DeviceHandle* h);

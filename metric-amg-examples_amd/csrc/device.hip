@@ -2287,7 +2287,10 @@ __global__ C2B_ATTR __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_
         ++g.k[q];
         g.head(vw, nc, q);
       }
-    if (FILL) { bcol[o] = (int32_t)J; bval[o] = v; }
+    if (FILL) {
+      bval[o] = v;
+      bcol[o] = (int32_t)J;
+    }
     ++o;
   }
   if (!FILL) bptr[I + 1] = o;
@@ -2527,8 +2530,8 @@ struct TBsr {
 };
 
 // scoped temporaries of the layout builder, null-stream ordered (dmem.h):
-// the layout kernels that read them are queued on the null stream, and
-// hipFreeAsync there returns a block to the pool only behind them
+// the layout kernels that read them are queued on the null stream, and a
+// block handed out again is used only by work queued behind them
 struct TmpPool {
   std::vector<void*> v;
   ~TmpPool() {
@@ -4428,7 +4431,11 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 bool g_contig_ok = true;
 void* placement_alloc(size_t b) {
   void* r = nullptr;
-  if (g_contig_ok) {
+  static const bool contig_env = [] {   // off by default
+    const char* e = std::getenv("MAMG_CONTIG");
+    return e && std::atoi(e) == 1;
+  }();
+  if (g_contig_ok && contig_env) {
     const auto t0 = std::chrono::steady_clock::now();
     if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
     if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 50.0)
@@ -4950,6 +4957,8 @@ void dev_setup_ms(const DeviceHandle* h, double* ms8) {
 void dev_layout_ms(const DeviceHandle* h, double* ms4) {
   for (int k = 0; k < 4; ++k) ms4[k] = h->layout_ms[k];
 }
+
+void dev_tmp_trim() { tmp_trim_all(); }
 
 void dev_destroy(DeviceHandle* h) {
   if (!h) return;

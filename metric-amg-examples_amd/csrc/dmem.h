@@ -1,17 +1,26 @@
 // dmem.h -- lifetimes of device buffers made during setup (device.hip,
 // gsetup.hip).
 //
-// Every kernel, memset and copy of the GPU setup and of the apply-layout
+// Every kernel, fill and copy of the GPU setup and of the apply-layout
 // builder runs on the null stream, and so do the temporaries' lifetimes:
-//  * temporaries (Scratch, TmpPool, GHier, the seed-ring blocks) come from
-//    hipMallocAsync and go back with hipFreeAsync on the null stream.  The
-//    pool hands a freed block to a later allocation only once the stream has
-//    passed the free, i.e. after every kernel queued before it that reads the
-//    block -- no drain of the device, and no reuse under a running reader;
+//  * temporaries (Scratch, TmpPool, GHier, the seed-ring blocks) come from a
+//    per-device cache of hipMalloc'd blocks (tmp_malloc / tmp_free).  A freed
+//    block goes back to the cache at once and the next tmp_malloc may hand it
+//    out again: its new users are queued on the null stream behind every
+//    kernel that read it before -- no drain of the device and no reuse under
+//    a running reader.  The cache is emptied at the end of every setup
+//    (tmp_trim, after the null stream has drained);
 //  * a long-lived (hipMalloc) array replaced during setup (operator re-homing,
 //    K region candidates) is freed after an event recorded on the null stream
 //    behind its last reader has completed (ordered_free): a wait on that one
 //    stream, not on the device.
+// Round 4 found (bench/contig_alias.hip) that the
+// runtime's stream-ordered pool (hipMallocAsync) hands out blocks that share
+// physical memory with other live blocks of the same pool: a block of a few
+// MiB read back another live block's words.  Rounds 3-4 took the setup's
+// temporaries from that pool; the intermittent wrong operators (whole lines
+// of a conversion's output replaced by other data) were that aliasing.  No
+// buffer of the library comes from hipMallocAsync any more.
 // Round 3 drained the whole device before every hipFree instead (free-after-
 // drain); DESIGN.md section 4.1 records what the round-4 diagnosis
 // (bench/free_race.hip, scripts/gpu_freediag.sh) measured about hipFree.
@@ -23,20 +32,22 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <unordered_map>
 
 namespace mamg {
 
 // Device fills and device-to-device copies by the library's own kernels
-// instead of hipMemset / hipMemcpy(DeviceToDevice).  Round 4 traced the
-// intermittent wrong operators to whole 128-byte
-// lines of a kernel's output that still held the bytes an earlier runtime
-// fill had left in the same recycled memory (zeros, or the NaN pattern of a
-// diagnosis fill) after the kernel had written them: the runtime's fill /
-// copy kernels' writes surfaced over later data.  Every fill and device
-// copy of the setup, the layout builder and the apply goes through these
-// (same stream semantics: ordered on stream s, asynchronous to the host).
+// instead of hipMemset / hipMemcpy(DeviceToDevice) (same stream semantics:
+// ordered on stream s, asynchronous to the host).  Round 4 moved every fill
+// and device copy here while it chased the wrong operators of section 4.1;
+// the cause turned out to be elsewhere (the pool aliasing above), but one
+// code path for all of them is kept: the fills and copies are plain
+// streaming kernels at HBM rate.
 namespace detail {
 template <class T>
 __global__ __launch_bounds__(256) void fill_words_kernel(T* __restrict__ p, T v, int64_t n) {
@@ -102,7 +113,7 @@ inline hipError_t dev_copy(void* d, const void* src, size_t bytes, hipStream_t s
   return hipGetLastError();
 }
 
-// 0: stream-ordered (default), 1: drain + hipFree, 2: plain hipFree; read
+// 0: null-stream ordered (default), 1: drain + hipFree, 2: plain hipFree; read
 // once per process (a block must be freed the way it was allocated)
 inline int free_mode() {
   static const int m = [] {
@@ -114,16 +125,111 @@ inline int free_mode() {
   return m;
 }
 
-// a setup temporary of b bytes (null-stream ordered)
+namespace detail {
+// hipMalloc'd temporaries of one device: idle blocks by size, and the size
+// of every block the cache made
+struct TmpBlock {
+  size_t bytes;
+  bool idle;
+};
+struct TmpCache {
+  std::mutex m;
+  std::multimap<size_t, void*> idle;
+  std::unordered_map<void*, TmpBlock> made;
+};
+inline TmpCache& tmp_cache_of(int d) {
+  static TmpCache c[64];
+  return c[d & 63];
+}
+inline TmpCache& tmp_cache() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return tmp_cache_of(d);
+}
+// 4 KiB granules up to 1 MiB, 2 MiB granules above
+inline size_t tmp_round(size_t b) {
+  b = std::max<size_t>(b, 1);
+  return b <= ((size_t)1 << 20) ? (b + 4095) & ~(size_t)4095 : (b + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+}
+}  // namespace detail
+
+// hipFree every idle cached block of the current device (after the null
+// stream has drained: the last users of an idle block were queued there)
+inline void tmp_trim() {
+  auto& c = detail::tmp_cache();
+  std::lock_guard<std::mutex> g(c.m);
+  if (c.idle.empty()) return;
+  (void)hipStreamSynchronize(nullptr);
+  for (auto& kv : c.idle) {
+    (void)hipFree(kv.second);
+    c.made.erase(kv.second);
+  }
+  c.idle.clear();
+}
+
+// tmp_trim on every device whose cache holds idle blocks (the end of a
+// setup: the current device is put back)
+inline void tmp_trim_all() {
+  int cur = -1;
+  for (int d = 0; d < 64; ++d) {
+    bool any;
+    {
+      auto& c = detail::tmp_cache_of(d);
+      std::lock_guard<std::mutex> g(c.m);
+      any = !c.idle.empty();
+    }
+    if (!any) continue;
+    if (cur < 0 && hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
+    if (hipSetDevice(d) != hipSuccess) { (void)hipGetLastError(); continue; }
+    tmp_trim();
+  }
+  if (cur >= 0) (void)hipSetDevice(cur);
+}
+
+// a setup temporary of b bytes (null-stream ordered): an idle cached block
+// of at most 5/4 of the rounded size, else a new hipMalloc (the idle blocks
+// are released and the allocation tried again when HBM runs out)
 inline hipError_t tmp_malloc(void** p, size_t b) {
   if (free_mode() != 0) return hipMalloc(p, b);
-  return hipMallocAsync(p, b, nullptr);
+  auto& c = detail::tmp_cache();
+  const size_t r = detail::tmp_round(b);
+  {
+    std::lock_guard<std::mutex> g(c.m);
+    auto it = c.idle.lower_bound(r);
+    if (it != c.idle.end() && it->first <= r + r / 4) {
+      *p = it->second;
+      c.idle.erase(it);
+      c.made[*p].idle = false;
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, r);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    tmp_trim();
+    e = hipMalloc(p, r);
+  }
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(c.m);
+  c.made[*p] = detail::TmpBlock{r, false};
+  return hipSuccess;
 }
 
 inline void tmp_free(void* p) {
   if (!p) return;
   switch (free_mode()) {
-    case 0: (void)hipFreeAsync(p, nullptr); break;
+    case 0: {
+      auto& c = detail::tmp_cache();
+      std::lock_guard<std::mutex> g(c.m);
+      auto it = c.made.find(p);
+      if (it == c.made.end() || it->second.idle) {   // not a live cached block: a bug of the caller
+        std::fprintf(stderr, "[mamg] tmp_free(%p): %s\n", p, it == c.made.end() ? "unknown block" : "freed twice");
+        break;
+      }
+      it->second.idle = true;
+      c.idle.emplace(it->second.bytes, p);
+      break;
+    }
     case 1: (void)hipDeviceSynchronize(); (void)hipFree(p); break;
     default: (void)hipFree(p); break;
   }
