@@ -2257,13 +2257,8 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
 // node I's four sorted column segments (rowstage.h stage_segs): q = 2 f + g
 // holds the entries of row f nr + I whose column lies in field g (node
 // column = col - g nc)
-#ifdef MAMG_C2B_OPTNONE   // diagnosis build: the row-merge conversion unoptimised
-#define C2B_ATTR __attribute__((optnone))
-#else
-#define C2B_ATTR
-#endif
 template <bool FILL>
-__global__ C2B_ATTR __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
+__global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
                                                      const int32_t* __restrict__ col,
                                                      const double* __restrict__ val, int64_t* bptr,
                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
@@ -2555,15 +2550,6 @@ struct TmpPool {
   }
 };
 
-// MAMG_DEBUG_SUMS=1: the layout builder's diagnosis traces (see debug_sums)
-bool debug_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("MAMG_DEBUG_SUMS");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B, std::string* err) {
   int rc;
   B->nr = nr; B->nc = nc; B->merged = false;
@@ -2575,21 +2561,8 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
-  if (debug_on()) HIPCHK(dev_memset(B->val, 0xff, B->nb * sizeof(dv4)));   // NaN: a lost store shows as NaN
-  static const int dflush = [] {   // diagnosis: 1 = flush the L2s after the fill, 2 = after the conversion
-    const char* e = std::getenv("MAMG_DEBUG_FLUSH");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (dflush == 1) HIPCHK(l2_flush());
-  // MAMG_C2B_LDS_PAD (diagnosis): extra dynamic LDS per workgroup, which
-  // lowers how many of these 48 KB workgroups share a CU's 160 KB
-  static const size_t pad = [] {
-    const char* e = std::getenv("MAMG_C2B_LDS_PAD");
-    return e ? (size_t)std::atoll(e) : (size_t)0;
-  }();
-  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES, pad>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
-  if (dflush == 2) HIPCHK(l2_flush());
   return MAMG_OK;
 }
 
@@ -3372,29 +3345,8 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   return MAMG_OK;   // ring_blocks_dev's buffers: freed by the guard, null-stream ordered
 }
 
-// MAMG_DEBUG_SUMS: hash of a device array (null-stream ordered copy)
-void debug_hash(const char* tag, int l, const void* p, size_t b) {
-  if (!debug_on() || !p || !b) return;
-  static const bool dsync = std::getenv("MAMG_DEBUG_SYNC") != nullptr;   // drain before reading back
-  if (dsync) (void)hipDeviceSynchronize();
-  std::vector<unsigned char> v(b);
-  if (hipMemcpy(v.data(), p, b, hipMemcpyDeviceToHost) != hipSuccess) { (void)hipGetLastError(); return; }
-  unsigned long long x = 1469598103934665603ull;
-  for (unsigned char c : v) x = (x ^ c) * 1099511628211ull;
-  std::fprintf(stderr, "[mamg sums] src L%d.%s %016llx (%zu B)\n", l, tag, x, b);
-}
-
 int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int lanesA, std::string* err) {
   DLevel& D = h->L[l];
-  if (l == 0) {
-    debug_hash("A.val", l, S.A.val, (size_t)S.A.nnz * 8);
-    debug_hash("P.col", l, S.P.col, (size_t)S.P.nnz * 4);
-    debug_hash("P.val", l, S.P.val, (size_t)S.P.nnz * 8);
-    debug_hash("AP.ptr", l, S.AP.ptr, (size_t)(S.AP.n + 1) * 8);
-    debug_hash("AP.col", l, S.AP.col, (size_t)S.AP.nnz * 4);
-    debug_hash("AP.val", l, S.AP.val, (size_t)S.AP.nnz * 8);
-    debug_hash("W", l, S.W, (size_t)(D.n / 2) * 32);
-  }
   const mamg_params& p = h->p;
   const int64_t nv = D.n / 2;
   int rc;
@@ -3434,51 +3386,10 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     TBsr Pb, Qb, M;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
     if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Qb, err))) return rc;
-    if (l == 0 && debug_on()) {   // the same conversion again: is it deterministic?
-      for (int rep = 0; rep < 3; ++rep) {
-        TBsr Q2;
-        if ((rc = dev_csr_to_bsr(&T, S.AP, nv, nvc, &Q2, err))) return rc;
-        debug_hash("Qb.ptr", l, Qb.ptr, (size_t)(Qb.nr + 1) * 8);
-        debug_hash("Q2.ptr", l, Q2.ptr, (size_t)(Q2.nr + 1) * 8);
-        debug_hash("Qb.col", l, Qb.col, (size_t)Qb.nb * 4);
-        debug_hash("Q2.col", l, Q2.col, (size_t)Q2.nb * 4);
-        debug_hash("Qb.val", l, Qb.val, (size_t)Qb.nb * 32);
-        debug_hash("Q2.val", l, Q2.val, (size_t)Q2.nb * 32);
-        debug_hash("AP.val again", l, S.AP.val, (size_t)S.AP.nnz * 8);
-        {   // where the two conversions differ
-          if (std::getenv("MAMG_DEBUG_SYNC")) (void)hipDeviceSynchronize();
-          std::vector<dv4> va(Qb.nb), vb(Qb.nb);
-          std::vector<int64_t> pa(Qb.nr + 1);
-          (void)hipMemcpy(va.data(), Qb.val, Qb.nb * sizeof(dv4), hipMemcpyDeviceToHost);
-          (void)hipMemcpy(vb.data(), Q2.val, Qb.nb * sizeof(dv4), hipMemcpyDeviceToHost);
-          (void)hipMemcpy(pa.data(), Qb.ptr, (Qb.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost);
-          int shown = 0;
-          int64_t ndiff = 0;
-          for (int64_t k = 0; k < Qb.nb; ++k) {
-            if (std::memcmp(&va[k], &vb[k], sizeof(dv4)) == 0) continue;
-            ++ndiff;
-            if (shown++ >= 6) continue;
-            const int64_t row = std::upper_bound(pa.begin(), pa.end(), k) - pa.begin() - 1;
-            std::fprintf(stderr, "[mamg sums] diff block %lld row %lld (wg %lld): %.17g %.17g %.17g %.17g vs %.17g %.17g %.17g %.17g\n",
-                         (long long)k, (long long)row, (long long)(row / RS_NODES), va[k].x, va[k].y, va[k].z, va[k].w,
-                         vb[k].x, vb[k].y, vb[k].z, vb[k].w);
-          }
-          if (ndiff) std::fprintf(stderr, "[mamg sums] %lld of %lld blocks differ\n", (long long)ndiff, (long long)Qb.nb);
-        }
-        T.release(Q2.ptr); T.release(Q2.col); T.release(Q2.val);
-      }
-    }
     if (g_post_k) {   // one operator K = P - W (A P) on AP's pattern,
                       // W = the first post-smoothing step's smoother
       const double* Wpost = reinterpret_cast<const double*>(step_wd(D, 0, false));
       if ((rc = dev_kmerge(&T, Pb, Qb, Wpost, &M, err))) return rc;
-      if (l == 0) {
-        debug_hash("Pb.val", l, Pb.val, (size_t)Pb.nb * 32);
-        debug_hash("Qb.val", l, Qb.val, (size_t)Qb.nb * 32);
-        debug_hash("Wpost", l, Wpost, (size_t)(D.n / 2) * 32);
-        debug_hash("Kraw.col", l, M.col, (size_t)M.nb * 4);
-        debug_hash("Kraw.val", l, M.val, (size_t)M.nb * 32);
-      }
     } else {          // P and AP blocks side by side in one row window
       if ((rc = dev_merge_rows(&T, Pb, Qb, &M, err))) return rc;
     }
@@ -4417,31 +4328,16 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // 0.51 vs 0.53 ms); re-homed contiguously 1.47-1.59 ms, 268.6-276.4 applies/s
 // against 263-264 for plain allocations on the same box (DESIGN.md section 5,
 // profiles/r02_rehome_level0.txt).  Same data: results are bitwise equal.
-// The arena's copies stay unused.
-// move one array into a fresh, physically contiguous allocation (plain
-// hipMalloc where the driver has none; the old copy is kept if both fail)
-// hipMalloc (the old copy is kept if both fail).  An old copy of its own
-// allocation is freed; one inside the pre-reserved arena stays (the arena is
-// one allocation).
-// a fresh allocation for a re-homed stream: physically contiguous where the
-// driver has it, plain hipMalloc otherwise.  A contiguous allocation that
-// takes longer than 50 ms (the driver compacting memory: on one round-3 box
-// the layout phase took 2.1 s against 0.23 s elsewhere) turns contiguous
-// allocations off for the rest of the process.
-bool g_contig_ok = true;
+// a fresh allocation for a re-homed stream (plain hipMalloc).  Rounds 3-4
+// took these from hipExtMallocWithFlags(hipDeviceMallocContiguous); with the
+// setup temporaries in the library's own block cache (dmem.h), a setup made
+// after a handle with contiguous re-homed arrays faulted in its first
+// kernels on every run, so contiguous allocations are
+// no longer made.  The K region search (select_k_region) keeps its value:
+// distinct plain allocations still differ by a few percent.
 void* placement_alloc(size_t b) {
   void* r = nullptr;
-  static const bool contig_env = [] {   // off by default
-    const char* e = std::getenv("MAMG_CONTIG");
-    return e && std::atoi(e) == 1;
-  }();
-  if (g_contig_ok && contig_env) {
-    const auto t0 = std::chrono::steady_clock::now();
-    if (hipExtMallocWithFlags(&r, b, hipDeviceMallocContiguous) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
-    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 50.0)
-      g_contig_ok = false;
-  }
-  if (!r && hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+  if (hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
   return r;
 }
 
@@ -4479,8 +4375,7 @@ void rehome_bsr(DeviceHandle* h, DBsr& M) {
 // with identical fabric request counts and no TLB misses (bench/kplace.py,
 // profiles/r03_k_placement.txt); slice order, split layouts and XCD row order
 // do not remove it.  So the values are copied into up to MAMG_KREGION_TRIES
-// (4) distinct fresh allocations (physically contiguous where the driver has
-// them), K is timed in each (one warm + three launches), and the fastest
+// (4) distinct fresh allocations, K is timed in each (one warm + three launches), and the fastest
 // region is kept.  Same bytes: results are bitwise equal.
 // Bounded (round 4): candidates are tried one at a time while the search has
 // spent less than MAMG_KREGION_BUDGET_MS (200) and a quarter of the HBM stays

@@ -62,17 +62,6 @@ inline unsigned words_grid(int64_t n) {
 }
 }  // namespace detail
 
-// write back and invalidate every XCD's L2 (a system-scope fence in
-// workgroups spread over all CUs); ordered on stream s
-namespace detail {
-template <int N>   // a template: one definition however many units include this
-__global__ __launch_bounds__(64) void l2_flush_kernel() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, ""); }
-}  // namespace detail
-inline hipError_t l2_flush(hipStream_t s = nullptr) {
-  detail::l2_flush_kernel<0><<<2048, 64, 0, s>>>();
-  return hipGetLastError();
-}
-
 inline hipError_t dev_memset(void* p, int v, size_t bytes, hipStream_t s = nullptr) {
   if (!bytes) return hipSuccess;
   const uint32_t b = (uint8_t)v, w = b * 0x01010101u;
