@@ -223,3 +223,18 @@ def test_num_functions_inference_is_reported_and_overridable(lib_built):
         assert _with_functions(None, P.parameters_standard, {}) == ({}, [])
     assert P.make_params(P.parameters_standard, **_with_functions(W, P.parameters_standard,
                                                                    {'num_functions': 1})[0]).num_functions == 1
+
+
+def test_no_stream_ordered_pool_or_contiguous_allocations(lib_built):
+    """the runtime's stream-ordered pool hands out
+    live blocks that share physical memory (bench/contig_alias.hip), and the
+    contiguous re-homed arrays broke the next setup; the library imports
+    neither allocator (its setup temporaries come from dmem.h's own cache)."""
+    import subprocess
+    so = os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg.so')
+    out = subprocess.run(['nm', '-D', '--undefined-only', so], capture_output=True, text=True,
+                         check=True).stdout
+    imported = set(re.findall(r'\b(hip\w+)@', out))
+    assert 'hipMalloc' in imported
+    for bad in ('hipMallocAsync', 'hipFreeAsync', 'hipMallocFromPoolAsync', 'hipExtMallocWithFlags'):
+        assert bad not in imported, bad
