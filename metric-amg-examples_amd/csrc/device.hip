@@ -455,6 +455,21 @@ __global__ __launch_bounds__(256) void msell_kernel(
 // Sums run lower part then upper part, each in column order: the full row's
 // block order, so the result is bitwise that of sell2_kernel.
 // ---------------------------------------------------------------------------
+// streams of hsell2_kernel touched once: row meta, lower slot pointers and
+// upper columns (level 1), and the b loads / output stores (level 2) are
+// non-temporal, so that they do not displace from L2 the upper values the
+// mirrors re-read.  Round 4 A/B at nrefs=6 (profiles/r04_hsell_nt.txt):
+// residual L2-miss bytes 6.30 -> 6.03 (1) -> 5.87 GB (2) per launch,
+// 1.077 -> 1.070 ms.  Build switch (0 = plain loads), default 2.
+#ifndef MAMG_HSELL_NT
+#define MAMG_HSELL_NT 2
+#endif
+template <class T>
+__device__ __forceinline__ T ld_once(const T* p) {
+  if constexpr (MAMG_HSELL_NT != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 template <int EPI, bool XFM, int U, bool GH, int TAG>
 __global__ __launch_bounds__(256) void hsell2_kernel(
     int64_t row0, int64_t nr, const int32_t* __restrict__ meta, const int32_t* __restrict__ ucol,
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
   const int64_t node = row0 + blk0 * 256 + threadIdx.x;   // rows [row0, nr)
   if (node >= nr) return;
   const double* offd = uval + 2 * nbs;
-  const int m = meta[node];
+  const int m = ld_once(meta + node);
   const int ulen = m & 0xff, llen = (m >> 8) & 0xff;
   const uint32_t urow = 64u * (uint32_t)hwu;
   double s0 = 0.0, s1 = 0.0;
@@ -478,7 +493,7 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
       dv4 v[U];
       double2 a[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) p[u] = (uint32_t)lptr[k + (int64_t)SELL_C * (j + u < llen ? j + u : llen - 1)];
+      for (int u = 0; u < U; ++u) p[u] = (uint32_t)ld_once(lptr + k + (int64_t)SELL_C * (j + u < llen ? j + u : llen - 1));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t c = (int32_t)((p[u] / urow) * 64u + (p[u] & 63u));
@@ -502,7 +517,7 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t kk = k + (int64_t)SELL_C * (j + u < ulen ? j + u : ulen - 1);
-        c[u] = ucol[kk];
+        c[u] = ld_once(ucol + kk);
         v[u] = blk<true>(uval, offd, kk);
       }
 #pragma unroll
@@ -542,7 +557,8 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
   double2 bb = {0.0, 0.0}, yy = {0.0, 0.0};
   dv4 w = {0.0, 0.0, 0.0, 0.0};
   if (EPI == EPI_RESID || EPI == EPI_BJAC)
-    bb = double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
+    bb = MAMG_HSELL_NT >= 2 ? double2{ld_once(b + (bs ? node : 2 * node)), ld_once(b + (bs ? bs + node : 2 * node + 1))}
+                            : double2{vget(b, bs, node, 0), vget(b, bs, node, 1)};
   if (EPI == EPI_YADD || EPI == EPI_BJAC) yy = reinterpret_cast<const double2*>(y)[node];
   if (EPI == EPI_BJAC) w = W[node];
   double o0, o1;
@@ -557,8 +573,13 @@ __global__ __launch_bounds__(256) void hsell2_kernel(
     o0 = yy.x + (w.x * r0 + w.y * r1);
     o1 = yy.y + (w.z * r0 + w.w * r1);
   }
-  vset(out, os, node, 0, o0);
-  vset(out, os, node, 1, o1);
+  if constexpr (MAMG_HSELL_NT >= 2) {
+    __builtin_nontemporal_store(o0, out + (os ? node : 2 * node));
+    __builtin_nontemporal_store(o1, out + (os ? os + node : 2 * node + 1));
+  } else {
+    vset(out, os, node, 0, o0);
+    vset(out, os, node, 1, o1);
+  }
 }
 
 // fused prolongation + first post sweep on a SELL-64 [P | AP] (see
