@@ -365,7 +365,8 @@ def main():
             tp2 = time.time() - t0
             profiles.append({'profile': name, 'niters': len(s2.residuals) - 1, 'pcg_s': round(tp2, 4),
                              'setup_s': round(ts, 4), 'setup_plus_pcg_s': round(ts + tp2, 4),
-                             'ms_per_apply': round(ms2, 4)})
+                             'ms_per_apply': round(ms2, 4),
+                             'setup_phases_ms': {k: round(v, 1) for k, v in B2.setup_timings.items()}})
             B2.close()
             del s2, z2
 
