@@ -310,12 +310,15 @@ __global__ __launch_bounds__(256) void sell2_kernel(
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b,
     int64_t bs, const dv4* __restrict__ W, double* out, int64_t os, int remap,
-    const int32_t* __restrict__ sched) {
-  const int64_t node = (sched ? (int64_t)sched[blockIdx.x] : row_block(remap)) * 256 + threadIdx.x;
-  if (node >= nr) return;
+    const int32_t* __restrict__ sched, int lsort) {
+  const int64_t slot = (sched ? (int64_t)sched[blockIdx.x] : row_block(remap)) * 256 + threadIdx.x;
+  if (slot >= nr) return;
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
-  const int len = meta[node] & 0xffff;
-  int64_t k = soff[node / SELL_C] + (node & (SELL_C - 1));
+  const int m = meta[slot];
+  const int len = m & 0xffff;
+  int64_t k = soff[slot / SELL_C] + (slot & (SELL_C - 1));
+  // the row this slot holds (DBsr::lsort: rows sorted by length in the slice)
+  const int64_t node = lsort ? (slot & ~(int64_t)(SELL_C - 1)) | ((m >> 16) & (SELL_C - 1)) : slot;
   double s0 = 0.0, s1 = 0.0;
   // chunks of U blocks, branch-free (slot clamped into the row, contribution
   // selected away): one load -> gather chain per chunk
@@ -380,14 +383,18 @@ __global__ __launch_bounds__(256) void msell_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os, int remap) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap, int lsort) {
   constexpr int RW = 64 / LPR;                          // rows per wavefront
   const int lane = threadIdx.x & 63, q = lane / RW;
-  const int64_t node = row_block(remap) * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
-  const bool live = node < nr;
-  const int64_t nd = live ? node : nr - 1;            // dead lanes mirror the last row, write nothing
-  const int len = meta[nd] & 0xffff;
-  const int64_t k = soff[nd / SELL_C] + (nd & (SELL_C - 1));
+  const int64_t slot = row_block(remap) * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
+  const bool live = slot < nr;
+  const int64_t ns = live ? slot : nr - 1;            // dead lanes mirror the last slot, write nothing
+  const int m = meta[ns];
+  const int len = m & 0xffff;
+  const int64_t k = soff[ns / SELL_C] + (ns & (SELL_C - 1));
+  // the row this slot holds (DBsr::lsort: rows sorted by length in the slice)
+  const int64_t node = lsort ? (ns & ~(int64_t)(SELL_C - 1)) | ((m >> 16) & (SELL_C - 1)) : ns;
+  const int64_t nd = node;
   const double* offd = SYM ? bval + 2 * nbs : nullptr;
   const int f = q & 1;
   const bool wr = q < 2;
@@ -1819,6 +1826,8 @@ inline unsigned nblocks(int64_t work) { return (unsigned)((work + 255) / 256); }
 //                       XCD (1; 0 = row order)
 //   MAMG_R_BANDS        plane-band schedule of the level-0 restriction: sub-bands
 //                       per XCD (1; 0 = XCD-contiguous rows)
+//   MAMG_K_SORT         level-0 K's rows sorted by length inside each SELL slice
+//                       (1; 0 = row order; sort_sell_slices)
 //   MAMG_POST_K         0: fused post sweep over [P | AP] instead of K = P - W A P (1)
 //   multi-GPU (mamg_setup_dist): MAMG_OVERLAP 0 = no interior-row launch during
 //   the forward halo (1); MAMG_DIST_TEST=dry: a virtual rank skips its exchanges
@@ -1834,6 +1843,7 @@ constexpr int64_t g_sell_max_len = 40;
 int g_half = 1;
 int g_half_bands = 1;
 int g_r_bands = 1;
+int g_k_sort = 1;
 int g_post_k = 1;
 int g_kvar = 0;
 int64_t g_sell_min_rows = 1 << 20;
@@ -1861,6 +1871,8 @@ void read_knobs() {
   g_half_bands = e ? std::atoi(e) : 1;
   e = std::getenv("MAMG_R_BANDS");
   g_r_bands = e ? std::atoi(e) : 1;
+  e = std::getenv("MAMG_K_SORT");
+  g_k_sort = e ? std::atoi(e) : 1;
 }
 
 // every block symmetric (bitwise): then 3 doubles per block carry it exactly
@@ -1909,6 +1921,8 @@ struct DBsr {              // 2x2 blocks, node-major
   int64_t* soff = nullptr;
   int32_t* meta = nullptr;
   int32_t* perm = nullptr;  // SELL-C-sigma: row held by each slot (merged matrices)
+  bool lsort = false;       // SELL rows sorted by length inside each slice: meta is per slot,
+                            // length | (row - slice start) << 16 (sort_sell_slices)
   // half-symmetric ELL-64 (half == true, A symmetric bitwise): col / val hold
   // the upper part I <= J < nr, hwu slots per row; lptr holds,
   // per lower entry J < I, the slot of the mirror block (J, I) in the upper
@@ -2423,6 +2437,49 @@ __global__ __launch_bounds__(256) void sell_fill_kernel(int64_t nr, const int64_
       sval[2 * nbs + kk] = v.y;
     } else {
       reinterpret_cast<dv4*>(sval)[kk] = v;
+    }
+  }
+}
+
+// SELL-64 rows sorted by length inside each slice (DBsr::lsort): one 64-lane
+// workgroup per slice; lane i's rank = rows longer than row i + equal rows
+// before it (stable, longest first).  nmeta[slot] = length | (row offset << 16),
+// src[slot] = the row offset the slot takes its blocks from.
+__global__ __launch_bounds__(64) void sell_sort_kernel(int64_t nr, const int32_t* __restrict__ meta,
+                                                      int32_t* __restrict__ nmeta, int32_t* __restrict__ src) {
+  __shared__ int len[SELL_C];
+  const int64_t r0 = (int64_t)blockIdx.x * SELL_C;
+  const int i = threadIdx.x;
+  const int cnt = (int)min((int64_t)SELL_C, nr - r0);
+  const int li = i < cnt ? meta[r0 + i] & 0xffff : -1;
+  len[i] = li;
+  __syncthreads();
+  if (i >= cnt) return;
+  int rank = 0;
+  for (int j = 0; j < cnt; ++j) rank += (len[j] > li) || (len[j] == li && j < i);
+  nmeta[r0 + rank] = li | (i << 16);
+  src[r0 + rank] = i;
+}
+
+// the slot arrays re-ordered to the sorted rows: slot p of slice s takes the
+// blocks of slot src[p] (width = the slice's, so every block moves whole)
+__global__ __launch_bounds__(64) void sell_permute_kernel(int64_t nr, const int64_t* __restrict__ soff,
+                                                         const int32_t* __restrict__ src, int64_t nbs, int per,
+                                                         const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                         int32_t* __restrict__ ncol, double* __restrict__ nval) {
+  const int64_t s = blockIdx.x, r0 = s * SELL_C;
+  const int p = threadIdx.x;
+  if (r0 + p >= nr) return;
+  const int64_t w = (soff[s + 1] - soff[s]) / SELL_C;
+  const int64_t d0 = soff[s] + p, s0 = soff[s] + src[r0 + p];
+  for (int64_t j = 0; j < w; ++j) {
+    const int64_t d = d0 + SELL_C * j, o = s0 + SELL_C * j;
+    ncol[d] = col[o];
+    if (per == 4) {
+      reinterpret_cast<dv4*>(nval)[d] = reinterpret_cast<const dv4*>(val)[o];
+    } else {
+      reinterpret_cast<dv2*>(nval)[d] = reinterpret_cast<const dv2*>(val)[o];
+      nval[2 * nbs + d] = val[2 * nbs + o];
     }
   }
 }
@@ -2959,6 +3016,38 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
   return MAMG_OK;
 }
 
+// Level-0 K's rows sorted by length inside each SELL slice (MAMG_K_SORT, default
+// on).  A 128-byte line of one block slot holds 4 neighbouring rows' blocks;
+// in row order their lengths differ, so the last slots of the longer rows pull
+// whole lines whose other quarters are padding: 13 % more line bytes than
+// stored blocks for the bidomain K.  Sorted, the rows sharing a line have equal
+// or neighbouring lengths (1.9 %).  Each row keeps its blocks and their order:
+// results are bitwise those of row order (test_k_row_sort_bitwise).
+template <class HT>
+int sort_sell_slices(HT* h, TmpPool* T, DBsr* D, std::string* err) {
+  int rc;
+  if (!D->sell || D->split || D->nr == 0) return MAMG_OK;
+  const int64_t ns = (D->nr + SELL_C - 1) / SELL_C, per = D->sym ? 3 : 4;
+  int32_t *nmeta = nullptr, *src = nullptr, *ncol = nullptr;
+  double* nval = nullptr;
+  if ((rc = T->alloc(&nmeta, D->nr, err)) || (rc = T->alloc(&src, D->nr, err)) ||
+      (rc = T->alloc(&ncol, std::max<int64_t>(D->nbs, 1), err)) ||
+      (rc = T->alloc(&nval, std::max<int64_t>(per * D->nbs, 1), err)))
+    return rc;
+  HIPCHK(dev_memset(ncol, 0, std::max<int64_t>(D->nbs, 1) * sizeof(int32_t)));
+  HIPCHK(dev_memset(nval, 0, std::max<int64_t>(per * D->nbs, 1) * sizeof(double)));
+  sell_sort_kernel<<<(unsigned)ns, SELL_C>>>(D->nr, D->meta, nmeta, src);
+  HIPCHK(hipGetLastError());
+  sell_permute_kernel<<<(unsigned)ns, SELL_C>>>(D->nr, D->soff, src, D->nbs, (int)per, D->col, D->val, ncol, nval);
+  HIPCHK(hipGetLastError());
+  HIPCHK(dev_copy(D->meta, nmeta, D->nr * sizeof(int32_t)));
+  HIPCHK(dev_copy(D->col, ncol, D->nbs * sizeof(int32_t)));
+  HIPCHK(dev_copy(D->val, nval, per * D->nbs * sizeof(double)));
+  T->release(nmeta); T->release(src); T->release(ncol); T->release(nval);
+  D->lsort = true;
+  return MAMG_OK;
+}
+
 // one BSR2 level from device-resident field-major CSRs (AP.n == 0: no fusion)
 struct LevelSrc {
   DevMat A, P, AP, R;
@@ -3422,6 +3511,8 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
     if ((rc = finalize_bsr(h, &T, M, g_post_k ? &D.KPb : &D.PAb, 0, false, err, g_post_k != 0, false,
                            l > 0 && g_post_k != 0)))
       return rc;
+    if (l == 0 && g_post_k && g_k_sort && D.KPb.sell && D.KPb.lpr <= 1)
+      if ((rc = sort_sell_slices(h, &T, &D.KPb, err))) return rc;
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -4032,7 +4123,7 @@ void launch_sell_u(const Op& o, hipStream_t s) {
   if (g == 0) return;
 #define SELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
     0, \
-    ((int64_t)g == M.nsched ? M.sched : nullptr)
+    ((int64_t)g == M.nsched ? M.sched : nullptr), M.lsort ? 1 : 0
   switch (o.epi) {
     case EPI_Y: sell2_kernel<EPI_Y, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
     case EPI_YADD: sell2_kernel<EPI_YADD, XFM, SYM, U, NT, TAG><<<g, 256, 0, s>>>(SELL_ARGS); break;
@@ -4052,7 +4143,7 @@ void launch_msell(const Op& o, hipStream_t s) {
   const unsigned g = (unsigned)((M.nr + rows - 1) / rows);
   if (g == 0) return;
 #define MSELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 && g_kvar == 3) ? 1 : 0
+    (TAG == 0 && g_kvar == 3) ? 1 : 0, M.lsort ? 1 : 0
   switch (o.epi) {
     case EPI_Y: msell_kernel<LPR, U, EPI_Y, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
     case EPI_YADD: msell_kernel<LPR, U, EPI_YADD, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;

@@ -538,6 +538,36 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
         b.close()
 
 
+@pytest.mark.parametrize('variant', ['0', '1', '2'])
+def test_k_row_sort_bitwise(lib_built, monkeypatch, variant):
+    """Level-0 K with its rows sorted by length inside each SELL slice
+    (MAMG_K_SORT=1, the default; sort_sell_slices) gives the bits of row
+    order, for the two-lane, one-lane and four-lane K kernels, on the graph
+    apply and the eager launches, and equals the oracle."""
+    import torch
+    M = _mamg()
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    monkeypatch.setenv('MAMG_K_VARIANT', variant)
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    zs = []
+    for srt in ('0', '1'):
+        monkeypatch.setenv('MAMG_K_SORT', srt)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        assert B.level_format(0)['post_sell']
+        z = B.matvec(r)
+        zz = torch.empty_like(z)
+        B.time_apply(r, zz, 1, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(zz, z)
+        zs.append(z.clone())
+        B.close()
+    assert torch.equal(zs[0], zs[1])
+    zo = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs).apply(mo.seeded_rhs(s.N))
+    assert rel(zs[1].cpu().numpy(), zo) < APPLY_TOL
+
+
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e4, dict(smoother='POLY')),
                                         (3, 16, 1e6, dict(presmooth_iter=2, postsmooth_iter=2))])
 def test_coarse_multilane_sell(lib_built, monkeypatch, dim, n, g, kw):
