@@ -80,7 +80,7 @@ def main():
         out['per_rank'].append({'rank': p, 'setup_s': round(t, 2), 'device_GB': round(held / 1e9, 2),
                                 'rss_growth_GB': round(r1 - r0, 2), 'process_peak_rss_GB': round(peak, 2),
                                 'nodes': [hs[-1].o0, hs[-1].o1],
-                                'apply_launches': hs[-1].apply_launches()})
+                                'apply_launches': hs[-1].apply_launches})
         print('rank %d: setup %.1fs, device %.2f GB, RSS +%.2f GB (now %.2f, peak %.2f)'
               % (p, t, held / 1e9, r1 - r0, r1, peak), flush=True)
     out['rank_rss_estimate_GB'] = round(out['rss_after_A0_GB'] + max(q['rss_growth_GB'] for q in out['per_rank']), 2)

@@ -6195,6 +6195,8 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
       }
       if ((rc = dev_kmerge(&T, tP, tAP, Wk, &tK, err))) return rc;
       if ((rc = finalize_bsr(h, &T, tK, &D.K, 0, false, err))) return rc;
+      if (l == 0 && g_k_sort && D.K.sell && D.K.lpr <= 1)   // rows sorted inside slices (section 4.1)
+        if ((rc = sort_sell_slices(h, &T, &D.K, err))) return rc;
     } else {
       if ((rc = dev_merge_rows(&T, tP, tAP, &tK, err))) return rc;
       if ((rc = finalize_bsr(h, &T, tK, &D.PA, 0, false, err))) return rc;
