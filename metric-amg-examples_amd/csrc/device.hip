@@ -2157,7 +2157,7 @@ int dalloc(HT* h, T** p, int64_t count, std::string* err) {
     return MAMG_OK;
   }
   void* q = nullptr;
-  HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
+  HIPCHK(dev_malloc(&q, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
   *p = (T*)q;
   poison_doubles(*p, (size_t)count * sizeof(T));
@@ -4449,7 +4449,7 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // distinct plain allocations still differ by a few percent.
 void* placement_alloc(size_t b) {
   void* r = nullptr;
-  if (hipMalloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+  if (dev_malloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
   return r;
 }
 
@@ -5449,7 +5449,7 @@ int ddalloc(DistHandle* h, T** p, int64_t count, std::string* err) {
   *p = nullptr;
   if (count <= 0) return MAMG_OK;
   void* q = nullptr;
-  HIPCHK(hipMalloc(&q, (size_t)count * sizeof(T)));
+  HIPCHK(dev_malloc(&q, (size_t)count * sizeof(T)));
   HIPCHK(dev_memset(q, 0, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
   *p = (T*)q;

@@ -175,6 +175,19 @@ inline void tmp_trim_all() {
   if (cur >= 0) (void)hipSetDevice(cur);
 }
 
+// hipMalloc for the library's long-lived arrays: when HBM runs out while the
+// setup temporaries' cache holds idle blocks, the cache is emptied and the
+// allocation tried once more
+inline hipError_t dev_malloc(void** p, size_t b) {
+  hipError_t e = hipMalloc(p, b);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    tmp_trim();
+    e = hipMalloc(p, b);
+  }
+  return e;
+}
+
 // a setup temporary of b bytes (null-stream ordered): an idle cached block
 // of at most 5/4 of the rounded size, else a new hipMalloc (the idle blocks
 // are released and the allocation tried again when HBM runs out)
