@@ -4431,16 +4431,14 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // ---------------------------------------------------------------------------
 // Re-home the level-0 streams -- K values and columns (6.4 GB at nrefs=6),
 // A_0's upper values and columns (4.3 GB), R_0's values (2.3 GB) -- and the
-// coarser levels' operators into fresh, physically contiguous allocations
-// (hipDeviceMallocContiguous; a plain allocation where the driver has none)
-// once the setup's temporaries are gone.  The kernels' DRAM rate depends on
-// where these arrays land, for the same bytes and the same PMC traffic: as
-// built in the pre-reserved arena K ran 1.59-1.71 ms; re-homed into plain
-// allocations 1.48-1.68 ms (residual 1.06-1.09 vs 1.09-1.10 ms, restriction
-// 0.51 vs 0.53 ms); re-homed contiguously 1.47-1.59 ms, 268.6-276.4 applies/s
-// against 263-264 for plain allocations on the same box (DESIGN.md section 5,
-// profiles/r02_rehome_level0.txt).  Same data: results are bitwise equal.
-// a fresh allocation for a re-homed stream (plain hipMalloc).  Rounds 3-4
+// coarser levels' operators into fresh allocations once the setup's
+// temporaries are gone.  The kernels' DRAM rate depends on where these arrays
+// land, for the same bytes and the same PMC traffic: as built in the
+// pre-reserved arena K ran 1.59-1.71 ms; re-homed into plain allocations
+// 1.48-1.68 ms (residual 1.06-1.09 vs 1.09-1.10 ms, restriction 0.51 vs
+// 0.53 ms) (profiles/r02_rehome_level0.txt).  Same data:
+// results are bitwise equal.
+// A fresh allocation for a re-homed stream (plain hipMalloc).  Rounds 2-4
 // took these from hipExtMallocWithFlags(hipDeviceMallocContiguous); with the
 // setup temporaries in the library's own block cache (dmem.h), a setup made
 // after a handle with contiguous re-homed arrays faulted in its first
