@@ -1416,50 +1416,113 @@ __global__ __launch_bounds__(256) void pkey_max_kernel(int64_t nr, const int64_t
   out[I] = m;
 }
 
-// colour bit of every coloured node (256-bit, PATCH_WORDS words per node)
-__global__ __launch_bounds__(256) void pmask_init_kernel(int64_t nr, const int16_t* __restrict__ c, uint64_t* __restrict__ m) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (I >= nr) return;
-  const int ci = c[I];
+// ---- distance-3 Jones-Plassmann colouring (mamg_oracle.patch_colouring) -----
+// Round-synchronous: an uncoloured node whose key is the largest uncoloured
+// key within 3 hops takes the lowest colour absent within 3 hops.  That
+// colours a node once every higher-keyed node within 3 hops is coloured, so
+// the result is the greedy colouring in descending key order whatever the
+// schedule.  Rounds 2-4 recomputed every node's 3-hop maxima and 256-bit
+// colour masks each round by three full key-max and three full mask-or passes
+// (12 ms per round, 341 rounds at nrefs=6: 4.2 s of the patch layout).  Since
+// round 5 each round keeps, per node, the 1-, 2- and
+// 3-hop maxima m1, m2, m3 of the uncoloured keys and a 1-hop colour mask:
+//  * a maximum changes only when the node it names (the key's low 32 bits)
+//    gets coloured, so each round re-derives just those entries (lazy refresh,
+//    one level from the one below, closed neighbourhoods);
+//  * a winner (m3 == own key) ORs the 1-hop masks of its 2-hop ball (= the
+//    colours within 3 hops) and adds its colour bit to its neighbours' 1-hop
+//    masks: two winners are > 3 hops apart, so no winner sees another's bit.
+// Same keys, same rounds, same colours (tests/test_gpu_patch.py).
+
+// m[I] refreshed from src (src == nullptr: the keys of uncoloured nodes):
+// kept unless the node it names was coloured.  FIND (the 3-hop level, 1024
+// threads): only uncoloured nodes, and those whose maximum is their own key
+// are appended to the winner list, one atomic per workgroup.  No winner means
+// no uncoloured node (the largest uncoloured key always wins).
+template <bool FIND>
+__global__ __launch_bounds__(FIND ? 1024 : 256) void pkey_refresh_kernel(
+    int64_t nr, const int64_t* __restrict__ ptr, const int32_t* __restrict__ col, const int16_t* __restrict__ c,
+    const uint64_t* __restrict__ src, uint64_t* __restrict__ m, int32_t* __restrict__ win,
+    unsigned int* __restrict__ nwin) {
+  constexpr int NT = FIND ? 1024 : 256;
+  const int64_t I = (int64_t)blockIdx.x * NT + threadIdx.x;
+  bool w = false;
+  if (I < nr) {
+    const bool unc = c[I] < 0;
+    uint64_t v = m[I];
+    if ((!FIND || unc) && v != 0 && c[(uint32_t)v] >= 0) {   // its maximum was coloured: recompute
+      v = src ? src[I] : (unc ? patch_key_dev(I) : 0ull);
+      for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
+        const int64_t J = col[k];
+        const uint64_t u = src ? src[J] : (c[J] < 0 ? patch_key_dev(J) : 0ull);
+        v = u > v ? u : v;
+      }
+      m[I] = v;
+    }
+    w = FIND && unc && v == patch_key_dev(I);
+  }
+  if constexpr (FIND) {   // workgroup-aggregated list appends
+    __shared__ unsigned int wc[NT / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long bw = __ballot(w);
+    if (lane == 0) wc[wv] = (unsigned int)__popcll(bw);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int t = 0;
+      for (int k = 0; k < NT / 64; ++k) { const unsigned int x = wc[k]; wc[k] = t; t += x; }
+      wc[NT / 64] = t ? atomicAdd(nwin, t) : 0u;
+    }
+    __syncthreads();
+    if (w) win[wc[NT / 64] + wc[wv] + __popcll(bw & ((1ull << lane) - 1))] = (int32_t)I;
+  }
+}
+
+// one wave per winner: the colours within 3 hops = OR of the 1-hop masks over
+// the closed 2-hop ball; the lowest free colour; the colour bit into the
+// 1-hop masks of the closed 1-ring
+__global__ __launch_bounds__(256) void patch_win_kernel(int64_t nwin, const int32_t* __restrict__ win,
+                                                        const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                        int16_t* __restrict__ c, unsigned long long* __restrict__ mask1,
+                                                        int* toomany) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= nwin) return;
+  const int64_t I = win[t];
+  const int64_t p0 = ptr[I];
+  const int d1 = (int)(ptr[I + 1] - p0) + 1;     // closed 1-ring: row I's columns, then I
+  // lane a < d1 holds the ring's a-th member u and u's row range
+  int64_t u = I, q0 = 0;
+  int lu = 0;
+  if (lane < d1) {
+    if (lane + 1 < d1) u = col[p0 + lane];
+    q0 = ptr[u];
+    lu = (int)(ptr[u + 1] - q0) + 1;             // closed: u's columns, then u
+  }
+  unsigned long long mk[PATCH_WORDS] = {0ull, 0ull, 0ull, 0ull};
+  // (a, b) pairs, 4 members of the ring at a time and 16 lanes per member
+  for (int a0 = 0; a0 < d1; a0 += 4) {
+    const int a = a0 + (lane >> 4);
+    const int64_t ua = __shfl(u, a & 63), qa = __shfl(q0, a & 63);
+    const int la = __shfl(lu, a & 63);
+    if (a < d1)
+      for (int b = lane & 15; b < la; b += 16) {
+        const int64_t x = b + 1 < la ? (int64_t)col[qa + b] : ua;
+#pragma unroll
+        for (int w = 0; w < PATCH_WORDS; ++w) mk[w] |= mask1[PATCH_WORDS * x + w];
+      }
+  }
 #pragma unroll
   for (int w = 0; w < PATCH_WORDS; ++w)
-    m[PATCH_WORDS * I + w] = (ci >= 0 && ci / 64 == w) ? (1ull << (ci % 64)) : 0ull;
-}
-
-// out[I] = OR of in over row I's node columns and I itself (one hop)
-__global__ __launch_bounds__(256) void pmask_or_kernel(int64_t nr, const int64_t* __restrict__ ptr,
-                                                       const int32_t* __restrict__ col, const uint64_t* __restrict__ in,
-                                                       uint64_t* __restrict__ out) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (I >= nr) return;
-  uint64_t m[PATCH_WORDS];
-#pragma unroll
-  for (int w = 0; w < PATCH_WORDS; ++w) m[w] = in[PATCH_WORDS * I + w];
-  for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
-    const int64_t J = col[k];
-#pragma unroll
-    for (int w = 0; w < PATCH_WORDS; ++w) m[w] |= in[PATCH_WORDS * J + w];
-  }
-#pragma unroll
-  for (int w = 0; w < PATCH_WORDS; ++w) out[PATCH_WORDS * I + w] = m[w];
-}
-
-// one distance-3 Jones-Plassmann round (mamg_oracle.patch_colouring): an
-// uncoloured node whose key is the 3-hop maximum (k3) takes the lowest colour
-// absent from the 3-hop colour mask (m3); two winners are > 3 hops apart
-__global__ __launch_bounds__(256) void patch_assign_kernel(int64_t nr, int16_t* __restrict__ c,
-                                                           const uint64_t* __restrict__ k3, const uint64_t* __restrict__ m3,
-                                                           unsigned long long* nleft, int* toomany) {
-  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (I >= nr || c[I] >= 0) return;
-  if (k3[I] != patch_key_dev(I)) { atomicAdd(nleft, 1ull); return; }
+    for (int o = 32; o > 0; o >>= 1) mk[w] |= __shfl_xor(mk[w], o);
   int cc = -1;
-  for (int w = 0; w < PATCH_WORDS && cc < 0; ++w) {
-    const uint64_t m = m3[PATCH_WORDS * I + w];
-    if (~m) cc = 64 * w + __ffsll((long long)~m) - 1;
+  for (int w = 0; w < PATCH_WORDS && cc < 0; ++w)
+    if (~mk[w]) cc = 64 * w + __ffsll((long long)~mk[w]) - 1;
+  if (cc < 0) {
+    if (lane == 0) *toomany = 1;
+    cc = 0;
   }
-  if (cc < 0) { *toomany = 1; cc = 0; }
-  c[I] = (int16_t)cc;
+  if (lane == 0) c[I] = (int16_t)cc;
+  if (lane < d1) atomicOr(&mask1[PATCH_WORDS * u + cc / 64], 1ull << (cc % 64));
 }
 
 __global__ __launch_bounds__(256) void pcolour_count_kernel(int64_t nr, const int16_t* __restrict__ c,
@@ -1497,6 +1560,14 @@ __device__ __forceinline__ int upk(int i, int j) { return i <= j ? j * (j + 1) /
 // without pivoting in mamg_oracle.batched_inverse's operation order (row k
 // divided by the pivot, then M_i -= M_ik M_k, no contraction); the packed
 // upper triangle of the inverse is stored (the oracle symmetrises the same).
+// lane l's double, broadcast to the wave (l wave-uniform)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_t* __restrict__ perm,
                                                         const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
                                                         const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
@@ -1535,18 +1606,24 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
 #pragma unroll
     for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = (lane - d == r) ? 1.0 : 0.0;
   }
-  for (int k = 0; k < d; ++k) {
-    double mk = 0.0;
+  // pivots unrolled (k a constant: no register selects), the pivot column's
+  // entries broadcast from lane k by v_readlane rather than LDS permutes: the
+  // same operations on the same values as the loop of rounds 2-4
+  // (300 -> see DESIGN.md 2.11 for the measured time)
 #pragma unroll
-    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) mk = r == k ? M[r] : mk;
-    const double p = __shfl(mk, k);
-    if (!(p > 0.0)) { if (lane == 0) atomicOr(bad, 1); return; }
-    mk = mk / p;
+  for (int k = 0; k < 2 * PATCH_MAX_NODES; ++k) {
+    if (k < d) {
+      const double p = readlane_f64(M[k], k);
+      if (!(p > 0.0)) { if (lane == 0) atomicOr(bad, 1); return; }
+      const double mk = M[k] / p;
 #pragma unroll
-    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) {
-      const double f = __shfl(M[r], k);
-      const double t = f * mk;
-      M[r] = r == k ? mk : M[r] - t;
+      for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) {
+        if (r == k) continue;
+        const double f = readlane_f64(M[r], k);
+        const double t = f * mk;
+        M[r] = M[r] - t;
+      }
+      M[k] = mk;
     }
   }
   if (lane >= d && lane < 2 * d) {
@@ -1852,8 +1929,11 @@ int64_t g_tail_nodes = 0;
 bool g_tail_set = false;   // MAMG_TAIL_NODES given: applies to every smoother (tests)   // off: coarse levels 0.41 -> 0.50 ms
 int g_tail_vl = 4;           // lanes per row cap inside the coarse tail (MAMG_TAIL_VL; 1/2/4/8/64 measured)
 void read_knobs() {
-  const char* e = std::getenv("MAMG_K_VARIANT");   // the level-0 K kernel (tests; read at upload)
+  const char* e = nullptr;
+#if MAMG_DIAG
+  e = std::getenv("MAMG_K_VARIANT");   // the level-0 K kernel (diagnosis build: tests, A/Bs; read at upload)
   g_kvar = e ? std::atoi(e) : 0;
+#endif
   e = std::getenv("MAMG_POST_K");
   g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
   e = std::getenv("MAMG_SELL_MIN_ROWS");
@@ -2066,7 +2146,7 @@ struct PcgGraph {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
     for (hipEvent_t e : ev) if (e) (void)hipEventDestroy(e);
-    if (hist) (void)hipFree(hist);
+    if (hist) (void)raw_free(hist);
     *this = PcgGraph();
   }
 };
@@ -2113,8 +2193,8 @@ struct DeviceHandle {
       if (g.graph) (void)hipGraphDestroy(g.graph);
     }
     for (auto& g : pcgs) g.release();
-    for (auto& t : tails) (void)hipFree(t.prog);
-    for (void* a : allocs) (void)hipFree(a);
+    for (auto& t : tails) (void)raw_free(t.prog);
+    for (void* a : allocs) (void)raw_free(a);
     if (hres) (void)hipHostFree(hres);
     if (cap) (void)hipStreamDestroy(cap);
   }
@@ -3292,33 +3372,42 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
     return MAMG_ERR_UNSUPPORTED;
   }
   int16_t* c = nullptr;
-  uint64_t *k1 = nullptr, *k2 = nullptr, *m1 = nullptr, *m2 = nullptr;
+  uint64_t *m1 = nullptr, *m2 = nullptr, *m3 = nullptr;
+  unsigned long long* mask1 = nullptr;
+  int32_t* win = nullptr;
+  unsigned int* wcnt = nullptr;                // winners of the round
   if ((rc = T->alloc(&c, nr, err))) return rc;
-  if ((rc = T->alloc(&k1, nr, err))) return rc;
-  if ((rc = T->alloc(&k2, nr, err))) return rc;
-  if ((rc = T->alloc(&m1, PATCH_WORDS * nr, err))) return rc;
-  if ((rc = T->alloc(&m2, PATCH_WORDS * nr, err))) return rc;
+  if ((rc = T->alloc(&m1, nr, err))) return rc;
+  if ((rc = T->alloc(&m2, nr, err))) return rc;
+  if ((rc = T->alloc(&m3, nr, err))) return rc;
+  if ((rc = T->alloc(&mask1, PATCH_WORDS * nr, err))) return rc;
+  if ((rc = T->alloc(&win, nr, err))) return rc;
+  if ((rc = T->alloc(&wcnt, 1, err))) return rc;
   HIPCHK(dev_memset(c, 0xff, nr * sizeof(int16_t)));
+  HIPCHK(dev_memset(mask1, 0, PATCH_WORDS * nr * sizeof(unsigned long long)));
+  // the 3-hop maxima of all keys (three full passes), then the winner list
+  pkey_init_kernel<<<nblocks(nr), 256>>>(nr, c, m3);
+  pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m3, m1);
+  pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m1, m2);
+  pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m2, m3);
+  const unsigned g1k = (unsigned)((nr + 1023) / 1024);
+  HIPCHK(dev_memset(wcnt, 0, sizeof(unsigned int)));
+  pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, c, m2, m3, win, wcnt);
+  HIPCHK(hipGetLastError());
   for (int round = 0;; ++round) {
-    unsigned long long nl = 0;
-    HIPCHK(dev_memset(left, 0, sizeof(unsigned long long)));
-    pkey_init_kernel<<<nblocks(nr), 256>>>(nr, c, k1);
-    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k1, k2);
-    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k2, k1);
-    pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, k1, k2);
-    pmask_init_kernel<<<nblocks(nr), 256>>>(nr, c, m1);
-    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m1, m2);
-    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m2, m1);
-    pmask_or_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m1, m2);
-    patch_assign_kernel<<<nblocks(nr), 256>>>(nr, c, k2, m2, left, flags + 1);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(&nl, left, sizeof(nl), hipMemcpyDeviceToHost));
-    if (nl == 0) break;
+    unsigned int nw = 0;
+    HIPCHK(hipMemcpy(&nw, wcnt, sizeof(nw), hipMemcpyDeviceToHost));
+    if (nw == 0) break;                        // every node coloured
     if (round > 100000) { *err = "node patches: colouring did not finish"; return MAMG_ERR_SETUP; }
+    patch_win_kernel<<<(unsigned)((nw + 3) / 4), 256>>>(nw, win, B.ptr, B.col, c, mask1, flags + 1);
+    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, c, nullptr, m1, nullptr, nullptr);
+    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, c, m1, m2, nullptr, nullptr);
+    HIPCHK(dev_memset(wcnt, 0, sizeof(unsigned int)));
+    pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, c, m2, m3, win, wcnt);
+    HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
-  if (hf[1]) { *err = "node patches: more than 256 colours"; return MAMG_ERR_UNSUPPORTED; }
-  T->release(k1); T->release(k2); T->release(m1); T->release(m2);
+  T->release(m1); T->release(m2); T->release(m3); T->release(mask1); T->release(win); T->release(wcnt);
   int32_t *ci = nullptr, *cs = nullptr;
   int64_t *iota = nullptr, *sorted = nullptr;
   if ((rc = T->alloc(&ci, nr, err))) return rc;
@@ -3847,12 +3936,15 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   if (!(attr_devices >> dev & 1)) {
     if (hipFuncSetAttribute((const void*)tail_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)TAIL_LDS_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void*)tail_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void*)tail_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess ||
+                            (int)TAIL_LDS_MAX) != hipSuccess
+#if MAMG_DIAG   // the stamped (profiling) variants
+        || hipFuncSetAttribute((const void*)tail_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)TAIL_LDS_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void*)tail_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess) {
+                            (int)TAIL_LDS_MAX) != hipSuccess
+#endif
+    ) {
       (void)hipGetLastError();
       return 0;                        // no large dynamic LDS: keep the global-vector program
     }
@@ -3915,10 +4007,10 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       }
     }
     void* d = nullptr;
-    if (hipMalloc(&d, (size_t)pbytes) != hipSuccess) { (void)hipGetLastError(); return false; }
+    if (raw_malloc(&d, (size_t)pbytes, "long") != hipSuccess) { (void)hipGetLastError(); return false; }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipGetLastError();
-      (void)hipFree(d);
+      (void)raw_free(d);
       return false;
     }
     h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl, prog_lds});
@@ -4447,7 +4539,7 @@ bool bsr_eligible(const Hierarchy& H, const CsrView& A0, const mamg_params& p) {
 // distinct plain allocations still differ by a few percent.
 void* placement_alloc(size_t b) {
   void* r = nullptr;
-  if (dev_malloc(&r, b) != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
+  if (dev_malloc(&r, b, "place") != hipSuccess) { (void)hipGetLastError(); r = nullptr; }
   return r;
 }
 
@@ -4457,7 +4549,7 @@ void rehome_array(DeviceHandle* h, void** ptr, size_t b) {
   if (!r) return;
   if (dev_copy(r, *ptr, b) != hipSuccess) {
     (void)hipGetLastError();
-    (void)hipFree(r);
+    (void)raw_free(r);
     return;
   }
   void* old = *ptr;
@@ -4506,10 +4598,10 @@ void select_k_region(DeviceHandle* h) {
   }
   double* out = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (hipMalloc(&out, L.n * sizeof(double)) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+  if (raw_malloc((void**)&out, L.n * sizeof(double), "tmp") != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
       hipEventCreate(&e1) != hipSuccess) {
     (void)hipGetLastError();
-    if (out) (void)hipFree(out);
+    if (out) (void)raw_free(out);
     rehome_array(h, (void**)&K.val, bytes);
     return;
   }
@@ -4542,7 +4634,7 @@ void select_k_region(DeviceHandle* h) {
   }
   if (bufs.empty()) {
     K.val = (double*)old;
-    (void)hipFree(out);
+    (void)raw_free(out);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
@@ -4606,7 +4698,7 @@ void rehome_operators(DeviceHandle* h) {
 void set_k_split(DBsr& K, int mode) {
   if (!K.sell || K.sym || K.split == mode || K.nbs == 0 || (K.nbs & 63)) return;
   void* t = nullptr;
-  if (hipMalloc(&t, (size_t)K.nbs * sizeof(dv4)) != hipSuccess) { (void)hipGetLastError(); return; }
+  if (raw_malloc((void**)&t, (size_t)K.nbs * sizeof(dv4), "tmp") != hipSuccess) { (void)hipGetLastError(); return; }
   const size_t bytes = (size_t)K.nbs * sizeof(dv4);
   if (K.split) {   // back to one block per slot first
     if (K.split == 2) unsplit_local_kernel<<<nblocks(K.nbs), 256>>>(K.nbs, K.val, (dv4*)t);
@@ -4801,7 +4893,7 @@ void dev_prereserve(int device, int64_t nnz, int nranks) {
   if (b <= 0 || nnz <= 0) return;
   if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return; }
   const size_t bytes = ((size_t)(b * (double)nnz) + (1 << 21)) & ~(size_t)((1 << 21) - 1);
-  if (hipMalloc(&g_pre, bytes) == hipSuccess) { g_pre_bytes = bytes; g_pre_dev = device; }
+  if (raw_malloc(&g_pre, bytes, "pre") == hipSuccess) { g_pre_bytes = bytes; g_pre_dev = device; }
   else { (void)hipGetLastError(); g_pre = nullptr; }
 }
 void dev_prereserve_release() {
@@ -4809,7 +4901,7 @@ void dev_prereserve_release() {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(g_pre_dev);
-    (void)hipFree(g_pre);
+    (void)raw_free(g_pre);
     (void)hipSetDevice(cur);
   }
   g_pre = nullptr;
@@ -4999,10 +5091,14 @@ void dev_kregion(const DeviceHandle* h, std::vector<double>* ms, int* kept) {
 // and before each apply, so two handles of one problem (which must hold the
 // same bytes wherever they live) name the array that differs
 void debug_sums(DeviceHandle* h, const char* stage, bool konly) {
+#if MAMG_DIAG
   static const bool on = [] {
     const char* e = std::getenv("MAMG_DEBUG_SUMS");
     return e && std::atoi(e) != 0;
   }();
+#else
+  constexpr bool on = false;   // diagnosis build only
+#endif
   if (!on) return;
   // no device-wide sync: the copies below are ordered on the null stream,
   // as every layout-builder step is
@@ -5128,7 +5224,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     PcgGraph q;
     q.x = d_x;
     q.maxiter = maxiter;
-    if (hipMalloc(&q.hist, (3 * (size_t)maxiter + 1) * sizeof(double)) != hipSuccess) {
+    if (raw_malloc((void**)&q.hist, (3 * (size_t)maxiter + 1) * sizeof(double), "long") != hipSuccess) {
       (void)hipGetLastError();
       *err = "PCG history allocation failed";
       return MAMG_ERR_HIP;
@@ -5257,6 +5353,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         q += 2;
       }
   }
+#if MAMG_DIAG
   if (mode == 1 && std::getenv("MAMG_OP_PROFILE")) {
     // diagnosis: event time per (op kind, rows) summed over one apply
     std::map<std::pair<int, int64_t>, std::pair<int, double>> acc;
@@ -5282,14 +5379,14 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
       std::vector<TOp> prog(tp.n);
       std::vector<uint64_t> st(tp.n + 1);
       uint64_t* dst = nullptr;
-      HIPCHK(hipMalloc(&dst, (tp.n + 1) * sizeof(uint64_t)));
+      HIPCHK(raw_malloc((void**)&dst, (tp.n + 1) * sizeof(uint64_t), "tmp"));
       HIPCHK(hipMemcpy(prog.data(), tp.prog, tp.n * sizeof(TOp), hipMemcpyDeviceToHost));
       for (int rep = 0; rep < 2; ++rep)
         if (tp.xl) tail_kernel<true, true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
         else tail_kernel<true, false><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
       HIPCHK(hipStreamSynchronize(s));
       HIPCHK(hipMemcpy(st.data(), dst, (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
-      (void)hipFree(dst);
+      (void)raw_free(dst);
       std::map<std::pair<int, int64_t>, std::pair<int, double>> acc;
       for (int k = 0; k < tp.n; ++k) {
         auto& a = acc[{prog[k].kind, prog[k].n}];
@@ -5309,6 +5406,7 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
                      kv.second.second / kv.second.first);
     }
   }
+#endif  // MAMG_DIAG
   for (auto& e : ev) (void)hipEventDestroy(e);
   return MAMG_OK;
 }
@@ -5435,7 +5533,7 @@ struct DistHandle {
     if (ev_out) (void)hipEventDestroy(ev_out);
     if (last) (void)hipEventDestroy(last);
     if (side) (void)hipStreamDestroy(side);
-    for (void* a : allocs) (void)hipFree(a);
+    for (void* a : allocs) (void)raw_free(a);
     if (comm) (void)ncclCommDestroy(comm);
   }
 };

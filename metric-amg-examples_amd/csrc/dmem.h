@@ -24,10 +24,20 @@
 // Round 3 drained the whole device before every hipFree instead (free-after-
 // drain); DESIGN.md section 4.1 records what the round-4 diagnosis
 // (bench/free_race.hip, scripts/gpu_freediag.sh) measured about hipFree.
-//   MAMG_FREE_MODE=drain   round 3's drain + hipFree (diagnosis only)
+// Diagnosis build only (make diag -> libmamg_diag.so, -DMAMG_DIAG=1; the
+// product library reads none of these):
+//   MAMG_FREE_MODE=drain   round 3's drain + hipFree
 //   MAMG_FREE_MODE=plain   hipMalloc / hipFree with no ordering of our own
-//                          (the round-2 code; diagnosis only)
+//                          (the round-2 code)
+//   MAMG_ALLOC_LOG=<file>  every device allocation and free of the library,
+//                          one line each ("M ptr bytes kind" / "F ptr"),
+//                          replayed by bench/alloc_replay.hip
+//   MAMG_DIAG_CONTIG=1     re-homed streams in physically contiguous
+//                          allocations (rounds 2-4)
 #pragma once
+#ifndef MAMG_DIAG
+#define MAMG_DIAG 0
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -102,9 +112,67 @@ inline hipError_t dev_copy(void* d, const void* src, size_t bytes, hipStream_t s
   return hipGetLastError();
 }
 
-// 0: null-stream ordered (default), 1: drain + hipFree, 2: plain hipFree; read
-// once per process (a block must be freed the way it was allocated)
+// ---- allocation log (diagnosis build) --------------------------------------
+namespace detail {
+inline FILE* alloc_log() {
+#if MAMG_DIAG
+  static FILE* f = [] {
+    const char* e = std::getenv("MAMG_ALLOC_LOG");
+    return e && *e ? std::fopen(e, "w") : (FILE*)nullptr;
+  }();
+  return f;
+#else
+  return nullptr;
+#endif
+}
+inline std::mutex& alloc_log_mu() {
+  static std::mutex m;
+  return m;
+}
+}  // namespace detail
+
+// every device allocation and free of the library goes through these two
+// (kind: tmp = setup temporary, long = handle-owned array, place = re-homed
+// stream, pre = the layout reservation, scratch = scan/sort storage)
+inline hipError_t raw_malloc(void** p, size_t b, const char* kind) {
+  hipError_t e;
+#if MAMG_DIAG
+  static const bool contig = [] {
+    const char* v = std::getenv("MAMG_DIAG_CONTIG");
+    return v && std::atoi(v) == 1;
+  }();
+  if (contig && std::strcmp(kind, "place") == 0) {
+    e = hipExtMallocWithFlags(p, b, hipDeviceMallocContiguous);
+    if (e != hipSuccess) { (void)hipGetLastError(); e = hipMalloc(p, b); }
+  } else {
+    e = hipMalloc(p, b);
+  }
+#else
+  e = hipMalloc(p, b);
+#endif
+  if (FILE* f = detail::alloc_log(); f && e == hipSuccess) {
+    std::lock_guard<std::mutex> g(detail::alloc_log_mu());
+    int d = 0;
+    (void)hipGetDevice(&d);
+    std::fprintf(f, "M %p %zu %s %d\n", *p, b, kind, d);
+    std::fflush(f);
+  }
+  return e;
+}
+inline hipError_t raw_free(void* p) {
+  if (FILE* f = detail::alloc_log(); f && p) {
+    std::lock_guard<std::mutex> g(detail::alloc_log_mu());
+    std::fprintf(f, "F %p\n", p);
+    std::fflush(f);
+  }
+  return hipFree(p);
+}
+
+// 0: null-stream ordered (the product), 1: drain + hipFree, 2: plain
+// hipFree (diagnosis build only); read once per process (a block must be
+// freed the way it was allocated)
 inline int free_mode() {
+#if MAMG_DIAG
   static const int m = [] {
     const char* e = std::getenv("MAMG_FREE_MODE");
     if (e && std::strcmp(e, "drain") == 0) return 1;
@@ -112,28 +180,33 @@ inline int free_mode() {
     return 0;
   }();
   return m;
+#else
+  return 0;
+#endif
 }
 
 namespace detail {
-// hipMalloc'd temporaries of one device: idle blocks by size, and the size
-// of every block the cache made
+// hipMalloc'd setup temporaries: every block the cache made, with its device
+// (so a block freed while another device is current goes back to its own
+// device's idle list), and the idle blocks of each device by size
 struct TmpBlock {
   size_t bytes;
+  int dev;
   bool idle;
 };
 struct TmpCache {
   std::mutex m;
-  std::multimap<size_t, void*> idle;
   std::unordered_map<void*, TmpBlock> made;
+  std::multimap<size_t, void*> idle[64];
 };
-inline TmpCache& tmp_cache_of(int d) {
-  static TmpCache c[64];
-  return c[d & 63];
-}
 inline TmpCache& tmp_cache() {
+  static TmpCache c;
+  return c;
+}
+inline int cur_device() {
   int d = 0;
   (void)hipGetDevice(&d);
-  return tmp_cache_of(d);
+  return d & 63;
 }
 // 4 KiB granules up to 1 MiB, 2 MiB granules above
 inline size_t tmp_round(size_t b) {
@@ -142,81 +215,88 @@ inline size_t tmp_round(size_t b) {
 }
 }  // namespace detail
 
-// hipFree every idle cached block of the current device (after the null
-// stream has drained: the last users of an idle block were queued there)
-inline void tmp_trim() {
+// hipFree every idle cached block of device d (after d's null stream has
+// drained: the last users of an idle block were queued there); the current
+// device is put back
+inline void tmp_trim_dev(int d) {
   auto& c = detail::tmp_cache();
   std::lock_guard<std::mutex> g(c.m);
-  if (c.idle.empty()) return;
+  auto& idle = c.idle[d & 63];
+  if (idle.empty()) return;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
+  if (cur != d && hipSetDevice(d) != hipSuccess) { (void)hipGetLastError(); return; }
   (void)hipStreamSynchronize(nullptr);
-  for (auto& kv : c.idle) {
-    (void)hipFree(kv.second);
+  for (auto& kv : idle) {
+    (void)raw_free(kv.second);
     c.made.erase(kv.second);
   }
-  c.idle.clear();
+  idle.clear();
+  if (cur != d) (void)hipSetDevice(cur);
 }
 
-// tmp_trim on every device whose cache holds idle blocks (the end of a
-// setup: the current device is put back)
+// the current device's idle blocks
+inline void tmp_trim() { tmp_trim_dev(detail::cur_device()); }
+
+// every device's idle blocks (the end of a setup)
 inline void tmp_trim_all() {
-  int cur = -1;
   for (int d = 0; d < 64; ++d) {
     bool any;
     {
-      auto& c = detail::tmp_cache_of(d);
+      auto& c = detail::tmp_cache();
       std::lock_guard<std::mutex> g(c.m);
-      any = !c.idle.empty();
+      any = !c.idle[d].empty();
     }
-    if (!any) continue;
-    if (cur < 0 && hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
-    if (hipSetDevice(d) != hipSuccess) { (void)hipGetLastError(); continue; }
-    tmp_trim();
+    if (any) tmp_trim_dev(d);
   }
-  if (cur >= 0) (void)hipSetDevice(cur);
 }
 
 // hipMalloc for the library's long-lived arrays: when HBM runs out while the
 // setup temporaries' cache holds idle blocks, the cache is emptied and the
 // allocation tried once more
-inline hipError_t dev_malloc(void** p, size_t b) {
-  hipError_t e = hipMalloc(p, b);
+inline hipError_t dev_malloc(void** p, size_t b, const char* kind = "long") {
+  hipError_t e = raw_malloc(p, b, kind);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
     tmp_trim();
-    e = hipMalloc(p, b);
+    e = raw_malloc(p, b, kind);
   }
   return e;
 }
 
 // a setup temporary of b bytes (null-stream ordered): an idle cached block
-// of at most 5/4 of the rounded size, else a new hipMalloc (the idle blocks
-// are released and the allocation tried again when HBM runs out)
+// of the current device of at most 5/4 of the rounded size, else a new
+// hipMalloc (the idle blocks are released and the allocation tried again
+// when HBM runs out)
 inline hipError_t tmp_malloc(void** p, size_t b) {
-  if (free_mode() != 0) return hipMalloc(p, b);
+  if (free_mode() != 0) return raw_malloc(p, b, "tmp");
   auto& c = detail::tmp_cache();
+  const int d = detail::cur_device();
   const size_t r = detail::tmp_round(b);
   {
     std::lock_guard<std::mutex> g(c.m);
-    auto it = c.idle.lower_bound(r);
-    if (it != c.idle.end() && it->first <= r + r / 4) {
+    auto& idle = c.idle[d];
+    auto it = idle.lower_bound(r);
+    if (it != idle.end() && it->first <= r + r / 4) {
       *p = it->second;
-      c.idle.erase(it);
+      idle.erase(it);
       c.made[*p].idle = false;
       return hipSuccess;
     }
   }
-  hipError_t e = hipMalloc(p, r);
+  hipError_t e = raw_malloc(p, r, "tmp");
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
     tmp_trim();
-    e = hipMalloc(p, r);
+    e = raw_malloc(p, r, "tmp");
   }
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.m);
-  c.made[*p] = detail::TmpBlock{r, false};
+  c.made[*p] = detail::TmpBlock{r, d, false};
   return hipSuccess;
 }
 
+// back to the idle list of the block's own device, whatever device is current
 inline void tmp_free(void* p) {
   if (!p) return;
   switch (free_mode()) {
@@ -229,12 +309,21 @@ inline void tmp_free(void* p) {
         break;
       }
       it->second.idle = true;
-      c.idle.emplace(it->second.bytes, p);
+      c.idle[it->second.dev].emplace(it->second.bytes, p);
       break;
     }
-    case 1: (void)hipDeviceSynchronize(); (void)hipFree(p); break;
-    default: (void)hipFree(p); break;
+    case 1: (void)hipDeviceSynchronize(); (void)raw_free(p); break;
+    default: (void)raw_free(p); break;
   }
+}
+
+// cached temporaries of device d: (live, idle) block counts (tests)
+inline void tmp_counts(int d, int64_t* live, int64_t* idle) {
+  auto& c = detail::tmp_cache();
+  std::lock_guard<std::mutex> g(c.m);
+  *live = *idle = 0;
+  for (auto& kv : c.made)
+    if (kv.second.dev == (d & 63)) ++(kv.second.idle ? *idle : *live);
 }
 
 // a hipMalloc'd array whose last reader is queued on the null stream
@@ -251,7 +340,7 @@ inline void ordered_free(void* p) {
   } else if (m == 1) {
     (void)hipDeviceSynchronize();
   }
-  (void)hipFree(p);
+  (void)raw_free(p);
 }
 
 }  // namespace mamg

@@ -46,7 +46,7 @@ void* scratch_get(size_t bytes, hipError_t* e) {
   }
   const size_t n = std::max<size_t>(bytes, (size_t)1 << 20);
   void* p = nullptr;
-  if ((*e = dev_malloc(&p, n)) != hipSuccess) return nullptr;
+  if ((*e = dev_malloc(&p, n, "scratch")) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(g_scratch_mu);
   g_scratch.push_back({dev, p, n, true});
   return p;

@@ -1198,7 +1198,9 @@ int check_ring_seeds(const mamg_params& p, const int32_t* idofs, int64_t n_idofs
     if (idofs[t] < 0 || idofs[t] >= n) { *err = "idofs out of range"; return MAMG_ERR_ARG; }
   if ((double)n_idofs * p.Schwarz_mmsize * p.Schwarz_mmsize > 4e9) {
     *err = "SCHWARZ_RINGS (dense overlapping seed blocks) is for sparse seed sets: " + std::to_string(n_idofs) +
-           " seeds of up to " + std::to_string(p.Schwarz_mmsize) + " dofs";
+           " seeds of up to " + std::to_string(p.Schwarz_mmsize) + " dofs (limit: seeds x Schwarz_mmsize^2 <= 4e9, "
+           "~400k seeds at mmsize 100); with a seed on every node use Schwarz_maxlvl 1 (the node patches, "
+           "SCHWARZ_PATCHES) or the GPU profile (drivers -profile mi355x, parameters_metric_mi355x)";
     return MAMG_ERR_UNSUPPORTED;
   }
   return MAMG_OK;

@@ -18,7 +18,18 @@ def lib_built():
     """Build libmamg.so and the oracle C library once (cross-compiles on CPU)."""
     import subprocess
     so = os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg.so')
-    subprocess.check_call(['make', '-s', '-j8', '-C', os.path.join(ROOT, 'metric-amg-examples_amd', 'csrc')])
+    # the product library and the diagnosis build (same sources, -DMAMG_DIAG=1;
+    # loaded only by child processes that test diagnosis switches)
+    subprocess.check_call(['make', '-s', '-j8', '-C', os.path.join(ROOT, 'metric-amg-examples_amd', 'csrc'),
+                           'all', 'diag'])
     subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
     assert os.path.exists(so)
     return so
+
+
+DIAG_LIB = os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg_diag.so')
+
+
+def diag_loaded():
+    """True when this process loads the diagnosis build (MAMG_LIB)."""
+    return os.path.realpath(os.environ.get('MAMG_LIB', '')) == os.path.realpath(DIAG_LIB)

@@ -27,6 +27,23 @@ def test_exports_every_declared_symbol(lib_built):
         assert s in M._lib.SIGNATURES, 'ctypes prototype missing for %s' % s
 
 
+DIAG_SWITCHES = ('MAMG_DEBUG_SUMS', 'MAMG_K_VARIANT', 'MAMG_TAIL_PROFILE', 'MAMG_OP_PROFILE', 'MAMG_FREE_MODE',
+                 'MAMG_ALLOC_LOG', 'MAMG_DIAG_CONTIG')
+
+
+def test_diagnosis_switches_only_in_the_diag_build(lib_built):
+    """the product library reads none of the diagnosis
+    switches (their names are not even in the binary); the diagnosis build
+    (make diag, -DMAMG_DIAG=1) has them all."""
+    prod = open(lib_built, 'rb').read()
+    for k in DIAG_SWITCHES:
+        assert k.encode() not in prod, k
+    from conftest import DIAG_LIB
+    diag = open(DIAG_LIB, 'rb').read()
+    for k in DIAG_SWITCHES:
+        assert k.encode() in diag, k
+
+
 def test_params_struct_layout(lib_built):
     import metric_amg_examples_amd as M
     p = M.parameters.make_params()

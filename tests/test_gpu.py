@@ -499,6 +499,13 @@ def test_k_block_layouts_bitwise(lib_built, monkeypatch):
     assert rel(zs[1].cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
 
 
+# MAMG_K_VARIANT exists only in the diagnosis build: these run in a child
+# process that loads it (tests/test_gpu_poison.py)
+needs_diag = pytest.mark.skipif(not __import__('conftest').diag_loaded(),
+                                reason='diagnosis build only (MAMG_LIB=libmamg_diag.so; run by test_gpu_poison.py)')
+
+
+@needs_diag
 @pytest.mark.parametrize('variant', ['0', '1', '2'])
 def test_k_kernel_variants(lib_built, monkeypatch, variant):
     """The level-0 K kernel with 2 lanes per row (default), 1 lane (round 2's
@@ -538,6 +545,7 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
         b.close()
 
 
+@needs_diag
 @pytest.mark.parametrize('variant', ['0', '1', '2'])
 def test_k_row_sort_bitwise(lib_built, monkeypatch, variant):
     """Level-0 K with its rows sorted by length inside each SELL slice
