@@ -127,6 +127,8 @@ def main():
     ap.add_argument('--poly-degree', type=int, default=2)
     ap.add_argument('--scaling', type=int, default=0, help='coarse-grid correction scaling (coarse_scaling ON)')
     ap.add_argument('--cycle', choices=('V', 'W'), default='V')
+    ap.add_argument('--dist-graph', type=int, default=1,
+                    help='N > 1 over RCCL: time hipGraph replays of the apply (checked bitwise against eager first)')
     ap.add_argument('--exchange', choices=('rccl', 'gloo'), default='rccl',
                     help='N > 1 transport: RCCL (default), or the host-staged gloo exchange '
                          '(mamg_dist_set_exchange; runs several ranks on one GPU, for rehearsals)')
@@ -257,14 +259,52 @@ def main():
     B.time_apply(r, z, max(1, args.warmup), 0, stream)
     barrier()
 
-    # ---- timed region: K eager applies, events around the dominant kernel
+    # ---- N > 1 over RCCL: the apply replayed from a hipGraph (RCCL calls
+    # inside the capture) when every rank's graph apply is bitwise its eager
+    # apply; otherwise the eager path (the line records which and why)
+    use_graph = False
+    graph_info = None
+    if world > 1 and not gloo and args.dist_graph:
+        # capture on every rank first (nothing launched), agree, then launch:
+        # a graph's RCCL calls wait for every peer's
+        zg = torch.full_like(z, float('nan'))
+        gerr = B.prepare_graph(r, zg) or B.prepare_graph(r, z)
+        captured = allsum(0.0 if gerr is None else 1.0) == 0.0
+        same = False
+        if captured:
+            B.apply_device(r, z, stream)
+            B.apply_graph(r, zg, stream)
+            torch.cuda.synchronize(dev)
+            same = allsum(0.0 if bool(torch.equal(z, zg)) else 1.0) == 0.0
+        use_graph = captured and same
+        graph_info = {'used': use_graph, 'captured_all_ranks': captured, 'bitwise_equal_eager_all_ranks': same,
+                      'rank0_error': gerr}
+        del zg
+        if use_graph:
+            B.time_apply(r, z, max(1, args.warmup), 2, stream)
+        barrier()
+
+    # ---- timed region: K applies (eager with events around the dominant
+    # kernels; N > 1: graph replays when checked above)
     t0 = time.perf_counter()
-    ms_ev, kms, cbytes = B.time_apply(r, z, args.steps, 0, stream)
+    ms_ev, kms, cbytes = B.time_apply(r, z, args.steps, 2 if use_graph else 0, stream)
     barrier()
     wall = allmax(time.perf_counter() - t0)
     ms_per_step = 1e3 * wall / args.steps
     value = args.steps / wall
     apply_bytes = allsum(B.apply_bytes)
+    if use_graph:
+        # the eager path on the same handles, for the record, and its kernel
+        # events (graph replays carry none) for the roofline
+        barrier()
+        t0 = time.perf_counter()
+        _, kms, cbytes = B.time_apply(r, z, args.steps, 0, stream)
+        barrier()
+        wall_e = allmax(time.perf_counter() - t0)
+        graph_info.update(ms_per_step_graph=round(ms_per_step, 4),
+                          ms_per_step_eager=round(1e3 * wall_e / args.steps, 4))
+    elif graph_info is not None:
+        graph_info.update(ms_per_step_graph=None, ms_per_step_eager=round(ms_per_step, 4))
 
     graph_ms = None
     if world == 1:                          # hipGraph replay of the same work
@@ -501,6 +541,7 @@ def main():
         'hbm_GBps_alg': round(apply_bytes / 1e9 / (ms_per_step * 1e-3), 1),
         'apply_GB_alg': round(apply_bytes / 1e9, 4),
         'graph_ms_per_step': graph_ms,
+        'dist_graph': graph_info,
         'roofline': roofline,
         'roofline_kernels': rooflines,
         'level0_format': fmt0,

@@ -19,7 +19,8 @@ in round 3.  --check-host additionally builds the host-source handles and
 checks the two virtual applies bitwise.
 
 With MAMG_DIST_TEST=dry it instead times each rank's cycle with the exchanges
-skipped: the compute part of the P-GPU apply (RCCL latency not included).
+skipped: the compute part of the P-GPU apply (RCCL latency not included),
+eager and as hipGraph replays.
 """
 import argparse
 import json
@@ -95,14 +96,21 @@ def main():
             h.time_apply(rs[p], zs[p], 3, 0)
             ms, _, _ = h.time_apply(rs[p], zs[p], 20, 0)
             ms1, kms, _ = h.time_apply(rs[p], zs[p], 5, 1)
+            h.time_apply(rs[p], zs[p], 3, 2)              # hipGraph replays (captured once)
+            msg, _, _ = h.time_apply(rs[p], zs[p], 20, 2)
             out['per_rank'][p]['compute_ms_per_apply'] = round(ms, 4)
+            out['per_rank'][p]['compute_ms_per_apply_graph'] = round(msg, 4)
             out['per_rank'][p]['classes_ms'] = {k: round(v, 4) for k, v in zip(names, kms) if v}
-            print('rank %d: compute-only %.3f ms/apply %s' % (p, ms, out['per_rank'][p]['classes_ms']),
+            print('rank %d: compute-only %.3f ms/apply eager, %.3f graph %s' % (p, ms, msg, out['per_rank'][p]['classes_ms']),
                   flush=True)
         print(json.dumps(out), flush=True)
         return
     M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    zg = [torch.full_like(x, float('nan')) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)      # the lockstep apply as one hipGraph
     torch.cuda.synchronize()
+    out['graph_equals_eager_bitwise'] = all(bool(torch.equal(a, b)) for a, b in zip(zs, zg))
+    del zg
     nv = s.N // 2
 
     def gather(hs, zs):

@@ -284,10 +284,27 @@ int mamg_dist_apply_bytes(const mamg_dhandle* h, double* bytes);
 int mamg_dist_apply_launches(const mamg_dhandle* h, int64_t counts[5]);
 int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r_local, double* d_z_local,
                            void* stream);
+/* The same apply replayed from a hipGraph: captured on the first call per
+ * (d_r_local, d_z_local) pair, with the rank's kernels, the interior-row
+ * side-stream fork and the RCCL send / receive groups and all-reduces inside
+ * the capture, then one hipGraphLaunch per call on `stream`.  Bitwise the
+ * eager apply's result (same kernels, same order).  MAMG_ERR_UNSUPPORTED for
+ * a handle without an RCCL communicator and more than one rank (host-staged
+ * or virtual exchanges) and after a failed capture on the handle (the message
+ * names the capture error; mamg_dist_apply_device stays available).  No
+ * reference counterpart (the reference is serial). */
+int mamg_dist_apply_graph(mamg_dhandle* h, const double* d_r_local, double* d_z_local, void* stream);
+/* Capture (or find) that graph without launching it: every rank can capture
+ * and agree on the outcome before any rank launches a graph whose RCCL calls
+ * wait for its peers. */
+int mamg_dist_graph_prepare(mamg_dhandle* h, const double* d_r_local, double* d_z_local);
 /* y = A x on the rank's rows (the PCG operator; x, y local field-major
  * slices): forward halo of x, then the rank-local A.  Replaces the A * d
  * product inside cbc.block ConjGrad (src/bidomain_3d.py:149) on N GPUs. */
 int mamg_dist_spmv_device(mamg_dhandle* h, const double* d_x_local, double* d_y_local, void* stream);
+/* mode 0: eager, events around the level-0 residual and K launches; 1:
+ * eager, events around every op; 2: mamg_dist_apply_graph replays (events
+ * around the whole run only, kernel_ms zero) */
 int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int reps, int mode,
                          double* ms_per_apply, double* kernel_ms, double* class_bytes,
                          void* stream);
@@ -296,6 +313,10 @@ int mamg_dist_time_apply(mamg_dhandle* h, const double* d_r, double* d_z, int re
 int mamg_dist_virtual_apply(mamg_dhandle** hs, int n, const double** d_r, double** d_z,
                             void* stream);
 int mamg_dist_virtual_spmv(mamg_dhandle** hs, int n, const double** d_x, double** d_y, void* stream);
+/* The virtual ranks' lockstep apply captured into one hipGraph and replayed
+ * once (tests: the graph path against the eager lockstep run). */
+int mamg_dist_virtual_apply_graph(mamg_dhandle** hs, int n, const double** d_r, double** d_z,
+                                  void* stream);
 void mamg_dist_destroy(mamg_dhandle* h);
 /* Host-staged exchange backend: a pluggable transport for a handle made
  * with comm_id == NULL (one process per rank, e.g. torch.distributed gloo).

@@ -101,6 +101,9 @@ SIGNATURES = {
     'mamg_dist_apply_bytes': (C.c_int, [VP, P_F64]),
     'mamg_dist_apply_launches': (C.c_int, [VP, C.POINTER(C.c_int64)]),
     'mamg_dist_apply_device': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_dist_apply_graph': (C.c_int, [VP, VP, VP, VP]),
+    'mamg_dist_graph_prepare': (C.c_int, [VP, VP, VP]),
+    'mamg_dist_virtual_apply_graph': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
     'mamg_dist_time_apply': (C.c_int, [VP, VP, VP, C.c_int, C.c_int, P_F64, P_F64, P_F64, VP]),
     'mamg_dist_virtual_apply': (C.c_int, [C.POINTER(VP), C.c_int, C.POINTER(VP), C.POINTER(VP), VP]),
     'mamg_dist_spmv_device': (C.c_int, [VP, VP, VP, VP]),

@@ -643,7 +643,24 @@ class DistMetricAMG:
                                                   _stream_ptr(stream)))
         return z
 
+    def apply_graph(self, r, z, stream=None):
+        """The apply replayed from a hipGraph (mamg_dist_apply_graph: captured
+        on first use per (r, z), RCCL calls inside the capture).  Raises
+        MamgError (MAMG_ERR_UNSUPPORTED) for host-staged / virtual exchanges
+        or after a failed capture; apply_device stays the eager path."""
+        _lib.check(self._L.mamg_dist_apply_graph(self._h, _device_ptr(r), _device_ptr(z), _stream_ptr(stream)))
+        return z
+
+    def prepare_graph(self, r, z):
+        """Capture (or find) the apply's hipGraph for (r, z) without launching
+        it (mamg_dist_graph_prepare).  Returns None on success, else the
+        library's message (the handle then stays eager)."""
+        rc = self._L.mamg_dist_graph_prepare(self._h, _device_ptr(r), _device_ptr(z))
+        return None if rc == 0 else self._L.mamg_last_error().decode(errors='replace')
+
     def time_apply(self, r, z, reps, mode=0, stream=None):
+        """mode 0: eager, events around the level-0 residual and K; 1: eager,
+        events around every op; 2: graph replays (kernel_ms zero)."""
         ms = C.c_double()
         kms = (C.c_double * 16)()
         cb = (C.c_double * 16)()
@@ -667,12 +684,15 @@ class DistMetricAMG:
         _lib.check(_lib.lib().mamg_dist_virtual_spmv(H, n, X, Y, _stream_ptr(stream)))
 
     @staticmethod
-    def virtual_apply(handles, rs, zs, stream=None):
+    def virtual_apply(handles, rs, zs, stream=None, graph=False):
+        """graph=True: the lockstep apply captured into one hipGraph and
+        replayed (mamg_dist_virtual_apply_graph)."""
         n = len(handles)
         H = (C.c_void_p * n)(*[h._h.value for h in handles])
         R = (C.c_void_p * n)(*[_device_ptr(r).value for r in rs])
         Z = (C.c_void_p * n)(*[_device_ptr(z).value for z in zs])
-        _lib.check(_lib.lib().mamg_dist_virtual_apply(H, n, R, Z, _stream_ptr(stream)))
+        f = _lib.lib().mamg_dist_virtual_apply_graph if graph else _lib.lib().mamg_dist_virtual_apply
+        _lib.check(f(H, n, R, Z, _stream_ptr(stream)))
 
     def close(self):
         if getattr(self, '_h', None):

@@ -492,6 +492,28 @@ int mamg_dist_apply_device(mamg_dhandle* h, const double* d_r, double* d_z, void
   DEV_CALL(mamg::dist_apply(h->d, d_r, d_z, stream, &err))
 }
 
+int mamg_dist_apply_graph(mamg_dhandle* h, const double* d_r, double* d_z, void* stream) {
+  DEV_CALL(mamg::dist_apply_graph(h->d, d_r, d_z, stream, &err))
+}
+
+int mamg_dist_graph_prepare(mamg_dhandle* h, const double* d_r, double* d_z) {
+  DEV_CALL(mamg::dist_graph_prepare(h->d, d_r, d_z, &err))
+}
+
+int mamg_dist_virtual_apply_graph(mamg_dhandle** hs, int n, const double** d_r, double** d_z, void* stream) {
+  GUARD_BEGIN
+  if (!hs || n < 1 || !d_r || !d_z) { set_error("null argument"); return MAMG_ERR_ARG; }
+  std::vector<mamg::DistHandle*> H(n);
+  std::vector<const double*> R(d_r, d_r + n);
+  std::vector<double*> Z(d_z, d_z + n);
+  for (int i = 0; i < n; ++i) H[i] = hs[i]->d;
+  std::string err;
+  int rc = mamg::dist_virtual_apply_graph(H, R, Z, stream, &err);
+  if (rc) set_error(err);
+  return rc;
+  GUARD_END
+}
+
 int mamg_dist_spmv_device(mamg_dhandle* h, const double* d_x, double* d_y, void* stream) {
   DEV_CALL(mamg::dist_spmv(h->d, d_x, d_y, stream, &err))
 }

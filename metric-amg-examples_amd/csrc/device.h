@@ -67,5 +67,13 @@ int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int
 int dist_set_exchange(DistHandle* h, const mamg_exchange& ex, std::string* err);
 int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
                        const std::vector<double*>& z, void* stream, std::string* err);
+// the apply replayed from a hipGraph captured on first use per (r, z) (RCCL
+// calls inside the capture); MAMG_ERR_UNSUPPORTED for host-staged / virtual
+// exchanges or after a failed capture (then the eager dist_apply)
+int dist_apply_graph(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err);
+// capture (or find) the graph of (r, z) without launching it
+int dist_graph_prepare(DistHandle* h, const double* d_r, double* d_z, std::string* err);
+int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
+                             const std::vector<double*>& z, void* stream, std::string* err);
 
 }  // namespace mamg

@@ -1451,10 +1451,17 @@ __global__ __launch_bounds__(FIND ? 1024 : 256) void pkey_refresh_kernel(
     const bool unc = c[I] < 0;
     uint64_t v = m[I];
     if ((!FIND || unc) && v != 0 && c[(uint32_t)v] >= 0) {   // its maximum was coloured: recompute
+      // rows hold <= PATCH_MAX_NODES columns (build_patches checks): every
+      // column load, then every gather, in flight together
       v = src ? src[I] : (unc ? patch_key_dev(I) : 0ull);
-      for (int64_t k = ptr[I]; k < ptr[I + 1]; ++k) {
-        const int64_t J = col[k];
-        const uint64_t u = src ? src[J] : (c[J] < 0 ? patch_key_dev(J) : 0ull);
+      const int64_t k0 = ptr[I];
+      const int len = (int)(ptr[I + 1] - k0);
+      int32_t J[PATCH_MAX_NODES];
+#pragma unroll
+      for (int q = 0; q < PATCH_MAX_NODES; ++q) J[q] = q < len ? col[k0 + q] : (int32_t)I;
+#pragma unroll
+      for (int q = 0; q < PATCH_MAX_NODES; ++q) {
+        const uint64_t u = src ? src[J[q]] : (c[J[q]] < 0 ? patch_key_dev(J[q]) : 0ull);
         v = u > v ? u : v;
       }
       m[I] = v;
@@ -5527,7 +5534,29 @@ struct DistHandle {
   std::vector<double*> hsend, hghost, hrecv;
   double* hred = nullptr;
   std::vector<void*> pinned;
+  // the apply replayed as a hipGraph (dist_apply_graph): one per (r, z) pair,
+  // captured on `cap` with the RCCL calls inside; graph_err set when a
+  // capture failed (the handle then stays eager)
+  struct Graph {
+    const double* r;
+    double* z;
+    hipGraph_t g;
+    hipGraphExec_t e;
+  };
+  std::vector<Graph> graphs;
+  hipStream_t cap = nullptr;
+  std::string graph_err;
+  void drop_graphs() {
+    for (auto& g : graphs) {
+      (void)hipGraphExecDestroy(g.e);
+      (void)hipGraphDestroy(g.g);
+    }
+    graphs.clear();
+  }
   ~DistHandle() {
+    if (last) (void)hipEventSynchronize(last);
+    drop_graphs();
+    if (cap) (void)hipStreamDestroy(cap);
     for (void* q : pinned) (void)hipHostFree(q);
     if (ev_in) (void)hipEventDestroy(ev_in);
     if (ev_out) (void)hipEventDestroy(ev_out);
@@ -5886,10 +5915,13 @@ int run_dop(DistHandle* h, const DOp& d, hipStream_t s, std::string* err) {
     launch(d.op, s);
     return MAMG_OK;
   }
-  if (h->nranks == 1) {                 // no peers: halos empty, sums over one rank
+  if (h->nranks == 1 && !h->comm) {     // no peers: halos empty, sums over one rank
     if (d.dk == D_OVERLAP) launch(d.op, s);
     return MAMG_OK;
   }
+  // (a 1-rank RCCL communicator takes the RCCL path below: empty send /
+  // receive groups, an all-reduce over one rank, the side-stream fork; the
+  // one-GPU tests exercise those calls, eager and inside a graph capture)
   if (!h->comm && h->dry) {            // compute-only timing of one rank (results meaningless)
     if (d.dk == D_OVERLAP) launch(d.op, s);
     return MAMG_OK;
@@ -6589,6 +6621,80 @@ int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::
   return dist_mark(h, (hipStream_t)stream, err);
 }
 
+// The op list of one apply captured into a hipGraph on the handle's capture
+// stream: kernels, the side-stream fork of the interior rows (events), and
+// the RCCL send / receive groups and all-reduces inside the capture.  A
+// failed capture leaves nothing behind and is reported (the caller stays
+// eager).
+int dist_capture(DistHandle* h, const std::vector<DOp>& ops, hipGraph_t* gr, hipGraphExec_t* ex, std::string* err) {
+  *gr = nullptr;
+  *ex = nullptr;
+  if (!h->cap) HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
+  HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
+  int rc = MAMG_OK;
+  for (const DOp& d : ops)
+    if ((rc = run_dop(h, d, h->cap, err))) break;
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->cap, &g);
+  if (rc || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (!rc) *err = std::string("stream capture of the distributed apply: ") + hipGetErrorString(e);
+    return rc ? rc : MAMG_ERR_HIP;
+  }
+  const hipError_t ei = hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
+  if (ei != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    *err = std::string("hipGraphInstantiate of the distributed apply: ") + hipGetErrorString(ei);
+    return MAMG_ERR_HIP;
+  }
+  *gr = g;
+  return MAMG_OK;
+}
+
+int dist_graph_exec(DistHandle* h, const double* d_r, double* d_z, hipGraphExec_t* ex, std::string* err) {
+  if (!h->comm && h->nranks > 1 && !h->dry) {
+    *err = "graph replay needs an RCCL communicator (or one rank): host-staged and virtual exchanges run eagerly";
+    return MAMG_ERR_UNSUPPORTED;
+  }
+  if (!h->graph_err.empty()) { *err = "graph capture failed on this handle: " + h->graph_err; return MAMG_ERR_UNSUPPORTED; }
+  for (auto& g : h->graphs)
+    if (g.r == d_r && g.z == d_z) { *ex = g.e; return MAMG_OK; }
+  if (h->graphs.size() >= 16) {   // evict the oldest once every launch on the handle finished
+    if (h->last) HIPCHK(hipEventSynchronize(h->last));
+    (void)hipGraphExecDestroy(h->graphs.front().e);
+    (void)hipGraphDestroy(h->graphs.front().g);
+    h->graphs.erase(h->graphs.begin());
+  }
+  std::vector<DOp> ops;
+  dapply_ops(h, d_r, d_z, &ops);
+  DistHandle::Graph g{d_r, d_z, nullptr, nullptr};
+  const int rc = dist_capture(h, ops, &g.g, &g.e, err);
+  if (rc) {
+    h->graph_err = *err;
+    return rc;
+  }
+  h->graphs.push_back(g);
+  *ex = g.e;
+  return MAMG_OK;
+}
+
+int dist_graph_prepare(DistHandle* h, const double* d_r, double* d_z, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  hipGraphExec_t ex = nullptr;
+  return dist_graph_exec(h, d_r, d_z, &ex, err);
+}
+
+int dist_apply_graph(DistHandle* h, const double* d_r, double* d_z, void* stream, std::string* err) {
+  HIPCHK(hipSetDevice(h->device));
+  hipGraphExec_t ex = nullptr;
+  const int rc = dist_graph_exec(h, d_r, d_z, &ex, err);
+  if (rc) return rc;
+  HIPCHK(hipGraphLaunch(ex, (hipStream_t)stream));
+  return dist_mark(h, (hipStream_t)stream, err);
+}
+
 int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int mode, double* ms,
                     double* kernel_ms, double* class_bytes, void* stream, std::string* err) {
   HIPCHK(hipSetDevice(h->device));
@@ -6600,6 +6706,26 @@ int dist_time_apply(DistHandle* h, const double* d_r, double* d_z, int reps, int
     for (const DOp& d : ops) class_bytes[d.cls] += d.bytes;
   }
   if (reps <= 0) { *ms = 0.0; return MAMG_OK; }
+  if (mode == 2) {   // graph replays, events around the whole run only
+    hipGraphExec_t ex = nullptr;
+    int rc = dist_graph_exec(h, d_r, d_z, &ex, err);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int rp = 0; rp < reps; ++rp) HIPCHK(hipGraphLaunch(ex, s));
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, e0, e1));
+    *ms = t / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (kernel_ms)
+      for (int c = 0; c < 16; ++c) kernel_ms[c] = 0.0;
+    return dist_mark(h, s, err);
+  }
   std::vector<int> inst;
   for (size_t k = 0; k < ops.size(); ++k)
     if (mode == 1 || ops[k].cls == C_L0_RESID || ops[k].cls == C_L0_SMOOTH) inst.push_back((int)k);
@@ -6655,7 +6781,7 @@ __global__ __launch_bounds__(256) void vsum_kernel(int64_t n, const double* __re
 
 // P ranks' op lists in lockstep on one stream
 int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vector<DOp>>& ops, hipStream_t s,
-                std::string* err) {
+                std::string* err, bool mark = true) {
   const int P = (int)hs.size();
   for (int p = 1; p < P; ++p)
     if (ops[p].size() != ops[0].size()) { *err = "rank schedules differ"; return MAMG_ERR_SETUP; }
@@ -6742,10 +6868,11 @@ int virtual_run(const std::vector<DistHandle*>& hs, const std::vector<std::vecto
     }
   }
   HIPCHK(hipGetLastError());
-  for (DistHandle* h : hs) {
-    const int rc = dist_mark(h, s, err);
-    if (rc) return rc;
-  }
+  if (mark)
+    for (DistHandle* h : hs) {
+      const int rc = dist_mark(h, s, err);
+      if (rc) return rc;
+    }
   return MAMG_OK;
 }
 
@@ -6791,6 +6918,47 @@ int dist_virtual_apply(const std::vector<DistHandle*>& hs, const std::vector<con
   std::vector<std::vector<DOp>> ops(P);
   for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
   return virtual_run(hs, ops, (hipStream_t)stream, err);
+}
+
+// the virtual ranks' lockstep apply captured into one hipGraph (rank 0's
+// capture stream), launched once and destroyed: the graph path's kernels,
+// forks and exchange order, checked bitwise against the eager lockstep run
+int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vector<const double*>& r,
+                             const std::vector<double*>& z, void* stream, std::string* err) {
+  const int P = (int)hs.size();
+  HIPCHK(hipSetDevice(hs[0]->device));
+  std::vector<std::vector<DOp>> ops(P);
+  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
+  DistHandle* h0 = hs[0];
+  if (!h0->cap) HIPCHK(hipStreamCreateWithFlags(&h0->cap, hipStreamNonBlocking));
+  HIPCHK(hipStreamBeginCapture(h0->cap, hipStreamCaptureModeThreadLocal));
+  int rc = virtual_run(hs, ops, h0->cap, err, false);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h0->cap, &g);
+  if (rc || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (!rc) *err = std::string("stream capture of the virtual apply: ") + hipGetErrorString(e);
+    return rc ? rc : MAMG_ERR_HIP;
+  }
+  hipGraphExec_t ex = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  if (ei != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    *err = std::string("hipGraphInstantiate of the virtual apply: ") + hipGetErrorString(ei);
+    return MAMG_ERR_HIP;
+  }
+  const hipError_t el = hipGraphLaunch(ex, (hipStream_t)stream);
+  const hipError_t es = hipStreamSynchronize((hipStream_t)stream);
+  (void)hipGraphExecDestroy(ex);
+  (void)hipGraphDestroy(g);
+  if (el != hipSuccess || es != hipSuccess) {
+    *err = std::string("virtual apply graph launch: ") + hipGetErrorString(el != hipSuccess ? el : es);
+    return MAMG_ERR_HIP;
+  }
+  for (DistHandle* h : hs)
+    if ((rc = dist_mark(h, (hipStream_t)stream, err))) return rc;
+  return MAMG_OK;
 }
 
 int dist_virtual_spmv(const std::vector<DistHandle*>& hs, const std::vector<const double*>& x,

@@ -34,6 +34,11 @@
 //                          replayed by bench/alloc_replay.hip
 //   MAMG_DIAG_CONTIG=1     re-homed streams in physically contiguous
 //                          allocations (rounds 2-4)
+//   MAMG_DEBUG_PTRS=1      every setup temporary checked, when handed out,
+//                          to be the start of a live runtime allocation at
+//                          least as large (hipMemGetAddressRange), and the
+//                          transpose's sort permutation checked before the
+//                          gather that indexes with it (gsetup.hip)
 #pragma once
 #ifndef MAMG_DIAG
 #define MAMG_DIAG 0
@@ -168,6 +173,33 @@ inline hipError_t raw_free(void* p) {
   return hipFree(p);
 }
 
+// diagnosis build: MAMG_DEBUG_PTRS checks (false in the product)
+inline bool debug_ptrs() {
+#if MAMG_DIAG
+  static const bool on = [] {
+    const char* e = std::getenv("MAMG_DEBUG_PTRS");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+#else
+  return false;
+#endif
+}
+
+// p must start a live runtime allocation of at least b bytes
+inline void check_block(const void* p, size_t b, const char* what) {
+  if (!debug_ptrs() || !p) return;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  const hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p);
+  if (e != hipSuccess || base != (hipDeviceptr_t)p || size < b) {
+    (void)hipGetLastError();
+    std::fprintf(stderr, "[mamg debug] %s %p (%zu B): %s, allocation base %p size %zu\n", what, p, b,
+                 e != hipSuccess ? hipGetErrorString(e) : "not the start of a large enough allocation", (void*)base,
+                 size);
+  }
+}
+
 // 0: null-stream ordered (the product), 1: drain + hipFree, 2: plain
 // hipFree (diagnosis build only); read once per process (a block must be
 // freed the way it was allocated)
@@ -281,6 +313,7 @@ inline hipError_t tmp_malloc(void** p, size_t b) {
       *p = it->second;
       idle.erase(it);
       c.made[*p].idle = false;
+      check_block(*p, r, "tmp_malloc (cached)");
       return hipSuccess;
     }
   }
@@ -291,6 +324,7 @@ inline hipError_t tmp_malloc(void** p, size_t b) {
     e = raw_malloc(p, r, "tmp");
   }
   if (e != hipSuccess) return e;
+  check_block(*p, r, "tmp_malloc (new)");
   std::lock_guard<std::mutex> g(c.m);
   c.made[*p] = detail::TmpBlock{r, d, false};
   return hipSuccess;

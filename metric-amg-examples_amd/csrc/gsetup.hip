@@ -1591,6 +1591,22 @@ int transpose(GHier* G, const DevMat& P, DevMat* R, std::string* err) {
   int bits = 1;
   while ((int64_t(1) << bits) < P.m && bits < 32) ++bits;
   RCHK(dsort_pairs_i32_i64(P.col, keys, idx, perm, nnz, bits, nullptr, err));
+  if (debug_ptrs()) {   // diagnosis build: the gather below indexes with perm
+    for (const void* q : {(const void*)perm, (const void*)rowof, (const void*)P.val, (const void*)R->col,
+                          (const void*)R->val})
+      check_block(q, 1, "transpose operand");
+    std::vector<int64_t> hp(nnz);
+    RCHK(to_host(hp.data(), perm, nnz, err));
+    std::vector<char> seen(nnz, 0);
+    for (int64_t d = 0; d < nnz; ++d) {
+      if (hp[d] < 0 || hp[d] >= nnz || seen[hp[d]]) {
+        *err = "debug: the transpose's sort permutation is not a permutation (entry " + std::to_string(d) + " = " +
+               std::to_string(hp[d]) + ")";
+        return MAMG_ERR_SETUP;
+      }
+      seen[hp[d]] = 1;
+    }
+  }
   transpose_gather_kernel<<<nblk(nnz), 256>>>(nnz, perm, rowof, P.val, R->col, R->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;

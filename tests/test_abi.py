@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol(lib_built):
 
 
 DIAG_SWITCHES = ('MAMG_DEBUG_SUMS', 'MAMG_K_VARIANT', 'MAMG_TAIL_PROFILE', 'MAMG_OP_PROFILE', 'MAMG_FREE_MODE',
-                 'MAMG_ALLOC_LOG', 'MAMG_DIAG_CONTIG')
+                 'MAMG_ALLOC_LOG', 'MAMG_DIAG_CONTIG', 'MAMG_DEBUG_PTRS')
 
 
 def test_diagnosis_switches_only_in_the_diag_build(lib_built):

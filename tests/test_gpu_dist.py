@@ -260,6 +260,65 @@ def test_single_rank_rccl(lib_built):
     d.close()
 
 
+def test_single_rank_rccl_graph(lib_built):
+    """the distributed apply replayed from a hipGraph with the
+    RCCL calls inside the capture (a 1-rank communicator: empty send/receive
+    groups, the all-reduces of coarse scaling, the side-stream fork of the
+    interior rows) is bitwise the eager apply, replay after replay."""
+    import torch
+    import metric_amg_examples_amd as M
+    s = M.problems.bidomain(3, 16, 1e4)
+    r = mo.seeded_rhs(s.N)
+    for kw in (dict(), dict(smoother=11, coarse_scaling=1, cycle_type=2, Schwarz_type=7)):
+        d = M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=0, nranks=1, comm_id=M.DistMetricAMG.unique_id(),
+                            rep_nodes=100, num_functions=2, **kw)
+        st = torch.cuda.current_stream()
+        rt = torch.as_tensor(d.local_slice(r)).cuda()
+        ze, zg = torch.zeros_like(rt), torch.full_like(rt, float('nan'))
+        d.apply_device(rt, ze, st)
+        d.apply_graph(rt, zg, st)
+        torch.cuda.synchronize()
+        assert torch.equal(ze, zg)
+        zg.fill_(float('nan'))
+        ms, _, _ = d.time_apply(rt, zg, 3, 2, st)       # graph replays
+        torch.cuda.synchronize()
+        assert ms > 0 and torch.equal(ze, zg)
+        h = mo.setup(s.scipy(), mo.Params(num_functions=2, **({} if not kw else dict(
+            smoother='SGS', coarse_scaling=1, cycle_type='W', Schwarz_type=7))), idofs=s.idofs)
+        zo = h.apply(r)
+        assert np.linalg.norm(ze.cpu().numpy() - zo) / np.linalg.norm(zo) < 1e-10
+        d.close()
+
+
+@pytest.mark.parametrize('P,kw', [(2, {}), (3, dict(smoother=11, coarse_scaling=1, cycle_type=2, Schwarz_type=7)),
+                                  (8, dict(smoother=12))])
+def test_virtual_ranks_graph_bitwise(lib_built, monkeypatch, P, kw):
+    """The virtual ranks' lockstep apply captured into one hipGraph (every
+    rank's kernels, halo packs, device-copy exchanges, reverse-adds and
+    all-reduce sums) is bitwise the eager lockstep apply: Jacobi (the
+    overlap split of the half-symmetric A), SGS + scaling + W (colour halos,
+    all-reduces), POLY at P = 8."""
+    import torch
+    import metric_amg_examples_amd as M
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(3, 16, 1e6)
+    r = mo.seeded_rhs(s.N)
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
+                          num_functions=2, **kw) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    ze = [torch.zeros_like(x) for x in rs]
+    zg = [torch.full_like(x, float('nan')) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, ze)
+    M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)
+    torch.cuda.synchronize()
+    for a, b in zip(ze, zg):
+        assert torch.equal(a, b)
+    for hh in hs:
+        with pytest.raises(M._lib.MamgError):      # no communicator: the graph path is refused
+            hh.apply_graph(rs[0], zg[0])
+        hh.close()
+
+
 @pytest.mark.parametrize('P', [2, 4])
 def test_virtual_ranks_half_bitwise(lib_built, monkeypatch, P):
     """Rank-local level-0 A in the half-symmetric format (owned part through
