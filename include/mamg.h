@@ -94,7 +94,10 @@ enum {                                                   /* Schwarz_type      */
   MAMG_SCHWARZ_SEED_BLOCKS = 7,
   /* symmetric multiplicative Schwarz on one block per seed = the seed and its
      breadth-first Schwarz_maxlvl ring (<= Schwarz_mmsize dofs), exact local
-     solves, blocks in a greedy conflict-colour order, plus node-block GS on
+     solves, blocks in a greedy conflict-colour order (a substitution for
+     HAZmath's sequential seed order: the same blocks and local solves in
+     another multiplicative order; the oracle's seed-order sweep gives the
+     same EMI PCG counts, tests/test_rings_oracle.py), plus node-block GS on
      the dofs in no block (src/utils.py:84: "the interface_dofs has the
      Schwarz and the rest the GS smoother"): the reference's SCHWARZ_SYMMETRIC
      for any seed set that is not one seed per node with 1-rings (EMI's

@@ -3469,6 +3469,10 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   const mamg_params& p = h->p;
   if (!S.seeds || S.seeds->empty()) { *err = "seed rings: no seeds"; return MAMG_ERR_ARG; }
   const int64_t n = S.A.n, nv = n / 2, ns = (int64_t)S.seeds->size();
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms_since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
   RingBlocks RB;
   int rc = ring_blocks_dev(S.A, S.seeds->data(), ns, p.Schwarz_maxlvl, p.Schwarz_mmsize, &RB, err);
   if (rc) return rc;
@@ -3490,10 +3494,18 @@ int build_rings(DeviceHandle* h, TmpPool* T, const TBsr& B, const LevelSrc& S, D
   CsrView Av;
   Av.n = Av.m = n; Av.ptr = aptr.data(); Av.col = acol.data();
   std::vector<int32_t> colour;
+  const double t_blocks = ms_since(t0);
+  const auto t1 = std::chrono::steady_clock::now();
   ring_colouring(Av, bptr, mem, &colour);
+  const double t_colour = ms_since(t1);
   std::vector<int32_t>().swap(acol);
   int ncol = 0;
   for (int32_t c : colour) ncol = std::max(ncol, c + 1);
+  if (p.print_level >= 1)   // what the seed rings cost at the drivers' sizes
+    std::fprintf(stderr, "[mamg] seed rings: %lld blocks, %lld member dofs (max %d per block), %d colours, "
+                 "blocks + inverses %.1f ms, host colouring %.1f ms, %.3f GB of inverses\n",
+                 (long long)ns, (long long)bptr[ns], mm, ncol, t_blocks, t_colour,
+                 [&] { double q = 0; for (int64_t k = 0; k < ns; ++k) q += (double)blen[k] * blen[k]; return 8e-9 * q; }());
   std::vector<int32_t> ord(ns);
   std::iota(ord.begin(), ord.end(), 0);
   std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return colour[a] < colour[b]; });

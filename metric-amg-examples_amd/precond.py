@@ -122,10 +122,25 @@ def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs
     """Plain (non-metric) AMG on the monolithic matrix (src/utils.py:15-42):
     no interface seeds.  ``parameters`` None -> the reference's default dict
     (src/utils.py:20-38, ``parameters.parameters_amg_default``: UA + VMB + W +
-    SGS + scaling); ``num_functions`` from W as for metricAMG."""
+    SGS + scaling).
+
+    Substitution: the reference's AMGhaz (src/utils.py:40) never
+    receives W, so HAZmath aggregates point-wise there.  Here W, when given,
+    makes the hierarchy nodal (num_functions = the number of equal blocks:
+    nodal aggregation and node-block SGS, the only SGS this build has);
+    ``num_functions=1`` gives point-wise aggregation with a point smoother
+    (SGS then needs a Jacobi-family ``smoother``).  The choice is recorded in
+    ``.substitutions`` instead of a warning on every call."""
+    import warnings
     params = dict(P.parameters_amg_default) if parameters is None else dict(parameters)
     params['Schwarz_levels'] = 0
-    return MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore', UserWarning)
+        B = MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
+    B.substitutions = [n for n in getattr(B, 'notes', [])] + (
+        ['nodal hierarchy from W (the reference AMGhaz gets no W: point-wise aggregation there)']
+        if B.params.num_functions > 1 and 'num_functions' not in kw and 'num_functions' not in params else [])
+    return B
 
 
 def solve_haznics(A, b, W, interface_dofs=None, parameters=None, tolerance=1e-8, maxiter=500):

@@ -1170,6 +1170,21 @@ class Rings:
         self.cov = np.zeros(n, dtype=bool)
         for b in self.blocks:
             self.cov[b] = True
+        self.seed_order = False      # True: sweep_seed_order (HAZmath's order) in the cycle
+
+    def sweep_seed_order(self, A: sp.csr_matrix, x: np.ndarray, b: np.ndarray, forward=True):
+        """HAZmath's order (SCHWARZ_SYMMETRIC, recalled): the blocks one at a
+        time in seed order (forward) or reverse seed order (backward), each
+        block's residual taken after every earlier block's update.  The GPU
+        runs the colour order of ``sweep`` instead (a substitution: the same
+        blocks and local solves, another multiplicative order); this one is
+        the oracle's reference for that difference (tests/test_rings_oracle.py)."""
+        ks = range(len(self.blocks)) if forward else range(len(self.blocks) - 1, -1, -1)
+        A = A.tocsr()
+        for k in ks:
+            blk = self.blocks[k]
+            x[blk] += self.Minv[k] @ (b[blk] - A[blk] @ x)
+        return x
 
     def sweep(self, A: sp.csr_matrix, x: np.ndarray, b: np.ndarray, forward=True):
         """x <- x + Minv_k (b - A x)|_k for the blocks of each colour in turn
@@ -1320,10 +1335,11 @@ class Hierarchy:
     def rings_step(lev, x, b):
         """One symmetric level-0 step of Schwarz_type RINGS: ring sweep
         forward, rest GS forward and backward, ring sweep backward."""
-        x = lev.rings.sweep(lev.A, x, b, True)
+        sw = lev.rings.sweep_seed_order if lev.rings.seed_order else lev.rings.sweep
+        x = sw(lev.A, x, b, True)
         x = lev.gs_sweep(x, b, True)
         x = lev.gs_sweep(x, b, False)
-        return lev.rings.sweep(lev.A, x, b, False)
+        return sw(lev.A, x, b, False)
 
     def apply(self, r: np.ndarray) -> np.ndarray:
         """z = B r: ``maxit`` cycles (src/amg_parameters.py:71), x0 = 0."""

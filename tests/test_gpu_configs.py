@@ -310,3 +310,42 @@ def test_emi_3d1d_sweep_two_processes(lib_built):
         say('sweep radius', radius, 'gamma', g, 'rank', row['rank'], 'its', row['niters'], 'oracle', n_or)
         assert row['niters'] == n_or
         assert row['relres'] <= 1e-6
+
+
+def test_bidomain_2d_config1_reference_cli(lib_built, tmp_path):
+    """BASELINE config 1 through the reference's own command line
+    (`bidomain_2d.py -nrefs 3 -gamma 1 -precond metric_mono`):
+    the driver's mesh loop n = 32, 64, 128 (src/bidomain_2d.py:168) with the
+    preset the reference's driver passes (parameters_metric_schwarz, src/
+    bidomain_3d.py:144-147: UA + HEM + W + SGS + scaling + the level-0 node
+    patches) and the manufactured right-hand side.  On every mesh the GPU PCG
+    iteration count equals the oracle's restatement of that algorithm on the
+    same right-hand side, and the iters file has the reference's schema."""
+    import importlib
+    M = _M()
+    D = importlib.import_module('metric_amg_examples_amd.drivers')
+    P = M.parameters
+    rows = D.bidomain(['-nrefs', '3', '-gamma', '1', '-precond', 'metric_mono', '-results', str(tmp_path)], 2)
+    assert [r[0] for r in rows] == [2 * 33 ** 2, 2 * 65 ** 2, 2 * 129 ** 2]
+    d = P.parameters_metric_schwarz
+    op = mo.Params(AMG_type='UA', cycle_type='W', aggregation_type='HEM', smoother='SGS',
+                   max_levels=d['max_levels'], maxit=d['maxit'], relaxation=d['relaxation'],
+                   presmooth_iter=d['presmooth_iter'], postsmooth_iter=d['postsmooth_iter'],
+                   coarse_dof=d['coarse_dof'], strong_coupled=d['strong_coupled'],
+                   coarse_scaling=d['coarse_scaling'], Schwarz_levels=d['Schwarz_levels'],
+                   Schwarz_mmsize=d['Schwarz_mmsize'], Schwarz_maxlvl=d['Schwarz_maxlvl'],
+                   Schwarz_type=d['Schwarz_type'], num_functions=2)
+    for (N, niters, cond, dt, r, h), n in zip(rows, (32, 64, 128)):
+        s = M.problems.bidomain(2, n, 1.0)
+        b = M.problems.bidomain_mms_rhs(2, n, 1.0, 2.0, 3.0)
+        t0 = time.time()
+        hh = mo.setup(s.scipy(), op, idofs=s.idofs)
+        ref = mo.pcg(s.scipy(), hh, b, 1e-8, 500)
+        say('config 1 n=%d: GPU %d iterations, oracle %d (%.1fs), timeKSP %.3fs' % (n, niters, ref.niters,
+                                                                                time.time() - t0, dt))
+        assert niters == ref.niters, (n, niters, ref.niters)
+        assert abs(r - ref.residuals[-1]) <= 1e-6 * ref.residuals[-1]
+    files = sorted((tmp_path / 'bidomain_2d').glob('iters_precondmetric_mono_*.txt'))
+    assert len(files) == 1, files
+    lines = files[0].read_text().split('\n')
+    assert lines[0] == 'ndofs niters cond timeKSP r h' and len([x for x in lines[1:] if x]) == 3

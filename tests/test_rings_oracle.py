@@ -130,6 +130,31 @@ def test_rings_emi_pcg_gamma_robust():
     assert max(its) <= 20, its
 
 
+@pytest.mark.parametrize('dim,n,g', [(3, 8, 1e6), (3, 16, 1e6), (3, 16, 1.0), (2, 32, 1e6)])
+def test_colour_order_vs_seed_order(dim, n, g):
+    """the GPU sweeps the seed-ring blocks colour by colour; the
+    reference's SCHWARZ_SYMMETRIC (recalled: HAZmath is absent) sweeps them
+    in seed order.  Same blocks and local solves, two multiplicative orders:
+    the EMI PCG counts (tolerance 1e-10, src/emi_3d.py:143) differ by at most
+    one iteration, and both cycles stay symmetric (DESIGN.md 2.12 records the
+    counts)."""
+    s = _emi(dim, n, g)
+    A = s.scipy()
+    b = mo.seeded_rhs(s.N)
+    h = _setup(s)
+    its_col = mo.pcg(A, h, b, 1e-10, 500).niters
+    h.levels[0].rings.seed_order = True
+    its_seed = mo.pcg(A, h, b, 1e-10, 500).niters
+    print('EMI %dD n=%d gamma=%g: PCG its colour order %d, seed order %d, colours %d, blocks %d'
+          % (dim, n, g, its_col, its_seed, h.levels[0].rings.ncolours, len(h.levels[0].rings.blocks)))
+    assert abs(its_col - its_seed) <= 1, (its_col, its_seed)
+    hs = _setup(s, coarse_scaling=0)
+    hs.levels[0].rings.seed_order = True
+    r1, r2 = mo.seeded_rhs(s.N, 1), mo.seeded_rhs(s.N, 2)
+    a, c = r2 @ hs.apply(r1), r1 @ hs.apply(r2)
+    assert abs(a - c) <= 1e-10 * abs(a)
+
+
 def test_resolution_of_the_reference_names():
     """SCHWARZ_SYMMETRIC resolves by the seeds (mirrors setup.cpp
     resolve_params): 1-rings with a seed on every node -> node patches,
