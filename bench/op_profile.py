@@ -13,6 +13,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# per-op event times (MAMG_OP_PROFILE) exist in the diagnosis build only
+os.environ.setdefault('MAMG_LIB', os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg_diag.so'))
 sys.path.insert(0, ROOT)
 
 PROFILES = {

@@ -16,6 +16,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# per-op event times and the coarse tail's stamps exist in the diagnosis build only
+if '--op-profile' in sys.argv or False:
+    os.environ.setdefault('MAMG_LIB', os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg_diag.so'))
 sys.path.insert(0, ROOT)
 
 

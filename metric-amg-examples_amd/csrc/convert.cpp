@@ -3,7 +3,6 @@
 #include <omp.h>
 
 #include <algorithm>
-#include <cstring>
 
 #include "host.h"
 
@@ -168,18 +167,6 @@ bool node_blocks_of(const CsrView& W, int64_t nv, std::vector<double>* blk) {
     }
   }
   return true;
-}
-
-// dst[0, bytes) = src[0, bytes) by the host threads (OpenMP), in 64 KiB
-// pieces: the host side of the staged uploads (gsetup.hip h2d_staged)
-void par_memcpy(void* dst, const void* src, size_t bytes) {
-  constexpr size_t PIECE = (size_t)64 << 10;
-  const int64_t np = (int64_t)((bytes + PIECE - 1) / PIECE);
-#pragma omp parallel for schedule(static)
-  for (int64_t k = 0; k < np; ++k) {
-    const size_t o = (size_t)k * PIECE;
-    std::memcpy((char*)dst + o, (const char*)src + o, std::min(PIECE, bytes - o));
-  }
 }
 
 }  // namespace mamg

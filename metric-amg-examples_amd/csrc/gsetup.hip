@@ -42,7 +42,6 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <mutex>
 
 #include "dist.h"
 #include "dmem.h"
@@ -2704,50 +2703,6 @@ int gen_bidomain_dev(int dim, int64_t n, double gamma, double k1, double k2, int
   return MAMG_OK;
 }
 
-// Host -> device copy of a pageable host array through pinned staging
-// buffers: the host threads copy chunk k + 1 into one buffer (par_memcpy)
-// while the DMA engine moves chunk k out of another.  A plain hipMemcpy from
-// pageable memory stages through the runtime's own buffers with one host
-// thread: 31-37 GB/s for A_0's 12 GB at nrefs=6.  The three
-// 64 MiB buffers are pinned once per process and reused.
-int h2d_staged(void* dst, const void* src, size_t bytes, std::string* err) {
-  constexpr size_t CH = (size_t)64 << 20;
-  constexpr int NB = 3;
-  static std::mutex mu;
-  static void* buf[NB] = {nullptr, nullptr, nullptr};
-  if (bytes < 2 * CH) {   // small arrays: the runtime's path
-    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-    return MAMG_OK;
-  }
-  std::lock_guard<std::mutex> g(mu);
-  for (int b = 0; b < NB; ++b)
-    if (!buf[b] && hipHostMalloc(&buf[b], CH, hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      buf[b] = nullptr;
-      HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));   // no pinned memory: the runtime's path
-      return MAMG_OK;
-    }
-  hipEvent_t ev[NB];
-  for (int b = 0; b < NB; ++b) HIPCHK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
-  int rc = MAMG_OK;
-  size_t k = 0;
-  for (size_t off = 0; off < bytes; off += CH, ++k) {
-    const int b = (int)(k % NB);
-    const size_t len = std::min(CH, bytes - off);
-    if (k >= NB && hipEventSynchronize(ev[b]) != hipSuccess) { rc = MAMG_ERR_HIP; break; }
-    par_memcpy(buf[b], (const char*)src + off, len);
-    if (hipMemcpyAsync((char*)dst + off, buf[b], len, hipMemcpyHostToDevice, nullptr) != hipSuccess ||
-        hipEventRecord(ev[b], nullptr) != hipSuccess) { rc = MAMG_ERR_HIP; break; }
-  }
-  const hipError_t es = hipStreamSynchronize(nullptr);
-  for (int b = 0; b < NB; ++b) (void)hipEventDestroy(ev[b]);
-  if (rc || es != hipSuccess) {
-    *err = std::string("staged upload: ") + hipGetErrorString(hipGetLastError());
-    return MAMG_ERR_HIP;
-  }
-  return MAMG_OK;
-}
-
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   HIPCHK(hipSetDevice(G->device));
   Clock clk;
@@ -2757,10 +2712,10 @@ int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   RCHK(galloc(G, &D->ptr, A.n + 1, err));
   RCHK(galloc(G, &D->col, D->nnz, err));
   RCHK(galloc(G, &D->val, D->nnz, err));
-  RCHK(h2d_staged(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), err));
+  HIPCHK(hipMemcpy(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (D->nnz) {
-    RCHK(h2d_staged(D->col, A.col, D->nnz * sizeof(int32_t), err));
-    RCHK(h2d_staged(D->val, A.val, D->nnz * sizeof(double), err));
+    HIPCHK(hipMemcpy(D->col, A.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D->val, A.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
   }
   G->phase_ms[GS_UPLOAD] = clk.lap();
   return MAMG_OK;

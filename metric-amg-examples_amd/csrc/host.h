@@ -135,9 +135,6 @@ struct HSell {
 };
 int to_sell(const HBsr& B, bool sym, int C, int sigma, HSell* S, std::string* err);
 
-// dst = src by the host's OpenMP threads (the staged H2D uploads)
-void par_memcpy(void* dst, const void* src, size_t bytes);
-
 // hash shared with the oracle (oracle/mamg_oracle.py:hash32)
 inline uint32_t hash32(uint64_t i, int level) {
   uint32_t x = (uint32_t)(i & 0xFFFFFFFFu);
