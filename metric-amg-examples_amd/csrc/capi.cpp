@@ -392,8 +392,10 @@ int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int3
     } else if (mode == 1 || G.generic) {   // generic smoothers: the host plan of the whole hierarchy
       rc = mamg::ghier_download(G, v, &H, &err);
     } else {
+      // node patches on N GPUs read and write within 3 hops of a rank's nodes
+      const bool patches = P.Schwarz_levels >= 1 && P.Schwarz_type == MAMG_SCHWARZ_PATCHES;
       rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, P.post_fusion != 0, &H,
-                                     &ghosts, &err, mode == 2);
+                                     &ghosts, &err, mode == 2, patches ? 3 : 1);
       pre = !rc;
       on_device = !rc && mode != 2;
     }

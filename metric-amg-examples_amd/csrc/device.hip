@@ -1561,12 +1561,6 @@ __global__ __launch_bounds__(256) void i64_to_i32_kernel(int64_t n, const int64_
 // column-packed upper triangle: U(i, j), i <= j, at j (j + 1) / 2 + i
 __device__ __forceinline__ int upk(int i, int j) { return i <= j ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j; }
 
-// Patch inverses, one wave per patch (4 per workgroup).  Lane j < 2d holds
-// column j of the augmented [A_p | I] (d = 2 m <= 32 rows in registers; local
-// dof i = 2 a + f, a = the node's position in row I, f = field).  Gauss-Jordan
-// without pivoting in mamg_oracle.batched_inverse's operation order (row k
-// divided by the pivot, then M_i -= M_ik M_k, no contraction); the packed
-// upper triangle of the inverse is stored (the oracle symmetrises the same).
 // lane l's double, broadcast to the wave (l wave-uniform)
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -1575,8 +1569,18 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// Patch inverses, one wave per patch (4 per workgroup).  Lane j < 2d holds
+// column j of the augmented [A_p | I] (d = 2 m <= 32 rows in registers; local
+// dof i = 2 a + f, a = the node's position in row I, f = field).  Gauss-Jordan
+// without pivoting in mamg_oracle.batched_inverse's operation order (row k
+// divided by the pivot, then M_i -= M_ik M_k, no contraction); the packed
+// upper triangle of the inverse is stored (the oracle symmetrises the same).
+// gcol: the rows' columns as global node ids, sorted per row (the search
+// keys; = col on one GPU, the rank-local rows keep the global column order
+// with local indices in col on N GPUs)
 __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_t* __restrict__ perm,
                                                         const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                        const int32_t* __restrict__ gcol,
                                                         const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
                                                         int* bad) {
 #pragma clang fp contract(off)
@@ -1591,7 +1595,7 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
 #pragma unroll
   for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = 0.0;
   if (lane < d) {
-    const int32_t Jb = col[q0 + (lane >> 1)];
+    const int32_t Jb = gcol[q0 + (lane >> 1)];
     const int g = lane & 1;
 #pragma unroll
     for (int a = 0; a < PATCH_MAX_NODES; ++a) {
@@ -1600,9 +1604,9 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
         int64_t lo = ptr[Ja], hi = ptr[Ja + 1];
         while (lo < hi) {
           const int64_t md = (lo + hi) >> 1;
-          if (col[md] < Jb) lo = md + 1; else hi = md;
+          if (gcol[md] < Jb) lo = md + 1; else hi = md;
         }
-        if (lo < ptr[Ja + 1] && col[lo] == Jb) {
+        if (lo < ptr[Ja + 1] && gcol[lo] == Jb) {
           const dv4 v = val[lo];
           M[2 * a] = g ? v.y : v.x;
           M[2 * a + 1] = g ? v.w : v.z;
@@ -3351,22 +3355,14 @@ inline bool patch_schwarz(const mamg_params& p) {
   return p.Schwarz_levels >= 1 && p.Schwarz_type == MAMG_SCHWARZ_PATCHES;
 }
 
-// Node-patch Schwarz data of level 0 from A_0's device BSR2 B: distance-3
-// colouring (rounds of three key-max and three mask-or hops, one 8-byte
-// readback each), patches sorted by colour (stable radix sort, ascending
-// centre within a colour), A_0 kept as plain BSR2 for the patch rows, and the
-// patch inverses (patch_inv_kernel).
-int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::string* err) {
+// the distance-3 colouring of the node graph of B (c[I], device, from T), its
+// colour count bound check and the longest row (node patches: <= 16 nodes)
+int patch_colour(TmpPool* T, const TBsr& B, int16_t** cout, int* maxlen, std::string* err) {
   int rc;
   const int64_t nr = B.nr;
-  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 256 colours, [2] bad pivot, [3] max row length
-  unsigned long long* left = nullptr;
-  unsigned long long* cnt = nullptr;
+  int* flags = nullptr;                 // [0] asymmetric pattern, [1] > 256 colours, [3] max row length
   if ((rc = T->alloc(&flags, 4, err))) return rc;
-  if ((rc = T->alloc(&left, 1, err))) return rc;
-  if ((rc = T->alloc(&cnt, 64 * PATCH_WORDS, err))) return rc;
   HIPCHK(dev_memset(flags, 0, 4 * sizeof(int)));
-  HIPCHK(dev_memset(cnt, 0, 64 * PATCH_WORDS * sizeof(unsigned long long)));
   pattern_sym_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, flags);
   patch_rowlen_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, flags + 3);
   HIPCHK(hipGetLastError());
@@ -3378,6 +3374,7 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
            std::to_string(PATCH_MAX_NODES) + " nodes per patch)";
     return MAMG_ERR_UNSUPPORTED;
   }
+  *maxlen = hf[3];
   int16_t* c = nullptr;
   uint64_t *m1 = nullptr, *m2 = nullptr, *m3 = nullptr;
   unsigned long long* mask1 = nullptr;
@@ -3414,7 +3411,29 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
+  if (hf[1]) { *err = "node patches: more than 256 colours"; return MAMG_ERR_UNSUPPORTED; }
   T->release(m1); T->release(m2); T->release(m3); T->release(mask1); T->release(win); T->release(wcnt);
+  T->release(flags);
+  *cout = c;
+  return MAMG_OK;
+}
+
+// Node-patch Schwarz data of level 0 from A_0's device BSR2 B: the distance-3
+// colouring (patch_colour), patches sorted by colour (stable radix sort,
+// ascending centre within a colour), A_0 kept as plain BSR2 for the patch
+// rows, and the patch inverses (patch_inv_kernel).
+int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::string* err) {
+  int rc;
+  const int64_t nr = B.nr;
+  int* flags = nullptr;                 // [2] bad pivot
+  unsigned long long* cnt = nullptr;
+  if ((rc = T->alloc(&flags, 4, err))) return rc;
+  if ((rc = T->alloc(&cnt, 64 * PATCH_WORDS, err))) return rc;
+  HIPCHK(dev_memset(flags, 0, 4 * sizeof(int)));
+  HIPCHK(dev_memset(cnt, 0, 64 * PATCH_WORDS * sizeof(unsigned long long)));
+  int16_t* c = nullptr;
+  int hf[4] = {0, 0, 0, 0};
+  if ((rc = patch_colour(T, B, &c, &hf[3], err))) return rc;
   int32_t *ci = nullptr, *cs = nullptr;
   int64_t *iota = nullptr, *sorted = nullptr;
   if ((rc = T->alloc(&ci, nr, err))) return rc;
@@ -3446,7 +3465,8 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
-  patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Sval, D->pus, D->pu, flags + 2);
+  patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
+                                                       flags + 2);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
@@ -5505,6 +5525,16 @@ struct DDLevel {
   std::vector<int64_t> gcs, gbk;
   int64_t *csend_idx = nullptr, *cghost_idx = nullptr;
   std::vector<int64_t> cs_off, cg_off;
+  // level-0 node-patch Schwarz on N ranks (dist_patches): the ghost region is
+  // the 3-hop ball of the owned nodes; the rank computes every patch centred
+  // within 1 hop of its nodes (pl: the patch rows of the nodes within 2 hops,
+  // columns local in the global column order, centres colour by colour,
+  // inverses); cs_off / cg_off above hold each colour's halo of the nodes
+  // its patches write; pb = b interleaved over [owned | ghost]
+  bool patches = false;
+  DLevel pl;
+  int32_t* Sgcol = nullptr;
+  double* pb = nullptr;
 };
 
 // D_CHALO: the forward halo of one colour's nodes (after that colour's GS step)
@@ -5761,10 +5791,61 @@ void dcycle_gs(const DistHandle* h, int l, const double* b, int64_t bs, double* 
   }
 }
 
+// one node-patch sweep of level 0 on N ranks: per colour the rank's patches
+// of that colour, then that colour's halo (the written nodes within 3 hops);
+// every rank emits every colour's exchange, also without patches of its own
+void dpatch_sweep(const DistHandle* h, bool fwd, double* x, std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[0];
+  const int nc = (int)D.pl.pcs.size() - 1;
+  for (int k = 0; k < nc; ++k) {
+    const int c = fwd ? k : nc - 1 - k;
+    ops->push_back(wrap(patch_op(D.pl, c, x, D.pb, 0, C_L0_SMOOTH)));   // empty: not launched
+    ops->push_back(chalo_op(0, c, x, D, h->nranks));
+  }
+}
+
+// multi-GPU level-0 cycle with the node-patch Schwarz (cycle_ops_bsr's
+// patch branch): b interleaved over [owned | ghost] + its halo; x = 0; pre
+// sweeps forward then backward; residual (ghosts current); the coarse
+// correction; x += P e and its halo; post sweeps forward then backward
+void dcycle_patch(const DistHandle* h, const double* b, int64_t bs, double* xout, int64_t os,
+                  std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[0];
+  const DDLevel& C = h->L[1];
+  double* X = D.t;
+  {
+    Op o;
+    o.kind = OP_ILV; o.cls = C_L0_WB; o.n = D.nloc; o.b = b; o.bs = bs; o.out = D.pb;
+    o.bytes = 32.0 * D.nloc;
+    ops->push_back(wrap(o));
+    ops->push_back(halo_op(0, D.pb, D, C_COMM));
+    Op z;
+    z.kind = OP_ZERO; z.cls = C_L0_WB; z.n = 2 * (D.nloc + D.ng); z.out = X; z.bytes = 8.0 * z.n;
+    ops->push_back(wrap(z));
+  }
+  for (int s = 0; s < h->p.presmooth_iter; ++s) {
+    dpatch_sweep(h, true, X, ops);
+    dpatch_sweep(h, false, X, ops);
+  }
+  ops->push_back(wrap(bsr_op(D.A, EPI_RESID, C_L0_RESID, 0, X, 0, nullptr, b, bs, nullptr, D.r, 0)));
+  dcoarse_ops(h, 0, ops);
+  ops->push_back(wrap(bsr_op(D.P, EPI_YADD, C_L0_P, 0, C.x, 0, X, nullptr, 0, nullptr, X, 0)));
+  ops->push_back(halo_op(0, X, D, C_COMM));
+  for (int s = 0; s < h->p.postsmooth_iter; ++s) {
+    dpatch_sweep(h, true, X, ops);
+    dpatch_sweep(h, false, X, ops);
+  }
+  Op o;
+  o.kind = OP_ILV; o.epi = 1; o.cls = C_L0_WB; o.n = D.nloc; o.b = X; o.out = xout; o.os = os;
+  o.bytes = 32.0 * D.nloc;
+  ops->push_back(wrap(o));
+}
+
 // multi-GPU cycle from x = 0 (V or W, nu1 / nu2 sweeps, optional coarse-grid
 // scaling): see dist.cpp / dist_ref.py
 void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
                 std::vector<DOp>* ops) {
+  if (l == 0 && h->L[0].patches) { dcycle_patch(h, b, bs, xout, os, ops); return; }
   if (!h->L[l].coarsest && h->L[l].gcs.size() > 1) { dcycle_gs(h, l, b, bs, xout, os, ops); return; }
   const DDLevel& D = h->L[l];
   const bool l0 = l == 0;
@@ -6206,6 +6287,236 @@ int dev_window_cols(TmpPool* T, const TBsr& B, int64_t w0, int64_t w1, TBsr* O, 
   return MAMG_OK;
 }
 
+// ---- node patches on N ranks (dist_patches) --------------------------------
+// hop distance of every node from the owned range (0 owned, 1..3, 127 beyond)
+__global__ __launch_bounds__(256) void hop_init_kernel(int64_t nv, int64_t o0, int64_t o1, int8_t* __restrict__ d) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I < nv) d[I] = (I >= o0 && I < o1) ? 0 : 127;
+}
+__global__ __launch_bounds__(256) void hop_step_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col, const int8_t* __restrict__ din,
+                                                       int8_t* __restrict__ dout, int k) {
+  const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (I >= nv) return;
+  int8_t v = din[I];
+  if (v == 127)
+    for (int64_t q = ptr[I]; q < ptr[I + 1]; ++q)
+      if (din[col[q]] == k - 1) { v = (int8_t)k; break; }
+  dout[I] = v;
+}
+// global id of local node li ([owned | ghost])
+__device__ __forceinline__ int64_t local_gid(int64_t li, int64_t nloc, int64_t o0, const int64_t* gh) {
+  return li < nloc ? o0 + li : gh[li - nloc];
+}
+// the rank's patch rows: local row li = B's row of its global node when that
+// node is within 2 hops of the owned range, else empty (len[li + 1])
+__global__ __launch_bounds__(256) void srow_len_kernel(int64_t nl, int64_t nloc, int64_t o0, const int64_t* __restrict__ gh,
+                                                       const int8_t* __restrict__ hop, const int64_t* __restrict__ bptr,
+                                                       int64_t* __restrict__ len) {
+  const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (li >= nl) return;
+  const int64_t g = local_gid(li, nloc, o0, gh);
+  len[li + 1] = hop[g] <= 2 ? bptr[g + 1] - bptr[g] : 0;
+}
+// ... its blocks in B's (global) column order: local columns (map) and the
+// global ids (the inverse kernel's search keys)
+__global__ __launch_bounds__(256) void srow_fill_kernel(int64_t nl, int64_t nloc, int64_t o0, const int64_t* __restrict__ gh,
+                                                        const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
+                                                        const dv4* __restrict__ bval, const int32_t* __restrict__ map,
+                                                        const int64_t* __restrict__ sptr, int32_t* __restrict__ scol,
+                                                        int32_t* __restrict__ sgcol, dv4* __restrict__ sval) {
+  const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (li >= nl || sptr[li + 1] == sptr[li]) return;
+  const int64_t g = local_gid(li, nloc, o0, gh);
+  int64_t o = sptr[li];
+  for (int64_t k = bptr[g]; k < bptr[g + 1]; ++k, ++o) {
+    scol[o] = map[bcol[k]];
+    sgcol[o] = bcol[k];
+    sval[o] = bval[k];
+  }
+}
+// per local node: its hop distance and colour (for the centre list)
+__global__ __launch_bounds__(256) void local_hop_colour_kernel(int64_t nl, int64_t nloc, int64_t o0,
+                                                               const int64_t* __restrict__ gh,
+                                                               const int8_t* __restrict__ hop,
+                                                               const int16_t* __restrict__ c, int8_t* __restrict__ lh,
+                                                               int16_t* __restrict__ lc) {
+  const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (li >= nl) return;
+  const int64_t g = local_gid(li, nloc, o0, gh);
+  lh[li] = hop[g];
+  lc[li] = c[g];
+}
+// colours of the patches that write node J (the centres in J's closed
+// neighbourhood), -1 padded: PATCH_MAX_NODES + 1 slots per node
+__global__ __launch_bounds__(256) void cover_kernel(int64_t cnt, const int64_t* __restrict__ nodes,
+                                                    const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
+                                                    const int16_t* __restrict__ c, int16_t* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= cnt) return;
+  const int64_t J = nodes[t];
+  int16_t* o = out + t * (PATCH_MAX_NODES + 1);
+  int k = 0;
+  bool self = false;
+  for (int64_t q = bptr[J]; q < bptr[J + 1] && k < PATCH_MAX_NODES + 1; ++q) {
+    self |= bcol[q] == J;
+    o[k++] = c[bcol[q]];
+  }
+  if (!self && k < PATCH_MAX_NODES + 1) o[k++] = c[J];
+  for (; k < PATCH_MAX_NODES + 1; ++k) o[k] = -1;
+}
+
+// Level-0 node patches of a rank: the global distance-3
+// colouring (every rank colours the whole level-0 graph, as the single-GPU
+// build_patches, so all ranks hold the same colours); the centres within 1
+// hop of the owned nodes (their patches write owned nodes; the owner of
+// every written node computes the same patch from the same x, so its bits
+// agree); their rows (nodes within 2 hops) with the global column order kept
+// (the patch's local dof order, hence its Gauss-Jordan, equals the single
+// GPU's); the inverses; and per colour the halo of the nodes its patches
+// write (send: owned nodes in a peer's 3-hop region, receive: ghosts), so
+// that the ghosts within 3 hops are current before the next colour.
+int dist_patches(DistHandle* h, const DevMat& A0d, const DistLevel& P, DDLevel* D, std::string* err) {
+  int rc;
+  TmpPool T;
+  const int64_t nv = P.nv, nloc = P.nloc, ng = (int64_t)P.ghosts.size(), nl = nloc + ng;
+  const int R = h->nranks;
+  TBsr B;
+  if ((rc = dev_csr_to_bsr(&T, A0d, nv, nv, &B, err))) return rc;
+  int16_t* c = nullptr;
+  int maxlen = 0;
+  if ((rc = patch_colour(&T, B, &c, &maxlen, err))) return rc;
+  int16_t hcol_max = 0;
+  {
+    std::vector<int16_t> hc(nv);
+    HIPCHK(hipMemcpy(hc.data(), c, nv * sizeof(int16_t), hipMemcpyDeviceToHost));
+    for (int16_t v : hc) hcol_max = std::max(hcol_max, v);
+  }
+  const int ncol = hcol_max + 1;
+  int8_t *hop = nullptr, *hop2 = nullptr;
+  if ((rc = T.alloc(&hop, nv, err)) || (rc = T.alloc(&hop2, nv, err))) return rc;
+  hop_init_kernel<<<nblocks(nv), 256>>>(nv, P.o0, P.o1, hop);
+  for (int k = 1; k <= 3; ++k) {
+    hop_step_kernel<<<nblocks(nv), 256>>>(nv, B.ptr, B.col, hop, hop2, k);
+    std::swap(hop, hop2);
+  }
+  HIPCHK(hipGetLastError());
+  int64_t* gh = nullptr;
+  if ((rc = T.alloc(&gh, std::max<int64_t>(ng, 1), err))) return rc;
+  if (ng) HIPCHK(hipMemcpy(gh, P.ghosts.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice));
+  int32_t* map = nullptr;
+  if ((rc = dev_col_map(&T, P, &map, err))) return rc;
+  // the patch rows
+  DLevel& L = D->pl;
+  if ((rc = ddalloc(h, &L.Sptr, nl + 1, err))) return rc;
+  if (nl) srow_len_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, hop, B.ptr, L.Sptr);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(L.Sptr, L.Sptr, nl + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&L.Snb, L.Sptr + nl, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((rc = ddalloc(h, &L.Scol, std::max<int64_t>(L.Snb, 1), err))) return rc;
+  if ((rc = ddalloc(h, &D->Sgcol, std::max<int64_t>(L.Snb, 1), err))) return rc;
+  if ((rc = ddalloc(h, &L.Sval, std::max<int64_t>(L.Snb, 1), err))) return rc;
+  if (nl) srow_fill_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, B.ptr, B.col, B.val, map, L.Sptr, L.Scol, D->Sgcol,
+                                                 L.Sval);
+  HIPCHK(hipGetLastError());
+  // the centres (within 1 hop), colour by colour, ascending global id inside a colour
+  std::vector<int8_t> lh(nl);
+  std::vector<int16_t> lc(nl);
+  {
+    int8_t* dlh = nullptr;
+    int16_t* dlc = nullptr;
+    if ((rc = T.alloc(&dlh, std::max<int64_t>(nl, 1), err)) || (rc = T.alloc(&dlc, std::max<int64_t>(nl, 1), err)))
+      return rc;
+    if (nl) local_hop_colour_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, hop, c, dlh, dlc);
+    HIPCHK(hipGetLastError());
+    if (nl) {
+      HIPCHK(hipMemcpy(lh.data(), dlh, nl, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(lc.data(), dlc, nl * sizeof(int16_t), hipMemcpyDeviceToHost));
+    }
+  }
+  std::vector<std::pair<int64_t, int64_t>> cen;   // (colour << 40 | global id, local id)
+  for (int64_t li = 0; li < nl; ++li)
+    if (lh[li] <= 1) {
+      const int64_t g = li < nloc ? P.o0 + li : P.ghosts[li - nloc];
+      cen.push_back({((int64_t)lc[li] << 40) | g, li});
+    }
+  std::sort(cen.begin(), cen.end());
+  const int64_t np = (int64_t)cen.size();
+  L.pcs.assign(ncol + 1, 0);
+  std::vector<int32_t> perm(np);
+  for (int64_t i = 0; i < np; ++i) {
+    perm[i] = (int32_t)cen[i].second;
+    ++L.pcs[(cen[i].first >> 40) + 1];
+  }
+  for (int k = 0; k < ncol; ++k) L.pcs[k + 1] += L.pcs[k];
+  L.n = 2 * np;
+  if ((rc = ddalloc(h, &L.pperm, std::max<int64_t>(np, 1), err))) return rc;
+  if (np) HIPCHK(hipMemcpy(L.pperm, perm.data(), np * sizeof(int32_t), hipMemcpyHostToDevice));
+  // inverses
+  const int64_t dmax = 2 * (int64_t)maxlen;
+  L.pus = dmax * (dmax + 1) / 2;
+  if ((rc = ddalloc(h, &L.pu, std::max<int64_t>(np * L.pus, 1), err))) return rc;
+  int* bad = nullptr;
+  if ((rc = T.alloc(&bad, 1, err))) return rc;
+  HIPCHK(dev_memset(bad, 0, sizeof(int)));
+  if (np)
+    patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
+  HIPCHK(hipGetLastError());
+  int hb = 0;
+  HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
+  if (hb) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
+  // each colour's halo: the listed nodes its patches write
+  const int64_t ns = P.send_off.empty() ? 0 : P.send_off.back();
+  std::vector<int64_t> lst(ns + ng);
+  for (int64_t t = 0; t < ns; ++t) lst[t] = P.o0 + P.send_idx[t];
+  for (int64_t g = 0; g < ng; ++g) lst[ns + g] = P.ghosts[g];
+  constexpr int CW = PATCH_MAX_NODES + 1;
+  std::vector<int16_t> cov((size_t)(ns + ng) * CW);
+  if (ns + ng) {
+    int64_t* dl = nullptr;
+    int16_t* dc = nullptr;
+    if ((rc = T.alloc(&dl, ns + ng, err)) || (rc = T.alloc(&dc, (ns + ng) * CW, err))) return rc;
+    HIPCHK(hipMemcpy(dl, lst.data(), (ns + ng) * sizeof(int64_t), hipMemcpyHostToDevice));
+    cover_kernel<<<nblocks(ns + ng), 256>>>(ns + ng, dl, B.ptr, B.col, c, dc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(cov.data(), dc, cov.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+  }
+  auto covers = [&](int64_t t, int col) {
+    for (int k = 0; k < CW; ++k)
+      if (cov[(size_t)t * CW + k] == col) return true;
+    return false;
+  };
+  std::vector<int64_t> cs, cg;
+  D->cs_off.assign((size_t)ncol * (R + 1), 0);
+  D->cg_off.assign((size_t)ncol * (R + 1), 0);
+  for (int col = 0; col < ncol; ++col) {
+    for (int q = 0; q < R; ++q) {
+      D->cs_off[(size_t)col * (R + 1) + q] = (int64_t)cs.size();
+      D->cg_off[(size_t)col * (R + 1) + q] = (int64_t)cg.size();
+      for (int64_t t = P.send_off[q]; t < P.send_off[q + 1]; ++t)
+        if (covers(t, col)) cs.push_back(P.send_idx[t]);
+      for (int64_t g = P.ghost_off[q]; g < P.ghost_off[q + 1]; ++g)
+        if (covers(ns + g, col)) cg.push_back(g);
+    }
+    D->cs_off[(size_t)col * (R + 1) + R] = (int64_t)cs.size();
+    D->cg_off[(size_t)col * (R + 1) + R] = (int64_t)cg.size();
+  }
+  if (!cs.empty()) {
+    if ((rc = ddalloc(h, &D->csend_idx, (int64_t)cs.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->csend_idx, cs.data(), cs.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (!cg.empty()) {
+    if ((rc = ddalloc(h, &D->cghost_idx, (int64_t)cg.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->cghost_idx, cg.data(), cg.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  D->patches = true;
+  if (h->p.print_level >= 2)
+    std::fprintf(stderr, "[mamg] rank %d/%d node patches: %d colours, %lld centres (%lld owned), %lld ghost nodes "
+                 "(3 hops), colour halos %lld sends / %lld receives in all\n", h->rank, R, ncol, (long long)np,
+                 (long long)nloc, (long long)ng, (long long)cs.size(), (long long)cg.size());
+  return MAMG_OK;
+}
+
 // each colour's halo of a distributed level: colour c's nodes in every send
 // list and ghost list, in list order (so the sender's subset and the
 // receiver's subset match), offsets per (colour, peer); gcol = the level's
@@ -6373,8 +6684,9 @@ int dist_check(const mamg_params& p, std::string* err) {
     *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (patch_schwarz(p) || rings_schwarz(p)) {
-    *err = "multi-GPU apply: node-patch / seed-ring Schwarz (SCHWARZ_PATCHES / SCHWARZ_RINGS) is single-GPU";
+  if (rings_schwarz(p)) {
+    *err = "multi-GPU apply: seed-ring Schwarz (SCHWARZ_RINGS) is single-GPU (the node patches, SCHWARZ_PATCHES, "
+           "run on N GPUs)";
     return MAMG_ERR_UNSUPPORTED;
   }
   return MAMG_OK;
@@ -6385,6 +6697,12 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
                 const GhostLists* ghosts, const GHier* G, const DevMat* A0d) {
   if (int rc = dist_check(p, err)) return rc;
   const bool gs = gs_smoother(p);
+  const bool patches = patch_schwarz(p);
+  if (patches && !(G && A0d && ghosts)) {
+    *err = "multi-GPU node patches need the rank operators and the 3-hop ghost lists built from the GPU hierarchy "
+           "(mamg_setup_dist with a GPU-setup profile)";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   if (gs && !G) {
     *err = "multi-GPU multicolour GS needs the rank operators built from the GPU hierarchy (mamg_setup_dist "
            "with a GPU-setup profile)";
@@ -6396,7 +6714,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   DistPlan plan;
   const auto tp0 = std::chrono::steady_clock::now();
   const double kw = p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0;
-  bool fuse = p.post_fusion != 0 && !gs;   // GS post-smooths after x += P e (as on one GPU)
+  bool fuse = p.post_fusion != 0 && !gs && !patches;   // GS / patches post-smooth after x += P e (as on one GPU)
   if (G)                   // operators from the GPU hierarchy: fusion needs its A P on every level
     for (size_t l = 0; l + 1 < G->levels.size() && fuse; ++l)
       if (!G->levels[l].coarsest && G->levels[l].AP.n != G->levels[l].n) fuse = false;
@@ -6454,7 +6772,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       TmpPool TC;
       int8_t* gcol = nullptr;
       int ncol = 0;
-      if (gs) {
+      if (gs && !(l == 0 && patches)) {
         TBsr B;
         if ((rc = dev_csr_to_bsr(&TC, l == 0 ? *A0d : G->levels[l].A, D.nv, D.nv, &B, err))) return rc;
         if ((rc = gs_colour(&TC, B, l, &gcol, &ncol, err))) return rc;
@@ -6462,6 +6780,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
         if (!D.replicated && (rc = colour_halo_lists(h.get(), P, gcol, ncol, &D, err))) return rc;
       }
       if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, gcol, ncol, err))) return rc;
+      if (l == 0 && patches && !D.coarsest && (rc = dist_patches(h.get(), *A0d, P, &D, err))) return rc;
     } else {
       if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
         int64_t best0 = 0, best1 = 0, run0 = 0;
@@ -6514,6 +6833,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     if ((rc = ddalloc(h.get(), &D.t2, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
     if (l == 0 && !D.coarsest && (rc = ddalloc(h.get(), &D.spx, 2 * full, err))) return rc;
+    if (D.patches && (rc = ddalloc(h.get(), &D.pb, 2 * full, err))) return rc;
     if (l > 0 && p.cycle_type == MAMG_W_CYCLE) {
       if ((rc = ddalloc(h.get(), &D.c, 2 * full, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.e, 2 * full, err))) return rc;
@@ -6523,12 +6843,16 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = ddalloc(h.get(), &D.part2, 2 * SCALE_BLOCKS, err))) return rc;
     }
     const int64_t ns = P.send_idx.size();
+    // colour halos: a node in the lists of every colour that writes it (node
+    // patches), so their totals may exceed the plain lists
+    const int64_t tcs = D.cs_off.empty() ? 0 : D.cs_off.back(), tcg = D.cg_off.empty() ? 0 : D.cg_off.back();
     if (ns) {
       if ((rc = ddalloc(h.get(), &D.send_idx, ns, err))) return rc;
       HIPCHK(hipMemcpy(D.send_idx, P.send_idx.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice));
-      if ((rc = ddalloc(h.get(), &D.sendbuf, 2 * ns, err))) return rc;
     }
-    if (std::max(ns, D.ng) > 0 && (rc = ddalloc(h.get(), &D.recvbuf, 2 * std::max(ns, D.ng), err))) return rc;
+    if (std::max(ns, tcs) > 0 && (rc = ddalloc(h.get(), &D.sendbuf, 2 * std::max(ns, tcs), err))) return rc;
+    const int64_t nrcv = std::max(std::max(ns, D.ng), tcg);
+    if (nrcv > 0 && (rc = ddalloc(h.get(), &D.recvbuf, 2 * nrcv, err))) return rc;
   }
   h->nv0 = plan.levels[0].nv;
   h->o0 = plan.levels[0].o0;
@@ -6909,8 +7233,10 @@ int dist_set_exchange(DistHandle* h, const mamg_exchange& ex, std::string* err) 
     for (int l = 0; l < nl; ++l) {
       const DDLevel& D = h->L[l];
       const int64_t ns = D.send_off.empty() ? 0 : D.send_off.back();
+      const int64_t tcs = D.cs_off.empty() ? 0 : D.cs_off.back(), tcg = D.cg_off.empty() ? 0 : D.cg_off.back();
       int rc;
-      if ((rc = pin(&h->hsend[l], 2 * ns)) || (rc = pin(&h->hghost[l], 2 * D.ng)) || (rc = pin(&h->hrecv[l], 2 * ns)))
+      if ((rc = pin(&h->hsend[l], 2 * std::max(ns, tcs))) || (rc = pin(&h->hghost[l], 2 * std::max(D.ng, tcg))) ||
+          (rc = pin(&h->hrecv[l], 2 * ns)))
         return rc;
       red = std::max(red, 2 * D.nv);
     }

@@ -65,7 +65,7 @@ int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string*
 int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H,
                         std::vector<std::vector<std::vector<int64_t>>>* ghosts, std::string* err,
-                        bool matrices = true);
+                        bool matrices = true, int hops0 = 1);
 // SCHWARZ_RINGS level-0 blocks (one per seed, setup.cpp overlap_smoother's
 // breadth-first rings: members sorted, <= mm dofs) and their Gauss-Jordan
 // inverses, from the device CSR A.  Device buffers (hipMalloc, the caller

@@ -2819,6 +2819,25 @@ __global__ void ghost_mark_kernel(const int64_t* __restrict__ ptr, const int32_t
   }
 }
 
+// one more hop of every rank's ghost region (node patches on N GPUs need the
+// 3-hop ball): a ghost I of rank q (min[q nc + I] set) marks its row's
+// columns outside q's range in mout (a copy of min beforehand)
+__global__ void ghost_expand_kernel(const int64_t* __restrict__ ptr, const int32_t* __restrict__ col, int64_t n,
+                                    int64_t nc, const int64_t* __restrict__ coln, int nranks,
+                                    const uint8_t* __restrict__ min, uint8_t* __restrict__ mout) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t I = i % nc;
+  for (int q = 0; q < nranks; ++q) {
+    if (!min[(int64_t)q * nc + I]) continue;
+    const int64_t c0 = coln[q], c1 = coln[q + 1];
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+      const int64_t J = col[k] % nc;
+      if (J < c0 || J >= c1) mout[(int64_t)q * nc + J] = 1;
+    }
+  }
+}
+
 struct DevScratch {             // a null-stream ordered temporary (dmem.h), freed on scope exit
   void* p = nullptr;
   ~DevScratch() { tmp_free(p); }
@@ -2828,7 +2847,7 @@ struct DevScratch {             // a null-stream ordered temporary (dmem.h), fre
 
 int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, int rank, int nranks,
                         int64_t rep_nodes, bool post_fusion, Hierarchy* H, GhostLists* ghosts,
-                        std::string* err, bool matrices) {
+                        std::string* err, bool matrices, int hops0) {
   if (nranks < 1 || rank < 0 || rank >= nranks) { *err = "bad rank/nranks"; return MAMG_ERR_ARG; }
   if (G.generic) { *err = "rank download of a hierarchy without node-block smoothers"; return MAMG_ERR_UNSUPPORTED; }
   H->params = G.params;
@@ -2887,9 +2906,10 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
   for (int l = 0; l < nl; ++l)
     if (!rep[l]) mark_bytes = std::max<int64_t>(mark_bytes, (int64_t)nranks * nv[l]);
   if (mark_bytes) {
-    DevScratch rng, mk;
+    DevScratch rng, mk, mk2;
     HIPCHK(tmp_malloc(&rng.p, (size_t)nl * (nranks + 1) * sizeof(int64_t)));
     HIPCHK(tmp_malloc(&mk.p, (size_t)mark_bytes));
+    if (hops0 > 1) HIPCHK(tmp_malloc(&mk2.p, (size_t)nranks * nv[0]));
     int64_t* drng = (int64_t*)rng.p;
     uint8_t* mark = (uint8_t*)mk.p;
     for (int l = 0; l < nl; ++l)
@@ -2905,6 +2925,12 @@ int ghier_download_rank(const GHier& G, const DevMat& A0d, const CsrView& A0, in
                                               drng + (size_t)l * (nranks + 1), nranks, mark);
       };
       marks(l == 0 ? A0d : G.levels[l].A, l);
+      for (int hop = 1; l == 0 && hop < hops0; ++hop) {   // the ghost ball grown hop by hop
+        uint8_t* m2 = (uint8_t*)mk2.p;
+        HIPCHK(dev_copy(m2, mark, (size_t)nranks * nv[0]));
+        ghost_expand_kernel<<<nblk(A0d.n), 256>>>(A0d.ptr, A0d.col, A0d.n, nv[0], drng, nranks, mark, m2);
+        HIPCHK(dev_copy(mark, m2, (size_t)nranks * nv[0]));
+      }
       if (l > 0) {
         marks(G.levels[l - 1].P, l - 1);
         if (fuse) marks(G.levels[l - 1].AP, l - 1);

@@ -265,3 +265,92 @@ def nodemajor_Ainv(Ainv):
 
 def local_slice(v, nv, o0, o1):
     return np.concatenate([v[o0:o1], v[nv + o0: nv + o1]])
+
+
+# --------------------------------------------------------------------------
+# Node-patch Schwarz on P ranks (device.hip dist_patches
+# / dcycle_patch): rank p owns the nodes [own[p], own[p+1]) (contiguous, as
+# the level-0 z-slabs); its local copy of x covers the owned nodes and every
+# node within 3 hops; it computes the patches centred within 1 hop of its
+# nodes (each patch that writes an owned node) from its local x, writes the
+# patch's dofs locally, and after each colour receives from the owners the
+# nodes that colour's patches wrote inside its 3-hop region.  The owner of a
+# written node computes the same patch from the same values, so the sweep is
+# the sequential multiplicative sweep (mamg_oracle.Patches.sweep) exactly.
+# --------------------------------------------------------------------------
+def _hops(Gd, seeds_mask, k):
+    """boolean mask of the nodes within k hops of the seeds (Gd: closed node graph)."""
+    m = seeds_mask.copy()
+    for _ in range(k):
+        m = m | (Gd.T @ m.astype(np.int64) > 0)
+    return m
+
+
+class PartitionedPatchSweep:
+    """P ranks of a node-patch sweep on one process (numpy), with the halo
+    lists of the product: ghost region = 3 hops, centres = 1 hop, per colour
+    the written nodes (a node is written by the colours of the patches
+    centred in its closed neighbourhood)."""
+
+    def __init__(self, A, patches, own):
+        import scipy.sparse as sp
+        from mamg_oracle import node_pattern
+        self.A = A.tocsr()
+        self.pt = patches
+        self.own = list(own)
+        nv = patches.nv
+        G = node_pattern(self.A, 2)
+        Gd = (G + sp.identity(nv, dtype=np.int8, format='csr')).tocsr()
+        Gd.data[:] = 1
+        self.Gd = Gd
+        self.P = len(own) - 1
+        # colours writing each node: the colours of the centres in its closed ring
+        self.writers = [set(patches.colour[Gd.indices[Gd.indptr[J]:Gd.indptr[J + 1]]].tolist()) for J in range(nv)]
+        self.region, self.centres, self.owner = [], [], np.zeros(nv, np.int64)
+        for p in range(self.P):
+            mine = np.zeros(nv, bool)
+            mine[own[p]:own[p + 1]] = True
+            self.owner[own[p]:own[p + 1]] = p
+            self.region.append(_hops(Gd, mine, 3))
+            self.centres.append(np.flatnonzero(_hops(Gd, mine, 1)))
+
+    def sweep(self, x, b, forward=True):
+        """the partitioned sweep from the global x (copied to every rank);
+        returns the gathered owned values"""
+        nv = self.pt.nv
+        xs = [x.copy() for _ in range(self.P)]          # rank p's valid entries: region[p]
+        cols = range(self.pt.ncolours) if forward else range(self.pt.ncolours - 1, -1, -1)
+        for c in cols:
+            written = []
+            for p in range(self.P):
+                I = self.centres[p][self.pt.colour[self.centres[p]] == c]
+                xp = xs[p]
+                D = self.pt.dofs[I]
+                ok = D >= 0
+                dd = D[ok]
+                # a patch reads x within 2 hops of its centre: inside rank p's region
+                rows = self.A[dd]
+                assert np.all(self.region[p][rows.indices % nv]), 'patch reads outside the 3-hop region'
+                res = np.zeros(D.shape)
+                res[ok] = b[dd] - rows @ xp
+                delta = np.einsum('kij,kj->ki', self.pt.Minv[I], res)
+                xp[dd] = xp[dd] + delta[ok]
+                written.append(set((dd % nv).tolist()))
+            # colour c's halo: every rank takes the owner's value of each node
+            # in its 3-hop region that colour c writes
+            upd = np.array(sorted(set().union(*written)), np.int64)
+            for p in range(self.P):
+                if not len(upd):
+                    break
+                mine = upd[self.region[p][upd]]
+                for J in mine:
+                    q = self.owner[J]
+                    if q != p:
+                        assert c in self.writers[J]
+                        for f in (0, 1):
+                            xs[p][f * nv + J] = xs[q][f * nv + J]
+        out = np.empty_like(x)
+        for p in range(self.P):
+            for f in (0, 1):
+                out[f * nv + self.own[p]:f * nv + self.own[p + 1]] = xs[p][f * nv + self.own[p]:f * nv + self.own[p + 1]]
+        return out

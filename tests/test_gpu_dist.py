@@ -319,6 +319,49 @@ def test_virtual_ranks_graph_bitwise(lib_built, monkeypatch, P, kw):
         hh.close()
 
 
+@pytest.mark.parametrize('preset,P', [('schwarz', 2), ('schwarz', 3), ('patch', 4), ('patch', 8)])
+def test_virtual_ranks_node_patches(lib_built, preset, P):
+    """the reference's level-0 smoother on N ranks.  The
+    preset the north-star driver passes (parameters_metric_schwarz, src/
+    bidomain_3d.py:144-147: UA + HEM + W + SGS + scaling + SCHWARZ_SYMMETRIC
+    1-rings = the node patches) and the GPU profile with the patches
+    (parameters_metric_mi355x_patch), row-partitioned over P virtual ranks:
+    every rank colours the whole level-0 graph (the same colours), computes
+    the patches centred within 1 hop of its nodes, and after each colour
+    exchanges the nodes that colour's patches wrote within 3 hops.  The
+    gathered apply equals the one-GPU apply to 1e-12 and the oracle's to
+    1e-10; the lockstep graph replay equals the eager run bitwise."""
+    import torch
+    import metric_amg_examples_amd as M
+    Pm = M.parameters
+    params = Pm.parameters_metric_schwarz if preset == 'schwarz' else Pm.parameters_metric_mi355x_patch
+    s = M.problems.bidomain(3, 16, 1e6)
+    r = mo.seeded_rhs(s.N)
+    B1 = M.MetricAMG(s, s.W, idofs=s.idofs, parameters=params)
+    assert B1.level_format(0)['patches']
+    z1 = B1 * r
+    hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, parameters=params, rank=p, nranks=P, comm_id=None,
+                          rep_nodes=100) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    zg = [torch.full_like(x, float('nan')) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)
+    torch.cuda.synchronize()
+    z = _gather(s, hs, zs)
+    assert np.linalg.norm(z - z1) / np.linalg.norm(z1) < 1e-12
+    for a, b in zip(zs, zg):
+        assert torch.equal(a, b)
+    if preset == 'schwarz':
+        from test_gpu_patch import _oracle_params
+        h = mo.setup(s.scipy(), _oracle_params(params, num_functions=2), idofs=s.idofs)
+        zo = h.apply(r)
+        assert np.linalg.norm(z - zo) / np.linalg.norm(zo) < 1e-10
+    for hh in hs:
+        hh.close()
+    B1.close()
+
+
 @pytest.mark.parametrize('P', [2, 4])
 def test_virtual_ranks_half_bitwise(lib_built, monkeypatch, P):
     """Rank-local level-0 A in the half-symmetric format (owned part through
@@ -479,7 +522,8 @@ def _host_exchange_worker(rank, world, port, q, problem, kw):
 
 
 @pytest.mark.parametrize('problem,kw', [('bidomain', {}), ('emi', dict(smoother=12, Schwarz_maxlvl=0)),
-                                        ('bidomain', dict(smoother=11, coarse_scaling=1, Schwarz_type=7))])
+                                        ('bidomain', dict(smoother=11, coarse_scaling=1, Schwarz_type=7)),
+                                        ('bidomain', dict(Schwarz_type=6))])
 def test_two_processes_host_exchange(lib_built, problem, kw):
     """Two rank processes on the one GPU of the box, exchanging through the
     host-staged gloo transport (RCCL refuses two ranks on one GPU): each
@@ -505,6 +549,8 @@ def test_two_processes_host_exchange(lib_built, problem, kw):
         okw = {'smoother': 'POLY', 'Schwarz_maxlvl': 0}
     elif kw.get('smoother') == 11:
         okw = {'smoother': 'SGS', 'coarse_scaling': 1, 'Schwarz_type': 7}
+    elif kw.get('Schwarz_type') == 6:       # node patches (colour halos through the host-staged transport)
+        okw = {'Schwarz_type': 6}
     A = s.scipy()
     h = mo.setup(A, mo.Params(num_functions=2, **okw), idofs=s.idofs)
     r = mo.seeded_rhs(s.N)
