@@ -46,6 +46,10 @@ def main():
     ap.add_argument('--ranks', type=int, default=8)
     ap.add_argument('--source', choices=('device', 'host'), default='device')
     ap.add_argument('--check-host', action='store_true')
+    ap.add_argument('--profile', choices=('mi355x', 'schwarz', 'patch'), default='mi355x',
+                    help='mi355x: the GPU profile (default); schwarz: the reference preset '
+                         'parameters_metric_schwarz verbatim (node patches on level 0); patch: '
+                         'parameters_metric_mi355x_patch')
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -60,7 +64,10 @@ def main():
         s = M.problems.bidomain(3, n, args.gamma)
         A = s
     r = M.problems.seeded_rhs(s.N)
-    out = {'N': s.N, 'ranks': args.ranks, 'source': args.source, 'rss_start_GB': round(rss_start, 2),
+    prm = {'mi355x': None, 'schwarz': M.parameters.parameters_metric_schwarz,
+           'patch': M.parameters.parameters_metric_mi355x_patch}[args.profile]
+    out = {'N': s.N, 'ranks': args.ranks, 'source': args.source, 'profile': args.profile,
+           'rss_start_GB': round(rss_start, 2),
            'rss_after_A0_GB': round(rss_gb(), 2), 'per_rank': []}
     hs = []
     for p in range(args.ranks):
@@ -69,7 +76,7 @@ def main():
         r0 = rss_gb()
         t0 = time.time()
         hs.append(M.DistMetricAMG(A, s.W, idofs=s.idofs, rank=p, nranks=args.ranks, comm_id=None,
-                                  num_functions=2, print_level=2))
+                                  parameters=prm, num_functions=2, print_level=2))
         torch.cuda.synchronize()
         t = time.time() - t0
         held = m0 - torch.cuda.mem_get_info()[0]
@@ -96,8 +103,11 @@ def main():
             h.time_apply(rs[p], zs[p], 3, 0)
             ms, _, _ = h.time_apply(rs[p], zs[p], 20, 0)
             ms1, kms, _ = h.time_apply(rs[p], zs[p], 5, 1)
-            h.time_apply(rs[p], zs[p], 3, 2)              # hipGraph replays (captured once)
-            msg, _, _ = h.time_apply(rs[p], zs[p], 20, 2)
+            try:
+                h.time_apply(rs[p], zs[p], 3, 2)          # hipGraph replays (captured once)
+                msg, _, _ = h.time_apply(rs[p], zs[p], 20, 2)
+            except M._lib.MamgError:                      # too many ops for one graph
+                msg = float('nan')
             out['per_rank'][p]['compute_ms_per_apply'] = round(ms, 4)
             out['per_rank'][p]['compute_ms_per_apply_graph'] = round(msg, 4)
             out['per_rank'][p]['classes_ms'] = {k: round(v, 4) for k, v in zip(names, kms) if v}
@@ -107,9 +117,12 @@ def main():
         return
     M.DistMetricAMG.virtual_apply(hs, rs, zs)
     zg = [torch.full_like(x, float('nan')) for x in rs]
-    M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)      # the lockstep apply as one hipGraph
-    torch.cuda.synchronize()
-    out['graph_equals_eager_bitwise'] = all(bool(torch.equal(a, b)) for a, b in zip(zs, zg))
+    try:
+        M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)      # the lockstep apply as one hipGraph
+        torch.cuda.synchronize()
+        out['graph_equals_eager_bitwise'] = all(bool(torch.equal(a, b)) for a, b in zip(zs, zg))
+    except M._lib.MamgError as e:          # too many ops for one graph: eager only
+        out['graph'] = str(e)
     del zg
     nv = s.N // 2
 
@@ -136,8 +149,13 @@ def main():
         for h in hh:
             h.close()
         del sh
-    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu')
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, parameters=prm, num_functions=2, setup='gpu')
     z1 = B * r
+    if args.profile != 'mi355x':      # the one-GPU apply's time, for the per-rank compute comparison
+        import torch as _t
+        rt = _t.as_tensor(r).cuda()
+        zt = _t.zeros_like(rt)
+        out['single_gpu_ms_per_apply'] = round(B.time_apply(rt, zt, 3, 0)[0], 3)
     out['rel_diff_vs_single_gpu'] = float(np.linalg.norm(z - z1) / np.linalg.norm(z1))
     print(json.dumps(out), flush=True)
 

@@ -6989,6 +6989,12 @@ int dist_capture(DistHandle* h, const std::vector<DOp>& ops, hipGraph_t* gr, hip
   return MAMG_OK;
 }
 
+// most ops one captured graph holds: the runtime crashed (host SIGSEGV) while
+// capturing the 8 virtual ranks' lockstep apply of the reference family at
+// nrefs=5 (W-cycle + colour steps: ~10^5 launches), and a one-GPU graph of
+// 1.2 x 10^4 launches (the same family) replays fine; longer op lists stay eager
+constexpr size_t DIST_GRAPH_MAX_OPS = 16384;
+
 int dist_graph_exec(DistHandle* h, const double* d_r, double* d_z, hipGraphExec_t* ex, std::string* err) {
   if (!h->comm && h->nranks > 1 && !h->dry) {
     *err = "graph replay needs an RCCL communicator (or one rank): host-staged and virtual exchanges run eagerly";
@@ -7005,6 +7011,11 @@ int dist_graph_exec(DistHandle* h, const double* d_r, double* d_z, hipGraphExec_
   }
   std::vector<DOp> ops;
   dapply_ops(h, d_r, d_z, &ops);
+  if (ops.size() > DIST_GRAPH_MAX_OPS) {
+    *err = "distributed apply of " + std::to_string(ops.size()) + " ops: longer than one graph holds (" +
+           std::to_string(DIST_GRAPH_MAX_OPS) + "); the eager apply serves it";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   DistHandle::Graph g{d_r, d_z, nullptr, nullptr};
   const int rc = dist_capture(h, ops, &g.g, &g.e, err);
   if (rc) {
@@ -7266,7 +7277,16 @@ int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vect
   const int P = (int)hs.size();
   HIPCHK(hipSetDevice(hs[0]->device));
   std::vector<std::vector<DOp>> ops(P);
-  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
+  size_t nops = 0;
+  for (int p = 0; p < P; ++p) {
+    dapply_ops(hs[p], r[p], z[p], &ops[p]);
+    nops += ops[p].size();
+  }
+  if (nops > DIST_GRAPH_MAX_OPS) {
+    *err = "virtual apply of " + std::to_string(nops) + " ops: longer than one graph holds (" +
+           std::to_string(DIST_GRAPH_MAX_OPS) + ")";
+    return MAMG_ERR_UNSUPPORTED;
+  }
   DistHandle* h0 = hs[0];
   if (!h0->cap) HIPCHK(hipStreamCreateWithFlags(&h0->cap, hipStreamNonBlocking));
   HIPCHK(hipStreamBeginCapture(h0->cap, hipStreamCaptureModeThreadLocal));
