@@ -59,7 +59,11 @@ namespace {
 // x' = x + W_I (b_I - s_I) (2x2 block, BSR only) |
 // z = x1_I + W_I r1_I + s_I with s = K e, K = P - W (A P) (BSR only: the
 // prolongation fused with the first post sweep through one operator)
-enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4, EPI_KPOST = 5 };
+enum Epi { EPI_Y = 0, EPI_YADD = 1, EPI_RESID = 2, EPI_JACOBI = 3, EPI_BJAC = 4, EPI_KPOST = 5, EPI_YBD = 6 };
+// EPI_YBD (bsr2_kernel only): out = A x as EPI_Y, and the next level's first
+// sweep from x = 0 in the same pass, y <- W out (the restriction b_c = R r
+// writing x1_c = W_c b_c: one launch and one b_c read fewer per coarse level;
+// the same two products as bd2_kernel, so the same bits)
 
 typedef double dv4 __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -116,6 +120,13 @@ __device__ __forceinline__ void vset(double* v, int64_t stride, int64_t I, int f
 // consecutive workgroups (neighbouring rows, which gather the same x entries)
 // would land in 8 different L2s.  Renumber so that every XCD walks one
 // contiguous range of rows (bijective for any grid size).
+// W_I b_I with the contraction spelled out (fma of the first product onto
+// the second), so that bd2_kernel and the restriction's EPI_YBD epilogue,
+// compiled in different contexts, produce the same bits
+__device__ __forceinline__ double2 wmul(const dv4& w, double b0, double b1) {
+  return double2{__builtin_fma(w.x, b0, w.y * b1), __builtin_fma(w.z, b0, w.w * b1)};
+}
+
 __device__ __forceinline__ int64_t row_block_of(uint32_t b, uint32_t G, int remap) {
   if (!remap) return b;
   const uint32_t q = G >> 3, r = G & 7, x = b & 7;
@@ -158,11 +169,16 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
     int64_t nr, const int64_t* __restrict__ bptr, const int32_t* __restrict__ bcol,
     const double* __restrict__ bval, const double* __restrict__ x, int64_t xs,
     const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os, int remap, const int32_t* __restrict__ sched) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap, const int32_t* __restrict__ sched,
+    int64_t rb0 = 0) {
   const int lane = threadIdx.x & (VL - 1);
-  const int64_t node = ((sched ? (int64_t)sched[blockIdx.x] : row_block(remap)) * 256 + threadIdx.x) / VL;
+  // rb0: first workgroup of a row-range launch (rows from 256 rb0 / VL)
+  const int64_t node = ((sched ? (int64_t)sched[blockIdx.x] : rb0 + row_block(remap)) * 256 + threadIdx.x) / VL;
   const double* offd = SYM ? bval + 2 * bptr[nr] : nullptr;
   double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+  // EPI_YBD's W block loaded with the row, not after the reduction (a
+  // dependent load at the end of every row measured +36 us on level 0's R)
+  const dv4 wy = (EPI == EPI_YBD && node < nr && lane == 0) ? W[node] : dv4{0.0, 0.0, 0.0, 0.0};
   if (node < nr) {
     // chunks of 2 VL blocks, branch-free: every lane issues both loads of a
     // chunk at once (index clamped into the row, contribution selected away),
@@ -193,6 +209,12 @@ __global__ __launch_bounds__(256) void bsr2_kernel(
     double o0, o1;
     if (EPI == EPI_Y) {
       o0 = s0; o1 = s1;
+    } else if (EPI == EPI_YBD) {
+      o0 = s0; o1 = s1;
+      const double2 wb = wmul(wy, o0, o1);
+      double* x1 = const_cast<double*>(y);
+      x1[2 * node] = wb.x;
+      x1[2 * node + 1] = wb.y;
     } else if (EPI == EPI_YADD) {
       o0 = y[2 * node] + s0; o1 = y[2 * node + 1] + s1;
     } else if (EPI == EPI_RESID) {
@@ -383,10 +405,11 @@ __global__ __launch_bounds__(256) void msell_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os, int remap, int lsort) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap, int lsort, int64_t rb0) {
   constexpr int RW = 64 / LPR;                          // rows per wavefront
   const int lane = threadIdx.x & 63, q = lane / RW;
-  const int64_t slot = row_block(remap) * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
+  // rb0: first workgroup of a row-range launch (rows [256 rb0 / LPR, ...))
+  const int64_t slot = (rb0 + row_block(remap)) * (4 * RW) + (threadIdx.x >> 6) * RW + (lane & (RW - 1));
   const bool live = slot < nr;
   const int64_t ns = live ? slot : nr - 1;            // dead lanes mirror the last slot, write nothing
   const int m = meta[ns];
@@ -646,8 +669,8 @@ __global__ __launch_bounds__(256) void bd2_kernel(int64_t nv, const dv4* __restr
   const int64_t I = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (I >= nv) return;
   const double b0 = vget(b, bs, I, 0), b1 = vget(b, bs, I, 1);
-  const dv4 w = W[I];
-  double o0 = w.x * b0 + w.y * b1, o1 = w.z * b0 + w.w * b1;
+  const double2 wb = wmul(W[I], b0, b1);
+  double o0 = wb.x, o1 = wb.y;
   if (ADD) { o0 += y[2 * I]; o1 += y[2 * I + 1]; }
   vset(out, os, I, 0, o0);
   vset(out, os, I, 1, o1);
@@ -1934,6 +1957,12 @@ int g_r_bands = 1;
 int g_k_sort = 1;
 int g_post_k = 1;
 int g_kvar = 0;
+// MAMG_FUSE_RBD: which restrictions write the next level's first sweep
+// (EPI_YBD): 2 those below level 0 (default), 1 all, 0 none.  A/B at
+// nrefs=6 (profiles/r05_fuse_rbd_ab.txt, 3 x 3 alternating runs): coarse
+// levels 0.400 -> 0.386 ms with 2; with 1 also level 0's restriction,
+// 0.461 -> 0.490 ms, a net loss
+int g_fuse_rbd = 2;
 int64_t g_sell_min_rows = 1 << 20;
 int64_t g_msell_min_rows = (int64_t)1 << 40;
 int64_t g_tail_nodes = 0;
@@ -1964,6 +1993,8 @@ void read_knobs() {
   g_r_bands = e ? std::atoi(e) : 1;
   e = std::getenv("MAMG_K_SORT");
   g_k_sort = e ? std::atoi(e) : 1;
+  e = std::getenv("MAMG_FUSE_RBD");
+  g_fuse_rbd = e ? std::atoi(e) : 2;
 }
 
 // every block symmetric (bitwise): then 3 doubles per block carry it exactly
@@ -3908,7 +3939,7 @@ bool to_tail(const Op& o, TOp* t) {
 }
 
 void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
-                   int64_t os, std::vector<Op>* ops, bool tail_ok = true);
+                   int64_t os, std::vector<Op>* ops, bool tail_ok = true, bool x1_ready = false);
 
 static_assert(sizeof(TOp) % 8 == 0, "TOp is copied into LDS as 8-byte words");
 constexpr int64_t TAIL_LDS_MAX = 160 * 1024 - 1024;   // gfx950: 160 KB per workgroup, minus the static arrays
@@ -4064,8 +4095,17 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
   return true;
 }
 
+// level l's cycle (launch path) begins with the first sweep X = W b into L.t
+// (OP_BD): the restriction into l may then write it (EPI_YBD)
+bool starts_with_bd(const DeviceHandle* h, int l) {
+  const DLevel& L = h->L[l];
+  return l > 0 && l != h->tail_level && !L.coarsest && L.gcs.size() <= 1 && L.pcs.size() <= 1 &&
+         L.rcs.size() <= 1;
+}
+
+// x1_ready: X = W b is already in L.t (written by the restriction's EPI_YBD)
 void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, double* xout,
-                   int64_t os, std::vector<Op>* ops, bool tail_ok) {
+                   int64_t os, std::vector<Op>* ops, bool tail_ok, bool x1_ready) {
   if (tail_ok && l > 0 && l == h->tail_level && bs == 0 && os == 0 && tail_ops(h, l, b, xout, ops)) return;
   const DLevel& L = h->L[l];
   const mamg_params& p = h->p;
@@ -4106,7 +4146,7 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
     Op o;
     o.kind = OP_BD; o.cls = clsW; o.n = nv; o.W = step_wd(L, 0, true); o.b = b; o.bs = bs; o.out = X;
     o.bytes = 32.0 * nv + 16.0 * nv + 16.0 * nv;
-    ops->push_back(o);
+    if (!x1_ready) ops->push_back(o);
     for (int s = 1; s < npre; ++s) {
       ops->push_back(bsr_op(L.Ab, EPI_BJAC, clsS, tagA, X, 0, X, b, bs, step_wd(L, s, true), X2, 0));
       std::swap(X, X2);
@@ -4117,7 +4157,18 @@ void cycle_ops_bsr(const DeviceHandle* h, int l, const double* b, int64_t bs, do
   ops->push_back(bsr_op(L.Rb, EPI_Y, l0 ? C_L0_R : C_COARSE, tagA, L.r, 0, nullptr, nullptr, 0,
                         nullptr, C.b, 0));
   ops->back().remap = 1;
-  cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops, tail_ok);
+  // the coarse level's first sweep in the restriction's epilogue (launch path,
+  // bsr2_kernel layouts only; the tail programs keep their own T_BD)
+  const bool ybd = (g_fuse_rbd == 1 || (g_fuse_rbd == 2 && l > 0)) && tail_ok && starts_with_bd(h, l + 1) &&
+                   !L.Rb.sell && !L.Rb.half && !L.Rb.sym && !L.Rb.split;
+  if (ybd) {
+    Op& r = ops->back();
+    r.epi = EPI_YBD;
+    r.W = step_wd(C, 0, true);
+    r.y = C.t;
+    r.bytes += 48.0 * (double)(C.n / 2);   // W_c read, x1_c written
+  }
+  cycle_ops_bsr(h, l + 1, C.b, 0, C.x, 0, ops, tail_ok, ybd);
   if (p.cycle_type == MAMG_W_CYCLE && !C.coarsest) {
     ops->push_back(bsr_op(C.Ab, EPI_RESID, C_MISC, 1, C.x, 0, nullptr, C.b, 0, nullptr, C.c, 0));
     cycle_ops_bsr(h, l + 1, C.c, 0, C.e, 0, ops, tail_ok);
@@ -4228,15 +4279,23 @@ void launch_csr_tag(const Op& o, hipStream_t s) {
   }
 }
 
+// rows [o.r0, o.r1) when o.r1 >= 0 (the distributed K's overlap split: r0 a
+// multiple of 256, r1 too or = nr, so each workgroup's rows lie in the range)
 template <int VL, bool XFM, bool SYM, int TAG>
 void launch_bsr_x(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
-  const unsigned g = nblocks(M.nr * (int64_t)VL);
-  if (g == 0) return;
-#define BSR_ARGS M.nr, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o), \
-    (M.rsched && M.rsched_vl == VL && (int64_t)g == M.nrsched) ? M.rsched : nullptr
+  const bool rng = o.r1 >= 0;
+  const int64_t r0 = rng ? o.r0 : 0, r1 = rng ? o.r1 : M.nr;
+  if (r1 <= r0) return;
+  const int64_t b0 = r0 * VL / 256;
+  const unsigned g = (unsigned)(nblocks(r1 * (int64_t)VL) - b0);
+#define BSR_ARGS r1, M.ptr, M.col, M.val, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, remap_of(o), \
+    (!rng && M.rsched && M.rsched_vl == VL && (int64_t)g == M.nrsched) ? M.rsched : nullptr, b0
   switch (o.epi) {
     case EPI_Y: bsr2_kernel<VL, EPI_Y, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
+    case EPI_YBD:   // restrictions only: node-interleaved, never symmetric
+      if constexpr (!XFM && !SYM) bsr2_kernel<VL, EPI_YBD, false, false, TAG><<<g, 256, 0, s>>>(BSR_ARGS);
+      break;
     case EPI_YADD: bsr2_kernel<VL, EPI_YADD, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_RESID: bsr2_kernel<VL, EPI_RESID, XFM, SYM, TAG><<<g, 256, 0, s>>>(BSR_ARGS); break;
     case EPI_KPOST:   // K is never symmetric and e is node-major
@@ -4267,14 +4326,19 @@ void launch_sell_u(const Op& o, hipStream_t s) {
 #undef SELL_ARGS
 }
 
+// rows [o.r0, o.r1) when o.r1 >= 0: the bounds are multiples of 256 (or
+// r1 = nr), so every workgroup of every LPR covers whole 64-row slices of
+// the range (dist K_ROWS_ALIGN)
 template <int LPR, int U, bool XFM, bool SYM, int SPL, int TAG, int PROBE = 0>
 void launch_msell(const Op& o, hipStream_t s) {
   const DBsr& M = *o.Mb;
   const int64_t rows = 256 / LPR;
-  const unsigned g = (unsigned)((M.nr + rows - 1) / rows);
-  if (g == 0) return;
-#define MSELL_ARGS M.nr, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 && g_kvar == 3) ? 1 : 0, M.lsort ? 1 : 0
+  const int64_t r0 = o.r1 < 0 ? 0 : o.r0, r1 = o.r1 < 0 ? M.nr : o.r1;
+  if (r1 <= r0) return;
+  const int64_t b0 = r0 / rows;
+  const unsigned g = (unsigned)((r1 + rows - 1) / rows - b0);
+#define MSELL_ARGS r1, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
+    (TAG == 0 && g_kvar == 3) ? 1 : 0, M.lsort ? 1 : 0, b0
   switch (o.epi) {
     case EPI_Y: msell_kernel<LPR, U, EPI_Y, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
     case EPI_YADD: msell_kernel<LPR, U, EPI_YADD, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
@@ -5512,6 +5576,7 @@ struct DDLevel {
   double *q = nullptr, *part2 = nullptr; // coarse scaling of this level's correction: A e, dot partials
   double* spx = nullptr;   // level 0: [owned | ghost] operand of the standalone SpMV
   int64_t ib0 = 0, ib1 = 0;  // longest run of A_loc rows without ghost columns
+  int64_t kb0 = 0, kb1 = 0;  // the same for K (coarse ghost columns), bounds multiples of K_ROWS_ALIGN or nloc
   int64_t* send_idx = nullptr;
   double *sendbuf = nullptr, *recvbuf = nullptr;
   std::vector<int64_t> send_off, ghost_off;
@@ -5698,7 +5763,8 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
 // coarse-grid correction of level l from its residual D.r: partial
 // restriction, reverse-add (or all-reduce into a replicated level), the
 // coarse cycle (W: twice), scaling, and the halo of the correction C.x
-void dcoarse_ops(const DistHandle* h, int l, std::vector<DOp>* ops) {
+// (left to the caller when defer_halo: it overlaps that halo with K)
+void dcoarse_ops(const DistHandle* h, int l, std::vector<DOp>* ops, bool defer_halo = false) {
   const DDLevel& D = h->L[l];
   const DDLevel& C = h->L[l + 1];
   const bool l0 = l == 0;
@@ -5726,7 +5792,32 @@ void dcoarse_ops(const DistHandle* h, int l, std::vector<DOp>* ops) {
     ops->push_back(wrap(axpy_op(2 * C.nloc, C.e, C.x)));
   }
   if (h->p.coarse_scaling) dscale_ops(h, l + 1, ops);      // ghosts of C.x scaled too
-  else if (!C.replicated) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+  else if (!C.replicated && !defer_halo) ops->push_back(halo_op(l + 1, C.x, C, C_COMM));
+}
+
+// level 0's K with the coarse-e halo in flight: rows [kb0, kb1) (no coarse
+// ghost columns) on the side stream during the halo (one D_OVERLAP), the
+// rest after it; the same kernel code computes every row either way
+void k_overlap(const DistHandle* h, const Op& k, std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[0];
+  const DDLevel& C = h->L[1];
+  const double n = (double)std::max<int64_t>(D.nloc, 1);
+  DOp ov = halo_op(1, C.x, C, k.cls);   // timed and counted with K's class
+  ov.dk = D_OVERLAP;
+  ov.op = k;
+  ov.op.r0 = D.kb0;
+  ov.op.r1 = D.kb1;
+  ov.op.bytes = k.bytes * (double)(D.kb1 - D.kb0) / n;
+  ov.bytes += ov.op.bytes;
+  ops->push_back(ov);
+  const int64_t lo[2] = {0, D.kb1}, hi[2] = {D.kb0, D.nloc};
+  for (int q = 0; q < 2; ++q) {   // both always emitted (possibly empty): one schedule on every rank
+    Op b = k;
+    b.r0 = lo[q];
+    b.r1 = hi[q];
+    b.bytes = k.bytes * (double)std::max<int64_t>(hi[q] - lo[q], 0) / n;
+    ops->push_back(wrap(b));
+  }
 }
 
 DOp chalo_op(int level, int c, double* x, const DDLevel& D, int P) {
@@ -5883,14 +5974,19 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
       halo_residual(h, l, X, res, ops);
     }
   }
-  dcoarse_ops(h, l, ops);
+  // K on its ghost-free rows while the coarse-e halo is in flight (level 0,
+  // no coarse scaling); the schedule's shape is the same on every rank (the
+  // overlap and both remainder launches are emitted, maybe empty)
+  const bool kov = l == 0 && h->overlap && D.K.nr > 0 && !C.replicated && !h->p.coarse_scaling && npost >= 1;
+  dcoarse_ops(h, l, ops, kov);
   int s0 = 0;
   if (D.K.nr > 0 || D.PA.nr > 0) {   // fused first post step (K built with its smoother), operands local
     const bool last = npost == 1;
-    if (D.K.nr > 0)   // X + W r + K e
-      ops->push_back(wrap(bsr_op(D.K, EPI_KPOST, clsS, tagA, C.x, 0, X, D.r, 0, wk(0, false),
-                                 last ? xout : X2, last ? os : 0)));
-    else              // X + P e + W (r - AP e)
+    if (D.K.nr > 0) { // X + W r + K e
+      const Op k = bsr_op(D.K, EPI_KPOST, clsS, tagA, C.x, 0, X, D.r, 0, wk(0, false), last ? xout : X2,
+                          last ? os : 0);
+      if (kov) k_overlap(h, k, ops); else ops->push_back(wrap(k));
+    } else            // X + P e + W (r - AP e)
       ops->push_back(wrap(post_op(D.PA, D.r, wk(0, false), clsS, tagA, C.x, X, last ? xout : X2,
                                   last ? os : 0)));
     if (last) return;
@@ -6553,6 +6649,29 @@ int colour_halo_lists(DistHandle* h, const DistLevel& P, const int8_t* gcol, int
   return MAMG_OK;
 }
 
+// the longest run [*r0, *r1) of M's rows whose columns are all < nown (owned:
+// no ghost), for the launches during a halo
+constexpr int64_t K_ROWS_ALIGN = 256;   // launch_msell row ranges: whole workgroups of every LPR
+int ghost_free_run(TmpPool* T, const TBsr& M, int64_t nown, int64_t* r0, int64_t* r1, std::string* err) {
+  int rc;
+  const int64_t n = M.nr;
+  uint8_t* fl = nullptr;
+  if ((rc = T->alloc(&fl, n, err))) return rc;
+  if (n) ghost_row_kernel<<<nblocks(n), 256>>>(n, M.ptr, M.col, (int32_t)nown, fl);
+  HIPCHK(hipGetLastError());
+  std::vector<uint8_t> hf(n);
+  if (n) HIPCHK(hipMemcpy(hf.data(), fl, n, hipMemcpyDeviceToHost));
+  int64_t best0 = 0, best1 = 0, run0 = 0;
+  for (int64_t I = 0; I <= n; ++I)
+    if (I == n || hf[I]) {
+      if (I - run0 > best1 - best0) { best0 = run0; best1 = I; }
+      run0 = I + 1;
+    }
+  *r0 = best0;
+  *r1 = best1;
+  return MAMG_OK;
+}
+
 // level l's A_loc (+ overlap window, band schedule), K / [P | AP] / P, R_loc
 // and W from the GPU hierarchy (the operator block of dist_upload)
 int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPlan& plan, int l, double kw,
@@ -6580,22 +6699,8 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
     if ((rc = dev_rows_to_bsr(&T, Am, nv, nv, nloc, nullptr, P.o0, &raw, err))) return rc;
     if (P.replicated) tA = raw;
     else if ((rc = dev_map_cols(&T, raw, map, nloc, nc, &tA, err))) return rc;
-    if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
-      uint8_t* fl = nullptr;
-      if ((rc = T.alloc(&fl, nloc, err))) return rc;
-      if (nloc) ghost_row_kernel<<<nblocks(nloc), 256>>>(nloc, tA.ptr, tA.col, (int32_t)nloc, fl);
-      HIPCHK(hipGetLastError());
-      std::vector<uint8_t> hf(nloc);
-      if (nloc) HIPCHK(hipMemcpy(hf.data(), fl, nloc, hipMemcpyDeviceToHost));
-      int64_t best0 = 0, best1 = 0, run0 = 0;
-      for (int64_t I = 0; I <= nloc; ++I)
-        if (I == nloc || hf[I]) {
-          if (I - run0 > best1 - best0) { best0 = run0; best1 = I; }
-          run0 = I + 1;
-        }
-      D.ib0 = best0;
-      D.ib1 = best1;
-    }
+    if (!P.replicated && (rc = ghost_free_run(&T, tA, nloc, &D.ib0, &D.ib1, err)))   // overlap window
+      return rc;
     bool half = false;
     if (l == 0 && g_half && tA.nr >= g_sell_min_rows && tA.nb > 0) {   // upload_half_or_bsr
       int* bad = nullptr;
@@ -6648,6 +6753,15 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
       if ((rc = finalize_bsr(h, &T, tK, &D.K, 0, false, err))) return rc;
       if (l == 0 && g_k_sort && D.K.sell && D.K.lpr <= 1)   // rows sorted inside slices (section 4.1)
         if ((rc = sort_sell_slices(h, &T, &D.K, err))) return rc;
+      // K's rows without coarse ghost columns, run while the coarse-e halo is
+      // in flight (level 0's SELL K: launch_msell takes row ranges)
+      if (l == 0 && !P.replicated && !C.replicated) {
+        int64_t k0 = 0, k1 = 0;
+        if ((rc = ghost_free_run(&T, tK, C.nloc, &k0, &k1, err))) return rc;
+        k0 = (k0 + K_ROWS_ALIGN - 1) / K_ROWS_ALIGN * K_ROWS_ALIGN;
+        k1 = k1 == nloc ? nloc : k1 / K_ROWS_ALIGN * K_ROWS_ALIGN;
+        if (k1 > k0) { D.kb0 = k0; D.kb1 = k1; }
+      }
     } else {
       if ((rc = dev_merge_rows(&T, tP, tAP, &tK, err))) return rc;
       if ((rc = finalize_bsr(h, &T, tK, &D.PA, 0, false, err))) return rc;
@@ -6782,19 +6896,29 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, gcol, ncol, err))) return rc;
       if (l == 0 && patches && !D.coarsest && (rc = dist_patches(h.get(), *A0d, P, &D, err))) return rc;
     } else {
-      if (!P.replicated) {      // longest run of rows without ghost columns (overlap window)
+      // longest run of rows without ghost columns (columns < nown): the
+      // overlap windows, as ghost_free_run on the device path
+      auto run_of = [](const HBsr& M, int64_t nown, int64_t* r0, int64_t* r1) {
         int64_t best0 = 0, best1 = 0, run0 = 0;
-        for (int64_t I = 0; I <= P.A.nr; ++I) {
-          bool ghost = I == P.A.nr;
-          for (int64_t k = I < P.A.nr ? P.A.ptr[I] : 0; !ghost && k < P.A.ptr[I + 1]; ++k)
-            ghost = P.A.col[k] >= P.A.nr;
+        for (int64_t I = 0; I <= M.nr; ++I) {
+          bool ghost = I == M.nr;
+          for (int64_t k = I < M.nr ? M.ptr[I] : 0; !ghost && k < M.ptr[I + 1]; ++k)
+            ghost = M.col[k] >= nown;
           if (ghost) {
             if (I - run0 > best1 - best0) { best0 = run0; best1 = I; }
             run0 = I + 1;
           }
         }
-        D.ib0 = best0;
-        D.ib1 = best1;
+        *r0 = best0;
+        *r1 = best1;
+      };
+      if (!P.replicated) run_of(P.A, P.A.nr, &D.ib0, &D.ib1);
+      if (l == 0 && !P.replicated && !plan.levels[1].replicated && P.K.nr > 0) {
+        int64_t k0 = 0, k1 = 0;
+        run_of(P.K, plan.levels[1].nloc, &k0, &k1);
+        k0 = (k0 + K_ROWS_ALIGN - 1) / K_ROWS_ALIGN * K_ROWS_ALIGN;
+        k1 = k1 == P.K.nr ? P.K.nr : k1 / K_ROWS_ALIGN * K_ROWS_ALIGN;
+        if (k1 > k0) { D.kb0 = k0; D.kb1 = k1; }
       }
       if (l == 0) {
         if ((rc = upload_half_or_bsr(h.get(), P.A, &D.A, err))) return rc;

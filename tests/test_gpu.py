@@ -301,6 +301,32 @@ def test_half_band_schedule_bitwise(lib_built, monkeypatch, bands):
     assert its[0] == its[1]
 
 
+@pytest.mark.parametrize('kw', [dict(), dict(smoother='POLY'), dict(cycle_type='W', coarse_scaling=1),
+                                dict(presmooth_iter=2, postsmooth_iter=2, maxit=2)])
+def test_restriction_first_sweep_fused_bitwise(lib_built, monkeypatch, kw):
+    """The coarse levels' first sweep x1 = W b written by the restriction's
+    epilogue (EPI_YBD, one launch fewer per coarse level) is bitwise the
+    separate bd2 launch: applies and the device PCG's history equal."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 32, 1e6)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    outs, its = [], []
+    for f in ('2', '1', '0'):   # default (below level 0), every level, none
+        monkeypatch.setenv('MAMG_FUSE_RBD', f)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
+        outs.append(B * r)
+        solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        solver * r
+        its.append(solver.residuals)
+        B.close()
+    for k in (1, 2):
+        assert np.array_equal(outs[0], outs[k])
+        assert its[0] == its[k]
+    h = mo.setup(A, mo.Params(num_functions=2, **kw), idofs=s.idofs)
+    assert rel(outs[0], h.apply(r)) < APPLY_TOL
+
+
 def test_half_symmetric_rejects_nonsymmetric(lib_built, monkeypatch):
     """A_0 whose 2x2 blocks are symmetric but A_IJ != A_JI in one ulp: the
     mirror check rejects the half format (full SELL-64 is used) and the apply

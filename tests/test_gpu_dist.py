@@ -423,17 +423,20 @@ def test_dist_pcg_virtual_ranks(lib_built, P):
         hh.close()
 
 
-def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch):
+@pytest.mark.parametrize('n,P,sell', [(16, 3, '1'), (32, 2, '1'), (32, 3, str(1 << 20))])
+def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch, n, P, sell):
     """Residual split into the ghost-free row window (run while the halo is
-    in flight) and the boundary rows (after it): bitwise the unsplit apply,
-    for the cycle and the rank SpMV."""
+    in flight) and the boundary rows (after it), and level 0's K split the
+    same way around the coarse-e halo (its rows without coarse ghost columns
+    in 256-row runs, SELL K or the lane-group BSR K): bitwise the unsplit
+    apply, for the cycle and the rank SpMV."""
     import torch
     import metric_amg_examples_amd as M
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
-    s = M.problems.bidomain(3, 16, 1e6)
+    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', sell)
+    s = M.problems.bidomain(3, n, 1e6)
     r = mo.seeded_rhs(s.N)
-    P = 3
     out = []
+    forks = []
     for ov in ('1', '0'):
         monkeypatch.setenv('MAMG_OVERLAP', ov)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
@@ -445,10 +448,15 @@ def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch):
         M.DistMetricAMG.virtual_spmv(hs, rs, ys)
         torch.cuda.synchronize()
         out.append([z.cpu().numpy() for z in zs] + [y.cpu().numpy() for y in ys])
+        forks.append([hh.apply_launches['stream_forks'] for hh in hs])
         for hh in hs:
             hh.close()
     for a, b in zip(out[0], out[1]):
         assert np.array_equal(a, b)
+    assert all(f == 0 for f in forks[1])
+    print('stream forks per apply with the overlap', forks[0])
+    # K's split always; the residual's window with the half-symmetric A (SELL sizes)
+    assert all(f >= (2 if sell == '1' else 1) for f in forks[0])
 
 
 def test_virtual_ranks_band_schedule_bitwise(lib_built, monkeypatch):
