@@ -79,6 +79,53 @@ int main(int argc, char** argv) {
     double t = now() - t0;
     std::printf("pageable hipMemcpy: %.1f ms, %.1f GB/s\n", t * 1e3, bytes / t / 1e9);
   }
+  // is the first copy's extra time the destination's first touch?  a fresh
+  // destination copied into directly, and one written by a device memset first
+  for (int rep = 0; rep < 2; ++rep) {
+    for (int pre : {0, 1}) {
+      void* d2 = nullptr;
+      CK(hipMalloc(&d2, bytes));
+      CK(hipDeviceSynchronize());
+      double t0 = now();
+      if (pre) CK(hipMemsetAsync(d2, 0, bytes, nullptr));
+      CK(hipDeviceSynchronize());
+      double t1 = now();
+      CK(hipMemcpy(d2, src, bytes, hipMemcpyHostToDevice));
+      double t2 = now();
+      std::printf("fresh destination%s: memset %.1f ms + pageable copy %.1f ms (%.1f GB/s)\n",
+                  pre ? " + device memset first" : "", (t1 - t0) * 1e3, (t2 - t1) * 1e3, bytes / (t2 - t1) / 1e9);
+      CK(hipFree(d2));
+    }
+  }
+  // fresh sources through the staged path, pinned buffers' allocation timed
+  // too (what the library pays once per process)
+  for (int rep = 0; rep < 2; ++rep) {
+    char* s3 = (char*)std::aligned_alloc(4096, bytes);
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)(bytes / 8); ++i) ((double*)s3)[i] = (double)i;
+    const size_t ch = (size_t)64 << 20;
+    double t0 = now();
+    void* pb[4];
+    for (auto& p : pb) CK(hipHostMalloc(&p, ch, hipHostMallocDefault));
+    double t1 = now();
+    for (auto& p : pb) CK(hipHostFree(p));
+    const double t = staged(dst, s3, bytes, ch, 4, omp_get_max_threads(), (size_t)64 << 10);
+    std::printf("fresh source, staged 64 MiB x 4, %d threads: %.1f ms (%.1f GB/s); 4 x 64 MiB hipHostMalloc %.1f ms\n",
+                omp_get_max_threads(), t * 1e3, bytes / t / 1e9, (t1 - t0) * 1e3);
+    std::free(s3);
+  }
+  // and a fresh source (the generator's just-written arrays) into the touched dst
+  {
+    char* s2 = (char*)std::aligned_alloc(4096, bytes);
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)(bytes / 8); ++i) ((double*)s2)[i] = (double)i;
+    CK(hipDeviceSynchronize());
+    double t0 = now();
+    CK(hipMemcpy(dst, s2, bytes, hipMemcpyHostToDevice));
+    double t = now() - t0;
+    std::printf("fresh source, touched destination: %.1f ms, %.1f GB/s\n", t * 1e3, bytes / t / 1e9);
+    std::free(s2);
+  }
   // a reference: device copy rate from a pinned buffer (PCIe ceiling)
   {
     void* pin = nullptr;
