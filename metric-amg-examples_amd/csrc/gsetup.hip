@@ -667,12 +667,25 @@ __device__ __forceinline__ uint32_t hash_insert(int32_t* keys, int32_t j, bool* 
   }
 }
 
+// one-pass staging of the count pass (spgemm_gl): a row of at most `stride`
+// entries is written, rank-sorted, at row * stride (st[row] = 1) while its
+// count is taken, so the fill pass only compacts it (stage_copy_kernel); a
+// longer row is listed in ulist for the fill launch
+struct SpStage {
+  int32_t* col = nullptr;   // nullptr: no staging (two passes)
+  double* val = nullptr;
+  int64_t stride = 0;
+  uint8_t* st = nullptr;
+  int32_t* ulist = nullptr;
+  int* uctr = nullptr;
+};
+
 template <int TS, int WPB, bool FILL, int GL, class BS>
 __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
     int64_t nrows, const int32_t* __restrict__ rows, const int64_t* __restrict__ ub, int64_t lim,
     const int64_t* __restrict__ aptr, const int32_t* __restrict__ acol, const double* __restrict__ aval,
     BS B, int64_t* cptr, int32_t* __restrict__ ccol, double* __restrict__ cval, int* overflow,
-    int32_t* spill) {
+    int32_t* spill, SpStage stg = SpStage()) {
   constexpr int NG = 64 / GL;
   __shared__ int32_t keys[WPB][TS];
   __shared__ double sums[WPB][TS];
@@ -755,17 +768,29 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int m = cnt[w];
+    int32_t* oc = ccol;
+    double* ov = cval;
+    int64_t base = 0;
     if (!FILL) {
       if (lane == 0) cptr[i + 1] = m;
-      continue;
+      if (!stg.col) continue;
+      if (m > stg.stride) {                  // too long to stage: the fill launch does it
+        if (lane == 0) stg.ulist[atomicAdd(stg.uctr, 1)] = (int32_t)i;
+        continue;
+      }
+      if (lane == 0) stg.st[i] = 1;
+      oc = stg.col;
+      ov = stg.val;
+      base = i * stg.stride;
+    } else {
+      base = cptr[i];
     }
-    const int64_t base = cptr[i];
     for (int e = lane; e < m; e += 64) {     // rank sort by column
       const int32_t key = ck[w][e];
       int rank = 0;
       for (int t = 0; t < m; ++t) rank += ck[w][t] < key;
-      ccol[base + rank] = key;
-      cval[base + rank] = cv[w][e];
+      oc[base + rank] = key;
+      ov[base + rank] = cv[w][e];
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1484,6 +1509,25 @@ struct Clock {
 
 int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
 
+// staged rows into place: row i's m = ptr[i + 1] - ptr[i] entries from
+// scol / sval at i * S (S lanes per row)
+template <int S>
+__global__ __launch_bounds__(256) void stage_copy_kernel(int64_t n, const uint8_t* __restrict__ st,
+                                                         const int32_t* __restrict__ scol,
+                                                         const double* __restrict__ sval,
+                                                         const int64_t* __restrict__ ptr, int32_t* __restrict__ col,
+                                                         double* __restrict__ val) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = t / S;
+  const int e = (int)(t % S);
+  if (i >= n || !st[i]) return;
+  const int64_t p0 = ptr[i];
+  if (e < ptr[i + 1] - p0) {
+    col[p0 + e] = scol[i * S + e];
+    val[p0 + e] = sval[i * S + e];
+  }
+}
+
 // exact output size + row pointers + entries of C = A B (hash SpGEMM).
 // Optimistic tiering: every row first runs in a 128-slot table (4 waves per
 // block, 12 KB of LDS, so LDS no longer caps the waves per CU); a row whose
@@ -1494,17 +1538,52 @@ int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, e
 // the table size, so every tier gives the same bits.  (Binning by the
 // product-count upper bound sent most Galerkin rows, whose product counts far
 // exceed their distinct counts, to the slow large-table launch.)
+// One pass for most rows (round 5): the tier-0 count pass also writes each
+// row of at most `stride` entries into a staging area (SpStage), and the fill
+// pass compacts those instead of recomputing them; the rows above `stride`
+// (ulist) and the spilled tiers keep the count + fill passes.  The staging
+// area is n * stride entries, stride the largest of 128 / 64 / 32 / 16 within
+// MAMG_SPGEMM_STAGE_GB (default 16; 0: two passes everywhere) and a quarter
+// of the free HBM (MAMG_SPGEMM_STAGE_STRIDE caps it: tests of the long-row
+// list).  Same kernel code, same rank sort: the same bits.
+int64_t spgemm_stage_stride(int64_t n) {
+  const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
+  const double cap_gb = e ? std::atof(e) : 16.0;
+  e = std::getenv("MAMG_SPGEMM_STAGE_STRIDE");
+  const int64_t smax = e ? std::atoll(e) : 128;
+  if (cap_gb <= 0.0 || n <= 0) return 0;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  const double cap = std::min(cap_gb * 1e9, 0.25 * (double)fr);
+  for (int64_t s : {128, 64, 32, 16})
+    if (s <= smax && (double)n * (double)s * 12.0 <= cap) return s;
+  return 0;
+}
+
 template <int GL, class BS>
 int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
   constexpr int TS0 = 128, TS1 = 512, TS2 = 2048;
   const int64_t n = A.n;
   Scratch S;
   int32_t *l1 = nullptr, *l2 = nullptr;
-  int* ctr = nullptr;   // [0] rows spilled by tier 0, [1] tier-2 overflow, [2] rows spilled by tier 1
+  int* ctr = nullptr;   // [0] rows spilled by tier 0, [1] tier-2 overflow, [2] rows spilled by tier 1, [3] fill
   RCHK(S.alloc(&l1, n, err));
   RCHK(S.alloc(&l2, n, err));
-  RCHK(S.alloc(&ctr, 4, err));
-  HIPCHK(dev_memset(ctr, 0, 4 * sizeof(int)));
+  RCHK(S.alloc(&ctr, 5, err));
+  HIPCHK(dev_memset(ctr, 0, 5 * sizeof(int)));
+  SpStage stg;
+  stg.stride = spgemm_stage_stride(n);
+  int32_t* l3 = nullptr;
+  int n3 = 0;
+  if (stg.stride) {
+    RCHK(S.alloc(&stg.col, n * stg.stride, err));
+    RCHK(S.alloc(&stg.val, n * stg.stride, err));
+    RCHK(S.alloc(&stg.st, n, err));
+    RCHK(S.alloc(&l3, n, err));
+    HIPCHK(dev_memset(stg.st, 0, (size_t)n));
+    stg.ulist = l3;
+    stg.uctr = ctr + 4;
+  }
   C->n = n;
   C->m = ncols;
   RCHK(galloc(G, &C->ptr, n + 1, err));
@@ -1523,9 +1602,10 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
     double* cv = pass ? C->val : nullptr;
     if (pass == 0) {
       spgemm_kernel<TS0, 4, false, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
-                                                ctr, l1);
+                                                ctr, l1, stg);
       HIPCHK(hipGetLastError());
       RCHK(read_int(ctr, &n1, err));
+      if (stg.stride) RCHK(read_int(ctr + 4, &n3, err));
       if (n1) {
         const unsigned g1 = (unsigned)std::min<int64_t>((n1 + 3) / 4, 65536);
         spgemm_kernel<TS1, 4, false, GL><<<g1, 256>>>(n1, l1, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
@@ -1537,8 +1617,21 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
         spgemm_kernel<TS2, 1, false, GL><<<(unsigned)std::min<int64_t>(n2, 65536), 64>>>(
             n2, l2, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr, nullptr);
     } else {
-      spgemm_kernel<TS0, 4, true, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
-                                               ctr + 3, l1);
+      if (!stg.stride) {
+        spgemm_kernel<TS0, 4, true, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
+                                                 ctr + 3, l1);
+      } else {
+        const unsigned gs = (unsigned)((n * stg.stride + 255) / 256);
+        switch (stg.stride) {
+          case 128: stage_copy_kernel<128><<<gs, 256>>>(n, stg.st, stg.col, stg.val, cp, cc, cv); break;
+          case 64: stage_copy_kernel<64><<<gs, 256>>>(n, stg.st, stg.col, stg.val, cp, cc, cv); break;
+          case 32: stage_copy_kernel<32><<<gs, 256>>>(n, stg.st, stg.col, stg.val, cp, cc, cv); break;
+          default: stage_copy_kernel<16><<<gs, 256>>>(n, stg.st, stg.col, stg.val, cp, cc, cv); break;
+        }
+        if (n3)   // tier-0 rows longer than the stride
+          spgemm_kernel<TS0, 4, true, GL><<<(unsigned)std::min<int64_t>((n3 + 3) / 4, 65536), 256>>>(
+              n3, l3, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr + 3, l1);
+      }
       if (n1)
         spgemm_kernel<TS1, 4, true, GL><<<(unsigned)std::min<int64_t>((n1 + 3) / 4, 65536), 256>>>(
             n1, l1, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr + 3, l2);
