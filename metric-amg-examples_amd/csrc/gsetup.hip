@@ -1515,6 +1515,141 @@ struct Clock {
 
 int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
 
+// The count + staging pass over row pairs (i, i + h) of a field-major
+// 2-function matrix (round 5): when the two rows hold the same columns (the
+// 2 x 2 node blocks of A_l, and of R = P^T), the wave loads each B row once
+// for both, inserts its columns once, and accumulates two sums per slot.
+// Each sum takes exactly its scalar row's terms in the same order (the same
+// batches, the same group-serialised adds), the table holds the same keys
+// (so the same tier), and each row is extracted and staged as alone: the
+// bits of spgemm_kernel row by row.  Pairs whose columns differ are listed
+// (mism) for spgemm_kernel; a full table spills both rows.
+template <int TS, int WPB, int GL, class BS>
+__global__ __launch_bounds__(64 * WPB) void spgemm_pair_kernel(
+    int64_t h, const int64_t* __restrict__ aptr, const int32_t* __restrict__ acol, const double* __restrict__ aval,
+    BS B, int64_t* cptr, int* overflow, int32_t* spill, SpStage stg, int32_t* mism, int* nmism) {
+  constexpr int NG = 64 / GL;
+  __shared__ int32_t keys[WPB][TS];
+  __shared__ double sums[WPB][2][TS];
+  __shared__ int32_t ck[WPB][TS];
+  __shared__ double cv[WPB][TS];
+  __shared__ int cnt[WPB];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane / GL, sub = lane % GL;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  for (int64_t pr = (int64_t)blockIdx.x * WPB + w; pr < h; pr += nw) {
+    const int64_t i0 = pr, i1 = pr + h;
+    const int64_t p0 = aptr[i0], p1 = aptr[i1], L = aptr[i0 + 1] - p0;
+    bool diff = aptr[i1 + 1] - p1 != L;
+    if (!diff) {
+      bool d = false;
+      for (int64_t t = lane; t < L; t += 64) d |= acol[p0 + t] != acol[p1 + t];
+      diff = __any(d);
+    }
+    if (diff) {
+      if (lane == 0) {
+        const int q = atomicAdd(nmism, 2);
+        mism[q] = (int32_t)i0;
+        mism[q + 1] = (int32_t)i1;
+      }
+      continue;
+    }
+    for (int s = lane; s < TS; s += 64) { keys[w][s] = -1; sums[w][0][s] = 0.0; sums[w][1][s] = 0.0; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    bool full = false;
+    for (int64_t kb = 0; kb < L; kb += NG) {
+      int64_t k = 0, len = 0;
+      double a0 = 0.0, a1 = 0.0;
+      if (kb + g < L) { k = acol[p0 + kb + g]; a0 = aval[p0 + kb + g]; a1 = aval[p1 + kb + g]; len = B.len(k); }
+      if (NG > 1 && !__any(len > GL)) {
+        const bool act = sub < len;
+        int32_t j = 0;
+        double bv = 0.0;
+        uint32_t slot = 0;
+        if (act) {
+          B.get(k, sub, &j, &bv);
+          slot = hash_insert<TS>(keys[w], j, &full);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (__any(full)) break;
+        for (int gg = 0; gg < NG; ++gg) {       // groups add in CSR order
+          if (g == gg && act) {
+            sums[w][0][slot] = sums[w][0][slot] + a0 * bv;
+            sums[w][1][slot] = sums[w][1][slot] + a1 * bv;
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        continue;
+      }
+      for (int gg = 0; gg < NG && kb + gg < L; ++gg) {   // one entry at a time
+        const int64_t k1 = acol[p0 + kb + gg];
+        const double x0 = aval[p0 + kb + gg], x1 = aval[p1 + kb + gg];
+        const int64_t len1 = B.len(k1);
+        for (int64_t t0 = 0; t0 < len1; t0 += 64) {
+          const int64_t t = t0 + lane;
+          if (t < len1) {
+            int32_t j;
+            double bv;
+            B.get(k1, t, &j, &bv);
+            const uint32_t slot = hash_insert<TS>(keys[w], j, &full);
+            if (!full) {
+              sums[w][0][slot] = sums[w][0][slot] + x0 * bv;
+              sums[w][1][slot] = sums[w][1][slot] + x1 * bv;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        if (__any(full)) break;
+      }
+      if (__any(full)) break;
+    }
+    if (__any(full)) {   // both rows to the next tier
+      if (lane == 0) {
+        const int q = atomicAdd(overflow, 2);
+        spill[q] = (int32_t)i0;
+        spill[q + 1] = (int32_t)i1;
+      }
+      continue;
+    }
+    for (int r = 0; r < 2; ++r) {
+      const int64_t i = r ? i1 : i0;
+      if (lane == 0) cnt[w] = 0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int s = lane; s < TS; s += 64) {   // nonzero entries (scipy drops exact zeros)
+        if (keys[w][s] != -1 && sums[w][r][s] != 0.0) {
+          const int q = atomicAdd(&cnt[w], 1);
+          ck[w][q] = keys[w][s];
+          cv[w][q] = sums[w][r][s];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const int m = cnt[w];
+      if (lane == 0) cptr[i + 1] = m;
+      if (m > stg.stride) {
+        if (lane == 0) stg.ulist[atomicAdd(stg.uctr, 1)] = (int32_t)i;
+      } else {
+        if (lane == 0) stg.st[i] = 1;
+        const int64_t base = i * stg.stride;
+        for (int e = lane; e < m; e += 64) {     // rank sort by column
+          const int32_t key = ck[w][e];
+          int rank = 0;
+          for (int t = 0; t < m; ++t) rank += ck[w][t] < key;
+          stg.col[base + rank] = key;
+          stg.val[base + rank] = cv[w][e];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  }
+}
+
 // staged rows into place: row i's m = ptr[i + 1] - ptr[i] entries from
 // scol / sval at i * S (S lanes per row)
 template <int S>
@@ -1552,6 +1687,12 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(int64_t n, const uint8_
 // MAMG_SPGEMM_STAGE_GB (default 16; 0: two passes everywhere) and a quarter
 // of the free HBM (MAMG_SPGEMM_STAGE_STRIDE caps it: tests of the long-row
 // list).  Same kernel code, same rank sort: the same bits.
+// MAMG_SPGEMM_PAIR=0: the staged count pass row by row (A/B, tests)
+bool spgemm_pair_on() {
+  const char* e = std::getenv("MAMG_SPGEMM_PAIR");
+  return e ? std::atoi(e) != 0 : true;
+}
+
 int64_t spgemm_stage_stride(int64_t n) {
   const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
   const double cap_gb = e ? std::atof(e) : 16.0;
@@ -1566,8 +1707,10 @@ int64_t spgemm_stage_stride(int64_t n) {
   return 0;
 }
 
+// pair: A is a field-major 2-function matrix (rows i, i + n / 2 of node i):
+// the staged count pass runs over row pairs (spgemm_pair_kernel)
 template <int GL, class BS>
-int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err) {
+int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, bool pair) {
   constexpr int TS0 = 128, TS1 = 512, TS2 = 2048;
   const int64_t n = A.n;
   Scratch S;
@@ -1607,8 +1750,24 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
     int32_t* cc = pass ? C->col : nullptr;
     double* cv = pass ? C->val : nullptr;
     if (pass == 0) {
-      spgemm_kernel<TS0, 4, false, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
-                                                ctr, l1, stg);
+      if (pair && stg.stride && n % 2 == 0 && spgemm_pair_on()) {
+        int32_t* lm = nullptr;
+        int* nm = nullptr;
+        RCHK(S.alloc(&lm, n, err));
+        RCHK(S.alloc(&nm, 1, err));
+        HIPCHK(dev_memset(nm, 0, sizeof(int)));
+        const unsigned gp = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n / 2 + 3) / 4), 65536);
+        spgemm_pair_kernel<TS0, 4, GL><<<gp, 256>>>(n / 2, A.ptr, A.col, A.val, B, cp, ctr, l1, stg, lm, nm);
+        HIPCHK(hipGetLastError());
+        int hm = 0;
+        RCHK(read_int(nm, &hm, err));
+        if (hm)   // pairs with different columns: row by row
+          spgemm_kernel<TS0, 4, false, GL><<<(unsigned)std::min<int64_t>((hm + 3) / 4, 65536), 256>>>(
+              hm, lm, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv, ctr, l1, stg);
+      } else {
+        spgemm_kernel<TS0, 4, false, GL><<<g0, 256>>>(n, nullptr, nullptr, 0, A.ptr, A.col, A.val, B, cp, cc, cv,
+                                                  ctr, l1, stg);
+      }
       HIPCHK(hipGetLastError());
       RCHK(read_int(ctr, &n1, err));
       if (stg.stride) RCHK(read_int(ctr + 4, &n3, err));
@@ -1659,11 +1818,12 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
 
 // lane-group width from B's mean row length (most B rows fit one group)
 template <class BS>
-int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, double blen) {
-  if (blen <= 1.5) return spgemm_gl<2>(G, A, B, ncols, C, err);
-  if (blen <= 5.0) return spgemm_gl<8>(G, A, B, ncols, C, err);
-  if (blen <= 11.0) return spgemm_gl<16>(G, A, B, ncols, C, err);
-  return spgemm_gl<32>(G, A, B, ncols, C, err);
+int spgemm(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, double blen,
+           bool pair = false) {
+  if (blen <= 1.5) return spgemm_gl<2>(G, A, B, ncols, C, err, pair);
+  if (blen <= 5.0) return spgemm_gl<8>(G, A, B, ncols, C, err, pair);
+  if (blen <= 11.0) return spgemm_gl<16>(G, A, B, ncols, C, err, pair);
+  return spgemm_gl<32>(G, A, B, ncols, C, err, pair);
 }
 
 // R = P^T (setup.cpp transpose: counting order == stable sort by column)
@@ -2556,7 +2716,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
       L.w_sa = w;
       GHier tmp;                    // A T lives only until P is built
       DevMat AT;
-      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, 2 * nagg, &AT, err, 1.0));
+      RCHK(spgemm(&tmp, cur, BTent{agg, nv, nagg}, 2 * nagg, &AT, err, 1.0, true));
       L.P.n = n;
       L.P.m = 2 * nagg;
       RCHK(galloc(G, &L.P.ptr, n + 1, err));
@@ -2609,9 +2769,11 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
     G->phase_ms[2] += clk.lap();
     // Galerkin: R = P^T, A P, A_c = R (A P)
     RCHK(transpose(G, L.P, &L.R, err));
-    RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err, (double)L.P.nnz / std::max<int64_t>(1, L.P.n)));
+    RCHK(spgemm(G, cur, BCsr{L.P.ptr, L.P.col, L.P.val}, L.P.m, &L.AP, err, (double)L.P.nnz / std::max<int64_t>(1, L.P.n),
+                nodal));
     DevMat next;
-    RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err, (double)L.AP.nnz / std::max<int64_t>(1, L.AP.n)));
+    RCHK(spgemm(G, L.R, BCsr{L.AP.ptr, L.AP.col, L.AP.val}, L.AP.m, &next, err, (double)L.AP.nnz / std::max<int64_t>(1, L.AP.n),
+                nodal));
     if (!p.post_fusion || !nodal) {   // host: A P kept for the fused post-smoothing of nodal levels
       for (void* q : {(void*)L.AP.ptr, (void*)L.AP.col, (void*)L.AP.val}) G->release(q);
       L.AP = DevMat();

@@ -73,18 +73,21 @@ def test_gpu_hierarchy_bitwise_equals_host(lib_built, dim, n, g, kw):
     Hg.close()
 
 
-@pytest.mark.parametrize('stage', [('16', '16'), ('16', '128'), ('0', '128')])
+@pytest.mark.parametrize('stage', [('16', '16', '1'), ('16', '128', '1'), ('16', '128', '0'), ('0', '128', '1')])
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e4, dict(aggregation_type=5)),
                                         (3, 16, 1e6, dict(AMG_type=1))])
 def test_gpu_spgemm_staging_bitwise(lib_built, monkeypatch, dim, n, g, kw, stage):
     """The one-pass SpGEMM (count pass staging rows of <= stride entries,
-    compacted after the scan; longer rows through the fill launch): stride
-    16 (most Galerkin rows take the long-row list), the default stride, and
-    staging off all give the host setup's hierarchy bit for bit."""
+    compacted after the scan; longer rows through the fill launch), with
+    the node's two rows of the 2-function matrices taken together
+    (spgemm_pair_kernel) or row by row: stride 16 (most Galerkin rows take
+    the long-row list), the default stride, pairs off, and staging off all
+    give the host setup's hierarchy bit for bit."""
     M = _mamg()
-    gb, stride = stage
+    gb, stride, pair = stage
     monkeypatch.setenv('MAMG_SPGEMM_STAGE_GB', gb)
     monkeypatch.setenv('MAMG_SPGEMM_STAGE_STRIDE', stride)
+    monkeypatch.setenv('MAMG_SPGEMM_PAIR', pair)
     s = M.problems.bidomain(dim, n, g)
     Hh = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **kw)
     Hg = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True, **kw)
