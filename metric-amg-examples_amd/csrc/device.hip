@@ -1957,6 +1957,8 @@ int g_r_bands = 1;
 int g_k_sort = 1;
 int g_post_k = 1;
 int g_kvar = 0;
+__global__ void warm_kernel() {}
+
 // MAMG_FUSE_RBD: which restrictions write the next level's first sweep
 // (EPI_YBD): 2 those below level 0 (default), 1 all, 0 none.  A/B at
 // nrefs=6 (profiles/r05_fuse_rbd_ab.txt, 3 x 3 alternating runs): coarse
@@ -6205,6 +6207,11 @@ void dspmv_ops(const DistHandle* h, const double* x, double* y, std::vector<DOp>
 }
 
 }  // namespace
+
+void device_warm(void* stream) {
+  warm_kernel<<<1, 64, 0, (hipStream_t)stream>>>();
+  (void)hipGetLastError();
+}
 
 int dist_get_unique_id(void* id, std::string* err) {
   ncclUniqueId u;

@@ -59,6 +59,22 @@ void scratch_put(void* p) {
 }
 }  // namespace
 
+void dprims_warm(void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int64_t* buf = nullptr;
+  size_t bytes = 0;
+  if (hipcub::DeviceScan::InclusiveSum(nullptr, bytes, buf, buf, (size_t)1, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  void* p = nullptr;   // two words + the scan's storage, kept for the process (no hipFree here)
+  if (dev_malloc(&p, 64 + bytes, "scratch") != hipSuccess) { (void)hipGetLastError(); return; }
+  buf = (int64_t*)p;
+  if (hipMemsetAsync(buf, 0, 16, s) != hipSuccess ||
+      hipcub::DeviceScan::InclusiveSum((char*)p + 64, bytes, buf, buf + 1, (size_t)1, s) != hipSuccess)
+    (void)hipGetLastError();
+}
+
 // out[i] = in[0] + ... + in[i]  (in == out allowed)
 int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std::string* err) {
   if (n <= 0) return MAMG_OK;

@@ -96,6 +96,11 @@ enum { GS_AGGREGATE = 0, GS_SMOOTHER = 1, GS_PROLONG = 2, GS_GALERKIN = 3, GS_CO
 
 // device primitives (dprims.hip)
 int dscan_incl_i64(const int64_t* in, int64_t* out, int64_t n, void* stream, std::string* err);
+// one tiny scan on `stream` (its own buffers, kept): loads dprims' code
+// object, which the runtime defers to the first launch (gsetup.hip warm_modules)
+void dprims_warm(void* stream);
+// one empty kernel of device.hip on `stream` (the same, for its code object)
+void device_warm(void* stream);
 int dsort_pairs_i32_i64(const int32_t* kin, int32_t* kout, const int64_t* vin, int64_t* vout,
                         int64_t n, int key_bits, void* stream, std::string* err);
 int dsort_pairs_u64_i64(const uint64_t* kin, uint64_t* kout, const int64_t* vin, int64_t* vout,

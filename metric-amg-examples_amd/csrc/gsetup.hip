@@ -41,7 +41,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
+#include <thread>
 
 #include "dist.h"
 #include "dmem.h"
@@ -2551,6 +2553,37 @@ int ring_blocks_dev(const DevMat& A, const int32_t* seeds, int64_t ns, int maxlv
   return MAMG_OK;
 }
 
+// The runtime loads a translation unit's code object at the first launch of
+// one of its kernels (deferred loading).  dprims' (the hipCUB scans and
+// sorts) took 46 ms inside the aggregation phase at nrefs=6, gsetup.hip's and
+// device.hip's ~5-6 ms each (profiles/r05_setup_gaps.txt).  A helper
+// thread launches one kernel of each while the host copies A_0 (or while the
+// setup's first kernels run), once per device and process.
+__global__ void gsetup_warm_kernel() {}
+
+struct ModuleWarm {
+  std::thread t;
+  explicit ModuleWarm(int dev) {
+    static std::atomic<uint64_t> done{0};
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.fetch_or(bit) & bit) return;
+    t = std::thread([dev] {
+      if (hipSetDevice(dev) != hipSuccess) { (void)hipGetLastError(); return; }
+      hipStream_t s = nullptr;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { (void)hipGetLastError(); return; }
+      gsetup_warm_kernel<<<1, 64, 0, s>>>();
+      dprims_warm(s);
+      device_warm(s);
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+      (void)hipGetLastError();
+    });
+  }
+  ~ModuleWarm() {
+    if (t.joinable()) t.join();
+  }
+};
+
 int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mamg_params& p, GHier* G,
               std::string* err) {
   int rc = check_params(p, err);
@@ -2568,6 +2601,7 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
   }
   G->params = p;
   G->device = p.device;
+  ModuleWarm warm(p.device);   // no-op when the A_0 upload did it
   G->levels.clear();
   G->seeds.clear();
   G->generic = false;
@@ -2977,6 +3011,7 @@ int gen_bidomain_dev(int dim, int64_t n, double gamma, double k1, double k2, int
 
 int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   HIPCHK(hipSetDevice(G->device));
+  ModuleWarm warm(G->device);
   Clock clk;
   D->n = A.n;
   D->m = A.m;
