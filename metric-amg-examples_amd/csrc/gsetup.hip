@@ -221,6 +221,18 @@ __global__ __launch_bounds__(256) void strength_kernel(int64_t n, const int64_t*
 }
 
 // ---------------------------------------------------------------------------
+// Sharded single-word reductions: one atomic per wave on one word serialises
+// at ~88 per microsecond (MI355X_MICROARCH.md, dequeue), so a 17 M-node grid's
+// 265 K wave atomics took ~3 ms (the MIS-2 key kernel: 3.17 ms per round for
+// 24 B per node).  The waves of block b add into shard b mod 64 (128 B
+// apart); the host sums (or maxes) the 64 shards.
+// ---------------------------------------------------------------------------
+constexpr int CSH = 64, CSTR = 16;
+__device__ __forceinline__ unsigned long long* shard_of(unsigned long long* c) {
+  return c + (blockIdx.x & (CSH - 1)) * CSTR;
+}
+
+// ---------------------------------------------------------------------------
 // MIS-2 aggregation (setup.cpp aggregate_mis2)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mis_init_kernel(int64_t n, const int64_t* __restrict__ ptr,
@@ -246,7 +258,7 @@ __global__ __launch_bounds__(256) void mis_key_kernel(int64_t n, const uint64_t*
     u = state[i] == ST_UND;
   }
   const unsigned long long b = __ballot(u);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(und, (unsigned long long)__popcll(b));
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(shard_of(und), (unsigned long long)__popcll(b));
 }
 
 __global__ __launch_bounds__(256) void mis_max_kernel(int64_t n, const int64_t* __restrict__ ptr,
@@ -393,7 +405,7 @@ __global__ __launch_bounds__(256) void hem_mutual_kernel(int64_t n, const int64_
     if (c >= 0 && choice[c] == i) { mate[i] = c; m = true; }
   }
   const unsigned long long b = __ballot(m);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(got, (unsigned long long)__popcll(b));
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(shard_of(got), (unsigned long long)__popcll(b));
 }
 
 // root = smallest member of a pair (or the unmatched node itself)
@@ -623,7 +635,7 @@ __global__ __launch_bounds__(64) void block_rho_kernel(int64_t nv, const int64_t
   // wave max first (the sums are >= +0, so the max is exact in any order),
   // then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(rho_bits, (unsigned long long)__double_as_longlong(s));
+  if ((threadIdx.x & 63) == 0) atomicMax(shard_of(rho_bits), (unsigned long long)__double_as_longlong(s));
 }
 
 __global__ __launch_bounds__(256) void scale_blocks_kernel(int64_t nv, double sc, const dv4_t* __restrict__ D,
@@ -1284,7 +1296,7 @@ __global__ __launch_bounds__(256) void rowabs_max_kernel(int64_t n, const int64_
     for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
       if (val[k] != 0.0) s += fabs(val[k]) * 1.0;
   for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(bits, (unsigned long long)__double_as_longlong(s));
+  if ((threadIdx.x & 63) == 0) atomicMax(shard_of(bits), (unsigned long long)__double_as_longlong(s));
 }
 
 __global__ __launch_bounds__(256) void scale_vals_kernel(int64_t n, double sc, double* __restrict__ v) {
@@ -1516,6 +1528,24 @@ struct Clock {
 };
 
 int read_int(const int* d, int* h, std::string* err) { return to_host(h, d, 1, err); }
+
+// a sharded counter (shard_of): allocate / zero, then read its sum or max
+int shards_alloc(Scratch* S, unsigned long long** c, std::string* err) {
+  RCHK(S->alloc(c, CSH * CSTR, err));
+  HIPCHK(dev_memset(*c, 0, CSH * CSTR * sizeof(unsigned long long)));
+  return MAMG_OK;
+}
+int shards_zero(unsigned long long* c) {
+  return dev_memset(c, 0, CSH * CSTR * sizeof(unsigned long long)) == hipSuccess ? MAMG_OK : MAMG_ERR_HIP;
+}
+int shards_read(const unsigned long long* c, bool max, unsigned long long* out, std::string* err) {
+  unsigned long long h[CSH * CSTR];
+  RCHK(to_host(h, c, CSH * CSTR, err));
+  unsigned long long r = 0;
+  for (int k = 0; k < CSH; ++k) r = max ? std::max(r, h[k * CSTR]) : r + h[k * CSTR];
+  *out = r;
+  return MAMG_OK;
+}
 
 // The count + staging pass over row pairs (i, i + h) of a field-major
 // 2-function matrix (round 5): when the two rows hold the same columns (the
@@ -1877,12 +1907,11 @@ int transpose(GHier* G, const DevMat& P, DevMat* R, std::string* err) {
 int block_rho(const DevMat& A, int64_t nv, const dv4_t* D, double* rho, std::string* err) {
   Scratch S;
   unsigned long long* rb = nullptr;
-  RCHK(S.alloc(&rb, 1, err));
-  HIPCHK(dev_memset(rb, 0, sizeof(unsigned long long)));
+  RCHK(shards_alloc(&S, &rb, err));
   block_rho_kernel<<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, D, rb);
   HIPCHK(hipGetLastError());
   unsigned long long h = 0;
-  RCHK(to_host(&h, rb, 1, err));
+  RCHK(shards_read(rb, true, &h, err));
   std::memcpy(rho, &h, sizeof(double));
   return MAMG_OK;
 }
@@ -1943,7 +1972,7 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
   iota_nonisol_kernel<<<nblk(n), 256>>>(n, act, agg);
   int64_t nagg = n;
   unsigned long long* got = nullptr;
-  RCHK(S.alloc(&got, 1, err));
+  RCHK(shards_alloc(&S, &got, err));
   for (int ps = 0; ps < PASSES; ++ps) {
     const int64_t m = W.n;
     int64_t *mate = nullptr, *choice = nullptr, *f = nullptr, *a = nullptr;
@@ -1953,12 +1982,12 @@ int aggregate_hem_dev(GHier* G, const DevMat& Gr, const uint8_t* flag, int level
     RCHK(S.alloc(&a, m, err));
     HIPCHK(dev_memset(mate, 0xff, m * sizeof(int64_t)));
     for (int round = 0; round < MAX_ROUNDS; ++round) {
-      HIPCHK(dev_memset(got, 0, sizeof(unsigned long long)));
+      RCHK(shards_zero(got));
       hem_pick_kernel<<<nblk(m), 256>>>(m, W.ptr, W.col, W.val, act, mate, 16 * level + ps, choice);
       hem_mutual_kernel<<<nblk(m), 256>>>(m, choice, mate, got);
       HIPCHK(hipGetLastError());
       unsigned long long hg = 0;
-      RCHK(to_host(&hg, got, 1, err));
+      RCHK(shards_read(got, false, &hg, err));
       if (!hg) break;
     }
     hem_root_kernel<<<nblk(m), 256>>>(m, act, mate, f);
@@ -2099,15 +2128,15 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   RCHK(S.alloc(&low, nv, err));
   RCHK(S.alloc(&key, nv, err));
   RCHK(S.alloc(&m1, nv, err));
-  RCHK(S.alloc(&und, 1, err));
+  RCHK(shards_alloc(&S, &und, err));
   mis_init_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, flag, level, state, low, nonisol);
   for (int rounds = 0;; ++rounds) {
     if (rounds > 10000) { *err = "mis2 did not converge"; return MAMG_ERR_SETUP; }
-    HIPCHK(dev_memset(und, 0, sizeof(unsigned long long)));
+    RCHK(shards_zero(und));
     mis_key_kernel<<<nblk(nv), 256>>>(nv, state, low, key, und);
     HIPCHK(hipGetLastError());
     unsigned long long hu = 0;
-    RCHK(to_host(&hu, und, 1, err));
+    RCHK(shards_read(und, false, &hu, err));
     if (hu == 0) break;
     mis_max_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, key, m1);
     mis_update_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
@@ -2354,12 +2383,11 @@ int block_rho_dev(const DevMat& D, const DevMat& A, double* rho, std::string* er
   RCHK(spgemm(&tmp, D, BCsr{A.ptr, A.col, A.val}, A.m, &C, err, A.n ? (double)A.nnz / (double)A.n : 1.0));
   Scratch S;
   unsigned long long* bits = nullptr;
-  RCHK(S.alloc(&bits, 1, err));
-  HIPCHK(dev_memset(bits, 0, sizeof(unsigned long long)));
+  RCHK(shards_alloc(&S, &bits, err));
   rowabs_max_kernel<<<nblk(C.n), 256>>>(C.n, C.ptr, C.val, bits);
   HIPCHK(hipGetLastError());
   unsigned long long h = 0;
-  RCHK(to_host(&h, bits, 1, err));
+  RCHK(shards_read(bits, true, &h, err));
   std::memcpy(rho, &h, sizeof(double));
   return MAMG_OK;
 }
