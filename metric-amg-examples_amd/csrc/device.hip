@@ -2421,7 +2421,7 @@ __global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, con
                                                      const int32_t* __restrict__ col,
                                                      const double* __restrict__ val, int64_t* bptr,
                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
-  __shared__ RowStage S;     // rowstage.h: the wave's rows staged through LDS
+  __shared__ RowStageT<FILL> S;   // rowstage.h: the wave's rows staged through LDS
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nr, I0, vw);

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_
                                                         const int32_t* __restrict__ col,
                                                         const double* __restrict__ val, int64_t* gptr,
                                                         int32_t* __restrict__ gcol, double* __restrict__ gval) {
-  __shared__ RowStage S;
+  __shared__ RowStageT<FILL> S;
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nv, I0, vw);

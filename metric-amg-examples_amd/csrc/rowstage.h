@@ -21,10 +21,14 @@ namespace mamg {
 constexpr int RS_NODES = 64;     // nodes per wave (= workgroup)
 constexpr int RS_CAP = 2048;     // staged entries per field (A0: ~1900)
 
-struct RowStage {
+// VALS false (the count passes): columns only, 16 KB instead of 48 KB of LDS
+// per workgroup, so 3 -> 10 waves per CU
+template <bool VALS>
+struct RowStageT {
   int32_t c[2][RS_CAP];
-  double v[2][RS_CAP];
+  double v[2][VALS ? RS_CAP : 1];
 };
+using RowStage = RowStageT<true>;
 
 // Row view of one field: entry k of the field's rows is LC[k - off],
 // LV[k - off] in the staged LDS copy (lds), else C[k], V[k] in global memory.
@@ -54,7 +58,7 @@ struct RowView {
 // fills view[2] (LDS when the ranges fit, else global).  Every lane of the
 // wave must call it (the loads and the barrier are wave-wide).
 template <bool VALS>
-__device__ __forceinline__ void stage_rows(RowStage& S, const int64_t* __restrict__ ptr,
+__device__ __forceinline__ void stage_rows(RowStageT<VALS>& S, const int64_t* __restrict__ ptr,
                                            const int32_t* __restrict__ col, const double* __restrict__ val,
                                            int64_t nr, int64_t I0, RowView* view) {
   const int lane = threadIdx.x & 63;
