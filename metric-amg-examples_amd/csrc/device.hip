@@ -2450,6 +2450,79 @@ __global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, con
   if (!FILL) bptr[I + 1] = o;
 }
 
+// The fill pass with columns only in LDS (16 KB, ~10 waves per CU instead
+// of 3 with the 48 KB column + value staging): each lane's merge writes, in
+// place of every staged column, the entry's slot in the output (4 (o - o0) + q,
+// o0 the workgroup's first block) and the zeros of its blocks' missing
+// components; then the wave sweeps the value ranges with coalesced loads and
+// stores each value into its slot.  Same blocks, same bits.  Ranges over
+// RS_CAP (not staged) merge from global memory as in csr2bsr_kernel.
+__global__ __launch_bounds__(64) void csr2bsr_fill_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const double* __restrict__ val, const int64_t* bptr,
+                                                          int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
+  __shared__ RowStageT<false> S;   // columns, then each entry's slot
+  const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
+  RowView vw[2];
+  stage_rows<false>(S, ptr, col, val, nr, I0, vw);
+  const bool lds = vw[0].lds;      // uniform over the workgroup
+  if (!lds) {                      // long ranges: values from global memory
+    if (I >= nr) return;
+    Seg4 g;
+    stage_segs(ptr, vw, nr, nc, I, g.k, g.e);
+    g.init(vw, nc);
+    int64_t o = bptr[I];
+    for (;;) {
+      const int64_t J = g.next();
+      if (J == INT64_MAX) break;
+      dv4 v = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (g.c[q] == J) {
+          v[q] = vw[q >> 1].val(g.k[q]);
+          ++g.k[q];
+          g.head(vw, nc, q);
+        }
+      bval[o] = v;
+      bcol[o] = (int32_t)J;
+      ++o;
+    }
+    return;
+  }
+  const int64_t o0 = bptr[I0];
+  double* bv = reinterpret_cast<double*>(bval + o0);
+  if (I < nr) {
+    Seg4 g;
+    stage_segs(ptr, vw, nr, nc, I, g.k, g.e);
+    g.init(vw, nc);
+    int64_t o = bptr[I];
+    for (;;) {
+      const int64_t J = g.next();
+      if (J == INT64_MAX) break;
+      const int32_t rel = (int32_t)(o - o0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (g.c[q] == J) {
+          S.c[q >> 1][g.k[q] - vw[q >> 1].off] = 4 * rel + q;   // this entry's slot (its column was read)
+          ++g.k[q];
+          g.head(vw, nc, q);
+        } else {
+          bv[4 * rel + q] = 0.0;
+        }
+      }
+      bcol[o] = (int32_t)J;
+      ++o;
+    }
+  }
+  __syncthreads();
+  const int64_t I1 = I0 + RS_NODES < nr ? I0 + RS_NODES : nr;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t b = ptr[f * nr + I0], n = ptr[f * nr + I1] - b;
+    for (int64_t t = threadIdx.x; t < n; t += 64) bv[S.c[f][t]] = val[b + t];
+  }
+}
+
 __global__ __launch_bounds__(256) void sym_check_kernel(int64_t nb, const dv4* __restrict__ v, int* bad) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k < nb && __double_as_longlong(v[k].y) != __double_as_longlong(v[k].z)) atomicOr(bad, 1);
@@ -2763,7 +2836,13 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
-  if (nr) csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  // MAMG_CSR2BSR_FILL=0: the column + value staged fill (csr2bsr_kernel<true>; tests, A/B)
+  const char* fe = std::getenv("MAMG_CSR2BSR_FILL");
+  const bool f2 = fe ? std::atoi(fe) != 0 : true;
+  if (nr && f2)
+    csr2bsr_fill_kernel<<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  else if (nr)
+    csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
 }
