@@ -118,6 +118,8 @@ SIGNATURES = {
                                         C.POINTER(VP)]),
     'mamg_gpu_host_setup': (C.c_int, [C.POINTER(mamg_csr), P_I32, C.c_int64, C.POINTER(mamg_params),
                                       C.POINTER(VP)]),
+    'mamg_sharded_galerkin_check': (C.c_int, [C.POINTER(mamg_csr), C.POINTER(mamg_csr), C.POINTER(mamg_csr),
+                                              C.c_int, C.c_int, P_I64]),
     'mamg_setup_timings': (C.c_int, [VP, P_F64]),
     'mamg_layout_timings': (C.c_int, [VP, P_F64]),
     'mamg_upload': (C.c_int, [VP, C.POINTER(mamg_csr), C.POINTER(mamg_params), C.POINTER(VP)]),

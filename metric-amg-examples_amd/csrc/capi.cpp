@@ -593,6 +593,20 @@ int mamg_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
   GUARD_END
 }
 
+int mamg_sharded_galerkin_check(const mamg_csr* A, const mamg_csr* P, const mamg_csr* Ac, int nranks, int device,
+                                int64_t* res6) {
+  GUARD_BEGIN
+  TmpTrim trim;
+  if (!res6) { set_error("null argument"); return MAMG_ERR_ARG; }
+  mamg::CsrView a, p, c;
+  int rc;
+  if ((rc = to_view(A, &a)) || (rc = to_view(P, &p)) || (rc = to_view(Ac, &c))) return rc;
+  std::string err;
+  if ((rc = mamg::sharded_galerkin_check(a, p, c, nranks, device, res6, &err))) set_error(err);
+  return rc;
+  GUARD_END
+}
+
 int mamg_setup_gpu(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                    const mamg_params* params, mamg_handle** out) {
   GUARD_BEGIN

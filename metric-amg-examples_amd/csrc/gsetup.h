@@ -57,6 +57,10 @@ int gpu_setup(const DevMat& A0, const int32_t* idofs, int64_t n_idofs, const mam
 // copy a GPU hierarchy into a host Hierarchy (same fields the host setup
 // fills; level-0 A is the given host view)
 int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string* err);
+// row-sharded Galerkin product on nranks virtual ranks, each row compared bit
+// for bit with the unsharded (A P) and with Ac (gsetup.hip; res[6])
+int sharded_galerkin_check(const CsrView& A, const CsrView& P, const CsrView& Ac, int nranks, int device,
+                           int64_t res[6], std::string* err);
 // multi-GPU: download only what rank `rank` of `nranks` reads (its node rows
 // of every distributed level, replicated levels whole, no R / aggregates) and
 // compute the ghost lists on the device (build_dist_plan's `pre`); A0d is the

@@ -3056,6 +3056,186 @@ int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   return MAMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Row-sharded Galerkin product on virtual ranks: the start of a
+// partition-local setup.  Rank p owns the
+// fine nodes [p nv / P, (p + 1) nv / P) (both fields' rows) and the coarse
+// nodes [p nc / P, (p + 1) nc / P).  It computes
+//   (A P) rows of its fine dofs  = A_p x P_ext,  P_ext = P's rows of the fine
+//       dofs A_p's columns reach (its own and a halo); every other row empty;
+//   A_c rows of its coarse dofs  = R_p x AP_ext, R_p = R = P^T's rows of its
+//       coarse dofs, AP_ext = the (A P) rows of the fine dofs R_p reaches,
+//       each taken from its OWNER's sharded result above (the exchange a
+//       multi-GPU setup makes); every other row empty;
+// with the setup's own SpGEMM (staged, node row pairs).  A row missing from a
+// halo leaves a product incomplete, so the check is also that the halos are
+// the right ones.  Each row is compared bit for bit: the (A P) rows with the
+// unsharded product, the A_c rows with Ac (the hierarchy's next level).
+// res[6]: (A P) rows that differ, A_c rows that differ, halo P rows read,
+// halo (A P) rows read (summed over ranks), (A P) rows, A_c rows compared.
+// Host-side row selection (a verification path, not a setup).
+// ---------------------------------------------------------------------------
+namespace {
+int up_csr(GHier* G, const Csr& h, DevMat* d, std::string* err) {
+  d->n = h.n; d->m = h.m; d->nnz = h.n ? h.ptr[h.n] : 0;
+  RCHK(galloc(G, &d->ptr, d->n + 1, err));
+  RCHK(galloc(G, &d->col, std::max<int64_t>(d->nnz, 1), err));
+  RCHK(galloc(G, &d->val, std::max<int64_t>(d->nnz, 1), err));
+  HIPCHK(hipMemcpy(d->ptr, h.ptr.data(), (d->n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (d->nnz) {
+    HIPCHK(hipMemcpy(d->col, h.col.data(), d->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->val, h.val.data(), d->nnz * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return MAMG_OK;
+}
+int down_csr(const DevMat& d, Csr* h, std::string* err) {
+  h->n = d.n; h->m = d.m;
+  h->ptr.resize(d.n + 1);
+  RCHK(to_host(h->ptr.data(), d.ptr, d.n + 1, err));
+  const int64_t nnz = h->ptr[d.n];
+  h->col.resize(nnz);
+  h->val.resize(nnz);
+  if (nnz) {
+    RCHK(to_host(h->col.data(), d.col, nnz, err));
+    RCHK(to_host(h->val.data(), d.val, nnz, err));
+  }
+  return MAMG_OK;
+}
+Csr view_csr(const CsrView& v) {
+  Csr c;
+  c.n = v.n; c.m = v.m;
+  const int64_t nnz = v.nnz();
+  c.ptr.assign(v.ptr, v.ptr + v.n + 1);
+  c.col.assign(v.col, v.col + nnz);
+  c.val.assign(v.val, v.val + nnz);
+  return c;
+}
+// rows `rows` of M, in that order
+Csr pick_rows(const Csr& M, const std::vector<int64_t>& rows) {
+  Csr o;
+  o.n = (int64_t)rows.size(); o.m = M.m;
+  o.ptr.assign(1, 0);
+  for (int64_t r : rows) {
+    o.col.insert(o.col.end(), M.col.begin() + M.ptr[r], M.col.begin() + M.ptr[r + 1]);
+    o.val.insert(o.val.end(), M.val.begin() + M.ptr[r], M.val.begin() + M.ptr[r + 1]);
+    o.ptr.push_back((int64_t)o.col.size());
+  }
+  return o;
+}
+bool row_equal(const Csr& X, int64_t i, const Csr& Y, int64_t j) {
+  const int64_t a = X.ptr[i], l = X.ptr[i + 1] - a, b = Y.ptr[j];
+  if (Y.ptr[j + 1] - b != l) return false;
+  return std::memcmp(&X.col[a], &Y.col[b], l * sizeof(int32_t)) == 0 &&
+         std::memcmp(&X.val[a], &Y.val[b], l * sizeof(double)) == 0;
+}
+// the field-major rows of node range [lo, hi) of a 2-function matrix of h nodes per field
+std::vector<int64_t> node_rows(int64_t lo, int64_t hi, int64_t h) {
+  std::vector<int64_t> r;
+  for (int f = 0; f < 2; ++f)
+    for (int64_t I = lo; I < hi; ++I) r.push_back(f * h + I);
+  return r;
+}
+}  // namespace
+
+int sharded_galerkin_check(const CsrView& Av, const CsrView& Pv, const CsrView& Acv, int nranks, int device,
+                           int64_t res[6], std::string* err) {
+  for (int k = 0; k < 6; ++k) res[k] = 0;
+  if (nranks < 1 || Av.n != Av.m || Av.n % 2 || Pv.n != Av.n || Pv.m % 2 || Acv.n != Pv.m || Acv.m != Pv.m) {
+    *err = "sharded Galerkin check: A (2 nv x 2 nv), P (2 nv x 2 nc) and A_c (2 nc x 2 nc), field-major, nranks >= 1";
+    return MAMG_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(device));
+  GHier G;
+  G.device = device;
+  const int64_t n = Av.n, nv = n / 2, m = Pv.m, nc = m / 2;
+  const Csr A = view_csr(Av), P = view_csr(Pv), Ac = view_csr(Acv);
+  DevMat dA, dP, dR, dAP;
+  RCHK(up_csr(&G, A, &dA, err));
+  RCHK(up_csr(&G, P, &dP, err));
+  RCHK(transpose(&G, dP, &dR, err));
+  const double blenP = (double)dP.nnz / (double)std::max<int64_t>(1, dP.n);
+  RCHK(spgemm(&G, dA, BCsr{dP.ptr, dP.col, dP.val}, m, &dAP, err, blenP, true));
+  Csr R, AP;
+  RCHK(down_csr(dR, &R, err));
+  RCHK(down_csr(dAP, &AP, err));
+  const double blenAP = (double)dAP.nnz / (double)std::max<int64_t>(1, dAP.n);
+  auto fine0 = [&](int p) { return (int64_t)p * nv / nranks; };
+  auto coarse0 = [&](int p) { return (int64_t)p * nc / nranks; };
+  std::vector<Csr> APp(nranks);
+  for (int p = 0; p < nranks; ++p) {   // (A P) rows of rank p's fine dofs
+    const int64_t o0 = fine0(p), o1 = fine0(p + 1);
+    const std::vector<int64_t> rows = node_rows(o0, o1, nv);
+    const Csr Ap = pick_rows(A, rows);
+    std::vector<char> need(n, 0);
+    for (int32_t c : Ap.col) need[c] = 1;
+    Csr Pext;
+    Pext.n = n; Pext.m = m;
+    Pext.ptr.assign(1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+      if (need[i]) {
+        Pext.col.insert(Pext.col.end(), P.col.begin() + P.ptr[i], P.col.begin() + P.ptr[i + 1]);
+        Pext.val.insert(Pext.val.end(), P.val.begin() + P.ptr[i], P.val.begin() + P.ptr[i + 1]);
+        const int64_t I = i % nv;
+        res[2] += !(I >= o0 && I < o1);
+      }
+      Pext.ptr.push_back((int64_t)Pext.col.size());
+    }
+    GHier T;
+    T.device = device;
+    DevMat dAp, dPe, dC;
+    RCHK(up_csr(&T, Ap, &dAp, err));
+    RCHK(up_csr(&T, Pext, &dPe, err));
+    RCHK(spgemm(&T, dAp, BCsr{dPe.ptr, dPe.col, dPe.val}, m, &dC, err, blenP, true));
+    RCHK(down_csr(dC, &APp[p], err));
+    for (int64_t r = 0; r < (int64_t)rows.size(); ++r) {
+      res[0] += !row_equal(APp[p], r, AP, rows[r]);
+      ++res[4];
+    }
+  }
+  auto owner = [&](int64_t I) {   // rank of fine node I
+    int p = (int)std::min<int64_t>(nranks - 1, I * nranks / std::max<int64_t>(nv, 1));
+    while (p > 0 && I < fine0(p)) --p;
+    while (p < nranks - 1 && I >= fine0(p + 1)) ++p;
+    return p;
+  };
+  for (int p = 0; p < nranks; ++p) {   // A_c rows of rank p's coarse dofs
+    const int64_t c0 = coarse0(p), c1 = coarse0(p + 1);
+    const std::vector<int64_t> rows = node_rows(c0, c1, nc);
+    const Csr Rp = pick_rows(R, rows);
+    std::vector<char> need(n, 0);
+    for (int32_t c : Rp.col) need[c] = 1;
+    Csr APe;
+    APe.n = n; APe.m = m;
+    APe.ptr.assign(1, 0);
+    const int64_t f0 = fine0(p), f1 = fine0(p + 1);
+    for (int64_t i = 0; i < n; ++i) {
+      if (need[i]) {           // the owner's row (fine dof i = f nv + I is row f (o1 - o0) + I - o0 there)
+        const int64_t I = i % nv, f = i / nv;
+        const int q = owner(I);
+        const int64_t lq = f * (fine0(q + 1) - fine0(q)) + (I - fine0(q));
+        const Csr& S = APp[q];
+        APe.col.insert(APe.col.end(), S.col.begin() + S.ptr[lq], S.col.begin() + S.ptr[lq + 1]);
+        APe.val.insert(APe.val.end(), S.val.begin() + S.ptr[lq], S.val.begin() + S.ptr[lq + 1]);
+        res[3] += !(I >= f0 && I < f1);
+      }
+      APe.ptr.push_back((int64_t)APe.col.size());
+    }
+    GHier T;
+    T.device = device;
+    DevMat dRp, dAPe, dC;
+    Csr Cp;
+    RCHK(up_csr(&T, Rp, &dRp, err));
+    RCHK(up_csr(&T, APe, &dAPe, err));
+    RCHK(spgemm(&T, dRp, BCsr{dAPe.ptr, dAPe.col, dAPe.val}, m, &dC, err, blenAP, true));
+    RCHK(down_csr(dC, &Cp, err));
+    for (int64_t r = 0; r < (int64_t)rows.size(); ++r) {
+      res[1] += !row_equal(Cp, r, Ac, rows[r]);
+      ++res[5];
+    }
+  }
+  return MAMG_OK;
+}
+
 int ghier_download(const GHier& G, const CsrView& A0, Hierarchy* H, std::string* err) {
   H->params = G.params;
   H->A0 = A0;

@@ -118,6 +118,40 @@ def test_csr2bsr_fill_variants_bitwise(lib_built, monkeypatch, dim, n, g, kw):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize('nranks', [2, 3, 8])
+@pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e4, dict()), (3, 16, 1e6, dict(AMG_type=1)),
+                                        (3, 24, 1e2, dict(aggregation_type=5))])
+def test_sharded_galerkin_equals_hierarchy(lib_built, dim, n, g, kw, nranks):
+    """The start of a partition-local setup: the Galerkin
+    products row-sharded over virtual ranks -- each rank's (A P) rows from its
+    A rows and the P rows of its halo, its coarse rows from its R rows and the
+    (A P) rows of the fine dofs they reach, taken from their owners' sharded
+    results -- equal the GPU hierarchy's next level bit for bit, at levels 0
+    and 1, and the halos are really read."""
+    import ctypes as C
+    M = _mamg()
+    L = M._lib
+    s = M.problems.bidomain(dim, n, g)
+    H = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True, **kw)
+    A0 = s.scipy().tocsr()
+    A0.sort_indices()
+    for lv in range(min(2, H.num_levels - 1)):
+        cur = H.level(lv, with_A=lv > 0)
+        nxt = H.level(lv + 1, with_A=True)
+        A = cur['A'] if lv > 0 else (A0.indptr.astype(np.int64), A0.indices.astype(np.int32),
+                                     A0.data.astype(np.float64), A0.shape)
+        mats = [A, cur['P'], nxt['A']]
+        st = [L.as_csr_struct(np.ascontiguousarray(m[0], np.int64), np.ascontiguousarray(m[1], np.int32),
+                              np.ascontiguousarray(m[2], np.float64), m[3][1]) for m in mats]
+        res = np.zeros(6, np.int64)
+        L.check(L.lib().mamg_sharded_galerkin_check(C.byref(st[0]), C.byref(st[1]), C.byref(st[2]), nranks, 0,
+                                                    L.ptr(res, C.c_int64)))
+        print('level', lv, 'ranks', nranks, 'res', res.tolist())
+        assert res[0] == 0 and res[1] == 0, res
+        assert res[4] == A[3][0] and res[5] == nxt['A'][3][0]
+        assert res[2] > 0 and res[3] > 0
+
+
 @pytest.mark.parametrize('dim,n,g,kw', CASES)
 def test_gpu_setup_apply_bitwise_equals_host_setup(lib_built, dim, n, g, kw):
     M = _mamg()
