@@ -185,6 +185,93 @@ __global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_
   if (!FILL) gptr[I + 1] = o;
 }
 
+// The fill pass with columns only in LDS (as device.hip csr2bsr_fill_kernel):
+// each lane's merge writes gcol, every entry's slot 4 (o - o0) + q in place of
+// its staged column and the zeros of its blocks' missing components into the
+// block scratch T; the wave then stores the values into their slots with
+// coalesced loads, and every block's sum of squares is taken in the order
+// (f0,g0) (f0,g1) (f1,g0) (f1,g1) -- a missing component adds +0 to a sum >= +0,
+// so the bits are those of node_graph_kernel<true>.  Ranges over RS_CAP: as
+// node_graph_kernel<true>.
+__global__ __launch_bounds__(64) void node_graph_fill_kernel(int64_t nv, const int64_t* __restrict__ ptr,
+                                                             const int32_t* __restrict__ col,
+                                                             const double* __restrict__ val,
+                                                             const int64_t* __restrict__ gptr,
+                                                             int32_t* __restrict__ gcol, double* __restrict__ gval,
+                                                             double* __restrict__ T) {
+  __shared__ RowStageT<false> S;
+  const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
+  RowView vw[2];
+  stage_rows<false>(S, ptr, col, val, nv, I0, vw);
+  if (!vw[0].lds) {
+    if (I >= nv) return;
+    Seg4 g;
+    stage_segs(ptr, vw, nv, nv, I, g.k, g.e);
+    g.init(vw, nv);
+    int64_t o = gptr[I];
+    for (;;) {
+      const int64_t J = g.next();
+      if (J == INT64_MAX) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (g.c[q] == J) {
+          const double a = vw[q >> 1].val(g.k[q]);
+          acc += a * a;
+          ++g.k[q];
+          g.head(vw, nv, q);
+        }
+      gcol[o] = (int32_t)J;
+      gval[o] = sqrt(acc);
+      ++o;
+    }
+    return;
+  }
+  const int64_t o0 = gptr[I0];
+  const int64_t I1 = I0 + RS_NODES < nv ? I0 + RS_NODES : nv;
+  double* tb = T + 4 * o0;
+  if (I < nv) {
+    Seg4 g;
+    stage_segs(ptr, vw, nv, nv, I, g.k, g.e);
+    g.init(vw, nv);
+    int64_t o = gptr[I];
+    for (;;) {
+      const int64_t J = g.next();
+      if (J == INT64_MAX) break;
+      const int32_t rel = (int32_t)(o - o0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (g.c[q] == J) {
+          S.c[q >> 1][g.k[q] - vw[q >> 1].off] = 4 * rel + q;
+          ++g.k[q];
+          g.head(vw, nv, q);
+        } else {
+          tb[4 * rel + q] = 0.0;
+        }
+      }
+      gcol[o] = (int32_t)J;
+      ++o;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int64_t b = ptr[f * nv + I0], n = ptr[f * nv + I1] - b;
+    for (int64_t t = threadIdx.x; t < n; t += 64) tb[S.c[f][t]] = val[b + t];
+  }
+  __syncthreads();
+  const int64_t ob = gptr[I1] - o0;
+  for (int64_t r = threadIdx.x; r < ob; r += 64) {
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double a = tb[4 * r + q];
+      acc += a * a;
+    }
+    gval[o0 + r] = sqrt(acc);
+  }
+}
+
 // |diagonal| of a square CSR (0 if absent)
 __global__ __launch_bounds__(256) void absdiag_kernel(int64_t n, const int64_t* __restrict__ ptr,
                                                       const int32_t* __restrict__ col, const double* __restrict__ val,
@@ -2068,7 +2155,17 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
     RCHK(S.alloc(&Gr.col, Gr.nnz, err));
     RCHK(S.alloc(&Gr.val, Gr.nnz, err));
-    node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+    const char* fe = std::getenv("MAMG_CSR2BSR_FILL");   // 0: the column + value staged merge (tests, A/B)
+    if (fe && std::atoi(fe) == 0) {
+      node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+    } else {
+      Scratch TS;
+      double* T = nullptr;
+      RCHK(TS.alloc(&T, 4 * std::max<int64_t>(Gr.nnz, 1), err));
+      node_graph_fill_kernel<<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr,
+                                                                                      Gr.col, Gr.val, T);
+      HIPCHK(hipGetLastError());
+    }
   }
   double* d = nullptr;
   uint8_t *flag = nullptr, *nonisol = nullptr;
