@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "dist.h"
@@ -1769,6 +1770,22 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_pair_kernel(
   }
 }
 
+// *diff += pairs (i, i + h) whose rows hold different columns (a pair kernel
+// would hand every such pair to the row kernel: for UA's R = T^T all of
+// them, since row J holds field-0 columns and row nc + J field-1 columns)
+__global__ __launch_bounds__(256) void pair_diff_kernel(int64_t h, const int64_t* __restrict__ aptr,
+                                                        const int32_t* __restrict__ acol, unsigned long long* diff) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool d = false;
+  if (p < h) {
+    const int64_t p0 = aptr[p], p1 = aptr[p + h], L = aptr[p + 1] - p0;
+    d = aptr[p + h + 1] - p1 != L;
+    for (int64_t t = 0; !d && t < L; ++t) d = acol[p0 + t] != acol[p1 + t];
+  }
+  const unsigned long long b = __ballot(d);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(shard_of(diff), (unsigned long long)__popcll(b));
+}
+
 // staged rows into place: row i's m = ptr[i + 1] - ptr[i] entries from
 // scol / sval at i * S (S lanes per row)
 template <int S>
@@ -1812,17 +1829,47 @@ bool spgemm_pair_on() {
   return e ? std::atoi(e) != 0 : true;
 }
 
-int64_t spgemm_stage_stride(int64_t n) {
+// The staging area is one block per device, allocated at its first use at
+// the cap size (min(MAMG_SPGEMM_STAGE_GB, a quarter of the free HBM)) and
+// kept for the process, like the scans' scratch: a large block allocated
+// later, in a heap that earlier handles have fragmented, was written ~50x
+// slower (the reference family's R (A P) at nrefs=6: 4.9 s against 0.1 s in a
+// fresh process, profiles/r05_spgemm_stage_pool.txt), the scattered row
+// writes paying a translation miss per small page.  Used in null-stream
+// order, as the setup temporaries are.
+struct StagePool {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_stage_mu;
+StagePool g_stage[64];
+
+size_t stage_pool(int dev, void** p) {
+  std::lock_guard<std::mutex> g(g_stage_mu);
+  StagePool& sp = g_stage[dev & 63];
+  if (!sp.p) {
+    const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
+    const double cap_gb = e ? std::atof(e) : 16.0;
+    size_t fr = 0, tot = 0;
+    if (cap_gb > 0.0 && hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const size_t b = (size_t)std::min(cap_gb * 1e9, 0.25 * (double)fr) & ~(((size_t)2 << 20) - 1);
+      if (b >= ((size_t)64 << 20) && dev_malloc(&sp.p, b, "scratch") == hipSuccess) sp.bytes = b;
+      else sp.p = nullptr;
+    }
+    (void)hipGetLastError();
+  }
+  *p = sp.p;
+  return sp.bytes;
+}
+
+int64_t spgemm_stage_stride(int64_t n, size_t pool) {
   const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
-  const double cap_gb = e ? std::atof(e) : 16.0;
+  if (e && std::atof(e) <= 0.0) return 0;
   e = std::getenv("MAMG_SPGEMM_STAGE_STRIDE");
   const int64_t smax = e ? std::atoll(e) : 128;
-  if (cap_gb <= 0.0 || n <= 0) return 0;
-  size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return 0; }
-  const double cap = std::min(cap_gb * 1e9, 0.25 * (double)fr);
+  if (n <= 0) return 0;
   for (int64_t s : {128, 64, 32, 16})
-    if (s <= smax && (double)n * (double)s * 12.0 <= cap) return s;
+    if (s <= smax && (double)n * (double)s * 12.0 <= (double)pool) return s;
   return 0;
 }
 
@@ -1830,6 +1877,12 @@ int64_t spgemm_stage_stride(int64_t n) {
 // the staged count pass runs over row pairs (spgemm_pair_kernel)
 template <int GL, class BS>
 int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::string* err, bool pair) {
+#if MAMG_DIAG
+  // MAMG_SPGEMM_TRACE (diagnosis build): one line per product on stderr
+  const bool trace = std::getenv("MAMG_SPGEMM_TRACE") != nullptr;
+  if (trace) (void)hipDeviceSynchronize();
+  const auto tr0 = std::chrono::steady_clock::now();
+#endif
   constexpr int TS0 = 128, TS1 = 512, TS2 = 2048;
   const int64_t n = A.n;
   Scratch S;
@@ -1840,18 +1893,25 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
   RCHK(S.alloc(&ctr, 5, err));
   HIPCHK(dev_memset(ctr, 0, 5 * sizeof(int)));
   SpStage stg;
-  stg.stride = spgemm_stage_stride(n);
+  void* pool = nullptr;
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  const size_t pool_bytes = stage_pool(dev, &pool);
+  stg.stride = pool ? spgemm_stage_stride(n, pool_bytes) : 0;
   int32_t* l3 = nullptr;
   int n3 = 0;
-  if (stg.stride) {
-    RCHK(S.alloc(&stg.col, n * stg.stride, err));
-    RCHK(S.alloc(&stg.val, n * stg.stride, err));
+  if (stg.stride) {   // values first (8-byte aligned), then the columns
+    stg.val = reinterpret_cast<double*>(pool);
+    stg.col = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pool) + (size_t)n * stg.stride * sizeof(double));
     RCHK(S.alloc(&stg.st, n, err));
     RCHK(S.alloc(&l3, n, err));
     HIPCHK(dev_memset(stg.st, 0, (size_t)n));
     stg.ulist = l3;
     stg.uctr = ctr + 4;
   }
+#if MAMG_DIAG
+  const auto tr1 = std::chrono::steady_clock::now();   // after the staging allocations
+#endif
   C->n = n;
   C->m = ncols;
   RCHK(galloc(G, &C->ptr, n + 1, err));
@@ -1869,6 +1929,15 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
     int32_t* cc = pass ? C->col : nullptr;
     double* cv = pass ? C->val : nullptr;
     if (pass == 0) {
+      if (pair && stg.stride && n % 2 == 0 && spgemm_pair_on()) {   // only when most pairs agree
+        unsigned long long* dc = nullptr;
+        RCHK(shards_alloc(&S, &dc, err));
+        pair_diff_kernel<<<nblk(n / 2), 256>>>(n / 2, A.ptr, A.col, dc);
+        HIPCHK(hipGetLastError());
+        unsigned long long nd = 0;
+        RCHK(shards_read(dc, false, &nd, err));
+        pair = nd * 8 <= (unsigned long long)(n / 2);
+      }
       if (pair && stg.stride && n % 2 == 0 && spgemm_pair_on()) {
         int32_t* lm = nullptr;
         int* nm = nullptr;
@@ -1932,6 +2001,18 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
       return MAMG_ERR_UNSUPPORTED;
     }
   }
+#if MAMG_DIAG
+  if (trace) {
+    (void)hipDeviceSynchronize();
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    const auto tr2 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[mamg spgemm] n %lld nnz %lld stride %lld pair %d: allocations %.2f ms, products %.2f ms, free %.1f GB\n",
+                 (long long)n, (long long)C->nnz, (long long)stg.stride, (int)pair,
+                 std::chrono::duration<double, std::milli>(tr1 - tr0).count(),
+                 std::chrono::duration<double, std::milli>(tr2 - tr1).count(), fr / 1e9);
+  }
+#endif
   return MAMG_OK;
 }
 
