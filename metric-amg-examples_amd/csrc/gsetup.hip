@@ -1773,9 +1773,12 @@ __global__ __launch_bounds__(64 * WPB) void spgemm_pair_kernel(
 // *diff += pairs (i, i + h) whose rows hold different columns (a pair kernel
 // would hand every such pair to the row kernel: for UA's R = T^T all of
 // them, since row J holds field-0 columns and row nc + J field-1 columns)
+// (a sample: every PAIR_SAMPLE-th pair; the decision needs a fraction, and the
+// full check, one lane walking both rows, cost 3 ms per level-0 product)
+constexpr int64_t PAIR_SAMPLE = 61;
 __global__ __launch_bounds__(256) void pair_diff_kernel(int64_t h, const int64_t* __restrict__ aptr,
                                                         const int32_t* __restrict__ acol, unsigned long long* diff) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) * PAIR_SAMPLE;
   bool d = false;
   if (p < h) {
     const int64_t p0 = aptr[p], p1 = aptr[p + h], L = aptr[p + 1] - p0;
@@ -1932,11 +1935,12 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
       if (pair && stg.stride && n % 2 == 0 && spgemm_pair_on()) {   // only when most pairs agree
         unsigned long long* dc = nullptr;
         RCHK(shards_alloc(&S, &dc, err));
-        pair_diff_kernel<<<nblk(n / 2), 256>>>(n / 2, A.ptr, A.col, dc);
+        const int64_t ns = (n / 2 + PAIR_SAMPLE - 1) / PAIR_SAMPLE;   // pairs sampled
+        pair_diff_kernel<<<nblk(ns), 256>>>(n / 2, A.ptr, A.col, dc);
         HIPCHK(hipGetLastError());
         unsigned long long nd = 0;
         RCHK(shards_read(dc, false, &nd, err));
-        pair = nd * 8 <= (unsigned long long)(n / 2);
+        pair = nd * 8 <= (unsigned long long)ns;
       }
       if (pair && stg.stride && n % 2 == 0 && spgemm_pair_on()) {
         int32_t* lm = nullptr;
