@@ -3229,10 +3229,46 @@ int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   RCHK(galloc(G, &D->ptr, A.n + 1, err));
   RCHK(galloc(G, &D->col, D->nnz, err));
   RCHK(galloc(G, &D->val, D->nnz, err));
-  HIPCHK(hipMemcpy(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if (D->nnz) {
-    HIPCHK(hipMemcpy(D->col, A.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(D->val, A.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
+  // the three arrays cut into k pieces each, copied by k host threads on
+  // streams of their own: a pageable copy stages through the runtime's
+  // pinned buffers on the calling thread, ~36 GB/s for one thread.  A/B at
+  // nrefs=6 (MAMG_UPLOAD_THREADS, profiles/r05_upload_threads.txt): k = 1
+  // 348-397 ms, 2 323 ms (default), 4 335 ms
+  const char* e = std::getenv("MAMG_UPLOAD_THREADS");
+  const int k = e ? std::max(1, std::min(16, std::atoi(e))) : 2;
+  if (k == 1) {
+    HIPCHK(hipMemcpy(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (D->nnz) {
+      HIPCHK(hipMemcpy(D->col, A.col, D->nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(D->val, A.val, D->nnz * sizeof(double), hipMemcpyHostToDevice));
+    }
+  } else {
+    struct Piece { void* d; const void* h; size_t b; };
+    std::vector<Piece> pieces;
+    auto cut = [&](void* d, const void* h, size_t b) {
+      const size_t q = (b + k - 1) / k;
+      for (size_t o = 0; o < b; o += q) pieces.push_back({(char*)d + o, (const char*)h + o, std::min(q, b - o)});
+    };
+    cut(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t));
+    if (D->nnz) {
+      cut(D->col, A.col, D->nnz * sizeof(int32_t));
+      cut(D->val, A.val, D->nnz * sizeof(double));
+    }
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    const int dev = G->device;
+    for (int t = 0; t < k; ++t)
+      th.emplace_back([&, t] {
+        if (hipSetDevice(dev) != hipSuccess) { bad = 1; return; }
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { bad = 1; return; }
+        for (size_t i = t; i < pieces.size(); i += k)
+          if (hipMemcpyAsync(pieces[i].d, pieces[i].h, pieces[i].b, hipMemcpyHostToDevice, st) != hipSuccess) bad = 1;
+        if (hipStreamSynchronize(st) != hipSuccess) bad = 1;
+        (void)hipStreamDestroy(st);
+      });
+    for (auto& x : th) x.join();
+    if (bad) { *err = "A0 upload: " + std::string(hipGetErrorString(hipGetLastError())); return MAMG_ERR_HIP; }
   }
   G->phase_ms[GS_UPLOAD] = clk.lap();
   return MAMG_OK;
