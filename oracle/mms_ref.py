@@ -29,9 +29,36 @@ from __future__ import annotations
 
 import itertools
 
+import math
+
 import numpy as np
 
-import metric_amg_examples_amd.problems as problems
+from mamg_oracle import _K_PATH   # the oracle's own generator (not the product's problems.py)
+
+
+def _mass_loc(d: int, meas: float) -> np.ndarray:
+    """P1 mass matrix of a d-simplex of measure meas: meas/((d+1)(d+2)) (1 + I)."""
+    return meas / ((d + 1) * (d + 2)) * (np.ones((d + 1, d + 1)) + np.eye(d + 1))
+
+
+def _assemble(simplices, index, nv, Kloc, Mloc):
+    """Element matrices summed into CSR (K, M) over the vertex numbering `index`."""
+    import scipy.sparse as sp
+    rows, cols, kv, mv = [], [], [], []
+    for verts in simplices:
+        ids = [index(v) for v in verts]
+        for a in range(len(ids)):
+            for b in range(len(ids)):
+                rows.append(ids[a])
+                cols.append(ids[b])
+                kv.append(np.full(len(ids[a]), Kloc[a, b]))
+                mv.append(np.full(len(ids[a]), Mloc[a, b]))
+    r, c = np.concatenate(rows), np.concatenate(cols)
+    K = sp.coo_matrix((np.concatenate(kv), (r, c)), shape=(nv, nv)).tocsr()
+    M = sp.coo_matrix((np.concatenate(mv), (r, c)), shape=(nv, nv)).tocsr()
+    K.sort_indices()
+    M.sort_indices()
+    return K, M
 
 _WAVE = {2: (np.array([1.0, 1.0]), np.array([1.0, -1.0])),
          3: (np.array([1.0, 1.0, 2.0]), np.array([1.0, -1.0, 1.0]))}
@@ -184,12 +211,12 @@ class BidomainMMS:
         given cells (default all)."""
         import scipy.sparse as sp
         d, h = self.dim, self.h
-        Kloc = problems._PATH_K[d] * h ** (d - 2)
-        Mloc = problems._mass_loc(d, h ** d / np.prod(np.arange(1, d + 1)))
+        Kloc = _K_PATH[d].astype(np.float64) / math.factorial(d) * h ** (d - 2)   # path-simplex stiffness
+        Mloc = _mass_loc(d, h ** d / math.factorial(d))
         if cells is None:
             cells = _lattice([self.n] * d)
         simp = [verts for _, verts in _paths(d, cells)]
-        K, M = problems._assemble(simp, self.index, self.nv, Kloc, Mloc)
+        K, M = _assemble(simp, self.index, self.nv, Kloc, Mloc)
         e = self.ex
         A = sp.bmat([[e.k1 * K + e.g * M, -e.g * M], [-e.g * M, e.k2 * K + e.g * M]], format='csr')
         A.sort_indices()
