@@ -2416,12 +2416,12 @@ int upload_bsr(HT* h, const HBsr& B, DBsr* D, int lanes, std::string* err,
 // node I's four sorted column segments (rowstage.h stage_segs): q = 2 f + g
 // holds the entries of row f nr + I whose column lies in field g (node
 // column = col - g nc)
-template <bool FILL>
+template <bool FILL, int CAP = RS_CAP>
 __global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
                                                      const int32_t* __restrict__ col,
                                                      const double* __restrict__ val, int64_t* bptr,
                                                      int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
-  __shared__ RowStageT<FILL> S;   // rowstage.h: the wave's rows staged through LDS
+  __shared__ RowStageT<FILL, CAP> S;   // rowstage.h: the wave's rows staged through LDS
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nr, I0, vw);
@@ -2456,12 +2456,13 @@ __global__ __launch_bounds__(64) void csr2bsr_kernel(int64_t nr, int64_t nc, con
 // o0 the workgroup's first block) and the zeros of its blocks' missing
 // components; then the wave sweeps the value ranges with coalesced loads and
 // stores each value into its slot.  Same blocks, same bits.  Ranges over
-// RS_CAP (not staged) merge from global memory as in csr2bsr_kernel.
+// CAP (not staged) merge from global memory as in csr2bsr_kernel.
+template <int CAP>
 __global__ __launch_bounds__(64) void csr2bsr_fill_kernel(int64_t nr, int64_t nc, const int64_t* __restrict__ ptr,
                                                           const int32_t* __restrict__ col,
                                                           const double* __restrict__ val, const int64_t* bptr,
                                                           int32_t* __restrict__ bcol, dv4* __restrict__ bval) {
-  __shared__ RowStageT<false> S;   // columns, then each entry's slot
+  __shared__ RowStageT<false, CAP> S;   // columns, then each entry's slot
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<false>(S, ptr, col, val, nr, I0, vw);
@@ -2519,13 +2520,20 @@ __global__ __launch_bounds__(64) void csr2bsr_fill_kernel(int64_t nr, int64_t nc
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     const int64_t b = ptr[f * nr + I0], n = ptr[f * nr + I1] - b;
-    for (int64_t t = threadIdx.x; t < n; t += 64) bv[S.c[f][t]] = val[b + t];
+    scatter_staged(S.c[f], val, b, n, bv);
   }
 }
 
+// *bad = 1 when some block has a01 != a10 (bitwise).  Grid-stride over at most
+// SYM_CHECK_BLOCKS workgroups, one atomic per workgroup: with one atomic per
+// mismatching wave, a non-symmetric level-1 operator (25.8 M blocks, nearly
+// all mismatching) serialised ~400 K atomics on one word (4.6 ms)
+constexpr unsigned SYM_CHECK_BLOCKS = 16384;
 __global__ __launch_bounds__(256) void sym_check_kernel(int64_t nb, const dv4* __restrict__ v, int* bad) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k < nb && __double_as_longlong(v[k].y) != __double_as_longlong(v[k].z)) atomicOr(bad, 1);
+  int d = 0;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nb; k += (int64_t)gridDim.x * 256)
+    d |= __double_as_longlong(v[k].y) != __double_as_longlong(v[k].z);
+  if (__syncthreads_or(d) && threadIdx.x == 0) atomicOr(bad, 1);
 }
 
 __global__ __launch_bounds__(256) void pack_sym_kernel(int64_t nb, const dv4* __restrict__ v,
@@ -2830,7 +2838,13 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   B->nr = nr; B->nc = nc; B->merged = false;
   if ((rc = T->alloc(&B->ptr, nr + 1, err))) return rc;
   HIPCHK(dev_memset(B->ptr, 0, sizeof(int64_t)));
-  if (nr) csr2bsr_kernel<false><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
+  // rows whose wave ranges average over RS_CAP (the coarse Galerkin products;
+  // A_0 averages ~1900) stage through the 64 KB column-only RS_CAP_LONG
+  // variant: 2 waves per CU, but coalesced (level 1: 14.9 -> 12.2 ms)
+  const unsigned g = (unsigned)((nr + RS_NODES - 1) / RS_NODES);
+  const bool lng = nr && (double)M.nnz / (double)(2 * nr) * RS_NODES > RS_CAP;
+  if (nr && lng) csr2bsr_kernel<false, RS_CAP_LONG><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
+  else if (nr) csr2bsr_kernel<false><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, nullptr, nullptr);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(B->ptr, B->ptr, nr + 1, nullptr, err))) return rc;
   HIPCHK(hipMemcpy(&B->nb, B->ptr + nr, sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -2839,10 +2853,12 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   // MAMG_CSR2BSR_FILL=0: the column + value staged fill (csr2bsr_kernel<true>; tests, A/B)
   const char* fe = std::getenv("MAMG_CSR2BSR_FILL");
   const bool f2 = fe ? std::atoi(fe) != 0 : true;
-  if (nr && f2)
-    csr2bsr_fill_kernel<<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  if (nr && f2 && lng)
+    csr2bsr_fill_kernel<RS_CAP_LONG><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+  else if (nr && f2)
+    csr2bsr_fill_kernel<RS_CAP><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   else if (nr)
-    csr2bsr_kernel<true><<<(unsigned)((nr + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
+    csr2bsr_kernel<true><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
   HIPCHK(hipGetLastError());
   return MAMG_OK;
 }
@@ -3165,7 +3181,7 @@ int finalize_bsr(HT* h, TmpPool* T, TBsr& B, DBsr* D, int lanes, bool sym_ok, st
     int* bad = nullptr;
     if ((rc = T->alloc(&bad, 1, err))) return rc;
     HIPCHK(dev_memset(bad, 0, sizeof(int)));
-    sym_check_kernel<<<nblocks(B.nb), 256>>>(B.nb, B.val, bad);
+    sym_check_kernel<<<std::min(nblocks(B.nb), SYM_CHECK_BLOCKS), 256>>>(B.nb, B.val, bad);
     int hb = 1;
     HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
     sym = hb == 0;
@@ -6792,7 +6808,7 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
       int* bad = nullptr;
       if ((rc = T.alloc(&bad, 1, err))) return rc;
       HIPCHK(dev_memset(bad, 0, sizeof(int)));
-      sym_check_kernel<<<nblocks(tA.nb), 256>>>(tA.nb, tA.val, bad);
+      sym_check_kernel<<<std::min(nblocks(tA.nb), SYM_CHECK_BLOCKS), 256>>>(tA.nb, tA.val, bad);
       int hb = 1;
       HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));
       if (hb == 0) {

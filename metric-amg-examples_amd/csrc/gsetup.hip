@@ -152,12 +152,12 @@ int to_host(T* dst, const T* src, int64_t count, std::string* err) {
 // node graph (setup.cpp node_graph, nf = 2): s_IJ = sqrt(sum of squares over
 // the 2x2 block), accumulated over rows I then nv + I, each in CSR order
 // ---------------------------------------------------------------------------
-template <bool FILL>
+template <bool FILL, int CAP = RS_CAP>
 __global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_t* __restrict__ ptr,
                                                         const int32_t* __restrict__ col,
                                                         const double* __restrict__ val, int64_t* gptr,
                                                         int32_t* __restrict__ gcol, double* __restrict__ gval) {
-  __shared__ RowStageT<FILL> S;
+  __shared__ RowStageT<FILL, CAP> S;
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<FILL>(S, ptr, col, val, nv, I0, vw);
@@ -194,13 +194,14 @@ __global__ __launch_bounds__(64) void node_graph_kernel(int64_t nv, const int64_
 // (f0,g0) (f0,g1) (f1,g0) (f1,g1) -- a missing component adds +0 to a sum >= +0,
 // so the bits are those of node_graph_kernel<true>.  Ranges over RS_CAP: as
 // node_graph_kernel<true>.
+template <int CAP>
 __global__ __launch_bounds__(64) void node_graph_fill_kernel(int64_t nv, const int64_t* __restrict__ ptr,
                                                              const int32_t* __restrict__ col,
                                                              const double* __restrict__ val,
                                                              const int64_t* __restrict__ gptr,
                                                              int32_t* __restrict__ gcol, double* __restrict__ gval,
                                                              double* __restrict__ T) {
-  __shared__ RowStageT<false> S;
+  __shared__ RowStageT<false, CAP> S;
   const int64_t I0 = (int64_t)blockIdx.x * RS_NODES, I = I0 + threadIdx.x;
   RowView vw[2];
   stage_rows<false>(S, ptr, col, val, nv, I0, vw);
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(64) void node_graph_fill_kernel(int64_t nv, const i
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     const int64_t b = ptr[f * nv + I0], n = ptr[f * nv + I1] - b;
-    for (int64_t t = threadIdx.x; t < n; t += 64) tb[S.c[f][t]] = val[b + t];
+    scatter_staged(S.c[f], val, b, n, tb);
   }
   __syncthreads();
   const int64_t ob = gptr[I1] - o0;
@@ -374,6 +375,62 @@ __global__ __launch_bounds__(256) void mis_update_kernel(int64_t n, const int64_
     if (flag[k]) m = max(m, m1[col[k]]);
   if (m == key[i]) state[i] = ST_IN;
   else if ((m >> 62) == ST_IN) state[i] = ST_OUT;
+}
+
+// The same two maxima with the workgroup's rows staged (round 5): lane t
+// loads entry b + t of the 256 nodes' contiguous entry range (coalesced col /
+// flag reads, MM_BATCH gathers in flight) and stores flag ? x[col] : 0 into
+// LDS; each node's lane then takes the max over its LDS range.  A max is
+// exact in any order and 0 is its identity over keys, so the results are those
+// of mis_max_kernel / mis_update_kernel (whose lane-per-row walks split every
+// load into ~64 cache-line requests: 1.6 ms per level-0 round, ~16 rounds).
+// Ranges over MM_CAP: the row walk.
+constexpr int MM_CAP = 6144, MM_BATCH = 4;
+template <bool UPDATE>
+__global__ __launch_bounds__(256) void mis_staged_kernel(int64_t n, const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const uint8_t* __restrict__ flag,
+                                                         const uint64_t* __restrict__ x,
+                                                         const uint64_t* __restrict__ key,
+                                                         uint64_t* __restrict__ out) {
+  __shared__ uint64_t L[MM_CAP];
+  const int64_t i0 = (int64_t)blockIdx.x * 256, i1 = i0 + 256 < n ? i0 + 256 : n, i = i0 + threadIdx.x;
+  const int64_t b = ptr[i0], m = ptr[i1] - b;
+  if (m > MM_CAP) {
+    if (i >= n || (UPDATE && out[i] != ST_UND)) return;
+    uint64_t v = x[i];
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+      if (flag[k]) v = max(v, x[col[k]]);
+    if (!UPDATE) out[i] = v;
+    else if (v == key[i]) out[i] = ST_IN;
+    else if ((v >> 62) == ST_IN) out[i] = ST_OUT;
+    return;
+  }
+  for (int64_t t0 = 0; t0 < m; t0 += 256 * MM_BATCH) {
+    int32_t c[MM_BATCH];
+    uint8_t f[MM_BATCH];
+#pragma unroll
+    for (int u = 0; u < MM_BATCH; ++u) {
+      const int64_t t = t0 + u * 256 + threadIdx.x;
+      f[u] = 0;
+      if (t < m) { c[u] = col[b + t]; f[u] = flag[b + t]; }
+    }
+    uint64_t v[MM_BATCH];
+#pragma unroll
+    for (int u = 0; u < MM_BATCH; ++u) v[u] = f[u] ? x[c[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < MM_BATCH; ++u) {
+      const int64_t t = t0 + u * 256 + threadIdx.x;
+      if (t < m) L[t] = v[u];
+    }
+  }
+  __syncthreads();
+  if (i >= n || (UPDATE && out[i] != ST_UND)) return;
+  uint64_t v = x[i];
+  for (int64_t k = ptr[i] - b, e = ptr[i + 1] - b; k < e; ++k) v = max(v, L[k]);
+  if (!UPDATE) out[i] = v;
+  else if (v == key[i]) out[i] = ST_IN;
+  else if ((v >> 62) == ST_IN) out[i] = ST_OUT;
 }
 
 __global__ __launch_bounds__(256) void root_flag_kernel(int64_t n, const uint64_t* __restrict__ state,
@@ -2234,7 +2291,11 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     Gr.n = Gr.m = nv;
     RCHK(S.alloc(&Gr.ptr, nv + 1, err));
     HIPCHK(dev_memset(Gr.ptr, 0, sizeof(int64_t)));
-    node_graph_kernel<false><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
+    // long rows (coarse levels): the 64 KB column-only staging (device.hip dev_csr_to_bsr)
+    const unsigned g = (unsigned)((nv + RS_NODES - 1) / RS_NODES);
+    const bool lng = (double)A.nnz / (double)std::max<int64_t>(1, 2 * nv) * RS_NODES > RS_CAP;
+    if (lng) node_graph_kernel<false, RS_CAP_LONG><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
+    else node_graph_kernel<false><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     RCHK(dscan_incl_i64(Gr.ptr, Gr.ptr, nv + 1, nullptr, err));
     RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
@@ -2242,13 +2303,13 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     RCHK(S.alloc(&Gr.val, Gr.nnz, err));
     const char* fe = std::getenv("MAMG_CSR2BSR_FILL");   // 0: the column + value staged merge (tests, A/B)
     if (fe && std::atoi(fe) == 0) {
-      node_graph_kernel<true><<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
+      node_graph_kernel<true><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
     } else {
       Scratch TS;
       double* T = nullptr;
       RCHK(TS.alloc(&T, 4 * std::max<int64_t>(Gr.nnz, 1), err));
-      node_graph_fill_kernel<<<(unsigned)((nv + RS_NODES - 1) / RS_NODES), RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr,
-                                                                                      Gr.col, Gr.val, T);
+      if (lng) node_graph_fill_kernel<RS_CAP_LONG><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val, T);
+      else node_graph_fill_kernel<RS_CAP><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val, T);
       HIPCHK(hipGetLastError());
     }
   }
@@ -2312,6 +2373,8 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   RCHK(S.alloc(&m1, nv, err));
   RCHK(shards_alloc(&S, &und, err));
   mis_init_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, flag, level, state, low, nonisol);
+  const char* ms = std::getenv("MAMG_MIS_STAGED");   // 0: the lane-per-row walks (tests, A/B)
+  const bool mis_staged = ms ? std::atoi(ms) != 0 : true;
   for (int rounds = 0;; ++rounds) {
     if (rounds > 10000) { *err = "mis2 did not converge"; return MAMG_ERR_SETUP; }
     RCHK(shards_zero(und));
@@ -2320,8 +2383,16 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     unsigned long long hu = 0;
     RCHK(shards_read(und, false, &hu, err));
     if (hu == 0) break;
-    mis_max_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, key, m1);
-    mis_update_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
+    if (mis_staged) {   // the update stages every entry: only while many nodes are undecided
+      mis_staged_kernel<false><<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, key, nullptr, m1);
+      if (hu * 4 > (unsigned long long)nv)
+        mis_staged_kernel<true><<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
+      else
+        mis_update_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
+    } else {
+      mis_max_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, key, m1);
+      mis_update_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, Gr.col, flag, m1, key, state);
+    }
   }
   int64_t *f = nullptr, *agg = nullptr, *agg2 = nullptr, *agg3 = nullptr;
   RCHK(S.alloc(&f, nv, err));

@@ -9,7 +9,7 @@
 // contiguous entry ranges of its 64 nodes' rows -- ptr[I0] .. ptr[I0 + 64] of
 // field 0 and the same of field 1 -- into LDS with coalesced loads, then each
 // lane merges from LDS in the same order as before.  Ranges longer than CAP
-// (coarse Galerkin rows) are read from global memory exactly as before.
+// are read from global memory exactly as before.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -20,13 +20,17 @@ namespace mamg {
 
 constexpr int RS_NODES = 64;     // nodes per wave (= workgroup)
 constexpr int RS_CAP = 2048;     // staged entries per field (A0: ~1900)
+constexpr int RS_CAP_LONG = 8192; // level-1 rows: ~83 entries, ~5.3 K per field and wave
+constexpr int RS_BATCH = 8;      // loads per lane in flight while staging
 
 // VALS false (the count passes): columns only, 16 KB instead of 48 KB of LDS
 // per workgroup, so 3 -> 10 waves per CU
-template <bool VALS>
+// CAP: entries per field (RS_CAP; RS_CAP_LONG for the coarse Galerkin rows'
+// column-only passes, 64 KB)
+template <bool VALS, int CAP = RS_CAP>
 struct RowStageT {
-  int32_t c[2][RS_CAP];
-  double v[2][VALS ? RS_CAP : 1];
+  int32_t c[2][CAP];
+  double v[2][VALS ? CAP : 1];
 };
 using RowStage = RowStageT<true>;
 
@@ -57,8 +61,8 @@ struct RowView {
 // Stage the rows of nodes [I0, I0 + RS_NODES) (clipped to nr) of both fields;
 // fills view[2] (LDS when the ranges fit, else global).  Every lane of the
 // wave must call it (the loads and the barrier are wave-wide).
-template <bool VALS>
-__device__ __forceinline__ void stage_rows(RowStageT<VALS>& S, const int64_t* __restrict__ ptr,
+template <bool VALS, int CAP>
+__device__ __forceinline__ void stage_rows(RowStageT<VALS, CAP>& S, const int64_t* __restrict__ ptr,
                                            const int32_t* __restrict__ col, const double* __restrict__ val,
                                            int64_t nr, int64_t I0, RowView* view) {
   const int lane = threadIdx.x & 63;
@@ -69,13 +73,32 @@ __device__ __forceinline__ void stage_rows(RowStageT<VALS>& S, const int64_t* __
     b[f] = ptr[f * nr + I0];
     n[f] = ptr[f * nr + I1] - b[f];
   }
-  const bool fits = n[0] <= RS_CAP && n[1] <= RS_CAP;
+  const bool fits = n[0] <= CAP && n[1] <= CAP;
   if (fits) {
+    // RS_BATCH loads in flight per lane before their LDS writes: one load per
+    // iteration waited out an HBM latency each time, and at 3 waves per CU
+    // (48 KB each) the copy, not the merge, set the kernels' time
 #pragma unroll
     for (int f = 0; f < 2; ++f)
-      for (int64_t t = lane; t < n[f]; t += 64) {
-        S.c[f][t] = col[b[f] + t];
-        if (VALS) S.v[f][t] = val[b[f] + t];
+      for (int64_t t0 = 0; t0 < n[f]; t0 += 64 * RS_BATCH) {
+        int32_t cc[RS_BATCH];
+        double vv[RS_BATCH];
+#pragma unroll
+        for (int u = 0; u < RS_BATCH; ++u) {
+          const int64_t t = t0 + u * 64 + lane;
+          if (t < n[f]) {
+            cc[u] = col[b[f] + t];
+            if (VALS) vv[u] = val[b[f] + t];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < RS_BATCH; ++u) {
+          const int64_t t = t0 + u * 64 + lane;
+          if (t < n[f]) {
+            S.c[f][t] = cc[u];
+            if (VALS) S.v[f][t] = vv[u];
+          }
+        }
       }
     __syncthreads();
 #pragma unroll
@@ -84,6 +107,26 @@ __device__ __forceinline__ void stage_rows(RowStageT<VALS>& S, const int64_t* __
   } else {
 #pragma unroll
     for (int f = 0; f < 2; ++f) view[f] = RowView{col, val, nullptr, nullptr, 0, false};
+  }
+}
+
+// dst[slot[t]] = val[b + t] for t < n (the two-phase fills' value sweep, slot
+// in LDS), RS_BATCH coalesced loads in flight per lane
+__device__ __forceinline__ void scatter_staged(const int32_t* slot, const double* __restrict__ val, int64_t b,
+                                               int64_t n, double* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t t0 = 0; t0 < n; t0 += 64 * RS_BATCH) {
+    double vv[RS_BATCH];
+#pragma unroll
+    for (int u = 0; u < RS_BATCH; ++u) {
+      const int64_t t = t0 + u * 64 + lane;
+      if (t < n) vv[u] = val[b + t];
+    }
+#pragma unroll
+    for (int u = 0; u < RS_BATCH; ++u) {
+      const int64_t t = t0 + u * 64 + lane;
+      if (t < n) dst[slot[t]] = vv[u];
+    }
   }
 }
 

@@ -96,19 +96,22 @@ def test_gpu_spgemm_staging_bitwise(lib_built, monkeypatch, dim, n, g, kw, stage
     Hg.close()
 
 
+@pytest.mark.parametrize('knob', ['MAMG_CSR2BSR_FILL', 'MAMG_MIS_STAGED'])
 @pytest.mark.parametrize('dim,n,g,kw', [(3, 16, 1e6, dict()), (2, 64, 1e4, dict(post_fusion=0)),
                                         (3, 32, 1e6, dict(smoother=12)), (3, 16, 1e2, dict(AMG_type=1))])
-def test_csr2bsr_fill_variants_bitwise(lib_built, monkeypatch, dim, n, g, kw):
+def test_csr2bsr_fill_variants_bitwise(lib_built, monkeypatch, dim, n, g, kw, knob):
     """The device CSR -> BSR2 fill pass with columns only in LDS (slots
     written in place, values scattered by a coalesced sweep; default) and the
     column + value staged merge (MAMG_CSR2BSR_FILL=0) give the same layouts:
-    every level's format and the applies are equal bit for bit."""
+    every level's format and the applies are equal bit for bit.  Likewise the
+    MIS-2 maxima over staged rows and the lane-per-row walks
+    (MAMG_MIS_STAGED=0)."""
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
     outs, fmts = [], []
     for f in ('1', '0'):
-        monkeypatch.setenv('MAMG_CSR2BSR_FILL', f)
+        monkeypatch.setenv(knob, f)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **kw)
         fmts.append([B.level_format(lv) for lv in range(B.num_levels)])
         outs.append([B * mo.seeded_rhs(s.N, seed) for seed in (1234, 7)])
