@@ -179,6 +179,12 @@ typedef struct mamg_hier mamg_hier;       /* host hierarchy (setup result)  */
 
 /* ---- library ---------------------------------------------------------- */
 int mamg_abi_version(void);
+/* Release the device blocks the GPU setups keep cached for the process's next
+ * setup (their temporaries: after a setup returns, none is in use).  Library
+ * housekeeping with no reference counterpart: a caller sharing the GPU with
+ * other allocators calls it after its setups; the library also releases them
+ * by itself when one of its own allocations runs out of HBM. */
+int mamg_release_setup_cache(void);
 const char* mamg_last_error(void);
 void mamg_params_default(mamg_params* p);
 

@@ -12,5 +12,15 @@ from . import _lib, fileio, parameters, precond, problems
 from .amg import DistMetricAMG, DistPlan, GlooExchange, HostHierarchy, MetricAMG, metricAMG
 from .krylov import ConjGrad, DistConjGrad, lanczos_eigenvalues
 
+
+def release_setup_cache():
+    """Release the device blocks the GPU setups keep cached for the process's
+    next setup (include/mamg.h mamg_release_setup_cache): for a caller that
+    shares the GPU with other allocators, after its setups."""
+    rc = _lib.lib().mamg_release_setup_cache()
+    if rc:
+        raise RuntimeError('mamg_release_setup_cache failed (%d)' % rc)
+
+
 __all__ = ['MetricAMG', 'metricAMG', 'HostHierarchy', 'DistPlan', 'DistMetricAMG', 'GlooExchange', 'ConjGrad', 'DistConjGrad',
-           'lanczos_eigenvalues', 'parameters', 'problems', 'precond', 'fileio', '_lib']
+           'lanczos_eigenvalues', 'release_setup_cache', 'parameters', 'problems', 'precond', 'fileio', '_lib']

@@ -67,6 +67,7 @@ class mamg_exchange(C.Structure):
 # every symbol include/mamg.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     'mamg_abi_version': (C.c_int, []),
+    'mamg_release_setup_cache': (C.c_int, []),
     'mamg_last_error': (C.c_char_p, []),
     'mamg_params_default': (None, [C.POINTER(mamg_params)]),
     'mamg_gen_bidomain_size': (C.c_int, [C.c_int, C.c_int64, P_I64, P_I64]),

@@ -60,10 +60,21 @@ using mamg::set_error;
   GUARD_END
 
 namespace {
-// releases the setup temporaries' cached blocks (dmem.h) when a setup
-// returns, after its own temporaries went back to the cache
+// The setup temporaries' cached blocks (dmem.h) stay cached for the
+// process's next setup: releasing them at the end of every setup made one
+// phase of one or two later setups of a long-lived process seconds long
+// (fresh blocks in a heap earlier setups had fragmented; the bench's profile
+// comparison: 5.5-5.9 s instead of 0.8 s, scripts/runs/gpu_r05z9.sh).
+// mamg_release_setup_cache() releases them; MAMG_TMP_KEEP=0 restores the
+// release at the end of every setup.
 struct TmpTrim {
-  ~TmpTrim() { mamg::dev_tmp_trim(); }
+  ~TmpTrim() {
+    static const bool keep = [] {
+      const char* e = std::getenv("MAMG_TMP_KEEP");
+      return e ? std::atoi(e) != 0 : true;
+    }();
+    if (!keep) mamg::dev_tmp_trim();
+  }
 };
 
 int to_view(const mamg_csr* A, mamg::CsrView* v) {
@@ -126,6 +137,13 @@ struct Seeds {
 extern "C" {
 
 int mamg_abi_version(void) { return MAMG_ABI_VERSION; }
+
+int mamg_release_setup_cache(void) {
+  GUARD_BEGIN
+  mamg::dev_tmp_trim();
+  return MAMG_OK;
+  GUARD_END
+}
 const char* mamg_last_error(void) { return mamg::g_err.c_str(); }
 
 void mamg_params_default(mamg_params* p) {

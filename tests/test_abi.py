@@ -261,3 +261,10 @@ def test_no_stream_ordered_pool_or_contiguous_allocations(lib_built):
     assert 'hipMalloc' in imported
     for bad in ('hipMallocAsync', 'hipFreeAsync', 'hipMallocFromPoolAsync', 'hipExtMallocWithFlags'):
         assert bad not in imported, bad
+
+
+def test_release_setup_cache_without_gpu(lib_built):
+    """mamg_release_setup_cache (include/mamg.h): with nothing cached it makes
+    no device call, so it returns 0 on a host without a GPU too."""
+    import metric_amg_examples_amd as M
+    M.release_setup_cache()

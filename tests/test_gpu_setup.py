@@ -294,3 +294,20 @@ def test_gpu_setup_large_3d_bitwise(lib_built):
     Hh = M.HostHierarchy(s, idofs=s.idofs, num_functions=2)
     Hg = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True)
     hierarchies_equal(Hh, Hg)
+
+
+def test_setups_with_kept_cache_then_released_bitwise(lib_built):
+    """The GPU setups keep their temporaries' blocks cached for the process's
+    next setup (capi.cpp TmpTrim, MAMG_TMP_KEEP): a setup from reused blocks,
+    and one after mamg_release_setup_cache, give the same applies bit for bit."""
+    M = _mamg()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    outs = []
+    for k in range(3):
+        if k == 2:
+            M.release_setup_cache()
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        outs.append(B * mo.seeded_rhs(s.N, 1234))
+        B.close()
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
