@@ -61,10 +61,11 @@ using mamg::set_error;
 
 namespace {
 // The setup temporaries' cached blocks (dmem.h) stay cached for the
-// process's next setup: releasing them at the end of every setup made one
-// phase of one or two later setups of a long-lived process seconds long
-// (fresh blocks in a heap earlier setups had fragmented; the bench's profile
-// comparison: 5.5-5.9 s instead of 0.8 s, scripts/runs/gpu_r05z9.sh).
+// process's next setup: with them released at the end of every setup, one
+// phase of one or two later setups of a long-lived process took seconds
+// (the bench's profile comparison: 5.5-5.9 s instead of 0.8 s in 2 of 2
+// runs, none with the cache kept; scripts/runs/gpu_r05z9.sh; fewer such
+// outliers since, not none: DESIGN.md section 5).
 // mamg_release_setup_cache() releases them; MAMG_TMP_KEEP=0 restores the
 // release at the end of every setup.
 struct TmpTrim {
