@@ -95,6 +95,63 @@ def cpu_model():
     return None
 
 
+def one_gpu_check(args, M, B, r, z, r_full, sysm, prof, dev, rdev, gloo, rank, world, dist_res, barrier, allsum):
+    """N > 1: z (this rank's slice of the distributed B r) and the distributed
+    PCG residual history against rank 0's one-GPU preconditioner on the same
+    matrix; returns the record (every rank computes the same one)."""
+    import torch
+    import torch.distributed as tdist
+    M.release_setup_cache()                 # the distributed setup's cached blocks
+    barrier()
+    t0 = time.time()
+    n = M.problems.finest_n(args.dim, args.nrefs, args.problem)
+    N = sysm.N
+    z1 = torch.empty(N, dtype=torch.float64, device=rdev)
+    meta = [None]
+    if rank == 0:
+        A0 = M.problems.bidomain_device(args.dim, n, args.gamma, device=dev)
+        B1 = M.MetricAMG(A0, sysm.W, idofs=sysm.idofs, num_functions=2, device=dev.index, setup='gpu', **prof)
+        rf = torch.as_tensor(r_full).to(dev)
+        zz = torch.zeros_like(rf)
+        B1.apply_device(rf, zz)
+        res1 = None
+        if dist_res is not None:
+            B1._Aop = sysm
+            cg = M.ConjGrad(sysm, precond=B1, tolerance=1e-8, maxiter=500)
+            cg.solve_device(rf)
+            res1 = [float(v) for v in cg.residuals]
+        torch.cuda.synchronize(dev)
+        z1.copy_(zz)
+        meta = [{'residuals': res1, 'setup_s': round(time.time() - t0, 3)}]
+        B1.close()
+        del A0, rf, zz
+        M.release_setup_cache()
+    tdist.broadcast(z1, src=0)
+    tdist.broadcast_object_list(meta, src=0)
+    z1 = z1.to(dev)
+    nv = B.nv
+    zl = torch.cat([z1[B.o0:B.o1], z1[nv + B.o0:nv + B.o1]])
+    num = allsum(float(((z - zl) ** 2).sum()))
+    den = allsum(float((zl ** 2).sum()))
+    rz_d = allsum(float((r * z).sum()))
+    rz_1 = allsum(float((r * zl).sum()))
+    del z1, zl
+    out = {'z_rel_vs_1gpu': float(np.sqrt(num / den)) if den > 0 else None,
+           'rz_dist': rz_d, 'rz_1gpu': rz_1, 'seed': 1234,
+           'one_gpu_setup_s': meta[0]['setup_s'],
+           'note': 'rank 0 set up the one-GPU preconditioner on the same matrix (A_0 regenerated in its HBM) '
+                   'after the timed region; z = B r of the %d ranks gathered against its z' % world}
+    res1 = meta[0]['residuals']
+    if res1 is not None and dist_res is not None:
+        out['pcg_niters_1gpu'] = len(res1) - 1
+        out['pcg_niters_dist'] = len(dist_res) - 1
+        out['pcg_niters_equal'] = len(res1) == len(dist_res)
+        out['max_rel_residual_diff'] = float(max(abs(a - b) / b for a, b in zip(dist_res, res1))) \
+            if len(res1) == len(dist_res) else None
+    barrier()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -111,9 +168,13 @@ def main():
     ap.add_argument('--cpu-sample', type=int, default=10,
                     help='CPU baseline: timed applies after 2 warm-ups, median reported (0: skip)')
     ap.add_argument('--no-breakdown', action='store_true')
-    ap.add_argument('--pcg', type=int, default=-1,
-                    help='run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL); '
-                         'default: on for N = 1, off for N > 1')
+    ap.add_argument('--pcg', type=int, default=1,
+                    help='run one full PCG solve (N = 1: device PCG; N > 1: DistConjGrad over RCCL, its '
+                         'iterations and residual history checked against the one-GPU solve)')
+    ap.add_argument('--check-1gpu', type=int, default=1,
+                    help='N > 1: rank 0 also sets up the one-GPU preconditioner on the same matrix after the '
+                         'timed region; the line carries z = B r gathered over the ranks against its z, and the '
+                         'distributed PCG against its PCG (north star: equal iteration count at 1/2/4/8)')
     ap.add_argument('--cpu-pcg', type=int, default=1,
                     help='N = 1: also run the CPU PCG (oracle C cycle + SpMV, host cores) on the same '
                          'hierarchy and report its iteration count next to the GPU one')
@@ -138,8 +199,6 @@ def main():
     ap.add_argument('--compare-host-setup', action='store_true',
                     help='also time the host setup of the same hierarchy (N = 1)')
     args = ap.parse_args()
-    if args.pcg < 0:
-        args.pcg = 1 if int(os.environ.get('WORLD_SIZE', '1')) == 1 else 0
     prof = dict(smoother={'jacobi': 3, 'poly': 12, 'sgs': 11, 'gs': 10}[args.smoother], coarse_scaling=args.scaling,
                 cycle_type={'V': 1, 'W': 2}[args.cycle], poly_degree=args.poly_degree,
                 Schwarz_type={'sgs': 7, 'gs': 7}.get(args.smoother, 4))
@@ -348,7 +407,19 @@ def main():
         solver.solve([r.clone()])
         barrier()
         pcg = {'niters': len(solver.residuals) - 1, 'residual': solver.residuals[-1],
-               'seconds': round(allmax(time.perf_counter() - t0), 3)}
+               'seconds': round(allmax(time.perf_counter() - t0), 3),
+               'note': 'DistConjGrad: cbc.block ConjGrad on the row-partitioned slices, dots all-reduced '
+                       '(src/bidomain_3d.py:149)'}
+        gpu_res = list(solver.residuals)
+
+    # ---- N > 1 parity against one GPU: rank 0 builds the
+    # single-GPU preconditioner on the same matrix (A_0 regenerated in its HBM)
+    # after everything timed; z = B r and the PCG solve are compared with the
+    # distributed ones
+    check_1gpu = None
+    if world > 1 and args.check_1gpu and args.problem == 'bidomain':
+        check_1gpu = one_gpu_check(args, M, B, r, z, r_full, sysm, prof, dev, rdev, gloo, rank, world,
+                                   gpu_res if args.pcg else None, barrier, allsum)
 
     # ---- the reference's smoother family on the GPU (multicolour SGS +
     # coarse-grid scaling): iterations and time to solution next to the default
@@ -550,6 +621,7 @@ def main():
         'setup': dict(setup_info, generate_s=round(t_gen, 2)),
         'breakdown': breakdown,
         'pcg': pcg,
+        'check_1gpu': check_1gpu,
         'pcg_profiles': profiles,
     }
     if rank == 0:

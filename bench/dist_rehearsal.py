@@ -55,6 +55,8 @@ def main():
     import torch
     import metric_amg_examples_amd as M
     n = M.problems.finest_n(3, args.nrefs)
+    if os.environ.get('MAMG_DIST_TEST'):       # the library reads no environment: pass it on
+        M._lib.set_option('MAMG_DIST_TEST', os.environ['MAMG_DIST_TEST'])
     torch.cuda.init()
     rss_start = rss_gb()
     if args.source == 'device':

@@ -185,6 +185,13 @@ int mamg_abi_version(void);
  * other allocators calls it after its setups; the library also releases them
  * by itself when one of its own allocations runs out of HBM. */
 int mamg_release_setup_cache(void);
+/* Bound of that cache, bytes per device: at the end of every setup the idle
+ * blocks above it are freed (largest first).  bytes < 0: the default, an
+ * eighth of the device's HBM; 0: everything released after every setup.
+ * The SpGEMM staging block of the GPU setup counts against it. */
+int mamg_set_setup_cache_limit(int64_t bytes);
+/* Idle cached bytes of a device and its current limit (either may be NULL). */
+int mamg_setup_cache_bytes(int device, int64_t* idle_bytes, int64_t* limit_bytes);
 const char* mamg_last_error(void);
 void mamg_params_default(mamg_params* p);
 
@@ -370,19 +377,6 @@ int mamg_setup_gpu_device(const mamg_csr* dA, const int32_t* idofs, int64_t n_id
  * planning); the hierarchy keeps a view of A as mamg_host_setup does. */
 int mamg_gpu_host_setup(const mamg_csr* A, const int32_t* idofs, int64_t n_idofs,
                         const mamg_params* params, mamg_hier** out);
-/* Verification of a row-sharded Galerkin product (the start of a
- * partition-local setup): on nranks
- * virtual ranks (fine nodes and coarse nodes split into even ranges), rank p
- * forms its (A P) rows from its A rows and the P rows of the fine dofs they
- * reach (its own and a halo), then its coarse rows of R (A P), R = P^T, from
- * its R rows and the (A P) rows of the fine dofs those reach, each taken from
- * the owner rank's sharded result; the GPU setup's own SpGEMM throughout.
- * A, P, Ac: one level's field-major 2-function operator, prolongator and the
- * hierarchy's next-level operator (host CSR).  res6: (A P) rows differing
- * from the unsharded product, A_c rows differing from Ac (bitwise), halo P
- * rows read, halo (A P) rows read, (A P) rows and A_c rows compared. */
-int mamg_sharded_galerkin_check(const mamg_csr* A, const mamg_csr* P, const mamg_csr* Ac, int nranks, int device,
-                                int64_t* res6);
 /* Setup phase timings of a GPU-setup handle, ms[8]: aggregation, smoothers,
  * prolongator, Galerkin, coarsest, apply-layout build, setup total, A upload
  * (zeros for handles from mamg_setup / mamg_upload). */

@@ -64,10 +64,14 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, VP, P_F64, C.c_int64)
 class mamg_exchange(C.Structure):
     _fields_ = [('ctx', VP), ('sendrecv', SENDRECV_FN), ('allreduce', ALLREDUCE_FN)]
 
-# every symbol include/mamg.h declares: name -> (restype, argtypes)
+# every symbol include/mamg.h and include/mamg_test.h declare: name -> (restype, argtypes)
 SIGNATURES = {
     'mamg_abi_version': (C.c_int, []),
     'mamg_release_setup_cache': (C.c_int, []),
+    'mamg_set_setup_cache_limit': (C.c_int, [C.c_int64]),
+    'mamg_setup_cache_bytes': (C.c_int, [C.c_int, P_I64, P_I64]),
+    'mamg_set_option': (C.c_int, [C.c_char_p, C.c_char_p]),
+    'mamg_option_names': (C.c_char_p, []),
     'mamg_last_error': (C.c_char_p, []),
     'mamg_params_default': (None, [C.POINTER(mamg_params)]),
     'mamg_gen_bidomain_size': (C.c_int, [C.c_int, C.c_int64, P_I64, P_I64]),
@@ -168,6 +172,17 @@ def lib():
             raise ImportError('libmamg ABI mismatch')
         _lib = L
     return _lib
+
+
+def set_option(name, value):
+    """mamg_set_option (include/mamg_test.h): set (value not None) or reset
+    one of the library's internal layout switches for the process."""
+    v = None if value is None else str(value).encode()
+    check(lib().mamg_set_option(name.encode(), v))
+
+
+def option_names():
+    return lib().mamg_option_names().decode().split(',')
 
 
 def check(rc):

@@ -12,6 +12,73 @@
 #include "device.h"
 #include "dist.h"
 #include "host.h"
+#include "mamg_test.h"
+#include "opts.h"
+
+#if MAMG_DIAG
+// Diagnosis build: a SIGSEGV tracer for host crashes inside the library or
+// the HIP runtime.  On an alternate signal stack
+// (a stack overflow leaves none), it prints the fault address, the faulting
+// thread's stack bounds, the frame depth and the innermost / outermost native
+// frames, then restores the previous handler (Python's faulthandler or the
+// default) and returns, so the re-executed access reports as before.
+#include <execinfo.h>
+#include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
+namespace {
+struct sigaction g_prev_segv;
+constexpr int SEGV_FRAMES = 1 << 18;
+void* g_frames[SEGV_FRAMES];
+void segv_write(const char* s, int n) {
+  while (n > 0) {
+    const ssize_t w = write(2, s, n);
+    if (w <= 0) return;
+    s += w;
+    n -= (int)w;
+  }
+}
+void segv_trace(int sig, siginfo_t* si, void*) {
+  char buf[512];
+  void* sb = nullptr;
+  size_t ss = 0;
+  pthread_attr_t a;
+  if (pthread_getattr_np(pthread_self(), &a) == 0) {
+    pthread_attr_getstack(&a, &sb, &ss);
+    pthread_attr_destroy(&a);
+  }
+  const int depth = backtrace(g_frames, SEGV_FRAMES);
+  int n = std::snprintf(buf, sizeof buf,
+                        "[mamg diag] signal %d at address %p; thread stack [%p, %p) = %.1f MiB; %d native frames%s\n",
+                        sig, si ? si->si_addr : nullptr, sb, (char*)sb + ss, ss / 1048576.0, depth,
+                        depth == SEGV_FRAMES ? " (buffer full)" : "");
+  segv_write(buf, n);
+  const int inner = depth < 48 ? depth : 48;
+  segv_write("[mamg diag] innermost frames:\n", 30);
+  backtrace_symbols_fd(g_frames, inner, 2);
+  if (depth > inner) {
+    const int outer = depth - inner < 32 ? depth - inner : 32;
+    segv_write("[mamg diag] outermost frames:\n", 30);
+    backtrace_symbols_fd(g_frames + depth - outer, outer, 2);
+  }
+  sigaction(SIGSEGV, &g_prev_segv, nullptr);
+}
+__attribute__((constructor)) void segv_install() {
+  static char alt[1 << 20];
+  stack_t st{};
+  st.ss_sp = alt;
+  st.ss_size = sizeof alt;
+  sigaltstack(&st, nullptr);
+  void* f[4];
+  (void)backtrace(f, 4);                 // loads the unwinder before any fault
+  struct sigaction sa{};
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+}  // namespace
+#endif
 
 namespace mamg {
 namespace {
@@ -61,21 +128,15 @@ using mamg::set_error;
 
 namespace {
 // The setup temporaries' cached blocks (dmem.h) stay cached for the
-// process's next setup: with them released at the end of every setup, one
-// phase of one or two later setups of a long-lived process took seconds
-// (the bench's profile comparison: 5.5-5.9 s instead of 0.8 s in 2 of 2
-// runs, none with the cache kept; scripts/runs/gpu_r05z9.sh; fewer such
-// outliers since, not none: DESIGN.md section 5).
-// mamg_release_setup_cache() releases them; MAMG_TMP_KEEP=0 restores the
-// release at the end of every setup.
+// process's next setup, up to the cache limit (mamg_set_setup_cache_limit;
+// default an eighth of the device's HBM): with them released at the end of
+// every setup, one phase of one or two later setups of a long-lived process
+// took seconds (the bench's profile comparison: 5.5-5.9 s instead of 0.8 s in
+// 2 of 2 runs, scripts/runs/gpu_r05z9.sh).  Above the
+// limit the largest idle blocks are freed at the end of every setup;
+// mamg_release_setup_cache() releases all of them.
 struct TmpTrim {
-  ~TmpTrim() {
-    static const bool keep = [] {
-      const char* e = std::getenv("MAMG_TMP_KEEP");
-      return e ? std::atoi(e) != 0 : true;
-    }();
-    if (!keep) mamg::dev_tmp_trim();
-  }
+  ~TmpTrim() { mamg::dev_tmp_trim_to_limit(); }
 };
 
 int to_view(const mamg_csr* A, mamg::CsrView* v) {
@@ -145,6 +206,34 @@ int mamg_release_setup_cache(void) {
   return MAMG_OK;
   GUARD_END
 }
+int mamg_set_setup_cache_limit(int64_t bytes) {
+  GUARD_BEGIN
+  mamg::dev_set_cache_limit(bytes < 0 ? -1 : bytes);
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_setup_cache_bytes(int device, int64_t* idle_bytes, int64_t* limit_bytes) {
+  GUARD_BEGIN
+  if (device < 0 || device > 63) { set_error("device out of range"); return MAMG_ERR_ARG; }
+  if (idle_bytes) *idle_bytes = mamg::dev_cache_idle_bytes(device);
+  if (limit_bytes) *limit_bytes = mamg::dev_cache_limit(device);
+  return MAMG_OK;
+  GUARD_END
+}
+
+int mamg_set_option(const char* name, const char* value) {
+  GUARD_BEGIN
+  if (!mamg::set_opt(name, value)) {
+    set_error(std::string("unknown option ") + (name ? name : "(null)") + "; known: " + mamg::opt_names());
+    return MAMG_ERR_ARG;
+  }
+  return MAMG_OK;
+  GUARD_END
+}
+
+const char* mamg_option_names(void) { return mamg::opt_names(); }
+
 const char* mamg_last_error(void) { return mamg::g_err.c_str(); }
 
 void mamg_params_default(mamg_params* p) {
@@ -396,7 +485,7 @@ int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int3
     // G in HBM.  MAMG_DIST_TEST=full: the whole hierarchy downloaded and
     // planned on the host; =rows: the rank's rows downloaded, planned on the
     // host (both bitwise the default; tests)
-    const char* e = std::getenv("MAMG_DIST_TEST");
+    const char* e = mamg::opt("MAMG_DIST_TEST");
     const std::string et = e ? e : "";
     const int mode = et == "full" ? 1 : et == "rows" ? 2 : 0;
     if (rc) {

@@ -24,6 +24,13 @@ void dev_layout_ms(const DeviceHandle* h, double* ms4);
 void dev_destroy(DeviceHandle* h);
 // release the cached blocks of the setup temporaries (dmem.h tmp_trim_all)
 void dev_tmp_trim();
+// the end of a setup: idle cached blocks above the cache limit freed
+void dev_tmp_trim_to_limit();
+// cache limit (bytes per device; < 0 default = HBM / 8, 0 = release every setup)
+void dev_set_cache_limit(int64_t bytes);
+int64_t dev_cache_limit(int device);
+// idle cached bytes of a device (idle temporaries + the SpGEMM staging block)
+int64_t dev_cache_idle_bytes(int device);
 int64_t dev_nrows(const DeviceHandle* h);
 int dev_num_levels(const DeviceHandle* h);
 int dev_layout(const DeviceHandle* h);

@@ -41,9 +41,55 @@
 
 #include "device.h"
 #include "dmem.h"
+#include "opts.h"
 #include "rowstage.h"
 
+#include <pthread.h>
+
 namespace mamg {
+
+// hipGraphInstantiate on a thread whose stack fits the graph.  The runtime
+// walks a captured graph recursively at instantiation, one 64-byte frame per
+// node of its longest dependency chain (a stream capture is one chain): the
+// 8 virtual ranks' lockstep apply of the reference preset at nrefs=5 overflowed
+// the 8 MiB main-thread stack after 130,903 frames and crashed the process
+// (SIGSEGV on the guard page inside hipGraphInstantiate; diagnosis-build tracer,
+// profiles/r06_graph_segv.txt).  Graphs of up to
+// GRAPH_INSTANTIATE_INLINE nodes instantiate on the caller's thread (at most
+// 1 MiB of its stack); larger ones on a helper thread with 256 B of stack per
+// node (4x the measured frame) + 16 MiB, reserved, touched only as deep as the
+// walk goes.
+constexpr size_t GRAPH_INSTANTIATE_INLINE = 16384;
+hipError_t graph_instantiate(hipGraphExec_t* ex, hipGraph_t g) {
+  size_t nodes = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &nodes);
+  if (e != hipSuccess) return e;
+  if (nodes <= GRAPH_INSTANTIATE_INLINE) return hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
+  struct Job {
+    hipGraphExec_t* ex;
+    hipGraph_t g;
+    int dev;
+    hipError_t e;
+  } job{ex, g, 0, hipSuccess};
+  if ((e = hipGetDevice(&job.dev)) != hipSuccess) return e;
+  pthread_attr_t a;
+  if (pthread_attr_init(&a) != 0) return hipErrorOutOfMemory;
+  const size_t stack = ((nodes * 256 + ((size_t)16 << 20)) + 4095) & ~(size_t)4095;
+  pthread_t t;
+  int rc = pthread_attr_setstacksize(&a, stack);
+  if (rc == 0)
+    rc = pthread_create(&t, &a, [](void* p) -> void* {
+      Job* j = static_cast<Job*>(p);
+      j->e = hipSetDevice(j->dev);
+      if (j->e == hipSuccess) j->e = hipGraphInstantiate(j->ex, j->g, nullptr, nullptr, 0);
+      return nullptr;
+    }, &job);
+  pthread_attr_destroy(&a);
+  if (rc != 0) return hipErrorOutOfMemory;
+  pthread_join(t, nullptr);
+  return job.e;
+}
+
 namespace {
 
 #define HIPCHK(expr)                                                                 \
@@ -1976,26 +2022,26 @@ void read_knobs() {
   e = std::getenv("MAMG_K_VARIANT");   // the level-0 K kernel (diagnosis build: tests, A/Bs; read at upload)
   g_kvar = e ? std::atoi(e) : 0;
 #endif
-  e = std::getenv("MAMG_POST_K");
+  e = opt("MAMG_POST_K");
   g_post_k = e ? std::atoi(e) : 1;   // 0: [P | AP]; 1: K (one block per slot); 2: K, split layout forced
-  e = std::getenv("MAMG_SELL_MIN_ROWS");
+  e = opt("MAMG_SELL_MIN_ROWS");
   g_sell_min_rows = e ? std::atoll(e) : (1 << 20);
-  e = std::getenv("MAMG_TAIL_NODES");
+  e = opt("MAMG_TAIL_NODES");
   g_tail_nodes = e ? std::atoll(e) : 0;
   g_tail_set = e != nullptr;
-  e = std::getenv("MAMG_TAIL_VL");
+  e = opt("MAMG_TAIL_VL");
   g_tail_vl = e ? std::max(1, std::min(64, std::atoi(e))) : 4;
-  e = std::getenv("MAMG_MSELL_MIN_ROWS");
+  e = opt("MAMG_MSELL_MIN_ROWS");
   g_msell_min_rows = e ? std::atoll(e) : ((int64_t)1 << 40);
-  e = std::getenv("MAMG_HALF");
+  e = opt("MAMG_HALF");
   g_half = e ? std::atoi(e) != 0 : 1;
-  e = std::getenv("MAMG_HALF_BANDS");
+  e = opt("MAMG_HALF_BANDS");
   g_half_bands = e ? std::atoi(e) : 1;
-  e = std::getenv("MAMG_R_BANDS");
+  e = opt("MAMG_R_BANDS");
   g_r_bands = e ? std::atoi(e) : 1;
-  e = std::getenv("MAMG_K_SORT");
+  e = opt("MAMG_K_SORT");
   g_k_sort = e ? std::atoi(e) : 1;
-  e = std::getenv("MAMG_FUSE_RBD");
+  e = opt("MAMG_FUSE_RBD");
   g_fuse_rbd = e ? std::atoi(e) : 2;
 }
 
@@ -2255,7 +2301,7 @@ enum { LT_BUILD = 0, LT_KREGION = 1, LT_REHOME = 2, LT_FINISH = 3 };
 template <class T>
 void poison_doubles(T* p, size_t bytes) {
   if constexpr (std::is_same<T, double>::value) {
-    const char* e = std::getenv("MAMG_POISON");
+    const char* e = opt("MAMG_POISON");
     if (e && std::atoi(e) != 0) (void)dev_memset(p, 0xff, bytes);
   }
 }
@@ -2879,7 +2925,7 @@ int dev_csr_to_bsr(TmpPool* T, const DevMat& M, int64_t nr, int64_t nc, TBsr* B,
   if ((rc = T->alloc(&B->col, B->nb, err))) return rc;
   if ((rc = T->alloc(&B->val, B->nb, err))) return rc;
   // MAMG_CSR2BSR_FILL=0: the column + value staged fill (csr2bsr_kernel<true>; tests, A/B)
-  const char* fe = std::getenv("MAMG_CSR2BSR_FILL");
+  const char* fe = opt("MAMG_CSR2BSR_FILL");
   const bool f2 = fe ? std::atoi(fe) != 0 : true;
   if (nr && f2 && lng)
     csr2bsr_fill_kernel<RS_CAP_LONG><<<g, RS_NODES>>>(nr, nc, M.ptr, M.col, M.val, B->ptr, B->col, B->val);
@@ -4075,7 +4121,7 @@ constexpr int64_t TAIL_LDS_MAX = 160 * 1024 - 1024;   // gfx950: 160 KB per work
 // written ones copied out last.  Returns the dynamic LDS bytes, or 0 (program
 // unchanged: global vectors) when the plan exceeds the LDS.
 int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
-  if (const char* e = std::getenv("MAMG_TAIL_LDS"))
+  if (const char* e = opt("MAMG_TAIL_LDS"))
     if (std::atoi(e) == 0) return 0;
   struct Vec {
     double* base;
@@ -4725,7 +4771,7 @@ int get_graph(DeviceHandle* h, const double* r, double* z, hipGraphExec_t* exec,
   HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
   for (const Op& o : ops) launch(o, h->cap);
   HIPCHK(hipStreamEndCapture(h->cap, &g.graph));
-  HIPCHK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+  HIPCHK(graph_instantiate(&g.exec, g.graph));
   h->graphs.push_back(g);
   *exec = g.exec;
   return MAMG_OK;
@@ -4816,9 +4862,9 @@ void select_k_region(DeviceHandle* h) {
   DLevel& L = h->L[0];
   DBsr& K = L.KPb;
   const size_t bytes = (size_t)K.nbs * 4 * sizeof(double);
-  const char* e = std::getenv("MAMG_KREGION_TRIES");
+  const char* e = opt("MAMG_KREGION_TRIES");
   const int tries = e ? std::atoi(e) : 4;
-  const char* eb = std::getenv("MAMG_KREGION_BUDGET_MS");
+  const char* eb = opt("MAMG_KREGION_BUDGET_MS");
   const double budget = eb ? std::atof(eb) : 200.0;
   if (tries <= 1 || K.sym || !L.r || !L.t || !L.Wd || !h->L[1].x) {
     rehome_array(h, (void**)&K.val, bytes);
@@ -4893,7 +4939,7 @@ void select_k_region(DeviceHandle* h) {
 }
 
 void rehome_operators(DeviceHandle* h) {
-  const char* e = std::getenv("MAMG_REHOME");   // 0: keep the operators where the layout builder put them (tests)
+  const char* e = opt("MAMG_REHOME");   // 0: keep the operators where the layout builder put them (tests)
   if (e && std::atoi(e) == 0) return;
   if (!h->bsr || h->L.size() < 2 || h->L[0].KPb.nr < g_sell_min_rows || !h->L[0].KPb.sell) return;
   DLevel& L = h->L[0];
@@ -5114,7 +5160,7 @@ static thread_local void* g_pre = nullptr;
 static thread_local size_t g_pre_bytes = 0;
 static thread_local int g_pre_dev = -1;
 void dev_prereserve(int device, int64_t nnz, int nranks) {
-  const char* e = std::getenv("MAMG_PRERESERVE_B_PER_NNZ");
+  const char* e = opt("MAMG_PRERESERVE_B_PER_NNZ");
   double b = e ? std::atof(e) : 20.0;
   if (nranks > 1) b = 1.25 * b / nranks + 0.5;
   dev_prereserve_release();
@@ -5284,6 +5330,14 @@ void dev_layout_ms(const DeviceHandle* h, double* ms4) {
 }
 
 void dev_tmp_trim() { tmp_trim_all(); }
+void dev_tmp_trim_to_limit() { tmp_trim_to_limit_all(); }
+void dev_set_cache_limit(int64_t bytes) { set_cache_limit(bytes); }
+int64_t dev_cache_limit(int device) { return cache_limit_dev(device); }
+int64_t dev_cache_idle_bytes(int device) {
+  int64_t b = tmp_idle_bytes(device);
+  std::lock_guard<std::mutex> g(detail::stage_mu());
+  return b + (int64_t)detail::stage_pools()[device & 63].bytes;
+}
 
 void dev_destroy(DeviceHandle* h) {
   if (!h) return;
@@ -5472,7 +5526,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
       pcg_d_kernel<<<g, 256, 0, h->cap>>>(n, st, h->cz, h->cd, d_x);
       e = hipStreamEndCapture(h->cap, &q.graph);
     }
-    if (e == hipSuccess) e = hipGraphInstantiate(&q.exec, q.graph, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = graph_instantiate(&q.exec, q.graph);
     for (hipEvent_t& x : q.ev)
       if (e == hipSuccess) e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -6981,9 +7035,9 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
   }
   {
-    const char* e = std::getenv("MAMG_OVERLAP");
+    const char* e = opt("MAMG_OVERLAP");
     h->overlap = e ? std::atoi(e) != 0 : true;
-    e = std::getenv("MAMG_DIST_TEST");
+    e = opt("MAMG_DIST_TEST");
     h->dry = !comm_id && e && std::string(e) == "dry";
   }
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
@@ -7232,7 +7286,7 @@ int dist_capture(DistHandle* h, const std::vector<DOp>& ops, hipGraph_t* gr, hip
     if (!rc) *err = std::string("stream capture of the distributed apply: ") + hipGetErrorString(e);
     return rc ? rc : MAMG_ERR_HIP;
   }
-  const hipError_t ei = hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
+  const hipError_t ei = graph_instantiate(ex, g);
   if (ei != hipSuccess) {
     (void)hipGraphDestroy(g);
     (void)hipGetLastError();
@@ -7242,12 +7296,6 @@ int dist_capture(DistHandle* h, const std::vector<DOp>& ops, hipGraph_t* gr, hip
   *gr = g;
   return MAMG_OK;
 }
-
-// most ops one captured graph holds: the runtime crashed (host SIGSEGV) while
-// capturing the 8 virtual ranks' lockstep apply of the reference family at
-// nrefs=5 (W-cycle + colour steps: ~10^5 launches), and a one-GPU graph of
-// 1.2 x 10^4 launches (the same family) replays fine; longer op lists stay eager
-constexpr size_t DIST_GRAPH_MAX_OPS = 16384;
 
 int dist_graph_exec(DistHandle* h, const double* d_r, double* d_z, hipGraphExec_t* ex, std::string* err) {
   if (!h->comm && h->nranks > 1 && !h->dry) {
@@ -7265,11 +7313,6 @@ int dist_graph_exec(DistHandle* h, const double* d_r, double* d_z, hipGraphExec_
   }
   std::vector<DOp> ops;
   dapply_ops(h, d_r, d_z, &ops);
-  if (ops.size() > DIST_GRAPH_MAX_OPS) {
-    *err = "distributed apply of " + std::to_string(ops.size()) + " ops: longer than one graph holds (" +
-           std::to_string(DIST_GRAPH_MAX_OPS) + "); the eager apply serves it";
-    return MAMG_ERR_UNSUPPORTED;
-  }
   DistHandle::Graph g{d_r, d_z, nullptr, nullptr};
   const int rc = dist_capture(h, ops, &g.g, &g.e, err);
   if (rc) {
@@ -7531,16 +7574,7 @@ int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vect
   const int P = (int)hs.size();
   HIPCHK(hipSetDevice(hs[0]->device));
   std::vector<std::vector<DOp>> ops(P);
-  size_t nops = 0;
-  for (int p = 0; p < P; ++p) {
-    dapply_ops(hs[p], r[p], z[p], &ops[p]);
-    nops += ops[p].size();
-  }
-  if (nops > DIST_GRAPH_MAX_OPS) {
-    *err = "virtual apply of " + std::to_string(nops) + " ops: longer than one graph holds (" +
-           std::to_string(DIST_GRAPH_MAX_OPS) + ")";
-    return MAMG_ERR_UNSUPPORTED;
-  }
+  for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
   DistHandle* h0 = hs[0];
   if (!h0->cap) HIPCHK(hipStreamCreateWithFlags(&h0->cap, hipStreamNonBlocking));
   HIPCHK(hipStreamBeginCapture(h0->cap, hipStreamCaptureModeThreadLocal));
@@ -7554,7 +7588,7 @@ int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vect
     return rc ? rc : MAMG_ERR_HIP;
   }
   hipGraphExec_t ex = nullptr;
-  const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  const hipError_t ei = graph_instantiate(&ex, g);
   if (ei != hipSuccess) {
     (void)hipGraphDestroy(g);
     *err = std::string("hipGraphInstantiate of the virtual apply: ") + hipGetErrorString(ei);

@@ -247,14 +247,54 @@ inline size_t tmp_round(size_t b) {
 }
 }  // namespace detail
 
-// hipFree every idle cached block of device d (after d's null stream has
-// drained: the last users of an idle block were queued there); the current
-// device is put back
+// ---- the SpGEMM staging block (gsetup.hip spgemm_gl) ------------------------
+// One block per device, allocated at its first use and kept, like the idle
+// temporaries, until the cache is released (tmp_trim_dev): a large block
+// allocated late, in a heap that earlier handles have fragmented, was written
+// ~50x slower (profiles/r05_spgemm_stage_pool.txt).  A product holds it for
+// the whole call (busy): a second host thread's setup on the same device
+// meanwhile gets none and runs the unstaged two-pass product (same bits).
+namespace detail {
+struct StagePool {
+  void* p = nullptr;
+  size_t bytes = 0;
+  bool busy = false;
+};
+inline std::mutex& stage_mu() {
+  static std::mutex m;
+  return m;
+}
+inline StagePool* stage_pools() {
+  static StagePool s[64];
+  return s;
+}
+}  // namespace detail
+
+// free device d's staging block unless a product holds it (the caller has
+// drained d's null stream, where its last users were queued)
+inline void stage_free_dev(int d) {
+  std::lock_guard<std::mutex> g(detail::stage_mu());
+  detail::StagePool& sp = detail::stage_pools()[d & 63];
+  if (!sp.p || sp.busy) return;
+  (void)raw_free(sp.p);
+  sp.p = nullptr;
+  sp.bytes = 0;
+}
+
+// hipFree every idle cached block of device d and its staging block (after
+// d's null stream has drained: the last users of an idle block were queued
+// there); the current device is put back
 inline void tmp_trim_dev(int d) {
   auto& c = detail::tmp_cache();
+  bool stage;
+  {
+    std::lock_guard<std::mutex> g(detail::stage_mu());
+    const detail::StagePool& sp = detail::stage_pools()[d & 63];
+    stage = sp.p && !sp.busy;
+  }
   std::lock_guard<std::mutex> g(c.m);
   auto& idle = c.idle[d & 63];
-  if (idle.empty()) return;
+  if (idle.empty() && !stage) return;
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); return; }
   if (cur != d && hipSetDevice(d) != hipSuccess) { (void)hipGetLastError(); return; }
@@ -264,13 +304,14 @@ inline void tmp_trim_dev(int d) {
     c.made.erase(kv.second);
   }
   idle.clear();
+  if (stage) stage_free_dev(d);
   if (cur != d) (void)hipSetDevice(cur);
 }
 
 // the current device's idle blocks
 inline void tmp_trim() { tmp_trim_dev(detail::cur_device()); }
 
-// every device's idle blocks (the end of a setup)
+// every device's idle blocks and staging blocks (mamg_release_setup_cache)
 inline void tmp_trim_all() {
   for (int d = 0; d < 64; ++d) {
     bool any;
@@ -279,9 +320,126 @@ inline void tmp_trim_all() {
       std::lock_guard<std::mutex> g(c.m);
       any = !c.idle[d].empty();
     }
+    {
+      std::lock_guard<std::mutex> g(detail::stage_mu());
+      any = any || detail::stage_pools()[d].p != nullptr;
+    }
     if (any) tmp_trim_dev(d);
   }
 }
+
+// Bound of the idle cache (bytes per device) kept after a setup: the idle
+// blocks above it are freed at the end of every setup, largest first, so the
+// next setup of the process still finds the common sizes.  < 0: the default,
+// an eighth of the device's HBM (36 GB on an MI355X); 0: everything released
+// at the end of every setup (mamg_set_setup_cache_limit).
+namespace detail {
+inline int64_t& cache_limit() {
+  static int64_t v = -1;
+  return v;
+}
+}  // namespace detail
+inline void set_cache_limit(int64_t bytes) { detail::cache_limit() = bytes; }
+inline int64_t cache_limit_dev(int d) {
+  const int64_t v = detail::cache_limit();
+  if (v >= 0) return v;
+  hipDeviceProp_t pr;
+  if (hipGetDeviceProperties(&pr, d) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  return (int64_t)(pr.totalGlobalMem / 8);
+}
+
+// idle bytes cached on device d (tests, the bound)
+inline int64_t tmp_idle_bytes(int d) {
+  auto& c = detail::tmp_cache();
+  std::lock_guard<std::mutex> g(c.m);
+  int64_t b = 0;
+  for (auto& kv : c.idle[d & 63]) b += (int64_t)kv.first;
+  return b;
+}
+
+// the end of a setup: every device's idle cache down to the bound (the
+// staging block is counted against it too; above the bound it is freed first)
+inline void tmp_trim_to_limit_all() {
+  for (int d = 0; d < 64; ++d) {
+    auto& c = detail::tmp_cache();
+    int64_t idle_b = 0;
+    size_t stage_b = 0;
+    {
+      std::lock_guard<std::mutex> g(c.m);
+      for (auto& kv : c.idle[d]) idle_b += (int64_t)kv.first;
+    }
+    {
+      std::lock_guard<std::mutex> g(detail::stage_mu());
+      const detail::StagePool& sp = detail::stage_pools()[d];
+      if (sp.p && !sp.busy) stage_b = sp.bytes;
+    }
+    if (idle_b == 0 && stage_b == 0) continue;
+    const int64_t lim = cache_limit_dev(d);
+    if (idle_b + (int64_t)stage_b <= lim) continue;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) { (void)hipGetLastError(); continue; }
+    if (cur != d && hipSetDevice(d) != hipSuccess) { (void)hipGetLastError(); continue; }
+    (void)hipStreamSynchronize(nullptr);
+    if (lim == 0 || (int64_t)stage_b > lim) {
+      stage_free_dev(d);
+      stage_b = 0;
+    }
+    {
+      std::lock_guard<std::mutex> g(c.m);
+      auto& idle = c.idle[d];
+      int64_t tot = 0;
+      for (auto& kv : idle) tot += (int64_t)kv.first;
+      while (!idle.empty() && tot + (int64_t)stage_b > lim) {
+        auto it = std::prev(idle.end());   // the largest idle block
+        tot -= (int64_t)it->first;
+        (void)raw_free(it->second);
+        c.made.erase(it->second);
+        idle.erase(it);
+      }
+    }
+    if (cur != d) (void)hipSetDevice(cur);
+  }
+}
+
+// the staging block of the current device for one product: its size and
+// pointer (0 / nullptr when none fits or another product holds it); the
+// product releases it when done (StageLease)
+inline size_t stage_acquire(size_t cap_bytes, void** p) {
+  const int d = detail::cur_device();
+  std::lock_guard<std::mutex> g(detail::stage_mu());
+  detail::StagePool& sp = detail::stage_pools()[d];
+  *p = nullptr;
+  if (sp.busy) return 0;
+  if (!sp.p && cap_bytes > 0) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const size_t b = (size_t)std::min((double)cap_bytes, 0.25 * (double)fr) & ~(((size_t)2 << 20) - 1);
+      if (b >= ((size_t)64 << 20) && raw_malloc(&sp.p, b, "scratch") == hipSuccess) sp.bytes = b;
+      else sp.p = nullptr;
+    }
+    (void)hipGetLastError();
+  }
+  if (!sp.p) return 0;
+  sp.busy = true;
+  *p = sp.p;
+  return sp.bytes;
+}
+inline void stage_release(int d) {
+  std::lock_guard<std::mutex> g(detail::stage_mu());
+  detail::stage_pools()[d & 63].busy = false;
+}
+// the staging block held for one product (released when it goes out of scope)
+struct StageLease {
+  int dev = 0;
+  void* p = nullptr;
+  size_t bytes = 0;
+  explicit StageLease(size_t cap_bytes) : dev(detail::cur_device()) { bytes = stage_acquire(cap_bytes, &p); }
+  ~StageLease() {
+    if (p) stage_release(dev);
+  }
+  StageLease(const StageLease&) = delete;
+  StageLease& operator=(const StageLease&) = delete;
+};
 
 // hipMalloc for the library's long-lived arrays: when HBM runs out while the
 // setup temporaries' cache holds idle blocks, the cache is emptied and the

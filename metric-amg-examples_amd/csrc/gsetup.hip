@@ -48,6 +48,7 @@
 
 #include "dist.h"
 #include "dmem.h"
+#include "opts.h"
 #include "gsetup.h"
 #include "rowstage.h"
 
@@ -1885,47 +1886,24 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(int64_t n, const uint8_
 // list).  Same kernel code, same rank sort: the same bits.
 // MAMG_SPGEMM_PAIR=0: the staged count pass row by row (A/B, tests)
 bool spgemm_pair_on() {
-  const char* e = std::getenv("MAMG_SPGEMM_PAIR");
+  const char* e = opt("MAMG_SPGEMM_PAIR");
   return e ? std::atoi(e) != 0 : true;
 }
 
-// The staging area is one block per device, allocated at its first use at
-// the cap size (min(MAMG_SPGEMM_STAGE_GB, a quarter of the free HBM)) and
-// kept for the process, like the scans' scratch: a large block allocated
-// later, in a heap that earlier handles have fragmented, was written ~50x
-// slower (the reference family's R (A P) at nrefs=6: 4.9 s against 0.1 s in a
-// fresh process, profiles/r05_spgemm_stage_pool.txt), the scattered row
-// writes paying a translation miss per small page.  Used in null-stream
-// order, as the setup temporaries are.
-struct StagePool {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
-std::mutex g_stage_mu;
-StagePool g_stage[64];
-
-size_t stage_pool(int dev, void** p) {
-  std::lock_guard<std::mutex> g(g_stage_mu);
-  StagePool& sp = g_stage[dev & 63];
-  if (!sp.p) {
-    const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
-    const double cap_gb = e ? std::atof(e) : 16.0;
-    size_t fr = 0, tot = 0;
-    if (cap_gb > 0.0 && hipMemGetInfo(&fr, &tot) == hipSuccess) {
-      const size_t b = (size_t)std::min(cap_gb * 1e9, 0.25 * (double)fr) & ~(((size_t)2 << 20) - 1);
-      if (b >= ((size_t)64 << 20) && dev_malloc(&sp.p, b, "scratch") == hipSuccess) sp.bytes = b;
-      else sp.p = nullptr;
-    }
-    (void)hipGetLastError();
-  }
-  *p = sp.p;
-  return sp.bytes;
+// The staging area is the per-device staging block of dmem.h (StageLease),
+// at most min(MAMG_SPGEMM_STAGE_GB, a quarter of the free HBM), kept for the
+// process until the setup cache is released; used in null-stream order, as
+// the setup temporaries are, and held by one product at a time.
+size_t stage_cap_bytes() {
+  const char* e = opt("MAMG_SPGEMM_STAGE_GB");
+  const double cap_gb = e ? std::atof(e) : 16.0;
+  return cap_gb > 0.0 ? (size_t)(cap_gb * 1e9) : 0;
 }
 
 int64_t spgemm_stage_stride(int64_t n, size_t pool) {
-  const char* e = std::getenv("MAMG_SPGEMM_STAGE_GB");
+  const char* e = opt("MAMG_SPGEMM_STAGE_GB");
   if (e && std::atof(e) <= 0.0) return 0;
-  e = std::getenv("MAMG_SPGEMM_STAGE_STRIDE");
+  e = opt("MAMG_SPGEMM_STAGE_STRIDE");
   const int64_t smax = e ? std::atoll(e) : 128;
   if (n <= 0) return 0;
   for (int64_t s : {128, 64, 32, 16})
@@ -1953,11 +1931,9 @@ int spgemm_gl(GHier* G, const DevMat& A, BS B, int64_t ncols, DevMat* C, std::st
   RCHK(S.alloc(&ctr, 5, err));
   HIPCHK(dev_memset(ctr, 0, 5 * sizeof(int)));
   SpStage stg;
-  void* pool = nullptr;
-  int dev = 0;
-  HIPCHK(hipGetDevice(&dev));
-  const size_t pool_bytes = stage_pool(dev, &pool);
-  stg.stride = pool ? spgemm_stage_stride(n, pool_bytes) : 0;
+  StageLease lease(stage_cap_bytes());     // held until the product returns
+  void* pool = lease.p;
+  stg.stride = pool ? spgemm_stage_stride(n, lease.bytes) : 0;
   int32_t* l3 = nullptr;
   int n3 = 0;
   if (stg.stride) {   // values first (8-byte aligned), then the columns
@@ -2301,7 +2277,7 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
     RCHK(to_host(&Gr.nnz, Gr.ptr + nv, 1, err));
     RCHK(S.alloc(&Gr.col, Gr.nnz, err));
     RCHK(S.alloc(&Gr.val, Gr.nnz, err));
-    const char* fe = std::getenv("MAMG_CSR2BSR_FILL");   // 0: the column + value staged merge (tests, A/B)
+    const char* fe = opt("MAMG_CSR2BSR_FILL");   // 0: the column + value staged merge (tests, A/B)
     if (fe && std::atoi(fe) == 0) {
       node_graph_kernel<true><<<g, RS_NODES>>>(nv, A.ptr, A.col, A.val, Gr.ptr, Gr.col, Gr.val);
     } else {
@@ -2373,7 +2349,7 @@ int aggregate(GHier* G, const DevMat& A, int64_t nv, int level, double theta, bo
   RCHK(S.alloc(&m1, nv, err));
   RCHK(shards_alloc(&S, &und, err));
   mis_init_kernel<<<nblk(nv), 256>>>(nv, Gr.ptr, flag, level, state, low, nonisol);
-  const char* ms = std::getenv("MAMG_MIS_STAGED");   // 0: the lane-per-row walks (tests, A/B)
+  const char* ms = opt("MAMG_MIS_STAGED");   // 0: the lane-per-row walks (tests, A/B)
   const bool mis_staged = ms ? std::atoi(ms) != 0 : true;
   for (int rounds = 0;; ++rounds) {
     if (rounds > 10000) { *err = "mis2 did not converge"; return MAMG_ERR_SETUP; }
@@ -3305,7 +3281,7 @@ int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
   // pinned buffers on the calling thread, ~36 GB/s for one thread.  A/B at
   // nrefs=6 (MAMG_UPLOAD_THREADS, profiles/r05_upload_threads.txt): k = 1
   // 348-397 ms, 2 323 ms (default), 4 335 ms
-  const char* e = std::getenv("MAMG_UPLOAD_THREADS");
+  const char* e = opt("MAMG_UPLOAD_THREADS");
   const int k = e ? std::max(1, std::min(16, std::atoi(e))) : 2;
   if (k == 1) {
     HIPCHK(hipMemcpy(D->ptr, A.ptr, (A.n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -3325,6 +3301,10 @@ int upload_a0(const CsrView& A, GHier* G, DevMat* D, std::string* err) {
       cut(D->col, A.col, D->nnz * sizeof(int32_t));
       cut(D->val, A.val, D->nnz * sizeof(double));
     }
+    // the three arrays may be cached blocks whose earlier users (a handle
+    // just closed, a previous setup) are still queued on the null stream;
+    // the upload streams are non-blocking, so they wait for it here
+    HIPCHK(hipStreamSynchronize(nullptr));
     std::vector<std::thread> th;
     std::atomic<int> bad{0};
     const int dev = G->device;

@@ -27,6 +27,28 @@ def lib_built():
     return so
 
 
+def set_opt(name, value):
+    """One of the library's internal layout switches for this process
+    (mamg_set_option, include/mamg_test.h); reset after every test by
+    _reset_options.  The product library reads no environment variables."""
+    import metric_amg_examples_amd as M
+    M._lib.set_option(name, value)
+    _SET.add(name)
+
+
+_SET = set()
+
+
+@pytest.fixture(autouse=True)
+def _reset_options():
+    yield
+    if _SET:
+        import metric_amg_examples_amd as M
+        for name in list(_SET):
+            M._lib.set_option(name, None)
+        _SET.clear()
+
+
 DIAG_LIB = os.path.join(ROOT, 'metric-amg-examples_amd', 'libmamg_diag.so')
 
 

@@ -12,7 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_symbols():
-    txt = open(os.path.join(ROOT, 'include', 'mamg.h')).read()
+    txt = ''.join(open(os.path.join(ROOT, 'include', f)).read() for f in sorted(os.listdir(os.path.join(ROOT, 'include')))
+                  if f.endswith('.h'))
     txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
     return sorted(set(re.findall(r'\b(mamg_[a-z_0-9]+)\s*\(', txt)))
 
@@ -268,3 +269,66 @@ def test_release_setup_cache_without_gpu(lib_built):
     no device call, so it returns 0 on a host without a GPU too."""
     import metric_amg_examples_amd as M
     M.release_setup_cache()
+
+
+PRODUCT_OPTIONS = ('MAMG_POST_K', 'MAMG_SELL_MIN_ROWS', 'MAMG_MSELL_MIN_ROWS', 'MAMG_TAIL_NODES', 'MAMG_TAIL_VL',
+                   'MAMG_TAIL_LDS', 'MAMG_HALF', 'MAMG_HALF_BANDS', 'MAMG_R_BANDS', 'MAMG_K_SORT', 'MAMG_FUSE_RBD',
+                   'MAMG_CSR2BSR_FILL', 'MAMG_KREGION_TRIES', 'MAMG_KREGION_BUDGET_MS', 'MAMG_REHOME',
+                   'MAMG_PRERESERVE_B_PER_NNZ', 'MAMG_POISON', 'MAMG_OVERLAP', 'MAMG_DIST_TEST', 'MAMG_SPGEMM_PAIR',
+                   'MAMG_SPGEMM_STAGE_GB', 'MAMG_SPGEMM_STAGE_STRIDE', 'MAMG_MIS_STAGED', 'MAMG_UPLOAD_THREADS')
+
+
+def _diag_regions(src):
+    """line numbers inside #if MAMG_DIAG ... (#else | #endif) blocks"""
+    inside, stack, out = False, [], set()
+    for i, line in enumerate(src.split('\n'), 1):
+        t = line.strip()
+        if t.startswith('#if'):
+            stack.append(t.startswith('#if MAMG_DIAG'))
+        elif t.startswith('#else') and stack:
+            stack[-1] = False if stack[-1] else stack[-1]
+        elif t.startswith('#endif') and stack:
+            stack.pop()
+        inside = any(stack)
+        if inside:
+            out.add(i)
+    return out
+
+
+def test_product_reads_no_environment(lib_built):
+    """the product library's switches are set only
+    through mamg_set_option (include/mamg_test.h), a fixed list; every getenv
+    in the library's sources sits in a diagnosis-build block (#if MAMG_DIAG)."""
+    import metric_amg_examples_amd as M
+    assert M._lib.option_names() == list(PRODUCT_OPTIONS)
+    with pytest.raises(M._lib.MamgError) as ei:
+        M._lib.set_option('MAMG_TMP_KEEP', '1')        # gone: the cache limit replaces it
+    assert ei.value.code == -1 and 'MAMG_HALF' in str(ei.value)
+    M._lib.set_option('MAMG_HALF', '0')
+    M._lib.set_option('MAMG_HALF', None)
+    csrc = os.path.join(ROOT, 'metric-amg-examples_amd', 'csrc')
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith(('.hip', '.cpp', '.h')):
+            continue
+        src = open(os.path.join(csrc, f)).read()
+        diag = _diag_regions(src)
+        for i, line in enumerate(src.split('\n'), 1):
+            code = line.split('//')[0]
+            if 'getenv(' in code:
+                assert i in diag, '%s:%d reads the environment outside #if MAMG_DIAG: %s' % (f, i, line.strip())
+    prod = open(lib_built, 'rb').read()
+    assert b'MAMG_TMP_KEEP' not in prod and b'MAMG_GRAPH_MAX_OPS' not in prod
+
+
+def test_setup_cache_limit_api(lib_built):
+    """mamg_set_setup_cache_limit / mamg_setup_cache_bytes (include/mamg.h):
+    the bound of the idle setup cache, default (< 0) an eighth of the device's
+    HBM (the GPU test checks the value and that a setup leaves at most that)."""
+    import metric_amg_examples_amd as M
+    L = M._lib.lib()
+    idle, lim = C.c_int64(-1), C.c_int64(-1)
+    M._lib.check(L.mamg_set_setup_cache_limit(5 * 10**9))
+    M._lib.check(L.mamg_setup_cache_bytes(0, C.byref(idle), C.byref(lim)))
+    assert lim.value == 5 * 10**9 and idle.value == 0
+    M._lib.check(L.mamg_set_setup_cache_limit(-1))
+    assert L.mamg_setup_cache_bytes(64, None, None) == -1

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import mamg_oracle as mo
+from conftest import set_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -203,12 +204,12 @@ def test_post_operator_k_equals_merged(lib_built, monkeypatch, sell):
     and the merged [P | AP] window (z = x1 + P e + W (r1 - AP e)) are the
     same cycle up to summation order."""
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1' if sell == '1' else str(1 << 20))
+    set_opt('MAMG_SELL_MIN_ROWS', '1' if sell == '1' else str(1 << 20))
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
     zs, fmts = [], []
     for k in ('1', '0'):
-        monkeypatch.setenv('MAMG_POST_K', k)
+        set_opt('MAMG_POST_K', k)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
         fmts.append(B.level_format(0))
         zs.append(B * mo.seeded_rhs(s.N))
@@ -228,13 +229,13 @@ def test_half_symmetric_a0_bitwise(lib_built, monkeypatch, dim, n, g, kw):
     through their mirrors) sums every row in the full row's block order: the
     apply and the device PCG are bitwise those of full SELL-64 storage."""
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
     r = mo.seeded_rhs(s.N)
     outs, its = [], []
     for half in ('1', '0'):
-        monkeypatch.setenv('MAMG_HALF', half)
+        set_opt('MAMG_HALF', half)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
         f = B.level_format(0)
         assert f['sell'] != (half == '1') and f['half'] == (half == '1') and f['sym']
@@ -265,7 +266,7 @@ def test_restriction_band_schedule_bitwise(lib_built, monkeypatch, bands):
     r = mo.seeded_rhs(s.N)
     outs, its = [], []
     for b in (bands, '0'):
-        monkeypatch.setenv('MAMG_R_BANDS', b)
+        set_opt('MAMG_R_BANDS', b)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
         assert B.level_format(0)['r_bands'] == (b != '0')
         outs.append(B * r)
@@ -288,7 +289,7 @@ def test_half_band_schedule_bitwise(lib_built, monkeypatch, bands):
     r = mo.seeded_rhs(s.N)
     outs, its = [], []
     for b in (bands, '0'):
-        monkeypatch.setenv('MAMG_HALF_BANDS', b)
+        set_opt('MAMG_HALF_BANDS', b)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
         f = B.level_format(0)
         assert f['half'] and f['bands'] == (b != '0')
@@ -313,7 +314,7 @@ def test_restriction_first_sweep_fused_bitwise(lib_built, monkeypatch, kw):
     r = mo.seeded_rhs(s.N)
     outs, its = [], []
     for f in ('2', '1', '0'):   # default (below level 0), every level, none
-        monkeypatch.setenv('MAMG_FUSE_RBD', f)
+        set_opt('MAMG_FUSE_RBD', f)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
         outs.append(B * r)
         solver = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
@@ -332,7 +333,7 @@ def test_half_symmetric_rejects_nonsymmetric(lib_built, monkeypatch):
     mirror check rejects the half format (full SELL-64 is used) and the apply
     still matches the oracle."""
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(3, 8, 1e2)
     A = s.scipy().tocsr().copy()
     row = int(np.argmax(np.diff(A.indptr)[:s.nv]))      # an interior field-0 row
@@ -356,7 +357,7 @@ def test_sell_layout_matches_oracle(lib_built, monkeypatch, dim, n, g, kw):
     """SELL-64 storage (one lane per node row; used for the level-0 operators
     at benchmark size) forced onto every short-row level of small problems:
     all epilogues, field-major x (maxit > 1, PCG), the fused post kernel."""
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
@@ -504,13 +505,13 @@ def test_k_block_layouts_bitwise(lib_built, monkeypatch):
     apply and the device PCG are bitwise equal."""
     import torch
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
     r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
     zs, its = [], []
     for mode in ('3', '2'):
-        monkeypatch.setenv('MAMG_POST_K', mode)
+        set_opt('MAMG_POST_K', mode)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
         assert B.level_format(0)['post_sell']
         zs.append(B.matvec(r))
@@ -541,7 +542,7 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
     give the bits of the un-moved ones."""
     import torch
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
     r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
@@ -557,7 +558,7 @@ def test_k_kernel_variants(lib_built, monkeypatch, variant):
     B.time_apply(r, zz, 1, 0)
     torch.cuda.synchronize()
     assert torch.equal(zz, z)
-    monkeypatch.setenv('MAMG_REHOME', '0')
+    set_opt('MAMG_REHOME', '0')
     B0 = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
     z0 = B0.matvec(r)
     torch.cuda.synchronize()
@@ -580,14 +581,14 @@ def test_k_row_sort_bitwise(lib_built, monkeypatch, variant):
     apply and the eager launches, and equals the oracle."""
     import torch
     M = _mamg()
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     monkeypatch.setenv('MAMG_K_VARIANT', variant)
     s = M.problems.bidomain(3, 16, 1e6)
     A = s.scipy()
     r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
     zs = []
     for srt in ('0', '1'):
-        monkeypatch.setenv('MAMG_K_SORT', srt)
+        set_opt('MAMG_K_SORT', srt)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
         assert B.level_format(0)['post_sell']
         z = B.matvec(r)
@@ -614,7 +615,7 @@ def test_coarse_multilane_sell(lib_built, monkeypatch, dim, n, g, kw):
     r = mo.seeded_rhs(s.N)
     zs = []
     for rows in ('1', str(1 << 30)):
-        monkeypatch.setenv('MAMG_MSELL_MIN_ROWS', rows)
+        set_opt('MAMG_MSELL_MIN_ROWS', rows)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
         assert B.level_format(1)['sell'] == (rows == '1')
         zs.append(B * r)

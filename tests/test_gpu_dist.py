@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 import mamg_oracle as mo
+from conftest import set_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -182,13 +183,13 @@ def test_rank_slice_download_bitwise(lib_built, monkeypatch, case, P, rep):
     if case == 'unfused':
         kw['post_fusion'] = 0
     elif case == 'sell':
-        monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')     # SELL / half-symmetric rank-local A with ghosts
+        set_opt('MAMG_SELL_MIN_ROWS', '1')     # SELL / half-symmetric rank-local A with ghosts
     elif case == 'merged':
-        monkeypatch.setenv('MAMG_POST_K', '0')
+        set_opt('MAMG_POST_K', '0')
     r = mo.seeded_rhs(s.N)
     out, nbytes = [], []
     for full in ('full', 'rows', ''):   # whole download + host plan, rank rows + host plan, built in HBM
-        monkeypatch.setenv('MAMG_DIST_TEST', full)
+        set_opt('MAMG_DIST_TEST', full)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=rep,
                               num_functions=2, **kw) for p in range(P)]
         rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
@@ -216,10 +217,10 @@ def test_virtual_ranks_storage_variants(lib_built, monkeypatch, mode):
     import metric_amg_examples_amd as M
     kw = {}
     if mode in ('sell', 'nohalf'):
-        monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
-        monkeypatch.setenv('MAMG_HALF', '1' if mode == 'sell' else '0')
+        set_opt('MAMG_SELL_MIN_ROWS', '1')
+        set_opt('MAMG_HALF', '1' if mode == 'sell' else '0')
     elif mode == 'merged':
-        monkeypatch.setenv('MAMG_POST_K', '0')
+        set_opt('MAMG_POST_K', '0')
     else:
         kw['post_fusion'] = 0
     s = M.problems.bidomain(3, 16, 1e6)
@@ -300,7 +301,7 @@ def test_virtual_ranks_graph_bitwise(lib_built, monkeypatch, P, kw):
     all-reduces), POLY at P = 8."""
     import torch
     import metric_amg_examples_amd as M
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(3, 16, 1e6)
     r = mo.seeded_rhs(s.N)
     hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
@@ -369,12 +370,12 @@ def test_virtual_ranks_half_bitwise(lib_built, monkeypatch, P):
     column order: bitwise the SELL-64 result, with fewer bytes per apply."""
     import torch
     import metric_amg_examples_amd as M
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', '1')
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
     s = M.problems.bidomain(3, 16, 1e6)
     r = mo.seeded_rhs(s.N)
     out, nbytes = [], []
     for half in ('1', '0'):
-        monkeypatch.setenv('MAMG_HALF', half)
+        set_opt('MAMG_HALF', half)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
                               num_functions=2) for p in range(P)]
         rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
@@ -432,13 +433,13 @@ def test_virtual_ranks_overlap_bitwise(lib_built, monkeypatch, n, P, sell):
     apply, for the cycle and the rank SpMV."""
     import torch
     import metric_amg_examples_amd as M
-    monkeypatch.setenv('MAMG_SELL_MIN_ROWS', sell)
+    set_opt('MAMG_SELL_MIN_ROWS', sell)
     s = M.problems.bidomain(3, n, 1e6)
     r = mo.seeded_rhs(s.N)
     out = []
     forks = []
     for ov in ('1', '0'):
-        monkeypatch.setenv('MAMG_OVERLAP', ov)
+        set_opt('MAMG_OVERLAP', ov)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None, rep_nodes=100,
                               num_functions=2) for p in range(P)]
         rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
@@ -471,7 +472,7 @@ def test_virtual_ranks_band_schedule_bitwise(lib_built, monkeypatch):
     P = 2
     out = []
     for bands in ('1', '0'):
-        monkeypatch.setenv('MAMG_HALF_BANDS', bands)
+        set_opt('MAMG_HALF_BANDS', bands)
         hs = [M.DistMetricAMG(s, s.W, idofs=s.idofs, rank=p, nranks=P, comm_id=None,
                               num_functions=2) for p in range(P)]
         rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]

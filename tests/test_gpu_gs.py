@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import mamg_oracle as mo
+from conftest import set_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -138,7 +139,7 @@ def test_coarse_tail_equals_launches(lib_built, monkeypatch, dim, n, g, kw):
     r = mo.seeded_rhs(s.N)
     zs = []
     for nodes in ('100000000', '0'):
-        monkeypatch.setenv('MAMG_TAIL_NODES', nodes)
+        set_opt('MAMG_TAIL_NODES', nodes)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
         zs.append(B * r)
         B.close()

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import mamg_oracle as mo
+from conftest import set_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -85,9 +86,9 @@ def test_gpu_spgemm_staging_bitwise(lib_built, monkeypatch, dim, n, g, kw, stage
     give the host setup's hierarchy bit for bit."""
     M = _mamg()
     gb, stride, pair = stage
-    monkeypatch.setenv('MAMG_SPGEMM_STAGE_GB', gb)
-    monkeypatch.setenv('MAMG_SPGEMM_STAGE_STRIDE', stride)
-    monkeypatch.setenv('MAMG_SPGEMM_PAIR', pair)
+    set_opt('MAMG_SPGEMM_STAGE_GB', gb)
+    set_opt('MAMG_SPGEMM_STAGE_STRIDE', stride)
+    set_opt('MAMG_SPGEMM_PAIR', pair)
     s = M.problems.bidomain(dim, n, g)
     Hh = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, **kw)
     Hg = M.HostHierarchy(s, idofs=s.idofs, num_functions=2, gpu=True, **kw)
@@ -111,7 +112,7 @@ def test_csr2bsr_fill_variants_bitwise(lib_built, monkeypatch, dim, n, g, kw, kn
     A = s.scipy()
     outs, fmts = [], []
     for f in ('1', '0'):
-        monkeypatch.setenv(knob, f)
+        set_opt(knob, f)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **kw)
         fmts.append([B.level_format(lv) for lv in range(B.num_levels)])
         outs.append([B * mo.seeded_rhs(s.N, seed) for seed in (1234, 7)])
@@ -311,3 +312,65 @@ def test_setups_with_kept_cache_then_released_bitwise(lib_built):
         outs.append(B * mo.seeded_rhs(s.N, 1234))
         B.close()
     assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+
+
+def test_setup_cache_limit_bounds_idle_blocks(lib_built):
+    """mamg_set_setup_cache_limit: the default bound is
+    an eighth of the device's HBM and a setup leaves at most that much idle
+    (the SpGEMM staging block included); limit 0 leaves nothing; the applies
+    are the same bits either way."""
+    import ctypes as C
+    import torch
+    M = _mamg()
+    L = M._lib.lib()
+    s = M.problems.bidomain(3, 16, 1e6)
+    A = s.scipy()
+    idle, lim = C.c_int64(), C.c_int64()
+    outs = []
+    try:
+        for limit in (-1, 0, 1 << 20):
+            M._lib.check(L.mamg_set_setup_cache_limit(limit))
+            B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+            M._lib.check(L.mamg_setup_cache_bytes(torch.cuda.current_device(), C.byref(idle), C.byref(lim)))
+            if limit < 0:
+                assert lim.value == torch.cuda.get_device_properties(0).total_memory // 8
+            else:
+                assert lim.value == limit
+            assert 0 <= idle.value <= lim.value, (limit, idle.value, lim.value)
+            outs.append(B * mo.seeded_rhs(s.N, 1234))
+            B.close()
+    finally:
+        L.mamg_set_setup_cache_limit(-1)
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+
+
+def test_concurrent_setups_share_the_staging_block_safely(lib_built):
+    """two host threads setting up on one device at once -- the
+    SpGEMM staging block is held by one product at a time (the other runs the
+    unstaged two-pass product, the same bits), so both hierarchies equal a
+    lone setup's bit for bit."""
+    import threading
+    M = _mamg()
+    s = M.problems.bidomain(3, 24, 1e6)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N, 1234)
+    B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+    ref = B * r
+    B.close()
+    outs, errs = [None] * 4, []
+
+    def run(k):
+        try:
+            h = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+            outs[k] = h * r
+            h.close()
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for o in outs:
+        assert np.array_equal(o, ref)
