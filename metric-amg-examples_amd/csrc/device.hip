@@ -2327,6 +2327,11 @@ int dalloc(HT* h, T** p, int64_t count, std::string* err) {
     return MAMG_OK;
   }
   void* q = nullptr;
+  // a very large long-lived array (the node patches' inverses: 63 GB at
+  // nrefs=6) is placed after the idle setup cache is released, so it is not
+  // laid out around the cached blocks (with them kept, the patch layout build
+  // took 2.2-2.8 s instead of 0.68 s, BENCH_r05 / profiles/r05_bench_g.json)
+  if ((size_t)count * sizeof(T) >= ((size_t)8 << 30)) tmp_trim();
   HIPCHK(dev_malloc(&q, (size_t)count * sizeof(T)));
   h->allocs.push_back(q);
   *p = (T*)q;
@@ -4541,6 +4546,13 @@ bool launch_kvariant(const Op& o, hipStream_t s) {
   }
 }
 
+// whether the level-0 K launch honours an op's row range [r0, r1) (the
+// multi-lane SELL and lane-group kernels do; launch_sell_u, reached only with
+// the diagnosis build's MAMG_K_VARIANT=1 on a K not split in two streams,
+// does not): the distributed apply splits K around the coarse halo only then
+// 
+bool k_ranges_ok(const DBsr& K) { return !K.sell || !(g_kvar == 1 && K.split != 2); }
+
 template <bool XFM, bool SYM, int TAG>
 void launch_sell_x(const Op& o, hipStream_t s) {
   // level-0 K operator: two lanes per row (launch_kvariant); multi-lane SELL
@@ -6156,7 +6168,8 @@ void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double*
   // K on its ghost-free rows while the coarse-e halo is in flight (level 0,
   // no coarse scaling); the schedule's shape is the same on every rank (the
   // overlap and both remainder launches are emitted, maybe empty)
-  const bool kov = l == 0 && h->overlap && D.K.nr > 0 && !C.replicated && !h->p.coarse_scaling && npost >= 1;
+  const bool kov = l == 0 && h->overlap && D.K.nr > 0 && !C.replicated && !h->p.coarse_scaling && npost >= 1 &&
+                   k_ranges_ok(D.K);
   dcoarse_ops(h, l, ops, kov);
   int s0 = 0;
   if (D.K.nr > 0 || D.PA.nr > 0) {   // fused first post step (K built with its smoother), operands local

@@ -129,13 +129,16 @@ def get_hazmath_amg_precond(A, W=None, bcs=None, parameters=None, interface_dofs
     makes the hierarchy nodal (num_functions = the number of equal blocks:
     nodal aggregation and node-block SGS, the only SGS this build has);
     ``num_functions=1`` gives point-wise aggregation with a point smoother
-    (SGS then needs a Jacobi-family ``smoother``).  The choice is recorded in
-    ``.substitutions`` instead of a warning on every call."""
+    (SGS then needs a Jacobi-family ``smoother``: this build's SGS is the
+    node-block multicolour one, so a point-wise default would substitute the
+    smoother instead).  The choice is recorded in ``.substitutions`` instead
+    of the num_functions warning on every call; every other warning of the
+    construction still reaches the caller."""
     import warnings
     params = dict(P.parameters_amg_default) if parameters is None else dict(parameters)
     params['Schwarz_levels'] = 0
     with warnings.catch_warnings():
-        warnings.simplefilter('ignore', UserWarning)
+        warnings.filterwarnings('ignore', message=r'num_functions -> ', category=UserWarning)
         B = MetricAMG(to_monolithic(A), W, idofs=None, parameters=params, **kw)
     B.substitutions = [n for n in getattr(B, 'notes', [])] + (
         ['nodal hierarchy from W (the reference AMGhaz gets no W: point-wise aggregation there)']
