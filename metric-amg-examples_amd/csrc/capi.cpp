@@ -135,7 +135,16 @@ namespace {
 // 2 of 2 runs, scripts/runs/gpu_r05z9.sh).  Above the
 // limit the largest idle blocks are freed at the end of every setup;
 // mamg_release_setup_cache() releases all of them.
+// It also holds the capture lock for a single-GPU setup (device.hip
+// capture_mutex): those setups run one at a time and never overlap another
+// thread's stream capture.  A multi-GPU rank's setup does not take it: it
+// waits in ncclCommInitRank for its peers, which may be threads of the same
+// process (one process per GPU is the intended use).
 struct TmpTrim {
+  std::unique_lock<std::recursive_mutex> lock;
+  explicit TmpTrim(bool serialize = true) {
+    if (serialize) lock = std::unique_lock<std::recursive_mutex>(mamg::capture_mutex());
+  }
   ~TmpTrim() { mamg::dev_tmp_trim_to_limit(); }
 };
 
@@ -442,7 +451,7 @@ namespace {
 int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int32_t* idofs, int64_t n_idofs,
                     const mamg_params* params, int rank, int nranks, const void* comm_id, int64_t rep_nodes,
                     mamg_dhandle** out) {
-  TmpTrim trim;
+  TmpTrim trim(false);
   int rc;
   const int64_t nnz0 = devA ? devA->nnz : v.nnz();
   const mamg_params P = mamg::resolve_params(*params, idofs, n_idofs, v.n);   // the reference's Schwarz names
@@ -500,10 +509,12 @@ int setup_dist_impl(const mamg::CsrView& v, const mamg::DevMat* devA, const int3
     } else if (mode == 1 || G.generic) {   // generic smoothers: the host plan of the whole hierarchy
       rc = mamg::ghier_download(G, v, &H, &err);
     } else {
-      // node patches on N GPUs read and write within 3 hops of a rank's nodes
+      // node patches on N GPUs read and write within 3 hops of a rank's
+      // nodes, seed rings within 2 Schwarz_maxlvl + 1
       const bool patches = P.Schwarz_levels >= 1 && P.Schwarz_type == MAMG_SCHWARZ_PATCHES;
+      const bool rings = P.Schwarz_levels >= 1 && P.Schwarz_type == MAMG_SCHWARZ_RINGS;
       rc = mamg::ghier_download_rank(G, dA, v, rank, nranks, rep_nodes, P.post_fusion != 0, &H,
-                                     &ghosts, &err, mode == 2, patches ? 3 : 1);
+                                     &ghosts, &err, mode == 2, patches ? 3 : rings ? 2 * P.Schwarz_maxlvl + 1 : 1);
       pre = !rc;
       on_device = !rc && mode != 2;
     }

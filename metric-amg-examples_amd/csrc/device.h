@@ -1,5 +1,6 @@
 // device.h -- device hierarchy interface (no HIP types; implemented in device.hip)
 #pragma once
+#include <mutex>
 #include <string>
 
 #include "gsetup.h"
@@ -24,6 +25,8 @@ void dev_layout_ms(const DeviceHandle* h, double* ms4);
 void dev_destroy(DeviceHandle* h);
 // release the cached blocks of the setup temporaries (dmem.h tmp_trim_all)
 void dev_tmp_trim();
+// held across the library's stream captures and its setups (device.hip)
+std::recursive_mutex& capture_mutex();
 // the end of a setup: idle cached blocks above the cache limit freed
 void dev_tmp_trim_to_limit();
 // cache limit (bytes per device; < 0 default = HBM / 8, 0 = release every setup)

@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <map>
 #include <numeric>
 #include <vector>
@@ -60,6 +61,18 @@ namespace mamg {
 // node (4x the measured frame) + 16 MiB, reserved, touched only as deep as the
 // walk goes.
 constexpr size_t GRAPH_INSTANTIATE_INLINE = 16384;
+
+// Held across every stream capture of the library and every setup (capi.cpp
+// TmpTrim): the HIP runtime invalidates a capture when another host thread
+// issues legacy null-stream work meanwhile (the setups' synchronous copies),
+// and refuses that work ("would make the legacy stream depend on a capturing
+// blocking stream"), thread-local capture mode notwithstanding (two threads
+// setting up and applying at once, tests/test_gpu_setup.py).  Setups of one
+// process therefore run one at a time.
+std::recursive_mutex& capture_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
 hipError_t graph_instantiate(hipGraphExec_t* ex, hipGraph_t g) {
   size_t nodes = 0;
   hipError_t e = hipGraphGetNodes(g, nullptr, &nodes);
@@ -4780,6 +4793,7 @@ int get_graph(DeviceHandle* h, const double* r, double* z, hipGraphExec_t* exec,
   apply_ops(h, r, z, &ops);
   Graph g;
   g.r = r; g.z = z;
+  std::lock_guard<std::recursive_mutex> capture_lock(capture_mutex());
   HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
   for (const Op& o : ops) launch(o, h->cap);
   HIPCHK(hipStreamEndCapture(h->cap, &g.graph));
@@ -5526,6 +5540,7 @@ int dev_pcg(DeviceHandle* h, const double* d_b, double* d_x, double tol, int max
     double *dres = q.hist, *dal = q.hist + maxiter + 1, *dbe = dal + maxiter;
     std::vector<Op> ops;
     apply_ops(h, h->cr, h->cz, &ops);
+    std::lock_guard<std::recursive_mutex> capture_lock(capture_mutex());
     hipError_t e = hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal);
     if (e == hipSuccess) {
       launch(a0_op(h, EPI_Y, h->cd, nullptr, h->cq), h->cap);           // q = A d
@@ -5791,6 +5806,14 @@ struct DDLevel {
   DLevel pl;
   int32_t* Sgcol = nullptr;
   double* pb = nullptr;
+  // level-0 seed-ring Schwarz on N ranks (dist_rings): the rank's blocks
+  // (rl: rcs, rmo, rmem, rio, rinv; the block rows Sptr / Scol / Sval over
+  // the local nodes), the ring colours' halos at cs_off / cg_off indices
+  // [0, nrc), the rest GS's colours at [nrc, nrc + gcs.size() - 1)
+  bool rings = false;
+  int nrc = 0;
+  DLevel rl;
+  uint8_t* rcov = nullptr;   // covered dofs of the owned nodes (bit f)
 };
 
 // D_CHALO: the forward halo of one colour's nodes (after that colour's GS step)
@@ -6123,11 +6146,74 @@ void dcycle_patch(const DistHandle* h, const double* b, int64_t bs, double* xout
   ops->push_back(wrap(o));
 }
 
+// one symmetric level-0 seed-ring step on N ranks (the single-GPU sweep of
+// cycle_ops_bsr, mamg_oracle.rings_step): forward = ring colours ascending,
+// then the rest's GS colours ascending; backward = the rest descending, then
+// the rings descending; each colour's step followed by its halo (every rank
+// emits every exchange, also for colours it has no work in)
+void dring_sweep(const DistHandle* h, bool fwd, double* x, std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[0];
+  const int nrc = D.nrc, ngc = (int)D.gcs.size() - 1, P = h->nranks;
+  auto rings = [&](bool f) {
+    for (int k = 0; k < nrc; ++k) {
+      const int c = f ? k : nrc - 1 - k;
+      ops->push_back(wrap(ring_op(D.rl, c, x, D.pb, 0, C_L0_SMOOTH)));   // empty: not launched
+      ops->push_back(chalo_op(0, c, x, D, P));
+    }
+  };
+  auto rest = [&](bool f) {
+    for (int k = 0; k < ngc; ++k) {
+      const int c = f ? k : ngc - 1 - k;
+      ops->push_back(wrap(gs_op(D, c, x, D.pb, 0, C_L0_SMOOTH)));
+      ops->push_back(chalo_op(0, nrc + c, x, D, P));
+    }
+  };
+  if (fwd) { rings(true); rest(true); } else { rest(false); rings(false); }
+}
+
+// multi-GPU level-0 cycle with the seed-ring Schwarz (cycle_ops_bsr's ring
+// branch): b interleaved over [owned | ghost] + its halo; x = 0; pre steps
+// forward then backward; residual; the coarse correction; x += P e and its
+// halo; post steps forward then backward
+void dcycle_rings(const DistHandle* h, const double* b, int64_t bs, double* xout, int64_t os,
+                  std::vector<DOp>* ops) {
+  const DDLevel& D = h->L[0];
+  const DDLevel& C = h->L[1];
+  double* X = D.t;
+  {
+    Op o;
+    o.kind = OP_ILV; o.cls = C_L0_WB; o.n = D.nloc; o.b = b; o.bs = bs; o.out = D.pb;
+    o.bytes = 32.0 * D.nloc;
+    ops->push_back(wrap(o));
+    ops->push_back(halo_op(0, D.pb, D, C_COMM));
+    Op z;
+    z.kind = OP_ZERO; z.cls = C_L0_WB; z.n = 2 * (D.nloc + D.ng); z.out = X; z.bytes = 8.0 * z.n;
+    ops->push_back(wrap(z));
+  }
+  for (int s = 0; s < h->p.presmooth_iter; ++s) {
+    dring_sweep(h, true, X, ops);
+    dring_sweep(h, false, X, ops);
+  }
+  ops->push_back(wrap(bsr_op(D.A, EPI_RESID, C_L0_RESID, 0, X, 0, nullptr, b, bs, nullptr, D.r, 0)));
+  dcoarse_ops(h, 0, ops);
+  ops->push_back(wrap(bsr_op(D.P, EPI_YADD, C_L0_P, 0, C.x, 0, X, nullptr, 0, nullptr, X, 0)));
+  ops->push_back(halo_op(0, X, D, C_COMM));
+  for (int s = 0; s < h->p.postsmooth_iter; ++s) {
+    dring_sweep(h, true, X, ops);
+    dring_sweep(h, false, X, ops);
+  }
+  Op o;
+  o.kind = OP_ILV; o.epi = 1; o.cls = C_L0_WB; o.n = D.nloc; o.b = X; o.out = xout; o.os = os;
+  o.bytes = 32.0 * D.nloc;
+  ops->push_back(wrap(o));
+}
+
 // multi-GPU cycle from x = 0 (V or W, nu1 / nu2 sweeps, optional coarse-grid
 // scaling): see dist.cpp / dist_ref.py
 void dcycle_ops(const DistHandle* h, int l, const double* b, int64_t bs, double* xout, int64_t os,
                 std::vector<DOp>* ops) {
   if (l == 0 && h->L[0].patches) { dcycle_patch(h, b, bs, xout, os, ops); return; }
+  if (l == 0 && h->L[0].rings) { dcycle_rings(h, b, bs, xout, os, ops); return; }
   if (!h->L[l].coarsest && h->L[l].gcs.size() > 1) { dcycle_gs(h, l, b, bs, xout, os, ops); return; }
   const DDLevel& D = h->L[l];
   const bool l0 = l == 0;
@@ -6601,15 +6687,16 @@ __global__ __launch_bounds__(256) void hop_step_kernel(int64_t nv, const int64_t
 __device__ __forceinline__ int64_t local_gid(int64_t li, int64_t nloc, int64_t o0, const int64_t* gh) {
   return li < nloc ? o0 + li : gh[li - nloc];
 }
-// the rank's patch rows: local row li = B's row of its global node when that
-// node is within 2 hops of the owned range, else empty (len[li + 1])
+// the rank's patch / ring-block rows: local row li = B's row of its global
+// node when that node is within hmax hops of the owned range, else empty
+// (len[li + 1])
 __global__ __launch_bounds__(256) void srow_len_kernel(int64_t nl, int64_t nloc, int64_t o0, const int64_t* __restrict__ gh,
                                                        const int8_t* __restrict__ hop, const int64_t* __restrict__ bptr,
-                                                       int64_t* __restrict__ len) {
+                                                       int64_t* __restrict__ len, int hmax) {
   const int64_t li = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (li >= nl) return;
   const int64_t g = local_gid(li, nloc, o0, gh);
-  len[li + 1] = hop[g] <= 2 ? bptr[g + 1] - bptr[g] : 0;
+  len[li + 1] = hop[g] <= hmax ? bptr[g + 1] - bptr[g] : 0;
 }
 // ... its blocks in B's (global) column order: local columns (map) and the
 // global ids (the inverse kernel's search keys)
@@ -6702,7 +6789,7 @@ int dist_patches(DistHandle* h, const DevMat& A0d, const DistLevel& P, DDLevel* 
   // the patch rows
   DLevel& L = D->pl;
   if ((rc = ddalloc(h, &L.Sptr, nl + 1, err))) return rc;
-  if (nl) srow_len_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, hop, B.ptr, L.Sptr);
+  if (nl) srow_len_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, hop, B.ptr, L.Sptr, 2);
   HIPCHK(hipGetLastError());
   if ((rc = dscan_incl_i64(L.Sptr, L.Sptr, nl + 1, nullptr, err))) return rc;
   HIPCHK(hipMemcpy(&L.Snb, L.Sptr + nl, sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -6807,6 +6894,191 @@ int dist_patches(DistHandle* h, const DevMat& A0d, const DistLevel& P, DDLevel* 
     std::fprintf(stderr, "[mamg] rank %d/%d node patches: %d colours, %lld centres (%lld owned), %lld ghost nodes "
                  "(3 hops), colour halos %lld sends / %lld receives in all\n", h->rank, R, ncol, (long long)np,
                  (long long)nloc, (long long)ng, (long long)cs.size(), (long long)cg.size());
+  return MAMG_OK;
+}
+
+// Level-0 seed-ring Schwarz of a rank (SCHWARZ_RINGS on N GPUs, DESIGN.md
+// 6.4): every rank builds the global blocks, inverses and
+// conflict colouring (ring_blocks_dev + ring_colouring, the single-GPU
+// build_rings' steps, so every rank holds the same blocks and colours) and
+// keeps the blocks with a member node it owns -- the owner of every written
+// node computes every block that writes it, from the same x, so its bits agree
+// with one GPU's.  A block's members lie within 2 maxlvl hops of an owned node
+// and its rows read x within 2 maxlvl + 1 hops: the ghost region.  The rest's
+// multicolour GS runs on the owned rows with the covered dofs masked
+// (dev_rank_ops, from *cov_owned).  One colour table serves both: ring colour
+// c at index c (the nodes its blocks write), GS colour g at nrc + g (the nodes
+// of that colour), each with the halo of those nodes in the send / ghost
+// lists, so the exchange code is the multicolour GS's.
+int dist_rings(DistHandle* h, const DevMat& A0d, const DistLevel& P, const std::vector<int32_t>& seeds,
+               const int8_t* gcol, int ngc, DDLevel* D, uint8_t** cov_owned, std::string* err) {
+  int rc;
+  TmpPool T;
+  const mamg_params& p = h->p;
+  const int64_t nv = P.nv, nloc = P.nloc, ng = (int64_t)P.ghosts.size(), nl = nloc + ng, n = A0d.n;
+  const int R = h->nranks, L = p.Schwarz_maxlvl;
+  const int64_t ns = (int64_t)seeds.size();
+  if (ns <= 0) { *err = "seed rings: no seeds"; return MAMG_ERR_ARG; }
+  // the global blocks and their conflict colouring (build_rings)
+  RingBlocks RB;
+  if ((rc = ring_blocks_dev(A0d, seeds.data(), ns, L, p.Schwarz_mmsize, &RB, err))) return rc;
+  struct Guard { RingBlocks* r; ~Guard() { ring_blocks_free(r); } } guard{&RB};
+  const int mm = RB.mm;
+  std::vector<int32_t> blk((size_t)ns * mm);
+  std::vector<int64_t> blen(ns);
+  HIPCHK(hipMemcpy(blk.data(), RB.blk, blk.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(blen.data(), RB.blen, ns * sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<int64_t> bptr(ns + 1, 0);
+  for (int64_t k = 0; k < ns; ++k) bptr[k + 1] = bptr[k] + blen[k];
+  std::vector<int32_t> mem(bptr[ns]);
+  for (int64_t k = 0; k < ns; ++k) std::copy(blk.begin() + k * mm, blk.begin() + k * mm + blen[k], mem.begin() + bptr[k]);
+  std::vector<int32_t>().swap(blk);
+  std::vector<int32_t> colour;
+  {
+    std::vector<int64_t> aptr(n + 1);
+    std::vector<int32_t> acol(A0d.nnz);
+    HIPCHK(hipMemcpy(aptr.data(), A0d.ptr, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(acol.data(), A0d.col, A0d.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    CsrView Av;
+    Av.n = Av.m = n; Av.ptr = aptr.data(); Av.col = acol.data();
+    ring_colouring(Av, bptr, mem, &colour);
+  }
+  int nrc = 0;
+  for (int32_t c : colour) nrc = std::max(nrc, c + 1);
+  std::vector<int32_t> ord(ns);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return colour[a] < colour[b]; });
+  // local node ids (owned first, then ghosts), covered dofs, the colours
+  // writing each node (one bit per ring colour)
+  std::vector<int32_t> loc(nv, -1);
+  for (int64_t i = 0; i < nloc; ++i) loc[P.o0 + i] = (int32_t)i;
+  for (int64_t g = 0; g < ng; ++g) loc[P.ghosts[g]] = (int32_t)(nloc + g);
+  const int CW = (nrc + 63) / 64;
+  std::vector<uint64_t> wr((size_t)nv * std::max(CW, 1), 0);
+  std::vector<uint8_t> cov(nv, 0);
+  for (int64_t k = 0; k < ns; ++k)
+    for (int64_t t = bptr[k]; t < bptr[k + 1]; ++t) {
+      const int64_t gd = mem[t], I = gd % nv, f = gd / nv;
+      cov[I] |= (uint8_t)(1u << f);
+      wr[(size_t)I * CW + colour[k] / 64] |= 1ull << (colour[k] % 64);
+    }
+  // the rank's blocks: a member node owned, colour by colour (seed order inside)
+  DLevel& RL = D->rl;
+  RL.rcs.assign(nrc + 1, 0);
+  std::vector<int32_t> mine;
+  std::vector<int64_t> mo(1, 0), io(1, 0);
+  std::vector<int32_t> rm;
+  for (int64_t j = 0; j < ns; ++j) {
+    const int32_t k = ord[j];
+    bool own = false;
+    for (int64_t t = bptr[k]; t < bptr[k + 1] && !own; ++t) {
+      const int64_t I = mem[t] % nv;
+      own = I >= P.o0 && I < P.o1;
+    }
+    if (!own) continue;
+    for (int64_t t = bptr[k]; t < bptr[k + 1]; ++t) {
+      const int64_t gd = mem[t], I = gd % nv, f = gd / nv;
+      if (loc[I] < 0) {
+        *err = "multi-GPU seed rings: a block member outside the rank's " + std::to_string(2 * L + 1) +
+               "-hop ghost region";
+        return MAMG_ERR_SETUP;
+      }
+      rm.push_back(2 * loc[I] + (int32_t)f);
+    }
+    mine.push_back(k);
+    mo.push_back(mo.back() + blen[k]);
+    io.push_back(io.back() + blen[k] * blen[k]);
+    ++RL.rcs[colour[k] + 1];
+  }
+  for (int c = 0; c < nrc; ++c) RL.rcs[c + 1] += RL.rcs[c];
+  const int64_t nb = (int64_t)mine.size();
+  RL.n = 2 * nl;
+  RL.rnm = mo.back();
+  RL.rinv_n = (double)io.back();
+  if ((rc = ddalloc(h, &RL.rmo, nb + 1, err)) || (rc = ddalloc(h, &RL.rio, nb + 1, err)) ||
+      (rc = ddalloc(h, &RL.rmem, std::max<int64_t>(RL.rnm, 1), err)) ||
+      (rc = ddalloc(h, &RL.rinv, std::max<int64_t>(io.back(), 1), err)))
+    return rc;
+  HIPCHK(hipMemcpy(RL.rmo, mo.data(), (nb + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(RL.rio, io.data(), (nb + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (RL.rnm) HIPCHK(hipMemcpy(RL.rmem, rm.data(), rm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (nb) {
+    int32_t* dmine = nullptr;
+    if ((rc = T.alloc(&dmine, nb, err))) return rc;
+    HIPCHK(hipMemcpy(dmine, mine.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice));
+    ring_perm_inv_kernel<<<(unsigned)nb, 256>>>(nb, dmine, RB.blen, RB.sq, RB.inv, RL.rio, RL.rinv);
+    HIPCHK(hipGetLastError());
+  }
+  // the block rows: A_0's node rows of the local nodes within 2 L hops,
+  // local columns (the ring kernel reads x through them)
+  TBsr B;
+  if ((rc = dev_csr_to_bsr(&T, A0d, nv, nv, &B, err))) return rc;
+  int8_t *hop = nullptr, *hop2 = nullptr;
+  if ((rc = T.alloc(&hop, nv, err)) || (rc = T.alloc(&hop2, nv, err))) return rc;
+  hop_init_kernel<<<nblocks(nv), 256>>>(nv, P.o0, P.o1, hop);
+  for (int k = 1; k <= 2 * L; ++k) {
+    hop_step_kernel<<<nblocks(nv), 256>>>(nv, B.ptr, B.col, hop, hop2, k);
+    std::swap(hop, hop2);
+  }
+  HIPCHK(hipGetLastError());
+  int64_t* gh = nullptr;
+  if ((rc = T.alloc(&gh, std::max<int64_t>(ng, 1), err))) return rc;
+  if (ng) HIPCHK(hipMemcpy(gh, P.ghosts.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice));
+  int32_t* map = nullptr;
+  if ((rc = dev_col_map(&T, P, &map, err))) return rc;
+  if ((rc = ddalloc(h, &RL.Sptr, nl + 1, err))) return rc;
+  if (nl) srow_len_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, hop, B.ptr, RL.Sptr, 2 * L);
+  HIPCHK(hipGetLastError());
+  if ((rc = dscan_incl_i64(RL.Sptr, RL.Sptr, nl + 1, nullptr, err))) return rc;
+  HIPCHK(hipMemcpy(&RL.Snb, RL.Sptr + nl, sizeof(int64_t), hipMemcpyDeviceToHost));
+  int32_t* sg = nullptr;
+  if ((rc = ddalloc(h, &RL.Scol, std::max<int64_t>(RL.Snb, 1), err)) ||
+      (rc = T.alloc(&sg, std::max<int64_t>(RL.Snb, 1), err)) ||
+      (rc = ddalloc(h, &RL.Sval, std::max<int64_t>(RL.Snb, 1), err)))
+    return rc;
+  if (nl) srow_fill_kernel<<<nblocks(nl), 256>>>(nl, nloc, P.o0, gh, B.ptr, B.col, B.val, map, RL.Sptr, RL.Scol, sg,
+                                                 RL.Sval);
+  HIPCHK(hipGetLastError());
+  // the covered dofs of the owned nodes (the rest's GS masks them)
+  if ((rc = ddalloc(h, cov_owned, std::max<int64_t>(nloc, 1), err))) return rc;
+  if (nloc) HIPCHK(hipMemcpy(*cov_owned, cov.data() + P.o0, nloc, hipMemcpyHostToDevice));
+  // the colour table: ring colours, then the rest GS's node colours
+  std::vector<int8_t> hc(nv);
+  if (nv) HIPCHK(hipMemcpy(hc.data(), gcol, nv, hipMemcpyDeviceToHost));
+  auto in = [&](int64_t I, int idx) {
+    return idx < nrc ? ((wr[(size_t)I * CW + idx / 64] >> (idx % 64)) & 1ull) != 0 : hc[I] == idx - nrc;
+  };
+  const int nct = nrc + ngc;
+  std::vector<int64_t> cs, cg;
+  D->cs_off.assign((size_t)nct * (R + 1), 0);
+  D->cg_off.assign((size_t)nct * (R + 1), 0);
+  for (int idx = 0; idx < nct; ++idx) {
+    for (int q = 0; q < R; ++q) {
+      D->cs_off[(size_t)idx * (R + 1) + q] = (int64_t)cs.size();
+      D->cg_off[(size_t)idx * (R + 1) + q] = (int64_t)cg.size();
+      for (int64_t t = P.send_off[q]; t < P.send_off[q + 1]; ++t)
+        if (in(P.o0 + P.send_idx[t], idx)) cs.push_back(P.send_idx[t]);
+      for (int64_t g = P.ghost_off[q]; g < P.ghost_off[q + 1]; ++g)
+        if (in(P.ghosts[g], idx)) cg.push_back(g);
+    }
+    D->cs_off[(size_t)idx * (R + 1) + R] = (int64_t)cs.size();
+    D->cg_off[(size_t)idx * (R + 1) + R] = (int64_t)cg.size();
+  }
+  if (!cs.empty()) {
+    if ((rc = ddalloc(h, &D->csend_idx, (int64_t)cs.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->csend_idx, cs.data(), cs.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (!cg.empty()) {
+    if ((rc = ddalloc(h, &D->cghost_idx, (int64_t)cg.size(), err))) return rc;
+    HIPCHK(hipMemcpy(D->cghost_idx, cg.data(), cg.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  D->rings = true;
+  D->nrc = nrc;
+  if (p.print_level >= 2)
+    std::fprintf(stderr, "[mamg] rank %d/%d seed rings: %lld of %lld blocks, %d ring colours + %d GS colours, "
+                 "%lld ghost nodes (%d hops), colour halos %lld sends / %lld receives in all\n", h->rank, R,
+                 (long long)nb, (long long)ns, nrc, ngc, (long long)ng, 2 * L + 1, (long long)cs.size(),
+                 (long long)cg.size());
   return MAMG_OK;
 }
 
@@ -6916,9 +7188,23 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
     }
     if (!half && (rc = finalize_bsr(h, &T, tA, &D.A, 0, true, err))) return rc;
     if (l == 0 && (rc = build_band_sched_range(h, &D.A, D.ib0, D.ib1, err))) return rc;
-    if (gcol && (rc = gs_layout(h, &T, tA, reinterpret_cast<const double*>(D.W), gcol + P.o0, ncol, l, &D.Gb,
-                                &D.gperm, &D.Gd, &D.gcs, &D.gbk, err)))
-      return rc;
+    if (gcol) {
+      // seed rings: the rest's GS, covered dofs masked (build_rings' rest_w /
+      // rest_mask on the owned rows)
+      const double* Wg = reinterpret_cast<const double*>(D.W);
+      if (D.rcov && nloc) {
+        dv4* Wp = nullptr;
+        if ((rc = T.alloc(&Wp, nloc, err))) return rc;
+        rest_w_kernel<<<nblocks(nloc), 256>>>(nloc, D.W, D.rcov, Wp);
+        HIPCHK(hipGetLastError());
+        Wg = reinterpret_cast<const double*>(Wp);
+      }
+      if ((rc = gs_layout(h, &T, tA, Wg, gcol + P.o0, ncol, l, &D.Gb, &D.gperm, &D.Gd, &D.gcs, &D.gbk, err)))
+        return rc;
+      const int64_t nrp = D.gcs.empty() ? 0 : D.gcs.back();
+      if (D.rcov && nrp) rest_mask_kernel<<<nblocks(nrp), 256>>>(nrp, D.gperm, D.rcov, D.Gd);
+      HIPCHK(hipGetLastError());
+    }
   }
   // prolongation side (level l+1 numbering)
   const DistLevel& C = plan.levels[l + 1];
@@ -6995,11 +7281,6 @@ int dist_check(const mamg_params& p, std::string* err) {
     *err = "multi-GPU apply supports maxit 1 (one cycle per application, src/amg_parameters.py:71)";
     return MAMG_ERR_UNSUPPORTED;
   }
-  if (rings_schwarz(p)) {
-    *err = "multi-GPU apply: seed-ring Schwarz (SCHWARZ_RINGS) is single-GPU (the node patches, SCHWARZ_PATCHES, "
-           "run on N GPUs)";
-    return MAMG_ERR_UNSUPPORTED;
-  }
   return MAMG_OK;
 }
 
@@ -7009,9 +7290,11 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   if (int rc = dist_check(p, err)) return rc;
   const bool gs = gs_smoother(p);
   const bool patches = patch_schwarz(p);
-  if (patches && !(G && A0d && ghosts)) {
-    *err = "multi-GPU node patches need the rank operators and the 3-hop ghost lists built from the GPU hierarchy "
-           "(mamg_setup_dist with a GPU-setup profile)";
+  const bool rings = rings_schwarz(p);
+  if ((patches || rings) && !(G && A0d && ghosts)) {
+    *err = std::string("multi-GPU ") + (patches ? "node patches need the rank operators and the 3-hop" :
+           "seed rings need the rank operators and the (2 Schwarz_maxlvl + 1)-hop") +
+           " ghost lists built from the GPU hierarchy (mamg_setup_dist with a GPU-setup profile)";
     return MAMG_ERR_UNSUPPORTED;
   }
   if (gs && !G) {
@@ -7025,7 +7308,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
   DistPlan plan;
   const auto tp0 = std::chrono::steady_clock::now();
   const double kw = p.smoother == MAMG_SMOOTHER_POLY ? pw[pm - 1] : 1.0;
-  bool fuse = p.post_fusion != 0 && !gs && !patches;   // GS / patches post-smooth after x += P e (as on one GPU)
+  bool fuse = p.post_fusion != 0 && !gs && !patches && !rings;   // GS / patches / rings post-smooth after x += P e (as on one GPU)
   if (G)                   // operators from the GPU hierarchy: fusion needs its A P on every level
     for (size_t l = 0; l + 1 < G->levels.size() && fuse; ++l)
       if (!G->levels[l].coarsest && G->levels[l].AP.n != G->levels[l].n) fuse = false;
@@ -7083,12 +7366,17 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
       TmpPool TC;
       int8_t* gcol = nullptr;
       int ncol = 0;
-      if (gs && !(l == 0 && patches)) {
+      const bool rl0 = l == 0 && rings && !G->seeds.empty();   // level-0 seed rings + the rest's GS
+      if ((gs || rl0) && !(l == 0 && patches)) {
         TBsr B;
         if ((rc = dev_csr_to_bsr(&TC, l == 0 ? *A0d : G->levels[l].A, D.nv, D.nv, &B, err))) return rc;
         if ((rc = gs_colour(&TC, B, l, &gcol, &ncol, err))) return rc;
         TC.release(B.ptr); TC.release(B.col); TC.release(B.val);
-        if (!D.replicated && (rc = colour_halo_lists(h.get(), P, gcol, ncol, &D, err))) return rc;
+        if (rl0) {
+          if ((rc = dist_rings(h.get(), *A0d, P, G->seeds, gcol, ncol, &D, &D.rcov, err))) return rc;
+        } else if (!D.replicated && (rc = colour_halo_lists(h.get(), P, gcol, ncol, &D, err))) {
+          return rc;
+        }
       }
       if ((rc = dev_rank_ops(h.get(), *G, *A0d, plan, l, kw, gcol, ncol, err))) return rc;
       if (l == 0 && patches && !D.coarsest && (rc = dist_patches(h.get(), *A0d, P, &D, err))) return rc;
@@ -7154,7 +7442,7 @@ int dist_upload(const Hierarchy& H, const CsrView& A0, const mamg_params& p, int
     if ((rc = ddalloc(h.get(), &D.t2, 2 * full, err))) return rc;
     if ((rc = ddalloc(h.get(), &D.r, 2 * full, err))) return rc;
     if (l == 0 && !D.coarsest && (rc = ddalloc(h.get(), &D.spx, 2 * full, err))) return rc;
-    if (D.patches && (rc = ddalloc(h.get(), &D.pb, 2 * full, err))) return rc;
+    if ((D.patches || D.rings) && (rc = ddalloc(h.get(), &D.pb, 2 * full, err))) return rc;
     if (l > 0 && p.cycle_type == MAMG_W_CYCLE) {
       if ((rc = ddalloc(h.get(), &D.c, 2 * full, err))) return rc;
       if ((rc = ddalloc(h.get(), &D.e, 2 * full, err))) return rc;
@@ -7286,6 +7574,7 @@ int dist_spmv(DistHandle* h, const double* d_x, double* d_y, void* stream, std::
 int dist_capture(DistHandle* h, const std::vector<DOp>& ops, hipGraph_t* gr, hipGraphExec_t* ex, std::string* err) {
   *gr = nullptr;
   *ex = nullptr;
+  std::lock_guard<std::recursive_mutex> capture_lock(capture_mutex());
   if (!h->cap) HIPCHK(hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking));
   HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
   int rc = MAMG_OK;
@@ -7589,6 +7878,7 @@ int dist_virtual_apply_graph(const std::vector<DistHandle*>& hs, const std::vect
   std::vector<std::vector<DOp>> ops(P);
   for (int p = 0; p < P; ++p) dapply_ops(hs[p], r[p], z[p], &ops[p]);
   DistHandle* h0 = hs[0];
+  std::lock_guard<std::recursive_mutex> capture_lock(capture_mutex());
   if (!h0->cap) HIPCHK(hipStreamCreateWithFlags(&h0->cap, hipStreamNonBlocking));
   HIPCHK(hipStreamBeginCapture(h0->cap, hipStreamCaptureModeThreadLocal));
   int rc = virtual_run(hs, ops, h0->cap, err, false);

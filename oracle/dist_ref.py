@@ -354,3 +354,80 @@ class PartitionedPatchSweep:
             for f in (0, 1):
                 out[f * nv + self.own[p]:f * nv + self.own[p + 1]] = xs[p][f * nv + self.own[p]:f * nv + self.own[p + 1]]
         return out
+
+
+# --------------------------------------------------------------------------
+# Seed-ring Schwarz on P ranks (device.hip dist_rings /
+# dcycle_rings): rank p owns the nodes [own[p], own[p+1]); its local copy of x
+# covers the owned nodes and every node within 2 maxlvl + 1 hops; it computes
+# every block with a member node it owns (all members lie within 2 maxlvl
+# hops of that node, their rows read within 2 maxlvl + 1) from its local x,
+# writes the block's dofs locally, and after each colour receives from the
+# owners the nodes that colour's blocks wrote inside its region.  The owner of
+# a written node computes every block that writes it from the same values,
+# so the sweep is mamg_oracle.Rings.sweep exactly.
+# --------------------------------------------------------------------------
+class PartitionedRingSweep:
+    """P ranks of a seed-ring sweep on one process (numpy), with the halo
+    lists of the product (region = 2 maxlvl + 1 hops, per colour the nodes
+    its blocks write)."""
+
+    def __init__(self, A, rings, own, maxlvl):
+        import scipy.sparse as sp
+        from mamg_oracle import node_pattern
+        self.A = A.tocsr()
+        self.rg = rings
+        self.own = list(own)
+        n = self.A.shape[0]
+        nv = n // 2
+        self.nv = nv
+        G = node_pattern(self.A, 2)
+        Gd = (G + sp.identity(nv, dtype=np.int8, format='csr')).tocsr()
+        Gd.data[:] = 1
+        self.P = len(own) - 1
+        self.owner = np.zeros(nv, np.int64)
+        self.region, self.blocks = [], []
+        bnodes = [np.unique(np.asarray(b) % nv) for b in rings.blocks]
+        for p in range(self.P):
+            mine = np.zeros(nv, bool)
+            mine[own[p]:own[p + 1]] = True
+            self.owner[own[p]:own[p + 1]] = p
+            self.region.append(_hops(Gd, mine, 2 * maxlvl + 1))
+            self.blocks.append([k for k, bn in enumerate(bnodes) if np.any(mine[bn])])
+
+    def sweep(self, x, b, forward=True):
+        """the partitioned sweep from the global x (copied to every rank);
+        returns the gathered owned values"""
+        nv, rg = self.nv, self.rg
+        xs = [x.copy() for _ in range(self.P)]
+        cols = range(rg.ncolours) if forward else range(rg.ncolours - 1, -1, -1)
+        for c in cols:
+            written = set()
+            for p in range(self.P):
+                ks = [k for k in self.blocks[p] if rg.colour[k] == c]
+                if not ks:
+                    continue
+                xp = xs[p]
+                rows = np.concatenate([rg.blocks[k] for k in ks])
+                assert np.all(self.region[p][self.A[rows].indices % nv]), 'a block reads outside the region'
+                res = b[rows] - self.A[rows] @ xp
+                off = 0
+                for k in ks:
+                    m = len(rg.blocks[k])
+                    xp[rg.blocks[k]] += rg.Minv[k] @ res[off:off + m]
+                    off += m
+                written |= set((rows % nv).tolist())
+            upd = np.array(sorted(written), np.int64)
+            for p in range(self.P):
+                if not len(upd):
+                    break
+                for J in upd[self.region[p][upd]]:
+                    q = self.owner[J]
+                    if q != p:
+                        for f in (0, 1):
+                            xs[p][f * nv + J] = xs[q][f * nv + J]
+        out = np.empty_like(x)
+        for p in range(self.P):
+            for f in (0, 1):
+                out[f * nv + self.own[p]:f * nv + self.own[p + 1]] = xs[p][f * nv + self.own[p]:f * nv + self.own[p + 1]]
+        return out

@@ -197,9 +197,9 @@ def _dist_rc(M, s, prm):
 def test_setup_dist_parameter_checks_before_gpu(lib_built):
     """mamg_setup_dist (include/mamg.h, multi-GPU section) takes V and W cycles:
     a W-cycle profile passes every parameter check and reaches the device
-    (no device here: MAMG_ERR_HIP), as does the node-patch Schwarz, while an
-    invalid cycle, maxit > 1 and the seed-ring Schwarz (single-GPU) are
-    refused before the rank touches its GPU."""
+    (no device here: MAMG_ERR_HIP), as do the node-patch and the seed-ring
+    Schwarz, while an invalid cycle and maxit > 1 are refused before the
+    rank touches its GPU."""
     import torch
     import metric_amg_examples_amd as M
     if torch.cuda.is_available():
@@ -216,10 +216,10 @@ def test_setup_dist_parameter_checks_before_gpu(lib_built):
     # the node patches run on N GPUs (round 5): they pass to the device
     rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_schwarz_gpu_mapped))
     assert rc == -2 and 'hip' in msg.lower(), msg
-    # the seed rings stay single-GPU: refused before the device
+    # the seed rings run on N GPUs too (round 6): they pass to the device
     rc, msg = _dist_rc(M, s, P.make_params(P.parameters_metric_mi355x_patch, Schwarz_type=P.SCHWARZ_RINGS,
                                            Schwarz_maxlvl=2))
-    assert rc == -4 and 'single-GPU' in msg, msg
+    assert rc == -2 and 'hip' in msg.lower(), msg
 
 
 def test_num_functions_inference_is_reported_and_overridable(lib_built):

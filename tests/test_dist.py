@@ -312,3 +312,29 @@ def test_partitioned_patch_sweep_equals_sequential(P):
         xs = pt.sweep(A, x0.copy(), b, fwd)
         xp = ps.sweep(x0.copy(), b, fwd)
         assert np.array_equal(xs, xp)
+
+
+@pytest.mark.parametrize('P', [2, 3, 5])
+def test_partitioned_ring_sweep_equals_sequential(P):
+    """The seed-ring design on N ranks ((2 maxlvl + 1)-hop
+    ghost regions, every block with an owned member computed redundantly, a
+    halo of the written nodes after each colour) restated on the CPU: forward
+    and backward sweeps on P contiguous node ranges equal the oracle's colour
+    sweep (mamg_oracle.Rings.sweep) bit for bit, for the EMI interface seeds'
+    2-rings of the reference's default dict (src/utils.py:60-82)."""
+    import metric_amg_examples_amd as M
+    import mamg_oracle as mo
+    from dist_ref import PartitionedRingSweep
+    s = M.problems.emi(3, 8, 1e6)
+    A = s.scipy()
+    rg = mo.Rings(A, s.idofs, 2, 100)
+    nv = A.shape[0] // 2
+    own = [round(k * nv / P) for k in range(P + 1)]
+    b = mo.seeded_rhs(A.shape[0])
+    x0 = mo.seeded_rhs(A.shape[0], 7)
+    ps = PartitionedRingSweep(A, rg, own, 2)
+    assert sum(len(k) for k in ps.blocks) > len(rg.blocks)      # blocks spanning ranks: computed twice
+    for fwd in (True, False):
+        xs = rg.sweep(A, x0.copy(), b, fwd)
+        xp = ps.sweep(x0.copy(), b, fwd)
+        assert np.array_equal(xs, xp)

@@ -140,6 +140,54 @@ def test_emi_3d_nrefs5_block_form(lib_built):
     H.close()
 
 
+def test_emi_3d_nrefs5_reference_default_rings_8_virtual_ranks(lib_built):
+    """BASELINE config 4 with the EMI drivers' own call on 8 ranks (VERDICT
+    r05 #7): get_hazmath_metric_precond_mono(A, W, interface_dofs) without
+    parameters = the default dict's seed rings, row-partitioned over 8 virtual
+    ranks (5-hop ghost regions, a halo per ring colour and per rest-GS
+    colour).  The gathered apply = the one-GPU apply to 1e-12 and the oracle's
+    to 1e-10; the distributed PCG (tolerance 1e-10, src/emi_3d.py:143) takes
+    the one-GPU iteration count."""
+    import torch
+    import mamg_oracle as mo
+    M = _M()
+    n = M.problems.finest_n(3, 5, 'emi')
+    s = M.problems.emi(3, n, 1e6)
+    assert s.N == 278850
+    A = s.tocsr()
+    B = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs, setup='gpu')
+    assert B.level_format(0)['rings']
+    r = M.problems.seeded_rhs(s.N)
+    z = B * r
+    P = 8
+    hs = [M.DistMetricAMG(A, s.W, idofs=s.idofs, parameters=M.parameters.parameters_metric_default, rank=p,
+                          nranks=P, comm_id=None, rep_nodes=4096) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    torch.cuda.synchronize()
+    zd = np.zeros(s.N)
+    for hh, zl in zip(hs, zs):
+        zl = zl.cpu().numpy()
+        zd[hh.o0:hh.o1] = zl[:hh.nloc]
+        zd[s.nv + hh.o0:s.nv + hh.o1] = zl[hh.nloc:]
+    h = mo.setup(A, mo.Params(AMG_type='UA', cycle_type='W', smoother='SGS', relaxation=1.2, coarse_scaling=1,
+                              aggregation_type='HEM', strong_coupled=0.1, Schwarz_levels=1, Schwarz_mmsize=100,
+                              Schwarz_maxlvl=2, Schwarz_type=3, num_functions=2), idofs=s.idofs)
+    e1, eo = rel(zd, z), rel(zd, h.apply(r))
+    cg1 = M.ConjGrad(A, precond=B, tolerance=1e-10, maxiter=500)
+    cg1 * r
+    dcg = M.DistConjGrad.for_handles(hs, tolerance=1e-10, maxiter=500)
+    dcg.solve([x.clone() for x in rs])
+    say('EMI 3-D nrefs=5, default dict (seed rings), 8 virtual ranks: vs one GPU %.2e, vs oracle %.2e, '
+        'PCG %d (one GPU %d)' % (e1, eo, len(dcg.residuals) - 1, len(cg1.residuals) - 1))
+    assert e1 < 1e-12 and eo < 1e-10
+    assert len(dcg.residuals) == len(cg1.residuals)
+    for hh in hs:
+        hh.close()
+    B.close()
+
+
 def test_emi_3d_nrefs5_node_aligned_8_virtual_ranks(lib_built):
     """BASELINE config 4 (emi_3d nrefs=5 gamma=1e6 row-partitioned over 8
     GPUs): the interface seeds with node-aligned blocks (Schwarz_maxlvl 0),

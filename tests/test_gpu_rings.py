@@ -137,16 +137,69 @@ def test_emi_block_form_reference_call(lib_built):
     assert np.allclose(solver.residuals, ref.residuals, rtol=1e-6, atol=0)
 
 
+def _gather(s, hs, zs):
+    nv = s.N // 2
+    z = np.zeros(s.N)
+    for h, zz in zip(hs, zs):
+        zz = zz.cpu().numpy()
+        k = h.o1 - h.o0
+        z[h.o0:h.o1] = zz[:k]
+        z[nv + h.o0:nv + h.o1] = zz[k:]
+    return z
+
+
+@pytest.mark.parametrize('dim,n,g,P', [(3, 16, 1e6, 2), (3, 16, 1e6, 3), (3, 16, 1e6, 8), (3, 16, 1.0, 3),
+                                       (2, 64, 1e6, 4)])
+def test_virtual_ranks_seed_rings(lib_built, dim, n, g, P):
+    """the EMI drivers' own call (get_hazmath_metric_precond
+    without parameters, src/emi_3d.py:139 -> the default dict of
+    src/utils.py:60-82: SCHWARZ_SYMMETRIC on the interface seeds' 2-rings =
+    SCHWARZ_RINGS) row-partitioned over P virtual ranks: every rank builds the
+    global blocks and colours, computes the blocks with a member it owns, and
+    after each colour (ring or rest-GS) exchanges the nodes it wrote within
+    the 5-hop ghost region.  The gathered apply = the one-GPU apply to 1e-12
+    and the oracle's to 1e-10; the lockstep graph replay = the eager run
+    bitwise; the distributed PCG takes the one-GPU count."""
+    import torch
+    M = _M()
+    prm = M.parameters.parameters_metric_default
+    s = M.problems.emi(dim, n, g)
+    A = s.scipy()
+    r = mo.seeded_rhs(s.N)
+    B1 = M.precond.get_hazmath_metric_precond_mono(A, s.W, interface_dofs=s.idofs)
+    assert B1.level_format(0)['rings']
+    z1 = B1 * r
+    hs = [M.DistMetricAMG(A, s.W, idofs=s.idofs, parameters=prm, rank=p, nranks=P, comm_id=None,
+                          rep_nodes=100) for p in range(P)]
+    rs = [torch.as_tensor(hh.local_slice(r)).cuda() for hh in hs]
+    zs = [torch.zeros_like(x) for x in rs]
+    zg = [torch.full_like(x, float('nan')) for x in rs]
+    M.DistMetricAMG.virtual_apply(hs, rs, zs)
+    M.DistMetricAMG.virtual_apply(hs, rs, zg, graph=True)
+    torch.cuda.synchronize()
+    z = _gather(s, hs, zs)
+    assert rel(z, z1) < 1e-12, rel(z, z1)
+    for a, b in zip(zs, zg):
+        assert torch.equal(a, b)
+    h = mo.setup(A, mo.Params(**REF_DEFAULT), idofs=s.idofs)
+    assert rel(z, h.apply(r)) < 1e-10
+    cg1 = M.ConjGrad(A, precond=B1, tolerance=1e-10, maxiter=500)
+    cg1 * r
+    dcg = M.DistConjGrad.for_handles(hs, tolerance=1e-10, maxiter=500)
+    dcg.solve([x.clone() for x in rs])
+    assert len(dcg.residuals) == len(cg1.residuals)
+    assert np.allclose(dcg.residuals, cg1.residuals, rtol=1e-8, atol=0)
+    for hh in hs:
+        hh.close()
+    B1.close()
+
+
 def test_rings_refused_where_not_built(lib_built):
-    """Seed rings are single-GPU and nodal: the multi-GPU setup refuses them
-    with a message; scalar systems refuse the multiplicative overlapping form."""
+    """Scalar systems refuse the multiplicative overlapping form (the seed
+    rings need the nodal BSR2 layout, on one GPU and on N)."""
     M = _M()
     s = M.problems.emi(3, 8, 1e4)
     A = s.scipy()
-    with pytest.raises(M._lib.MamgError) as ei:
-        M.DistMetricAMG(A, s.W, idofs=s.idofs, parameters=M.parameters.parameters_metric_default,
-                        rank=0, nranks=1)
-    assert ei.value.code == -4 and 'SCHWARZ_RINGS' in str(ei.value)
     with pytest.raises(M._lib.MamgError) as ei:
         M.MetricAMG(A, None, idofs=s.idofs, parameters=dict(M.parameters.parameters_metric_default,
                                                              smoother=M.parameters.SMOOTHER_JACOBI_RHO))

@@ -345,10 +345,12 @@ def test_setup_cache_limit_bounds_idle_blocks(lib_built):
 
 
 def test_concurrent_setups_share_the_staging_block_safely(lib_built):
-    """two host threads setting up on one device at once -- the
-    SpGEMM staging block is held by one product at a time (the other runs the
-    unstaged two-pass product, the same bits), so both hierarchies equal a
-    lone setup's bit for bit."""
+    """host threads setting up and applying on one device at
+    once.  Single-GPU setups take the library's capture lock (the HIP runtime
+    invalidates a stream capture when another thread issues legacy
+    null-stream work, so setups never overlap a capture and run one at a
+    time); the SpGEMM staging block is leased per product; every thread's
+    apply equals a lone setup's bit for bit."""
     import threading
     M = _mamg()
     s = M.problems.bidomain(3, 24, 1e6)
