@@ -84,7 +84,7 @@ enum {                                                   /* Schwarz_type      */
   /* symmetric multiplicative Schwarz on the seeds' overlapping 1-ring blocks
      (the reference's SCHWARZ_SYMMETRIC with Schwarz_maxlvl 1): one patch per
      node = both fields of its closed neighbourhood, exact local solves, in a
-     distance-3 multicolour order; level 0, BSR2 layout, single GPU; needs a
+     distance-3 multicolour order; level 0, BSR2 layout, 1 or N GPUs; needs a
      seed dof on every node (the bidomain's idofs) */
   MAMG_SCHWARZ_PATCHES = 6,
   /* the level smoother applied to NON-overlapping seed blocks (a seed plus
@@ -102,7 +102,7 @@ enum {                                                   /* Schwarz_type      */
      Schwarz and the rest the GS smoother"): the reference's SCHWARZ_SYMMETRIC
      for any seed set that is not one seed per node with 1-rings (EMI's
      interface seeds, the default dict of src/utils.py:60-82); level 0, BSR2
-     layout (num_functions 2), single GPU */
+     layout (num_functions 2), 1 or N GPUs */
   MAMG_SCHWARZ_RINGS = 8
 };
 enum { MAMG_OFF = 0, MAMG_ON = 1 };
