@@ -1728,6 +1728,109 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
   }
 }
 
+// Patch inverses, two patches per wave (round 6): the same
+// operations on the same values as patch_inv_kernel, so the same bits, with
+// half the instructions per patch.
+//  * In place: half-wave h (lanes 32 h .. 32 h + 31) holds one patch, lane j
+//    < d column j of A_p (d = 2 m <= 32).  At pivot k, column k of the
+//    augmented [A_p | I] becomes e_k and identity column k is e_k until then
+//    (exactly: every update of it adds -(f x +0) = +0), so lane k takes
+//    over identity column k: row k = 1 / p, row r = 0 - f_r (1 / p), the
+//    augmented code's own operations on it.  The other lanes update as
+//    before (row k divided by the pivot, then M_r -= f_r M_k, no
+//    contraction); f_r = column k's row r, broadcast within the half by
+//    ds_bpermute (one instruction serves both patches) before lane k
+//    overwrites it.
+//  * Assembly: each lane's block searches in the patch rows run as
+//    PATCH_MAX_NODES independent fixed-depth binary searches (5 steps for
+//    rows of <= 16 blocks), so their loads are in flight together instead of
+//    one data-dependent loop per row after another.
+__global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32_t* __restrict__ perm,
+                                                         const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                         const int32_t* __restrict__ gcol,
+                                                         const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
+                                                         int* bad) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
+  const int64_t i = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+  const bool live = i < np;
+  const int32_t I = live ? perm[i] : 0;
+  const int64_t q0 = ptr[I];
+  const int m = live ? (int)(ptr[I + 1] - q0) : 0;
+  const int d = 2 * m;
+  double M[2 * PATCH_MAX_NODES];
+#pragma unroll
+  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = 0.0;
+  if (hl < d) {
+    const int32_t Jb = gcol[q0 + (hl >> 1)];
+    const int g = hl & 1;
+    int64_t base[PATCH_MAX_NODES], len[PATCH_MAX_NODES];
+#pragma unroll
+    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
+      const int32_t Ja = a < m ? col[q0 + a] : I;
+      base[a] = ptr[Ja];
+      len[a] = a < m ? ptr[Ja + 1] - base[a] : 0;
+    }
+    // lower bound of Jb in each row, the rows' steps interleaved
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+#pragma unroll
+      for (int a = 0; a < PATCH_MAX_NODES; ++a) {
+        if (len[a] > 0) {
+          const int64_t h2 = len[a] >> 1;
+          if (gcol[base[a] + h2] < Jb) { base[a] += h2 + 1; len[a] -= h2 + 1; }
+          else len[a] = h2;
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
+      if (a < m) {
+        const int32_t Ja = col[q0 + a];
+        const int64_t lo = base[a];
+        if (lo < ptr[Ja + 1] && gcol[lo] == Jb) {
+          const dv4 v = val[lo];
+          M[2 * a] = g ? v.y : v.x;
+          M[2 * a + 1] = g ? v.w : v.z;
+        }
+      }
+    }
+  }
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 2 * PATCH_MAX_NODES; ++k) {
+    // every lane takes part in the broadcasts (the other half may have k < d)
+    const double p = __shfl(M[k], hb + k);
+    const bool act = k < d && ok;
+    if (act && !(p > 0.0)) ok = false;
+    const bool upd = act && ok && hl < d;
+    const bool own = hl == k;
+    const double mk = own ? 1.0 / p : M[k] / p;
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) {
+      if (r == k) continue;
+      const double f = __shfl(M[r], hb + k);
+      const double t = f * mk;
+      if (upd) M[r] = (own ? 0.0 : M[r]) - t;
+    }
+    if (upd) M[k] = mk;
+  }
+  if (!ok && hl == 0) atomicOr(bad, 1);
+  if (live && ok && hl < d) {
+    double* Up = U + i * ustride + hl * (hl + 1) / 2;
+#pragma unroll
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r)
+      if (r <= hl) Up[r] = M[r];
+  }
+}
+
+// MAMG_PATCH_INV=1: the round-5 kernel (one patch per wave; A/B and the
+// bitwise test of the two, tests/test_gpu_patch.py)
+bool patch_inv_v1() {
+  const char* e = opt("MAMG_PATCH_INV");
+  return e && std::atoi(e) == 1;
+}
+
 // One colour of a patch sweep, one wave per patch (4 per workgroup), in place
 // on x (node-interleaved):  x|_p += Minv_p (b - A x)|_p.  The patch's node rows
 // are reduced by 4 lanes each (lanes 4a..4a+3 = node a); lane i < d then forms
@@ -3685,8 +3788,12 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
-  patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
-                                                       flags + 2);
+  if (patch_inv_v1())
+    patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
+                                                         flags + 2);
+  else
+    patch_inv2_kernel<<<(unsigned)((nr + 7) / 8), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
+                                                          flags + 2);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
@@ -6839,8 +6946,10 @@ int dist_patches(DistHandle* h, const DevMat& A0d, const DistLevel& P, DDLevel* 
   int* bad = nullptr;
   if ((rc = T.alloc(&bad, 1, err))) return rc;
   HIPCHK(dev_memset(bad, 0, sizeof(int)));
-  if (np)
+  if (np && patch_inv_v1())
     patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
+  else if (np)
+    patch_inv2_kernel<<<(unsigned)((np + 7) / 8), 256>>>(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
   HIPCHK(hipGetLastError());
   int hb = 0;
   HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import mamg_oracle as mo
+from conftest import set_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -235,3 +236,33 @@ def test_patches_refused_on_the_csr_layout(lib_built):
             M.MetricAMG(s.scipy(), s.W, idofs=idofs, num_functions=2, setup=setup,
                         Schwarz_type=M.parameters.SCHWARZ_PATCHES)
         assert ei.value.code == -4 and 'BSR2' in str(ei.value), (setup, str(ei.value))
+
+
+@pytest.mark.parametrize('dim,n', [(3, 16), (3, 32), (2, 64)])
+def test_patch_inverse_kernels_bitwise(lib_built, dim, n):
+    """the node-patch inverses two patches per wave, in place
+    (patch_inv2_kernel: lane k takes over identity column k at pivot k, the
+    rows' block searches interleaved) perform the round-5 kernel's operations
+    on the same values (MAMG_PATCH_INV=1: one patch per wave, the augmented
+    [A_p | I] in 64 lanes), so the applies and the PCG iterates are bitwise
+    equal; on the verbatim preset too (UA + HEM + W + SGS + scaling)."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, 1e6)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    for prm in (dict(num_functions=2, Schwarz_type=PATCHES),
+                dict(parameters=M.parameters.parameters_metric_schwarz)):
+        zs, xs = [], []
+        for v in ('1', '2'):
+            set_opt('MAMG_PATCH_INV', v)
+            B = M.MetricAMG(A, s.W, idofs=s.idofs, setup='gpu', **prm)
+            assert B.level_format(0)['patches']
+            zs.append(B.matvec(r).clone())
+            B._Aop = A
+            cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+            xs.append((list(cg.residuals) if cg.solve_device(r) is not None else None, cg.residuals))
+            torch.cuda.synchronize()
+            B.close()
+        assert torch.equal(zs[0], zs[1])
+        assert xs[0][1] == xs[1][1]
