@@ -1521,18 +1521,25 @@ __global__ __launch_bounds__(256) void pkey_max_kernel(int64_t nr, const int64_t
 // threads): only uncoloured nodes, and those whose maximum is their own key
 // are appended to the winner list, one atomic per workgroup.  No winner means
 // no uncoloured node (the largest uncoloured key always wins).
+// whether node x is coloured: one bit per node (round 6), so the lookups of
+// the nodes the maxima name hit the 2 MB bitmap in L2 instead of gathering
+// 2-byte colours from a 34 MB array (the same tests, the same colours)
+__device__ __forceinline__ bool coloured(const uint32_t* __restrict__ cb, int64_t x) {
+  return (cb[x >> 5] >> (x & 31)) & 1u;
+}
+
 template <bool FIND>
 __global__ __launch_bounds__(FIND ? 1024 : 256) void pkey_refresh_kernel(
-    int64_t nr, const int64_t* __restrict__ ptr, const int32_t* __restrict__ col, const int16_t* __restrict__ c,
+    int64_t nr, const int64_t* __restrict__ ptr, const int32_t* __restrict__ col, const uint32_t* __restrict__ cb,
     const uint64_t* __restrict__ src, uint64_t* __restrict__ m, int32_t* __restrict__ win,
     unsigned int* __restrict__ nwin) {
   constexpr int NT = FIND ? 1024 : 256;
   const int64_t I = (int64_t)blockIdx.x * NT + threadIdx.x;
   bool w = false;
   if (I < nr) {
-    const bool unc = c[I] < 0;
+    const bool unc = !coloured(cb, I);
     uint64_t v = m[I];
-    if ((!FIND || unc) && v != 0 && c[(uint32_t)v] >= 0) {   // its maximum was coloured: recompute
+    if ((!FIND || unc) && v != 0 && coloured(cb, (uint32_t)v)) {   // its maximum was coloured: recompute
       // rows hold <= PATCH_MAX_NODES columns (build_patches checks): every
       // column load, then every gather, in flight together
       v = src ? src[I] : (unc ? patch_key_dev(I) : 0ull);
@@ -1543,7 +1550,7 @@ __global__ __launch_bounds__(FIND ? 1024 : 256) void pkey_refresh_kernel(
       for (int q = 0; q < PATCH_MAX_NODES; ++q) J[q] = q < len ? col[k0 + q] : (int32_t)I;
 #pragma unroll
       for (int q = 0; q < PATCH_MAX_NODES; ++q) {
-        const uint64_t u = src ? src[J[q]] : (c[J[q]] < 0 ? patch_key_dev(J[q]) : 0ull);
+        const uint64_t u = src ? src[J[q]] : (!coloured(cb, J[q]) ? patch_key_dev(J[q]) : 0ull);
         v = u > v ? u : v;
       }
       m[I] = v;
@@ -1571,8 +1578,8 @@ __global__ __launch_bounds__(FIND ? 1024 : 256) void pkey_refresh_kernel(
 // 1-hop masks of the closed 1-ring
 __global__ __launch_bounds__(256) void patch_win_kernel(int64_t nwin, const int32_t* __restrict__ win,
                                                         const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
-                                                        int16_t* __restrict__ c, unsigned long long* __restrict__ mask1,
-                                                        int* toomany) {
+                                                        int16_t* __restrict__ c, uint32_t* __restrict__ cb,
+                                                        unsigned long long* __restrict__ mask1, int* toomany) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= nwin) return;
@@ -1610,7 +1617,10 @@ __global__ __launch_bounds__(256) void patch_win_kernel(int64_t nwin, const int3
     if (lane == 0) *toomany = 1;
     cc = 0;
   }
-  if (lane == 0) c[I] = (int16_t)cc;
+  if (lane == 0) {
+    c[I] = (int16_t)cc;
+    atomicOr(&cb[I >> 5], 1u << (I & 31));
+  }
   if (lane < d1) atomicOr(&mask1[PATCH_WORDS * u + cc / 64], 1ull << (cc % 64));
 }
 
@@ -3703,7 +3713,10 @@ int patch_colour(TmpPool* T, const TBsr& B, int16_t** cout, int* maxlen, std::st
   unsigned long long* mask1 = nullptr;
   int32_t* win = nullptr;
   unsigned int* wcnt = nullptr;                // winners of the round
+  uint32_t* cb = nullptr;                      // coloured nodes, one bit each
   if ((rc = T->alloc(&c, nr, err))) return rc;
+  if ((rc = T->alloc(&cb, nr / 32 + 1, err))) return rc;
+  HIPCHK(dev_memset(cb, 0, (nr / 32 + 1) * sizeof(uint32_t)));
   if ((rc = T->alloc(&m1, nr, err))) return rc;
   if ((rc = T->alloc(&m2, nr, err))) return rc;
   if ((rc = T->alloc(&m3, nr, err))) return rc;
@@ -3719,24 +3732,24 @@ int patch_colour(TmpPool* T, const TBsr& B, int16_t** cout, int* maxlen, std::st
   pkey_max_kernel<<<nblocks(nr), 256>>>(nr, B.ptr, B.col, m2, m3);
   const unsigned g1k = (unsigned)((nr + 1023) / 1024);
   HIPCHK(dev_memset(wcnt, 0, sizeof(unsigned int)));
-  pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, c, m2, m3, win, wcnt);
+  pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, cb, m2, m3, win, wcnt);
   HIPCHK(hipGetLastError());
   for (int round = 0;; ++round) {
     unsigned int nw = 0;
     HIPCHK(hipMemcpy(&nw, wcnt, sizeof(nw), hipMemcpyDeviceToHost));
     if (nw == 0) break;                        // every node coloured
     if (round > 100000) { *err = "node patches: colouring did not finish"; return MAMG_ERR_SETUP; }
-    patch_win_kernel<<<(unsigned)((nw + 3) / 4), 256>>>(nw, win, B.ptr, B.col, c, mask1, flags + 1);
-    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, c, nullptr, m1, nullptr, nullptr);
-    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, c, m1, m2, nullptr, nullptr);
+    patch_win_kernel<<<(unsigned)((nw + 3) / 4), 256>>>(nw, win, B.ptr, B.col, c, cb, mask1, flags + 1);
+    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, cb, nullptr, m1, nullptr, nullptr);
+    pkey_refresh_kernel<false><<<nblocks(nr), 256>>>(nr, B.ptr, B.col, cb, m1, m2, nullptr, nullptr);
     HIPCHK(dev_memset(wcnt, 0, sizeof(unsigned int)));
-    pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, c, m2, m3, win, wcnt);
+    pkey_refresh_kernel<true><<<g1k, 1024>>>(nr, B.ptr, B.col, cb, m2, m3, win, wcnt);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[1]) { *err = "node patches: more than 256 colours"; return MAMG_ERR_UNSUPPORTED; }
   T->release(m1); T->release(m2); T->release(m3); T->release(mask1); T->release(win); T->release(wcnt);
-  T->release(flags);
+  T->release(flags); T->release(cb);
   *cout = c;
   return MAMG_OK;
 }
