@@ -1653,6 +1653,13 @@ __global__ __launch_bounds__(256) void i64_to_i32_kernel(int64_t n, const int64_
 // column-packed upper triangle: U(i, j), i <= j, at j (j + 1) / 2 + i
 __device__ __forceinline__ int upk(int i, int j) { return i <= j ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j; }
 
+// lane src's double (src may differ per lane): two ds_bpermute_b32
+__device__ __forceinline__ double bperm_f64(double v, int src) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)u);
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 // lane l's double, broadcast to the wave (l wave-uniform)
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -1752,9 +1759,12 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
 //    ds_bpermute (one instruction serves both patches) before lane k
 //    overwrites it.
 //  * Assembly: each lane's block searches in the patch rows run as
-//    PATCH_MAX_NODES independent fixed-depth binary searches (5 steps for
-//    rows of <= 16 blocks), so their loads are in flight together instead of
-//    one data-dependent loop per row after another.
+//    PATCH_MAX_NODES independent branch-free binary searches (5 steps for
+//    rows of <= 16 blocks, every load in bounds), one straight-line block
+//    whose loads overlap, instead of one data-dependent loop per row after
+//    another.
+//  * The pivot and row loops are fully unrolled (a partly rolled loop put M
+//    in scratch: 272 B per lane, 1.8 s at nrefs=6).
 __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ gcol,
@@ -1774,52 +1784,45 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
   if (hl < d) {
     const int32_t Jb = gcol[q0 + (hl >> 1)];
     const int g = hl & 1;
-    int64_t base[PATCH_MAX_NODES], len[PATCH_MAX_NODES];
+    // each row's lower bound of Jb by a branch-free 5-step binary search
+    // (rows of <= 16 blocks), every load in bounds, so the rows' searches
+    // form one straight-line block and their loads overlap
 #pragma unroll
     for (int a = 0; a < PATCH_MAX_NODES; ++a) {
-      const int32_t Ja = a < m ? col[q0 + a] : I;
-      base[a] = ptr[Ja];
-      len[a] = a < m ? ptr[Ja + 1] - base[a] : 0;
-    }
-    // lower bound of Jb in each row, the rows' steps interleaved
+      const bool va = a < m;
+      const int32_t Ja = va ? col[q0 + a] : I;
+      const int64_t p0 = ptr[Ja];
+      const int n = va ? (int)(ptr[Ja + 1] - p0) : 0;
+      int64_t b = p0;
+      int l = n;
 #pragma unroll
-    for (int st = 0; st < 5; ++st) {
-#pragma unroll
-      for (int a = 0; a < PATCH_MAX_NODES; ++a) {
-        if (len[a] > 0) {
-          const int64_t h2 = len[a] >> 1;
-          if (gcol[base[a] + h2] < Jb) { base[a] += h2 + 1; len[a] -= h2 + 1; }
-          else len[a] = h2;
-        }
+      for (int st = 0; st < 5; ++st) {
+        const int h = l >> 1;
+        const bool lt = gcol[l > 0 ? b + h : p0] < Jb;
+        b = (l > 0 && lt) ? b + h + 1 : b;
+        l = l > 0 ? (lt ? l - h - 1 : h) : 0;
       }
-    }
-#pragma unroll
-    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
-      if (a < m) {
-        const int32_t Ja = col[q0 + a];
-        const int64_t lo = base[a];
-        if (lo < ptr[Ja + 1] && gcol[lo] == Jb) {
-          const dv4 v = val[lo];
-          M[2 * a] = g ? v.y : v.x;
-          M[2 * a + 1] = g ? v.w : v.z;
-        }
+      if (va && b < p0 + n && gcol[b] == Jb) {
+        const dv4 v = val[b];
+        M[2 * a] = g ? v.y : v.x;
+        M[2 * a + 1] = g ? v.w : v.z;
       }
     }
   }
   bool ok = true;
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int k = 0; k < 2 * PATCH_MAX_NODES; ++k) {
     // every lane takes part in the broadcasts (the other half may have k < d)
-    const double p = __shfl(M[k], hb + k);
+    const double p = bperm_f64(M[k], hb + k);
     const bool act = k < d && ok;
     if (act && !(p > 0.0)) ok = false;
     const bool upd = act && ok && hl < d;
     const bool own = hl == k;
     const double mk = own ? 1.0 / p : M[k] / p;
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) {
       if (r == k) continue;
-      const double f = __shfl(M[r], hb + k);
+      const double f = bperm_f64(M[r], hb + k);
       const double t = f * mk;
       if (upd) M[r] = (own ? 0.0 : M[r]) - t;
     }
