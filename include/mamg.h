@@ -412,7 +412,8 @@ enum { MAMG_FMT_SELL = 1, MAMG_FMT_SYM = 2, MAMG_FMT_POST_FUSED = 4, MAMG_FMT_PO
        MAMG_FMT_PATCHES = 128,  /* smoother: multiplicative node-patch Schwarz (SCHWARZ_PATCHES) */
        MAMG_FMT_GS = 256,       /* smoother: multicolour node-block GS / SGS sweeps */
        MAMG_FMT_RINGS = 512,    /* smoother: multiplicative seed-ring Schwarz + GS on the rest (SCHWARZ_RINGS) */
-       MAMG_FMT_R_BANDS = 1024 };  /* restriction rows walked plane band by plane band per XCD */
+       MAMG_FMT_R_BANDS = 1024,    /* restriction rows walked plane band by plane band per XCD */
+       MAMG_FMT_K_COL16 = 2048 };  /* K's columns as 16-bit offsets from a per-slice base */
 int mamg_level_format(const mamg_handle* h, int level);
 /* The parameters the handle runs (as mamg_hier_params). */
 int mamg_handle_params(const mamg_handle* h, mamg_params* out);

@@ -253,7 +253,7 @@ class MetricAMG:
         return {'sell': bool(f & 1), 'sym': bool(f & 2), 'post_fused': bool(f & 4),
                 'post_k': bool(f & 8), 'post_sell': bool(f & 16), 'half': bool(f & 32),
                 'bands': bool(f & 64), 'patches': bool(f & 128), 'gs': bool(f & 256),
-                'rings': bool(f & 512), 'r_bands': bool(f & 1024)}
+                'rings': bool(f & 512), 'r_bands': bool(f & 1024), 'k_col16': bool(f & 2048)}
 
     @property
     def kregion(self) -> dict:

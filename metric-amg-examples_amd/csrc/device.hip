@@ -459,12 +459,13 @@ __global__ __launch_bounds__(256) void sell2_kernel(
 // the block loop.  Used for the level-0 fused post operator
 // z = x1 + W r1 + K e (EPI_KPOST, LPR 2, U 5: K 1.69 -> 1.54 ms on one
 // upload) and the SELL-stored coarse operators.
-template <int LPR, int U, int EPI, bool XFM, bool SYM, int SPL, int TAG, int PROBE = 0>
+template <int LPR, int U, int EPI, bool XFM, bool SYM, int SPL, int TAG, int PROBE = 0, bool C16 = false>
 __global__ __launch_bounds__(256) void msell_kernel(
     int64_t nr, const int64_t* __restrict__ soff, const int32_t* __restrict__ meta,
     const int32_t* __restrict__ bcol, const double* __restrict__ bval, int64_t nbs,
     const double* __restrict__ x, int64_t xs, const double* y, const double* __restrict__ b, int64_t bs,
-    const dv4* __restrict__ W, double* out, int64_t os, int remap, int lsort, int64_t rb0) {
+    const dv4* __restrict__ W, double* out, int64_t os, int remap, int lsort, int64_t rb0,
+    const uint16_t* __restrict__ c16, const int32_t* __restrict__ cbase) {
   constexpr int RW = 64 / LPR;                          // rows per wavefront
   const int lane = threadIdx.x & 63, q = lane / RW;
   // rb0: first workgroup of a row-range launch (rows [256 rb0 / LPR, ...))
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256) void msell_kernel(
   const double2 bb = NB && wr ? double2{vget(b, bs, nd, 0), vget(b, bs, nd, 1)} : double2{0.0, 0.0};
   double s0 = 0.0, s1 = 0.0;
   const int j0 = q * U, j1 = q == LPR - 1 ? len : (len < j0 + U ? len : j0 + U);
+  const int32_t cb0 = C16 ? cbase[ns / SELL_C] : 0;
   for (int j = j0; j < j1; j += U) {
     int32_t c[U];
     dv4 v[U];
@@ -495,7 +497,8 @@ __global__ __launch_bounds__(256) void msell_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
-      c[u] = PROBE == 2 ? __builtin_nontemporal_load(bcol + kk) : bcol[kk];
+      if constexpr (C16) c[u] = cb0 + (int32_t)c16[kk];
+      else c[u] = PROBE == 2 ? __builtin_nontemporal_load(bcol + kk) : bcol[kk];
       v[u] = SPL ? blk_any<SPL>(bval, nbs, kk) : blk<SYM, (PROBE >= 2)>(bval, offd, kk);
     }
 #pragma unroll
@@ -2132,6 +2135,7 @@ int g_r_bands = 1;
 int g_k_sort = 1;
 int g_post_k = 1;
 int g_kvar = 0;
+int g_k_c16 = 1;   // MAMG_K_COL16: level-0 K's columns as 16-bit offsets from a per-slice base
 __global__ void warm_kernel() {}
 
 // MAMG_FUSE_RBD: which restrictions write the next level's first sweep
@@ -2172,6 +2176,8 @@ void read_knobs() {
   g_k_sort = e ? std::atoi(e) : 1;
   e = opt("MAMG_FUSE_RBD");
   g_fuse_rbd = e ? std::atoi(e) : 2;
+  e = opt("MAMG_K_COL16");
+  g_k_c16 = e ? std::atoi(e) : 1;
 }
 
 // every block symmetric (bitwise): then 3 doubles per block carry it exactly
@@ -2222,6 +2228,11 @@ struct DBsr {              // 2x2 blocks, node-major
   int32_t* perm = nullptr;  // SELL-C-sigma: row held by each slot (merged matrices)
   bool lsort = false;       // SELL rows sorted by length inside each slice: meta is per slot,
                             // length | (row - slice start) << 16 (sort_sell_slices)
+  // SELL columns as 16-bit offsets from a per-slice base (level-0 K, round
+  // 6: compress_sell_cols); col is kept for the layout code, the kernel reads
+  // col16 + cbase
+  uint16_t* col16 = nullptr;
+  int32_t* cbase = nullptr;
   // half-symmetric ELL-64 (half == true, A symmetric bitwise): col / val hold
   // the upper part I <= J < nr, hwu slots per row; lptr holds,
   // per lower entry J < I, the slot of the mirror block (J, I) in the upper
@@ -3475,6 +3486,76 @@ int sort_sell_slices(HT* h, TmpPool* T, DBsr* D, std::string* err) {
   return MAMG_OK;
 }
 
+// SELL columns as 16-bit offsets from a per-slice base (round 6, level-0 K:
+// MAMG_K_COL16, default on).  K's columns are coarse node ids; the 64 rows of
+// a slice reach the aggregates of a few neighbouring planes, so every slice's
+// columns span far less than 2^16 (at nrefs=6: 4-byte columns are 11 % of K's
+// stream).  cbase[s] = the slice's smallest column; a matrix with any slice
+// spanning more keeps its 32-bit columns (then nothing changes).  The kernel
+// adds the base back: the same columns, the same sums, bitwise the 32-bit
+// layout (tests/test_gpu.py::test_k_col16_bitwise).
+__global__ __launch_bounds__(64) void sell_span_kernel(int64_t nr, const int64_t* __restrict__ soff,
+                                                       const int32_t* __restrict__ meta,
+                                                       const int32_t* __restrict__ col, int32_t* __restrict__ cbase,
+                                                       int* wide) {
+  const int64_t s = blockIdx.x, slot = s * SELL_C + threadIdx.x;
+  int32_t lo = INT32_MAX, hi = INT32_MIN;
+  if (slot < nr) {
+    const int len = meta[slot] & 0xffff;
+    const int64_t k = soff[s] + threadIdx.x;
+    for (int j = 0; j < len; ++j) {
+      const int32_t c = col[k + (int64_t)SELL_C * j];
+      lo = c < lo ? c : lo;
+      hi = c > hi ? c : hi;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if (threadIdx.x == 0) {
+    cbase[s] = lo == INT32_MAX ? 0 : lo;
+    if (hi != INT32_MIN && (int64_t)hi - (int64_t)lo > 65535) atomicOr(wide, 1);
+  }
+}
+__global__ __launch_bounds__(64) void sell_col16_kernel(int64_t nr, const int64_t* __restrict__ soff,
+                                                        const int32_t* __restrict__ meta,
+                                                        const int32_t* __restrict__ col,
+                                                        const int32_t* __restrict__ cbase, uint16_t* __restrict__ c16) {
+  const int64_t s = blockIdx.x, slot = s * SELL_C + threadIdx.x;
+  if (slot >= nr) return;
+  const int len = meta[slot] & 0xffff;
+  const int64_t k = soff[s] + threadIdx.x;
+  const int32_t b = cbase[s];
+  for (int j = 0; j < len; ++j) c16[k + (int64_t)SELL_C * j] = (uint16_t)(col[k + (int64_t)SELL_C * j] - b);
+}
+template <class HT>
+int compress_sell_cols(HT* h, TmpPool* T, DBsr* D, std::string* err) {
+  int rc;
+  if (!D->sell || D->half || D->nr == 0 || D->nbs == 0) return MAMG_OK;
+  const int64_t ns = (D->nr + SELL_C - 1) / SELL_C;
+  int32_t* base = nullptr;
+  int* wide = nullptr;
+  if ((rc = T->alloc(&wide, 1, err))) return rc;
+  HIPCHK(dev_memset(wide, 0, sizeof(int)));
+  if ((rc = dalloc(h, &base, ns, err))) return rc;
+  sell_span_kernel<<<(unsigned)ns, SELL_C>>>(D->nr, D->soff, D->meta, D->col, base, wide);
+  HIPCHK(hipGetLastError());
+  int hw = 1;
+  HIPCHK(hipMemcpy(&hw, wide, sizeof(int), hipMemcpyDeviceToHost));
+  T->release(wide);
+  if (hw) return MAMG_OK;   // a slice spans more than 16 bits: 32-bit columns (base stays unused)
+  uint16_t* c16 = nullptr;
+  if ((rc = dalloc(h, &c16, D->nbs, err))) return rc;
+  HIPCHK(dev_memset(c16, 0, D->nbs * sizeof(uint16_t)));
+  sell_col16_kernel<<<(unsigned)ns, SELL_C>>>(D->nr, D->soff, D->meta, D->col, base, c16);
+  HIPCHK(hipGetLastError());
+  D->col16 = c16;
+  D->cbase = base;
+  return MAMG_OK;
+}
+
 // one BSR2 level from device-resident field-major CSRs (AP.n == 0: no fusion)
 struct LevelSrc {
   DevMat A, P, AP, R;
@@ -3984,6 +4065,8 @@ int build_bsr_level(DeviceHandle* h, int l, const LevelSrc& S, int64_t nvc, int 
       return rc;
     if (l == 0 && g_post_k && g_k_sort && D.KPb.sell && D.KPb.lpr <= 1)
       if ((rc = sort_sell_slices(h, &T, &D.KPb, err))) return rc;
+    if (l == 0 && g_post_k && D.KPb.sell && g_k_c16)
+      if ((rc = compress_sell_cols(h, &T, &D.KPb, err))) return rc;
   } else {
     TBsr Pb;
     if ((rc = dev_csr_to_bsr(&T, S.P, nv, nvc, &Pb, err))) return rc;
@@ -4650,13 +4733,18 @@ void launch_msell(const Op& o, hipStream_t s) {
   const int64_t b0 = r0 / rows;
   const unsigned g = (unsigned)((r1 + rows - 1) / rows - b0);
 #define MSELL_ARGS r1, M.soff, M.meta, M.col, M.val, M.nbs, o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, \
-    (TAG == 0 && g_kvar == 3) ? 1 : 0, M.lsort ? 1 : 0, b0
+    (TAG == 0 && g_kvar == 3) ? 1 : 0, M.lsort ? 1 : 0, b0, M.col16, M.cbase
   switch (o.epi) {
     case EPI_Y: msell_kernel<LPR, U, EPI_Y, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
     case EPI_YADD: msell_kernel<LPR, U, EPI_YADD, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
     case EPI_RESID: msell_kernel<LPR, U, EPI_RESID, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
     case EPI_KPOST:
-      if constexpr (!XFM && !SYM) msell_kernel<LPR, U, EPI_KPOST, false, false, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS);
+      if constexpr (!XFM && !SYM) {
+        if (TAG == 0 && PROBE == 0 && M.col16)   // level-0 K with 16-bit columns (compress_sell_cols)
+          msell_kernel<LPR, U, EPI_KPOST, false, false, SPL, TAG, 0, true><<<g, 256, 0, s>>>(MSELL_ARGS);
+        else
+          msell_kernel<LPR, U, EPI_KPOST, false, false, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS);
+      }
       break;
     default: msell_kernel<LPR, U, EPI_BJAC, XFM, SYM, SPL, TAG, PROBE><<<g, 256, 0, s>>>(MSELL_ARGS); break;
   }
@@ -5100,7 +5188,8 @@ void rehome_operators(DeviceHandle* h) {
   };
   select_k_region(h);            // the largest stream first, placed by measurement
   h->layout_ms[LT_KREGION] = lap();
-  rehome_array(h, (void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
+  if (L.KPb.col16) rehome_array(h, (void**)&L.KPb.col16, (size_t)L.KPb.nbs * sizeof(uint16_t));
+  else rehome_array(h, (void**)&L.KPb.col, (size_t)L.KPb.nbs * sizeof(int32_t));
   if (L.Ab.half) rehome_bsr(h, L.Ab);
   if (!L.Rb.sell && !L.Rb.sym)
     rehome_array(h, (void**)&L.Rb.val, (size_t)L.Rb.nb * 4 * sizeof(double));
@@ -5508,7 +5597,8 @@ int dev_level_format(const DeviceHandle* h, int level) {
          (L.PAb.nr > 0 || L.KPb.nr > 0 ? MAMG_FMT_POST_FUSED : 0) | (L.KPb.nr > 0 ? MAMG_FMT_POST_K : 0) |
          (L.KPb.sell ? MAMG_FMT_POST_SELL : 0) | (L.Ab.nsched > 0 || L.Ab.nsched_r > 0 ? MAMG_FMT_BANDS : 0) |
          (L.pcs.size() > 1 ? MAMG_FMT_PATCHES : 0) | (L.gcs.size() > 1 ? MAMG_FMT_GS : 0) |
-         (L.rcs.size() > 1 ? MAMG_FMT_RINGS : 0) | (L.Rb.nrsched > 0 ? MAMG_FMT_R_BANDS : 0);
+         (L.rcs.size() > 1 ? MAMG_FMT_RINGS : 0) | (L.Rb.nrsched > 0 ? MAMG_FMT_R_BANDS : 0) |
+         (L.KPb.col16 ? MAMG_FMT_K_COL16 : 0);
 }
 
 mamg_params dev_params(const DeviceHandle* h) { return h->p; }

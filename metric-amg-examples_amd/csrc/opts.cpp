@@ -28,6 +28,7 @@ constexpr const char* kNames[] = {
     "MAMG_HALF_BANDS",            // 1: plane-band schedule of the half-symmetric kernel
     "MAMG_R_BANDS",               // 1: plane-band schedule of the level-0 restriction
     "MAMG_K_SORT",                // 1: K rows sorted by length inside SELL slices
+    "MAMG_K_COL16",               // 1: level-0 K's columns as 16-bit offsets from a per-slice base
     "MAMG_FUSE_RBD",              // which restrictions write the next first sweep (2)
     "MAMG_CSR2BSR_FILL",          // 1: column-only LDS fill of CSR -> BSR2; 0: staged merge
     "MAMG_KREGION_TRIES",         // K value regions timed at upload

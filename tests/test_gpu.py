@@ -526,6 +526,35 @@ def test_k_block_layouts_bitwise(lib_built, monkeypatch):
     assert rel(zs[1].cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
 
 
+@pytest.mark.parametrize('dim,n,g', [(3, 16, 1e6), (3, 32, 1e6), (2, 128, 1e4)])
+def test_k_col16_bitwise(lib_built, dim, n, g):
+    """Level-0 K's columns as 16-bit offsets from a per-slice base (round 6,
+    MAMG_K_COL16=1, the default): the kernel adds the base back, so the apply
+    and the device PCG are bitwise those of the 32-bit columns, and = the
+    oracle."""
+    import torch
+    M = _mamg()
+    set_opt('MAMG_SELL_MIN_ROWS', '1')
+    s = M.problems.bidomain(dim, n, g)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    zs, its = [], []
+    for c16 in ('0', '1'):
+        set_opt('MAMG_K_COL16', c16)
+        B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2)
+        assert B.level_format(0)['post_sell'] and B.level_format(0)['k_col16'] == (c16 == '1')
+        zs.append(B.matvec(r))
+        cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        x = cg * mo.seeded_rhs(s.N)
+        its.append((len(cg.residuals), np.asarray(x.cpu() if hasattr(x, 'cpu') else x)))
+        torch.cuda.synchronize()
+        B.close()
+    assert torch.equal(zs[0], zs[1])
+    assert its[0][0] == its[1][0] and np.array_equal(its[0][1], its[1][1])
+    h = mo.setup(A, mo.Params(num_functions=2), idofs=s.idofs)
+    assert rel(zs[1].cpu().numpy(), h.apply(mo.seeded_rhs(s.N))) < APPLY_TOL
+
+
 # MAMG_K_VARIANT exists only in the diagnosis build: these run in a child
 # process that loads it (tests/test_gpu_poison.py)
 needs_diag = pytest.mark.skipif(not __import__('conftest').diag_loaded(),
