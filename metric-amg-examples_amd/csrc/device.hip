@@ -4114,7 +4114,8 @@ double bsr_bytes(const DBsr& M, int epi) {
   // lower block + row meta; the mirrors' values are re-reads, not counted
   double b = M.half ? 28.0 * (M.nb - M.nlo) + 4.0 * M.nlo + 4.0 * M.nr + (M.ngs ? 8.0 * (M.nr / SELL_C + 2) : 0.0) +
                           16.0 * M.nc + 16.0 * M.nr
-                    : (M.sym ? 28.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) + 16.0 * M.nc + 16.0 * M.nr;
+                    : (M.sym ? 28.0 : M.col16 ? 34.0 : 36.0) * M.nb + index_bytes(M, M.nr + 1) +
+                          (M.col16 ? 4.0 * (M.nr / SELL_C + 1) : 0.0) + 16.0 * M.nc + 16.0 * M.nr;
   if (epi == EPI_YADD) b += 16.0 * M.nr;
   if (epi == EPI_RESID) b += 16.0 * M.nr;
   if (epi == EPI_BJAC || epi == EPI_KPOST) b += 16.0 * M.nr + 16.0 * M.nr + 32.0 * M.nr;   // y, b, W
