@@ -30,11 +30,19 @@ def main():
     ap.add_argument('--tail-nodes', type=int, default=None)
     ap.add_argument('--op-profile', action='store_true')
     ap.add_argument('--timeline', action='store_true', help='with --op-profile: every tail op')
+    ap.add_argument('--tail-res', type=int, default=None, help='MAMG_TAIL_RES (register-resident tail operators)')
+    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE: a layout switch (mamg_set_option)')
+    ap.add_argument('--pcg', action='store_true', help='also the device PCG iterations (rtol 1e-6)')
     args = ap.parse_args()
-    if args.tail_nodes is not None:
-        os.environ['MAMG_TAIL_NODES'] = str(args.tail_nodes)
     import torch
     import metric_amg_examples_amd as M
+    if args.tail_nodes is not None:
+        M._lib.set_option('MAMG_TAIL_NODES', args.tail_nodes)
+    if args.tail_res is not None:
+        M._lib.set_option('MAMG_TAIL_RES', args.tail_res)
+    for kv in args.opt:
+        k, v = kv.split('=', 1)
+        M._lib.set_option(k, v)
     n = M.problems.finest_n(3, args.nrefs)
     s = M.problems.bidomain(3, n, 1e6)
     A = s.scipy()
@@ -51,6 +59,16 @@ def main():
         B.apply_device(r, z)
     torch.cuda.synchronize()
     print('ms/apply %.3f' % ((time.time() - t) / args.reps * 1e3), flush=True)
+    print('znorm %.17g' % float(torch.linalg.norm(z)), flush=True)
+    if args.pcg:   # bench.py's PCG (cbc.block ConjGrad, 1e-8), device-resident
+        B._Aop = A
+        cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+        torch.cuda.synchronize()
+        t = time.time()
+        cg * r
+        torch.cuda.synchronize()
+        print('pcg niters %d residual %.6e %.3f s' % (len(cg.residuals) - 1, cg.residuals[-1], time.time() - t),
+              flush=True)
     if args.op_profile:
         os.environ['MAMG_OP_PROFILE'] = '1'
         os.environ['MAMG_TAIL_PROFILE'] = '2' if args.timeline else '1'

@@ -967,7 +967,7 @@ __global__ __launch_bounds__(256) void gs2_kernel(
 // this replaces tens of thousands of ~5 us launches per apply.
 // ---------------------------------------------------------------------------
 enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, T_DOT2 = 6, T_CSCALE = 7,
-             T_COPY = 8 };
+             T_COPY = 8, T_RLOAD = 9 };
 // LDS residency (tail_lds_plan): the program itself and every work vector of
 // the tail levels live in the workgroup's LDS for the whole launch; a vector
 // field of a TOp then holds (byte offset in the dynamic LDS) | 1 instead of a
@@ -976,8 +976,16 @@ enum TKind { T_BSR = 0, T_BD = 1, T_GEMV = 2, T_AXPY = 3, T_ZERO = 4, T_GS = 5, 
 // written ones out.  The colour steps' dependent chain becomes LDS op
 // descriptor (scalar loads) -> global (L2) row pointers, columns, values ->
 // LDS x gathers.
+// Register residency (tail_kernel RES, tail_res_plan): the rows of the tail
+// levels' operators are spread over the workgroup's threads, one row per
+// thread, and held in registers for the whole launch (T_RLOAD ops at the
+// start load them).  An op with res = 1 on such a matrix: thread t computes
+// row t - rbase if that lies in the op's (compact) row range [r0, r1), from
+// registers; ridx maps compact rows to the matrix's rows (a GS layout pads
+// each colour to whole 64-row slices).  A colour step is then LDS descriptor
+// -> LDS x gathers -> LDS store, with no global round trip.
 struct TOp {
-  int kind = 0, epi = 0, vl = 1, sym = 0;
+  int kind = 0, epi = 0, vl = 1, sym = 0, res = 0, rbase = 0;
   int64_t n = 0, r0 = 0, r1 = 0, nb = 0;
   const int64_t* ptr = nullptr;
   const int32_t* col = nullptr;
@@ -987,6 +995,7 @@ struct TOp {
   double* out = nullptr;
   const int32_t* perm = nullptr;
   double* part = nullptr;
+  const int32_t* ridx = nullptr;
 };
 // 512 threads: 256 VGPRs per lane (1024 would cap them at 128 and spill the
 // interpreter's loop state to scratch); the tail's ops hold a few hundred
@@ -1078,7 +1087,9 @@ struct TailMat {
 // rows of a lane-group BSR2 op (bsr2_kernel's per-row code, node-major
 // vectors); GS: rows [r0, r1) of the colour-permuted matrix, update in place.
 // XL: the gathered vector x lives in LDS
-template <bool XL>
+// LIGHT (the register-resident kernel, whose generic ops are the few
+// non-resident transfers): no first-chunk prefetch, fewer live registers
+template <bool XL, bool LIGHT = false>
 __device__ void tail_bsr(const TOp& o, const TOpnd& V, bool gs) {
   const TailMat M(o);
   // 32-bit row arithmetic (tail levels are small) and shifts by log2(VL):
@@ -1114,7 +1125,7 @@ __device__ void tail_bsr(const TOp& o, const TOpnd& V, bool gs) {
       gb1 = V.b.ld(2 * gIc + 1);
       gx = tail_x<XL>(X, gIc);
     }
-    if (p1 > p0) {
+    if (!LIGHT && p1 > p0) {
       // the first two chunks: all column and value loads issued before any
       // gather, so a row of up to 4 VL blocks is one load -> gather round trip
       {
@@ -1144,7 +1155,9 @@ __device__ void tail_bsr(const TOp& o, const TOpnd& V, bool gs) {
           t1 += hh[q + 1] ? vv[q + 1].z * xa[q + 1].x + vv[q + 1].w * xa[q + 1].y : 0.0;
         }
       }
-      for (int kb0 = p0 + 4 * VL; kb0 < p1; kb0 += 2 * VL) {
+    }
+    if (p1 > p0) {
+      for (int kb0 = LIGHT ? p0 : p0 + 4 * VL; kb0 < p1; kb0 += 2 * VL) {
         const int ka = kb0 + lane, kb = ka + VL;
         const bool ha = ka < p1, hb = kb < p1;
         const int la = ha ? ka : p1 - 1, lb = hb ? kb : p1 - 1;
@@ -1206,6 +1219,139 @@ __device__ void tail_bsr(const TOp& o, const TOpnd& V, bool gs) {
   }
 }
 
+// a thread's register-resident row (see TOp): up to RES_RB blocks; the rest
+// of a longer row in the LDS region (values at ovv, 16-bit columns at ovc,
+// the GS block inverse at gdo; byte offsets)
+constexpr int RES_RB = 12;
+struct TRes {
+  int len = 0, gI = -1, ovv = 0, ovc = 0, gdo = 0;
+  uint32_t c[RES_RB / 2];   // two 16-bit node columns (the tail levels have < 2^16 nodes)
+  dv4 v[RES_RB];
+  __device__ __forceinline__ int col(int k) const { return (int)((c[k >> 1] >> (16 * (k & 1))) & 0xffffu); }
+};
+
+// T_RLOAD: threads [rbase, rbase + n) take compact rows 0 .. n - 1 of the
+// op's matrix (ridx[2 j]: compact -> matrix row, ridx[2 j + 1]: the row's
+// first block in the LDS overflow; perm: matrix row -> node; W: the rows' GS
+// block inverses).  The LDS region at byte r0: one block inverse per thread
+// (TAIL_THREADS x 32 B), r1 overflow blocks' values (32 B), their columns (2 B)
+__device__ __forceinline__ void tail_rload(const TOp& o, TRes& R, char* lds) {
+  const int t = (int)threadIdx.x, j = t - o.rbase;
+  if (j < 0 || j >= (int)o.n) return;
+  const TailMat M(o);
+  const int i = gload(o.ridx + 2 * j), ov = gload(o.ridx + 2 * j + 1);
+  const int p0 = M.P(i);
+  R.len = M.P(i + 1) - p0;
+  const int ovb = (int)o.r0 + 32 * TAIL_THREADS;
+  R.ovv = ovb + 32 * ov;
+  R.ovc = ovb + 32 * (int)o.r1 + 2 * ov;
+  R.gdo = (int)o.r0 + 32 * t;
+  const int nov = R.len > RES_RB ? (R.len - RES_RB + 3) / 4 * 4 : 0;   // padded to whole fours
+  for (int k = 0; k < nov; ++k) {
+    const bool h = RES_RB + k < R.len;
+    *(AS3 dv4*)(lds + R.ovv + 32 * k) = h ? M.V(p0 + RES_RB + k) : dv4{0.0, 0.0, 0.0, 0.0};
+    *(AS3 uint16_t*)(lds + R.ovc + 2 * k) = h ? (uint16_t)M.C(p0 + RES_RB + k) : (uint16_t)0;
+  }
+  R.gI = o.perm ? M.perm(i) : i;
+  *(AS3 dv4*)(lds + R.gdo) = o.W ? M.W(i) : dv4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < RES_RB; k += 2) {
+    const bool h0 = k < R.len, h1 = k + 1 < R.len;
+    const uint32_t c0 = h0 ? (uint32_t)M.C(p0 + k) : 0u, c1 = h1 ? (uint32_t)M.C(p0 + k + 1) : 0u;
+    R.c[k >> 1] = c0 | (c1 << 16);
+    R.v[k] = h0 ? M.V(p0 + k) : dv4{0.0, 0.0, 0.0, 0.0};
+    R.v[k + 1] = h1 ? M.V(p0 + k + 1) : dv4{0.0, 0.0, 0.0, 0.0};
+  }
+}
+
+// a row of a T_BSR / T_GS op from the thread's resident row (tail_bsr's
+// operations at node gI; one lane per row, blocks summed in row order over
+// two alternating accumulators)
+template <bool XL>
+__device__ __forceinline__ void tail_res(const TOp& o, const TOpnd& V, const TRes& R, bool gs, const char* lds) {
+  const int j = (int)threadIdx.x - o.rbase;
+  if (j < (int)o.r0 || j >= (int)o.r1) return;
+  const int node = R.gI;
+  const TVec& X = V.x;
+  double gb0 = 0.0, gb1 = 0.0;
+  double2 gx = {0.0, 0.0};
+  if (gs) {
+    gb0 = V.b.ld(2 * node);
+    gb1 = V.b.ld(2 * node + 1);
+    gx = tail_x<XL>(X, node);
+  }
+  double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+  constexpr int GQ = RES_RB / 2;   // gathers in flight
+#pragma unroll
+  for (int k0 = 0; k0 < RES_RB; k0 += GQ) {
+    double2 xa[GQ];
+#pragma unroll
+    for (int q = 0; q < GQ; ++q) xa[q] = tail_x<XL>(X, R.col(k0 + q));
+    // blocks past the row's length are zero (tail_rload) and gather x(0):
+    // no predicate, 0 * x(0) adds +-0
+#pragma unroll
+    for (int q = 0; q < GQ; q += 2) {   // fused multiply-adds into four accumulators
+      const int k = k0 + q;
+      s0 = fma(R.v[k].y, xa[q].y, fma(R.v[k].x, xa[q].x, s0));
+      s1 = fma(R.v[k].w, xa[q].y, fma(R.v[k].z, xa[q].x, s1));
+      t0 = fma(R.v[k + 1].y, xa[q + 1].y, fma(R.v[k + 1].x, xa[q + 1].x, t0));
+      t1 = fma(R.v[k + 1].w, xa[q + 1].y, fma(R.v[k + 1].z, xa[q + 1].x, t1));
+    }
+  }
+  // a long row's remaining blocks, from the LDS region, four at a time:
+  // their column, value and x loads issued together (two LDS round trips
+  // per four blocks, not two per block); past the row's end: column 0, zero
+  // values (tail_rload pads the region's last row to a multiple of 4)
+  for (int k0 = 0; k0 < R.len - RES_RB; k0 += 4) {
+    int c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = (int)*(const AS3 uint16_t*)(lds + R.ovc + 2 * (k0 + q));
+    dv4 v[4];
+    double2 a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = *(const AS3 dv4*)(lds + R.ovv + 32 * (k0 + q));
+      a[q] = tail_x<XL>(X, c[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      s0 = fma(v[q].y, a[q].y, fma(v[q].x, a[q].x, s0));
+      s1 = fma(v[q].w, a[q].y, fma(v[q].z, a[q].x, s1));
+      t0 = fma(v[q + 1].y, a[q + 1].y, fma(v[q + 1].x, a[q + 1].x, t0));
+      t1 = fma(v[q + 1].w, a[q + 1].y, fma(v[q + 1].z, a[q + 1].x, t1));
+    }
+  }
+  s0 += t0;
+  s1 += t1;
+  if (gs) {
+    const double r0 = gb0 - s0, r1 = gb1 - s1;
+    const dv4 gd = *(const AS3 dv4*)(lds + R.gdo);
+    V.out.st(2 * node, gx.x + (gd.x * r0 + gd.y * r1));
+    V.out.st(2 * node + 1, gx.y + (gd.z * r0 + gd.w * r1));
+    return;
+  }
+  double o0, o1;
+  if (o.epi == EPI_Y) {
+    o0 = s0; o1 = s1;
+  } else if (o.epi == EPI_YADD) {
+    o0 = V.y.ld(2 * node) + s0; o1 = V.y.ld(2 * node + 1) + s1;
+  } else if (o.epi == EPI_RESID) {
+    o0 = V.b.ld(2 * node) - s0; o1 = V.b.ld(2 * node + 1) - s1;
+  } else if (o.epi == EPI_KPOST) {
+    const double r0 = V.b.ld(2 * node), r1 = V.b.ld(2 * node + 1);
+    const dv4 w = gload(o.W + node);
+    o0 = V.y.ld(2 * node) + (w.x * r0 + w.y * r1) + s0;
+    o1 = V.y.ld(2 * node + 1) + (w.z * r0 + w.w * r1) + s1;
+  } else {  // EPI_BJAC
+    const double r0 = V.b.ld(2 * node) - s0, r1 = V.b.ld(2 * node + 1) - s1;
+    const dv4 w = gload(o.W + node);
+    o0 = V.y.ld(2 * node) + (w.x * r0 + w.y * r1);
+    o1 = V.y.ld(2 * node + 1) + (w.z * r0 + w.w * r1);
+  }
+  V.out.st(2 * node, o0);
+  V.out.st(2 * node + 1, o1);
+}
+
 // STAMP: thread 0 records the 100 MHz wall clock at the start and after every
 // op's barrier (stamps[0..nops]; MAMG_TAIL_PROFILE diagnosis, dev_time_apply)
 // dynamic LDS: the tail levels' work vectors (tail_lds_plan)
@@ -1213,13 +1359,15 @@ extern __shared__ double tail_lds[];
 
 // XL: every SpMV / GS op of the program gathers from an LDS-resident x
 // (tail_lds_plan placed all of them), so the gathers are ds_reads
-template <bool STAMP, bool XL>
+// RES: the program has register-resident rows (T_RLOAD, res ops)
+template <bool STAMP, bool XL, bool RES>
 __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restrict__ gprog, int nops, int prog_lds,
                                                            uint64_t* __restrict__ stamps) {
   __shared__ double red[TAIL_THREADS / 64][2];
+  TRes R;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   char* lds = reinterpret_cast<char*>(tail_lds);
-  if (STAMP && t == 0) stamps[0] = wall_clock64();
+  if (STAMP && t == 0) { stamps[0] = wall_clock64(); stamps[nops + 1] = clock64(); }
   // the op descriptors: copied whole into the dynamic LDS at prog_lds (>= 0)
   // once, so an op starts on LDS reads, with no global round trip on the
   // way from one op to the next; else read from global memory per op
@@ -1244,7 +1392,13 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
     if (prog_lds >= 0) {
       uint64_t w[TW];
 #pragma unroll
-      for (int q = 0; q < TW; ++q) w[q] = lw[k * TW + q];
+      for (int q = 0; q < TW; ++q) {
+        // the descriptor is uniform: into scalar registers, not 2 VGPRs per word
+        const uint64_t v = lw[k * TW + q];
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        w[q] = ((uint64_t)hi << 32) | lo;
+      }
       __builtin_memcpy(&od, w, sizeof(TOp));
     } else {
       od = gprog[k];
@@ -1260,8 +1414,17 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       case T_COPY:
         for (int64_t i = t; i < o.n; i += TAIL_THREADS) V.out.st(i, V.x.ld(i));
         break;
-      case T_BSR: tail_bsr<XL>(o, V, false); break;
-      case T_GS: tail_bsr<XL>(o, V, true); break;
+      case T_BSR:
+        if (RES && o.res) tail_res<XL>(o, V, R, false, lds);
+        else tail_bsr<XL, RES>(o, V, false);
+        break;
+      case T_GS:
+        if (RES && o.res) tail_res<XL>(o, V, R, true, lds);
+        else tail_bsr<XL, RES>(o, V, true);
+        break;
+      case T_RLOAD:
+        if (RES) tail_rload(o, R, lds);
+        break;
       case T_BD:
         for (int64_t I = t; I < o.n; I += TAIL_THREADS) {
           const double b0 = V.b.ld(2 * I), b1 = V.b.ld(2 * I + 1);
@@ -1357,7 +1520,18 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       default: break;
     }
     __syncthreads();   // the next op reads what this one wrote (workgroup-scope visibility)
-    if (STAMP && t == 0) stamps[k + 1] = wall_clock64();
+    if (STAMP && t == 0) { stamps[k + 1] = wall_clock64(); stamps[nops + 2 + k] = clock64(); }
+  }
+}
+
+// one tail_kernel launch; flags bit 0: XL, bit 1: RES
+template <bool STAMP>
+void tail_launch(int flags, const TOp* prog, int n, int prog_lds, size_t lds, uint64_t* stamps, hipStream_t s) {
+  switch (flags & 3) {
+    case 0: tail_kernel<STAMP, false, false><<<1, TAIL_THREADS, lds, s>>>(prog, n, prog_lds, stamps); break;
+    case 1: tail_kernel<STAMP, true, false><<<1, TAIL_THREADS, lds, s>>>(prog, n, prog_lds, stamps); break;
+    case 2: tail_kernel<STAMP, false, true><<<1, TAIL_THREADS, lds, s>>>(prog, n, prog_lds, stamps); break;
+    default: tail_kernel<STAMP, true, true><<<1, TAIL_THREADS, lds, s>>>(prog, n, prog_lds, stamps); break;
   }
 }
 
@@ -2401,7 +2575,7 @@ struct DeviceHandle {
   int tail_level = 0;
   std::vector<double> kregion_ms;  // select_k_region: K ms per candidate region, the one kept
   int kregion_best = -1;
-  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; bool xl; int prog_lds; };
+  struct TailProg { const double* b; double* x; TOp* prog; int n; double bytes; int64_t lds; bool xl; int prog_lds; bool res; };
   mutable std::vector<TailProg> tails;
   double* hr = nullptr;            // host-apply staging (device)
   double* hz = nullptr;
@@ -4400,17 +4574,17 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   static std::atomic<uint64_t> attr_devices{0};   // the attribute is set once per device
   const int dev = h->device & 63;
   if (!(attr_devices >> dev & 1)) {
-    if (hipFuncSetAttribute((const void*)tail_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void*)tail_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess
+    const void* fns[] = {(const void*)tail_kernel<false, false, false>, (const void*)tail_kernel<false, true, false>,
+                         (const void*)tail_kernel<false, false, true>, (const void*)tail_kernel<false, true, true>,
 #if MAMG_DIAG   // the stamped (profiling) variants
-        || hipFuncSetAttribute((const void*)tail_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)TAIL_LDS_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void*)tail_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TAIL_LDS_MAX) != hipSuccess
+                         (const void*)tail_kernel<true, false, false>, (const void*)tail_kernel<true, true, false>,
+                         (const void*)tail_kernel<true, false, true>, (const void*)tail_kernel<true, true, true>,
 #endif
-    ) {
+    };
+    bool ok = true;
+    for (const void* f : fns)
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TAIL_LDS_MAX) == hipSuccess;
+    if (!ok) {
       (void)hipGetLastError();
       return 0;                        // no large dynamic LDS: keep the global-vector program
     }
@@ -4442,6 +4616,71 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   return off;
 }
 
+// Register residency of a coarse-tail program (TOp, tail_kernel RES): the
+// operators of levels l, l + 1, .. get one row per thread, while their rows
+// fit the workgroup.  A level with a multicolour GS layout holds it (Gb:
+// colour-permuted, each colour padded to 64-row slices); the level's other
+// ops on A (residual, scaling) then read Gb's row i at node perm(i) -- the
+// same blocks in the same order as A's row.  T_RLOAD ops that load the rows
+// are put in front.  tab: per compact row its matrix row and its first block
+// in the LDS overflow region (blocks past RES_RB; *nov in all), stored after
+// the program; a T_RLOAD's ridx holds (offset in tab + 1) until the caller
+// sets the device pointer, and its r0 / r1 the region's place once the LDS
+// plan is known.  Returns false when nothing is resident.
+bool tail_res_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, std::vector<int32_t>* tab, int64_t* nov) {
+  *nov = 0;
+  if (const char* e = opt("MAMG_TAIL_RES"))
+    if (std::atoi(e) == 0) return false;
+  std::vector<TOp> loads;
+  int rbase = 0;
+  for (size_t ll = (size_t)l; ll < h->L.size(); ++ll) {
+    const DLevel& L = h->L[ll];
+    const bool hasg = L.gcs.size() > 1;
+    const DBsr& M = hasg ? L.Gb : L.Ab;
+    if (!M.ptr || M.sell || M.half || M.split || M.nr <= 0) continue;
+    std::vector<int64_t> comp(M.nr + 1, 0);   // rows before -> compact rows before
+    std::vector<int32_t> rows;                // compact -> M row
+    std::vector<int32_t> pm(M.nr);
+    std::vector<int64_t> ptr(M.nr + 1);
+    if ((hasg && hipMemcpy(pm.data(), L.gperm, M.nr * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) ||
+        hipMemcpy(ptr.data(), M.ptr, (M.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    for (int64_t i = 0; i < M.nr; ++i) {
+      if (!hasg || pm[i] >= 0) rows.push_back((int32_t)i);
+      comp[i + 1] = (int64_t)rows.size();
+    }
+    const int n = (int)rows.size();
+    if (rbase + n > TAIL_THREADS) continue;   // a deeper level may still fit
+    TOp ld;
+    ld.kind = T_RLOAD; ld.n = n; ld.rbase = rbase; ld.sym = M.sym ? 1 : 0; ld.nb = M.nb;
+    ld.ptr = M.ptr; ld.col = M.col; ld.val = M.val; ld.r0 = -1;
+    if (hasg) { ld.perm = L.gperm; ld.W = L.Gd; }
+    ld.ridx = reinterpret_cast<const int32_t*>((uintptr_t)(tab->size() + 1));
+    for (int32_t i : rows) {
+      const int64_t len = ptr[i + 1] - ptr[i];
+      tab->push_back(i);
+      tab->push_back((int32_t)*nov);
+      *nov += len > RES_RB ? (len - RES_RB + 3) / 4 * 4 : 0;   // whole fours (tail_res)
+    }
+    loads.push_back(ld);
+    for (TOp& t : *prog) {
+      if (t.kind == T_GS && hasg && t.ptr == L.Gb.ptr) {
+        t.res = 1; t.rbase = rbase; t.r0 = comp[t.r0]; t.r1 = comp[t.r1];
+      } else if (t.kind == T_BSR && t.ptr == L.Ab.ptr) {
+        t.res = 1; t.rbase = rbase; t.r0 = 0; t.r1 = n;
+        t.ptr = M.ptr; t.col = M.col; t.val = M.val; t.sym = M.sym ? 1 : 0; t.nb = M.nb;
+        t.perm = hasg ? L.gperm : nullptr;
+      }
+    }
+    rbase += n;
+  }
+  if (loads.empty()) return false;
+  prog->insert(prog->begin(), loads.begin(), loads.end());
+  return true;
+}
+
 // the cycle of level l and everything below as one tail_kernel launch; the
 // device op list is built once per (b, x) and kept on the handle
 bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::vector<Op>* ops) {
@@ -4457,6 +4696,10 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       if (!to_tail(sub[k], &prog[k])) return false;
       bytes += sub[k].bytes;
     }
+    std::vector<int32_t> tab;
+    int64_t nov = 0;
+    const std::vector<TOp> plain = prog;
+    bool res = tail_res_plan(h, l, &prog, &tab, &nov);
     int64_t lds = tail_lds_plan(h, l, &prog);
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
@@ -4464,28 +4707,60 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     // the program itself into the LDS after the vectors when it fits
     // (TAIL_LDS_MAX); the dynamic LDS then covers both
     int prog_lds = -1;
-    const int64_t pbytes = (int64_t)(prog.size() * sizeof(TOp));
-    if (lds > 0) {
+    int64_t pbytes = (int64_t)(prog.size() * sizeof(TOp));
+    const char* pl_opt = opt("MAMG_TAIL_PROG_LDS");
+    const bool prog_in_lds = pl_opt ? std::atoi(pl_opt) != 0 : true;
+    if (lds > 0 && prog_in_lds) {
       const int64_t off = (lds + 15) / 16 * 16;
       if (off + pbytes <= TAIL_LDS_MAX) {
         prog_lds = (int)off;
         lds = off + pbytes;
       }
     }
+    // the resident rows' LDS region (block inverses, overflow blocks) after
+    // both; without room for it (or for the program) the tail keeps its
+    // operators in global memory
+    if (res) {
+      const int64_t off = (lds + 15) / 16 * 16, need = 32 * TAIL_THREADS + 34 * nov;
+      if (lds > 0 && off + need <= TAIL_LDS_MAX) {
+        for (TOp& t : prog)
+          if (t.kind == T_RLOAD) { t.r0 = off; t.r1 = nov; }
+        lds = off + need;
+      } else {
+        res = false;
+        tab.clear();
+        prog = plain;
+        lds = tail_lds_plan(h, l, &prog);
+        prog_lds = -1;
+        pbytes = (int64_t)(prog.size() * sizeof(TOp));
+        if (lds > 0 && prog_in_lds) {
+          const int64_t o2 = (lds + 15) / 16 * 16;
+          if (o2 + pbytes <= TAIL_LDS_MAX) {
+            prog_lds = (int)o2;
+            lds = o2 + pbytes;
+          }
+        }
+      }
+    }
     void* d = nullptr;
-    if (raw_malloc(&d, (size_t)pbytes, "long") != hipSuccess) { (void)hipGetLastError(); return false; }
-    if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess) {
+    const size_t tbytes = tab.size() * sizeof(int32_t);
+    if (raw_malloc(&d, (size_t)pbytes + tbytes, "long") != hipSuccess) { (void)hipGetLastError(); return false; }
+    const int32_t* dtab = reinterpret_cast<const int32_t*>(static_cast<char*>(d) + pbytes);
+    for (TOp& t : prog)
+      if (t.ridx) t.ridx = dtab + ((uintptr_t)t.ridx - 1);
+    if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess ||
+        (tbytes && hipMemcpy(static_cast<char*>(d) + pbytes, tab.data(), tbytes, hipMemcpyHostToDevice) != hipSuccess)) {
       (void)hipGetLastError();
       (void)raw_free(d);
       return false;
     }
-    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl, prog_lds});
+    h->tails.push_back({b, xout, (TOp*)d, (int)prog.size(), bytes, lds, xl, prog_lds, res});
     tp = &h->tails.back();
   }
   Op o;
   o.kind = OP_TAIL; o.cls = C_COARSE; o.prog = tp->prog; o.n = tp->n; o.bytes = tp->bytes;
   o.r0 = tp->lds;   // dynamic LDS bytes (0: the program reads global vectors)
-  o.r1 = tp->xl ? 1 : 0;
+  o.r1 = (tp->xl ? 1 : 0) | (tp->res ? 2 : 0);
   o.tail_pl = tp->prog_lds;
   ops->push_back(o);
   return true;
@@ -4967,11 +5242,8 @@ void launch(const Op& o, hipStream_t s) {
     case OP_DOT2:
       if (o.n) dot2_partial_kernel<<<SCALE_BLOCKS, 256, 0, s>>>(o.n, o.b, o.x, o.y, o.part);
       break;
-    case OP_TAIL:
-      if (o.n && o.r1 == 1)
-        tail_kernel<false, true><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, o.tail_pl, nullptr);
-      else if (o.n)
-        tail_kernel<false, false><<<1, TAIL_THREADS, (size_t)o.r0, s>>>(o.prog, (int)o.n, o.tail_pl, nullptr);
+    case OP_TAIL:   // r1: bit 0 = every gathered x in LDS, bit 1 = register-resident rows
+      if (o.n) tail_launch<false>((int)o.r1, o.prog, (int)o.n, o.tail_pl, (size_t)o.r0, nullptr, s);
       break;
     case OP_CSCALE:
       if (o.n) cscale_kernel<<<(unsigned)std::min<int64_t>(SCALE_BLOCKS, nblocks(o.n)), 256, 0, s>>>(o.n, SCALE_BLOCKS, o.part, o.out);
@@ -5897,18 +6169,40 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
                    kv.second.second / reps, 1e3 * kv.second.second / kv.second.first);
   }
   if (std::getenv("MAMG_TAIL_PROFILE")) {
+    // diagnosis: the interpreter's cost per op with nothing to do (200 ops
+    // with no rows), the program in LDS and in global memory
+    {
+      const int nn = 200;
+      std::vector<TOp> np(nn);
+      for (auto& t : np) { t.kind = T_ZERO; t.n = 0; }
+      TOp* dp = nullptr;
+      uint64_t* dst = nullptr;
+      HIPCHK(raw_malloc((void**)&dp, nn * sizeof(TOp), "tmp"));
+      HIPCHK(raw_malloc((void**)&dst, 2 * (nn + 1) * sizeof(uint64_t), "tmp"));
+      HIPCHK(hipMemcpy(dp, np.data(), nn * sizeof(TOp), hipMemcpyHostToDevice));
+      std::vector<uint64_t> st(2 * (nn + 1));
+      for (int pl : {0, -1}) {
+        for (int rep = 0; rep < 3; ++rep) tail_launch<true>(0, dp, nn, pl, pl == 0 ? nn * sizeof(TOp) : 0, dst, s);
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(st.data(), dst, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[mamg tail] %d empty ops, program in %s: %.3f us/op, %.0f cycles/op\n", nn,
+                     pl == 0 ? "LDS" : "global", (double)(st[nn] - st[0]) * 0.01 / nn,
+                     (double)(st[2 * nn + 1] - st[nn + 1]) / nn);
+      }
+      (void)raw_free(dp);
+      (void)raw_free(dst);
+    }
     // diagnosis: wall-clock stamps after every op of each coarse-tail program
     for (const auto& tp : h->tails) {
       std::vector<TOp> prog(tp.n);
-      std::vector<uint64_t> st(tp.n + 1);
+      std::vector<uint64_t> st(2 * (tp.n + 1));   // 100 MHz stamps, then shader-clock stamps
       uint64_t* dst = nullptr;
-      HIPCHK(raw_malloc((void**)&dst, (tp.n + 1) * sizeof(uint64_t), "tmp"));
+      HIPCHK(raw_malloc((void**)&dst, 2 * (tp.n + 1) * sizeof(uint64_t), "tmp"));
       HIPCHK(hipMemcpy(prog.data(), tp.prog, tp.n * sizeof(TOp), hipMemcpyDeviceToHost));
       for (int rep = 0; rep < 2; ++rep)
-        if (tp.xl) tail_kernel<true, true><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
-        else tail_kernel<true, false><<<1, TAIL_THREADS, (size_t)tp.lds, s>>>(tp.prog, tp.n, tp.prog_lds, dst);
+        tail_launch<true>((tp.xl ? 1 : 0) | (tp.res ? 2 : 0), tp.prog, tp.n, tp.prog_lds, (size_t)tp.lds, dst, s);
       HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipMemcpy(st.data(), dst, (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(st.data(), dst, 2 * (tp.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
       (void)raw_free(dst);
       std::map<std::pair<int, int64_t>, std::pair<int, double>> acc;
       for (int k = 0; k < tp.n; ++k) {
@@ -5916,7 +6210,9 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         a.first += 1;
         a.second += (double)(st[k + 1] - st[k]) * 0.01;   // 100 MHz ticks -> us
       }
-      std::fprintf(stderr, "[mamg tail] program of %d ops: %.1f us\n", tp.n, (double)(st[tp.n] - st[0]) * 0.01);
+      const double us = (double)(st[tp.n] - st[0]) * 0.01, cyc = (double)(st[2 * tp.n + 1] - st[tp.n + 1]);
+      std::fprintf(stderr, "[mamg tail] program of %d ops: %.1f us, %.0f shader cycles (%.0f MHz)\n", tp.n, us, cyc,
+                   us > 0 ? cyc / us : 0.0);
       if (std::atoi(std::getenv("MAMG_TAIL_PROFILE")) > 1)
         for (int k = 0; k < tp.n; ++k)
           std::fprintf(stderr, "[mamg tail op] %d kind %d n %lld rows [%lld, %lld) vl %d lds %d us %.2f\n", k,

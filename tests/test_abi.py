@@ -272,7 +272,7 @@ def test_release_setup_cache_without_gpu(lib_built):
 
 
 PRODUCT_OPTIONS = ('MAMG_POST_K', 'MAMG_SELL_MIN_ROWS', 'MAMG_MSELL_MIN_ROWS', 'MAMG_TAIL_NODES', 'MAMG_TAIL_VL',
-                   'MAMG_TAIL_LDS', 'MAMG_HALF', 'MAMG_HALF_BANDS', 'MAMG_R_BANDS', 'MAMG_K_SORT', 'MAMG_K_COL16',
+                   'MAMG_TAIL_LDS', 'MAMG_TAIL_PROG_LDS', 'MAMG_TAIL_RES', 'MAMG_HALF', 'MAMG_HALF_BANDS', 'MAMG_R_BANDS', 'MAMG_K_SORT', 'MAMG_K_COL16',
                    'MAMG_FUSE_RBD',
                    'MAMG_CSR2BSR_FILL', 'MAMG_KREGION_TRIES', 'MAMG_KREGION_BUDGET_MS', 'MAMG_REHOME',
                    'MAMG_PRERESERVE_B_PER_NNZ', 'MAMG_POISON', 'MAMG_OVERLAP', 'MAMG_DIST_TEST', 'MAMG_SPGEMM_PAIR',

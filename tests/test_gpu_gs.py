@@ -138,11 +138,15 @@ def test_coarse_tail_equals_launches(lib_built, monkeypatch, dim, n, g, kw):
     A = s.scipy()
     r = mo.seeded_rhs(s.N)
     zs = []
-    for nodes in ('100000000', '0'):
+    # the whole cycle below level 1 in the tail, no tail, the default tail
+    # level with and without its register-resident operators (TOp.res)
+    for nodes, res in (('100000000', None), ('0', None), (None, None), (None, '0')):
         set_opt('MAMG_TAIL_NODES', nodes)
+        set_opt('MAMG_TAIL_RES', res)
         B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, **to_c(kw))
         zs.append(B * r)
         B.close()
-    assert rel(zs[0], zs[1]) < 1e-13
+    for z in zs[:1] + zs[2:]:
+        assert rel(z, zs[1]) < 1e-13
     h = mo.setup(A, mo.Params(num_functions=2, **kw), idofs=s.idofs)
     assert rel(zs[0], h.apply(r)) < 1e-10
