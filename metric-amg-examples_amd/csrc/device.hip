@@ -1230,38 +1230,40 @@ struct TRes {
   __device__ __forceinline__ int col(int k) const { return (int)((c[k >> 1] >> (16 * (k & 1))) & 0xffffu); }
 };
 
-// T_RLOAD: threads [rbase, rbase + n) take compact rows 0 .. n - 1 of the
-// op's matrix (ridx[2 j]: compact -> matrix row, ridx[2 j + 1]: the row's
-// first block in the LDS overflow; perm: matrix row -> node; W: the rows' GS
-// block inverses).  The LDS region at byte r0: one block inverse per thread
-// (TAIL_THREADS x 32 B), r1 overflow blocks' values (32 B), their columns (2 B)
+// T_RLOAD: every resident row of the program from an image built at plan
+// time (tail_res_plan): its blocks slot-major (val: dv4 [RES_RB][TAIL_THREADS],
+// col: packed 16-bit column pairs [RES_RB / 2][TAIL_THREADS]), its header
+// (ridx: length, node, first overflow block; [3][TAIL_THREADS]) and the LDS
+// region's bytes (b: n bytes -> LDS byte r0: the GS block inverses, one per
+// thread (TAIL_THREADS x 32 B), r1 overflow blocks' values (32 B), their
+// 16-bit columns).  One coalesced round trip instead of the chain row index
+// -> row pointer -> columns and values.
 __device__ __forceinline__ void tail_rload(const TOp& o, TRes& R, char* lds) {
-  const int t = (int)threadIdx.x, j = t - o.rbase;
-  if (j < 0 || j >= (int)o.n) return;
-  const TailMat M(o);
-  const int i = gload(o.ridx + 2 * j), ov = gload(o.ridx + 2 * j + 1);
-  const int p0 = M.P(i);
-  R.len = M.P(i + 1) - p0;
-  const int ovb = (int)o.r0 + 32 * TAIL_THREADS;
-  R.ovv = ovb + 32 * ov;
-  R.ovc = ovb + 32 * (int)o.r1 + 2 * ov;
-  R.gdo = (int)o.r0 + 32 * t;
-  const int nov = R.len > RES_RB ? (R.len - RES_RB + 3) / 4 * 4 : 0;   // padded to whole fours
-  for (int k = 0; k < nov; ++k) {
-    const bool h = RES_RB + k < R.len;
-    *(AS3 dv4*)(lds + R.ovv + 32 * k) = h ? M.V(p0 + RES_RB + k) : dv4{0.0, 0.0, 0.0, 0.0};
-    *(AS3 uint16_t*)(lds + R.ovc + 2 * k) = h ? (uint16_t)M.C(p0 + RES_RB + k) : (uint16_t)0;
+  const int t = (int)threadIdx.x;
+  {   // the LDS region first (fewer live registers than after the rows' loads)
+    const dv2* src = reinterpret_cast<const dv2*>(o.b);
+    AS3 dv2* dst = (AS3 dv2*)(lds + o.r0);
+    const int n16 = (int)(o.n / 16);
+    for (int i0 = t; i0 < n16; i0 += 2 * TAIL_THREADS) {   // two 16-byte loads in flight per lane
+      const bool h1 = i0 + TAIL_THREADS < n16;
+      const dv2 w0 = gload(src + i0), w1 = h1 ? gload(src + i0 + TAIL_THREADS) : dv2{0.0, 0.0};
+      dst[i0] = w0;
+      if (h1) dst[i0 + TAIL_THREADS] = w1;
+    }
   }
-  R.gI = o.perm ? M.perm(i) : i;
-  *(AS3 dv4*)(lds + R.gdo) = o.W ? M.W(i) : dv4{0.0, 0.0, 0.0, 0.0};
+  const dv4* iv = reinterpret_cast<const dv4*>(o.val);
+  const uint32_t* ic = reinterpret_cast<const uint32_t*>(o.col);
+  R.len = gload(o.ridx + t);
+  R.gI = gload(o.ridx + TAIL_THREADS + t);
+  const int ovs = gload(o.ridx + 2 * TAIL_THREADS + t);
 #pragma unroll
-  for (int k = 0; k < RES_RB; k += 2) {
-    const bool h0 = k < R.len, h1 = k + 1 < R.len;
-    const uint32_t c0 = h0 ? (uint32_t)M.C(p0 + k) : 0u, c1 = h1 ? (uint32_t)M.C(p0 + k + 1) : 0u;
-    R.c[k >> 1] = c0 | (c1 << 16);
-    R.v[k] = h0 ? M.V(p0 + k) : dv4{0.0, 0.0, 0.0, 0.0};
-    R.v[k + 1] = h1 ? M.V(p0 + k + 1) : dv4{0.0, 0.0, 0.0, 0.0};
-  }
+  for (int k = 0; k < RES_RB; ++k) R.v[k] = gload(iv + k * TAIL_THREADS + t);
+#pragma unroll
+  for (int k = 0; k < RES_RB / 2; ++k) R.c[k] = gload(ic + k * TAIL_THREADS + t);
+  const int ovb = (int)o.r0 + 32 * TAIL_THREADS;
+  R.ovv = ovb + 32 * ovs;
+  R.ovc = ovb + 32 * (int)o.r1 + 2 * ovs;
+  R.gdo = (int)o.r0 + 32 * t;
 }
 
 // a row of a T_BSR / T_GS op from the thread's resident row (tail_bsr's
@@ -4621,50 +4623,79 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
 // fit the workgroup.  A level with a multicolour GS layout holds it (Gb:
 // colour-permuted, each colour padded to 64-row slices); the level's other
 // ops on A (residual, scaling) then read Gb's row i at node perm(i) -- the
-// same blocks in the same order as A's row.  T_RLOAD ops that load the rows
-// are put in front.  tab: per compact row its matrix row and its first block
-// in the LDS overflow region (blocks past RES_RB; *nov in all), stored after
-// the program; a T_RLOAD's ridx holds (offset in tab + 1) until the caller
-// sets the device pointer, and its r0 / r1 the region's place once the LDS
-// plan is known.  Returns false when nothing is resident.
-bool tail_res_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, std::vector<int32_t>* tab, int64_t* nov) {
+// same blocks in the same order as A's row.  One T_RLOAD op in front loads
+// every resident row from an image (see tail_rload) built here from the
+// matrices; img holds it, and the T_RLOAD's val / col / ridx / b fields hold
+// (byte offset in img + 1) until the caller sets device pointers, its r0 / r1
+// the LDS region's place once the LDS plan is known.  Returns false when
+// nothing is resident.
+bool tail_res_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, std::vector<char>* img, int64_t* nov) {
   *nov = 0;
   if (const char* e = opt("MAMG_TAIL_RES"))
     if (std::atoi(e) == 0) return false;
-  std::vector<TOp> loads;
+  constexpr int T = TAIL_THREADS;
+  std::vector<dv4> iv((size_t)RES_RB * T, dv4{0.0, 0.0, 0.0, 0.0});
+  std::vector<uint32_t> ic((size_t)RES_RB / 2 * T, 0u);
+  std::vector<int32_t> hdr((size_t)3 * T, 0);
+  std::vector<dv4> gd(T, dv4{0.0, 0.0, 0.0, 0.0});
+  std::vector<dv4> ovv;
+  std::vector<uint16_t> ovc;
+  auto get = [](void* dst, const void* src, size_t bytes) {
+    if (hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess) return true;
+    (void)hipGetLastError();
+    return false;
+  };
   int rbase = 0;
   for (size_t ll = (size_t)l; ll < h->L.size(); ++ll) {
     const DLevel& L = h->L[ll];
     const bool hasg = L.gcs.size() > 1;
     const DBsr& M = hasg ? L.Gb : L.Ab;
-    if (!M.ptr || M.sell || M.half || M.split || M.nr <= 0) continue;
+    if (!M.ptr || M.sell || M.half || M.split || M.nr <= 0 || M.nc > 65536) continue;
+    std::vector<int32_t> pm(hasg ? M.nr : 0);
+    std::vector<int64_t> ptr(M.nr + 1);
+    if ((hasg && !get(pm.data(), L.gperm, M.nr * sizeof(int32_t))) ||
+        !get(ptr.data(), M.ptr, (M.nr + 1) * sizeof(int64_t)))
+      return false;
     std::vector<int64_t> comp(M.nr + 1, 0);   // rows before -> compact rows before
     std::vector<int32_t> rows;                // compact -> M row
-    std::vector<int32_t> pm(M.nr);
-    std::vector<int64_t> ptr(M.nr + 1);
-    if ((hasg && hipMemcpy(pm.data(), L.gperm, M.nr * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) ||
-        hipMemcpy(ptr.data(), M.ptr, (M.nr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
     for (int64_t i = 0; i < M.nr; ++i) {
       if (!hasg || pm[i] >= 0) rows.push_back((int32_t)i);
       comp[i + 1] = (int64_t)rows.size();
     }
     const int n = (int)rows.size();
-    if (rbase + n > TAIL_THREADS) continue;   // a deeper level may still fit
-    TOp ld;
-    ld.kind = T_RLOAD; ld.n = n; ld.rbase = rbase; ld.sym = M.sym ? 1 : 0; ld.nb = M.nb;
-    ld.ptr = M.ptr; ld.col = M.col; ld.val = M.val; ld.r0 = -1;
-    if (hasg) { ld.perm = L.gperm; ld.W = L.Gd; }
-    ld.ridx = reinterpret_cast<const int32_t*>((uintptr_t)(tab->size() + 1));
-    for (int32_t i : rows) {
-      const int64_t len = ptr[i + 1] - ptr[i];
-      tab->push_back(i);
-      tab->push_back((int32_t)*nov);
-      *nov += len > RES_RB ? (len - RES_RB + 3) / 4 * 4 : 0;   // whole fours (tail_res)
+    if (rbase + n > T) continue;   // a deeper level may still fit
+    const int64_t nb = M.nb;
+    std::vector<int32_t> col(nb);
+    std::vector<double> val((size_t)(M.sym ? 3 : 4) * nb);
+    std::vector<dv4> W(hasg ? M.nr : 0);
+    if (!get(col.data(), M.col, nb * sizeof(int32_t)) || !get(val.data(), M.val, val.size() * sizeof(double)) ||
+        (hasg && !get(W.data(), L.Gd, M.nr * sizeof(dv4))))
+      return false;
+    auto blk = [&](int64_t k) {
+      if (!M.sym) return dv4{val[4 * k], val[4 * k + 1], val[4 * k + 2], val[4 * k + 3]};
+      const double b = val[2 * nb + k];
+      return dv4{val[2 * k], b, b, val[2 * k + 1]};
+    };
+    for (int j = 0; j < n; ++j) {
+      const int t = rbase + j, i = rows[j];
+      const int64_t p0 = ptr[i], len = ptr[i + 1] - p0;
+      hdr[t] = (int)len;
+      hdr[T + t] = hasg ? pm[i] : i;
+      hdr[2 * T + t] = (int)ovv.size();
+      for (int k = 0; k < RES_RB && k < len; ++k) {
+        iv[(size_t)k * T + t] = blk(p0 + k);
+        ic[(size_t)(k / 2) * T + t] |= (uint32_t)col[p0 + k] << (16 * (k & 1));
+      }
+      if (len > RES_RB) {   // whole fours (tail_res), zero-padded
+        const int64_t nk = (len - RES_RB + 3) / 4 * 4;
+        for (int64_t k = 0; k < nk; ++k) {
+          const bool in = RES_RB + k < len;
+          ovv.push_back(in ? blk(p0 + RES_RB + k) : dv4{0.0, 0.0, 0.0, 0.0});
+          ovc.push_back(in ? (uint16_t)col[p0 + RES_RB + k] : (uint16_t)0);
+        }
+      }
+      if (hasg) gd[t] = W[i];
     }
-    loads.push_back(ld);
     for (TOp& t : *prog) {
       if (t.kind == T_GS && hasg && t.ptr == L.Gb.ptr) {
         t.res = 1; t.rbase = rbase; t.r0 = comp[t.r0]; t.r1 = comp[t.r1];
@@ -4676,8 +4707,30 @@ bool tail_res_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, std::ve
     }
     rbase += n;
   }
-  if (loads.empty()) return false;
-  prog->insert(prog->begin(), loads.begin(), loads.end());
+  if (rbase == 0) return false;
+  *nov = (int64_t)ovv.size();
+  // the image: values, columns, header, then the LDS region's bytes (block
+  // inverses, overflow values, overflow columns padded to 16 B)
+  auto put = [&](const void* p, size_t bytes) {
+    const size_t off = img->size();
+    img->insert(img->end(), static_cast<const char*>(p), static_cast<const char*>(p) + bytes);
+    img->resize((img->size() + 15) / 16 * 16, 0);
+    return off;
+  };
+  TOp ld;
+  ld.kind = T_RLOAD; ld.r0 = -1; ld.r1 = *nov;
+  const size_t ov = put(iv.data(), iv.size() * sizeof(dv4));
+  const size_t oc = put(ic.data(), ic.size() * sizeof(uint32_t));
+  const size_t oh = put(hdr.data(), hdr.size() * sizeof(int32_t));
+  const size_t og = put(gd.data(), gd.size() * sizeof(dv4));
+  if (!ovv.empty()) put(ovv.data(), ovv.size() * sizeof(dv4));
+  if (!ovc.empty()) put(ovc.data(), ovc.size() * sizeof(uint16_t));
+  ld.n = (int64_t)(img->size() - og);   // the LDS region's bytes (a multiple of 16)
+  ld.val = reinterpret_cast<const double*>((uintptr_t)ov + 1);
+  ld.col = reinterpret_cast<const int32_t*>((uintptr_t)oc + 1);
+  ld.ridx = reinterpret_cast<const int32_t*>((uintptr_t)oh + 1);
+  ld.b = reinterpret_cast<const double*>((uintptr_t)og + 1);
+  prog->insert(prog->begin(), ld);
   return true;
 }
 
@@ -4696,10 +4749,10 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       if (!to_tail(sub[k], &prog[k])) return false;
       bytes += sub[k].bytes;
     }
-    std::vector<int32_t> tab;
+    std::vector<char> img;
     int64_t nov = 0;
     const std::vector<TOp> plain = prog;
-    bool res = tail_res_plan(h, l, &prog, &tab, &nov);
+    bool res = tail_res_plan(h, l, &prog, &img, &nov);
     int64_t lds = tail_lds_plan(h, l, &prog);
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
@@ -4709,7 +4762,9 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     int prog_lds = -1;
     int64_t pbytes = (int64_t)(prog.size() * sizeof(TOp));
     const char* pl_opt = opt("MAMG_TAIL_PROG_LDS");
-    const bool prog_in_lds = pl_opt ? std::atoi(pl_opt) != 0 : true;
+    // default: scalar loads (s_load of a uniform descriptor: 795 vs 1262
+    // cycles per empty op)
+    const bool prog_in_lds = pl_opt ? std::atoi(pl_opt) != 0 : false;
     if (lds > 0 && prog_in_lds) {
       const int64_t off = (lds + 15) / 16 * 16;
       if (off + pbytes <= TAIL_LDS_MAX) {
@@ -4721,14 +4776,17 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     // both; without room for it (or for the program) the tail keeps its
     // operators in global memory
     if (res) {
-      const int64_t off = (lds + 15) / 16 * 16, need = 32 * TAIL_THREADS + 34 * nov;
+      int64_t need = 0;   // the T_RLOAD's LDS region bytes
+      for (const TOp& t : prog)
+        if (t.kind == T_RLOAD) need = t.n;
+      const int64_t off = (lds + 15) / 16 * 16;
       if (lds > 0 && off + need <= TAIL_LDS_MAX) {
         for (TOp& t : prog)
           if (t.kind == T_RLOAD) { t.r0 = off; t.r1 = nov; }
         lds = off + need;
       } else {
         res = false;
-        tab.clear();
+        img.clear();
         prog = plain;
         lds = tail_lds_plan(h, l, &prog);
         prog_lds = -1;
@@ -4743,13 +4801,17 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
       }
     }
     void* d = nullptr;
-    const size_t tbytes = tab.size() * sizeof(int32_t);
-    if (raw_malloc(&d, (size_t)pbytes + tbytes, "long") != hipSuccess) { (void)hipGetLastError(); return false; }
-    const int32_t* dtab = reinterpret_cast<const int32_t*>(static_cast<char*>(d) + pbytes);
+    const int64_t ioff = (pbytes + 15) / 16 * 16;
+    const size_t tbytes = img.size();
+    if (raw_malloc(&d, (size_t)ioff + tbytes, "long") != hipSuccess) { (void)hipGetLastError(); return false; }
+    char* dimg = static_cast<char*>(d) + ioff;
+    auto fix = [&](auto*& f) {
+      if (f) f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dimg + ((uintptr_t)f - 1));
+    };
     for (TOp& t : prog)
-      if (t.ridx) t.ridx = dtab + ((uintptr_t)t.ridx - 1);
+      if (t.kind == T_RLOAD) { fix(t.val); fix(t.col); fix(t.ridx); fix(t.b); }
     if (hipMemcpy(d, prog.data(), prog.size() * sizeof(TOp), hipMemcpyHostToDevice) != hipSuccess ||
-        (tbytes && hipMemcpy(static_cast<char*>(d) + pbytes, tab.data(), tbytes, hipMemcpyHostToDevice) != hipSuccess)) {
+        (tbytes && hipMemcpy(dimg, img.data(), tbytes, hipMemcpyHostToDevice) != hipSuccess)) {
       (void)hipGetLastError();
       (void)raw_free(d);
       return false;
@@ -6188,6 +6250,35 @@ int dev_time_apply(DeviceHandle* h, const double* d_r, double* d_z, int reps, in
         std::fprintf(stderr, "[mamg tail] %d empty ops, program in %s: %.3f us/op, %.0f cycles/op\n", nn,
                      pl == 0 ? "LDS" : "global", (double)(st[nn] - st[0]) * 0.01 / nn,
                      (double)(st[2 * nn + 1] - st[nn + 1]) / nn);
+      }
+      // without stamps: event time of 200 vs 2000 empty ops, 512 and 64 threads
+      {
+        const int nb = 2000;
+        std::vector<TOp> nq(nb);
+        for (auto& t : nq) { t.kind = T_ZERO; t.n = 0; }
+        TOp* dq = nullptr;
+        HIPCHK(raw_malloc((void**)&dq, nb * sizeof(TOp), "tmp"));
+        HIPCHK(hipMemcpy(dq, nq.data(), nb * sizeof(TOp), hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        for (int th : {TAIL_THREADS, 64}) {
+          float tt[2] = {0.f, 0.f};
+          for (int v = 0; v < 2; ++v) {
+            const int cnt = v ? nb : nn;
+            tail_kernel<false, false, false><<<1, th, 0, s>>>(dq, cnt, -1, nullptr);
+            HIPCHK(hipEventRecord(e0, s));
+            for (int rep = 0; rep < 10; ++rep) tail_kernel<false, false, false><<<1, th, 0, s>>>(dq, cnt, -1, nullptr);
+            HIPCHK(hipEventRecord(e1, s));
+            HIPCHK(hipEventSynchronize(e1));
+            HIPCHK(hipEventElapsedTime(&tt[v], e0, e1));
+          }
+          std::fprintf(stderr, "[mamg tail] empty op without stamps, %d threads: %.3f us/op\n", th,
+                       1e3 * (tt[1] - tt[0]) / 10.0 / (nb - nn));
+        }
+        HIPCHK(hipEventDestroy(e0));
+        HIPCHK(hipEventDestroy(e1));
+        (void)raw_free(dq);
       }
       (void)raw_free(dp);
       (void)raw_free(dst);

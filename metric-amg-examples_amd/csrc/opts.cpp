@@ -24,7 +24,7 @@ constexpr const char* kNames[] = {
     "MAMG_TAIL_NODES",            // coarse tail: first level with at most this many nodes (auto)
     "MAMG_TAIL_VL",               // coarse tail: lanes per row cap (4)
     "MAMG_TAIL_LDS",              // coarse tail: LDS program size (auto)
-    "MAMG_TAIL_PROG_LDS",         // 1: coarse tail's op descriptors copied into LDS; 0: scalar loads
+    "MAMG_TAIL_PROG_LDS",         // 1: coarse tail's op descriptors copied into LDS; 0: scalar loads (default)
     "MAMG_TAIL_RES",              // 1: coarse tail's operators held in registers, one row per thread
     "MAMG_HALF",                  // 1: half-symmetric level-0 A; 0: SELL-64
     "MAMG_HALF_BANDS",            // 1: plane-band schedule of the half-symmetric kernel
