@@ -4521,7 +4521,7 @@ constexpr int64_t TAIL_LDS_MAX = 160 * 1024 - 1024;   // gfx950: 160 KB per work
 // to tagged LDS offsets, vectors read before written are copied in first and
 // written ones copied out last.  Returns the dynamic LDS bytes, or 0 (program
 // unchanged: global vectors) when the plan exceeds the LDS.
-int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
+int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, int64_t reserve = 0) {
   if (const char* e = opt("MAMG_TAIL_LDS"))
     if (std::atoi(e) == 0) return 0;
   struct Vec {
@@ -4567,7 +4567,7 @@ int64_t tail_lds_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog) {
   int64_t off = 0;
   for (Vec* v : order) {
     const int64_t sz = (v->n * 8 + 15) / 16 * 16;
-    if (off + sz > TAIL_LDS_MAX) continue;
+    if (off + sz > TAIL_LDS_MAX - reserve) continue;
     v->lds = true;
     v->off = off;
     off += sz;
@@ -4753,7 +4753,10 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
     int64_t nov = 0;
     const std::vector<TOp> plain = prog;
     bool res = tail_res_plan(h, l, &prog, &img, &nov);
-    int64_t lds = tail_lds_plan(h, l, &prog);
+    int64_t region = 0;   // the resident rows' LDS region, kept free of vectors
+    for (const TOp& t : prog)
+      if (t.kind == T_RLOAD) region = t.n;
+    int64_t lds = tail_lds_plan(h, l, &prog, region + 16);
     bool xl = lds > 0;   // every gathered x in LDS: the ds_read variant of the kernel
     for (const TOp& t : prog)
       if ((t.kind == T_BSR || t.kind == T_GS) && !((uintptr_t)t.x & 1)) xl = false;
