@@ -25,9 +25,13 @@ def main():
                     help='ref: the verbatim preset; patch: mi355x_patch (node-block Jacobi below level 0)')
     ap.add_argument('--check', type=int, default=0,
                     help='n > 0: compare the first n patch inverses with a float64 numpy inverse')
+    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE: a layout switch (mamg_set_option)')
     args = ap.parse_args()
     import torch
     import metric_amg_examples_amd as M
+    for kv in args.opt:
+        k, v = kv.split('=', 1)
+        M._lib.set_option(k, v)
     n = M.problems.finest_n(3, args.nrefs)
     s = M.problems.bidomain(3, n, 1e6)
     A = s.scipy()

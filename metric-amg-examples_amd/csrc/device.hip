@@ -1924,6 +1924,70 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
   }
 }
 
+// ---- patch matrices through LDS (round 6): the assembly and the packed
+// store of the patch inverse kernels.  A patch's 32 x 32 matrix (zero past
+// d, the identity on the padded diagonal when `pad`) sits column-major with
+// stride PATCH_LD doubles (33: the tile reads of patch_inv3_kernel hit 32
+// banks).
+constexpr int PATCH_LD = 33;
+
+// Assembly by rows: lane a (< 16) of the patch's lane group takes row node
+// a (Ja = the centre row's a-th column), loads Ja's <= 16 keys at once, finds
+// every patch node's key among them by comparisons in registers, then loads
+// the found blocks at once: three dependent loads instead of one five-step
+// binary search per (row, column) pair.  A pair absent from Ja's row stays 0.
+// The values are copies: the assembled matrix is the one the searches built.
+__device__ __forceinline__ void patch_assemble(double* S, int sub, int nl, int64_t q0, int m, bool pad,
+                                               const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                               const int32_t* __restrict__ gcol, const dv4* __restrict__ val) {
+  const int d = 2 * m;
+  for (int k = sub; k < 32 * PATCH_LD; k += nl) {
+    const int j = k / PATCH_LD, r = k - j * PATCH_LD;
+    S[k] = (pad && r == j && j >= d) ? 1.0 : 0.0;
+  }
+  if (sub >= m) return;
+  const int32_t Ja = col[q0 + sub];
+  const int64_t p0 = ptr[Ja];
+  const int n = (int)(ptr[Ja + 1] - p0);
+  int32_t kr[PATCH_MAX_NODES], kb[PATCH_MAX_NODES];
+#pragma unroll
+  for (int k = 0; k < PATCH_MAX_NODES; ++k) {
+    kr[k] = k < n ? gcol[p0 + k] : -1;
+    kb[k] = k < m ? gcol[q0 + k] : -2;
+  }
+  int pos[PATCH_MAX_NODES];
+#pragma unroll
+  for (int b = 0; b < PATCH_MAX_NODES; ++b) {
+    int q = -1;
+#pragma unroll
+    for (int k = 0; k < PATCH_MAX_NODES; ++k) q = kr[k] == kb[b] ? k : q;
+    pos[b] = q;
+  }
+  dv4 v[PATCH_MAX_NODES];
+#pragma unroll
+  for (int b = 0; b < PATCH_MAX_NODES; ++b) v[b] = pos[b] >= 0 ? val[p0 + pos[b]] : dv4{0.0, 0.0, 0.0, 0.0};
+  const int a2 = 2 * sub;
+#pragma unroll
+  for (int b = 0; b < PATCH_MAX_NODES; ++b)
+    if (pos[b] >= 0) {
+      double* c0 = S + (2 * b) * PATCH_LD + a2;
+      double* c1 = c0 + PATCH_LD;
+      c0[0] = v[b].x; c1[0] = v[b].y; c0[1] = v[b].z; c1[1] = v[b].w;
+    }
+}
+
+// the packed upper triangle (column j: rows 0 .. j, at j (j + 1) / 2) of
+// sign * the LDS matrix, written by nl lanes with consecutive addresses
+__device__ __forceinline__ void patch_store(const double* S, int sub, int nl, int d, double sign, double* __restrict__ Up) {
+  const int nt = d * (d + 1) / 2;
+  for (int k = sub; k < nt; k += nl) {
+    int j = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
+    j += (j + 1) * (j + 2) / 2 <= k ? 1 : 0;
+    j -= j * (j + 1) / 2 > k ? 1 : 0;
+    Up[k] = sign * S[j * PATCH_LD + (k - j * (j + 1) / 2)];
+  }
+}
+
 // Patch inverses, two patches per wave (round 6): the same
 // operations on the same values as patch_inv_kernel, so the same bits, with
 // half the instructions per patch.
@@ -1950,44 +2014,22 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
                                                          const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
                                                          int* bad) {
 #pragma clang fp contract(off)
+  __shared__ double sm[8][32 * PATCH_LD];   // per patch (two per wave)
   const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
-  const int64_t i = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+  const int ps = (threadIdx.x >> 6) * 2 + (lane >> 5);
+  const int64_t i = (int64_t)blockIdx.x * 8 + ps;
   const bool live = i < np;
   const int32_t I = live ? perm[i] : 0;
   const int64_t q0 = ptr[I];
   const int m = live ? (int)(ptr[I + 1] - q0) : 0;
   const int d = 2 * m;
+  double* S = sm[ps];
+  // assembly by rows into LDS (patch_assemble), then lane hl reads column hl
+  patch_assemble(S, hl, 32, q0, m, false, ptr, col, gcol, val);
+  __syncthreads();
   double M[2 * PATCH_MAX_NODES];
 #pragma unroll
-  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = 0.0;
-  if (hl < d) {
-    const int32_t Jb = gcol[q0 + (hl >> 1)];
-    const int g = hl & 1;
-    // each row's lower bound of Jb by a branch-free 5-step binary search
-    // (rows of <= 16 blocks), every load in bounds, so the rows' searches
-    // form one straight-line block and their loads overlap
-#pragma unroll
-    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
-      const bool va = a < m;
-      const int32_t Ja = va ? col[q0 + a] : I;
-      const int64_t p0 = ptr[Ja];
-      const int n = va ? (int)(ptr[Ja + 1] - p0) : 0;
-      int64_t b = p0;
-      int l = n;
-#pragma unroll
-      for (int st = 0; st < 5; ++st) {
-        const int h = l >> 1;
-        const bool lt = gcol[l > 0 ? b + h : p0] < Jb;
-        b = (l > 0 && lt) ? b + h + 1 : b;
-        l = l > 0 ? (lt ? l - h - 1 : h) : 0;
-      }
-      if (va && b < p0 + n && gcol[b] == Jb) {
-        const dv4 v = val[b];
-        M[2 * a] = g ? v.y : v.x;
-        M[2 * a + 1] = g ? v.w : v.z;
-      }
-    }
-  }
+  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = hl < d ? S[hl * PATCH_LD + r] : 0.0;
   bool ok = true;
 #pragma clang loop unroll(full)
   for (int k = 0; k < 2 * PATCH_MAX_NODES; ++k) {
@@ -2008,19 +2050,164 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
     if (upd) M[k] = mk;
   }
   if (!ok && hl == 0) atomicOr(bad, 1);
-  if (live && ok && hl < d) {
-    double* Up = U + i * ustride + hl * (hl + 1) / 2;
+  // the inverse's columns back into LDS, then the packed upper triangle with
+  // consecutive addresses (column hl's rows 0 .. hl are the inverse's U(:, hl))
+  __syncthreads();
+  if (hl < d) {
 #pragma unroll
-    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r)
-      if (r <= hl) Up[r] = M[r];
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) S[hl * PATCH_LD + r] = M[r];
   }
+  __syncthreads();
+  if (live && ok) patch_store(S, hl, 32, d, 1.0, U + i * ustride);
 }
 
-// MAMG_PATCH_INV=1: the round-5 kernel (one patch per wave; A/B and the
-// bitwise test of the two, tests/test_gpu_patch.py)
-bool patch_inv_v1() {
+// Patch inverses on the matrix cores (round 6):
+// one patch per wave, the 32 x 32 (zero-padded to the identity past d)
+// patch matrix as four 16 x 16 f64 tiles in the v_mfma_f64_16x16x4 C/D
+// layout (lane l, register r: row 16a + (l >> 4) + 4r, column 16b + (l & 15)),
+// inverted by the symmetric block sweep on 4 x 4 pivot blocks K:
+//   P = M(K, K), R = M(K, :), S = P^-1 R               (one MFMA per tile column)
+//   M(i, j) -= S(:, i)^T R(:, j)  for all i, j          (four MFMAs: the A operand
+//                                                        is S itself, the B operand R
+//                                                        itself -- no data movement)
+//   M(K, :) = S, M(:, K) = S^T (ds_bpermute), M(K, K) = -P^-1,
+// which leaves M = -A_p^-1 after the eight blocks (Goodnight's sweep;
+// symmetry is what makes the column panel S^T, so the row panel alone feeds
+// both operands).  A_p is SPD, so no pivoting: a non-positive pivot of a 4 x 4
+// block sets *bad as the scalar kernels do.  Assembly as patch_inv2_kernel
+// (lane j < 32 builds column j), then an LDS transpose into the tile layout.
+// The rounding differs from the scalar Gauss-Jordan: the inverses equal
+// patch_inv2_kernel's to ~1e-14 relative (tests/test_gpu_patch.py).
+// PART (diagnosis build only, MAMG_PATCH_INV 4 / 5): 1 = assembly and
+// stores without the sweep, 2 = the sweep on the identity without assembly
+template <int PART = 0>
+__global__ __launch_bounds__(256) void patch_inv3_kernel(int64_t np, const int32_t* __restrict__ perm,
+                                                         const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
+                                                         const int32_t* __restrict__ gcol,
+                                                         const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
+                                                         int* bad) {
+  constexpr int LD = PATCH_LD;
+  __shared__ double sm[4][32 * LD];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  const bool live = i < np;
+  const int32_t I = live ? perm[i] : 0;
+  const int64_t q0 = ptr[I];
+  const int m = live ? (int)(ptr[I + 1] - q0) : 0;
+  const int d = 2 * m;
+  double* S = sm[w];
+  if (PART == 2) {   // diagnosis: the identity
+    for (int k = lane; k < 32 * LD; k += 64) S[k] = (k % LD == k / LD) ? 1.0 : 0.0;
+  } else {
+    patch_assemble(S, lane, 64, q0, m, true, ptr, col, gcol, val);
+  }
+  __syncthreads();
+  dv4 T[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[a][b][r] = S[(16 * b + lc) * LD + 16 * a + lr + 4 * r];
+  bool ok = true;
+#pragma unroll
+  for (int K = 0; K < (PART == 1 ? 0 : 8); ++K) {
+    const int t = K >> 2, rr = K & 3;
+    // the pivot block, broadcast (its 16 entries sit in lanes 16 kk + 4 rr + c of T[t][t][rr])
+    double q[4][4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) q[kk][c] = readlane_f64(T[t][t][rr], 16 * kk + 4 * rr + c);
+    // its inverse by the scalar sweep (q <- -P^-1), uniform in every lane
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const double dp = q[p][p];
+      ok = ok && dp > 0.0;
+      const double inv = 1.0 / dp;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (a != p && c != p) q[a][c] -= q[a][p] * q[p][c] * inv;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        if (a != p) { q[a][p] *= inv; q[p][a] *= inv; }
+      q[p][p] = -inv;
+    }
+    // A operand of S = P^-1 R: lane l holds (P^-1)(l & 15, l >> 4) for (l & 15) < 4, else 0
+    double pa = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pa = (lc == a && lr == c) ? -q[a][c] : pa;
+    const double R0 = T[t][0][rr], R1 = T[t][1][rr];
+    const dv4 z = {0.0, 0.0, 0.0, 0.0};
+    const double S0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, R0, z, 0, 0, 0)[0];   // S(lr, lc) of column tile 0
+    const double S1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, R1, z, 0, 0, 0)[0];
+    // M -= S^T R on every tile (rows and columns K are rewritten below)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const double sa = a ? -S1 : -S0;
+      T[a][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa, R0, T[a][0], 0, 0, 0);
+      T[a][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa, R1, T[a][1], 0, 0, 0);
+    }
+    // row panel K <- S (the same lanes), column panel K <- S^T
+    T[t][0][rr] = S0;
+    T[t][1][rr] = S1;
+    const bool inK = lc >= 4 * rr && lc < 4 * rr + 4;
+    const int kk = inK ? lc - 4 * rr : 0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double v = bperm_f64(a ? S1 : S0, 16 * kk + lr + 4 * r);
+        if (inK) T[a][t][r] = v;
+      }
+    // pivot block K <- -P^-1 (= q)
+    double qk = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) qk = (lr == a && kk == c) ? q[a][c] : qk;
+    if (inK) T[t][t][rr] = qk;
+  }
+  if (!ok && lane == 0 && live) atomicOr(bad, 1);
+  // M = -A_p^-1: the tiles back into LDS, then the packed upper triangle of -M
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(16 * b + lc) * LD + 16 * a + lr + 4 * r] = T[a][b][r];
+  __syncthreads();
+  if (live && ok) patch_store(S, lane, 64, d, -1.0, U + i * ustride);
+}
+
+// MAMG_PATCH_INV: 1 the round-5 kernel (one patch per wave), 2 two patches
+// per wave (bitwise the same), default 3 the matrix-core block sweep
+int patch_inv_version() {
   const char* e = opt("MAMG_PATCH_INV");
-  return e && std::atoi(e) == 1;
+  const int v = e ? std::atoi(e) : 3;
+#if MAMG_DIAG
+  if (v == 4 || v == 5) return v;
+#endif
+  return v == 1 || v == 2 ? v : 3;
+}
+
+void launch_patch_inv(int64_t np, const int32_t* perm, const int64_t* ptr, const int32_t* col, const int32_t* gcol,
+                      const dv4* val, int64_t ustride, double* U, int* bad) {
+  if (np <= 0) return;
+  switch (patch_inv_version()) {
+    case 1: patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+    case 2: patch_inv2_kernel<<<(unsigned)((np + 7) / 8), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+#if MAMG_DIAG
+    case 4: patch_inv3_kernel<1><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+    case 5: patch_inv3_kernel<2><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+#endif
+    default: patch_inv3_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+  }
 }
 
 // One colour of a patch sweep, one wave per patch (4 per workgroup), in place
@@ -4061,12 +4248,7 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
-  if (patch_inv_v1())
-    patch_inv_kernel<<<(unsigned)((nr + 3) / 4), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
-                                                         flags + 2);
-  else
-    patch_inv2_kernel<<<(unsigned)((nr + 7) / 8), 256>>>(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu,
-                                                          flags + 2);
+  launch_patch_inv(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu, flags + 2);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
@@ -7443,10 +7625,7 @@ int dist_patches(DistHandle* h, const DevMat& A0d, const DistLevel& P, DDLevel* 
   int* bad = nullptr;
   if ((rc = T.alloc(&bad, 1, err))) return rc;
   HIPCHK(dev_memset(bad, 0, sizeof(int)));
-  if (np && patch_inv_v1())
-    patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
-  else if (np)
-    patch_inv2_kernel<<<(unsigned)((np + 7) / 8), 256>>>(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
+  launch_patch_inv(np, L.pperm, L.Sptr, L.Scol, D->Sgcol, L.Sval, L.pus, L.pu, bad);
   HIPCHK(hipGetLastError());
   int hb = 0;
   HIPCHK(hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost));

@@ -45,7 +45,7 @@ constexpr const char* kNames[] = {
     "MAMG_SPGEMM_STAGE_STRIDE",   // staging stride cap (128)
     "MAMG_MIS_STAGED",            // 1: MIS-2 maxima over staged rows
     "MAMG_UPLOAD_THREADS",        // host threads copying A0 (2)
-    "MAMG_PATCH_INV",             // 1: node-patch inverses one patch per wave (round 5); 2: two per wave
+    "MAMG_PATCH_INV",             // node-patch inverses: 1 one patch per wave (round 5), 2 two per wave, 3 matrix cores (default)
 };
 
 struct Table {

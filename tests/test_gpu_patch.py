@@ -80,13 +80,17 @@ def test_patch_apply_matches_oracle(lib_built, dim, n, g, kw, setup):
 @pytest.mark.parametrize('dim,n,g', [(3, 16, 1e6), (2, 64, 1e4), (3, 8, 1e10), (3, 16, 1e10)])
 def test_patch_pcg_matches_oracle(lib_built, dim, n, g):
     """Device PCG with the node-patch profile against the oracle's PCG:
-    the same iteration count; every residual sqrt(<r, Br>) within rtol 1e-6,
-    or within 1e-12 of the first residual (fp64 rounding of the Krylov
-    recurrences: at gamma = 1e10 the 4th residual, 1e-9 of the first, agrees
-    to 4e-6 relative, i.e. 6e-14 absolute = 3e-15 of the first); the true
-    relative residual ||b - Ax|| / ||b|| of both solutions at the level the
-    oracle's own solution reaches, and the solutions equal in the energy of
-    A to 1e-6 of b."""
+    the same iteration count; every residual sqrt(<r, Br>) within rtol 1e-6
+    (gamma <= 1e6) or 1e-4 (gamma = 1e10), or within 1e-12 of the first
+    residual; the true relative residual ||b - Ax|| / ||b|| of both solutions
+    at the level the oracle's own solution reaches, and the solutions equal in
+    the energy of A to 1e-6 of b.  Why 1e-4 at gamma = 1e10: the patch
+    matrices' condition numbers are ~gamma, so any two inverses computed in a
+    different operation order (the oracle's scalar Gauss-Jordan, the device's
+    matrix-core block sweep, patch_inv3_kernel) differ by ~gamma * eps = 1e-6
+    relative, and the Krylov residuals inherit it (measured 8.7e-6 at the
+    4th residual); the scalar kernels (MAMG_PATCH_INV=1, 2) repeat the
+    oracle's order and stay within 1e-6 (round 5)."""
     M = _mamg()
     s = M.problems.bidomain(dim, n, g)
     A = s.scipy()
@@ -100,7 +104,8 @@ def test_patch_pcg_matches_oracle(lib_built, dim, n, g):
     assert len(solver.residuals) == len(ref.residuals)
     res, rres = np.asarray(solver.residuals), np.asarray(ref.residuals)
     assert res[-1] <= 1e-8 and rres[-1] <= 1e-8
-    assert np.allclose(res, rres, rtol=1e-6, atol=1e-12 * rres[0]), np.abs(res - rres) / rres
+    rtol = 1e-6 if g <= 1e6 else 1e-4
+    assert np.allclose(res, rres, rtol=rtol, atol=1e-12 * rres[0]), np.abs(res - rres) / rres
     bn = np.linalg.norm(b)
     rel_true, rel_true_o = np.linalg.norm(b - A @ x) / bn, np.linalg.norm(b - A @ ref.x) / bn
     assert rel_true <= max(2.0 * rel_true_o, 1e-12), (rel_true, rel_true_o)
@@ -266,3 +271,36 @@ def test_patch_inverse_kernels_bitwise(lib_built, dim, n):
             B.close()
         assert torch.equal(zs[0], zs[1])
         assert xs[0][1] == xs[1][1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dim,n', [(3, 8), (3, 16), (2, 32)])
+def test_patch_inverse_matrix_cores(lib_built, dim, n):
+    """the patch inverses by the f64 matrix-core block sweep
+    (patch_inv3_kernel, MAMG_PATCH_INV=3, the default) against the scalar
+    Gauss-Jordan kernel (MAMG_PATCH_INV=2): a different rounding, so not
+    bitwise -- the applies agree to 1e-10, the PCG takes the same
+    iterations and its residual history agrees to 1e-6; the oracle parity of
+    the default path is test_patch_apply_matches_oracle."""
+    import torch
+    M = _mamg()
+    s = M.problems.bidomain(dim, n, 1e6)
+    A = s.scipy()
+    r = torch.as_tensor(mo.seeded_rhs(s.N)).cuda()
+    for prm in (dict(num_functions=2, Schwarz_type=PATCHES),
+                dict(parameters=M.parameters.parameters_metric_schwarz)):
+        zs, hs = [], []
+        for v in ('2', '3'):
+            set_opt('MAMG_PATCH_INV', v)
+            B = M.MetricAMG(A, s.W, idofs=s.idofs, setup='gpu', **prm)
+            assert B.level_format(0)['patches']
+            zs.append(B.matvec(r).clone())
+            B._Aop = A
+            cg = M.ConjGrad(A, precond=B, tolerance=1e-8, maxiter=500)
+            cg.solve_device(r)
+            hs.append(list(cg.residuals))
+            torch.cuda.synchronize()
+            B.close()
+        assert float(torch.linalg.norm(zs[0] - zs[1]) / torch.linalg.norm(zs[0])) < 1e-10
+        assert len(hs[0]) == len(hs[1])
+        assert all(abs(a - b) <= 1e-6 * abs(a) for a, b in zip(hs[0], hs[1]))
