@@ -1931,48 +1931,52 @@ __global__ __launch_bounds__(256) void patch_inv_kernel(int64_t np, const int32_
 // banks).
 constexpr int PATCH_LD = 33;
 
-// Assembly by rows: lane a (< 16) of the patch's lane group takes row node
-// a (Ja = the centre row's a-th column), loads Ja's <= 16 keys at once, finds
-// every patch node's key among them by comparisons in registers, then loads
+// Assembly by rows: the patch's nl lanes take its row nodes, L = nl / 16
+// lanes per row node a (Ja = the centre row's a-th column) and the patch
+// nodes b = q, q + L, .. of lane q; each lane loads Ja's <= 16 keys at once,
+// finds its nodes' keys among them by comparisons in registers, then loads
 // the found blocks at once: three dependent loads instead of one five-step
 // binary search per (row, column) pair.  A pair absent from Ja's row stays 0.
 // The values are copies: the assembled matrix is the one the searches built.
-__device__ __forceinline__ void patch_assemble(double* S, int sub, int nl, int64_t q0, int m, bool pad,
+template <int L>
+__device__ __forceinline__ void patch_assemble(double* S, int sub, int q0i, int64_t q0, int m, bool pad,
                                                const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
                                                const int32_t* __restrict__ gcol, const dv4* __restrict__ val) {
+  (void)q0i;
+  constexpr int nl = 16 * L, NB = PATCH_MAX_NODES / L;
   const int d = 2 * m;
   for (int k = sub; k < 32 * PATCH_LD; k += nl) {
     const int j = k / PATCH_LD, r = k - j * PATCH_LD;
     S[k] = (pad && r == j && j >= d) ? 1.0 : 0.0;
   }
-  if (sub >= m) return;
-  const int32_t Ja = col[q0 + sub];
+  const int a = sub / L, q = sub % L;
+  if (a >= m) return;
+  const int32_t Ja = col[q0 + a];
   const int64_t p0 = ptr[Ja];
   const int n = (int)(ptr[Ja + 1] - p0);
-  int32_t kr[PATCH_MAX_NODES], kb[PATCH_MAX_NODES];
+  int32_t kr[PATCH_MAX_NODES], kb[NB];
 #pragma unroll
-  for (int k = 0; k < PATCH_MAX_NODES; ++k) {
-    kr[k] = k < n ? gcol[p0 + k] : -1;
-    kb[k] = k < m ? gcol[q0 + k] : -2;
+  for (int k = 0; k < PATCH_MAX_NODES; ++k) kr[k] = k < n ? gcol[p0 + k] : -1;
+#pragma unroll
+  for (int t = 0; t < NB; ++t) kb[t] = q + L * t < m ? gcol[q0 + q + L * t] : -2;
+  int pos[NB];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    int x = -1;
+#pragma unroll
+    for (int k = 0; k < PATCH_MAX_NODES; ++k) x = kr[k] == kb[t] ? k : x;
+    pos[t] = x;
   }
-  int pos[PATCH_MAX_NODES];
+  dv4 v[NB];
 #pragma unroll
-  for (int b = 0; b < PATCH_MAX_NODES; ++b) {
-    int q = -1;
+  for (int t = 0; t < NB; ++t) v[t] = pos[t] >= 0 ? val[p0 + pos[t]] : dv4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < PATCH_MAX_NODES; ++k) q = kr[k] == kb[b] ? k : q;
-    pos[b] = q;
-  }
-  dv4 v[PATCH_MAX_NODES];
-#pragma unroll
-  for (int b = 0; b < PATCH_MAX_NODES; ++b) v[b] = pos[b] >= 0 ? val[p0 + pos[b]] : dv4{0.0, 0.0, 0.0, 0.0};
-  const int a2 = 2 * sub;
-#pragma unroll
-  for (int b = 0; b < PATCH_MAX_NODES; ++b)
-    if (pos[b] >= 0) {
-      double* c0 = S + (2 * b) * PATCH_LD + a2;
+  for (int t = 0; t < NB; ++t)
+    if (pos[t] >= 0) {
+      const int b = q + L * t;
+      double* c0 = S + (2 * b) * PATCH_LD + 2 * a;
       double* c1 = c0 + PATCH_LD;
-      c0[0] = v[b].x; c1[0] = v[b].y; c0[1] = v[b].z; c1[1] = v[b].w;
+      c0[0] = v[t].x; c1[0] = v[t].y; c0[1] = v[t].z; c1[1] = v[t].w;
     }
 }
 
@@ -2014,22 +2018,44 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
                                                          const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
                                                          int* bad) {
 #pragma clang fp contract(off)
-  __shared__ double sm[8][32 * PATCH_LD];   // per patch (two per wave)
   const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
-  const int ps = (threadIdx.x >> 6) * 2 + (lane >> 5);
-  const int64_t i = (int64_t)blockIdx.x * 8 + ps;
+  const int64_t i = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
   const bool live = i < np;
   const int32_t I = live ? perm[i] : 0;
   const int64_t q0 = ptr[I];
   const int m = live ? (int)(ptr[I + 1] - q0) : 0;
   const int d = 2 * m;
-  double* S = sm[ps];
-  // assembly by rows into LDS (patch_assemble), then lane hl reads column hl
-  patch_assemble(S, hl, 32, q0, m, false, ptr, col, gcol, val);
-  __syncthreads();
   double M[2 * PATCH_MAX_NODES];
 #pragma unroll
-  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = hl < d ? S[hl * PATCH_LD + r] : 0.0;
+  for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) M[r] = 0.0;
+  if (hl < d) {
+    const int32_t Jb = gcol[q0 + (hl >> 1)];
+    const int g = hl & 1;
+    // each row's lower bound of Jb by a branch-free 5-step binary search
+    // (rows of <= 16 blocks), every load in bounds, so the rows' searches
+    // form one straight-line block and their loads overlap
+#pragma unroll
+    for (int a = 0; a < PATCH_MAX_NODES; ++a) {
+      const bool va = a < m;
+      const int32_t Ja = va ? col[q0 + a] : I;
+      const int64_t p0 = ptr[Ja];
+      const int n = va ? (int)(ptr[Ja + 1] - p0) : 0;
+      int64_t b = p0;
+      int l = n;
+#pragma unroll
+      for (int st = 0; st < 5; ++st) {
+        const int h = l >> 1;
+        const bool lt = gcol[l > 0 ? b + h : p0] < Jb;
+        b = (l > 0 && lt) ? b + h + 1 : b;
+        l = l > 0 ? (lt ? l - h - 1 : h) : 0;
+      }
+      if (va && b < p0 + n && gcol[b] == Jb) {
+        const dv4 v = val[b];
+        M[2 * a] = g ? v.y : v.x;
+        M[2 * a + 1] = g ? v.w : v.z;
+      }
+    }
+  }
   bool ok = true;
 #pragma clang loop unroll(full)
   for (int k = 0; k < 2 * PATCH_MAX_NODES; ++k) {
@@ -2050,15 +2076,12 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
     if (upd) M[k] = mk;
   }
   if (!ok && hl == 0) atomicOr(bad, 1);
-  // the inverse's columns back into LDS, then the packed upper triangle with
-  // consecutive addresses (column hl's rows 0 .. hl are the inverse's U(:, hl))
-  __syncthreads();
-  if (hl < d) {
+  if (live && ok && hl < d) {
+    double* Up = U + i * ustride + hl * (hl + 1) / 2;
 #pragma unroll
-    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r) S[hl * PATCH_LD + r] = M[r];
+    for (int r = 0; r < 2 * PATCH_MAX_NODES; ++r)
+      if (r <= hl) Up[r] = M[r];
   }
-  __syncthreads();
-  if (live && ok) patch_store(S, hl, 32, d, 1.0, U + i * ustride);
 }
 
 // Patch inverses on the matrix cores (round 6):
@@ -2080,18 +2103,23 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
 // patch_inv2_kernel's to ~1e-14 relative (tests/test_gpu_patch.py).
 // PART (diagnosis build only, MAMG_PATCH_INV 4 / 5): 1 = assembly and
 // stores without the sweep, 2 = the sweep on the identity without assembly
+// ipos (may be null): node -> position in the colour order; then wave w
+// takes node w (not position w), so that the waves in flight assemble
+// neighbouring patches, whose rows overlap, from L2 (colour order puts a
+// patch's neighbours in other colours, far apart), and stores at ipos[node].
 template <int PART = 0>
-__global__ __launch_bounds__(256) void patch_inv3_kernel(int64_t np, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(256, 4) void patch_inv3_kernel(int64_t np, const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ gcol,
                                                          const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
-                                                         int* bad) {
+                                                         int* bad, const int32_t* __restrict__ ipos) {
   constexpr int LD = PATCH_LD;
   __shared__ double sm[4][32 * LD];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
-  const int64_t i = (int64_t)blockIdx.x * 4 + w;
-  const bool live = i < np;
-  const int32_t I = live ? perm[i] : 0;
+  const int64_t iw = (int64_t)blockIdx.x * 4 + w;
+  const bool live = iw < np;
+  const int32_t I = live ? (ipos ? (int32_t)iw : perm[iw]) : 0;
+  const int64_t i = live && ipos ? (int64_t)ipos[iw] : iw;   // the output position
   const int64_t q0 = ptr[I];
   const int m = live ? (int)(ptr[I + 1] - q0) : 0;
   const int d = 2 * m;
@@ -2099,7 +2127,7 @@ __global__ __launch_bounds__(256) void patch_inv3_kernel(int64_t np, const int32
   if (PART == 2) {   // diagnosis: the identity
     for (int k = lane; k < 32 * LD; k += 64) S[k] = (k % LD == k / LD) ? 1.0 : 0.0;
   } else {
-    patch_assemble(S, lane, 64, q0, m, true, ptr, col, gcol, val);
+    patch_assemble<4>(S, lane, 0, q0, m, true, ptr, col, gcol, val);
   }
   __syncthreads();
   dv4 T[2][2];
@@ -2113,34 +2141,29 @@ __global__ __launch_bounds__(256) void patch_inv3_kernel(int64_t np, const int32
 #pragma unroll
   for (int K = 0; K < (PART == 1 ? 0 : 8); ++K) {
     const int t = K >> 2, rr = K & 3;
-    // the pivot block, broadcast (its 16 entries sit in lanes 16 kk + 4 rr + c of T[t][t][rr])
-    double q[4][4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) q[kk][c] = readlane_f64(T[t][t][rr], 16 * kk + 4 * rr + c);
-    // its inverse by the scalar sweep (q <- -P^-1), uniform in every lane
+    // the pivot block spread over 16 lanes: lane l holds Q(l & 15, l >> 4)
+    // for (l & 15) < 4 (P(kk, c) sits in lane 16 kk + 4 rr + c of T[t][t][rr]),
+    // swept in place (Q <- -P^-1): per pivot one broadcast and two permutes
+    const bool qv = lc < 4;
+    double Q = bperm_f64(T[t][t][rr], qv ? 16 * lc + 4 * rr + lr : lane);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const double dp = q[p][p];
+      const double dp = readlane_f64(Q, 17 * p);
       ok = ok && dp > 0.0;
-      const double inv = 1.0 / dp;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (a != p && c != p) q[a][c] -= q[a][p] * q[p][c] * inv;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (a != p) { q[a][p] *= inv; q[p][a] *= inv; }
-      q[p][p] = -inv;
+      // 1 / dp: v_rcp_f64 and two Newton steps (the IEEE division sequence
+      // is a 10-deep dependent chain, four per block)
+      double inv = __builtin_amdgcn_rcp(dp);
+      inv = fma(inv, fma(-dp, inv, 1.0), inv);
+      inv = fma(inv, fma(-dp, inv, 1.0), inv);
+      const double qrp = bperm_f64(Q, 16 * p + lc), qpc = bperm_f64(Q, 16 * lr + p);
+      const bool rp = lc == p, cp = lr == p;
+      // every candidate computed, then selected (no divergent branches)
+      const double upd = Q - qrp * qpc * inv, scl = Q * inv;
+      const double q1 = (rp || cp) ? scl : upd;
+      Q = (rp && cp) ? -inv : q1;
     }
     // A operand of S = P^-1 R: lane l holds (P^-1)(l & 15, l >> 4) for (l & 15) < 4, else 0
-    double pa = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) pa = (lc == a && lr == c) ? -q[a][c] : pa;
+    const double pa = qv ? -Q : 0.0;
     const double R0 = T[t][0][rr], R1 = T[t][1][rr];
     const dv4 z = {0.0, 0.0, 0.0, 0.0};
     const double S0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa, R0, z, 0, 0, 0)[0];   // S(lr, lc) of column tile 0
@@ -2162,15 +2185,11 @@ __global__ __launch_bounds__(256) void patch_inv3_kernel(int64_t np, const int32
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double v = bperm_f64(a ? S1 : S0, 16 * kk + lr + 4 * r);
-        if (inK) T[a][t][r] = v;
+        T[a][t][r] = inK ? v : T[a][t][r];
       }
-    // pivot block K <- -P^-1 (= q)
-    double qk = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) qk = (lr == a && kk == c) ? q[a][c] : qk;
-    if (inK) T[t][t][rr] = qk;
+    // pivot block K <- -P^-1 (= Q): (lr, kk) from lane 16 kk + lr
+    const double qk = bperm_f64(Q, 16 * kk + lr);
+    T[t][t][rr] = inK ? qk : T[t][t][rr];
   }
   if (!ok && lane == 0 && live) atomicOr(bad, 1);
   // M = -A_p^-1: the tiles back into LDS, then the packed upper triangle of -M
@@ -2196,17 +2215,24 @@ int patch_inv_version() {
   return v == 1 || v == 2 ? v : 3;
 }
 
+__global__ __launch_bounds__(256) void inv_perm_kernel(int64_t n, const int32_t* __restrict__ perm, int32_t* __restrict__ ipos) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) ipos[perm[i]] = (int32_t)i;
+}
+
+// ipos: node -> position of perm (patch_inv3_kernel's node-order
+// traversal; null: position order)
 void launch_patch_inv(int64_t np, const int32_t* perm, const int64_t* ptr, const int32_t* col, const int32_t* gcol,
-                      const dv4* val, int64_t ustride, double* U, int* bad) {
+                      const dv4* val, int64_t ustride, double* U, int* bad, const int32_t* ipos = nullptr) {
   if (np <= 0) return;
   switch (patch_inv_version()) {
     case 1: patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
     case 2: patch_inv2_kernel<<<(unsigned)((np + 7) / 8), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
 #if MAMG_DIAG
-    case 4: patch_inv3_kernel<1><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
-    case 5: patch_inv3_kernel<2><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+    case 4: patch_inv3_kernel<1><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
+    case 5: patch_inv3_kernel<2><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
 #endif
-    default: patch_inv3_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+    default: patch_inv3_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
   }
 }
 
@@ -4248,7 +4274,11 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
-  launch_patch_inv(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu, flags + 2);
+  int32_t* ipos = nullptr;   // every node is a patch centre: perm is a permutation of the nodes
+  if ((rc = T->alloc(&ipos, std::max<int64_t>(nr, 1), err))) return rc;
+  if (nr) inv_perm_kernel<<<nblocks(nr), 256>>>(nr, D->pperm, ipos);
+  launch_patch_inv(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu, flags + 2, ipos);
+  T->release(ipos);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
