@@ -26,6 +26,10 @@ def main():
     ap.add_argument('--check', type=int, default=0,
                     help='n > 0: compare the first n patch inverses with a float64 numpy inverse')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE: a layout switch (mamg_set_option)')
+    ap.add_argument('--pause', type=float, default=0.0, help='--sequence: seconds to wait after each close')
+    ap.add_argument('--sequence', default=None,
+                    help='comma-separated profiles (ref, patch) set up and closed one after another in this '
+                         'process (the bench\'s long-lived process), each timed')
     args = ap.parse_args()
     import torch
     import metric_amg_examples_amd as M
@@ -35,11 +39,32 @@ def main():
     n = M.problems.finest_n(3, args.nrefs)
     s = M.problems.bidomain(3, n, 1e6)
     A = s.scipy()
-    if args.profile == 'ref':
-        kw = dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
-                  strong_coupled=0.1, Schwarz_type=6, relaxation=1.2, Schwarz_maxlvl=1)
-    else:
-        kw = dict(smoother=3, Schwarz_type=6, Schwarz_maxlvl=1)
+    def kw_of(prof):
+        if prof == 'ref':
+            return dict(AMG_type=1, aggregation_type=5, cycle_type=2, smoother=11, coarse_scaling=1,
+                        strong_coupled=0.1, Schwarz_type=6, relaxation=1.2, Schwarz_maxlvl=1)
+        return dict(smoother=3, Schwarz_type=6, Schwarz_maxlvl=1)
+    if args.sequence:
+        for prof in args.sequence.split(','):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu', **kw_of(prof))
+            torch.cuda.synchronize()
+            ts = time.time() - t0
+            r = torch.as_tensor(M.problems.seeded_rhs(s.N)).cuda()
+            z = torch.zeros_like(r)
+            ms, _, _ = B.time_apply(r, z, 2, 0, torch.cuda.current_stream())
+            print(json.dumps({'profile': prof, 'setup_s': round(ts, 3), 'ms_per_apply': round(ms, 3),
+                              'hbm_free_gb': round(torch.cuda.mem_get_info()[0] / 2**30, 1),
+                              'phases_ms': {k: round(v, 1) for k, v in B.setup_timings.items()}}), flush=True)
+            t0 = time.time()
+            B.close()
+            torch.cuda.synchronize()
+            print(json.dumps({'close_s': round(time.time() - t0, 3)}), flush=True)
+            if args.pause:
+                time.sleep(args.pause)
+        return
+    kw = kw_of(args.profile)
     torch.cuda.synchronize()
     t0 = time.time()
     B = M.MetricAMG(A, s.W, idofs=s.idofs, num_functions=2, setup='gpu', **kw)

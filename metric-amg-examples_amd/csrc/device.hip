@@ -2103,23 +2103,23 @@ __global__ __launch_bounds__(256) void patch_inv2_kernel(int64_t np, const int32
 // patch_inv2_kernel's to ~1e-14 relative (tests/test_gpu_patch.py).
 // PART (diagnosis build only, MAMG_PATCH_INV 4 / 5): 1 = assembly and
 // stores without the sweep, 2 = the sweep on the identity without assembly
-// ipos (may be null): node -> position in the colour order; then wave w
-// takes node w (not position w), so that the waves in flight assemble
-// neighbouring patches, whose rows overlap, from L2 (colour order puts a
-// patch's neighbours in other colours, far apart), and stores at ipos[node].
+// Waves take patches in colour order, so the 4.2 KB inverses are written in
+// address order.  (Node order -- neighbouring patches, whose rows overlap,
+// assembled together from L2 -- was 1.3 ms faster in a fresh process but
+// 2.9 s slower in a process that had just freed another 63 GB inverse array:
+// writes scattered over 72 GB)
 template <int PART = 0>
 __global__ __launch_bounds__(256, 4) void patch_inv3_kernel(int64_t np, const int32_t* __restrict__ perm,
                                                          const int64_t* __restrict__ ptr, const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ gcol,
                                                          const dv4* __restrict__ val, int64_t ustride, double* __restrict__ U,
-                                                         int* bad, const int32_t* __restrict__ ipos) {
+                                                         int* bad) {
   constexpr int LD = PATCH_LD;
   __shared__ double sm[4][32 * LD];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
-  const int64_t iw = (int64_t)blockIdx.x * 4 + w;
-  const bool live = iw < np;
-  const int32_t I = live ? (ipos ? (int32_t)iw : perm[iw]) : 0;
-  const int64_t i = live && ipos ? (int64_t)ipos[iw] : iw;   // the output position
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  const bool live = i < np;
+  const int32_t I = live ? perm[i] : 0;
   const int64_t q0 = ptr[I];
   const int m = live ? (int)(ptr[I + 1] - q0) : 0;
   const int d = 2 * m;
@@ -2215,24 +2215,17 @@ int patch_inv_version() {
   return v == 1 || v == 2 ? v : 3;
 }
 
-__global__ __launch_bounds__(256) void inv_perm_kernel(int64_t n, const int32_t* __restrict__ perm, int32_t* __restrict__ ipos) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) ipos[perm[i]] = (int32_t)i;
-}
-
-// ipos: node -> position of perm (patch_inv3_kernel's node-order
-// traversal; null: position order)
 void launch_patch_inv(int64_t np, const int32_t* perm, const int64_t* ptr, const int32_t* col, const int32_t* gcol,
-                      const dv4* val, int64_t ustride, double* U, int* bad, const int32_t* ipos = nullptr) {
+                      const dv4* val, int64_t ustride, double* U, int* bad) {
   if (np <= 0) return;
   switch (patch_inv_version()) {
     case 1: patch_inv_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
     case 2: patch_inv2_kernel<<<(unsigned)((np + 7) / 8), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
 #if MAMG_DIAG
-    case 4: patch_inv3_kernel<1><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
-    case 5: patch_inv3_kernel<2><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
+    case 4: patch_inv3_kernel<1><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
+    case 5: patch_inv3_kernel<2><<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
 #endif
-    default: patch_inv3_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad, ipos); break;
+    default: patch_inv3_kernel<<<(unsigned)((np + 3) / 4), 256>>>(np, perm, ptr, col, gcol, val, ustride, U, bad); break;
   }
 }
 
@@ -4274,11 +4267,7 @@ int build_patches(DeviceHandle* h, TmpPool* T, const TBsr& B, DLevel* D, std::st
   const int64_t dmax = 2 * (int64_t)hf[3];
   D->pus = dmax * (dmax + 1) / 2;
   if ((rc = dalloc(h, &D->pu, nr * D->pus, err))) return rc;
-  int32_t* ipos = nullptr;   // every node is a patch centre: perm is a permutation of the nodes
-  if ((rc = T->alloc(&ipos, std::max<int64_t>(nr, 1), err))) return rc;
-  if (nr) inv_perm_kernel<<<nblocks(nr), 256>>>(nr, D->pperm, ipos);
-  launch_patch_inv(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu, flags + 2, ipos);
-  T->release(ipos);
+  launch_patch_inv(nr, D->pperm, D->Sptr, D->Scol, D->Scol, D->Sval, D->pus, D->pu, flags + 2);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(hf, flags, 4 * sizeof(int), hipMemcpyDeviceToHost));
   if (hf[2]) { *err = "node patches: a patch matrix is not SPD (non-positive Gauss-Jordan pivot)"; return MAMG_ERR_SETUP; }
