@@ -480,13 +480,12 @@ def main():
                              'setup_phases_ms': {k: round(v, 1) for k, v in B2.setup_timings.items()}})
             B2.close()
             del s2, z2
-            if kw.get('Schwarz_type') == 6:
-                # the node-patch profiles free ~63 GB of patch inverses at close; the driver
-                # reclaims that VRAM asynchronously and the next setup in the process stalls
-                # 3-6 s until it is done (bench/prof_patch_setup.py --sequence),
-                # so the next profile starts after a pause, outside every timed region
-                torch.cuda.synchronize(dev)
-                time.sleep(5.0)
+            # a closed handle's VRAM (~20 GB; ~80 GB with node patches) is reclaimed by the
+            # driver asynchronously, and the next setup in the process can stall 3-6 s until
+            # that is done (bench/prof_patch_setup.py --sequence), so the next
+            # profile starts after a pause, outside every timed region
+            torch.cuda.synchronize(dev)
+            time.sleep(5.0)
 
     # ---- CPU baseline: oracle C restatement on the same hierarchy, host cores
     cpu = None
