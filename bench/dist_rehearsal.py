@@ -55,8 +55,9 @@ def main():
     import torch
     import metric_amg_examples_amd as M
     n = M.problems.finest_n(3, args.nrefs)
-    if os.environ.get('MAMG_DIST_TEST'):       # the library reads no environment: pass it on
-        M._lib.set_option('MAMG_DIST_TEST', os.environ['MAMG_DIST_TEST'])
+    for name in ('MAMG_DIST_TEST', 'MAMG_K_COL16'):   # the library reads no environment: pass them on
+        if os.environ.get(name):
+            M._lib.set_option(name, os.environ[name])
     torch.cuda.init()
     rss_start = rss_gb()
     if args.source == 'device':
