@@ -489,10 +489,7 @@ __global__ __launch_bounds__(256) void msell_kernel(
   const double2 bb = NB && wr ? double2{vget(b, bs, nd, 0), vget(b, bs, nd, 1)} : double2{0.0, 0.0};
   double s0 = 0.0, s1 = 0.0;
   const int j0 = q * U, j1 = q == LPR - 1 ? len : (len < j0 + U ? len : j0 + U);
-  // a wavefront's rows lie in one slice: its base is uniform (-1: a wide
-  // slice that kept 32-bit columns, the multi-GPU K's ghost-column slices)
-  const int32_t cb0 = C16 ? __builtin_amdgcn_readfirstlane(cbase[ns / SELL_C]) : 0;
-  const bool n16 = C16 && cb0 >= 0;
+  const int32_t cb0 = C16 ? cbase[ns / SELL_C] : 0;
   for (int j = j0; j < j1; j += U) {
     int32_t c[U];
     dv4 v[U];
@@ -500,7 +497,7 @@ __global__ __launch_bounds__(256) void msell_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kk = k + (int64_t)SELL_C * (j + u < j1 ? j + u : j1 - 1);
-      if (n16) c[u] = cb0 + (int32_t)c16[kk];
+      if constexpr (C16) c[u] = cb0 + (int32_t)c16[kk];
       else c[u] = PROBE == 2 ? __builtin_nontemporal_load(bcol + kk) : bcol[kk];
       v[u] = SPL ? blk_any<SPL>(bval, nbs, kk) : blk<SYM, (PROBE >= 2)>(bval, offd, kk);
     }
@@ -3875,10 +3872,8 @@ int sort_sell_slices(HT* h, TmpPool* T, DBsr* D, std::string* err) {
 // MAMG_K_COL16, default on).  K's columns are coarse node ids; the 64 rows of
 // a slice reach the aggregates of a few neighbouring planes, so every slice's
 // columns span far less than 2^16 (at nrefs=6: 4-byte columns are 11 % of K's
-// stream).  cbase[s] = the slice's smallest column, or -1 for a slice whose
-// columns span more (such a slice keeps reading its 32-bit columns: on N
-// GPUs the slices whose rows reach ghost columns, numbered after the owned
-// ones); a matrix with no narrow slice stays as it was.  The kernel
+// stream).  cbase[s] = the slice's smallest column; a matrix with any slice
+// spanning more keeps its 32-bit columns (then nothing changes).  The kernel
 // adds the base back: the same columns, the same sums, bitwise the 32-bit
 // layout (tests/test_gpu.py::test_k_col16_bitwise).
 __global__ __launch_bounds__(64) void sell_span_kernel(int64_t nr, const int64_t* __restrict__ soff,
@@ -3901,10 +3896,9 @@ __global__ __launch_bounds__(64) void sell_span_kernel(int64_t nr, const int64_t
     lo = a < lo ? a : lo;
     hi = b > hi ? b : hi;
   }
-  if (threadIdx.x == 0) {   // a slice spanning more than 16 bits keeps its 32-bit columns: base -1
-    const bool w = hi != INT32_MIN && (int64_t)hi - (int64_t)lo > 65535;
-    cbase[s] = w ? -1 : (lo == INT32_MAX ? 0 : lo);
-    if (!w) atomicAdd(wide, 1);   // narrow slices
+  if (threadIdx.x == 0) {
+    cbase[s] = lo == INT32_MAX ? 0 : lo;
+    if (hi != INT32_MIN && (int64_t)hi - (int64_t)lo > 65535) atomicOr(wide, 1);
   }
 }
 __global__ __launch_bounds__(64) void sell_col16_kernel(int64_t nr, const int64_t* __restrict__ soff,
@@ -3916,7 +3910,6 @@ __global__ __launch_bounds__(64) void sell_col16_kernel(int64_t nr, const int64_
   const int len = meta[slot] & 0xffff;
   const int64_t k = soff[s] + threadIdx.x;
   const int32_t b = cbase[s];
-  if (b < 0) return;   // a wide slice: its 32-bit columns stay in use
   for (int j = 0; j < len; ++j) c16[k + (int64_t)SELL_C * j] = (uint16_t)(col[k + (int64_t)SELL_C * j] - b);
 }
 template <class HT>
@@ -3931,10 +3924,10 @@ int compress_sell_cols(HT* h, TmpPool* T, DBsr* D, std::string* err) {
   if ((rc = dalloc(h, &base, ns, err))) return rc;
   sell_span_kernel<<<(unsigned)ns, SELL_C>>>(D->nr, D->soff, D->meta, D->col, base, wide);
   HIPCHK(hipGetLastError());
-  int narrow = 0;
-  HIPCHK(hipMemcpy(&narrow, wide, sizeof(int), hipMemcpyDeviceToHost));
+  int hw = 1;
+  HIPCHK(hipMemcpy(&hw, wide, sizeof(int), hipMemcpyDeviceToHost));
   T->release(wide);
-  if (narrow == 0) return MAMG_OK;   // every slice spans more than 16 bits: 32-bit columns (base unused)
+  if (hw) return MAMG_OK;   // a slice spans more than 16 bits: 32-bit columns (base stays unused)
   uint16_t* c16 = nullptr;
   if ((rc = dalloc(h, &c16, D->nbs, err))) return rc;
   HIPCHK(dev_memset(c16, 0, D->nbs * sizeof(uint16_t)));
@@ -8051,8 +8044,6 @@ int dev_rank_ops(DistHandle* h, const GHier& G, const DevMat& A0d, const DistPla
       if ((rc = finalize_bsr(h, &T, tK, &D.K, 0, false, err))) return rc;
       if (l == 0 && g_k_sort && D.K.sell && D.K.lpr <= 1)   // rows sorted inside slices (section 4.1)
         if ((rc = sort_sell_slices(h, &T, &D.K, err))) return rc;
-      if (l == 0 && D.K.sell && g_k_c16)   // 16-bit columns where a slice spans <= 65535 (section 4.1)
-        if ((rc = compress_sell_cols(h, &T, &D.K, err))) return rc;
       // K's rows without coarse ghost columns, run while the coarse-e halo is
       // in flight (level 0's SELL K: launch_msell takes row ranges)
       if (l == 0 && !P.replicated && !C.replicated) {
