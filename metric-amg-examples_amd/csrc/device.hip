@@ -5402,16 +5402,12 @@ void launch_half_u(const Op& o, hipStream_t s) {
     o.x, o.xs, o.y, o.b, o.bs, o.W, o.out, o.os, 1, \
     (r0 == 0 && r1 == M.nr && (int64_t)g == M.nsched) ? M.sched \
     : (r0 == M.sr0 && r1 == M.sr1 && (int64_t)g == M.nsched_r) ? M.sched_r : nullptr
-  size_t pad = 0;   // diagnosis: dynamic LDS per workgroup, to cap the workgroups per CU
-#if MAMG_DIAG
-  if (const char* e = std::getenv("MAMG_HALF_LDS_PAD")) pad = (size_t)std::atol(e);
-#endif
   switch (o.epi) {
-    case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, pad, s>>>(HALF_ARGS); break;
-    case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, pad, s>>>(HALF_ARGS); break;
-    case EPI_RESID: hsell2_kernel<EPI_RESID, XFM, U, GH, TAG><<<g, 256, pad, s>>>(HALF_ARGS); break;
+    case EPI_Y: hsell2_kernel<EPI_Y, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_YADD: hsell2_kernel<EPI_YADD, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
+    case EPI_RESID: hsell2_kernel<EPI_RESID, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
     case EPI_KPOST: break;   // A is never the K operator
-    default: hsell2_kernel<EPI_BJAC, XFM, U, GH, TAG><<<g, 256, pad, s>>>(HALF_ARGS); break;
+    default: hsell2_kernel<EPI_BJAC, XFM, U, GH, TAG><<<g, 256, 0, s>>>(HALF_ARGS); break;
   }
 #undef HALF_ARGS
 }
