@@ -1444,11 +1444,17 @@ __global__ __launch_bounds__(TAIL_THREADS) void tail_kernel(const TOp* __restric
       case T_GEMV:   // gemv_kernel: one wave per row; small: one thread per row
         if (o.n <= TAIL_THREADS) {   // no shuffle tree on the dependent chain
           if (t < o.n) {
-            const double* a = o.w + (int64_t)t * o.n;
             double s0 = 0.0, s1 = 0.0;
             int j = 0;
-            for (; j + 1 < (int)o.n; j += 2) { s0 += gload(a + j) * V.x.ld(j); s1 += gload(a + j + 1) * V.x.ld(j + 1); }
-            if (j < (int)o.n) s0 += gload(a + j) * V.x.ld(j);
+            if ((uintptr_t)o.w & 1) {   // the matrix in the resident rows' LDS region (tail_res_plan)
+              const AS3 double* a = (const AS3 double*)(lds + ((uintptr_t)o.w & ~(uintptr_t)1)) + (int64_t)t * o.n;
+              for (; j + 1 < (int)o.n; j += 2) { s0 += a[j] * V.x.ld(j); s1 += a[j + 1] * V.x.ld(j + 1); }
+              if (j < (int)o.n) s0 += a[j] * V.x.ld(j);
+            } else {
+              const double* a = o.w + (int64_t)t * o.n;
+              for (; j + 1 < (int)o.n; j += 2) { s0 += gload(a + j) * V.x.ld(j); s1 += gload(a + j + 1) * V.x.ld(j + 1); }
+              if (j < (int)o.n) s0 += gload(a + j) * V.x.ld(j);
+            }
             V.out.st(t, s0 + s1);
           }
           break;
@@ -4920,12 +4926,35 @@ bool tail_res_plan(const DeviceHandle* h, int l, std::vector<TOp>* prog, std::ve
   };
   TOp ld;
   ld.kind = T_RLOAD; ld.r0 = -1; ld.r1 = *nov;
+  // the coarsest level's dense inverse (T_GEMV, n <= 64) joins the region:
+  // its op's w becomes (offset in the region + 1) with res = 2, turned into
+  // a tagged LDS address with the region's (tail_ops)
+  std::vector<double> dense;
+  std::vector<std::pair<const double*, size_t>> dmap;
+  for (TOp& t : *prog) {
+    if (t.kind != T_GEMV || !t.w || t.n > 64 || t.n <= 0) continue;
+    size_t at = SIZE_MAX;
+    for (const auto& q : dmap)
+      if (q.first == t.w) at = q.second;
+    if (at == SIZE_MAX) {
+      at = dense.size();
+      dense.resize(at + (size_t)(t.n * t.n));
+      if (!get(dense.data() + at, t.w, (size_t)(t.n * t.n) * sizeof(double))) return false;
+      dmap.push_back({t.w, at});
+    }
+    t.res = 2;
+    t.w = reinterpret_cast<const double*>((uintptr_t)at);   // doubles into the dense part
+  }
   const size_t ov = put(iv.data(), iv.size() * sizeof(dv4));
   const size_t oc = put(ic.data(), ic.size() * sizeof(uint32_t));
   const size_t oh = put(hdr.data(), hdr.size() * sizeof(int32_t));
   const size_t og = put(gd.data(), gd.size() * sizeof(dv4));
   if (!ovv.empty()) put(ovv.data(), ovv.size() * sizeof(dv4));
   if (!ovc.empty()) put(ovc.data(), ovc.size() * sizeof(uint16_t));
+  const size_t odn = img->size();
+  if (!dense.empty()) put(dense.data(), dense.size() * sizeof(double));
+  for (TOp& t : *prog)   // byte offset of each dense matrix in the region
+    if (t.kind == T_GEMV && t.res == 2) t.w = reinterpret_cast<const double*>((uintptr_t)(odn - og + 8 * (uintptr_t)t.w));
   ld.n = (int64_t)(img->size() - og);   // the LDS region's bytes (a multiple of 16)
   ld.val = reinterpret_cast<const double*>((uintptr_t)ov + 1);
   ld.col = reinterpret_cast<const int32_t*>((uintptr_t)oc + 1);
@@ -4985,8 +5014,11 @@ bool tail_ops(const DeviceHandle* h, int l, const double* b, double* xout, std::
         if (t.kind == T_RLOAD) need = t.n;
       const int64_t off = (lds + 15) / 16 * 16;
       if (lds > 0 && off + need <= TAIL_LDS_MAX) {
-        for (TOp& t : prog)
+        for (TOp& t : prog) {
           if (t.kind == T_RLOAD) { t.r0 = off; t.r1 = nov; }
+          if (t.kind == T_GEMV && t.res == 2)   // its matrix in the region: a tagged LDS address
+            t.w = reinterpret_cast<const double*>((uintptr_t)(off + (uintptr_t)t.w) | 1);
+        }
         lds = off + need;
       } else {
         res = false;
