@@ -4124,6 +4124,22 @@ int build_gs(HT* h, TmpPool* T, const TBsr& B, const double* W, int level, DLeve
   if (rc) return rc;
   rc = gs_layout(h, T, B, W, ca, ncol, level, &D->Gb, &D->gperm, &D->Gd, &D->gcs, &D->gbk, err);
   T->release(ca);
+  // the colour steps of small coarse levels (<= 20000 node rows: a launch of
+  // a few hundred rows, bound by its dependent load chain) take the largest
+  // power of two <= 1.25 x the mean row length as lanes per row (about one
+  // block per lane) instead of the SpMV rule's ~two: the reference family at
+  // nrefs=6, level 7 8 -> 16 lanes, 142.4 -> 139.9 ms per apply
+  // (profiles/r06_ab_misc.txt)
+  if (rc == MAMG_OK && level > 0 && B.nr <= 20000 && D->Gb.nr > 0) {
+    const double avg = (double)D->Gb.nb / (double)std::max<int64_t>(1, (int64_t)(B.nr));
+    int l = 2;
+    while (l < 64 && (double)(2 * l) <= 1.25 * avg) l *= 2;
+    D->Gb.lanes = l;
+  }
+#if MAMG_DIAG   // diagnosis: lanes per row of the launched colour steps on levels of <= 20000 node rows
+  if (const char* e = std::getenv("MAMG_GS_LANES"))
+    if (rc == MAMG_OK && level > 0 && B.nr <= 20000 && std::atoi(e) > 0) D->Gb.lanes = std::atoi(e);
+#endif
   return rc;
 }
 
